@@ -1,0 +1,197 @@
+"""bench.py -- EM iterations/s of the PPLS_simult inner loop on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2] [--no-cpu]
+
+One "step" = one EM iteration = sweep over X, Y (E-step sufficient statistics + log-likelihood of
+the current theta) + deterministic reduction + [RCCL all-reduce] + finalize (M-step incl. polar
+factor).  Workload: BASELINE config C3 (n = 1e6, p = q = 2000, r = 5, fp64) by default; samples
+are sharded over ranks (strong scaling: n is fixed).  Data are synthetic (simulC model, Philox
+normals) generated on the device before the timed region.  Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+CONFIGS = {
+    "c3": dict(n=1_000_000, p=2000, q=2000, r=5, name="C3: n=1e6, p=q=2000, r=5, fp64 (headline)"),
+    "c2": dict(n=100_000, p=1000, q=1000, r=3, name="C2: n=1e5, p=q=1000, r=3, fp64"),
+}
+METRIC = "EM iterations/sec + log-lik rel-err vs CPU ref, n=1e6 p=q=2000 r=5"
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+
+
+def polar(M):
+    U, _, Vt = np.linalg.svd(M, full_matrices=False)
+    return U @ Vt
+
+
+def make_truth_and_theta0(p, q, r):
+    """Truth: t_k = exp(-0.1(k-1)), b_k = exp(log 1.5 - 0.3(k-1)), sigE = sigF = 0.5,
+    sigH = 0.1, W/C = polar(N(0,1)) seeds 1/2; theta0: W0/C0 = polar(N(0,1)) seeds 3/4, B0 = sigT0 = I,
+    sigmas 1."""
+    from ppls_amd import Theta
+    k = np.arange(r)
+    W = polar(np.random.default_rng(1).standard_normal((p, r)))
+    C = polar(np.random.default_rng(2).standard_normal((q, r)))
+    truth = Theta(W, C, np.exp(np.log(1.5) - 0.3 * k), 0.5, 0.5, 0.1, np.exp(-0.1 * k))
+    W0 = polar(np.random.default_rng(3).standard_normal((p, r)))
+    C0 = polar(np.random.default_rng(4).standard_normal((q, r)))
+    th0 = Theta(W0, C0, np.ones(r), 1.0, 1.0, 1.0, np.ones(r))
+    return truth, th0
+
+
+def load_traffic(workload_key):
+    """HBM bytes per sweep launch from a committed rocprofv3 PMC pass (profiles/), or None."""
+    path = os.path.join(ROOT, "profiles", f"pmc_sweep_{workload_key}.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        with open(path) as f:
+            return json.load(f).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def cpu_baseline(ctx, th0, cfg, seconds_target=15.0):
+    """Time the C restatement of the reference path (oracle/cpu_ref.c, OpenMP) on the host cores on
+    a bounded sample of the same rows; compare its log-likelihood trace with the GPU's on the
+    identical sample."""
+    from oracle import cpu_ref
+    from ppls_amd import Context
+    n_s = min(ctx.n_local, 20000)
+    X, Y = ctx.get_data(0, n_s)
+    Xs, Ys = np.ascontiguousarray(X), np.ascontiguousarray(Y)
+    th = th0.as_dict()
+    cores = cpu_ref.load().cpu_ref_max_threads()
+    t0 = time.perf_counter()
+    cpu_ref.em_steps(Xs, Ys, th, 1)
+    t1 = time.perf_counter() - t0
+    steps = int(max(2, min(20, seconds_target / max(t1, 1e-3))))
+    t0 = time.perf_counter()
+    th_cpu, ll_cpu = cpu_ref.em_steps(Xs, Ys, th, steps)
+    dt = time.perf_counter() - t0
+    row_iters_per_s = n_s * steps / dt
+    # GPU on the identical sample, same theta0, same number of iterations
+    with Context(ctx_device(ctx)) as c2:
+        c2.set_data(Xs, Ys)
+        est, ll_gpu, _, _ = c2.em_run(th0, steps, -np.inf, 0, want_eout=False)
+    rel = float(np.abs(ll_gpu - ll_cpu).max() / np.abs(ll_cpu).max())
+    werr = float(np.abs(est.W - th_cpu["W"]).max())
+    return dict(value=row_iters_per_s / cfg["n"], unit="EM iterations/s", cores=int(cores), kind="port",
+                sample=f"{steps} EM iterations on the first {n_s} of n={cfg['n']} rows in {dt:.1f} s "
+                       f"(oracle/cpu_ref.c, reference pass structure, OpenMP {cores} threads, -O3 "
+                       f"-march=native); value = rows*iterations/s / n"), rel, werr
+
+
+_DEVICE = {}
+
+
+def ctx_device(ctx):
+    return _DEVICE.get(id(ctx), 0)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--sweep", type=int, default=0, help="0 auto, 1 fused, 2 two-pass")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and world > 1:
+        print(f"warning: WORLD_SIZE={world} != --gpus {args.gpus}", file=sys.stderr)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist  # gloo: barriers, max-over-ranks, RCCL id exchange
+        dist.init_process_group("gloo")
+
+    import torch
+    from ppls_amd import Context
+
+    cfg = CONFIGS[args.config]
+    n, p, q, r = cfg["n"], cfg["p"], cfg["q"], cfg["r"]
+    ctx = Context(local)
+    _DEVICE[id(ctx)] = local
+    ctx.set_option("sweep", args.sweep)
+    if world > 1:
+        uid = [Context.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        ctx.comm_init(world, rank, uid[0])
+    row0, n_local = Context.shard_range(n, world, rank)
+    truth, th0 = make_truth_and_theta0(p, q, r)
+    ctx.generate_synthetic(n, p, q, truth, seed=20261015, row0=row0, n_local=n_local)
+
+    def barrier():
+        ctx.synchronize()
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+
+    ctx.em_begin(th0)
+    ctx.em_iterate(args.warmup)
+    barrier()
+    ctx.set_option("timing", 1)
+    ctx.sweep_timing(reset=True)
+    t0 = time.perf_counter()
+    ctx.em_iterate(args.steps)
+    barrier()
+    dt = time.perf_counter() - t0
+    ctx.set_option("timing", 0)
+    kern_ms, launches = ctx.sweep_timing(reset=True)
+    if dist is not None:
+        tt = torch.tensor([dt], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    est, ll = ctx.em_state()
+    info = ctx.sweep_info(r)
+
+    if rank == 0:
+        its = args.steps / dt
+        avg_kernel_ms = kern_ms / max(launches, 1)
+        achieved = info["bytes_per_sweep"] / (avg_kernel_ms * 1e-3) / 1e9 if launches else None
+        wl = f"{args.config}_{'dp%d' % world}"
+        roofline = dict(bound="hbm", achieved=achieved, peak=HBM_PEAK_GBS, unit="GB/s",
+                        frac=(achieved / HBM_PEAK_GBS) if achieved else None,
+                        traffic=load_traffic(wl), kernel=f"ppls_sweep ({info['variant']})",
+                        avg_kernel_ms=avg_kernel_ms, bytes_per_launch=info["bytes_per_sweep"],
+                        grid=info["grid"])
+        out = dict(metric=METRIC, value=its, unit="EM iterations/s", n_gpus=world, steps=args.steps,
+                   warmup=args.warmup, ms_per_step=1e3 * dt / args.steps, higher_is_better=True,
+                   scaling="strong", vs_baseline=None, dtype="f64",
+                   data="synthetic (simulC model: X=TW'+sigE E, Y=UC'+sigF F; Philox normals on device)",
+                   config=dict(workload=cfg["name"], n=n, p=p, q=q, r=r,
+                               parallelism=f"dp{world} (rows sharded, 1 RCCL all-reduce/iteration)"),
+                   roofline=roofline,
+                   loglik_last=float(ll[-1]) if len(ll) else None)
+        if world == 1 and not args.no_cpu:
+            cb, rel, werr = cpu_baseline(ctx, th0, cfg, args.cpu_seconds)
+            out["cpu_baseline"] = cb
+            out["loglik_rel_err_vs_cpu"] = rel
+            out["W_abs_err_vs_cpu"] = werr
+        else:
+            out["cpu_baseline"] = None
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

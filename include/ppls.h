@@ -1,0 +1,148 @@
+/* ppls.h -- C ABI of the MI355X-native PPLS_simult EM inner loop (libppls_amd.so).
+ *
+ * Drop-in boundary for the hot path of selbouhaddani/PPLS (paths relative to the reference):
+ *   - the only native call on the loop today is
+ *       .Call('PPLS_loglC_fast', PACKAGE='PPLS', W, C, X, Y, sigX, sigY, sig2T, c1, c2, c3, Kc)
+ *     Package/PPLS/R/RcppExports.R:32-34 -> Package/PPLS/src/RcppExports.cpp:79-99
+ *     -> Package/PPLS/src/loglC.cpp:318-338;              replaced by ppls_loglC_fast()
+ *   - the R closures on the loop have no native boundary; their C-ABI counterparts are
+ *       Expect_M   Package/PPLS/R/EM_W_multi.R:637-717      -> ppls_estep()
+ *       Maximiz_M  Package/PPLS/R/EM_W_multi.R:729-742      -> ppls_mstep()
+ *       Expect_M %>% Maximiz_M (one loop body, :782)         -> ppls_em_step()
+ *       logl_W     Package/PPLS/R/EM_W_multi.R:297-323      -> ppls_loglik()
+ *       PPLS_simult loop :780-807 (given theta0)             -> ppls_em_run()
+ *
+ * Conventions: all matrices crossing the ABI are column-major fp64 (R's layout), sizes are
+ * int64_t for the sample dimension, the caller owns every host buffer, the context owns every
+ * device buffer.  No exception crosses the ABI: every call returns PPLS_OK (0) or a negative
+ * PPLS_E_* code, with a message in ppls_last_error(ctx).  A context is bound to one GPU and one
+ * host thread; it is not re-entrant.
+ */
+#ifndef PPLS_AMD_PPLS_H
+#define PPLS_AMD_PPLS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PPLS_OK 0
+#define PPLS_E_ARG (-1)     /* invalid argument (R: stop()) */
+#define PPLS_E_HIP (-2)     /* HIP runtime / device error */
+#define PPLS_E_NUMERIC (-3) /* rank-deficient X'mu_T / Y'mu_U, non-finite update */
+#define PPLS_E_STATE (-4)   /* no data loaded / wrong call order */
+#define PPLS_E_COMM (-5)    /* RCCL error */
+#define PPLS_E_NOMEM (-6)   /* device allocation failed */
+
+#define PPLS_ORTH_SVD 0 /* orth(., type = "SVD"): polar factor U V' (default of PPLS_simult) */
+#define PPLS_ORTH_QR 1  /* orth(., type = "QR"):  qr.Q(qr(.)) */
+
+#define PPLS_LAYOUT_COLMAJOR 0 /* R matrices */
+#define PPLS_LAYOUT_ROWMAJOR 1
+
+typedef struct ppls_ctx ppls_ctx;
+
+/* theta = (W, C, B, sigE, sigF, sigH, sigT) of Expect_M's argument list (EM_W_multi.R:637). */
+typedef struct {
+  double* W;    /* p x r column-major */
+  double* C;    /* q x r column-major */
+  double* B;    /* r: diag(B) */
+  double* sigT; /* r: diag(sigT) (standard deviations) */
+  double sigE;  /* == sigX */
+  double sigF;  /* == sigY */
+  double sigH;
+} ppls_theta;
+
+/* Expect_M's return list (EM_W_multi.R:715-716).  Ctt, Cuu, Cut are diagonal r x r matrices in the
+ * reference; only their diagonals are exchanged.  mu_T / mu_U may be NULL (not requested). */
+typedef struct {
+  double* mu_T; /* n_local x r column-major (this rank's rows) */
+  double* mu_U; /* n_local x r column-major */
+  double* Ctt;  /* r */
+  double* Cuu;  /* r */
+  double* Cut;  /* r */
+  double Cee;
+  double Cff;
+  double* Chh;  /* r x r column-major */
+} ppls_expect;
+
+int ppls_version(void);
+const char* ppls_strerror(int code);
+
+/* ---- context ---------------------------------------------------------------------------- */
+int ppls_ctx_create(int device, ppls_ctx** out);
+void ppls_ctx_destroy(ppls_ctx* ctx);
+const char* ppls_last_error(const ppls_ctx* ctx);
+/* keys: "sweep" (0 auto, 1 fused single-pass, 2 generic two-pass), "grid" (workgroups, 0 = auto),
+ *       "timing" (1: record HIP events around every sweep launch) */
+int ppls_set_option(ppls_ctx* ctx, const char* key, int64_t value);
+
+/* ---- multi-GPU: samples are sharded over ranks; one RCCL all-reduce per EM iteration ---- */
+void ppls_shard_range(int64_t n_total, int nranks, int rank, int64_t* row0, int64_t* n_local);
+int ppls_comm_unique_id(char id[128]);
+int ppls_comm_init(ppls_ctx* ctx, int nranks, int rank, const char id[128]);
+
+/* ---- data (X: n_local x p, Y: n_local x q; this rank's rows of an n_total-sample problem) ---- */
+int ppls_set_data(ppls_ctx* ctx, const double* X, const double* Y, int64_t n_local, int p, int q,
+                  int layout, int64_t n_total);
+/* simulC-model synthetic data generated on the device (src/loglC.cpp:268-315, r >= 1):
+ * X = T W' + sigE E, Y = U C' + sigF F, U = T B + H, T = N(0,1) diag(sigT), H = sigH N(0,1);
+ * counter-based Philox4x32-10 normals keyed by (seed, element index): independent of sharding. */
+int ppls_generate_synthetic(ppls_ctx* ctx, int64_t n_total, int64_t row0, int64_t n_local, int p,
+                            int q, int r, const ppls_theta* truth, uint64_t seed);
+int ppls_get_data(ppls_ctx* ctx, double* X, double* Y, int64_t row_begin, int64_t nrows);
+int ppls_data_ssq(ppls_ctx* ctx, double* ssqX, double* ssqY);   /* global (all ranks) */
+
+/* ---- the hot path ------------------------------------------------------------------------ */
+int ppls_estep(ppls_ctx* ctx, const ppls_theta* th, int r, ppls_expect* out);
+int ppls_mstep(ppls_ctx* ctx, const ppls_expect* fit, int r, int type, ppls_theta* out);
+int ppls_em_step(ppls_ctx* ctx, const ppls_theta* in, int r, int type, ppls_theta* out,
+                 ppls_expect* fit /* nullable: Expect_M of `in` */);
+int ppls_loglik(ppls_ctx* ctx, const ppls_theta* th, int r, double* out);
+/* PPLS_simult's loop and tail (EM_W_multi.R:773-806) from an explicit theta0 (in `th`).
+ * On return `th` holds the canonicalised estimates (:794-799), loglik[0..*steps_done-1] the
+ * log-likelihood trace, and eout (nullable) Expect_M at the un-canonicalised final theta (:802).
+ * Returns PPLS_OK; *negative_increment = 1 where the reference warns (:801). */
+int ppls_em_run(ppls_ctx* ctx, ppls_theta* th, int r, int max_steps, double atol, int type,
+                double* loglik, int* steps_done, int* negative_increment, ppls_expect* eout);
+
+/* Device-resident iteration (benchmark / long runs): ppls_em_begin uploads theta0 (canonicalised as
+ * :773-778); ppls_em_iterate enqueues exactly `nsteps` EM iterations (sweep + reduce + all-reduce +
+ * finalize each, no host synchronisation, no stop rule); ppls_em_state downloads the current theta
+ * (un-canonicalised) and the log-likelihood history logl(theta_1..theta_{k-1}) after k iterations. */
+int ppls_em_begin(ppls_ctx* ctx, const ppls_theta* theta0, int r);
+int ppls_em_iterate(ppls_ctx* ctx, int nsteps, int type);
+int ppls_em_state(ppls_ctx* ctx, ppls_theta* out, double* loglik, int loglik_cap, int* n_loglik);
+int ppls_synchronize(ppls_ctx* ctx);
+
+/* loglC_fast (src/loglC.cpp:318-338) with the reference's argument list.  X, Y (column-major
+ * n x p / n x q host matrices) are uploaded into ctx like Rcpp's input_parameter copies them;
+ * pass X = Y = NULL to evaluate on the data already resident in ctx (zero-copy). */
+int ppls_loglC_fast(ppls_ctx* ctx, const double* W, const double* C, const double* X, const double* Y,
+                    int64_t n, int p, int q, int a, double sigX, double sigY, const double* sig2T,
+                    const double* c1, const double* c2, const double* c3, const double* Kc,
+                    double* out);
+
+/* ---- measurement ---------------------------------------------------------------------------- */
+/* Sum of HIP-event durations of the sweep kernel launches recorded since the last reset. */
+int ppls_sweep_timing(ppls_ctx* ctx, double* total_ms, int64_t* launches, int reset);
+/* Shape facts for the roofline: bytes of X and Y one sweep reads (algorithmic), kernel variant. */
+int ppls_sweep_info(ppls_ctx* ctx, int r, int64_t* bytes_per_sweep, int* variant, int* grid);
+
+/* ---- host-side algebra (no GPU; the same code the device finalize runs) ------------------------ */
+/* From the all-reduced sufficient statistics of one sweep with theta (stats = [X'mu_T p x r |
+ * Y'mu_U q x r | Gram 2r x 2r], all column-major) compute Expect_M's moments, logl_W(theta) and
+ * the M-step scalars.  W_next/C_next (nullable) receive orth(X'mu_T)/orth(Y'mu_U). */
+int ppls_finalize_host(const double* SX, const double* SY, const double* G, double ssqX, double ssqY,
+                       double N, int p, int q, int r, const ppls_theta* th, int type,
+                       ppls_theta* next, ppls_expect* moments, double* loglik);
+/* alpha, beta, gamma, delta (4r) with mu_T = Xw diag(alpha) + Yc diag(beta) and
+ * mu_U = Xw diag(gamma) + Yc diag(delta) (EM_W_multi.R:691-694). */
+int ppls_mu_coefficients(const ppls_theta* th, int r, double* coef4r);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PPLS_AMD_PPLS_H */

@@ -1,0 +1,350 @@
+"""CPU oracle for the PPLS_simult EM inner loop -- TEST INFRASTRUCTURE ONLY.
+
+This module is a literal numpy restatement of the reference R code on the hot path. It is
+the parity checker: only ``tests/``, ``__graft_entry__.smoke()`` and the ``cpu_baseline``
+leg of ``bench.py`` may import it.  The product (``ppls_amd``) never calls it.
+
+Every function cites the reference line it restates (paths relative to /root/reference):
+
+* ``expect_m``           Package/PPLS/R/EM_W_multi.R:637-717 (closed form :668-714)
+* ``expect_m_dense``     Package/PPLS/R/EM_W_multi.R:643-667 (debug=TRUE), sseXY_W :606-618
+* ``maximiz_m``          Package/PPLS/R/EM_W_multi.R:729-742, tr() Package/PPLS/R/PJSC.R:1-5
+* ``logl_w``             Package/PPLS/R/EM_W_multi.R:297-323
+* ``loglc_fast``         Package/PPLS/src/loglC.cpp:318-338 (the ``src/`` copy; src-x64 has p, not p+q)
+* ``ppls_simult``        Package/PPLS/R/EM_W_multi.R:758-807 (init :762-771 replaced by an explicit theta0)
+* ``orth``               OmicsPLS::orth (not vendored); semantics Package/functions.R:252-260
+* ``ssq``                OmicsPLS::ssq (not vendored); semantics Package/functions.R:380-385
+
+Parity pinning: R/Rcpp/Eigen are absent from this image, so the reference cannot run here.
+The restatement is pinned by the reference's own known-answer identity checks
+(Package/rank_one_inverse.R:45-59, Package/Benchmark.R:36-45) and by its own independent
+dense formulation (Expect_M(debug=TRUE)); see tests/test_oracle.py.  ``orth`` (OmicsPLS,
+unpinned version) is unpinned by any reference test.
+
+Conventions: R matrices are column-major; here X, Y are numpy arrays (n x p, n x q) and the
+diagonal parameter matrices B, sigT are carried as r x r diagonal matrices exactly as in R.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+
+
+# ----------------------------------------------------------------------------- helpers
+
+def tr(X):
+    """tr() -- Package/PPLS/R/PJSC.R:1-5."""
+    X = np.atleast_2d(np.asarray(X, dtype=np.float64))
+    return float(np.sum(np.diag(X)))
+
+
+def ssq(X):
+    """OmicsPLS::ssq -- semantics Package/functions.R:380-385: sum(X^2)."""
+    X = np.asarray(X, dtype=np.float64)
+    return float(np.sum(X * X))
+
+
+def orth(X, type="SVD"):
+    """OmicsPLS::orth -- semantics Package/functions.R:252-260.
+
+    type "SVD": thin SVD X = U S V' -> U V' (the polar factor; R's svd() is LAPACK dgesdd,
+    numpy's svd is LAPACK gesdd as well).  type "QR": qr.Q(qr(X)) -- Householder QR, for which
+    LINPACK dqrdc2 and LAPACK geqrf share the sign convention R[k,k] = -sign(x_kk)*||x||.
+    """
+    X = np.asarray(X, dtype=np.float64)
+    if X.ndim == 1:
+        X = X[:, None]
+    if type == "SVD":
+        U, _, Vt = np.linalg.svd(X, full_matrices=False)
+        return U @ Vt
+    if type == "QR":
+        Q, _ = np.linalg.qr(X, mode="reduced")
+        return Q
+    raise ValueError("type must be 'SVD' or 'QR'")
+
+
+def blockm(A, B, C):
+    """blockm -- Package/PPLS/R/EM_W_multi.R:594-602."""
+    return np.block([[A, B], [B.T, C]])
+
+
+def sse_xy_w(W, C, B_T, sigX, sigY, sigH, sigT):
+    """sseXY_W -- Package/PPLS/R/EM_W_multi.R:606-618 (the dense (p+q)^2 covariance)."""
+    p = W.shape[0]
+    q = C.shape[0]
+    SX = (W @ sigT) @ (W @ sigT).T + sigX ** 2 * np.eye(p)
+    SXY = W @ B_T @ (sigT @ sigT) @ C.T
+    CBs = C @ B_T.T @ sigT
+    SY = CBs @ CBs.T + (C @ C.T) * sigH ** 2 + sigY ** 2 * np.eye(q)
+    return blockm(SX, SXY, SY)
+
+
+def _diag(v):
+    return np.diag(np.asarray(v, dtype=np.float64))
+
+
+def coefficients(B, sigE, sigF, sigH, sigT):
+    """Per-component Woodbury coefficients -- Expect_M closed form, EM_W_multi.R:669-686.
+
+    B, sigT: r x r diagonal matrices (or vectors).  Returns vectors g, Kw, Kc, Kwc, c1, c2, c3.
+    """
+    t = np.diag(sigT) if np.ndim(sigT) == 2 else np.asarray(sigT, dtype=np.float64)
+    b = np.diag(B) if np.ndim(B) == 2 else np.asarray(B, dtype=np.float64)
+    g = t ** 2 * b ** 2 + sigH ** 2
+    Kw = t ** 2 - t ** 4 * b ** 2 / sigF ** 2 + t ** 4 * b ** 2 * g / (sigF ** 2 * (g + sigF ** 2))
+    Kc = g - t ** 4 * b ** 2 / sigE ** 2 + t ** 6 * b ** 2 / (sigE ** 2 * (t ** 2 + sigE ** 2))
+    Kwc = (t ** 2 * b / (sigE ** 2 * sigF ** 2)
+           - Kc * t ** 2 * b / (sigE ** 2 * sigF ** 2 * (Kc + sigF ** 2))
+           - t ** 4 * b / (sigE ** 2 * sigF ** 2 * (t ** 2 + sigE ** 2))
+           + Kc * t ** 4 * b / (sigE ** 2 * sigF ** 2 * (Kc + sigF ** 2) * (t ** 2 + sigE ** 2)))
+    c1 = Kw / (sigE ** 2 * (Kw + sigE ** 2))
+    c3 = Kc / (sigF ** 2 * (Kc + sigF ** 2))
+    c2 = Kwc
+    return dict(g=g, Kw=Kw, Kc=Kc, Kwc=Kwc, c1=c1, c2=c2, c3=c3)
+
+
+# ----------------------------------------------------------------------------- E step
+
+def expect_m(X, Y, W, C, B, sigE, sigF, sigH, sigT):
+    """Expect_M closed form -- Package/PPLS/R/EM_W_multi.R:668-716.
+
+    The matrix expressions are evaluated in R's left-to-right order.
+    """
+    X = np.asarray(X, dtype=np.float64)
+    Y = np.asarray(Y, dtype=np.float64)
+    W = np.asarray(W, dtype=np.float64).reshape(X.shape[1], -1)
+    C = np.asarray(C, dtype=np.float64).reshape(Y.shape[1], -1)
+    N, p = X.shape
+    q = Y.shape[1]
+    a = W.shape[1]
+    B = _diag(np.diag(B) if np.ndim(B) == 2 else B)
+    sigT = _diag(np.diag(sigT) if np.ndim(sigT) == 2 else sigT)
+    cf = coefficients(B, sigE, sigF, sigH, sigT)
+    c1 = _diag(cf["c1"])
+    c2 = _diag(cf["c2"])
+    c3 = _diag(cf["c3"])
+    sT2 = sigT @ sigT
+    sT4 = sT2 @ sT2
+    B2 = B @ B
+    varU = sT2 @ B2 + np.diag(np.full(a, sigH ** 2))                      # :688
+    Xw = X @ W                                                            # :689
+    Yc = Y @ C                                                            # :690
+    mu_T = (sigE ** -2 * (Xw @ sT2) + sigF ** -2 * (Yc @ sT2 @ B) - Xw @ c1 @ sT2
+            - Xw @ c2 @ sT2 @ B - Yc @ c2 @ sT2 - Yc @ c3 @ B @ sT2)       # :691-692
+    mu_U = (sigE ** -2 * (Xw @ sT2 @ B) + sigF ** -2 * (Yc @ varU)
+            - Xw @ c1 @ sT2 @ B - Xw @ c2 @ varU - Yc @ c2 @ sT2 @ B - Yc @ c3 @ varU)  # :693-694
+    Ctt = (sT2 - sigE ** -2 * sT4 - sigF ** -2 * (sT4 @ B2) + sT4 @ c1 + 2 * (sT4 @ B @ c2)
+           + sT4 @ B2 @ c3 + (mu_T.T @ mu_T) / N)                          # :696-697
+    Cuu = (varU - sigE ** -2 * (sT4 @ B2) - sigF ** -2 * (varU @ varU) + sT4 @ B2 @ c1
+           + 2 * (sT2 @ B @ varU @ c2) + varU @ varU @ c3 + (mu_U.T @ mu_U) / N)   # :698-699
+    Cut = (sT2 @ B - sigE ** -2 * (sT4 @ B) - sigF ** -2 * (sT2 @ B @ varU) + sT4 @ B @ c1
+           + sT2 @ varU @ c2 + sT4 @ B2 @ c2 + sT2 @ B @ varU @ c3 + (mu_U.T @ mu_T) / N)  # :700-701
+    mu_E = X - sigE ** 2 * (Xw @ c1 @ W.T) - sigE ** 2 * (Yc @ c2 @ W.T)  # :703
+    Cee = (p * sigE ** 2 - p * sigE ** 2 + sigE ** 4 * np.sum(np.diag(c1)) + ssq(mu_E) / N) / p   # :706
+    mu_F = Y - sigF ** 2 * (Yc @ c3 @ C.T) - sigF ** 2 * (Xw @ c2 @ C.T)  # :708
+    Cff = (q * sigF ** 2 - q * sigF ** 2 + sigF ** 4 * np.sum(np.diag(c3)) + ssq(mu_F) / N) / q   # :709
+    mu_H = sigF ** -2 * sigH ** 2 * Yc - sigH ** 2 * (Xw @ c2 + Yc @ c3)  # :711
+    Chh = np.diag(np.full(a, sigH ** 2 - sigH ** 4 / sigF ** 2)) + sigH ** 4 * c3 + (mu_H.T @ mu_H) / N  # :712
+    I = np.eye(a)
+    return dict(mu_T=mu_T, mu_U=mu_U, Ctt=np.abs(Ctt) * I, Cuu=np.abs(Cuu) * I, Cut=Cut * I,
+                Cee=np.array([[Cee]]), Cff=np.array([[Cff]]), Chh=np.abs(Chh))   # :715-716
+
+
+def expect_m_dense(X, Y, W, C, B, sigE, sigF, sigH, sigT):
+    """Expect_M(debug=TRUE) -- Package/PPLS/R/EM_W_multi.R:643-667: dense Sigma^{-1} via solve().
+
+    The reference's independent formulation; O(n (p+q)^2), small sizes only.
+    """
+    X = np.asarray(X, dtype=np.float64)
+    Y = np.asarray(Y, dtype=np.float64)
+    N, p = X.shape
+    q = Y.shape[1]
+    B = _diag(np.diag(B) if np.ndim(B) == 2 else B)
+    sigT = _diag(np.diag(sigT) if np.ndim(sigT) == 2 else sigT)
+    a = W.shape[1]
+    sT2 = sigT @ sigT
+    covT = np.vstack([W @ sT2, C @ B @ sT2])
+    covU = np.vstack([W @ B @ sT2, C @ B @ B @ sT2 + sigH ** 2 * C])
+    invS = np.linalg.solve(sse_xy_w(W, C, B, sigE, sigF, sigH, sigT), np.eye(p + q))
+    XY = np.hstack([X, Y])
+    mu_T = XY @ invS @ covT
+    mu_U = XY @ invS @ covU
+    sigU2 = sT2 @ B @ B + np.diag(np.full(a, sigH ** 2))
+    Ctt = sT2 - covT.T @ invS @ covT + mu_T.T @ mu_T / N
+    Cuu = sigU2 - covU.T @ invS @ covU + mu_U.T @ mu_U / N
+    Cut = sT2 @ B - covU.T @ invS @ covT + mu_U.T @ mu_T / N
+    covE = np.vstack([np.diag(np.full(p, sigE ** 2)), np.zeros((q, p))])
+    mu_E = XY @ invS @ covE
+    Cee = tr(np.diag(np.full(p, sigE ** 2)) - covE.T @ invS @ covE + mu_E.T @ mu_E / N) / p
+    covF = np.vstack([np.zeros((p, q)), np.diag(np.full(q, sigF ** 2))])
+    mu_F = XY @ invS @ covF
+    Cff = tr(np.diag(np.full(q, sigF ** 2)) - covF.T @ invS @ covF + mu_F.T @ mu_F / N) / q
+    covH = np.vstack([0 * W, sigH ** 2 * C])
+    mu_H = XY @ invS @ covH
+    Chh = np.diag(np.full(a, sigH ** 2)) - covH.T @ invS @ covH + mu_H.T @ mu_H / N
+    I = np.eye(a)
+    return dict(mu_T=mu_T, mu_U=mu_U, Ctt=np.abs(Ctt) * I, Cuu=np.abs(Cuu) * I, Cut=Cut * I,
+                Cee=np.array([[Cee]]), Cff=np.array([[Cff]]), Chh=np.abs(Chh))
+
+
+# ----------------------------------------------------------------------------- M step
+
+def maximiz_m(fit, X, Y, type="SVD"):
+    """Maximiz_M -- Package/PPLS/R/EM_W_multi.R:729-742."""
+    a = fit["Ctt"].shape[0]
+    I = np.eye(a)
+    Ctt = fit["Ctt"]
+    # B = Cut %*% solve(Ctt) * diag(1,a): Ctt is diagonal after the :715 mask, so LAPACK's
+    # solve returns 1/Ctt_kk exactly rounded and the product is Cut_kk * (1/Ctt_kk).
+    inv = np.linalg.solve(Ctt, I)
+    return dict(
+        W=orth(X.T @ fit["mu_T"], type=type),                            # :732
+        C=orth(Y.T @ fit["mu_U"], type=type),                            # :733
+        B=(fit["Cut"] @ inv) * I,                                        # :734
+        sigE=math.sqrt(tr(fit["Cee"]) / fit["Cee"].shape[1]),            # :735
+        sigF=math.sqrt(tr(fit["Cff"]) / fit["Cff"].shape[1]),            # :736
+        sigH=math.sqrt(tr(fit["Chh"]) / fit["Chh"].shape[1]),            # :737
+        sigT=np.sqrt(Ctt * I),                                           # :738
+    )
+
+
+# ----------------------------------------------------------------------------- log-likelihood
+
+def loglc_fast(W, C, X, Y, sigX, sigY, sig2T, c1, c2, c3, Kc):
+    """loglC_fast -- Package/PPLS/src/loglC.cpp:318-338 (Eigen, single-threaded)."""
+    W = np.asarray(W, dtype=np.float64).reshape(X.shape[1], -1)
+    C = np.asarray(C, dtype=np.float64).reshape(Y.shape[1], -1)
+    sig2X = sigX * sigX
+    sig2Y = sigY * sigY
+    N = X.shape[0]
+    p = W.shape[0]
+    q = C.shape[0]
+    a = W.shape[1]
+    sig2T = np.asarray(sig2T, dtype=np.float64).ravel()
+    Kc = np.asarray(Kc, dtype=np.float64).ravel()
+    Logdiag = (np.sum(np.log(sig2X + sig2T)) + (p - a) * math.log(sig2X)
+               + np.sum(np.log(sig2Y + Kc)) + (q - a) * math.log(sig2Y))      # :331
+    XW = X @ W                                                                # :332
+    YC = Y @ C                                                                # :333
+    traceL = 1 / sig2X * float(np.sum(X * X)) + 1 / sig2Y * float(np.sum(Y * Y))   # :334
+    for i in range(a):                                                        # :335
+        traceL += (-c1[i] * float(XW[:, i] @ XW[:, i]) - 2 * c2[i] * float(XW[:, i] @ YC[:, i])
+                   - c3[i] * float(YC[:, i] @ YC[:, i]))
+    return -0.5 * N * (p + q) * math.log(2 * math.pi) - 0.5 * N * Logdiag - 0.5 * traceL   # :336
+
+
+def logl_coefficients(B_T, sigX, sigY, sigH, sigT):
+    """The coefficient block of logl_W -- Package/PPLS/R/EM_W_multi.R:304-320.
+
+    Differs from Expect_M's block only in taking g = sqrt(...) and then squaring it (:312).
+    """
+    t = np.diag(sigT) if np.ndim(sigT) == 2 else np.atleast_1d(np.asarray(sigT, dtype=np.float64))
+    b = np.diag(B_T) if np.ndim(B_T) == 2 else np.atleast_1d(np.asarray(B_T, dtype=np.float64))
+    g = np.sqrt(t ** 2 * b ** 2 + sigH ** 2)
+    Kw = t ** 2 - t ** 4 * b ** 2 / sigY ** 2 + t ** 4 * b ** 2 * g ** 2 / (sigY ** 2 * (g ** 2 + sigY ** 2))
+    Kc = g ** 2 - t ** 4 * b ** 2 / sigX ** 2 + t ** 6 * b ** 2 / (sigX ** 2 * (t ** 2 + sigX ** 2))
+    Kwc = (t ** 2 * b / (sigX ** 2 * sigY ** 2)
+           - Kc * t ** 2 * b / (sigX ** 2 * sigY ** 2 * (Kc + sigY ** 2))
+           - t ** 4 * b / (sigX ** 2 * sigY ** 2 * (t ** 2 + sigX ** 2))
+           + Kc * t ** 4 * b / (sigX ** 2 * sigY ** 2 * (Kc + sigY ** 2) * (t ** 2 + sigX ** 2)))
+    c1 = Kw / (sigX ** 2 * (Kw + sigX ** 2))
+    c3 = Kc / (sigY ** 2 * (Kc + sigY ** 2))
+    return dict(sig2T=t ** 2, c1=c1, c2=Kwc, c3=c3, Kc=Kc)
+
+
+def logl_w(X, Y, W, C, B_T, sigX, sigY, sigH, sigT):
+    """logl_W -- Package/PPLS/R/EM_W_multi.R:297-323 -> loglC_fast."""
+    sigX = float(np.ravel(sigX)[0])
+    sigY = float(np.ravel(sigY)[0])
+    sigH = float(np.ravel(sigH)[0])
+    cf = logl_coefficients(B_T, sigX, sigY, sigH, sigT)
+    return loglc_fast(W, C, X, Y, sigX, sigY, cf["sig2T"], cf["c1"], cf["c2"], cf["c3"], cf["Kc"])
+
+
+# ----------------------------------------------------------------------------- the loop
+
+def canonicalize(W, C, B, sigT):
+    """Sign/order canonicalisation -- EM_W_multi.R:773-778 and :794-799.
+
+    signLoad = sign(diag(sigT B)); rotLoad = order(diag(sigT B diag(signLoad)), decreasing=TRUE)
+    (R's order() is stable for ties, as is a stable argsort of the negated key).
+    """
+    a = W.shape[1]
+    sB = np.diag(sigT) * np.diag(B)
+    signLoad = np.sign(sB)
+    key = np.diag(sigT @ B @ np.diag(signLoad))
+    rot = np.argsort(-key, kind="stable")
+    W2 = W[:, rot] @ np.diag(signLoad)
+    C2 = C[:, rot] @ np.diag(signLoad)
+    B2 = np.diag(np.diag(B @ np.diag(signLoad))[rot])
+    T2 = np.diag(np.diag(sigT)[rot])
+    return W2, C2, B2, T2
+
+
+def ppls_simult(X, Y, a, EMsteps=10, atol=1e-4, type="SVD", theta0=None):
+    """PPLS_simult -- Package/PPLS/R/EM_W_multi.R:758-807.
+
+    The reference draws theta0 from a sequential PPLS(...,'random') fit with R's RNG
+    (:762-771); here theta0 = dict(W, C, B, sigE, sigF, sigH, sigT) is passed explicitly and
+    the rest of the function (canonicalisation :773-778, loop :780-793, final canonicalisation
+    :794-799, Eout :802, return :803-806) is restated line by line.
+    """
+    X = np.asarray(X, dtype=np.float64)
+    Y = np.asarray(Y, dtype=np.float64)
+    W = np.asarray(theta0["W"], dtype=np.float64).reshape(X.shape[1], a)
+    C = np.asarray(theta0["C"], dtype=np.float64).reshape(Y.shape[1], a)
+    B = _diag(np.diag(theta0["B"]) if np.ndim(theta0["B"]) == 2 else np.broadcast_to(theta0["B"], (a,)))
+    sigE = float(theta0["sigE"])
+    sigF = float(theta0["sigF"])
+    sigH = float(theta0["sigH"])
+    sigT = _diag(np.diag(theta0["sigT"]) if np.ndim(theta0["sigT"]) == 2
+                 else np.broadcast_to(theta0["sigT"], (a,)))
+    W, C, B, sigT = canonicalize(W, C, B, sigT)                          # :773-778
+    logl = []
+    outp = None
+    for i in range(1, EMsteps + 1):                                     # :781
+        fit = expect_m(X, Y, W, C, B, sigE, sigF, sigH, sigT)
+        outp = maximiz_m(fit, X, Y, type)                               # :782
+        W, C, B = outp["W"], outp["C"], outp["B"]
+        sigE, sigF, sigH, sigT = outp["sigE"], outp["sigF"], outp["sigH"], outp["sigT"]
+        logl.append(logl_w(X, Y, W, C, B, sigE, sigF, sigH, sigT))      # :791
+        if i > 1 and logl[i - 1] - logl[i - 2] < atol:                  # :792
+            break
+    est = dict(outp)
+    est["W"], est["C"], est["B"], est["sigT"] = canonicalize(W, C, B, sigT)   # :794-799
+    warn = bool(np.any(np.diff(logl) < 0))                              # :801
+    Eout = expect_m(X, Y, W, C, B, sigE, sigF, sigH, sigT)              # :802 (un-canonicalised)
+    return dict(Expectations=Eout, loglik=np.array(logl), estimates=est, warning_negative=warn)
+
+
+# ----------------------------------------------------------------------------- sufficient statistics
+
+def sweep_stats(X, Y, W, C, coef):
+    """One-pass sufficient statistics of the build's sweep.
+
+    Given mu_T = Xw diag(alpha) + Yc diag(beta), mu_U = Xw diag(gamma) + Yc diag(delta):
+    returns S_X = X' mu_T (p x r), S_Y = Y' mu_U (q x r), G = [Xw Yc]'[Xw Yc] (2r x 2r).
+    Used by the tests to check the device sweep and the sharded (gloo) reduction.
+    """
+    Xw = X @ W
+    Yc = Y @ C
+    mu_T = Xw * coef["alpha"] + Yc * coef["beta"]
+    mu_U = Xw * coef["gamma"] + Yc * coef["delta"]
+    Z = np.hstack([Xw, Yc])
+    return dict(SX=X.T @ mu_T, SY=Y.T @ mu_U, G=Z.T @ Z, mu_T=mu_T, mu_U=mu_U)
+
+
+def mu_coefficients(B, sigE, sigF, sigH, sigT):
+    """alpha, beta, gamma, delta with mu_T[:,k] = alpha_k Xw_k + beta_k Yc_k and
+    mu_U[:,k] = gamma_k Xw_k + delta_k Yc_k -- EM_W_multi.R:691-694 collected per column."""
+    t = np.diag(sigT) if np.ndim(sigT) == 2 else np.asarray(sigT, dtype=np.float64)
+    b = np.diag(B) if np.ndim(B) == 2 else np.asarray(B, dtype=np.float64)
+    cf = coefficients(b, sigE, sigF, sigH, t)
+    t2 = t * t
+    v = t2 * b * b + sigH ** 2
+    alpha = t2 / sigE ** 2 - cf["c1"] * t2 - cf["c2"] * t2 * b
+    beta = t2 * b / sigF ** 2 - cf["c2"] * t2 - cf["c3"] * b * t2
+    gamma = t2 * b / sigE ** 2 - cf["c1"] * t2 * b - cf["c2"] * v
+    delta = v / sigF ** 2 - cf["c2"] * t2 * b - cf["c3"] * v
+    return dict(alpha=alpha, beta=beta, gamma=gamma, delta=delta, **cf)

@@ -1,0 +1,346 @@
+"""Host-side mirror of the reference's R interface for the PPLS_simult hot path.
+
+Same names, argument meaning, return structure and error behaviour as the R functions
+(paths relative to /root/reference):
+
+* ``PPLS_simult``  Package/PPLS/R/EM_W_multi.R:758-807
+* ``Expect_M``     Package/PPLS/R/EM_W_multi.R:637-717
+* ``Maximiz_M``    Package/PPLS/R/EM_W_multi.R:729-742
+* ``logl_W``       Package/PPLS/R/EM_W_multi.R:297-323
+* ``loglC_fast``   Package/PPLS/src/loglC.cpp:318-338 (via RcppExports.R:32-34)
+
+Every call goes through the C ABI (include/ppls.h) into the HIP kernels on the GPU; matrices
+are numpy arrays, R lists are dicts.  Passing ``X=None, Y=None`` uses the data already resident
+in the context (no copy), which is how multi-GPU shards and large synthetic problems are driven.
+"""
+from __future__ import annotations
+
+import ctypes as ct
+import math
+import warnings
+
+import numpy as np
+
+from . import _lib
+from ._lib import Expect, PplsError, Theta, dptr
+
+
+class Context:
+    """One GPU, one HIP stream, resident X/Y (``ppls_ctx``)."""
+
+    def __init__(self, device: int = 0):
+        self._L = _lib.lib()
+        h = ct.c_void_p()
+        rc = self._L.ppls_ctx_create(int(device), ct.byref(h))
+        if rc != 0:
+            raise PplsError(rc, f"ppls_ctx_create(device={device}) failed: "
+                                f"{self._L.ppls_strerror(rc).decode()} (is a GPU visible?)")
+        self.h = h
+        self.p = self.q = None
+        self.n_local = self.n_total = None
+        self.row0 = 0
+
+    # -- plumbing
+    def _chk(self, rc):
+        if rc != 0:
+            raise PplsError(rc, self._L.ppls_last_error(self.h).decode())
+
+    def close(self):
+        if getattr(self, "h", None):
+            self._L.ppls_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def set_option(self, key: str, value: int):
+        self._chk(self._L.ppls_set_option(self.h, key.encode(), int(value)))
+
+    # -- multi-GPU
+    @staticmethod
+    def shard_range(n_total, nranks, rank):
+        L = _lib.lib()
+        r0, nl = ct.c_int64(), ct.c_int64()
+        L.ppls_shard_range(int(n_total), int(nranks), int(rank), ct.byref(r0), ct.byref(nl))
+        return r0.value, nl.value
+
+    @staticmethod
+    def comm_unique_id() -> bytes:
+        buf = ct.create_string_buffer(128)
+        rc = _lib.lib().ppls_comm_unique_id(buf)
+        if rc != 0:
+            raise PplsError(rc, "ncclGetUniqueId failed")
+        return buf.raw
+
+    def comm_init(self, nranks: int, rank: int, uid: bytes):
+        assert len(uid) == 128
+        self._chk(self._L.ppls_comm_init(self.h, int(nranks), int(rank), uid))
+
+    # -- data
+    def set_data(self, X, Y, n_total=None):
+        X = np.asarray(X, dtype=np.float64)
+        Y = np.asarray(Y, dtype=np.float64)
+        if X.ndim != 2 or Y.ndim != 2 or X.shape[0] != Y.shape[0]:
+            raise ValueError("X and Y must be matrices with the same number of rows")
+        if X.flags.f_contiguous and Y.flags.f_contiguous and not (X.flags.c_contiguous and Y.flags.c_contiguous):
+            layout = _lib.PPLS_LAYOUT_COLMAJOR
+        else:
+            X = np.ascontiguousarray(X)
+            Y = np.ascontiguousarray(Y)
+            layout = _lib.PPLS_LAYOUT_ROWMAJOR
+        n, p = X.shape
+        q = Y.shape[1]
+        nt = n if n_total is None else int(n_total)
+        self._chk(self._L.ppls_set_data(self.h, dptr(X), dptr(Y), n, p, q, layout, nt))
+        self.p, self.q, self.n_local, self.n_total = p, q, n, nt
+
+    def generate_synthetic(self, n_total, p, q, truth: Theta, seed: int, row0=0, n_local=None):
+        nl = n_total - row0 if n_local is None else int(n_local)
+        t = truth.struct()
+        self._chk(self._L.ppls_generate_synthetic(self.h, int(n_total), int(row0), nl, int(p), int(q),
+                                                  truth.r, ct.byref(t), ct.c_uint64(int(seed))))
+        self.p, self.q, self.n_local, self.n_total, self.row0 = p, q, nl, int(n_total), int(row0)
+
+    def get_data(self, row_begin=0, nrows=None):
+        nrows = self.n_local - row_begin if nrows is None else nrows
+        X = np.zeros((nrows, self.p), order="F")
+        Y = np.zeros((nrows, self.q), order="F")
+        self._chk(self._L.ppls_get_data(self.h, dptr(X), dptr(Y), int(row_begin), int(nrows)))
+        return X, Y
+
+    def ssq(self):
+        a, b = ct.c_double(), ct.c_double()
+        self._chk(self._L.ppls_data_ssq(self.h, ct.byref(a), ct.byref(b)))
+        return a.value, b.value
+
+    # -- hot path
+    def estep(self, th: Theta, want_mu=True) -> Expect:
+        e = Expect(th.r, self.n_local, want_mu)
+        s = e.struct()
+        t = th.struct()
+        self._chk(self._L.ppls_estep(self.h, ct.byref(t), th.r, ct.byref(s)))
+        e.pull(s)
+        return e
+
+    def mstep(self, fit: Expect, type_: int = _lib.PPLS_ORTH_SVD) -> Theta:
+        out = Theta.empty(self.p, self.q, fit.r)
+        s = fit.struct()
+        o = out.struct()
+        self._chk(self._L.ppls_mstep(self.h, ct.byref(s), fit.r, int(type_), ct.byref(o)))
+        out.pull(o)
+        return out
+
+    def em_step(self, th: Theta, type_: int = _lib.PPLS_ORTH_SVD, want_fit=False):
+        out = Theta.empty(self.p, self.q, th.r)
+        fit = Expect(th.r, self.n_local, want_fit) if want_fit else None
+        t, o = th.struct(), out.struct()
+        fs = fit.struct() if fit is not None else None
+        self._chk(self._L.ppls_em_step(self.h, ct.byref(t), th.r, int(type_), ct.byref(o),
+                                       ct.byref(fs) if fs is not None else None))
+        out.pull(o)
+        if fit is not None:
+            fit.pull(fs)
+        return out, fit
+
+    def loglik(self, th: Theta) -> float:
+        out = ct.c_double()
+        t = th.struct()
+        self._chk(self._L.ppls_loglik(self.h, ct.byref(t), th.r, ct.byref(out)))
+        return out.value
+
+    def em_run(self, th: Theta, max_steps=10, atol=1e-4, type_=_lib.PPLS_ORTH_SVD, want_eout=True,
+               want_mu=True):
+        """PPLS_simult's loop from theta0 = th (copied); returns (estimates, loglik, eout, warn)."""
+        est = Theta(th.W, th.C, th.B, th.sigE, th.sigF, th.sigH, th.sigT)
+        ll = np.zeros(max_steps)
+        steps = ct.c_int()
+        neg = ct.c_int()
+        eout = Expect(th.r, self.n_local, want_mu) if want_eout else None
+        t = est.struct()
+        es = eout.struct() if eout is not None else None
+        self._chk(self._L.ppls_em_run(self.h, ct.byref(t), th.r, int(max_steps), float(atol), int(type_),
+                                      dptr(ll), ct.byref(steps), ct.byref(neg),
+                                      ct.byref(es) if es is not None else None))
+        est.pull(t)
+        if eout is not None:
+            eout.pull(es)
+        return est, ll[: steps.value].copy(), eout, bool(neg.value)
+
+    def em_begin(self, th: Theta):
+        t = th.struct()
+        self._chk(self._L.ppls_em_begin(self.h, ct.byref(t), th.r))
+        self._em_r = th.r
+
+    def em_iterate(self, nsteps: int, type_: int = _lib.PPLS_ORTH_SVD):
+        self._chk(self._L.ppls_em_iterate(self.h, int(nsteps), int(type_)))
+
+    def em_state(self):
+        out = Theta.empty(self.p, self.q, self._em_r)
+        cap = 1 << 16
+        ll = np.zeros(cap)
+        n = ct.c_int()
+        o = out.struct()
+        self._chk(self._L.ppls_em_state(self.h, ct.byref(o), dptr(ll), cap, ct.byref(n)))
+        out.pull(o)
+        return out, ll[: n.value].copy()
+
+    def synchronize(self):
+        self._chk(self._L.ppls_synchronize(self.h))
+
+    def loglC_fast(self, W, C, X, Y, sigX, sigY, sig2T, c1, c2, c3, Kc) -> float:
+        W = np.asfortranarray(W, dtype=np.float64)
+        C = np.asfortranarray(C, dtype=np.float64)
+        a = W.shape[1] if W.ndim == 2 else 1
+        vec = [np.ascontiguousarray(np.ravel(v), dtype=np.float64) for v in (sig2T, c1, c2, c3, Kc)]
+        out = ct.c_double()
+        if X is None:
+            n, p, q = self.n_total, self.p, self.q
+            xp = yp = None
+        else:
+            X = np.asfortranarray(X, dtype=np.float64)
+            Y = np.asfortranarray(Y, dtype=np.float64)
+            n, p = X.shape
+            q = Y.shape[1]
+            xp, yp = dptr(X), dptr(Y)
+            self.p, self.q, self.n_local, self.n_total = p, q, n, n
+        self._chk(self._L.ppls_loglC_fast(self.h, dptr(W), dptr(C), xp, yp, int(n), int(p), int(q), int(a),
+                                          float(sigX), float(sigY), *[dptr(v) for v in vec],
+                                          ct.byref(out)))
+        return out.value
+
+    # -- measurement
+    def sweep_timing(self, reset=True):
+        ms, n = ct.c_double(), ct.c_int64()
+        self._chk(self._L.ppls_sweep_timing(self.h, ct.byref(ms), ct.byref(n), int(reset)))
+        return ms.value, n.value
+
+    def sweep_info(self, r):
+        b, v, g = ct.c_int64(), ct.c_int(), ct.c_int()
+        self._chk(self._L.ppls_sweep_info(self.h, int(r), ct.byref(b), ct.byref(v), ct.byref(g)))
+        return dict(bytes_per_sweep=b.value, variant={1: "fused", 2: "twopass"}[v.value], grid=g.value)
+
+
+# ================================================================================ R mirror
+_DEFAULT_CTX = None
+
+
+def default_context() -> Context:
+    global _DEFAULT_CTX
+    if _DEFAULT_CTX is None:
+        _DEFAULT_CTX = Context(0)
+    return _DEFAULT_CTX
+
+
+def _orth_type(type):
+    if isinstance(type, (list, tuple)):
+        type = type[0]            # match.arg(type) picks the first choice, EM_W_multi.R:761
+    if type not in ("SVD", "QR"):
+        raise ValueError("'arg' should be one of \"SVD\", \"QR\"")
+    return _lib.PPLS_ORTH_SVD if type == "SVD" else _lib.PPLS_ORTH_QR
+
+
+def _ctx_with(X, Y, ctx):
+    ctx = ctx or default_context()
+    if X is not None:
+        ctx.set_data(X, Y)
+    elif ctx.n_local is None:
+        raise ValueError("no data: pass X and Y or a context with resident data")
+    return ctx
+
+
+def Expect_M(X, Y, W, C, B, sigE, sigF, sigH, sigT, debug=False, ctx=None):
+    """Expect_M (EM_W_multi.R:637-717): posterior first and second moments."""
+    if debug:
+        raise NotImplementedError("debug=TRUE (dense Sigma^-1, EM_W_multi.R:643-667) is an O(n(p+q)^2) "
+                                  "cross-check; it lives in the test oracle, not on the GPU path")
+    ctx = _ctx_with(X, Y, ctx)
+    th = Theta(W, C, B, sigE, sigF, sigH, sigT)
+    return ctx.estep(th, want_mu=True).as_dict()
+
+
+def Maximiz_M(fit, X, Y, type=("SVD", "QR"), ctx=None):
+    """Maximiz_M (EM_W_multi.R:729-742): W = orth(X'mu_T), C = orth(Y'mu_U), scalar updates."""
+    ctx = _ctx_with(X, Y, ctx)
+    r = np.asarray(fit["Ctt"]).shape[0]
+    e = Expect(r, ctx.n_local, True)
+    e.mu_T[:] = np.asarray(fit["mu_T"])
+    e.mu_U[:] = np.asarray(fit["mu_U"])
+    e.Ctt[:] = np.diag(np.asarray(fit["Ctt"]))
+    e.Cuu[:] = np.diag(np.asarray(fit["Cuu"]))
+    e.Cut[:] = np.diag(np.asarray(fit["Cut"]))
+    e.Cee = float(np.trace(np.atleast_2d(fit["Cee"])) / np.atleast_2d(fit["Cee"]).shape[1])
+    e.Cff = float(np.trace(np.atleast_2d(fit["Cff"])) / np.atleast_2d(fit["Cff"]).shape[1])
+    e.Chh[:] = np.asarray(fit["Chh"])
+    th = ctx.mstep(e, _orth_type(type))
+    d = th.as_dict()
+    return dict(W=d["W"], C=d["C"], B=d["B"], sigE=d["sigE"], sigF=d["sigF"], sigH=d["sigH"], sigT=d["sigT"])
+
+
+def logl_W(X, Y, W, C, B_T, sigX, sigY, sigH, sigT, ctx=None):
+    """logl_W (EM_W_multi.R:297-323)."""
+    ctx = _ctx_with(X, Y, ctx)
+    W = np.array(W, dtype=np.float64, ndmin=2)
+    if W.shape[0] == 1 and ctx.p != 1:
+        W = W.T
+    C = np.array(C, dtype=np.float64, ndmin=2)
+    if C.shape[0] == 1 and ctx.q != 1:
+        C = C.T
+    return ctx.loglik(Theta(W, C, B_T, sigX, sigY, sigH, sigT))
+
+
+def loglC_fast(W, C, X, Y, sigX, sigY, sig2T, c1, c2, c3, Kc, ctx=None):
+    """loglC_fast (src/loglC.cpp:318-338) -- the drop-in of .Call('PPLS_loglC_fast', ...)."""
+    ctx = ctx or default_context()
+    return ctx.loglC_fast(W, C, X, Y, sigX, sigY, sig2T, c1, c2, c3, Kc)
+
+
+def random_theta0(p, q, a, seed=0):
+    """Deterministic theta0: W0 = orth(N(0,1)), C0 = orth(N(0,1)), B0 = I, sigT0 = I, sigmas = 1.
+
+    The reference draws theta0 from a sequential PPLS(X, Y, a, 20, 1e-4, 'random') fit with R's
+    RNG (EM_W_multi.R:762-771); that initialiser is the next tier of this build.
+    """
+    rng = np.random.default_rng(seed)
+
+    def polar(M):
+        U, _, Vt = np.linalg.svd(M, full_matrices=False)
+        return U @ Vt
+
+    return dict(W=polar(rng.standard_normal((p, a))), C=polar(rng.standard_normal((q, a))),
+                B=np.eye(a), sigE=1.0, sigF=1.0, sigH=1.0, sigT=np.eye(a))
+
+
+def PPLS_simult(X, Y, a, EMsteps=10, atol=1e-4, type=("SVD", "QR"), init=None, ctx=None, **kw):
+    """PPLS_simult (EM_W_multi.R:758-807) on the GPU.
+
+    ``init``: dict(W, C, B, sigE, sigF, sigH, sigT) used as theta0 (the reference's f0); default
+    ``random_theta0``.  Returns dict(Expectations, loglik, estimates) like the R list of class
+    "PPLS_simult"; warns "Negative increments of likelihood" where the reference does (:801).
+    """
+    if kw.get("debug"):
+        raise NotImplementedError("debug=TRUE is an oracle-only cross-check")
+    ctx = _ctx_with(X, Y, ctx)
+    t = _orth_type(type)
+    if init is None:
+        init = random_theta0(ctx.p, ctx.q, a, kw.get("seed", 0))
+    th = Theta(init["W"], init["C"], init["B"], init["sigE"], init["sigF"], init["sigH"], init["sigT"])
+    if th.r != a:
+        raise ValueError(f"init has {th.r} components, a = {a}")
+    est, ll, eout, neg = ctx.em_run(th, int(EMsteps), float(atol), t, want_eout=True, want_mu=True)
+    if neg:
+        warnings.warn("Negative increments of likelihood")
+    d = est.as_dict()
+    estimates = dict(W=d["W"], C=d["C"], B=d["B"], sigE=d["sigE"], sigF=d["sigF"], sigH=d["sigH"],
+                     sigT=d["sigT"])
+    out = dict(Expectations=eout.as_dict(), loglik=ll, estimates=estimates)
+    out["class"] = "PPLS_simult"
+    return out

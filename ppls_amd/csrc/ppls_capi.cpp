@@ -1,0 +1,963 @@
+// ppls_capi.cpp -- host runtime + C ABI (include/ppls.h) of the MI355X PPLS_simult EM inner loop.
+//
+// One context = one GPU = one process rank.  Per EM iteration the host enqueues, on one HIP
+// stream and without synchronising: sweep (1 pass over X, Y) -> deterministic reduction of the
+// workgroup partials -> [RCCL all-reduce of (p+q) r + 4 r^2 doubles] -> finalize (E-step moments,
+// log-likelihood, M-step incl. the polar factor).  The host only reads back the log-likelihood
+// when the convergence test of PPLS_simult (EM_W_multi.R:792) needs it.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "../../include/ppls.h"
+#include "ppls_kernels.h"
+#include "ppls_math.h"
+
+struct ppls_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::string err;
+  int num_cus = 256;
+  // options
+  int sweep_mode = 0;
+  int grid_opt = 0;
+  int timing = 0;
+  // communicator
+  ncclComm_t comm = nullptr;
+  int nranks = 1, rank = 0;
+  // data
+  bool have_data = false;
+  int64_t n_local = 0, n_total = 0;
+  int p = 0, q = 0, ldx = 0, ldy = 0;
+  double* X = nullptr;
+  double* Y = nullptr;
+  double* ssq = nullptr;       // {||X||^2, ||Y||^2} (global)
+  double ssq_host[2] = {0, 0};
+  // per-r state
+  int r_alloc = 0;
+  double* W[2] = {nullptr, nullptr};
+  double* C[2] = {nullptr, nullptr};
+  PplsScalars* sc[2] = {nullptr, nullptr};
+  PplsMoments* mom = nullptr;
+  double* stats = nullptr;
+  double* part = nullptr;
+  int64_t part_ld = 0;
+  int part_groups = 0;
+  double* Z = nullptr;
+  double* mu = nullptr;
+  double* loglik = nullptr;
+  int loglik_cap = 0;
+  double* work = nullptr;
+  int* status = nullptr;
+  double* coefs = nullptr;     // loglC_fast coefficient block (5r)
+  double* scratch = nullptr;   // generic device scratch
+  size_t scratch_bytes = 0;
+  // device-resident iteration state (ppls_em_begin / ppls_em_iterate)
+  int em_r = 0, em_cur = 0, em_iter = 0;
+  bool em_active = false;
+  // timing
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;
+  size_t ev_used = 0;
+  double timed_ms = 0.0;
+  int64_t timed_launches = 0;
+};
+
+namespace {
+
+int fail(ppls_ctx* c, int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  if (c) c->err = buf;
+  return code;
+}
+
+#define HIPCHK(c, call)                                                                   \
+  do {                                                                                    \
+    hipError_t e_ = (call);                                                               \
+    if (e_ != hipSuccess)                                                                 \
+      return fail((c), PPLS_E_HIP, "%s: %s (%s:%d)", #call, hipGetErrorString(e_), __FILE__, \
+                  __LINE__);                                                              \
+  } while (0)
+
+#define RCCLCHK(c, call)                                                                  \
+  do {                                                                                    \
+    ncclResult_t e_ = (call);                                                             \
+    if (e_ != ncclSuccess)                                                                \
+      return fail((c), PPLS_E_COMM, "%s: %s", #call, ncclGetErrorString(e_));            \
+  } while (0)
+
+template <typename T>
+int dalloc(ppls_ctx* c, T** p, size_t count) {
+  if (*p) {
+    (void)hipFree(*p);
+    *p = nullptr;
+  }
+  if (count == 0) count = 1;
+  hipError_t e = hipMalloc((void**)p, count * sizeof(T));
+  if (e != hipSuccess) {
+    *p = nullptr;
+    return fail(c, PPLS_E_NOMEM, "hipMalloc(%zu bytes): %s", count * sizeof(T), hipGetErrorString(e));
+  }
+  return PPLS_OK;
+}
+
+template <typename T>
+void dfree(T*& p) {
+  if (p) (void)hipFree(p);
+  p = nullptr;
+}
+
+int ld_of(int p) { return (p + 1) & ~1; }
+
+int check_theta(ppls_ctx* c, const ppls_theta* th, int r) {
+  if (!th || !th->W || !th->C || !th->B || !th->sigT) return fail(c, PPLS_E_ARG, "theta has NULL fields");
+  if (r < 1 || r > PPLS_RMAX) return fail(c, PPLS_E_ARG, "r=%d outside [1,%d]", r, PPLS_RMAX);
+  if (!(th->sigE > 0) || !(th->sigF > 0) || !(th->sigH >= 0))
+    return fail(c, PPLS_E_ARG, "variances must be positive");
+  return PPLS_OK;
+}
+
+PplsScalars scalars_of(const ppls_theta* th, int r) {
+  PplsScalars s;
+  memset(&s, 0, sizeof s);
+  for (int k = 0; k < r; ++k) {
+    s.b[k] = th->B[k];
+    s.t[k] = th->sigT[k];
+  }
+  s.sigE = th->sigE;
+  s.sigF = th->sigF;
+  s.sigH = th->sigH;
+  ppls_mu_coef(&s, r);
+  return s;
+}
+
+int ensure_r(ppls_ctx* c, int r, int max_steps) {
+  int rc;
+  if (r != c->r_alloc) {
+    for (int i = 0; i < 2; ++i) {
+      if ((rc = dalloc(c, &c->W[i], (size_t)c->ldx * r))) return rc;
+      if ((rc = dalloc(c, &c->C[i], (size_t)c->ldy * r))) return rc;
+      if ((rc = dalloc(c, &c->sc[i], 1))) return rc;
+    }
+    if ((rc = dalloc(c, &c->mom, 1))) return rc;
+    c->part_ld = (int64_t)r * c->ldx + (int64_t)r * c->ldy + 4 * (int64_t)r * r;
+    if ((rc = dalloc(c, &c->stats, (size_t)c->part_ld))) return rc;
+    if ((rc = dalloc(c, &c->work, (size_t)2 * (c->p + c->q) * r + 16))) return rc;
+    if ((rc = dalloc(c, &c->status, 1))) return rc;
+    if ((rc = dalloc(c, &c->coefs, (size_t)5 * r))) return rc;
+    dfree(c->part);
+    dfree(c->Z);
+    dfree(c->mu);
+    c->part_groups = 0;
+    c->r_alloc = r;
+  }
+  if (max_steps + 2 > c->loglik_cap) {
+    if ((rc = dalloc(c, &c->loglik, (size_t)max_steps + 2))) return rc;
+    c->loglik_cap = max_steps + 2;
+  }
+  return PPLS_OK;
+}
+
+int upload_theta(ppls_ctx* c, const ppls_theta* th, int r, int slot) {
+  // W, C: p x r column-major -> ldx x r padded
+  std::vector<double> buf((size_t)std::max(c->ldx, c->ldy) * r, 0.0);
+  for (int k = 0; k < r; ++k)
+    for (int i = 0; i < c->ldx; ++i) buf[(size_t)k * c->ldx + i] = i < c->p ? th->W[(size_t)k * c->p + i] : 0.0;
+  HIPCHK(c, hipMemcpyAsync(c->W[slot], buf.data(), sizeof(double) * c->ldx * r, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  for (int k = 0; k < r; ++k)
+    for (int i = 0; i < c->ldy; ++i) buf[(size_t)k * c->ldy + i] = i < c->q ? th->C[(size_t)k * c->q + i] : 0.0;
+  HIPCHK(c, hipMemcpyAsync(c->C[slot], buf.data(), sizeof(double) * c->ldy * r, hipMemcpyHostToDevice, c->stream));
+  PplsScalars s = scalars_of(th, r);
+  HIPCHK(c, hipMemcpyAsync(c->sc[slot], &s, sizeof s, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return PPLS_OK;
+}
+
+int download_theta(ppls_ctx* c, int r, int slot, ppls_theta* th) {
+  std::vector<double> buf((size_t)std::max(c->ldx, c->ldy) * r);
+  HIPCHK(c, hipMemcpy(buf.data(), c->W[slot], sizeof(double) * c->ldx * r, hipMemcpyDeviceToHost));
+  for (int k = 0; k < r; ++k)
+    for (int i = 0; i < c->p; ++i) th->W[(size_t)k * c->p + i] = buf[(size_t)k * c->ldx + i];
+  HIPCHK(c, hipMemcpy(buf.data(), c->C[slot], sizeof(double) * c->ldy * r, hipMemcpyDeviceToHost));
+  for (int k = 0; k < r; ++k)
+    for (int i = 0; i < c->q; ++i) th->C[(size_t)k * c->q + i] = buf[(size_t)k * c->ldy + i];
+  PplsScalars s;
+  HIPCHK(c, hipMemcpy(&s, c->sc[slot], sizeof s, hipMemcpyDeviceToHost));
+  for (int k = 0; k < r; ++k) {
+    th->B[k] = s.b[k];
+    th->sigT[k] = s.t[k];
+  }
+  th->sigE = s.sigE;
+  th->sigF = s.sigF;
+  th->sigH = s.sigH;
+  return PPLS_OK;
+}
+
+int download_moments(ppls_ctx* c, int r, ppls_expect* e) {
+  if (!e) return PPLS_OK;
+  PplsMoments m;
+  HIPCHK(c, hipMemcpy(&m, c->mom, sizeof m, hipMemcpyDeviceToHost));
+  for (int k = 0; k < r; ++k) {
+    if (e->Ctt) e->Ctt[k] = m.Ctt[k];
+    if (e->Cuu) e->Cuu[k] = m.Cuu[k];
+    if (e->Cut) e->Cut[k] = m.Cut[k];
+  }
+  e->Cee = m.Cee;
+  e->Cff = m.Cff;
+  if (e->Chh)
+    for (int i = 0; i < r * r; ++i) e->Chh[i] = m.Chh[i];
+  return PPLS_OK;
+}
+
+int download_mu(ppls_ctx* c, int r, ppls_expect* e) {
+  if (!e || (!e->mu_T && !e->mu_U) || c->n_local == 0) return PPLS_OK;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  const size_t blk = sizeof(double) * (size_t)c->n_local * r;
+  if (e->mu_T) HIPCHK(c, hipMemcpy(e->mu_T, c->mu, blk, hipMemcpyDeviceToHost));
+  if (e->mu_U) HIPCHK(c, hipMemcpy(e->mu_U, c->mu + (size_t)c->n_local * r, blk, hipMemcpyDeviceToHost));
+  return PPLS_OK;
+}
+
+bool use_fused(ppls_ctx* c, int r, int* ns) {
+  *ns = ppls_fused_supported(r, c->ldx, c->ldy);
+  if (c->sweep_mode == 2) return false;
+  return *ns > 0;
+}
+
+int grid_of(ppls_ctx* c) { return c->grid_opt > 0 ? c->grid_opt : c->num_cus; }
+
+// Allreduce in place (sum) over ranks, on the context stream.
+int allreduce(ppls_ctx* c, double* buf, size_t count) {
+  if (!c->comm || c->nranks <= 1) return PPLS_OK;
+  RCCLCHK(c, ncclAllReduce(buf, buf, count, ncclDouble, ncclSum, c->comm, c->stream));
+  return PPLS_OK;
+}
+
+// One sweep with theta[slot] -> c->stats (all-reduced).
+int sweep(ppls_ctx* c, int r, int slot, bool write_mu) {
+  int rc, ns = 0;
+  const bool fused = use_fused(c, r, &ns);
+  const int grid = grid_of(c);
+  const int groups = fused ? grid : ppls_twopass_groups(std::max<int64_t>(c->n_local, 1), grid);
+  if (groups > c->part_groups || !c->part) {
+    if ((rc = dalloc(c, &c->part, (size_t)groups * c->part_ld))) return rc;
+    c->part_groups = groups;
+  }
+  if (write_mu && !c->mu)
+    if ((rc = dalloc(c, &c->mu, (size_t)std::max<int64_t>(c->n_local, 1) * 2 * r))) return rc;
+  if (!fused && !c->Z)
+    if ((rc = dalloc(c, &c->Z, (size_t)std::max<int64_t>(c->n_local, 1) * 2 * r))) return rc;
+  if (c->n_local == 0) {
+    HIPCHK(c, hipMemsetAsync(c->stats, 0, sizeof(double) * c->part_ld, c->stream));
+  } else {
+    PplsSweepArgs a;
+    a.X = c->X;
+    a.Y = c->Y;
+    a.n_local = c->n_local;
+    a.ldx = c->ldx;
+    a.ldy = c->ldy;
+    a.Wp = c->W[slot];
+    a.Cp = c->C[slot];
+    a.sc = c->sc[slot];
+    a.part = c->part;
+    a.part_ld = c->part_ld;
+    a.mu = write_mu ? c->mu : nullptr;
+    a.write_mu = write_mu ? 1 : 0;
+    a.r = r;
+    a.ns = ns;
+    a.grid = grid;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (c->timing) {
+      if (c->ev_used == c->ev.size()) {
+        std::pair<hipEvent_t, hipEvent_t> pr;
+        HIPCHK(c, hipEventCreate(&pr.first));
+        HIPCHK(c, hipEventCreate(&pr.second));
+        c->ev.push_back(pr);
+      }
+      e0 = c->ev[c->ev_used].first;
+      e1 = c->ev[c->ev_used].second;
+      ++c->ev_used;
+      HIPCHK(c, hipEventRecord(e0, c->stream));
+    }
+    if (fused) HIPCHK(c, ppls_launch_sweep_fused(&a, c->stream));
+    else HIPCHK(c, ppls_launch_sweep_twopass(&a, c->Z, c->stream));
+    if (c->timing) HIPCHK(c, hipEventRecord(e1, c->stream));
+    HIPCHK(c, ppls_launch_reduce(c->part, groups, c->part_ld, c->part_ld, c->stats, 0, c->stream));
+  }
+  return allreduce(c, c->stats, (size_t)c->part_ld);
+}
+
+int finalize(ppls_ctx* c, int r, int cur, int nxt, int logl_index, int type) {
+  PplsFinalizeArgs f;
+  f.stats = c->stats;
+  f.ssq = c->ssq;
+  f.N = (double)c->n_total;
+  f.p = c->p;
+  f.q = c->q;
+  f.r = r;
+  f.ldx = c->ldx;
+  f.ldy = c->ldy;
+  f.Wc = c->W[cur];
+  f.Cc = c->C[cur];
+  f.sc_cur = c->sc[cur];
+  f.Wn = c->W[nxt];
+  f.Cn = c->C[nxt];
+  f.sc_nxt = c->sc[nxt];
+  f.mom = c->mom;
+  f.loglik = c->loglik;
+  f.logl_index = logl_index;
+  f.work = c->work;
+  f.status = c->status;
+  f.qr = type == PPLS_ORTH_QR ? 1 : 0;
+  f.mode = 3;
+  HIPCHK(c, ppls_launch_finalize(&f, c->stream));
+  return PPLS_OK;
+}
+
+int check_status(ppls_ctx* c) {
+  int st = 0;
+  HIPCHK(c, hipMemcpy(&st, c->status, sizeof st, hipMemcpyDeviceToHost));
+  if (st != 0) return fail(c, PPLS_E_NUMERIC, "rank-deficient X'mu_T or Y'mu_U in the M-step (status %d)", st);
+  return PPLS_OK;
+}
+
+int compute_ssq(ppls_ctx* c) {
+  int rc;
+  const int nb = 1024;
+  if ((rc = dalloc(c, &c->scratch, nb + 8))) return rc;
+  HIPCHK(c, hipMemsetAsync(c->ssq, 0, 2 * sizeof(double), c->stream));
+  if (c->n_local > 0) {
+    HIPCHK(c, ppls_launch_sumsq(c->X, c->n_local * c->ldx, c->scratch, nb, c->ssq, 0, c->stream));
+    HIPCHK(c, ppls_launch_sumsq(c->Y, c->n_local * c->ldy, c->scratch, nb, c->ssq + 1, 0, c->stream));
+  }
+  if ((rc = allreduce(c, c->ssq, 2))) return rc;
+  HIPCHK(c, hipMemcpyAsync(c->ssq_host, c->ssq, 2 * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  dfree(c->scratch);
+  return PPLS_OK;
+}
+
+int alloc_data(ppls_ctx* c, int64_t n_local, int p, int q, int64_t n_total) {
+  int rc;
+  if (n_local < 0 || p < 1 || q < 1) return fail(c, PPLS_E_ARG, "bad shape n=%lld p=%d q=%d", (long long)n_local, p, q);
+  c->n_local = n_local;
+  c->n_total = n_total > 0 ? n_total : n_local;
+  c->p = p;
+  c->q = q;
+  c->ldx = ld_of(p);
+  c->ldy = ld_of(q);
+  if ((rc = dalloc(c, &c->X, (size_t)std::max<int64_t>(n_local, 1) * c->ldx))) return rc;
+  if ((rc = dalloc(c, &c->Y, (size_t)std::max<int64_t>(n_local, 1) * c->ldy))) return rc;
+  if (!c->ssq && (rc = dalloc(c, &c->ssq, 2))) return rc;
+  c->r_alloc = 0;   // force per-r buffers to be re-sized for the new shape
+  dfree(c->part);
+  dfree(c->Z);
+  dfree(c->mu);
+  c->part_groups = 0;
+  c->have_data = false;
+  return PPLS_OK;
+}
+
+// Canonicalisation of EM_W_multi.R:773-778 / :794-799 applied to a host theta.
+void canonicalize(ppls_theta* th, int p, int q, int r) {
+  int rot[PPLS_RMAX];
+  double sgn[PPLS_RMAX];
+  ppls_canonical_order(th->sigT, th->B, r, rot, sgn);
+  std::vector<double> W((size_t)p * r), C((size_t)q * r);
+  double B[PPLS_RMAX], T[PPLS_RMAX];
+  for (int j = 0; j < r; ++j) {
+    // W.[,rotLoad] %*% diag(signLoad): column j <- old column rot[j] scaled by signLoad[j]
+    for (int i = 0; i < p; ++i) W[(size_t)j * p + i] = th->W[(size_t)rot[j] * p + i] * sgn[j];
+    for (int i = 0; i < q; ++i) C[(size_t)j * q + i] = th->C[(size_t)rot[j] * q + i] * sgn[j];
+    B[j] = th->B[rot[j]] * sgn[rot[j]];   // diag(B %*% diag(signLoad))[rotLoad]
+    T[j] = th->sigT[rot[j]];
+  }
+  memcpy(th->W, W.data(), sizeof(double) * W.size());
+  memcpy(th->C, C.data(), sizeof(double) * C.size());
+  for (int j = 0; j < r; ++j) {
+    th->B[j] = B[j];
+    th->sigT[j] = T[j];
+  }
+}
+
+// Host polar factor / QR factor of the p x r matrix S (ld p): sequential Householder QR, then the
+// same small Jacobi polar as the device.  out: p x r.
+int host_orth(const double* S, int p, int r, int type, double* out) {
+  std::vector<double> A(S, S + (size_t)p * r), E((size_t)p * r, 0.0), vtv(r);
+  double R[PPLS_RMAX * PPLS_RMAX] = {0}, P[PPLS_RMAX * PPLS_RMAX];
+  for (int k = 0; k < r; ++k) {
+    double s2 = 0.0;
+    for (int i = k; i < p; ++i) s2 += A[(size_t)k * p + i] * A[(size_t)k * p + i];
+    const double sig = std::sqrt(s2), akk = A[(size_t)k * p + k];
+    if (!(sig > 0.0)) return PPLS_E_NUMERIC;
+    const double alpha = akk >= 0.0 ? -sig : sig;
+    vtv[k] = 2.0 * sig * (sig + std::fabs(akk));
+    A[(size_t)k * p + k] = akk - alpha;
+    R[k * r + k] = alpha;
+    for (int j = k + 1; j < r; ++j) {
+      double d = 0.0;
+      for (int i = k; i < p; ++i) d += A[(size_t)k * p + i] * A[(size_t)j * p + i];
+      const double f = 2.0 * d / vtv[k];
+      for (int i = k; i < p; ++i) A[(size_t)j * p + i] -= f * A[(size_t)k * p + i];
+      R[j * r + k] = A[(size_t)j * p + k];
+    }
+  }
+  for (int j = 0; j < r; ++j) E[(size_t)j * p + j] = 1.0;
+  for (int k = r - 1; k >= 0; --k)
+    for (int j = 0; j < r; ++j) {
+      double d = 0.0;
+      for (int i = k; i < p; ++i) d += A[(size_t)k * p + i] * E[(size_t)j * p + i];
+      const double f = 2.0 * d / vtv[k];
+      for (int i = k; i < p; ++i) E[(size_t)j * p + i] -= f * A[(size_t)k * p + i];
+    }
+  if (type == PPLS_ORTH_QR) {
+    memcpy(out, E.data(), sizeof(double) * E.size());
+    return PPLS_OK;
+  }
+  if (ppls_small_polar(R, r, P) != 0) return PPLS_E_NUMERIC;
+  for (int j = 0; j < r; ++j)
+    for (int i = 0; i < p; ++i) {
+      double s = 0.0;
+      for (int k = 0; k < r; ++k) s += E[(size_t)k * p + i] * P[j * r + k];
+      out[(size_t)j * p + i] = s;
+    }
+  return PPLS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ppls_version(void) { return 100; }
+
+const char* ppls_strerror(int code) {
+  switch (code) {
+    case PPLS_OK: return "ok";
+    case PPLS_E_ARG: return "invalid argument";
+    case PPLS_E_HIP: return "HIP runtime error";
+    case PPLS_E_NUMERIC: return "numerical failure";
+    case PPLS_E_STATE: return "invalid state";
+    case PPLS_E_COMM: return "RCCL error";
+    case PPLS_E_NOMEM: return "out of device memory";
+    default: return "unknown error";
+  }
+}
+
+int ppls_ctx_create(int device, ppls_ctx** out) {
+  if (!out) return PPLS_E_ARG;
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return PPLS_E_HIP;
+  if (device < 0 || device >= ndev) return PPLS_E_ARG;
+  ppls_ctx* c = new ppls_ctx();
+  c->device = device;
+  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return PPLS_E_HIP;
+  }
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
+    c->num_cus = prop.multiProcessorCount;
+  *out = c;
+  return PPLS_OK;
+}
+
+void ppls_ctx_destroy(ppls_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  if (c->comm) ncclCommDestroy(c->comm);
+  dfree(c->X); dfree(c->Y); dfree(c->ssq);
+  for (int i = 0; i < 2; ++i) { dfree(c->W[i]); dfree(c->C[i]); dfree(c->sc[i]); }
+  dfree(c->mom); dfree(c->stats); dfree(c->part); dfree(c->Z); dfree(c->mu); dfree(c->loglik);
+  dfree(c->work); dfree(c->status); dfree(c->coefs); dfree(c->scratch);
+  for (auto& e : c->ev) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+const char* ppls_last_error(const ppls_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int ppls_set_option(ppls_ctx* c, const char* key, int64_t value) {
+  if (!c || !key) return PPLS_E_ARG;
+  if (!strcmp(key, "sweep")) {
+    if (value < 0 || value > 2) return fail(c, PPLS_E_ARG, "sweep must be 0, 1 or 2");
+    c->sweep_mode = (int)value;
+  } else if (!strcmp(key, "grid")) {
+    if (value < 0 || value > 65535) return fail(c, PPLS_E_ARG, "grid out of range");
+    c->grid_opt = (int)value;
+    c->part_groups = 0;
+    dfree(c->part);
+  } else if (!strcmp(key, "timing")) {
+    c->timing = value ? 1 : 0;
+  } else {
+    return fail(c, PPLS_E_ARG, "unknown option '%s'", key);
+  }
+  return PPLS_OK;
+}
+
+void ppls_shard_range(int64_t n_total, int nranks, int rank, int64_t* row0, int64_t* n_local) {
+  if (nranks < 1) nranks = 1;
+  const int64_t b = n_total * rank / nranks, e = n_total * (rank + 1) / nranks;
+  if (row0) *row0 = b;
+  if (n_local) *n_local = e - b;
+}
+
+int ppls_comm_unique_id(char id[128]) {
+  ncclUniqueId u;
+  if (ncclGetUniqueId(&u) != ncclSuccess) return PPLS_E_COMM;
+  static_assert(sizeof(u.internal) == 128, "unexpected ncclUniqueId size");
+  memcpy(id, u.internal, 128);
+  return PPLS_OK;
+}
+
+int ppls_comm_init(ppls_ctx* c, int nranks, int rank, const char id[128]) {
+  if (!c || nranks < 1 || rank < 0 || rank >= nranks) return PPLS_E_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  if (c->comm) { ncclCommDestroy(c->comm); c->comm = nullptr; }
+  c->nranks = nranks;
+  c->rank = rank;
+  if (nranks > 1 || id) {
+    ncclUniqueId u;
+    memcpy(u.internal, id, 128);
+    RCCLCHK(c, ncclCommInitRank(&c->comm, nranks, u, rank));
+  }
+  if (c->have_data) return compute_ssq(c);
+  return PPLS_OK;
+}
+
+int ppls_set_data(ppls_ctx* c, const double* X, const double* Y, int64_t n_local, int p, int q,
+                  int layout, int64_t n_total) {
+  if (!c || (n_local > 0 && (!X || !Y))) return c ? fail(c, PPLS_E_ARG, "NULL data") : PPLS_E_ARG;
+  if (layout != PPLS_LAYOUT_COLMAJOR && layout != PPLS_LAYOUT_ROWMAJOR)
+    return fail(c, PPLS_E_ARG, "layout must be 0 (column-major) or 1 (row-major)");
+  HIPCHK(c, hipSetDevice(c->device));
+  int rc = alloc_data(c, n_local, p, q, n_total);
+  if (rc) return rc;
+  if (n_local > 0) {
+    for (int m = 0; m < 2; ++m) {
+      const double* src = m == 0 ? X : Y;
+      const int cols = m == 0 ? p : q, ld = m == 0 ? c->ldx : c->ldy;
+      double* dst = m == 0 ? c->X : c->Y;
+      if (layout == PPLS_LAYOUT_ROWMAJOR) {
+        HIPCHK(c, hipMemset2DAsync(dst, sizeof(double) * ld, 0, sizeof(double) * ld, n_local, c->stream));
+        HIPCHK(c, hipMemcpy2DAsync(dst, sizeof(double) * ld, src, sizeof(double) * cols, sizeof(double) * cols,
+                                   n_local, hipMemcpyHostToDevice, c->stream));
+      } else {
+        double* tmp = nullptr;
+        if ((rc = dalloc(c, &tmp, (size_t)n_local * cols))) return rc;
+        HIPCHK(c, hipMemcpyAsync(tmp, src, sizeof(double) * n_local * cols, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(c, ppls_launch_to_rowmajor(tmp, n_local, cols, ld, dst, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        dfree(tmp);
+      }
+    }
+  }
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->have_data = true;
+  return compute_ssq(c);
+}
+
+int ppls_generate_synthetic(ppls_ctx* c, int64_t n_total, int64_t row0, int64_t n_local, int p, int q,
+                            int r, const ppls_theta* truth, uint64_t seed) {
+  if (!c) return PPLS_E_ARG;
+  int rc;
+  if ((rc = check_theta(c, truth, r))) return rc;
+  if (row0 < 0 || n_local < 0 || row0 + n_local > n_total) return fail(c, PPLS_E_ARG, "bad row range");
+  HIPCHK(c, hipSetDevice(c->device));
+  if ((rc = alloc_data(c, n_local, p, q, n_total))) return rc;
+  double *Wt = nullptr, *Ct = nullptr, *TU = nullptr;
+  if ((rc = dalloc(c, &Wt, (size_t)p * r))) return rc;
+  if ((rc = dalloc(c, &Ct, (size_t)q * r))) { dfree(Wt); return rc; }
+  if ((rc = dalloc(c, &TU, (size_t)std::max<int64_t>(n_local, 1) * 2 * r))) { dfree(Wt); dfree(Ct); return rc; }
+  PplsScalars s = scalars_of(truth, r);
+  hipError_t e = hipMemcpy(Wt, truth->W, sizeof(double) * p * r, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(Ct, truth->C, sizeof(double) * q * r, hipMemcpyHostToDevice);
+  if (e == hipSuccess)
+    e = ppls_launch_generate(n_local, row0, p, q, c->ldx, c->ldy, r, &s, Wt, Ct, seed, TU, c->X, c->Y, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  dfree(Wt); dfree(Ct); dfree(TU);
+  if (e != hipSuccess) return fail(c, PPLS_E_HIP, "synthetic generation: %s", hipGetErrorString(e));
+  c->have_data = true;
+  return compute_ssq(c);
+}
+
+int ppls_get_data(ppls_ctx* c, double* X, double* Y, int64_t row_begin, int64_t nrows) {
+  if (!c) return PPLS_E_ARG;
+  if (!c->have_data) return fail(c, PPLS_E_STATE, "no data");
+  if (row_begin < 0 || nrows < 0 || row_begin + nrows > c->n_local) return fail(c, PPLS_E_ARG, "bad row range");
+  if (nrows == 0) return PPLS_OK;
+  HIPCHK(c, hipSetDevice(c->device));
+  int rc;
+  for (int m = 0; m < 2; ++m) {
+    double* dst = m == 0 ? X : Y;
+    if (!dst) continue;
+    const int cols = m == 0 ? c->p : c->q, ld = m == 0 ? c->ldx : c->ldy;
+    const double* src = (m == 0 ? c->X : c->Y) + row_begin * ld;
+    double* tmp = nullptr;
+    if ((rc = dalloc(c, &tmp, (size_t)nrows * cols))) return rc;
+    HIPCHK(c, ppls_launch_to_colmajor(src, nrows, cols, ld, tmp, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    hipError_t e = hipMemcpy(dst, tmp, sizeof(double) * nrows * cols, hipMemcpyDeviceToHost);
+    dfree(tmp);
+    if (e != hipSuccess) return fail(c, PPLS_E_HIP, "copy back: %s", hipGetErrorString(e));
+  }
+  return PPLS_OK;
+}
+
+int ppls_data_ssq(ppls_ctx* c, double* ssqX, double* ssqY) {
+  if (!c) return PPLS_E_ARG;
+  if (!c->have_data) return fail(c, PPLS_E_STATE, "no data");
+  if (ssqX) *ssqX = c->ssq_host[0];
+  if (ssqY) *ssqY = c->ssq_host[1];
+  return PPLS_OK;
+}
+
+int ppls_estep(ppls_ctx* c, const ppls_theta* th, int r, ppls_expect* out) {
+  if (!c) return PPLS_E_ARG;
+  if (!c->have_data) return fail(c, PPLS_E_STATE, "no data");
+  int rc;
+  if ((rc = check_theta(c, th, r))) return rc;
+  HIPCHK(c, hipSetDevice(c->device));
+  if ((rc = ensure_r(c, r, 1))) return rc;
+  if ((rc = upload_theta(c, th, r, 0))) return rc;
+  HIPCHK(c, hipMemsetAsync(c->status, 0, sizeof(int), c->stream));
+  const bool wm = out && (out->mu_T || out->mu_U);
+  if ((rc = sweep(c, r, 0, wm))) return rc;
+  if ((rc = finalize(c, r, 0, 1, -1, PPLS_ORTH_SVD))) return rc;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if ((rc = download_moments(c, r, out))) return rc;
+  return download_mu(c, r, out);
+}
+
+int ppls_em_step(ppls_ctx* c, const ppls_theta* in, int r, int type, ppls_theta* out, ppls_expect* fit) {
+  if (!c) return PPLS_E_ARG;
+  if (!c->have_data) return fail(c, PPLS_E_STATE, "no data");
+  int rc;
+  if ((rc = check_theta(c, in, r))) return rc;
+  if (!out || !out->W || !out->C || !out->B || !out->sigT) return fail(c, PPLS_E_ARG, "NULL output theta");
+  HIPCHK(c, hipSetDevice(c->device));
+  if ((rc = ensure_r(c, r, 1))) return rc;
+  if ((rc = upload_theta(c, in, r, 0))) return rc;
+  HIPCHK(c, hipMemsetAsync(c->status, 0, sizeof(int), c->stream));
+  const bool wm = fit && (fit->mu_T || fit->mu_U);
+  if ((rc = sweep(c, r, 0, wm))) return rc;
+  if ((rc = finalize(c, r, 0, 1, -1, type))) return rc;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if ((rc = check_status(c))) return rc;
+  if ((rc = download_moments(c, r, fit))) return rc;
+  if ((rc = download_mu(c, r, fit))) return rc;
+  return download_theta(c, r, 1, out);
+}
+
+int ppls_mstep(ppls_ctx* c, const ppls_expect* fit, int r, int type, ppls_theta* out) {
+  if (!c) return PPLS_E_ARG;
+  if (!c->have_data) return fail(c, PPLS_E_STATE, "no data");
+  if (!fit || !fit->mu_T || !fit->mu_U || !fit->Ctt || !fit->Cut || !fit->Chh)
+    return fail(c, PPLS_E_ARG, "Maximiz_M needs mu_T, mu_U, Ctt, Cut, Cee, Cff, Chh");
+  if (!out || !out->W || !out->C || !out->B || !out->sigT) return fail(c, PPLS_E_ARG, "NULL output theta");
+  if (r < 1 || r > PPLS_RMAX) return fail(c, PPLS_E_ARG, "bad r");
+  HIPCHK(c, hipSetDevice(c->device));
+  int rc;
+  if ((rc = ensure_r(c, r, 1))) return rc;
+  const int grid = grid_of(c);
+  const int groups = ppls_twopass_groups(std::max<int64_t>(c->n_local, 1), grid);
+  if (groups > c->part_groups || !c->part) {
+    if ((rc = dalloc(c, &c->part, (size_t)groups * c->part_ld))) return rc;
+    c->part_groups = groups;
+  }
+  if (!c->Z && (rc = dalloc(c, &c->Z, (size_t)std::max<int64_t>(c->n_local, 1) * 2 * r))) return rc;
+  // Z = [mu_T | mu_U] row-major, coefficients alpha = delta = 1, beta = gamma = 0:
+  // the accumulate pass then computes exactly X'mu_T and Y'mu_U (EM_W_multi.R:732-733).
+  PplsScalars s;
+  memset(&s, 0, sizeof s);
+  for (int k = 0; k < r; ++k) { s.alpha[k] = 1.0; s.delta[k] = 1.0; }
+  HIPCHK(c, hipMemcpy(c->sc[0], &s, sizeof s, hipMemcpyHostToDevice));
+  if (c->n_local > 0) {
+    double* tmp = nullptr;
+    if ((rc = dalloc(c, &tmp, (size_t)c->n_local * 2 * r))) return rc;
+    HIPCHK(c, hipMemcpy(tmp, fit->mu_T, sizeof(double) * c->n_local * r, hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy(tmp + (size_t)c->n_local * r, fit->mu_U, sizeof(double) * c->n_local * r, hipMemcpyHostToDevice));
+    HIPCHK(c, ppls_launch_to_rowmajor(tmp, c->n_local, 2 * r, 2 * r, c->Z, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    dfree(tmp);
+    PplsSweepArgs a;
+    memset(&a, 0, sizeof a);
+    a.X = c->X; a.Y = c->Y; a.n_local = c->n_local; a.ldx = c->ldx; a.ldy = c->ldy;
+    a.sc = c->sc[0]; a.part = c->part; a.part_ld = c->part_ld; a.r = r; a.grid = grid;
+    HIPCHK(c, ppls_launch_accumulate(&a, c->Z, c->stream));
+    HIPCHK(c, ppls_launch_reduce(c->part, groups, c->part_ld, c->part_ld, c->stats, 0, c->stream));
+  } else {
+    HIPCHK(c, hipMemsetAsync(c->stats, 0, sizeof(double) * c->part_ld, c->stream));
+  }
+  if ((rc = allreduce(c, c->stats, (size_t)c->part_ld))) return rc;
+  HIPCHK(c, hipMemsetAsync(c->status, 0, sizeof(int), c->stream));
+  PplsFinalizeArgs f;
+  memset(&f, 0, sizeof f);
+  f.stats = c->stats; f.ssq = c->ssq; f.N = (double)c->n_total; f.p = c->p; f.q = c->q; f.r = r;
+  f.ldx = c->ldx; f.ldy = c->ldy; f.Wn = c->W[1]; f.Cn = c->C[1]; f.work = c->work; f.status = c->status;
+  f.logl_index = -1; f.qr = type == PPLS_ORTH_QR ? 1 : 0; f.mode = 1;   // polar only
+  HIPCHK(c, ppls_launch_finalize(&f, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if ((rc = check_status(c))) return rc;
+  // scalar updates on the given moments (EM_W_multi.R:734-738)
+  PplsMoments m;
+  memset(&m, 0, sizeof m);
+  for (int k = 0; k < r; ++k) { m.Ctt[k] = fit->Ctt[k]; m.Cut[k] = fit->Cut[k]; m.Cuu[k] = fit->Cuu ? fit->Cuu[k] : 0.0; }
+  m.Cee = fit->Cee;
+  m.Cff = fit->Cff;
+  for (int i = 0; i < r * r; ++i) m.Chh[i] = fit->Chh[i];
+  PplsScalars nx;
+  memset(&nx, 0, sizeof nx);
+  ppls_mstep_scalars(&m, r, &nx);
+  HIPCHK(c, hipMemcpy(c->sc[1], &nx, sizeof nx, hipMemcpyHostToDevice));
+  return download_theta(c, r, 1, out);
+}
+
+int ppls_loglik(ppls_ctx* c, const ppls_theta* th, int r, double* out) {
+  if (!c || !out) return PPLS_E_ARG;
+  if (!c->have_data) return fail(c, PPLS_E_STATE, "no data");
+  int rc;
+  if ((rc = check_theta(c, th, r))) return rc;
+  HIPCHK(c, hipSetDevice(c->device));
+  if ((rc = ensure_r(c, r, 1))) return rc;
+  if ((rc = upload_theta(c, th, r, 0))) return rc;
+  if ((rc = sweep(c, r, 0, false))) return rc;
+  if ((rc = finalize(c, r, 0, 1, 0, PPLS_ORTH_SVD))) return rc;
+  HIPCHK(c, hipMemcpyAsync(out, c->loglik, sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return PPLS_OK;
+}
+
+int ppls_em_run(ppls_ctx* c, ppls_theta* th, int r, int max_steps, double atol, int type, double* loglik,
+                int* steps_done, int* negative_increment, ppls_expect* eout) {
+  if (!c) return PPLS_E_ARG;
+  if (!c->have_data) return fail(c, PPLS_E_STATE, "no data");
+  int rc;
+  if ((rc = check_theta(c, th, r))) return rc;
+  if (max_steps < 1) return fail(c, PPLS_E_ARG, "EMsteps must be >= 1");
+  if (type != PPLS_ORTH_SVD && type != PPLS_ORTH_QR) return fail(c, PPLS_E_ARG, "type must be SVD (0) or QR (1)");
+  HIPCHK(c, hipSetDevice(c->device));
+  if ((rc = ensure_r(c, r, max_steps))) return rc;
+  // :773-778 canonicalise theta0 (on a copy; th is overwritten with the estimates at the end)
+  {
+    std::vector<double> W(th->W, th->W + (size_t)c->p * r), C(th->C, th->C + (size_t)c->q * r);
+    std::vector<double> B(th->B, th->B + r), T(th->sigT, th->sigT + r);
+    ppls_theta t0 = {W.data(), C.data(), B.data(), T.data(), th->sigE, th->sigF, th->sigH};
+    canonicalize(&t0, c->p, c->q, r);
+    if ((rc = upload_theta(c, &t0, r, 0))) return rc;
+  }
+  HIPCHK(c, hipMemsetAsync(c->status, 0, sizeof(int), c->stream));
+  const bool want_mu = eout && (eout->mu_T || eout->mu_U);
+  const bool do_check = !(atol == -INFINITY);   // atol = -Inf: the stop rule never fires
+  int cur = 0, i_final = max_steps;
+  std::vector<double> hl(max_steps + 2, NAN);
+  for (int s = 1; s <= max_steps + 1; ++s) {
+    const int nxt = cur ^ 1;
+    const bool wm = want_mu && (do_check || s == max_steps + 1);
+    if ((rc = sweep(c, r, cur, wm))) return rc;
+    if ((rc = finalize(c, r, cur, nxt, s >= 2 ? s - 2 : -1, type))) return rc;
+    if (do_check && s >= 3) {
+      // logl[i] - logl[i-1] < atol with i = s-1 (EM_W_multi.R:792)
+      HIPCHK(c, hipMemcpyAsync(&hl[s - 3], c->loglik + (s - 3), 2 * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+      if (hl[s - 2] - hl[s - 3] < atol) {
+        i_final = s - 1;
+        break;
+      }
+    }
+    if (s == max_steps + 1) break;
+    cur = nxt;
+  }
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if ((rc = check_status(c))) return rc;
+  if (loglik) HIPCHK(c, hipMemcpy(loglik, c->loglik, sizeof(double) * i_final, hipMemcpyDeviceToHost));
+  if (negative_increment) {
+    std::vector<double> l(i_final);
+    HIPCHK(c, hipMemcpy(l.data(), c->loglik, sizeof(double) * i_final, hipMemcpyDeviceToHost));
+    int neg = 0;
+    for (int i = 1; i < i_final; ++i) neg |= (l[i] - l[i - 1] < 0);
+    *negative_increment = neg;   // warning("Negative increments of likelihood"), :801
+  }
+  if (steps_done) *steps_done = i_final;
+  if ((rc = download_theta(c, r, cur, th))) return rc;
+  canonicalize(th, c->p, c->q, r);   // :794-799
+  if ((rc = download_moments(c, r, eout))) return rc;
+  return download_mu(c, r, eout);
+}
+
+int ppls_em_begin(ppls_ctx* c, const ppls_theta* th, int r) {
+  if (!c) return PPLS_E_ARG;
+  if (!c->have_data) return fail(c, PPLS_E_STATE, "no data");
+  int rc;
+  if ((rc = check_theta(c, th, r))) return rc;
+  HIPCHK(c, hipSetDevice(c->device));
+  if ((rc = ensure_r(c, r, 1 << 16))) return rc;
+  std::vector<double> W(th->W, th->W + (size_t)c->p * r), C(th->C, th->C + (size_t)c->q * r);
+  std::vector<double> B(th->B, th->B + r), T(th->sigT, th->sigT + r);
+  ppls_theta t0 = {W.data(), C.data(), B.data(), T.data(), th->sigE, th->sigF, th->sigH};
+  canonicalize(&t0, c->p, c->q, r);
+  if ((rc = upload_theta(c, &t0, r, 0))) return rc;
+  HIPCHK(c, hipMemsetAsync(c->status, 0, sizeof(int), c->stream));
+  c->em_r = r;
+  c->em_cur = 0;
+  c->em_iter = 0;
+  c->em_active = true;
+  return PPLS_OK;
+}
+
+int ppls_em_iterate(ppls_ctx* c, int nsteps, int type) {
+  if (!c) return PPLS_E_ARG;
+  if (!c->em_active || c->r_alloc != c->em_r) return fail(c, PPLS_E_STATE, "call ppls_em_begin first");
+  if (nsteps < 0) return fail(c, PPLS_E_ARG, "nsteps < 0");
+  if (c->em_iter + nsteps + 2 > c->loglik_cap) return fail(c, PPLS_E_ARG, "too many iterations for one run");
+  HIPCHK(c, hipSetDevice(c->device));
+  int rc;
+  for (int s = 0; s < nsteps; ++s) {
+    const int nxt = c->em_cur ^ 1;
+    if ((rc = sweep(c, c->em_r, c->em_cur, false))) return rc;
+    if ((rc = finalize(c, c->em_r, c->em_cur, nxt, c->em_iter >= 1 ? c->em_iter - 1 : -1, type))) return rc;
+    c->em_cur = nxt;
+    ++c->em_iter;
+  }
+  return PPLS_OK;
+}
+
+int ppls_em_state(ppls_ctx* c, ppls_theta* out, double* loglik, int cap, int* n_loglik) {
+  if (!c) return PPLS_E_ARG;
+  if (!c->em_active) return fail(c, PPLS_E_STATE, "call ppls_em_begin first");
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  int rc;
+  if ((rc = check_status(c))) return rc;
+  if (out && (rc = download_theta(c, c->em_r, c->em_cur, out))) return rc;
+  const int n = c->em_iter >= 1 ? c->em_iter - 1 : 0;
+  if (n_loglik) *n_loglik = n;
+  if (loglik && n > 0) HIPCHK(c, hipMemcpy(loglik, c->loglik, sizeof(double) * std::min(n, cap), hipMemcpyDeviceToHost));
+  return PPLS_OK;
+}
+
+int ppls_synchronize(ppls_ctx* c) {
+  if (!c) return PPLS_E_ARG;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return PPLS_OK;
+}
+
+int ppls_loglC_fast(ppls_ctx* c, const double* W, const double* C, const double* X, const double* Y, int64_t n,
+                    int p, int q, int a, double sigX, double sigY, const double* sig2T, const double* c1,
+                    const double* c2, const double* c3, const double* Kc, double* out) {
+  if (!c || !W || !C || !sig2T || !c1 || !c2 || !c3 || !Kc || !out) return c ? fail(c, PPLS_E_ARG, "NULL argument") : PPLS_E_ARG;
+  if (a < 1 || a > PPLS_RMAX) return fail(c, PPLS_E_ARG, "a=%d outside [1,%d]", a, PPLS_RMAX);
+  int rc;
+  if (X || Y) {
+    if (!X || !Y) return fail(c, PPLS_E_ARG, "X and Y must both be given or both be NULL");
+    if ((rc = ppls_set_data(c, X, Y, n, p, q, PPLS_LAYOUT_COLMAJOR, n))) return rc;
+  } else if (!c->have_data || c->p != p || c->q != q) {
+    return fail(c, PPLS_E_STATE, "no resident data of shape p=%d q=%d", p, q);
+  }
+  HIPCHK(c, hipSetDevice(c->device));
+  if ((rc = ensure_r(c, a, 1))) return rc;
+  std::vector<double> B(a, 0.0), T(a, 1.0);
+  ppls_theta th = {const_cast<double*>(W), const_cast<double*>(C), B.data(), T.data(), sigX, sigY, 0.0};
+  if ((rc = upload_theta(c, &th, a, 0))) return rc;
+  if ((rc = sweep(c, a, 0, false))) return rc;
+  std::vector<double> cf(5 * (size_t)a);
+  for (int k = 0; k < a; ++k) {
+    cf[k] = sig2T[k]; cf[a + k] = c1[k]; cf[2 * a + k] = c2[k]; cf[3 * a + k] = c3[k]; cf[4 * a + k] = Kc[k];
+  }
+  HIPCHK(c, hipMemcpyAsync(c->coefs, cf.data(), sizeof(double) * cf.size(), hipMemcpyHostToDevice, c->stream));
+  const double* G = c->stats + (int64_t)a * c->ldx + (int64_t)a * c->ldy;
+  HIPCHK(c, ppls_launch_loglc(G, c->ssq, (double)c->n_total, p, q, a, sigX, sigY, c->coefs, c->loglik, c->stream));
+  HIPCHK(c, hipMemcpyAsync(out, c->loglik, sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return PPLS_OK;
+}
+
+int ppls_sweep_timing(ppls_ctx* c, double* total_ms, int64_t* launches, int reset) {
+  if (!c) return PPLS_E_ARG;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  for (size_t i = 0; i < c->ev_used; ++i) {
+    float ms = 0.f;
+    HIPCHK(c, hipEventElapsedTime(&ms, c->ev[i].first, c->ev[i].second));
+    c->timed_ms += ms;
+    ++c->timed_launches;
+  }
+  c->ev_used = 0;
+  if (total_ms) *total_ms = c->timed_ms;
+  if (launches) *launches = c->timed_launches;
+  if (reset) { c->timed_ms = 0.0; c->timed_launches = 0; }
+  return PPLS_OK;
+}
+
+int ppls_sweep_info(ppls_ctx* c, int r, int64_t* bytes_per_sweep, int* variant, int* grid) {
+  if (!c) return PPLS_E_ARG;
+  int ns = 0;
+  const bool fused = use_fused(c, r, &ns);
+  if (bytes_per_sweep) *bytes_per_sweep = (int64_t)8 * c->n_local * ((int64_t)c->p + c->q);
+  if (variant) *variant = fused ? 1 : 2;
+  if (grid) *grid = grid_of(c);
+  return PPLS_OK;
+}
+
+int ppls_mu_coefficients(const ppls_theta* th, int r, double* coef) {
+  if (!th || !th->B || !th->sigT || !coef || r < 1 || r > PPLS_RMAX) return PPLS_E_ARG;
+  PplsScalars s = scalars_of(th, r);
+  for (int k = 0; k < r; ++k) {
+    coef[k] = s.alpha[k]; coef[r + k] = s.beta[k]; coef[2 * r + k] = s.gamma[k]; coef[3 * r + k] = s.delta[k];
+  }
+  return PPLS_OK;
+}
+
+int ppls_finalize_host(const double* SX, const double* SY, const double* G, double ssqX, double ssqY, double N,
+                       int p, int q, int r, const ppls_theta* th, int type, ppls_theta* next,
+                       ppls_expect* mom_out, double* loglik) {
+  if (!G || !th || !th->W || !th->C || !th->B || !th->sigT || r < 1 || r > PPLS_RMAX || p < 1 || q < 1)
+    return PPLS_E_ARG;
+  PplsScalars s = scalars_of(th, r);
+  double WtW[PPLS_RMAX * PPLS_RMAX], CtC[PPLS_RMAX * PPLS_RMAX];
+  for (int a = 0; a < r; ++a)
+    for (int b = 0; b < r; ++b) {
+      double w = 0.0, cc = 0.0;
+      for (int i = 0; i < p; ++i) w += th->W[(size_t)a * p + i] * th->W[(size_t)b * p + i];
+      for (int i = 0; i < q; ++i) cc += th->C[(size_t)a * q + i] * th->C[(size_t)b * q + i];
+      WtW[b * r + a] = w;
+      CtC[b * r + a] = cc;
+    }
+  if (loglik) *loglik = ppls_loglik_from_gram(G, ssqX, ssqY, N, p, q, r, &s);
+  PplsMoments m;
+  ppls_estep_moments(G, WtW, CtC, ssqX, ssqY, N, p, q, r, &s, &m);
+  if (mom_out) {
+    for (int k = 0; k < r; ++k) {
+      if (mom_out->Ctt) mom_out->Ctt[k] = m.Ctt[k];
+      if (mom_out->Cuu) mom_out->Cuu[k] = m.Cuu[k];
+      if (mom_out->Cut) mom_out->Cut[k] = m.Cut[k];
+    }
+    mom_out->Cee = m.Cee;
+    mom_out->Cff = m.Cff;
+    if (mom_out->Chh) memcpy(mom_out->Chh, m.Chh, sizeof(double) * r * r);
+  }
+  if (next) {
+    PplsScalars nx = s;
+    ppls_mstep_scalars(&m, r, &nx);
+    if (next->B) for (int k = 0; k < r; ++k) next->B[k] = nx.b[k];
+    if (next->sigT) for (int k = 0; k < r; ++k) next->sigT[k] = nx.t[k];
+    next->sigE = nx.sigE;
+    next->sigF = nx.sigF;
+    next->sigH = nx.sigH;
+    if (next->W && SX && host_orth(SX, p, r, type, next->W) != PPLS_OK) return PPLS_E_NUMERIC;
+    if (next->C && SY && host_orth(SY, q, r, type, next->C) != PPLS_OK) return PPLS_E_NUMERIC;
+  }
+  return PPLS_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,71 @@
+// ppls_kernels.h -- internal launch interface between the host runtime and the HIP kernels.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "ppls_math.h"
+
+#define PPLS_SWEEP_THREADS 512   // 8 waves, one workgroup per CU
+#define PPLS_SWEEP_SLOTS 4       // LDS-DMA ring depth (rows)
+#define PPLS_FUSED_RMAX 8
+
+struct PplsSweepArgs {
+  const double* X;
+  const double* Y;
+  int64_t n_local;
+  int ldx, ldy;          // leading dimensions (doubles, even)
+  const double* Wp;      // ldx x r column-major (padded rows are 0)
+  const double* Cp;      // ldy x r
+  const PplsScalars* sc; // device scalars (alpha..delta)
+  double* part;          // grid x part_ld partials
+  int64_t part_ld;       // r*ldx + r*ldy + 4 r^2
+  double* mu;            // n_local x 2r column-major [mu_T | mu_U] or nullptr
+  int write_mu;
+  int r;
+  int ns;                // column pairs per thread (fused)
+  int grid;              // workgroups (fused) / row chunks (two-pass)
+};
+
+struct PplsFinalizeArgs {
+  const double* stats;   // reduced [SX][SY][G]
+  const double* ssq;     // {||X||^2, ||Y||^2}
+  double N;
+  int p, q, r, ldx, ldy;
+  const double* Wc;
+  const double* Cc;
+  const PplsScalars* sc_cur;
+  double* Wn;
+  double* Cn;
+  PplsScalars* sc_nxt;
+  PplsMoments* mom;
+  double* loglik;
+  int logl_index;        // <0: do not write
+  double* work;          // 2 (p+q) r doubles
+  int* status;
+  int qr;                // orth type: 0 SVD (polar), 1 QR
+  int mode;              // bit0: W/C update (polar), bit1: scalars (moments, loglik, M-step)
+};
+
+extern "C" {
+int ppls_fused_supported(int r, int ldx, int ldy);
+size_t ppls_fused_lds_bytes(int r, int ldx, int ldy);
+hipError_t ppls_launch_sweep_fused(const PplsSweepArgs* a, hipStream_t st);
+hipError_t ppls_launch_sweep_twopass(const PplsSweepArgs* a, double* Z, hipStream_t st);
+hipError_t ppls_launch_accumulate(const PplsSweepArgs* a, const double* Z, hipStream_t st);
+int ppls_twopass_groups(int64_t n_local, int grid);
+hipError_t ppls_launch_reduce(const double* part, int ngroups, int64_t ld, int64_t len, double* out,
+                              int accumulate, hipStream_t st);
+hipError_t ppls_launch_finalize(const PplsFinalizeArgs* f, hipStream_t st);
+hipError_t ppls_launch_loglc(const double* G, const double* ssq, double N, int p, int q, int r,
+                             double sigX, double sigY, const double* coefs, double* out, hipStream_t st);
+hipError_t ppls_launch_sumsq(const double* a, int64_t len, double* part, int nblocks, double* out,
+                             int out_accumulate, hipStream_t st);
+hipError_t ppls_launch_generate(int64_t n_local, int64_t row0, int p, int q, int ldx, int ldy, int r,
+                                const PplsScalars* truth, const double* Wt, const double* Ct,
+                                uint64_t seed, double* TU, double* X, double* Y, hipStream_t st);
+hipError_t ppls_launch_to_rowmajor(const double* src, int64_t n, int p, int ld, double* dst,
+                                   hipStream_t st);
+hipError_t ppls_launch_to_colmajor(const double* src, int64_t n, int p, int ld, double* dst,
+                                   hipStream_t st);
+}

@@ -1,0 +1,289 @@
+// ppls_math.h -- O(r) / O(r^2) scalar algebra of one PPLS_simult EM step, shared verbatim by the
+// device finalize kernel and the host-side (CPU-testable) entry points.
+//
+// Everything here is derived from the one-pass sufficient statistics of a sweep:
+//   G  = [Xw Yc]'[Xw Yc]    (2r x 2r, column-major, ld = 2r)
+//   ssqX = ||X||^2, ssqY = ||Y||^2, N = total number of samples,
+//   WtW = W'W, CtC = C'C    (r x r) of the parameters the sweep used.
+// Reference lines restated (paths relative to /root/reference):
+//   coefficients          Package/PPLS/R/EM_W_multi.R:669-686 (Expect_M) and :312-320 (logl_W)
+//   mu coefficients       EM_W_multi.R:691-694
+//   E-step moments        EM_W_multi.R:696-716
+//   M-step scalars        EM_W_multi.R:734-738, tr() Package/PPLS/R/PJSC.R:1-5
+//   log-likelihood        Package/PPLS/src/loglC.cpp:318-338
+#pragma once
+
+#include <math.h>
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#define PPLS_HD __host__ __device__ inline
+#else
+#define PPLS_HD inline
+#endif
+
+#define PPLS_RMAX 16
+
+// Scalar parameters of theta plus the derived per-component coefficients the sweep consumes.
+struct PplsScalars {
+  double b[PPLS_RMAX];      // diag(B)
+  double t[PPLS_RMAX];      // diag(sigT)  (standard deviations, as in the reference)
+  double sigE, sigF, sigH;  // sigE == sigX, sigF == sigY
+  double pad0;
+  // mu_T[:,k] = alpha_k Xw_k + beta_k Yc_k ; mu_U[:,k] = gamma_k Xw_k + delta_k Yc_k
+  double alpha[PPLS_RMAX], beta[PPLS_RMAX], gamma[PPLS_RMAX], delta[PPLS_RMAX];
+};
+
+// Expectations returned by Expect_M (EM_W_multi.R:715-716); Ctt/Cuu/Cut are diagonal there.
+struct PplsMoments {
+  double Ctt[PPLS_RMAX], Cuu[PPLS_RMAX], Cut[PPLS_RMAX];
+  double Cee, Cff;
+  double Chh[PPLS_RMAX * PPLS_RMAX];  // full r x r, column-major, abs() applied
+};
+
+// Expect_M coefficient block, EM_W_multi.R:670-686.
+PPLS_HD void ppls_coef_estep(double t, double b, double sigE, double sigF, double sigH,
+                             double* c1, double* c2, double* c3, double* Kc_out) {
+  const double t2 = t * t, t4 = t2 * t2, t6 = t4 * t2, b2 = b * b;
+  const double sE2 = sigE * sigE, sF2 = sigF * sigF;
+  const double g = t2 * b2 + sigH * sigH;
+  const double Kw = t2 - t4 * b2 / sF2 + t4 * b2 * g / (sF2 * (g + sF2));
+  const double Kc = g - t4 * b2 / sE2 + t6 * b2 / (sE2 * (t2 + sE2));
+  const double Kwc = t2 * b / (sE2 * sF2) - Kc * t2 * b / (sE2 * sF2 * (Kc + sF2)) -
+                     t4 * b / (sE2 * sF2 * (t2 + sE2)) +
+                     Kc * t4 * b / (sE2 * sF2 * (Kc + sF2) * (t2 + sE2));
+  *c1 = Kw / (sE2 * (Kw + sE2));
+  *c3 = Kc / (sF2 * (Kc + sF2));
+  *c2 = Kwc;
+  if (Kc_out) *Kc_out = Kc;
+}
+
+// logl_W coefficient block, EM_W_multi.R:312-320: identical except g = sqrt(.) then squared.
+PPLS_HD void ppls_coef_logl(double t, double b, double sigX, double sigY, double sigH,
+                            double* c1, double* c2, double* c3, double* Kc_out) {
+  const double t2 = t * t, t4 = t2 * t2, t6 = t4 * t2, b2 = b * b;
+  const double sX2 = sigX * sigX, sY2 = sigY * sigY;
+  const double gs = sqrt(t2 * b2 + sigH * sigH);
+  const double g2 = gs * gs;
+  const double Kw = t2 - t4 * b2 / sY2 + t4 * b2 * g2 / (sY2 * (g2 + sY2));
+  const double Kc = g2 - t4 * b2 / sX2 + t6 * b2 / (sX2 * (t2 + sX2));
+  const double Kwc = t2 * b / (sX2 * sY2) - Kc * t2 * b / (sX2 * sY2 * (Kc + sY2)) -
+                     t4 * b / (sX2 * sY2 * (t2 + sX2)) +
+                     Kc * t4 * b / (sX2 * sY2 * (Kc + sY2) * (t2 + sX2));
+  *c1 = Kw / (sX2 * (Kw + sX2));
+  *c3 = Kc / (sY2 * (Kc + sY2));
+  *c2 = Kwc;
+  *Kc_out = Kc;
+}
+
+// alpha..delta of the per-row posterior means, EM_W_multi.R:691-694 collected per column.
+PPLS_HD void ppls_mu_coef(PplsScalars* s, int r) {
+  for (int k = 0; k < r; ++k) {
+    double c1, c2, c3;
+    ppls_coef_estep(s->t[k], s->b[k], s->sigE, s->sigF, s->sigH, &c1, &c2, &c3, nullptr);
+    const double t2 = s->t[k] * s->t[k], b = s->b[k];
+    const double v = t2 * b * b + s->sigH * s->sigH;   // varU, :688
+    const double iE = 1.0 / (s->sigE * s->sigE), iF = 1.0 / (s->sigF * s->sigF);
+    s->alpha[k] = iE * t2 - c1 * t2 - c2 * t2 * b;
+    s->beta[k] = iF * t2 * b - c2 * t2 - c3 * b * t2;
+    s->gamma[k] = iE * t2 * b - c1 * t2 * b - c2 * v;
+    s->delta[k] = iF * v - c2 * t2 * b - c3 * v;
+  }
+}
+
+// Gram accessors: G is 2r x 2r column-major; A = Xw'Xw, D = Xw'Yc, Bm = Yc'Yc.
+#define PPLS_GA(G, r, k, l) (G)[(size_t)(l) * (2 * (r)) + (k)]
+#define PPLS_GD(G, r, k, l) (G)[(size_t)((r) + (l)) * (2 * (r)) + (k)]
+#define PPLS_GB(G, r, k, l) (G)[(size_t)((r) + (l)) * (2 * (r)) + (r) + (k)]
+
+// Expect_M second moments (EM_W_multi.R:696-716) from the sufficient statistics of a sweep that
+// used theta = (W, C, s).  ssq(mu_E) and ssq(mu_F) are expanded exactly:
+//   ||X - sE^2 Z W'||^2 = ||X||^2 - 2 sE^2 tr(Z'Xw) + sE^4 tr(Z'Z W'W),  Z = Xw c1 + Yc c2.
+PPLS_HD void ppls_estep_moments(const double* G, const double* WtW, const double* CtC,
+                                double ssqX, double ssqY, double N, int64_t p, int64_t q, int r,
+                                const PplsScalars* s, PplsMoments* m) {
+  double c1[PPLS_RMAX], c2[PPLS_RMAX], c3[PPLS_RMAX];
+  for (int k = 0; k < r; ++k)
+    ppls_coef_estep(s->t[k], s->b[k], s->sigE, s->sigF, s->sigH, &c1[k], &c2[k], &c3[k], nullptr);
+  const double sE2 = s->sigE * s->sigE, sF2 = s->sigF * s->sigF, sH2 = s->sigH * s->sigH;
+  const double iE = 1.0 / sE2, iF = 1.0 / sF2;
+  for (int k = 0; k < r; ++k) {
+    const double t2 = s->t[k] * s->t[k], t4 = t2 * t2, b = s->b[k], b2 = b * b;
+    const double v = t2 * b2 + sH2;
+    const double A = PPLS_GA(G, r, k, k), D = PPLS_GD(G, r, k, k), Bm = PPLS_GB(G, r, k, k);
+    const double al = s->alpha[k], be = s->beta[k], ga = s->gamma[k], de = s->delta[k];
+    const double tt = al * al * A + 2.0 * al * be * D + be * be * Bm;   // crossprod(mu_T)_kk
+    const double uu = ga * ga * A + 2.0 * ga * de * D + de * de * Bm;   // crossprod(mu_U)_kk
+    const double ut = ga * al * A + (ga * be + de * al) * D + de * be * Bm;
+    const double Ctt = t2 - iE * t4 - iF * (t4 * b2) + t4 * c1[k] + 2.0 * (t4 * b * c2[k]) +
+                       t4 * b2 * c3[k] + tt / N;                                       // :696-697
+    const double Cuu = v - iE * (t4 * b2) - iF * (v * v) + t4 * b2 * c1[k] +
+                       2.0 * (t2 * b * v * c2[k]) + v * v * c3[k] + uu / N;            // :698-699
+    const double Cut = t2 * b - iE * (t4 * b) - iF * (t2 * b * v) + t4 * b * c1[k] +
+                       t2 * v * c2[k] + t4 * b2 * c2[k] + t2 * b * v * c3[k] + ut / N;  // :700-701
+    m->Ctt[k] = fabs(Ctt);   // abs(Ctt)*I, :715
+    m->Cuu[k] = fabs(Cuu);
+    m->Cut[k] = Cut;
+  }
+  // ssq(mu_E), ssq(mu_F) (:703-709)
+  double xz = 0.0, zz = 0.0, yz = 0.0, ww = 0.0, sc1 = 0.0, sc3 = 0.0;
+  for (int k = 0; k < r; ++k) {
+    xz += c1[k] * PPLS_GA(G, r, k, k) + c2[k] * PPLS_GD(G, r, k, k);
+    yz += c3[k] * PPLS_GB(G, r, k, k) + c2[k] * PPLS_GD(G, r, k, k);
+    sc1 += c1[k];
+    sc3 += c3[k];
+  }
+  for (int l = 0; l < r; ++l)
+    for (int k = 0; k < r; ++k) {
+      // (Z'Z)_kl with Z_k = c1_k a_k + c2_k b_k ; D(k,l) = sum a_k b_l
+      const double zkl = c1[k] * c1[l] * PPLS_GA(G, r, k, l) + c1[k] * c2[l] * PPLS_GD(G, r, k, l) +
+                         c2[k] * c1[l] * PPLS_GD(G, r, l, k) + c2[k] * c2[l] * PPLS_GB(G, r, k, l);
+      // (Z'_F Z_F)_kl with Z_F,k = c3_k b_k + c2_k a_k
+      const double fkl = c3[k] * c3[l] * PPLS_GB(G, r, k, l) + c3[k] * c2[l] * PPLS_GD(G, r, l, k) +
+                         c2[k] * c3[l] * PPLS_GD(G, r, k, l) + c2[k] * c2[l] * PPLS_GA(G, r, k, l);
+      zz += zkl * WtW[l * r + k];
+      ww += fkl * CtC[l * r + k];
+    }
+  const double ssqE = ssqX - 2.0 * sE2 * xz + sE2 * sE2 * zz;
+  const double ssqF = ssqY - 2.0 * sF2 * yz + sF2 * sF2 * ww;
+  const double pd = (double)p, qd = (double)q;
+  m->Cee = (pd * sE2 - pd * sE2 + sE2 * sE2 * sc1 + ssqE / N) / pd;   // :706
+  m->Cff = (qd * sF2 - qd * sF2 + sF2 * sF2 * sc3 + ssqF / N) / qd;   // :709
+  // Chh (:711-712): mu_H,k = h1_k Yc_k + h2_k Xw_k
+  for (int l = 0; l < r; ++l)
+    for (int k = 0; k < r; ++k) {
+      const double h1k = iF * sH2 - sH2 * c3[k], h2k = -sH2 * c2[k];
+      const double h1l = iF * sH2 - sH2 * c3[l], h2l = -sH2 * c2[l];
+      const double hh = h1k * h1l * PPLS_GB(G, r, k, l) + h1k * h2l * PPLS_GD(G, r, l, k) +
+                        h2k * h1l * PPLS_GD(G, r, k, l) + h2k * h2l * PPLS_GA(G, r, k, l);
+      double v = hh / N;
+      if (k == l) v = (sH2 - sH2 * sH2 / sF2) + sH2 * sH2 * c3[k] + v;
+      m->Chh[l * r + k] = fabs(v);   // abs(Chh), :716
+    }
+}
+
+// loglC_fast (loglC.cpp:318-338) for theta = (W, C, s) from the Gram of the sweep that used W, C.
+PPLS_HD double ppls_loglik_from_gram(const double* G, double ssqX, double ssqY, double N, int64_t p,
+                                     int64_t q, int r, const PplsScalars* s) {
+  const double sX2 = s->sigE * s->sigE, sY2 = s->sigF * s->sigF;
+  double logdet = 0.0, a1 = 0.0, a2 = 0.0;
+  double c1[PPLS_RMAX], c2[PPLS_RMAX], c3[PPLS_RMAX], Kc[PPLS_RMAX];
+  for (int k = 0; k < r; ++k) {
+    ppls_coef_logl(s->t[k], s->b[k], s->sigE, s->sigF, s->sigH, &c1[k], &c2[k], &c3[k], &Kc[k]);
+    a1 += log(sX2 + s->t[k] * s->t[k]);
+    a2 += log(sY2 + Kc[k]);
+  }
+  logdet = a1 + (double)(p - r) * log(sX2) + a2 + (double)(q - r) * log(sY2);   // :331
+  double traceL = 1.0 / sX2 * ssqX + 1.0 / sY2 * ssqY;                          // :334
+  for (int k = 0; k < r; ++k)                                                   // :335
+    traceL += -c1[k] * PPLS_GA(G, r, k, k) - 2.0 * c2[k] * PPLS_GD(G, r, k, k) -
+              c3[k] * PPLS_GB(G, r, k, k);
+  return -0.5 * N * (double)(p + q) * log(2.0 * M_PI) - 0.5 * N * logdet - 0.5 * traceL;  // :336
+}
+
+// Generic loglC_fast from explicit coefficient vectors (the drop-in for the .Call boundary).
+PPLS_HD double ppls_loglc_fast_from_gram(const double* G, double ssqX, double ssqY, double N,
+                                         int64_t p, int64_t q, int r, double sigX, double sigY,
+                                         const double* sig2T, const double* c1, const double* c2,
+                                         const double* c3, const double* Kc) {
+  const double sX2 = sigX * sigX, sY2 = sigY * sigY;
+  double a1 = 0.0, a2 = 0.0;
+  for (int k = 0; k < r; ++k) { a1 += log(sX2 + sig2T[k]); a2 += log(sY2 + Kc[k]); }
+  const double logdet = a1 + (double)(p - r) * log(sX2) + a2 + (double)(q - r) * log(sY2);
+  double traceL = 1.0 / sX2 * ssqX + 1.0 / sY2 * ssqY;
+  for (int k = 0; k < r; ++k)
+    traceL += -c1[k] * PPLS_GA(G, r, k, k) - 2.0 * c2[k] * PPLS_GD(G, r, k, k) -
+              c3[k] * PPLS_GB(G, r, k, k);
+  return -0.5 * N * (double)(p + q) * log(2.0 * M_PI) - 0.5 * N * logdet - 0.5 * traceL;
+}
+
+// Maximiz_M scalar updates, EM_W_multi.R:734-738.
+PPLS_HD void ppls_mstep_scalars(const PplsMoments* m, int r, PplsScalars* nx) {
+  double trChh = 0.0;
+  for (int k = 0; k < r; ++k) {
+    nx->b[k] = m->Cut[k] * (1.0 / m->Ctt[k]);   // Cut %*% solve(Ctt) * I
+    nx->t[k] = sqrt(m->Ctt[k]);                 // sqrt(Ctt * I)
+    trChh += m->Chh[k * r + k];
+  }
+  nx->sigE = sqrt(m->Cee / 1.0);
+  nx->sigF = sqrt(m->Cff / 1.0);
+  nx->sigH = sqrt(trChh / (double)r);
+  ppls_mu_coef(nx, r);
+}
+
+// Polar factor U_R V_R' of a small r x r matrix R (column-major, ld r) by one-sided (Hestenes)
+// Jacobi: R V = U S.  Returns 0 on success, -1 if R is numerically rank deficient.
+// P (r x r, column-major) receives U_R V_R'.
+PPLS_HD int ppls_small_polar(const double* R, int r, double* P) {
+  double A[PPLS_RMAX * PPLS_RMAX], V[PPLS_RMAX * PPLS_RMAX];
+  for (int i = 0; i < r * r; ++i) A[i] = R[i];
+  for (int j = 0; j < r; ++j)
+    for (int i = 0; i < r; ++i) V[j * r + i] = (i == j) ? 1.0 : 0.0;
+  for (int sweep = 0; sweep < 60; ++sweep) {
+    double off = 0.0;
+    for (int i = 0; i < r - 1; ++i)
+      for (int j = i + 1; j < r; ++j) {
+        double a = 0.0, b = 0.0, g = 0.0;
+        for (int k = 0; k < r; ++k) {
+          a += A[i * r + k] * A[i * r + k];
+          b += A[j * r + k] * A[j * r + k];
+          g += A[i * r + k] * A[j * r + k];
+        }
+        if (g == 0.0) continue;
+        const double rel = fabs(g) / sqrt(a * b);
+        if (rel > off) off = rel;
+        if (rel < 1e-17) continue;
+        const double zeta = (b - a) / (2.0 * g);
+        const double tt = (zeta >= 0.0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
+        const double c = 1.0 / sqrt(1.0 + tt * tt), sn = c * tt;
+        for (int k = 0; k < r; ++k) {
+          const double x = A[i * r + k], y = A[j * r + k];
+          A[i * r + k] = c * x - sn * y;
+          A[j * r + k] = sn * x + c * y;
+          const double vx = V[i * r + k], vy = V[j * r + k];
+          V[i * r + k] = c * vx - sn * vy;
+          V[j * r + k] = sn * vx + c * vy;
+        }
+      }
+    if (off < 1e-15) break;
+  }
+  double smax = 0.0, sv[PPLS_RMAX];
+  for (int i = 0; i < r; ++i) {
+    double nrm = 0.0;
+    for (int k = 0; k < r; ++k) nrm += A[i * r + k] * A[i * r + k];
+    sv[i] = sqrt(nrm);
+    if (sv[i] > smax) smax = sv[i];
+  }
+  int rc = 0;
+  for (int i = 0; i < r; ++i) {
+    if (!(sv[i] > smax * 1e-14)) { rc = -1; sv[i] = 1.0; }
+    for (int k = 0; k < r; ++k) A[i * r + k] /= sv[i];   // U_R column i
+  }
+  // P = U V'
+  for (int j = 0; j < r; ++j)
+    for (int i = 0; i < r; ++i) {
+      double acc = 0.0;
+      for (int k = 0; k < r; ++k) acc += A[k * r + i] * V[k * r + j];
+      P[j * r + i] = acc;
+    }
+  return rc;
+}
+
+// Sign/order canonicalisation, EM_W_multi.R:773-778 / :794-799.  Produces the permutation rot
+// (stable decreasing order of |t_k b_k|) and the signs sign(t_k b_k).
+PPLS_HD void ppls_canonical_order(const double* t, const double* b, int r, int* rot, double* sgn) {
+  double key[PPLS_RMAX];
+  for (int k = 0; k < r; ++k) {
+    const double sb = t[k] * b[k];
+    sgn[k] = (sb > 0.0) ? 1.0 : ((sb < 0.0) ? -1.0 : 0.0);
+    key[k] = t[k] * (b[k] * sgn[k]);
+    rot[k] = k;
+  }
+  // stable insertion sort, decreasing
+  for (int i = 1; i < r; ++i) {
+    const int cur = rot[i];
+    int j = i - 1;
+    while (j >= 0 && key[rot[j]] < key[cur]) { rot[j + 1] = rot[j]; --j; }
+    rot[j + 1] = cur;
+  }
+}

@@ -1,0 +1,53 @@
+"""Generate the golden fixtures of tests/golden/ from the CPU oracle (oracle/ppls_oracle.py).
+
+The reference (R + Rcpp/RcppEigen + OmicsPLS) cannot run in this image, so the vectors come
+from the oracle's line-by-line restatement, which tests/test_oracle.py pins against the
+reference's own identity checks and dense formulation.  Run from the repo root:
+    python tests/golden/make_golden.py
+"""
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+from conftest import make_problem  # noqa: E402
+from oracle import ppls_oracle as o  # noqa: E402
+
+CASES = [
+    # name, n, p, q, r, EMsteps, atol, type, seed
+    ("c1_n200_p50_q50_r2", 200, 50, 50, 2, 10, float("-inf"), "SVD", 1),
+    ("r1_n150_p30_q20", 150, 30, 20, 1, 10, float("-inf"), "SVD", 2),
+    ("r5_n300_p41_q37", 300, 41, 37, 5, 8, float("-inf"), "SVD", 3),
+    ("qr_n200_p24_q18_r3", 200, 24, 18, 3, 6, float("-inf"), "QR", 4),
+    ("atol_n250_p20_q16_r2", 250, 20, 16, 2, 300, 5e-3, "SVD", 5),
+]
+
+
+def main():
+    here = os.path.dirname(os.path.abspath(__file__))
+    for name, n, p, q, r, steps, atol, typ, seed in CASES:
+        X, Y, th0 = make_problem(n, p, q, r, seed=seed)
+        res = o.ppls_simult(X, Y, r, EMsteps=steps, atol=atol, type=typ, theta0=th0)
+        one = o.ppls_simult(X, Y, r, EMsteps=1, atol=atol, type=typ, theta0=th0)
+        two = o.ppls_simult(X, Y, r, EMsteps=2, atol=atol, type=typ, theta0=th0)
+        est, E = res["estimates"], res["Expectations"]
+        meta = dict(n=n, p=p, q=q, r=r, EMsteps=steps, atol=atol, type=typ, seed=seed,
+                    steps_done=int(len(res["loglik"])))
+        np.savez_compressed(
+            os.path.join(here, name + ".npz"), meta=json.dumps(meta), X=X, Y=Y,
+            W0=th0["W"], C0=th0["C"], B0=np.diag(th0["B"]), T0=np.diag(th0["sigT"]),
+            sig0=np.array([th0["sigE"], th0["sigF"], th0["sigH"]]),
+            loglik=res["loglik"], W=est["W"], C=est["C"], B=np.diag(est["B"]), T=np.diag(est["sigT"]),
+            sig=np.array([est["sigE"], est["sigF"], est["sigH"]]),
+            W1=one["estimates"]["W"], loglik1=one["loglik"], W2=two["estimates"]["W"], loglik2=two["loglik"],
+            mu_T=E["mu_T"], mu_U=E["mu_U"], Ctt=np.diag(E["Ctt"]), Cuu=np.diag(E["Cuu"]),
+            Cut=np.diag(E["Cut"]), Cee=E["Cee"][0, 0], Cff=E["Cff"][0, 0], Chh=E["Chh"])
+        print(name, "steps", len(res["loglik"]), "loglik", res["loglik"][-1])
+
+
+if __name__ == "__main__":
+    main()

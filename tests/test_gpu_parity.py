@@ -1,0 +1,217 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU oracle and the golden fixtures.
+
+Tolerances (fp64 throughout): log-likelihood 1e-10 relative; loadings W, C 1e-8 absolute on
+unit-norm columns (BASELINE.json: "loadings within 1e-8 rel-err"); variances / B / sigT 1e-8
+relative; moments 1e-9 relative.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import make_problem
+from oracle import ppls_oracle as o
+
+pytestmark = pytest.mark.gpu
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+SWEEPS = [1, 2]   # 1 = fused single-pass kernel, 2 = generic two-pass kernels
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    from ppls_amd import Context
+    c = Context(0)
+    yield c
+    c.close()
+
+
+def _theta(th):
+    from ppls_amd import Theta
+    return Theta(th["W"], th["C"], th["B"], th["sigE"], th["sigF"], th["sigH"], th["sigT"])
+
+
+def _relerr(a, b):
+    a, b = np.asarray(a, dtype=float), np.asarray(b, dtype=float)
+    return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-300))
+
+
+def _golden():
+    return sorted(f for f in os.listdir(GOLD) if f.endswith(".npz"))
+
+
+@pytest.mark.parametrize("sweep", SWEEPS)
+@pytest.mark.parametrize("name", _golden())
+def test_em_run_matches_golden(ctx, name, sweep):
+    g = np.load(os.path.join(GOLD, name))
+    meta = json.loads(str(g["meta"]))
+    ctx.set_option("sweep", sweep)
+    ctx.set_option("grid", 0)
+    ctx.set_data(g["X"], g["Y"])
+    th0 = dict(W=g["W0"], C=g["C0"], B=np.diag(g["B0"]), sigE=g["sig0"][0], sigF=g["sig0"][1],
+               sigH=g["sig0"][2], sigT=np.diag(g["T0"]))
+    typ = 0 if meta["type"] == "SVD" else 1
+    est, ll, eout, neg = ctx.em_run(_theta(th0), meta["EMsteps"], meta["atol"], typ)
+    assert len(ll) == meta["steps_done"]
+    assert _relerr(ll, g["loglik"]) < 1e-10
+    assert np.abs(est.W - g["W"]).max() < 1e-8
+    assert np.abs(est.C - g["C"]).max() < 1e-8
+    assert _relerr(est.B, g["B"]) < 1e-8
+    assert _relerr(est.sigT, g["T"]) < 1e-8
+    assert _relerr([est.sigE, est.sigF, est.sigH], g["sig"]) < 1e-8
+    assert _relerr(eout.mu_T, g["mu_T"]) < 1e-8
+    assert _relerr(eout.mu_U, g["mu_U"]) < 1e-8
+    assert _relerr(eout.Ctt, g["Ctt"]) < 1e-8
+    assert _relerr(eout.Cut, g["Cut"]) < 1e-8
+    assert _relerr(eout.Chh, g["Chh"]) < 1e-8
+    assert abs(eout.Cee - g["Cee"]) / g["Cee"] < 1e-8
+    assert abs(eout.Cff - g["Cff"]) / g["Cff"] < 1e-8
+    assert not neg
+
+
+@pytest.mark.parametrize("sweep", SWEEPS)
+@pytest.mark.parametrize("n,p,q,r", [(200, 50, 50, 2), (97, 33, 7, 1), (301, 64, 31, 5), (50, 9, 12, 8),
+                                     (3, 5, 4, 2), (1, 6, 3, 1), (700, 1025, 3, 2), (400, 2, 1500, 3)])
+def test_estep_mstep_loglik_vs_oracle(ctx, sweep, n, p, q, r):
+    X, Y, th0 = make_problem(n, p, q, r, seed=n + p + q + r)
+    ctx.set_option("sweep", sweep)
+    ctx.set_data(X, Y)
+    th = _theta(th0)
+    e = ctx.estep(th)
+    ref = o.expect_m(X, Y, th0["W"], th0["C"], th0["B"], th0["sigE"], th0["sigF"], th0["sigH"], th0["sigT"])
+    assert _relerr(e.mu_T, ref["mu_T"]) < 1e-11
+    assert _relerr(e.mu_U, ref["mu_U"]) < 1e-11
+    assert _relerr(e.Ctt, np.diag(ref["Ctt"])) < 1e-10
+    assert _relerr(e.Cuu, np.diag(ref["Cuu"])) < 1e-10
+    assert _relerr(e.Cut, np.diag(ref["Cut"])) < 1e-10
+    assert abs(e.Cee - ref["Cee"][0, 0]) / ref["Cee"][0, 0] < 1e-10
+    assert abs(e.Cff - ref["Cff"][0, 0]) / ref["Cff"][0, 0] < 1e-10
+    assert _relerr(e.Chh, ref["Chh"]) < 1e-9
+    if n >= r:
+        nx, _ = ctx.em_step(th)
+        m = o.maximiz_m(ref, X, Y)
+        assert np.abs(nx.W - m["W"]).max() < 1e-10
+        assert np.abs(nx.C - m["C"]).max() < 1e-10
+        assert _relerr(nx.B, np.diag(m["B"])) < 1e-10
+        assert _relerr(nx.sigT, np.diag(m["sigT"])) < 1e-10
+        assert _relerr([nx.sigE, nx.sigF, nx.sigH], [m["sigE"], m["sigF"], m["sigH"]]) < 1e-10
+        # Maximiz_M from an explicit fit (the accumulate pass with mu given)
+        mm = ctx.mstep(e)
+        assert np.abs(mm.W - m["W"]).max() < 1e-10
+        assert np.abs(mm.C - m["C"]).max() < 1e-10
+    ll = ctx.loglik(th)
+    ref_ll = o.logl_w(X, Y, th0["W"], th0["C"], th0["B"], th0["sigE"], th0["sigF"], th0["sigH"], th0["sigT"])
+    assert abs(ll - ref_ll) / abs(ref_ll) < 1e-11
+
+
+def test_loglC_fast_dropin(ctx):
+    from ppls_amd import loglC_fast
+    X, Y, th0 = make_problem(123, 20, 15, 3, seed=77)
+    cf = o.logl_coefficients(th0["B"], th0["sigE"], th0["sigF"], th0["sigH"], th0["sigT"])
+    args = (th0["W"], th0["C"], X, Y, th0["sigE"], th0["sigF"], cf["sig2T"], cf["c1"], cf["c2"], cf["c3"], cf["Kc"])
+    ref = o.loglc_fast(*args)
+    got = loglC_fast(*args, ctx=ctx)
+    assert abs(got - ref) / abs(ref) < 1e-12
+    # zero-copy form on resident data
+    got2 = ctx.loglC_fast(th0["W"], th0["C"], None, None, *args[4:])
+    assert abs(got2 - ref) / abs(ref) < 1e-12
+
+
+def test_colmajor_and_rowmajor_uploads_agree(ctx):
+    X, Y, th0 = make_problem(150, 21, 19, 2, seed=5)
+    ctx.set_option("sweep", 0)
+    ctx.set_data(np.asfortranarray(X), np.asfortranarray(Y))
+    a = ctx.estep(_theta(th0))
+    Xb, Yb = ctx.get_data()
+    assert np.array_equal(Xb, X) and np.array_equal(Yb, Y)
+    ctx.set_data(np.ascontiguousarray(X), np.ascontiguousarray(Y))
+    b = ctx.estep(_theta(th0))
+    assert np.array_equal(a.mu_T, b.mu_T) and a.Cee == b.Cee
+
+
+@pytest.mark.parametrize("grid", [1, 7, 256, 1000])
+def test_grid_invariance(ctx, grid):
+    X, Y, th0 = make_problem(2000, 130, 90, 3, seed=11)
+    ctx.set_option("sweep", 1)
+    ctx.set_data(X, Y)
+    ctx.set_option("grid", 0)
+    a = ctx.estep(_theta(th0))
+    ctx.set_option("grid", grid)
+    b = ctx.estep(_theta(th0))
+    ctx.set_option("grid", 0)
+    assert _relerr(b.Ctt, a.Ctt) < 1e-12 and _relerr(b.Chh, a.Chh) < 1e-11
+    assert np.array_equal(a.mu_T, b.mu_T)
+
+
+def test_fused_and_twopass_agree_midsize(ctx):
+    from ppls_amd import Theta
+    p, q, r = 600, 500, 3
+    rng = np.random.default_rng(1)
+    W = np.linalg.qr(rng.standard_normal((p, r)))[0]
+    C = np.linalg.qr(rng.standard_normal((q, r)))[0]
+    truth = Theta(W, C, np.exp(np.log(1.5) - 0.3 * np.arange(r)), 0.5, 0.5, 0.1, np.exp(-0.1 * np.arange(r)))
+    ctx.generate_synthetic(30000, p, q, truth, seed=20261015)
+    th0 = _theta(dict(W=np.linalg.qr(rng.standard_normal((p, r)))[0], C=np.linalg.qr(rng.standard_normal((q, r)))[0],
+                      B=np.eye(r), sigE=1.0, sigF=1.0, sigH=1.0, sigT=np.eye(r)))
+    out = {}
+    for sw in (1, 2):
+        ctx.set_option("sweep", sw)
+        out[sw] = ctx.em_run(th0, 6, -np.inf, 0)
+    (e1, l1, x1, _), (e2, l2, x2, _) = out[1], out[2]
+    assert _relerr(l1, l2) < 1e-12
+    assert np.abs(e1.W - e2.W).max() < 1e-10
+    assert np.all(np.diff(l1) > 0)
+    # against the oracle on the same (copied back) data
+    X, Y = ctx.get_data()
+    ref = o.ppls_simult(X, Y, r, EMsteps=6, atol=-np.inf, theta0=th0.as_dict())
+    assert _relerr(l1, ref["loglik"]) < 1e-10
+    assert np.abs(e1.W - ref["estimates"]["W"]).max() < 1e-8
+    assert np.abs(e1.C - ref["estimates"]["C"]).max() < 1e-8
+    ctx.set_option("sweep", 0)
+
+
+def test_synthetic_generator_properties(ctx):
+    from ppls_amd import Context, Theta
+    p, q, r, n = 40, 30, 2, 5000
+    rng = np.random.default_rng(2)
+    W = np.linalg.qr(rng.standard_normal((p, r)))[0]
+    C = np.linalg.qr(rng.standard_normal((q, r)))[0]
+    truth = Theta(W, C, [1.5, 1.1], 0.5, 0.5, 0.1, [1.0, 0.9])
+    ctx.generate_synthetic(n, p, q, truth, seed=7)
+    X, Y = ctx.get_data()
+    ctx.generate_synthetic(n, p, q, truth, seed=7)
+    X2, _ = ctx.get_data()
+    assert np.array_equal(X, X2)                                  # deterministic
+    # shard invariance: rows [1000, 3000) generated as a shard are bit-identical
+    ctx.generate_synthetic(n, p, q, truth, seed=7, row0=1000, n_local=2000)
+    Xs, Ys = ctx.get_data()
+    assert np.array_equal(Xs, X[1000:3000]) and np.array_equal(Ys, Y[1000:3000])
+    # model moments: Cov(X) = W diag(t^2) W' + sigE^2 I
+    S = X.T @ X / n
+    ref = W @ np.diag([1.0, 0.81]) @ W.T + 0.25 * np.eye(p)
+    assert np.abs(S - ref).max() < 0.12
+    ssx, ssy = ctx.ssq()
+    assert abs(ssx - np.sum(Xs * Xs)) / ssx < 1e-12
+
+
+def test_monotone_em_c2_shape(ctx):
+    """Size-independent properties at BASELINE config C2 (n=1e5, p=q=1000, r=3)."""
+    from ppls_amd import Theta
+    p = q = 1000
+    r, n = 3, 100_000
+    rng = np.random.default_rng(3)
+    W = np.linalg.qr(rng.standard_normal((p, r)))[0]
+    C = np.linalg.qr(rng.standard_normal((q, r)))[0]
+    truth = Theta(W, C, np.exp(np.log(1.5) - 0.3 * np.arange(r)), 0.5, 0.5, 0.1, np.exp(-0.1 * np.arange(r)))
+    ctx.set_option("sweep", 0)
+    ctx.generate_synthetic(n, p, q, truth, seed=20261015)
+    th0 = _theta(dict(W=np.linalg.qr(rng.standard_normal((p, r)))[0], C=np.linalg.qr(rng.standard_normal((q, r)))[0],
+                      B=np.eye(r), sigE=1.0, sigF=1.0, sigH=1.0, sigT=np.eye(r)))
+    est, ll, eout, neg = ctx.em_run(th0, 8, -np.inf, 0, want_mu=False)
+    assert len(ll) == 8 and not neg and np.all(np.diff(ll) > 0)
+    assert np.abs(est.W.T @ est.W - np.eye(r)).max() < 1e-12
+    assert np.abs(est.C.T @ est.C - np.eye(r)).max() < 1e-12
+    # EM approaches the truth
+    assert np.all(np.abs(np.diag(est.W.T @ W)) > 0.99)
+    assert abs(est.sigE - 0.5) < 0.01
