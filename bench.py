@@ -67,15 +67,18 @@ def cpu_baseline(ctx, th0, cfg, seconds_target=15.0):
     identical sample."""
     from oracle import cpu_ref
     from ppls_amd import Context
-    n_s = min(ctx.n_local, 20000)
-    X, Y = ctx.get_data(0, n_s)
-    Xs, Ys = np.ascontiguousarray(X), np.ascontiguousarray(Y)
     th = th0.as_dict()
     cores = cpu_ref.load().cpu_ref_max_threads()
+    n_probe = min(ctx.n_local, 5000)
+    X, Y = ctx.get_data(0, n_probe)
     t0 = time.perf_counter()
-    cpu_ref.em_steps(Xs, Ys, th, 1)
-    t1 = time.perf_counter() - t0
-    steps = int(max(2, min(20, seconds_target / max(t1, 1e-3))))
+    cpu_ref.em_steps(np.ascontiguousarray(X), np.ascontiguousarray(Y), th, 1)
+    per_row_iter = (time.perf_counter() - t0) / n_probe
+    n_s = int(min(ctx.n_local, 150_000))
+    steps = int(min(200, max(2, seconds_target / (n_s * per_row_iter))))
+    X, Y = ctx.get_data(0, n_s)
+    Xs, Ys = np.ascontiguousarray(X), np.ascontiguousarray(Y)
+    del X, Y
     t0 = time.perf_counter()
     th_cpu, ll_cpu = cpu_ref.em_steps(Xs, Ys, th, steps)
     dt = time.perf_counter() - t0
@@ -85,7 +88,9 @@ def cpu_baseline(ctx, th0, cfg, seconds_target=15.0):
         c2.set_data(Xs, Ys)
         est, ll_gpu, _, _ = c2.em_run(th0, steps, -np.inf, 0, want_eout=False)
     rel = float(np.abs(ll_gpu - ll_cpu).max() / np.abs(ll_cpu).max())
-    werr = float(np.abs(est.W - th_cpu["W"]).max())
+    from oracle.ppls_oracle import canonicalize   # the GPU estimates are canonicalised (:794-799)
+    Wc, _, _, _ = canonicalize(th_cpu["W"], th_cpu["C"], th_cpu["B"], th_cpu["sigT"])
+    werr = float(np.abs(est.W - Wc).max())
     return dict(value=row_iters_per_s / cfg["n"], unit="EM iterations/s", cores=int(cores), kind="port",
                 sample=f"{steps} EM iterations on the first {n_s} of n={cfg['n']} rows in {dt:.1f} s "
                        f"(oracle/cpu_ref.c, reference pass structure, OpenMP {cores} threads, -O3 "
@@ -106,6 +111,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--sweep", type=int, default=0, help="0 auto, 1 fused, 2 two-pass")
+    ap.add_argument("--threads", type=int, default=0, help="fused workgroup size: 0 auto, 512, 1024")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     args = ap.parse_args()
@@ -128,6 +134,7 @@ def main():
     ctx = Context(local)
     _DEVICE[id(ctx)] = local
     ctx.set_option("sweep", args.sweep)
+    ctx.set_option("threads", args.threads)
     if world > 1:
         uid = [Context.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)

@@ -28,6 +28,9 @@ struct ppls_ctx {
   // options
   int sweep_mode = 0;
   int grid_opt = 0;
+  int threads_opt = 0;
+  int rp_opt = 0;   // rows per pipeline step: 0 auto (2 where the kernel fits in registers)
+  int ablate = 0;
   int timing = 0;
   // communicator
   ncclComm_t comm = nullptr;
@@ -124,6 +127,9 @@ int check_theta(ppls_ctx* c, const ppls_theta* th, int r) {
   if (r < 1 || r > PPLS_RMAX) return fail(c, PPLS_E_ARG, "r=%d outside [1,%d]", r, PPLS_RMAX);
   if (!(th->sigE > 0) || !(th->sigF > 0) || !(th->sigH >= 0))
     return fail(c, PPLS_E_ARG, "variances must be positive");
+  // PPLS: stopifnot(ncol(X) >= nr_comp, ncol(Y) >= nr_comp)  (EM_W_multi.R:245)
+  if (c && c->p > 0 && (c->p < r || c->q < r))
+    return fail(c, PPLS_E_ARG, "ncol(X)=%d, ncol(Y)=%d must be >= number of components %d", c->p, c->q, r);
   return PPLS_OK;
 }
 
@@ -229,8 +235,13 @@ int download_mu(ppls_ctx* c, int r, ppls_expect* e) {
   return PPLS_OK;
 }
 
-bool use_fused(ppls_ctx* c, int r, int* ns) {
-  *ns = ppls_fused_supported(r, c->ldx, c->ldy);
+// Fused workgroup size: option "threads" (512 / 1024) is a preference that falls back to the other
+// size when unsupported; auto = 512 (measured faster than 1024 at every shape tried).
+bool use_fused(ppls_ctx* c, int r, int* ns, int* threads) {
+  int t = c->threads_opt ? c->threads_opt : 512;
+  if (!ppls_fused_supported(r, c->ldx, c->ldy, t)) t = (t == 512) ? 1024 : 512;
+  *threads = t;
+  *ns = ppls_fused_supported(r, c->ldx, c->ldy, t);
   if (c->sweep_mode == 2) return false;
   return *ns > 0;
 }
@@ -246,8 +257,8 @@ int allreduce(ppls_ctx* c, double* buf, size_t count) {
 
 // One sweep with theta[slot] -> c->stats (all-reduced).
 int sweep(ppls_ctx* c, int r, int slot, bool write_mu) {
-  int rc, ns = 0;
-  const bool fused = use_fused(c, r, &ns);
+  int rc, ns = 0, threads = 512;
+  const bool fused = use_fused(c, r, &ns, &threads);
   const int grid = grid_of(c);
   const int groups = fused ? grid : ppls_twopass_groups(std::max<int64_t>(c->n_local, 1), grid);
   if (groups > c->part_groups || !c->part) {
@@ -276,7 +287,10 @@ int sweep(ppls_ctx* c, int r, int slot, bool write_mu) {
     a.write_mu = write_mu ? 1 : 0;
     a.r = r;
     a.ns = ns;
+    a.threads = threads;
     a.grid = grid;
+    a.ablate = c->ablate;
+    a.rp = (c->rp_opt != 1 && ns == 1 && r <= 4 && threads == 512) ? 2 : 1;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (c->timing) {
       if (c->ev_used == c->ev.size()) {
@@ -499,6 +513,15 @@ int ppls_set_option(ppls_ctx* c, const char* key, int64_t value) {
     c->grid_opt = (int)value;
     c->part_groups = 0;
     dfree(c->part);
+  } else if (!strcmp(key, "threads")) {
+    if (value != 0 && value != 512 && value != 1024) return fail(c, PPLS_E_ARG, "threads must be 0, 512 or 1024");
+    c->threads_opt = (int)value;
+  } else if (!strcmp(key, "rows_per_step")) {
+    if (value < 0 || value > 2) return fail(c, PPLS_E_ARG, "rows_per_step must be 0 (auto), 1 or 2");
+    c->rp_opt = (int)value;
+  } else if (!strcmp(key, "ablate")) {
+    if (value < 0 || value > 3) return fail(c, PPLS_E_ARG, "ablate must be in [0,3]");
+    c->ablate = (int)value;   // timing experiments only: results are wrong while set
   } else if (!strcmp(key, "timing")) {
     c->timing = value ? 1 : 0;
   } else {
@@ -901,10 +924,10 @@ int ppls_sweep_timing(ppls_ctx* c, double* total_ms, int64_t* launches, int rese
 
 int ppls_sweep_info(ppls_ctx* c, int r, int64_t* bytes_per_sweep, int* variant, int* grid) {
   if (!c) return PPLS_E_ARG;
-  int ns = 0;
-  const bool fused = use_fused(c, r, &ns);
+  int ns = 0, threads = 512;
+  const bool fused = use_fused(c, r, &ns, &threads);
   if (bytes_per_sweep) *bytes_per_sweep = (int64_t)8 * c->n_local * ((int64_t)c->p + c->q);
-  if (variant) *variant = fused ? 1 : 2;
+  if (variant) *variant = fused ? (threads == 1024 ? 3 : 1) : 2;
   if (grid) *grid = grid_of(c);
   return PPLS_OK;
 }

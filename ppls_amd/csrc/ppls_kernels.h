@@ -24,7 +24,10 @@ struct PplsSweepArgs {
   int write_mu;
   int r;
   int ns;                // column pairs per thread (fused)
+  int threads;           // fused workgroup size: 512 or 1024
+  int rp;                // fused rows per pipeline step (1 or 2)
   int grid;              // workgroups (fused) / row chunks (two-pass)
+  int ablate;            // timing experiments only (fused): 1 no compute, 2 no HBM copies
 };
 
 struct PplsFinalizeArgs {
@@ -48,8 +51,8 @@ struct PplsFinalizeArgs {
 };
 
 extern "C" {
-int ppls_fused_supported(int r, int ldx, int ldy);
-size_t ppls_fused_lds_bytes(int r, int ldx, int ldy);
+int ppls_fused_supported(int r, int ldx, int ldy, int threads);
+size_t ppls_fused_lds_bytes(int r, int ldx, int ldy, int threads);
 hipError_t ppls_launch_sweep_fused(const PplsSweepArgs* a, hipStream_t st);
 hipError_t ppls_launch_sweep_twopass(const PplsSweepArgs* a, double* Z, hipStream_t st);
 hipError_t ppls_launch_accumulate(const PplsSweepArgs* a, const double* Z, hipStream_t st);

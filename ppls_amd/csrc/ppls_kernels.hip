@@ -170,9 +170,15 @@ __global__ void ppls_reduce_partials_kernel(const double* __restrict__ part, int
                                             int64_t len, double* __restrict__ out, int accumulate) {
   const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= len) return;
-  double s = 0.0;
-  for (int g = 0; g < ngroups; ++g) s += part[(int64_t)g * ld + j];
-  out[j] = accumulate ? out[j] + s : s;
+  double s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  int g = 0;
+  for (; g + 8 <= ngroups; g += 8) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s[u] += part[(int64_t)(g + u) * ld + j];
+  }
+  for (int u = 0; g < ngroups; ++g, ++u) s[u] += part[(int64_t)g * ld + j];
+  const double t = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
+  out[j] = accumulate ? out[j] + t : t;
 }
 
 // ============================================================================ wave reduce-scatter
@@ -274,38 +280,48 @@ __device__ __forceinline__ void ppls_lds_barrier() {
 }
 
 // ============================================================================ fused sweep
-// One workgroup (512 threads, one per CU) owns a contiguous block of rows. Each thread owns NS
+// One workgroup (NT threads, one per CU) owns a contiguous block of rows.  Each thread owns NS
 // column pairs of X and NS of Y for the whole sweep: it keeps W/C for those columns and the
-// X'mu_T / Y'mu_U accumulators in registers.  Rows stream HBM -> LDS through a SLOTS-deep ring
-// of LDS-DMA (global_load_lds_dwordx4) copies; per row: partial dots -> wave reduce-scatter ->
-// cross-wave sum in LDS -> mu_T/mu_U (registers) -> rank-1 update of the accumulators, plus the
-// 2r x 2r Gram of [Xw Yc].  X and Y are read from HBM exactly once.
-template <int R, int NS, int SLOTS>
-__global__ __launch_bounds__(PPLS_SWEEP_THREADS, 2) void ppls_sweep_fused_kernel(
+// X'mu_T / Y'mu_U accumulators in registers.  Rows stream HBM -> LDS through a ring of SLOTS row
+// slots filled by LDS-DMA (global_load_lds_dwordx4; the first ceil(nch/CPW) waves copy CPW 1-KiB
+// chunks of every row, so the steady-state vmcnt is a compile-time immediate).  The loop handles
+// RP rows per step, software-pipelined: step g sums group g's dots (cross-wave, LDS), computes
+// group g+1's dots + wave reduce-scatter, then applies group g's rank-RP update -- ONE workgroup
+// barrier per step (reduction scratch double-buffered).  mu_T / mu_U and [Xw Yc] rows are
+// broadcast through a per-wave LDS scratch (no readlane / SGPR traffic).  X, Y are read once.
+template <int R, int NS, int NT, int RP, int SLOTS, int CPW>
+__global__ __launch_bounds__(NT, 2 * NT / 512) void ppls_sweep_fused_kernel(
     const double* __restrict__ X, const double* __restrict__ Y, int64_t n_local, int ldx, int ldy,
     const double* __restrict__ Wp, const double* __restrict__ Cp, const PplsScalars* __restrict__ sc,
-    double* __restrict__ part, int64_t part_ld, double* __restrict__ mu, int write_mu) {
+    double* __restrict__ part, int64_t part_ld, double* __restrict__ mu, int write_mu, int ablate) {
+  // ablate (timing experiments only; results are garbage): bit0 skips the per-row compute,
+  // bit1 skips the HBM->LDS copies.
+  static_assert(SLOTS >= 2 * RP, "ring must hold the group being read and the group in flight");
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int V = 2 * R;
-  constexpr int VP = (V < 2) ? 2 : V + (V & 1) + 2;   // reduce-scatter scratch (pads)
-  constexpr int NWAVES = PPLS_SWEEP_THREADS / 64;
+  constexpr int V = 2 * R * RP;                       // partial dots per thread per step
+  constexpr int VP = V;                               // reduce-scatter scratch (V is even)
+  constexpr int NWAVES = NT / 64;
+  constexpr int AHEAD = SLOTS / RP - 2;               // groups in flight beyond the next one
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int nchx = (ldx * 8 + 1023) >> 10, nchy = (ldy * 8 + 1023) >> 10;
   const int nch = nchx + nchy;
   const int slot_bytes = nch << 10;
-  const int ndma = (nch + NWAVES - 1) / NWAVES;
-  double* red = (double*)(smem + (size_t)SLOTS * slot_bytes);
+  const bool dma_wave = wave * CPW < nch;
+  double* red = (double*)(smem + (size_t)SLOTS * slot_bytes);          // [2][NWAVES][V]
+  double* bc = red + 2 * NWAVES * V + wave * V;                       // per wave: [Xw Yc] rows
+  double* cf = red + 3 * NWAVES * V;                                  // alpha | beta | gamma | delta
   const int64_t g = blockIdx.x, G = gridDim.x;
   const int64_t rb = n_local * g / G, re = n_local * (g + 1) / G;
   const int nrows = (int)(re - rb);
+  const int ngroups = (nrows + RP - 1) / RP;
   const int npx = ldx >> 1, npy = ldy >> 1;
 
   bool vx[NS], vy[NS];
   double2 w[NS][R], c[NS][R], ax[NS][R], ay[NS][R];
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
-    const int px = tid + s * PPLS_SWEEP_THREADS;
+    const int px = tid + s * NT;
     vx[s] = px < npx;
     vy[s] = px < npy;
 #pragma unroll
@@ -316,13 +332,14 @@ __global__ __launch_bounds__(PPLS_SWEEP_THREADS, 2) void ppls_sweep_fused_kernel
       ay[s][k] = make_double2(0.0, 0.0);
     }
   }
-  double al[R], be[R], ga[R], de[R];
-#pragma unroll
-  for (int k = 0; k < R; ++k) {
-    al[k] = sc->alpha[k];
-    be[k] = sc->beta[k];
-    ga[k] = sc->gamma[k];
-    de[k] = sc->delta[k];
+  // lane m < R*RP of every wave turns (a, b) = (Xw, Yc) of row m/R, component m%R into mu_T, mu_U;
+  // the coefficients live in LDS (no registers, no VMEM inside the DMA-counted loop)
+  const int mj = lane / R, mk = lane - (lane / R) * R;
+  if (tid < R) {
+    cf[tid] = sc->alpha[tid];
+    cf[R + tid] = sc->beta[tid];
+    cf[2 * R + tid] = sc->gamma[tid];
+    cf[3 * R + tid] = sc->delta[tid];
   }
   // Gram entry owned by this thread (upper triangle of the 2R x 2R Gram, one entry per thread)
   const int ge = wave * 64 + lane;
@@ -338,109 +355,148 @@ __global__ __launch_bounds__(PPLS_SWEEP_THREADS, 2) void ppls_sweep_fused_kernel
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
   const uint32_t lds_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
-  auto issue_row = [&](int i, int slot) {
+  auto issue_row = [&](int i) {
+    if ((ablate & 2) || !dma_wave) return;
     const int64_t row = rb + i;
     const char* xr = (const char*)(X + row * (int64_t)ldx);
     const char* yr = (const char*)(Y + row * (int64_t)ldy);
-    const uint32_t sb = lds_base + (uint32_t)(slot * slot_bytes);
-    for (int j = 0; j < ndma; ++j) {
-      int ch = wave + j * NWAVES;
-      while (ch >= nch) ch -= nch;   // surplus issues duplicate a real chunk (identical bytes)
+    const uint32_t sb = lds_base + (uint32_t)((i % SLOTS) * slot_bytes);
+#pragma unroll
+    for (int j = 0; j < CPW; ++j) {
+      const int ch = min(wave * CPW + j, nch - 1);   // surplus issues repeat the last chunk
       const char* src;
-      if (ch < nchx) {
-        const int off = ch * 1024 + lane * 16;
-        src = xr + min(off, ldx * 8 - 16);
-      } else {
-        const int off = (ch - nchx) * 1024 + lane * 16;
-        src = yr + min(off, ldy * 8 - 16);
-      }
+      if (ch < nchx) src = xr + min(ch * 1024 + lane * 16, ldx * 8 - 16);
+      else src = yr + min((ch - nchx) * 1024 + lane * 16, ldy * 8 - 16);
       ppls_dma16(src, sb + (uint32_t)(ch * 1024));
     }
   };
-
-  for (int i = 0; i < SLOTS - 1 && i < nrows; ++i) issue_row(i, i);
-
-  for (int i = 0; i < nrows; ++i) {
-    const int ahead = min(SLOTS - 2, nrows - 1 - i);
-    ppls_wait_vmcnt(write_mu ? 0 : ahead * ndma);
-    ppls_lds_barrier();
-    if (i + SLOTS - 1 < nrows) issue_row(i + SLOTS - 1, (i + SLOTS - 1) % SLOTS);
-    const char* sb = smem + (size_t)(i % SLOTS) * slot_bytes;
-    double2 xv[NS], yv[NS];
-#pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      const int px = tid + s * PPLS_SWEEP_THREADS;
-      xv[s] = vx[s] ? *(const double2*)(sb + px * 16) : make_double2(0.0, 0.0);
-      yv[s] = vy[s] ? *(const double2*)(sb + nchx * 1024 + px * 16) : make_double2(0.0, 0.0);
-    }
+  auto issue_group = [&](int grp) {
+    for (int j = 0; j < RP; ++j)
+      if (grp * RP + j < nrows) issue_row(grp * RP + j);
+  };
+  // group grp's partial dots -> wave reduce-scatter -> red[grp & 1]; keeps the rows' x/y pairs
+  auto dots_group = [&](int grp, double2 (&xv)[RP][NS], double2 (&yv)[RP][NS]) {
+    if (ablate & 1) return;
     double v[VP];
 #pragma unroll
-    for (int k = 0; k < R; ++k) {
-      double sx = 0.0, sy = 0.0;
+    for (int j = 0; j < RP; ++j) {
+      const int row = min(grp * RP + j, nrows - 1);   // a partial last group repeats its last row
+      const char* sb = smem + (size_t)(row % SLOTS) * slot_bytes;
 #pragma unroll
       for (int s = 0; s < NS; ++s) {
-        sx = fma(xv[s].x, w[s][k].x, sx);
-        sx = fma(xv[s].y, w[s][k].y, sx);
-        sy = fma(yv[s].x, c[s][k].x, sy);
-        sy = fma(yv[s].y, c[s][k].y, sy);
+        const int px = tid + s * NT;
+        xv[j][s] = vx[s] ? *(const double2*)(sb + px * 16) : make_double2(0.0, 0.0);
+        yv[j][s] = vy[s] ? *(const double2*)(sb + nchx * 1024 + px * 16) : make_double2(0.0, 0.0);
       }
-      v[k] = sx;
-      v[R + k] = sy;
+#pragma unroll
+      for (int k = 0; k < R; ++k) {
+        double sx = 0.0, sy = 0.0;
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+          sx = fma(xv[j][s].x, w[s][k].x, sx);
+          sx = fma(xv[j][s].y, w[s][k].y, sx);
+          sy = fma(yv[j][s].x, c[s][k].x, sy);
+          sy = fma(yv[j][s].y, c[s][k].y, sy);
+        }
+        v[j * 2 * R + k] = sx;
+        v[j * 2 * R + R + k] = sy;
+      }
     }
 #pragma unroll
     for (int k = V; k < VP; ++k) v[k] = 0.0;
     int idx = 0;
     bool canon = true;
     ppls_rs<V, 0, VP>(v, lane, idx, canon);
-    if (canon && idx < V) red[wave * V + idx] = v[0];
+    if (canon && idx < V) red[((grp & 1) * NWAVES + wave) * V + idx] = v[0];
+  };
+
+  if (ngroups > 0) {
+    const int npro = min(SLOTS, nrows);
+    for (int i = 0; i < npro; ++i) issue_row(i);
+    if (write_mu) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else ppls_wait_vmcnt((npro - min(RP, nrows)) * CPW);
     ppls_lds_barrier();
-    double z = 0.0;
-    if (lane < V) {
-#pragma unroll
-      for (int ww = 0; ww < NWAVES; ++ww) z += red[ww * V + lane];
-    }
-    double za[R], zb[R];
-#pragma unroll
-    for (int k = 0; k < R; ++k) {
-      za[k] = __hiloint2double(__builtin_amdgcn_readlane((int)__double2hiint(z), k),
-                               __builtin_amdgcn_readlane((int)__double2loint(z), k));
-      zb[k] = __hiloint2double(__builtin_amdgcn_readlane((int)__double2hiint(z), R + k),
-                               __builtin_amdgcn_readlane((int)__double2loint(z), R + k));
-    }
-    {
-      const double zi = __shfl(z, gi, 64), zj = __shfl(z, gj, 64);
-      if (has_g) gacc = fma(zi, zj, gacc);
-    }
-    double mt[R], mu_u[R];
-#pragma unroll
-    for (int k = 0; k < R; ++k) {
-      mt[k] = al[k] * za[k] + be[k] * zb[k];
-      mu_u[k] = ga[k] * za[k] + de[k] * zb[k];
-    }
-    if (write_mu && wave == 0 && lane < R) {
-      double a = 0.0, b = 0.0;
-#pragma unroll
-      for (int k = 0; k < R; ++k)
-        if (lane == k) { a = mt[k]; b = mu_u[k]; }
-      mu[(int64_t)lane * n_local + rb + i] = a;
-      mu[(int64_t)(R + lane) * n_local + rb + i] = b;
-    }
-#pragma unroll
-    for (int s = 0; s < NS; ++s)
-#pragma unroll
-      for (int k = 0; k < R; ++k) {
-        ax[s][k].x = fma(xv[s].x, mt[k], ax[s][k].x);
-        ax[s][k].y = fma(xv[s].y, mt[k], ax[s][k].y);
-        ay[s][k].x = fma(yv[s].x, mu_u[k], ay[s][k].x);
-        ay[s][k].y = fma(yv[s].y, mu_u[k], ay[s][k].y);
+    double2 xc[RP][NS] = {}, yc[RP][NS] = {};
+    dots_group(0, xc, yc);
+    for (int gg = 0; gg < ngroups; ++gg) {
+      // rows issued after group gg+1: steady state AHEAD groups (compile-time wait)
+      if (write_mu) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      } else if ((gg + 2 + AHEAD) * RP <= nrows && gg >= 1) {
+        if constexpr (AHEAD * RP * CPW == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        else ppls_wait_vmcnt(AHEAD * RP * CPW);
+      } else {
+        const int last_issued = min(gg >= 1 ? (gg - 1) * RP + SLOTS + RP - 1 : SLOTS - 1, nrows - 1);
+        ppls_wait_vmcnt(max(0, last_issued - ((gg + 2) * RP - 1)) * CPW);
       }
+      ppls_lds_barrier();   // red[gg&1] complete, group gg+1 landed, slots of group gg free
+      if (gg * RP + SLOTS < nrows) issue_group(gg + SLOTS / RP);
+      if (ablate & 1) continue;
+      // cross-wave sums of group gg: lane m < R*RP holds (a, b) = (Xw, Yc)[row m/R][comp m%R]
+      // and its mu_T / mu_U; [Xw Yc] rows go to the per-wave LDS scratch for the Gram
+      double mta = 0.0, mua = 0.0;
+      if (lane < R * RP) {
+        const double* rr = red + (gg & 1) * NWAVES * V;
+        double a = 0.0, b = 0.0;
+#pragma unroll
+        for (int ww = 0; ww < NWAVES; ++ww) {
+          a += rr[ww * V + mj * 2 * R + mk];
+          b += rr[ww * V + mj * 2 * R + R + mk];
+        }
+        bc[mj * 2 * R + mk] = a;
+        bc[mj * 2 * R + R + mk] = b;
+        mta = cf[mk] * a + cf[R + mk] * b;           // mu_T (EM_W_multi.R:691-692)
+        mua = cf[2 * R + mk] * a + cf[3 * R + mk] * b;   // mu_U (EM_W_multi.R:693-694)
+      }
+      double2 xn[RP][NS] = {}, yn[RP][NS] = {};
+      if (gg + 1 < ngroups) dots_group(gg + 1, xn, yn);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's bc writes are visible
+#pragma unroll
+      for (int j = 0; j < RP; ++j) {
+        if (gg * RP + j >= nrows) break;
+        if (has_g) gacc = fma(bc[j * 2 * R + gi], bc[j * 2 * R + gj], gacc);
+        double mt[R], mu_u[R];
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
+          mt[k] = __hiloint2double(__builtin_amdgcn_readlane((int)__double2hiint(mta), j * R + k),
+                                   __builtin_amdgcn_readlane((int)__double2loint(mta), j * R + k));
+          mu_u[k] = __hiloint2double(__builtin_amdgcn_readlane((int)__double2hiint(mua), j * R + k),
+                                     __builtin_amdgcn_readlane((int)__double2loint(mua), j * R + k));
+        }
+        if (write_mu && wave == 0 && lane < R) {
+          const int64_t row = rb + gg * RP + j;
+          double a = 0.0, b = 0.0;
+#pragma unroll
+          for (int k = 0; k < R; ++k)
+            if (lane == k) { a = mt[k]; b = mu_u[k]; }
+          mu[(int64_t)lane * n_local + row] = a;
+          mu[(int64_t)(R + lane) * n_local + row] = b;
+        }
+#pragma unroll
+        for (int s = 0; s < NS; ++s)
+#pragma unroll
+          for (int k = 0; k < R; ++k) {
+            ax[s][k].x = fma(xc[j][s].x, mt[k], ax[s][k].x);
+            ax[s][k].y = fma(xc[j][s].y, mt[k], ax[s][k].y);
+            ay[s][k].x = fma(yc[j][s].x, mu_u[k], ay[s][k].x);
+            ay[s][k].y = fma(yc[j][s].y, mu_u[k], ay[s][k].y);
+          }
+      }
+#pragma unroll
+      for (int j = 0; j < RP; ++j)
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+          xc[j][s] = xn[j][s];
+          yc[j][s] = yn[j][s];
+        }
+    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   // partials: [SX ldx*R][SY ldy*R][G 4R^2]
   double* pg = part + g * part_ld;
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
-    const int px = tid + s * PPLS_SWEEP_THREADS;
+    const int px = tid + s * NT;
 #pragma unroll
     for (int k = 0; k < R; ++k) {
       if (vx[s]) *(double2*)(pg + (int64_t)k * ldx + 2 * px) = ax[s][k];
@@ -449,8 +505,8 @@ __global__ __launch_bounds__(PPLS_SWEEP_THREADS, 2) void ppls_sweep_fused_kernel
   }
   if (has_g) {
     double* G2 = pg + (int64_t)R * ldx + (int64_t)R * ldy;
-    G2[gj * V + gi] = gacc;
-    G2[gi * V + gj] = gacc;
+    G2[gj * 2 * R + gi] = gacc;
+    G2[gi * 2 * R + gj] = gacc;
   }
 }
 
@@ -651,9 +707,238 @@ __device__ void ppls_block_polar(const double* S, int64_t lds, int p, int r, dou
     }
 }
 
-// Block 0: W_next = polar(S_X); block 1: C_next = polar(S_Y); block 2: scalars.
-// stats = [SX ldx*r][SY ldy*r][G 4r^2];  ssq = {||X||^2, ||Y||^2}.
+// Block-wide sum of NV values per thread with a compile-time count (registers, no scratch).
+template <int NV>
+__device__ __forceinline__ void ppls_block_sum_t(double (&vals)[NV], double* sh) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const double s = ppls_wave_sum(vals[k]);
+    if (lane == 0) sh[wave * NV + k] = s;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    double t = 0.0;
+    for (int w = 0; w < nwaves; ++w) t += sh[w * NV + k];
+    vals[k] = t;
+  }
+  __syncthreads();
+}
+
+// Upper Cholesky G = R'R of an r x r SPD matrix (column-major); false if not numerically SPD.
+template <int R>
+__device__ bool ppls_chol_upper(const double* G, double* Rm) {
+  for (int j = 0; j < R; ++j) {
+    for (int i = 0; i <= j; ++i) {
+      double s = G[j * R + i];
+      for (int k = 0; k < i; ++k) s -= Rm[i * R + k] * Rm[j * R + k];
+      if (i == j) {
+        if (!(s > 0.0)) return false;
+        Rm[j * R + j] = sqrt(s);
+      } else {
+        Rm[j * R + i] = s / Rm[i * R + i];
+      }
+    }
+    for (int i = j + 1; i < R; ++i) Rm[j * R + i] = 0.0;
+  }
+  return true;
+}
+
+// inv(U) for upper-triangular U (column-major), into Ui.
+template <int R>
+__device__ void ppls_inv_upper(const double* U, double* Ui) {
+  for (int j = 0; j < R; ++j)
+    for (int i = R - 1; i >= 0; --i) {
+      double s = (i == j) ? 1.0 : 0.0;
+      for (int k = i + 1; k < R; ++k) s -= U[k * R + i] * Ui[j * R + k];
+      Ui[j * R + i] = (i <= j) ? s / U[i * R + i] : 0.0;
+    }
+}
+
+// Polar factor U V' of the p x r matrix S (column-major, ld lds) by Cholesky-QR2:
+//   G1 = S'S = R1'R1, Q1 = S R1^-1, G2 = Q1'Q1 = R2'R2, R = R2 R1 (orthogonality O(eps kappa)),
+//   R = U_R Sigma V_R' (one-sided Jacobi), polar(S) = S R^-1 U_R V_R'.
+// Two block reductions instead of the 3r of Householder.  Returns false when a Cholesky pivot
+// fails (kappa(S) ~> 1e8); the caller then falls back to Householder.
+template <int R>
+__device__ bool ppls_block_polar_cholqr2(const double* S, int64_t lds, int p, double* out, int64_t ldo,
+                                        int ldo_rows, double* sh, double* sm /* >= 4 R^2 */) {
+  constexpr int NG = R * (R + 1) / 2;
+  const int tid = threadIdx.x, nt = blockDim.x;
+  double* R1 = sm;
+  double* M = sm + R * R;          // R1^-1, later R1^-1 R2^-1 U V'
+  double* T = sm + 2 * R * R;
+  __shared__ int ok;
+  double vals[NG];
+  // G1 = S'S
+#pragma unroll
+  for (int e = 0; e < NG; ++e) vals[e] = 0.0;
+  for (int i = tid; i < p; i += nt) {
+    double x[R];
+#pragma unroll
+    for (int k = 0; k < R; ++k) x[k] = S[(int64_t)k * lds + i];
+    int e = 0;
+#pragma unroll
+    for (int b = 0; b < R; ++b)
+#pragma unroll
+      for (int a = 0; a <= b; ++a) vals[e++] = fma(x[a], x[b], vals[e]);
+  }
+  ppls_block_sum_t<NG>(vals, sh);
+  if (tid == 0) {
+    double G[R * R];
+    int e = 0;
+    for (int b = 0; b < R; ++b)
+      for (int a = 0; a <= b; ++a) { G[b * R + a] = vals[e]; G[a * R + b] = vals[e]; ++e; }
+    ok = ppls_chol_upper<R>(G, R1);
+    if (ok) ppls_inv_upper<R>(R1, M);
+  }
+  __syncthreads();
+  if (!ok) return false;
+  // G2 = Q1'Q1 with Q1 = S R1^-1 (rows recomputed on the fly)
+#pragma unroll
+  for (int e = 0; e < NG; ++e) vals[e] = 0.0;
+  for (int i = tid; i < p; i += nt) {
+    double x[R], qv[R];
+#pragma unroll
+    for (int k = 0; k < R; ++k) x[k] = S[(int64_t)k * lds + i];
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      double s = 0.0;
+#pragma unroll
+      for (int k = 0; k <= j; ++k) s = fma(x[k], M[j * R + k], s);
+      qv[j] = s;
+    }
+    int e = 0;
+#pragma unroll
+    for (int b = 0; b < R; ++b)
+#pragma unroll
+      for (int a = 0; a <= b; ++a) vals[e++] = fma(qv[a], qv[b], vals[e]);
+  }
+  ppls_block_sum_t<NG>(vals, sh);
+  if (tid == 0) {
+    double G[R * R], R2[R * R], Rr[R * R], R2i[R * R], P[R * R];
+    int e = 0;
+    for (int b = 0; b < R; ++b)
+      for (int a = 0; a <= b; ++a) { G[b * R + a] = vals[e]; G[a * R + b] = vals[e]; ++e; }
+    ok = ppls_chol_upper<R>(G, R2);
+    if (ok) {
+      // R = R2 R1 (upper); P = U_R V_R'; M <- R1^-1 R2^-1 P
+      for (int j = 0; j < R; ++j)
+        for (int i = 0; i < R; ++i) {
+          double s = 0.0;
+          for (int k = 0; k < R; ++k) s += R2[k * R + i] * R1[j * R + k];
+          Rr[j * R + i] = s;
+        }
+      ok = ppls_small_polar_n<R>(Rr, R, P) == 0;
+      ppls_inv_upper<R>(R2, R2i);
+      for (int j = 0; j < R; ++j)
+        for (int i = 0; i < R; ++i) {
+          double s = 0.0;
+          for (int k = 0; k < R; ++k) s += R2i[k * R + i] * P[j * R + k];
+          T[j * R + i] = s;
+        }
+      for (int j = 0; j < R; ++j)
+        for (int i = 0; i < R; ++i) {
+          double s = 0.0;
+          for (int k = 0; k < R; ++k) s += M[k * R + i] * T[j * R + k];
+          R1[j * R + i] = s;   // reuse R1 as the final r x r multiplier
+        }
+    }
+  }
+  __syncthreads();
+  if (!ok) return false;
+  for (int i = tid; i < ldo_rows; i += nt) {
+    double x[R];
+#pragma unroll
+    for (int k = 0; k < R; ++k) x[k] = (i < p) ? S[(int64_t)k * lds + i] : 0.0;
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      double s = 0.0;
+#pragma unroll
+      for (int k = 0; k < R; ++k) s = fma(x[k], R1[j * R + k], s);
+      out[(int64_t)j * ldo + i] = s;
+    }
+  }
+  return true;
+}
+
+// Block 0: W_next = orth(S_X); block 1: C_next = orth(S_Y); block 2: scalars (moments, loglik,
+// M-step).  stats = [SX ldx*R][SY ldy*R][G 4R^2];  ssq = {||X||^2, ||Y||^2}.
+template <int R>
 __global__ __launch_bounds__(256) void ppls_finalize_kernel(
+    const double* __restrict__ stats, const double* __restrict__ ssq, double N, int p, int q, int ldx,
+    int ldy, const double* __restrict__ Wc, const double* __restrict__ Cc,
+    const PplsScalars* __restrict__ sc_cur, double* __restrict__ Wn, double* __restrict__ Cn,
+    PplsScalars* __restrict__ sc_nxt, PplsMoments* __restrict__ mom, double* __restrict__ loglik,
+    int logl_index, double* __restrict__ work, int* __restrict__ status, int qr, int mode) {
+  __shared__ double sh[4 * R * (R + 1)];
+  __shared__ double sm[4 * R * R];
+  const double* SX = stats;
+  const double* SY = stats + (int64_t)R * ldx;
+  const double* G = SY + (int64_t)R * ldy;
+  if (blockIdx.x < 2) {
+    if (!(mode & 1)) return;
+    const bool isx = blockIdx.x == 0;
+    const double* S = isx ? SX : SY;
+    const int ld = isx ? ldx : ldy, rows = isx ? p : q;
+    double* out = isx ? Wn : Cn;
+    double* w2 = work + (isx ? 0 : 2 * (int64_t)p * R);
+    if (qr || !ppls_block_polar_cholqr2<R>(S, ld, rows, out, ld, ld, sh, sm))
+      ppls_block_polar(S, ld, rows, R, out, ld, ld, w2, w2 + (int64_t)rows * R, status, qr);
+    return;
+  }
+  if (!(mode & 2)) return;
+  // W'W and C'C of the parameters the sweep used (one batched reduction)
+  constexpr int NG = R * (R + 1) / 2;
+  double vals[2 * NG];
+#pragma unroll
+  for (int e = 0; e < 2 * NG; ++e) vals[e] = 0.0;
+  for (int i = threadIdx.x; i < (p > q ? p : q); i += blockDim.x) {
+    double wv[R], cv[R];
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+      wv[k] = (i < p) ? Wc[(int64_t)k * ldx + i] : 0.0;
+      cv[k] = (i < q) ? Cc[(int64_t)k * ldy + i] : 0.0;
+    }
+    int e = 0;
+#pragma unroll
+    for (int b = 0; b < R; ++b)
+#pragma unroll
+      for (int a = 0; a <= b; ++a) {
+        vals[e] = fma(wv[a], wv[b], vals[e]);
+        vals[NG + e] = fma(cv[a], cv[b], vals[NG + e]);
+        ++e;
+      }
+  }
+  ppls_block_sum_t<2 * NG>(vals, sh);
+  if (threadIdx.x == 0) {
+    double WtW[R * R], CtC[R * R];
+    int e = 0;
+    for (int b = 0; b < R; ++b)
+      for (int a = 0; a <= b; ++a) {
+        WtW[b * R + a] = WtW[a * R + b] = vals[e];
+        CtC[b * R + a] = CtC[a * R + b] = vals[NG + e];
+        ++e;
+      }
+    double Gl[4 * R * R];
+    for (int i = 0; i < 4 * R * R; ++i) Gl[i] = G[i];
+    const PplsScalars cur = *sc_cur;
+    const double s0 = ssq[0], s1 = ssq[1];
+    if (logl_index >= 0) loglik[logl_index] = ppls_loglik_from_gram(Gl, s0, s1, N, p, q, R, &cur);
+    PplsMoments m;
+    ppls_estep_moments(Gl, WtW, CtC, s0, s1, N, p, q, R, &cur, &m);
+    *mom = m;
+    PplsScalars nx = cur;
+    ppls_mstep_scalars(&m, R, &nx);
+    *sc_nxt = nx;
+  }
+}
+
+// Generic finalize for r > 8 (runtime r; Householder polar).  Block 0: W_next = orth(S_X);
+// block 1: C_next = orth(S_Y); block 2: scalars.
+// stats = [SX ldx*r][SY ldy*r][G 4r^2];  ssq = {||X||^2, ||Y||^2}.
+__global__ __launch_bounds__(256) void ppls_finalize_generic_kernel(
     const double* __restrict__ stats, const double* __restrict__ ssq, double N, int p, int q, int r,
     int ldx, int ldy, const double* __restrict__ Wc, const double* __restrict__ Cc,
     const PplsScalars* __restrict__ sc_cur, double* __restrict__ Wn, double* __restrict__ Cn,
@@ -719,48 +1004,87 @@ __global__ void ppls_loglc_kernel(const double* __restrict__ G, const double* __
 
 // ============================================================================ launchers
 namespace {
-template <int R, int NS, int SLOTS>
+template <int R>
+hipError_t launch_finalize_t(const PplsFinalizeArgs* f, hipStream_t st) {
+  hipLaunchKernelGGL(ppls_finalize_kernel<R>, dim3(3), dim3(256), 0, st, f->stats, f->ssq, f->N, f->p,
+                     f->q, f->ldx, f->ldy, f->Wc, f->Cc, f->sc_cur, f->Wn, f->Cn, f->sc_nxt, f->mom,
+                     f->loglik, f->logl_index, f->work, f->status, f->qr, f->mode);
+  return hipGetLastError();
+}
+
+
+size_t fused_lds(int r, int ldx, int ldy, int threads, int rp) {
+  const int nch = ((ldx * 8 + 1023) >> 10) + ((ldy * 8 + 1023) >> 10);
+  const int v = 2 * r * rp, nw = threads / 64;
+  return (size_t)PPLS_SWEEP_SLOTS * (nch << 10) + (size_t)(3 * nw * v + 4 * r) * 8;
+}
+
+template <int R, int NS, int NT, int RP, int CPW>
 hipError_t launch_fused_t(const PplsSweepArgs& a, hipStream_t st) {
-  auto kern = ppls_sweep_fused_kernel<R, NS, SLOTS>;
+  auto kern = ppls_sweep_fused_kernel<R, NS, NT, RP, PPLS_SWEEP_SLOTS, CPW>;
   static bool attr_set = false;
-  const int nch = ((a.ldx * 8 + 1023) >> 10) + ((a.ldy * 8 + 1023) >> 10);
-  const size_t lds = (size_t)SLOTS * (nch << 10) + (size_t)(PPLS_SWEEP_THREADS / 64) * 2 * R * 8;
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
                                        160 * 1024);
     if (e != hipSuccess) return e;
     attr_set = true;
   }
-  hipLaunchKernelGGL(kern, dim3(a.grid), dim3(PPLS_SWEEP_THREADS), lds, st, a.X, a.Y, a.n_local,
-                     a.ldx, a.ldy, a.Wp, a.Cp, a.sc, a.part, a.part_ld, a.mu, a.write_mu);
+  hipLaunchKernelGGL(kern, dim3(a.grid), dim3(NT), fused_lds(R, a.ldx, a.ldy, NT, RP), st, a.X, a.Y,
+                     a.n_local, a.ldx, a.ldy, a.Wp, a.Cp, a.sc, a.part, a.part_ld, a.mu, a.write_mu,
+                     a.ablate);
   return hipGetLastError();
 }
 
+template <int R, int NS, int NT, int RP>
+hipError_t launch_fused_cpw(const PplsSweepArgs& a, hipStream_t st) {
+  const int nch = ((a.ldx * 8 + 1023) >> 10) + ((a.ldy * 8 + 1023) >> 10);
+  const int need = (nch + NT / 64 - 1) / (NT / 64);   // chunks per wave with every wave copying
+  if (need <= 2) return launch_fused_t<R, NS, NT, RP, 2>(a, st);
+  if (need <= 4) return launch_fused_t<R, NS, NT, RP, 4>(a, st);
+  return hipErrorInvalidValue;   // cannot happen: nch <= 16 * NS (ppls_fused_supported)
+}
+
+// Only the (R, NS, NT, RP) combinations ppls_fused_supported admits are instantiated (the others
+// would not fit in 256 VGPRs).
 template <int R>
 hipError_t launch_fused_r(const PplsSweepArgs& a, hipStream_t st) {
-  switch (a.ns) {
-    case 1: return launch_fused_t<R, 1, PPLS_SWEEP_SLOTS>(a, st);
-    case 2: return launch_fused_t<R, 2, PPLS_SWEEP_SLOTS>(a, st);
-    default: return hipErrorInvalidValue;
+  if (a.threads == 1024) {
+    if constexpr (R <= 3) {
+      if (a.ns == 1) return launch_fused_cpw<R, 1, 1024, 1>(a, st);
+    }
+    return hipErrorInvalidValue;
   }
+  if constexpr (R <= 4) {
+    if (a.rp == 2 && a.ns == 1) return launch_fused_cpw<R, 1, 512, 2>(a, st);
+  }
+  if (a.ns == 1) return launch_fused_cpw<R, 1, 512, 1>(a, st);
+  if constexpr (2 * R <= 10) {
+    if (a.ns == 2) return launch_fused_cpw<R, 2, 512, 1>(a, st);
+  }
+  return hipErrorInvalidValue;
 }
 }  // namespace
 
 extern "C" {
 
-int ppls_fused_supported(int r, int ldx, int ldy) {
+int ppls_fused_supported(int r, int ldx, int ldy, int threads) {
   const int npmax = (ldx > ldy ? ldx : ldy) / 2;
-  const int ns = (npmax + PPLS_SWEEP_THREADS - 1) / PPLS_SWEEP_THREADS;
-  if (ns < 1 || ns > 2 || r < 1 || r > PPLS_FUSED_RMAX) return 0;
-  if (ns * r > 10) return 0;   // register budget (W, C and accumulators stay in VGPRs)
+  const int ns = (npmax + threads - 1) / threads;
+  if (r < 1 || r > PPLS_FUSED_RMAX) return 0;
+  if (threads == 1024) {
+    if (ns != 1 || r > 3) return 0;   // 4 waves/SIMD: W, C, accumulators in <= 128 VGPRs
+  } else if (threads == 512) {
+    if (ns < 1 || ns > 2 || ns * r > 10) return 0;   // W, C and accumulators stay in VGPRs
+  } else {
+    return 0;
+  }
   const int nch = ((ldx * 8 + 1023) >> 10) + ((ldy * 8 + 1023) >> 10);
-  const size_t lds = (size_t)PPLS_SWEEP_SLOTS * (nch << 10) + 8 * 2 * r * 8;
-  return lds <= 160 * 1024 ? ns : 0;
+  if (nch > 4 * (threads / 64)) return 0;   // at most 4 DMA chunks per wave per row
+  return ppls_fused_lds_bytes(r, ldx, ldy, threads) <= 160 * 1024 ? ns : 0;
 }
 
-size_t ppls_fused_lds_bytes(int r, int ldx, int ldy) {
-  const int nch = ((ldx * 8 + 1023) >> 10) + ((ldy * 8 + 1023) >> 10);
-  return (size_t)PPLS_SWEEP_SLOTS * (nch << 10) + 8 * 2 * r * 8;
+size_t ppls_fused_lds_bytes(int r, int ldx, int ldy, int threads) {
+  return fused_lds(r, ldx, ldy, threads, 2);
 }
 
 hipError_t ppls_launch_sweep_fused(const PplsSweepArgs* a, hipStream_t st) {
@@ -816,10 +1140,21 @@ hipError_t ppls_launch_reduce(const double* part, int ngroups, int64_t ld, int64
 }
 
 hipError_t ppls_launch_finalize(const PplsFinalizeArgs* f, hipStream_t st) {
-  hipLaunchKernelGGL(ppls_finalize_kernel, dim3(3), dim3(256), 0, st, f->stats, f->ssq, f->N, f->p,
-                     f->q, f->r, f->ldx, f->ldy, f->Wc, f->Cc, f->sc_cur, f->Wn, f->Cn, f->sc_nxt,
-                     f->mom, f->loglik, f->logl_index, f->work, f->status, f->qr, f->mode);
-  return hipGetLastError();
+  switch (f->r) {
+    case 1: return launch_finalize_t<1>(f, st);
+    case 2: return launch_finalize_t<2>(f, st);
+    case 3: return launch_finalize_t<3>(f, st);
+    case 4: return launch_finalize_t<4>(f, st);
+    case 5: return launch_finalize_t<5>(f, st);
+    case 6: return launch_finalize_t<6>(f, st);
+    case 7: return launch_finalize_t<7>(f, st);
+    case 8: return launch_finalize_t<8>(f, st);
+    default:
+      hipLaunchKernelGGL(ppls_finalize_generic_kernel, dim3(3), dim3(256), 0, st, f->stats, f->ssq, f->N,
+                         f->p, f->q, f->r, f->ldx, f->ldy, f->Wc, f->Cc, f->sc_cur, f->Wn, f->Cn,
+                         f->sc_nxt, f->mom, f->loglik, f->logl_index, f->work, f->status, f->qr, f->mode);
+      return hipGetLastError();
+  }
 }
 
 hipError_t ppls_launch_loglc(const double* G, const double* ssq, double N, int p, int q, int r,

@@ -214,8 +214,10 @@ PPLS_HD void ppls_mstep_scalars(const PplsMoments* m, int r, PplsScalars* nx) {
 // Polar factor U_R V_R' of a small r x r matrix R (column-major, ld r) by one-sided (Hestenes)
 // Jacobi: R V = U S.  Returns 0 on success, -1 if R is numerically rank deficient.
 // P (r x r, column-major) receives U_R V_R'.
-PPLS_HD int ppls_small_polar(const double* R, int r, double* P) {
-  double A[PPLS_RMAX * PPLS_RMAX], V[PPLS_RMAX * PPLS_RMAX];
+template <int RC>
+PPLS_HD int ppls_small_polar_n(const double* R, int r, double* P) {
+  // RC: compile-time capacity (arrays stay in registers when RC == r is a constant)
+  double A[RC * RC], V[RC * RC];
   for (int i = 0; i < r * r; ++i) A[i] = R[i];
   for (int j = 0; j < r; ++j)
     for (int i = 0; i < r; ++i) V[j * r + i] = (i == j) ? 1.0 : 0.0;
@@ -247,7 +249,7 @@ PPLS_HD int ppls_small_polar(const double* R, int r, double* P) {
       }
     if (off < 1e-15) break;
   }
-  double smax = 0.0, sv[PPLS_RMAX];
+  double smax = 0.0, sv[RC];
   for (int i = 0; i < r; ++i) {
     double nrm = 0.0;
     for (int k = 0; k < r; ++k) nrm += A[i * r + k] * A[i * r + k];
@@ -267,6 +269,10 @@ PPLS_HD int ppls_small_polar(const double* R, int r, double* P) {
       P[j * r + i] = acc;
     }
   return rc;
+}
+
+PPLS_HD int ppls_small_polar(const double* R, int r, double* P) {
+  return ppls_small_polar_n<PPLS_RMAX>(R, r, P);
 }
 
 // Sign/order canonicalisation, EM_W_multi.R:773-778 / :794-799.  Produces the permutation rot

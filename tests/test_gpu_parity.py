@@ -16,7 +16,9 @@ from oracle import ppls_oracle as o
 pytestmark = pytest.mark.gpu
 
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
-SWEEPS = [1, 2]   # 1 = fused single-pass kernel, 2 = generic two-pass kernels
+# (sweep, threads, rows_per_step): fused single-pass (512 / 1024 threads, 1 or 2 rows per step),
+# generic two-pass
+SWEEPS = [(1, 512, 1), (1, 512, 2), (1, 1024, 1), (2, 0, 1)]
 
 
 @pytest.fixture(scope="module")
@@ -25,6 +27,14 @@ def ctx():
     c = Context(0)
     yield c
     c.close()
+
+
+@pytest.fixture(autouse=True)
+def _reset_options(ctx):
+    for k in ("sweep", "threads", "grid"):
+        ctx.set_option(k, 0)
+    ctx.set_option("rows_per_step", 0)
+    yield
 
 
 def _theta(th):
@@ -46,7 +56,9 @@ def _golden():
 def test_em_run_matches_golden(ctx, name, sweep):
     g = np.load(os.path.join(GOLD, name))
     meta = json.loads(str(g["meta"]))
-    ctx.set_option("sweep", sweep)
+    ctx.set_option("sweep", sweep[0])
+    ctx.set_option("threads", sweep[1])
+    ctx.set_option("rows_per_step", sweep[2])
     ctx.set_option("grid", 0)
     ctx.set_data(g["X"], g["Y"])
     th0 = dict(W=g["W0"], C=g["C0"], B=np.diag(g["B0"]), sigE=g["sig0"][0], sigF=g["sig0"][1],
@@ -72,10 +84,13 @@ def test_em_run_matches_golden(ctx, name, sweep):
 
 @pytest.mark.parametrize("sweep", SWEEPS)
 @pytest.mark.parametrize("n,p,q,r", [(200, 50, 50, 2), (97, 33, 7, 1), (301, 64, 31, 5), (50, 9, 12, 8),
-                                     (3, 5, 4, 2), (1, 6, 3, 1), (700, 1025, 3, 2), (400, 2, 1500, 3)])
+                                     (3, 5, 4, 2), (1, 6, 3, 1), (700, 1025, 3, 2), (400, 3, 1500, 3),
+                                     (150, 17, 14, 10), (90, 24, 20, 16)])
 def test_estep_mstep_loglik_vs_oracle(ctx, sweep, n, p, q, r):
     X, Y, th0 = make_problem(n, p, q, r, seed=n + p + q + r)
-    ctx.set_option("sweep", sweep)
+    ctx.set_option("sweep", sweep[0])
+    ctx.set_option("threads", sweep[1])
+    ctx.set_option("rows_per_step", sweep[2])
     ctx.set_data(X, Y)
     th = _theta(th0)
     e = ctx.estep(th)
@@ -103,6 +118,14 @@ def test_estep_mstep_loglik_vs_oracle(ctx, sweep, n, p, q, r):
     ll = ctx.loglik(th)
     ref_ll = o.logl_w(X, Y, th0["W"], th0["C"], th0["B"], th0["sigE"], th0["sigF"], th0["sigH"], th0["sigT"])
     assert abs(ll - ref_ll) / abs(ref_ll) < 1e-11
+
+
+def test_fewer_columns_than_components_is_an_argument_error(ctx):
+    from ppls_amd import PplsError
+    X, Y, th0 = make_problem(50, 4, 6, 2, seed=1)
+    ctx.set_data(X[:, :1], Y)
+    with pytest.raises(PplsError, match="must be >= number of components"):
+        ctx.estep(_theta(dict(th0, W=th0["W"][:1])))
 
 
 def test_loglC_fast_dropin(ctx):
@@ -208,10 +231,10 @@ def test_monotone_em_c2_shape(ctx):
     ctx.generate_synthetic(n, p, q, truth, seed=20261015)
     th0 = _theta(dict(W=np.linalg.qr(rng.standard_normal((p, r)))[0], C=np.linalg.qr(rng.standard_normal((q, r)))[0],
                       B=np.eye(r), sigE=1.0, sigF=1.0, sigH=1.0, sigT=np.eye(r)))
-    est, ll, eout, neg = ctx.em_run(th0, 8, -np.inf, 0, want_mu=False)
-    assert len(ll) == 8 and not neg and np.all(np.diff(ll) > 0)
+    est, ll, eout, neg = ctx.em_run(th0, 40, -np.inf, 0, want_mu=False)
+    assert len(ll) == 40 and not neg and np.all(np.diff(ll) > 0)
     assert np.abs(est.W.T @ est.W - np.eye(r)).max() < 1e-12
     assert np.abs(est.C.T @ est.C - np.eye(r)).max() < 1e-12
-    # EM approaches the truth
-    assert np.all(np.abs(np.diag(est.W.T @ W)) > 0.99)
-    assert abs(est.sigE - 0.5) < 0.01
+    # EM approaches the true subspace (canonicalisation may permute/flip components)
+    assert np.linalg.svd(est.W.T @ W, compute_uv=False).min() > 0.95
+    assert abs(est.sigE - 0.5) < 0.02
