@@ -131,8 +131,10 @@ def main():
 
     cfg = CONFIGS[args.config]
     n, p, q, r = cfg["n"], cfg["p"], cfg["q"], cfg["r"]
-    ctx = Context(local)
-    _DEVICE[id(ctx)] = local
+    ndev = max(1, torch.cuda.device_count())   # does not initialise the GPU
+    device = local % ndev
+    ctx = Context(device)
+    _DEVICE[id(ctx)] = device
     ctx.set_option("sweep", args.sweep)
     ctx.set_option("threads", args.threads)
     if world > 1:

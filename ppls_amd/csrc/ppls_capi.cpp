@@ -250,7 +250,7 @@ int grid_of(ppls_ctx* c) { return c->grid_opt > 0 ? c->grid_opt : c->num_cus; }
 
 // Allreduce in place (sum) over ranks, on the context stream.
 int allreduce(ppls_ctx* c, double* buf, size_t count) {
-  if (!c->comm || c->nranks <= 1) return PPLS_OK;
+  if (!c->comm) return PPLS_OK;   // a 1-rank communicator still takes the RCCL path
   RCCLCHK(c, ncclAllReduce(buf, buf, count, ncclDouble, ncclSum, c->comm, c->stream));
   return PPLS_OK;
 }

@@ -238,3 +238,20 @@ def test_monotone_em_c2_shape(ctx):
     # EM approaches the true subspace (canonicalisation may permute/flip components)
     assert np.linalg.svd(est.W.T @ W, compute_uv=False).min() > 0.95
     assert abs(est.sigE - 0.5) < 0.02
+
+
+def test_rccl_single_rank_communicator_path():
+    """ppls_comm_init + the per-iteration ncclAllReduce on a 1-rank communicator (the 8-GPU path
+    is run by the driver; here the RCCL calls themselves are exercised on the one GPU)."""
+    from ppls_amd import Context
+    X, Y, th0 = make_problem(400, 30, 26, 3, seed=8)
+    a = Context(0)
+    a.set_data(X, Y)
+    ra = a.em_run(_theta(th0), 5, -np.inf, 0)
+    a.close()
+    b = Context(0)
+    b.comm_init(1, 0, Context.comm_unique_id())
+    b.set_data(X, Y)
+    rb = b.em_run(_theta(th0), 5, -np.inf, 0)
+    b.close()
+    assert np.array_equal(ra[1], rb[1]) and np.array_equal(ra[0].W, rb[0].W)
