@@ -30,6 +30,8 @@ struct ppls_ctx {
   int grid_opt = 0;
   int threads_opt = 0;
   int rp_opt = 0;   // rows per pipeline step: 0 auto (2 where the kernel fits in registers)
+  int kernel_opt = 0;   // fused sweep kernel: 0 auto, 2 = shared ownership (v2), 3 = split ownership
+  int pipe_opt = 1;     // split kernel: software-pipelined order
   int ablate = 0;
   int timing = 0;
   // communicator
@@ -255,29 +257,58 @@ int allreduce(ppls_ctx* c, double* buf, size_t count) {
   return PPLS_OK;
 }
 
+// Which sweep kernel runs for this shape: 3 = split ownership (default), 1 = shared ownership
+// (v2, option kernel=2), 2 = generic two-pass; *grid is the workgroup count.
+int sweep_plan(ppls_ctx* c, int r, PplsSweepArgs* a) {
+  int ns = 0, threads = 512;
+  const bool fused = use_fused(c, r, &ns, &threads);
+  const int nsplit = ppls_split_supported(r, c->ldx, c->ldy);
+  memset(a, 0, sizeof *a);
+  a->ldx = c->ldx;
+  a->ldy = c->ldy;
+  a->r = r;
+  a->threads = threads;
+  if (c->sweep_mode != 2 && nsplit > 0 && c->kernel_opt != 2) {
+    a->ns = nsplit;
+    a->pipe = c->pipe_opt;
+    a->rp = c->rp_opt;             // 0 = auto: two rows per step wherever instantiated
+    int occ = 0;
+    a->occ_out = &occ;
+    if (ppls_launch_sweep_split(a, c->stream) != hipSuccess || occ < 1) occ = 1;
+    a->occ_out = nullptr;
+    a->grid = c->grid_opt > 0 ? c->grid_opt : c->num_cus * occ;
+    return 3;
+  }
+  if (fused) {
+    a->ns = ns;
+    a->rp = (c->rp_opt != 1 && ns == 1 && r <= 4 && threads == 512) ? 2 : 1;
+    a->grid = grid_of(c);
+    return 1;
+  }
+  a->grid = grid_of(c);
+  return 2;
+}
+
 // One sweep with theta[slot] -> c->stats (all-reduced).
 int sweep(ppls_ctx* c, int r, int slot, bool write_mu) {
-  int rc, ns = 0, threads = 512;
-  const bool fused = use_fused(c, r, &ns, &threads);
-  const int grid = grid_of(c);
-  const int groups = fused ? grid : ppls_twopass_groups(std::max<int64_t>(c->n_local, 1), grid);
+  int rc;
+  PplsSweepArgs a;
+  const int plan = sweep_plan(c, r, &a);
+  const int groups = plan == 2 ? ppls_twopass_groups(std::max<int64_t>(c->n_local, 1), a.grid) : a.grid;
   if (groups > c->part_groups || !c->part) {
     if ((rc = dalloc(c, &c->part, (size_t)groups * c->part_ld))) return rc;
     c->part_groups = groups;
   }
   if (write_mu && !c->mu)
     if ((rc = dalloc(c, &c->mu, (size_t)std::max<int64_t>(c->n_local, 1) * 2 * r))) return rc;
-  if (!fused && !c->Z)
+  if (plan == 2 && !c->Z)
     if ((rc = dalloc(c, &c->Z, (size_t)std::max<int64_t>(c->n_local, 1) * 2 * r))) return rc;
   if (c->n_local == 0) {
     HIPCHK(c, hipMemsetAsync(c->stats, 0, sizeof(double) * c->part_ld, c->stream));
   } else {
-    PplsSweepArgs a;
     a.X = c->X;
     a.Y = c->Y;
     a.n_local = c->n_local;
-    a.ldx = c->ldx;
-    a.ldy = c->ldy;
     a.Wp = c->W[slot];
     a.Cp = c->C[slot];
     a.sc = c->sc[slot];
@@ -285,12 +316,7 @@ int sweep(ppls_ctx* c, int r, int slot, bool write_mu) {
     a.part_ld = c->part_ld;
     a.mu = write_mu ? c->mu : nullptr;
     a.write_mu = write_mu ? 1 : 0;
-    a.r = r;
-    a.ns = ns;
-    a.threads = threads;
-    a.grid = grid;
     a.ablate = c->ablate;
-    a.rp = (c->rp_opt != 1 && ns == 1 && r <= 4 && threads == 512) ? 2 : 1;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (c->timing) {
       if (c->ev_used == c->ev.size()) {
@@ -304,7 +330,8 @@ int sweep(ppls_ctx* c, int r, int slot, bool write_mu) {
       ++c->ev_used;
       HIPCHK(c, hipEventRecord(e0, c->stream));
     }
-    if (fused) HIPCHK(c, ppls_launch_sweep_fused(&a, c->stream));
+    if (plan == 3) HIPCHK(c, ppls_launch_sweep_split(&a, c->stream));
+    else if (plan == 1) HIPCHK(c, ppls_launch_sweep_fused(&a, c->stream));
     else HIPCHK(c, ppls_launch_sweep_twopass(&a, c->Z, c->stream));
     if (c->timing) HIPCHK(c, hipEventRecord(e1, c->stream));
     HIPCHK(c, ppls_launch_reduce(c->part, groups, c->part_ld, c->part_ld, c->stats, 0, c->stream));
@@ -519,6 +546,11 @@ int ppls_set_option(ppls_ctx* c, const char* key, int64_t value) {
   } else if (!strcmp(key, "rows_per_step")) {
     if (value < 0 || value > 2) return fail(c, PPLS_E_ARG, "rows_per_step must be 0 (auto), 1 or 2");
     c->rp_opt = (int)value;
+  } else if (!strcmp(key, "kernel")) {
+    if (value != 0 && value != 2 && value != 3) return fail(c, PPLS_E_ARG, "kernel must be 0, 2 or 3");
+    c->kernel_opt = (int)value;
+  } else if (!strcmp(key, "pipe")) {
+    c->pipe_opt = value ? 1 : 0;
   } else if (!strcmp(key, "ablate")) {
     if (value < 0 || value > 3) return fail(c, PPLS_E_ARG, "ablate must be in [0,3]");
     c->ablate = (int)value;   // timing experiments only: results are wrong while set
@@ -924,11 +956,11 @@ int ppls_sweep_timing(ppls_ctx* c, double* total_ms, int64_t* launches, int rese
 
 int ppls_sweep_info(ppls_ctx* c, int r, int64_t* bytes_per_sweep, int* variant, int* grid) {
   if (!c) return PPLS_E_ARG;
-  int ns = 0, threads = 512;
-  const bool fused = use_fused(c, r, &ns, &threads);
+  PplsSweepArgs a;
+  const int plan = sweep_plan(c, r, &a);
   if (bytes_per_sweep) *bytes_per_sweep = (int64_t)8 * c->n_local * ((int64_t)c->p + c->q);
-  if (variant) *variant = fused ? (threads == 1024 ? 3 : 1) : 2;
-  if (grid) *grid = grid_of(c);
+  if (variant) *variant = plan == 3 ? 4 : plan == 1 ? (a.threads == 1024 ? 3 : 1) : 2;
+  if (grid) *grid = a.grid;
   return PPLS_OK;
 }
 

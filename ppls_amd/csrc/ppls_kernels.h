@@ -26,6 +26,8 @@ struct PplsSweepArgs {
   int ns;                // column pairs per thread (fused)
   int threads;           // fused workgroup size: 512 or 1024
   int rp;                // fused rows per pipeline step (1 or 2)
+  int pipe;              // split kernel: 1 = dots(g+1) before update(g), 0 = after
+  int* occ_out;          // split kernel: if set, report resident WGs per CU instead of launching
   int grid;              // workgroups (fused) / row chunks (two-pass)
   int ablate;            // timing experiments only (fused): 1 no compute, 2 no HBM copies
 };
@@ -54,6 +56,8 @@ extern "C" {
 int ppls_fused_supported(int r, int ldx, int ldy, int threads);
 size_t ppls_fused_lds_bytes(int r, int ldx, int ldy, int threads);
 hipError_t ppls_launch_sweep_fused(const PplsSweepArgs* a, hipStream_t st);
+int ppls_split_supported(int r, int ldx, int ldy);
+hipError_t ppls_launch_sweep_split(const PplsSweepArgs* a, hipStream_t st);
 hipError_t ppls_launch_sweep_twopass(const PplsSweepArgs* a, double* Z, hipStream_t st);
 hipError_t ppls_launch_accumulate(const PplsSweepArgs* a, const double* Z, hipStream_t st);
 int ppls_twopass_groups(int64_t n_local, int grid);

@@ -510,6 +510,234 @@ __global__ __launch_bounds__(NT, 2 * NT / 512) void ppls_sweep_fused_kernel(
   }
 }
 
+// ============================================================================ fused sweep v3
+// Same ring and pipeline as above, but column ownership is split by matrix: threads [0, NT/2) own
+// NSH column pairs of X, threads [NT/2, NT) own NSH pairs of Y.  A wave's partial dots are then
+// Xw only or Yc only, so the per-row wave reduce-scatter handles R*RP values (not 2R*RP) and each
+// wave broadcasts only the mu it uses (mu_T for X waves, mu_U for Y waves).
+//   PIPE = true : step g computes group g+1's dots before group g's update (x of both in VGPRs)
+//   PIPE = false: step g applies group g's update, then computes group g+1's dots (one x set)
+template <int R, int NSH, int NT, int RP, bool PIPE, int SLOTS, int CPW>
+__global__ __launch_bounds__(NT, 2 * NT / 512) void ppls_sweep_split_kernel(
+    const double* __restrict__ X, const double* __restrict__ Y, int64_t n_local, int ldx, int ldy,
+    const double* __restrict__ Wp, const double* __restrict__ Cp, const PplsScalars* __restrict__ sc,
+    double* __restrict__ part, int64_t part_ld, double* __restrict__ mu, int write_mu, int ablate) {
+  static_assert(SLOTS >= 2 * RP, "ring must hold the group being read and the group in flight");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int V = R * RP;                           // partial dots per thread per step
+  constexpr int VP = V + (V & 1);                     // reduce-scatter scratch
+  constexpr int NWAVES = NT / 64;
+  constexpr int HT = NT / 2;                          // threads per matrix
+  constexpr int AHEAD = SLOTS / RP - 2;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const bool isx = wave < NWAVES / 2;                 // wave-uniform
+  const int th = tid - (isx ? 0 : HT);
+  const int nchx = (ldx * 8 + 1023) >> 10, nchy = (ldy * 8 + 1023) >> 10;
+  const int nch = nchx + nchy;
+  const int slot_bytes = nch << 10;
+  const bool dma_wave = wave * CPW < nch;
+  double* red = (double*)(smem + (size_t)SLOTS * slot_bytes);          // [2][NWAVES][V]
+  double* bc = red + 2 * NWAVES * V + wave * (2 * V);                 // per wave: [Xw Yc] rows
+  double* cf = red + 2 * NWAVES * V + NWAVES * 2 * V;                 // alpha | beta | gamma | delta
+  const int64_t g = blockIdx.x, G = gridDim.x;
+  const int64_t rb = n_local * g / G, re = n_local * (g + 1) / G;
+  const int nrows = (int)(re - rb);
+  const int ngroups = (nrows + RP - 1) / RP;
+  const int np = isx ? (ldx >> 1) : (ldy >> 1);
+  const int ld = isx ? ldx : ldy;
+  const double* Wm = isx ? Wp : Cp;
+  const int xoff = isx ? 0 : nchx * 1024;             // byte offset of this matrix in a slot
+
+  bool vs[NSH];
+  double2 w[NSH][R], acc[NSH][R];
+#pragma unroll
+  for (int s = 0; s < NSH; ++s) {
+    const int pp = th + s * HT;
+    vs[s] = pp < np;
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+      w[s][k] = vs[s] ? *(const double2*)(Wm + (int64_t)k * ld + 2 * pp) : make_double2(0.0, 0.0);
+      acc[s][k] = make_double2(0.0, 0.0);
+    }
+  }
+  const int mj = lane / R, mk = lane - (lane / R) * R;
+  if (tid < R) {
+    cf[tid] = sc->alpha[tid];
+    cf[R + tid] = sc->beta[tid];
+    cf[2 * R + tid] = sc->gamma[tid];
+    cf[3 * R + tid] = sc->delta[tid];
+  }
+  const int ge = wave * 64 + lane;
+  int gi = 0, gj = 0;
+  const bool has_g = ge < R * (2 * R + 1);
+  if (has_g) {
+    int e = ge, j = 0;
+    while (e >= j + 1) { e -= j + 1; ++j; }
+    gi = e;
+    gj = j;
+  }
+  double gacc = 0.0;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  const uint32_t lds_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
+  auto issue_row = [&](int i) {
+    if ((ablate & 2) || !dma_wave) return;
+    const int64_t row = rb + i;
+    const char* xr = (const char*)(X + row * (int64_t)ldx);
+    const char* yr = (const char*)(Y + row * (int64_t)ldy);
+    const uint32_t sb = lds_base + (uint32_t)((i % SLOTS) * slot_bytes);
+#pragma unroll
+    for (int j = 0; j < CPW; ++j) {
+      const int ch = min(wave * CPW + j, nch - 1);
+      const char* src;
+      if (ch < nchx) src = xr + min(ch * 1024 + lane * 16, ldx * 8 - 16);
+      else src = yr + min((ch - nchx) * 1024 + lane * 16, ldy * 8 - 16);
+      ppls_dma16(src, sb + (uint32_t)(ch * 1024));
+    }
+  };
+  auto issue_group = [&](int grp) {
+    for (int j = 0; j < RP; ++j)
+      if (grp * RP + j < nrows) issue_row(grp * RP + j);
+  };
+  auto load_x = [&](int grp, double2 (&xv)[RP][NSH]) {
+#pragma unroll
+    for (int j = 0; j < RP; ++j) {
+      const int row = min(grp * RP + j, nrows - 1);
+      const char* sb = smem + (size_t)(row % SLOTS) * slot_bytes + xoff;
+#pragma unroll
+      for (int s = 0; s < NSH; ++s)
+        xv[j][s] = vs[s] ? *(const double2*)(sb + (th + s * HT) * 16) : make_double2(0.0, 0.0);
+    }
+  };
+  // partial dots of group grp (x already loaded) -> reduce-scatter -> red[grp & 1]
+  auto dots = [&](int grp, const double2 (&xv)[RP][NSH]) {
+    double v[VP];
+#pragma unroll
+    for (int j = 0; j < RP; ++j)
+#pragma unroll
+      for (int k = 0; k < R; ++k) {
+        double sx = 0.0;
+#pragma unroll
+        for (int s = 0; s < NSH; ++s) {
+          sx = fma(xv[j][s].x, w[s][k].x, sx);
+          sx = fma(xv[j][s].y, w[s][k].y, sx);
+        }
+        v[j * R + k] = sx;
+      }
+    if constexpr (VP > V) v[V] = 0.0;
+    int idx = 0;
+    bool canon = true;
+    ppls_rs<V, 0, VP>(v, lane, idx, canon);
+    if (canon && idx < V) red[((grp & 1) * NWAVES + wave) * V + idx] = v[0];
+  };
+  // cross-wave sums of group gg: lane m < R*RP -> (a, b, mu_T, mu_U) of row m/R, comp m%R
+  auto zsum = [&](int gg, double& mta, double& mua) {
+    if (lane < R * RP) {
+      const double* rr = red + (gg & 1) * NWAVES * V;
+      double a = 0.0, b = 0.0;
+#pragma unroll
+      for (int ww = 0; ww < NWAVES / 2; ++ww) {
+        a += rr[ww * V + lane];
+        b += rr[(ww + NWAVES / 2) * V + lane];
+      }
+      bc[mj * 2 * R + mk] = a;
+      bc[mj * 2 * R + R + mk] = b;
+      mta = cf[mk] * a + cf[R + mk] * b;               // mu_T (EM_W_multi.R:691-692)
+      mua = cf[2 * R + mk] * a + cf[3 * R + mk] * b;   // mu_U (EM_W_multi.R:693-694)
+    }
+  };
+  auto update = [&](int gg, double mta, double mua, const double2 (&xv)[RP][NSH]) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's bc writes are visible
+    const double msel = isx ? mta : mua;                   // wave-uniform choice
+#pragma unroll
+    for (int j = 0; j < RP; ++j) {
+      if (gg * RP + j >= nrows) break;
+      if (has_g) gacc = fma(bc[j * 2 * R + gi], bc[j * 2 * R + gj], gacc);
+      double m[R];
+#pragma unroll
+      for (int k = 0; k < R; ++k)
+        m[k] = __hiloint2double(__builtin_amdgcn_readlane((int)__double2hiint(msel), j * R + k),
+                                __builtin_amdgcn_readlane((int)__double2loint(msel), j * R + k));
+      if (write_mu && (wave == 0 || wave == NWAVES / 2) && lane < R) {
+        const int64_t row = rb + gg * RP + j;
+        double a = 0.0;
+#pragma unroll
+        for (int k = 0; k < R; ++k)
+          if (lane == k) a = m[k];
+        mu[(int64_t)((isx ? 0 : R) + lane) * n_local + row] = a;
+      }
+#pragma unroll
+      for (int s = 0; s < NSH; ++s)
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
+          acc[s][k].x = fma(xv[j][s].x, m[k], acc[s][k].x);
+          acc[s][k].y = fma(xv[j][s].y, m[k], acc[s][k].y);
+        }
+    }
+  };
+
+  if (ngroups > 0) {
+    const int npro = min(SLOTS, nrows);
+    for (int i = 0; i < npro; ++i) issue_row(i);
+    if (write_mu) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else ppls_wait_vmcnt((npro - min(RP, nrows)) * CPW);
+    ppls_lds_barrier();
+    double2 xc[RP][NSH] = {};
+    load_x(0, xc);
+    if (!(ablate & 1)) dots(0, xc);
+    for (int gg = 0; gg < ngroups; ++gg) {
+      if (write_mu) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      } else if ((gg + 2 + AHEAD) * RP <= nrows && gg >= 1) {
+        if constexpr (AHEAD * RP * CPW == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        else ppls_wait_vmcnt(AHEAD * RP * CPW);
+      } else {
+        const int last_issued = min(gg >= 1 ? (gg - 1) * RP + SLOTS + RP - 1 : SLOTS - 1, nrows - 1);
+        ppls_wait_vmcnt(max(0, last_issued - ((gg + 2) * RP - 1)) * CPW);
+      }
+      ppls_lds_barrier();   // red[gg&1] complete, group gg+1 landed, slots of group gg free
+      if (gg * RP + SLOTS < nrows) issue_group(gg + SLOTS / RP);
+      if (ablate & 1) continue;
+      double mta = 0.0, mua = 0.0;
+      zsum(gg, mta, mua);
+      if constexpr (PIPE) {
+        double2 xn[RP][NSH] = {};
+        if (gg + 1 < ngroups) {
+          load_x(gg + 1, xn);
+          dots(gg + 1, xn);
+        }
+        update(gg, mta, mua, xc);
+#pragma unroll
+        for (int j = 0; j < RP; ++j)
+#pragma unroll
+          for (int s = 0; s < NSH; ++s) xc[j][s] = xn[j][s];
+      } else {
+        update(gg, mta, mua, xc);
+        if (gg + 1 < ngroups) {
+          load_x(gg + 1, xc);
+          dots(gg + 1, xc);
+        }
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  double* pg = part + g * part_ld;
+  double* po = pg + (isx ? 0 : (int64_t)R * ldx);
+#pragma unroll
+  for (int s = 0; s < NSH; ++s) {
+    const int pp = th + s * HT;
+#pragma unroll
+    for (int k = 0; k < R; ++k)
+      if (vs[s]) *(double2*)(po + (int64_t)k * ld + 2 * pp) = acc[s][k];
+  }
+  if (has_g) {
+    double* G2 = pg + (int64_t)R * ldx + (int64_t)R * ldy;
+    G2[gj * 2 * R + gi] = gacc;
+    G2[gi * 2 * R + gj] = gacc;
+  }
+}
+
 // ============================================================================ generic two-pass
 // Pass 1: Z = [X W | Y C] (n_local x 2R row-major), one wave per row.
 __global__ __launch_bounds__(256) void ppls_dots_kernel(
@@ -1046,6 +1274,68 @@ hipError_t launch_fused_cpw(const PplsSweepArgs& a, hipStream_t st) {
 
 // Only the (R, NS, NT, RP) combinations ppls_fused_supported admits are instantiated (the others
 // would not fit in 256 VGPRs).
+size_t split_lds(int r, int ldx, int ldy, int threads, int rp) {
+  const int nch = ((ldx * 8 + 1023) >> 10) + ((ldy * 8 + 1023) >> 10);
+  const int v = r * rp, nw = threads / 64;
+  return (size_t)PPLS_SWEEP_SLOTS * (nch << 10) + (size_t)(2 * nw * v + nw * 2 * v + 4 * r) * 8;
+}
+
+template <int R, int NSH, int RP, bool PIPE, int CPW>
+hipError_t launch_split_t(const PplsSweepArgs& a, hipStream_t st) {
+  auto kern = ppls_sweep_split_kernel<R, NSH, 512, RP, PIPE, PPLS_SWEEP_SLOTS, CPW>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       160 * 1024);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  if (a.occ_out) {   // query: resident workgroups per CU for this instantiation and shape
+    int nb = 0;
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)kern, 512,
+                                                                split_lds(R, a.ldx, a.ldy, 512, RP));
+    *a.occ_out = nb;
+    return e;
+  }
+  hipLaunchKernelGGL(kern, dim3(a.grid), dim3(512), split_lds(R, a.ldx, a.ldy, 512, RP), st, a.X, a.Y,
+                     a.n_local, a.ldx, a.ldy, a.Wp, a.Cp, a.sc, a.part, a.part_ld, a.mu, a.write_mu,
+                     a.ablate);
+  return hipGetLastError();
+}
+
+template <int R, int NSH, int RP, bool PIPE>
+hipError_t launch_split_cpw(const PplsSweepArgs& a, hipStream_t st) {
+  const int nch = ((a.ldx * 8 + 1023) >> 10) + ((a.ldy * 8 + 1023) >> 10);
+  const int need = (nch + 7) / 8;
+  if (need <= 2) return launch_split_t<R, NSH, RP, PIPE, 2>(a, st);
+  if (need <= 4) return launch_split_t<R, NSH, RP, PIPE, 4>(a, st);
+  return hipErrorInvalidValue;
+}
+
+// split-ownership variants (512 threads): NSH pairs per thread in {1, 2, 4}; RP/PIPE from a.rp,
+// a.pipe.  Instantiated only where they fit in registers (see ppls_split_supported).
+template <int R>
+hipError_t launch_split_r(const PplsSweepArgs& a, hipStream_t st) {
+  if (a.ns <= 1) {
+    if (a.rp != 1) return launch_split_cpw<R, 1, 2, true>(a, st);
+    return launch_split_cpw<R, 1, 1, true>(a, st);
+  }
+  if (a.ns == 2) {
+    if constexpr (R <= 6) {
+      if (a.rp != 1) return launch_split_cpw<R, 2, 2, true>(a, st);
+    }
+    return launch_split_cpw<R, 2, 1, true>(a, st);
+  }
+  if constexpr (R <= 5) {
+    if (a.ns <= 4) {
+      if (a.rp != 1) return launch_split_cpw<R, 4, 2, false>(a, st);
+      if (a.pipe) return launch_split_cpw<R, 4, 1, true>(a, st);
+      return launch_split_cpw<R, 4, 1, false>(a, st);
+    }
+  }
+  return hipErrorInvalidValue;
+}
+
 template <int R>
 hipError_t launch_fused_r(const PplsSweepArgs& a, hipStream_t st) {
   if (a.threads == 1024) {
@@ -1085,6 +1375,31 @@ int ppls_fused_supported(int r, int ldx, int ldy, int threads) {
 
 size_t ppls_fused_lds_bytes(int r, int ldx, int ldy, int threads) {
   return fused_lds(r, ldx, ldy, threads, 2);
+}
+
+int ppls_split_supported(int r, int ldx, int ldy) {
+  const int npmax = (ldx > ldy ? ldx : ldy) / 2;
+  const int nsh = (npmax + 255) / 256;
+  if (r < 1 || r > PPLS_FUSED_RMAX) return 0;
+  int ns = nsh <= 1 ? 1 : nsh <= 2 ? 2 : nsh <= 4 ? 4 : 0;
+  if (ns == 0 || (ns == 4 && r > 5)) return 0;
+  const int nch = ((ldx * 8 + 1023) >> 10) + ((ldy * 8 + 1023) >> 10);
+  if (nch > 32) return 0;
+  return split_lds(r, ldx, ldy, 512, 2) <= 160 * 1024 ? ns : 0;
+}
+
+hipError_t ppls_launch_sweep_split(const PplsSweepArgs* a, hipStream_t st) {
+  switch (a->r) {
+    case 1: return launch_split_r<1>(*a, st);
+    case 2: return launch_split_r<2>(*a, st);
+    case 3: return launch_split_r<3>(*a, st);
+    case 4: return launch_split_r<4>(*a, st);
+    case 5: return launch_split_r<5>(*a, st);
+    case 6: return launch_split_r<6>(*a, st);
+    case 7: return launch_split_r<7>(*a, st);
+    case 8: return launch_split_r<8>(*a, st);
+    default: return hipErrorInvalidValue;
+  }
 }
 
 hipError_t ppls_launch_sweep_fused(const PplsSweepArgs* a, hipStream_t st) {

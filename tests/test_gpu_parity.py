@@ -16,9 +16,14 @@ from oracle import ppls_oracle as o
 pytestmark = pytest.mark.gpu
 
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
-# (sweep, threads, rows_per_step): fused single-pass (512 / 1024 threads, 1 or 2 rows per step),
-# generic two-pass
-SWEEPS = [(1, 512, 1), (1, 512, 2), (1, 1024, 1), (2, 0, 1)]
+# sweep-kernel variants (context options): split ownership (default; auto = 2 rows per step,
+# occupancy grid), split 1 row/step pipelined / unpipelined, shared ownership v2 (512 / 1024
+# threads, 1 or 2 rows per step), generic two-pass
+SWEEPS = [dict(), dict(kernel=3, rows_per_step=1, pipe=1), dict(kernel=3, rows_per_step=1, pipe=0),
+          dict(kernel=2, threads=512, rows_per_step=1), dict(kernel=2, threads=512, rows_per_step=2),
+          dict(kernel=2, threads=1024), dict(sweep=2)]
+SWEEP_IDS = ["split", "split_rp1", "split_rp1_nopipe", "v2_512", "v2_512_rp2", "v2_1024", "twopass"]
+DEFAULTS = dict(sweep=0, threads=0, grid=0, rows_per_step=0, kernel=0, pipe=1)
 
 
 @pytest.fixture(scope="module")
@@ -31,10 +36,14 @@ def ctx():
 
 @pytest.fixture(autouse=True)
 def _reset_options(ctx):
-    for k in ("sweep", "threads", "grid"):
-        ctx.set_option(k, 0)
-    ctx.set_option("rows_per_step", 0)
+    for k, v in DEFAULTS.items():
+        ctx.set_option(k, v)
     yield
+
+
+def _apply(ctx, opts):
+    for k, v in opts.items():
+        ctx.set_option(k, v)
 
 
 def _theta(th):
@@ -51,15 +60,12 @@ def _golden():
     return sorted(f for f in os.listdir(GOLD) if f.endswith(".npz"))
 
 
-@pytest.mark.parametrize("sweep", SWEEPS)
+@pytest.mark.parametrize("sweep", SWEEPS, ids=SWEEP_IDS)
 @pytest.mark.parametrize("name", _golden())
 def test_em_run_matches_golden(ctx, name, sweep):
     g = np.load(os.path.join(GOLD, name))
     meta = json.loads(str(g["meta"]))
-    ctx.set_option("sweep", sweep[0])
-    ctx.set_option("threads", sweep[1])
-    ctx.set_option("rows_per_step", sweep[2])
-    ctx.set_option("grid", 0)
+    _apply(ctx, sweep)
     ctx.set_data(g["X"], g["Y"])
     th0 = dict(W=g["W0"], C=g["C0"], B=np.diag(g["B0"]), sigE=g["sig0"][0], sigF=g["sig0"][1],
                sigH=g["sig0"][2], sigT=np.diag(g["T0"]))
@@ -82,15 +88,13 @@ def test_em_run_matches_golden(ctx, name, sweep):
     assert not neg
 
 
-@pytest.mark.parametrize("sweep", SWEEPS)
+@pytest.mark.parametrize("sweep", SWEEPS, ids=SWEEP_IDS)
 @pytest.mark.parametrize("n,p,q,r", [(200, 50, 50, 2), (97, 33, 7, 1), (301, 64, 31, 5), (50, 9, 12, 8),
                                      (3, 5, 4, 2), (1, 6, 3, 1), (700, 1025, 3, 2), (400, 3, 1500, 3),
                                      (150, 17, 14, 10), (90, 24, 20, 16)])
 def test_estep_mstep_loglik_vs_oracle(ctx, sweep, n, p, q, r):
     X, Y, th0 = make_problem(n, p, q, r, seed=n + p + q + r)
-    ctx.set_option("sweep", sweep[0])
-    ctx.set_option("threads", sweep[1])
-    ctx.set_option("rows_per_step", sweep[2])
+    _apply(ctx, sweep)
     ctx.set_data(X, Y)
     th = _theta(th0)
     e = ctx.estep(th)
@@ -181,6 +185,10 @@ def test_fused_and_twopass_agree_midsize(ctx):
     for sw in (1, 2):
         ctx.set_option("sweep", sw)
         out[sw] = ctx.em_run(th0, 6, -np.inf, 0)
+    ctx.set_option("sweep", 0)
+    ctx.set_option("kernel", 2)
+    out[3] = ctx.em_run(th0, 6, -np.inf, 0)
+    assert _relerr(out[3][1], out[1][1]) < 1e-12
     (e1, l1, x1, _), (e2, l2, x2, _) = out[1], out[2]
     assert _relerr(l1, l2) < 1e-12
     assert np.abs(e1.W - e2.W).max() < 1e-10
