@@ -257,6 +257,16 @@ int allreduce(ppls_ctx* c, double* buf, size_t count) {
   return PPLS_OK;
 }
 
+// Per-group partials plus, behind them, the two-stage reduction's chunk sums (sized for the largest
+// group count seen, so the tail pointer part + part_groups * part_ld is always in bounds).
+int ensure_part(ppls_ctx* c, int groups) {
+  if (groups <= c->part_groups && c->part) return PPLS_OK;
+  const size_t tmp = (size_t)ppls_reduce_tmp_len(groups, c->part_ld);
+  int rc = dalloc(c, &c->part, (size_t)groups * c->part_ld + tmp);
+  c->part_groups = rc ? 0 : groups;
+  return rc;
+}
+
 // Which sweep kernel runs for this shape: 3 = split ownership (default), 1 = shared ownership
 // (v2, option kernel=2), 2 = generic two-pass; *grid is the workgroup count.
 int sweep_plan(ppls_ctx* c, int r, PplsSweepArgs* a) {
@@ -295,10 +305,7 @@ int sweep(ppls_ctx* c, int r, int slot, bool write_mu) {
   PplsSweepArgs a;
   const int plan = sweep_plan(c, r, &a);
   const int groups = plan == 2 ? ppls_twopass_groups(std::max<int64_t>(c->n_local, 1), a.grid) : a.grid;
-  if (groups > c->part_groups || !c->part) {
-    if ((rc = dalloc(c, &c->part, (size_t)groups * c->part_ld))) return rc;
-    c->part_groups = groups;
-  }
+  if ((rc = ensure_part(c, groups))) return rc;
   if (write_mu && !c->mu)
     if ((rc = dalloc(c, &c->mu, (size_t)std::max<int64_t>(c->n_local, 1) * 2 * r))) return rc;
   if (plan == 2 && !c->Z)
@@ -334,7 +341,8 @@ int sweep(ppls_ctx* c, int r, int slot, bool write_mu) {
     else if (plan == 1) HIPCHK(c, ppls_launch_sweep_fused(&a, c->stream));
     else HIPCHK(c, ppls_launch_sweep_twopass(&a, c->Z, c->stream));
     if (c->timing) HIPCHK(c, hipEventRecord(e1, c->stream));
-    HIPCHK(c, ppls_launch_reduce(c->part, groups, c->part_ld, c->part_ld, c->stats, 0, c->stream));
+    HIPCHK(c, ppls_launch_reduce2(c->part, groups, c->part_ld, c->part_ld, c->stats,
+                                  c->part + (size_t)c->part_groups * c->part_ld, c->stream));
   }
   return allreduce(c, c->stats, (size_t)c->part_ld);
 }
@@ -361,7 +369,7 @@ int finalize(ppls_ctx* c, int r, int cur, int nxt, int logl_index, int type) {
   f.work = c->work;
   f.status = c->status;
   f.qr = type == PPLS_ORTH_QR ? 1 : 0;
-  f.mode = 3;
+  f.mode = 3 & ~(c->ablate >> 2);   // ablate bit2: skip polar, bit3: skip scalars (timing only)
   HIPCHK(c, ppls_launch_finalize(&f, c->stream));
   return PPLS_OK;
 }
@@ -552,7 +560,7 @@ int ppls_set_option(ppls_ctx* c, const char* key, int64_t value) {
   } else if (!strcmp(key, "pipe")) {
     c->pipe_opt = value ? 1 : 0;
   } else if (!strcmp(key, "ablate")) {
-    if (value < 0 || value > 3) return fail(c, PPLS_E_ARG, "ablate must be in [0,3]");
+    if (value < 0 || value > 15) return fail(c, PPLS_E_ARG, "ablate must be in [0,15]");
     c->ablate = (int)value;   // timing experiments only: results are wrong while set
   } else if (!strcmp(key, "timing")) {
     c->timing = value ? 1 : 0;
@@ -728,10 +736,7 @@ int ppls_mstep(ppls_ctx* c, const ppls_expect* fit, int r, int type, ppls_theta*
   if ((rc = ensure_r(c, r, 1))) return rc;
   const int grid = grid_of(c);
   const int groups = ppls_twopass_groups(std::max<int64_t>(c->n_local, 1), grid);
-  if (groups > c->part_groups || !c->part) {
-    if ((rc = dalloc(c, &c->part, (size_t)groups * c->part_ld))) return rc;
-    c->part_groups = groups;
-  }
+  if ((rc = ensure_part(c, groups))) return rc;
   if (!c->Z && (rc = dalloc(c, &c->Z, (size_t)std::max<int64_t>(c->n_local, 1) * 2 * r))) return rc;
   // Z = [mu_T | mu_U] row-major, coefficients alpha = delta = 1, beta = gamma = 0:
   // the accumulate pass then computes exactly X'mu_T and Y'mu_U (EM_W_multi.R:732-733).

@@ -64,6 +64,9 @@ int ppls_twopass_groups(int64_t n_local, int grid);
 hipError_t ppls_launch_reduce(const double* part, int ngroups, int64_t ld, int64_t len, double* out,
                               int accumulate, hipStream_t st);
 hipError_t ppls_launch_finalize(const PplsFinalizeArgs* f, hipStream_t st);
+int64_t ppls_reduce_tmp_len(int ngroups, int64_t len);
+hipError_t ppls_launch_reduce2(const double* part, int ngroups, int64_t ld, int64_t len, double* out,
+                               double* tmp, hipStream_t st);
 hipError_t ppls_launch_loglc(const double* G, const double* ssq, double N, int p, int q, int r,
                              double sigX, double sigY, const double* coefs, double* out, hipStream_t st);
 hipError_t ppls_launch_sumsq(const double* a, int64_t len, double* part, int nblocks, double* out,

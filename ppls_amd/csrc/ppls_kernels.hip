@@ -181,6 +181,22 @@ __global__ void ppls_reduce_partials_kernel(const double* __restrict__ part, int
   out[j] = accumulate ? out[j] + t : t;
 }
 
+// Stage 1 of the two-stage reduction: tmp[chunk][j] = sum of groups [chunk*32, chunk*32+32).
+__global__ void ppls_reduce_chunks_kernel(const double* __restrict__ part, int ngroups, int64_t ld,
+                                          int64_t len, double* __restrict__ tmp) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= len) return;
+  const int g0 = blockIdx.y * 32, g1 = min(ngroups, g0 + 32);
+  double s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  int g = g0;
+  for (; g + 8 <= g1; g += 8) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s[u] += part[(int64_t)(g + u) * ld + j];
+  }
+  for (int u = 0; g < g1; ++g, ++u) s[u] += part[(int64_t)g * ld + j];
+  tmp[(int64_t)blockIdx.y * len + j] = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
+}
+
 // ============================================================================ wave reduce-scatter
 // V values per lane -> after 6 butterfly levels lane holds the full wave sum of value `idx`.
 // Levels: 0 permlane32_swap (bit5), 1 permlane16_swap (bit4), 2 row_mirror (bit3),
@@ -852,6 +868,7 @@ __device__ void ppls_block_polar(const double* S, int64_t lds, int p, int r, dou
   __shared__ double sh[16 * PPLS_RMAX];
   __shared__ double Rm[PPLS_RMAX * PPLS_RMAX];
   __shared__ double P[PPLS_RMAX * PPLS_RMAX];
+  __shared__ double jw[2 * PPLS_RMAX * PPLS_RMAX];   // Jacobi workspace
   __shared__ double vtv_s[PPLS_RMAX];
   const int tid = threadIdx.x, nt = blockDim.x;
   for (int k = 0; k < r; ++k)
@@ -921,7 +938,7 @@ __device__ void ppls_block_polar(const double* S, int64_t lds, int p, int r, dou
     if (qr) {
       for (int j = 0; j < r; ++j)
         for (int i = 0; i < r; ++i) P[j * r + i] = (i == j) ? 1.0 : 0.0;
-    } else if (ppls_small_polar(Rm, r, P) != 0) {
+    } else if (ppls_small_polar_ws<PPLS_RMAX>(Rm, r, P, jw, jw + r * r) != 0) {
       *status = -3;
     }
   }
@@ -987,19 +1004,26 @@ __device__ void ppls_inv_upper(const double* U, double* Ui) {
 // Polar factor U V' of the p x r matrix S (column-major, ld lds) by Cholesky-QR2:
 //   G1 = S'S = R1'R1, Q1 = S R1^-1, G2 = Q1'Q1 = R2'R2, R = R2 R1 (orthogonality O(eps kappa)),
 //   R = U_R Sigma V_R' (one-sided Jacobi), polar(S) = S R^-1 U_R V_R'.
-// Two block reductions instead of the 3r of Householder.  Returns false when a Cholesky pivot
-// fails (kappa(S) ~> 1e8); the caller then falls back to Householder.
+// Two block reductions instead of the 3r of Householder.  The r x r algebra runs on one thread
+// with every operand in LDS (sm: >= 10 R^2 doubles).  Returns false when a Cholesky pivot fails
+// (kappa(S) ~> 1e8); the caller then falls back to Householder.
 template <int R>
 __device__ bool ppls_block_polar_cholqr2(const double* S, int64_t lds, int p, double* out, int64_t ldo,
-                                        int ldo_rows, double* sh, double* sm /* >= 4 R^2 */) {
+                                        int ldo_rows, double* sh, double* sm) {
   constexpr int NG = R * (R + 1) / 2;
+  constexpr int RR = R * R;
   const int tid = threadIdx.x, nt = blockDim.x;
-  double* R1 = sm;
-  double* M = sm + R * R;          // R1^-1, later R1^-1 R2^-1 U V'
-  double* T = sm + 2 * R * R;
+  double* R1 = sm;               // R1, later the final r x r multiplier
+  double* M = sm + RR;           // R1^-1
+  double* Gm = sm + 2 * RR;
+  double* R2 = sm + 3 * RR;
+  double* Rr = sm + 4 * RR;
+  double* R2i = sm + 5 * RR;
+  double* P = sm + 6 * RR;
+  double* T = sm + 7 * RR;
+  double* A = sm + 8 * RR;       // Jacobi workspace (2 RR)
   __shared__ int ok;
   double vals[NG];
-  // G1 = S'S
 #pragma unroll
   for (int e = 0; e < NG; ++e) vals[e] = 0.0;
   for (int i = tid; i < p; i += nt) {
@@ -1010,20 +1034,18 @@ __device__ bool ppls_block_polar_cholqr2(const double* S, int64_t lds, int p, do
 #pragma unroll
     for (int b = 0; b < R; ++b)
 #pragma unroll
-      for (int a = 0; a <= b; ++a) vals[e++] = fma(x[a], x[b], vals[e]);
+      for (int a = 0; a <= b; ++a) { vals[e] = fma(x[a], x[b], vals[e]); ++e; }
   }
   ppls_block_sum_t<NG>(vals, sh);
   if (tid == 0) {
-    double G[R * R];
     int e = 0;
     for (int b = 0; b < R; ++b)
-      for (int a = 0; a <= b; ++a) { G[b * R + a] = vals[e]; G[a * R + b] = vals[e]; ++e; }
-    ok = ppls_chol_upper<R>(G, R1);
+      for (int a = 0; a <= b; ++a) { Gm[b * R + a] = vals[e]; Gm[a * R + b] = vals[e]; ++e; }
+    ok = ppls_chol_upper<R>(Gm, R1);
     if (ok) ppls_inv_upper<R>(R1, M);
   }
   __syncthreads();
   if (!ok) return false;
-  // G2 = Q1'Q1 with Q1 = S R1^-1 (rows recomputed on the fly)
 #pragma unroll
   for (int e = 0; e < NG; ++e) vals[e] = 0.0;
   for (int i = tid; i < p; i += nt) {
@@ -1041,36 +1063,34 @@ __device__ bool ppls_block_polar_cholqr2(const double* S, int64_t lds, int p, do
 #pragma unroll
     for (int b = 0; b < R; ++b)
 #pragma unroll
-      for (int a = 0; a <= b; ++a) vals[e++] = fma(qv[a], qv[b], vals[e]);
+      for (int a = 0; a <= b; ++a) { vals[e] = fma(qv[a], qv[b], vals[e]); ++e; }
   }
   ppls_block_sum_t<NG>(vals, sh);
   if (tid == 0) {
-    double G[R * R], R2[R * R], Rr[R * R], R2i[R * R], P[R * R];
     int e = 0;
     for (int b = 0; b < R; ++b)
-      for (int a = 0; a <= b; ++a) { G[b * R + a] = vals[e]; G[a * R + b] = vals[e]; ++e; }
-    ok = ppls_chol_upper<R>(G, R2);
+      for (int a = 0; a <= b; ++a) { Gm[b * R + a] = vals[e]; Gm[a * R + b] = vals[e]; ++e; }
+    ok = ppls_chol_upper<R>(Gm, R2);
     if (ok) {
-      // R = R2 R1 (upper); P = U_R V_R'; M <- R1^-1 R2^-1 P
-      for (int j = 0; j < R; ++j)
+      for (int j = 0; j < R; ++j)            // R = R2 R1
         for (int i = 0; i < R; ++i) {
           double s = 0.0;
           for (int k = 0; k < R; ++k) s += R2[k * R + i] * R1[j * R + k];
           Rr[j * R + i] = s;
         }
-      ok = ppls_small_polar_n<R>(Rr, R, P) == 0;
+      ok = ppls_small_polar_ws<R>(Rr, R, P, A, A + RR) == 0;
       ppls_inv_upper<R>(R2, R2i);
-      for (int j = 0; j < R; ++j)
+      for (int j = 0; j < R; ++j)            // T = R2^-1 P
         for (int i = 0; i < R; ++i) {
           double s = 0.0;
           for (int k = 0; k < R; ++k) s += R2i[k * R + i] * P[j * R + k];
           T[j * R + i] = s;
         }
-      for (int j = 0; j < R; ++j)
+      for (int j = 0; j < R; ++j)            // R1 <- R1^-1 R2^-1 P
         for (int i = 0; i < R; ++i) {
           double s = 0.0;
           for (int k = 0; k < R; ++k) s += M[k * R + i] * T[j * R + k];
-          R1[j * R + i] = s;   // reuse R1 as the final r x r multiplier
+          R1[j * R + i] = s;
         }
     }
   }
@@ -1092,7 +1112,8 @@ __device__ bool ppls_block_polar_cholqr2(const double* S, int64_t lds, int p, do
 }
 
 // Block 0: W_next = orth(S_X); block 1: C_next = orth(S_Y); block 2: scalars (moments, loglik,
-// M-step).  stats = [SX ldx*R][SY ldy*R][G 4R^2];  ssq = {||X||^2, ||Y||^2}.
+// M-step).  stats = [SX ldx*R][SY ldy*R][G 4R^2];  ssq = {||X||^2, ||Y||^2}.  Every sequential
+// working set lives in LDS (no private-memory scratch).
 template <int R>
 __global__ __launch_bounds__(256) void ppls_finalize_kernel(
     const double* __restrict__ stats, const double* __restrict__ ssq, double N, int p, int q, int ldx,
@@ -1100,11 +1121,16 @@ __global__ __launch_bounds__(256) void ppls_finalize_kernel(
     const PplsScalars* __restrict__ sc_cur, double* __restrict__ Wn, double* __restrict__ Cn,
     PplsScalars* __restrict__ sc_nxt, PplsMoments* __restrict__ mom, double* __restrict__ loglik,
     int logl_index, double* __restrict__ work, int* __restrict__ status, int qr, int mode) {
-  __shared__ double sh[4 * R * (R + 1)];
-  __shared__ double sm[4 * R * R];
+  constexpr int NG = R * (R + 1) / 2;
+  __shared__ double sh[4 * 2 * NG];
+  __shared__ double sm[10 * R * R];
+  __shared__ PplsScalars s_cur, s_nx;
+  __shared__ PplsMoments s_m;
+  __shared__ double s_G[4 * R * R], s_WtW[R * R], s_CtC[R * R];
   const double* SX = stats;
   const double* SY = stats + (int64_t)R * ldx;
   const double* G = SY + (int64_t)R * ldy;
+  const int tid = threadIdx.x;
   if (blockIdx.x < 2) {
     if (!(mode & 1)) return;
     const bool isx = blockIdx.x == 0;
@@ -1117,12 +1143,18 @@ __global__ __launch_bounds__(256) void ppls_finalize_kernel(
     return;
   }
   if (!(mode & 2)) return;
+  // stage theta's scalars and the Gram in LDS (all threads)
+  {
+    const double* src = (const double*)sc_cur;
+    double* dst = (double*)&s_cur;
+    for (int i = tid; i < (int)(sizeof(PplsScalars) / 8); i += blockDim.x) dst[i] = src[i];
+    for (int i = tid; i < 4 * R * R; i += blockDim.x) s_G[i] = G[i];
+  }
   // W'W and C'C of the parameters the sweep used (one batched reduction)
-  constexpr int NG = R * (R + 1) / 2;
   double vals[2 * NG];
 #pragma unroll
   for (int e = 0; e < 2 * NG; ++e) vals[e] = 0.0;
-  for (int i = threadIdx.x; i < (p > q ? p : q); i += blockDim.x) {
+  for (int i = tid; i < (p > q ? p : q); i += blockDim.x) {
     double wv[R], cv[R];
 #pragma unroll
     for (int k = 0; k < R; ++k) {
@@ -1140,26 +1172,28 @@ __global__ __launch_bounds__(256) void ppls_finalize_kernel(
       }
   }
   ppls_block_sum_t<2 * NG>(vals, sh);
-  if (threadIdx.x == 0) {
-    double WtW[R * R], CtC[R * R];
+  if (tid == 0) {
     int e = 0;
     for (int b = 0; b < R; ++b)
       for (int a = 0; a <= b; ++a) {
-        WtW[b * R + a] = WtW[a * R + b] = vals[e];
-        CtC[b * R + a] = CtC[a * R + b] = vals[NG + e];
+        s_WtW[b * R + a] = s_WtW[a * R + b] = vals[e];
+        s_CtC[b * R + a] = s_CtC[a * R + b] = vals[NG + e];
         ++e;
       }
-    double Gl[4 * R * R];
-    for (int i = 0; i < 4 * R * R; ++i) Gl[i] = G[i];
-    const PplsScalars cur = *sc_cur;
     const double s0 = ssq[0], s1 = ssq[1];
-    if (logl_index >= 0) loglik[logl_index] = ppls_loglik_from_gram(Gl, s0, s1, N, p, q, R, &cur);
-    PplsMoments m;
-    ppls_estep_moments(Gl, WtW, CtC, s0, s1, N, p, q, R, &cur, &m);
-    *mom = m;
-    PplsScalars nx = cur;
-    ppls_mstep_scalars(&m, R, &nx);
-    *sc_nxt = nx;
+    if (logl_index >= 0) loglik[logl_index] = ppls_loglik_from_gram(s_G, s0, s1, N, p, q, R, &s_cur);
+    ppls_estep_moments(s_G, s_WtW, s_CtC, s0, s1, N, p, q, R, &s_cur, &s_m);
+    s_nx = s_cur;
+    ppls_mstep_scalars(&s_m, R, &s_nx);
+  }
+  __syncthreads();
+  {
+    const double* a = (const double*)&s_m;
+    double* b = (double*)mom;
+    for (int i = tid; i < (int)(sizeof(PplsMoments) / 8); i += blockDim.x) b[i] = a[i];
+    const double* c = (const double*)&s_nx;
+    double* d = (double*)sc_nxt;
+    for (int i = tid; i < (int)(sizeof(PplsScalars) / 8); i += blockDim.x) d[i] = c[i];
   }
 }
 
@@ -1447,6 +1481,29 @@ int ppls_twopass_groups(int64_t n_local, int grid) {
   return (int)((n_local + rpc - 1) / rpc);
 }
 
+// Fixed-order two-stage reduction: stage 1 sums chunks of RCHUNK groups (many blocks busy), stage 2
+// sums the chunk results.  tmp: ceil(ngroups / RCHUNK) * len doubles (taken from the tail of part
+// when the caller passes tmp == nullptr is not allowed; see ppls_reduce_tmp_len).
+#define PPLS_RCHUNK 32
+int64_t ppls_reduce_tmp_len(int ngroups, int64_t len) {
+  return ngroups > PPLS_RCHUNK ? (int64_t)((ngroups + PPLS_RCHUNK - 1) / PPLS_RCHUNK) * len : 0;
+}
+
+hipError_t ppls_launch_reduce2(const double* part, int ngroups, int64_t ld, int64_t len, double* out,
+                               double* tmp, hipStream_t st) {
+  if (ngroups <= PPLS_RCHUNK || tmp == nullptr) {
+    hipLaunchKernelGGL(ppls_reduce_partials_kernel, dim3((unsigned)((len + 255) / 256)), dim3(256), 0,
+                       st, part, ngroups, ld, len, out, 0);
+    return hipGetLastError();
+  }
+  const int nch = (ngroups + PPLS_RCHUNK - 1) / PPLS_RCHUNK;
+  hipLaunchKernelGGL(ppls_reduce_chunks_kernel, dim3((unsigned)((len + 255) / 256), nch), dim3(256), 0,
+                     st, part, ngroups, ld, len, tmp);
+  hipLaunchKernelGGL(ppls_reduce_partials_kernel, dim3((unsigned)((len + 255) / 256)), dim3(256), 0,
+                     st, tmp, nch, len, len, out, 0);
+  return hipGetLastError();
+}
+
 hipError_t ppls_launch_reduce(const double* part, int ngroups, int64_t ld, int64_t len, double* out,
                               int accumulate, hipStream_t st) {
   hipLaunchKernelGGL(ppls_reduce_partials_kernel, dim3((unsigned)((len + 255) / 256)), dim3(256), 0,
@@ -1462,9 +1519,7 @@ hipError_t ppls_launch_finalize(const PplsFinalizeArgs* f, hipStream_t st) {
     case 4: return launch_finalize_t<4>(f, st);
     case 5: return launch_finalize_t<5>(f, st);
     case 6: return launch_finalize_t<6>(f, st);
-    case 7: return launch_finalize_t<7>(f, st);
-    case 8: return launch_finalize_t<8>(f, st);
-    default:
+    default:   // r = 7..16: runtime-r finalize (the unrolled batched reductions would spill)
       hipLaunchKernelGGL(ppls_finalize_generic_kernel, dim3(3), dim3(256), 0, st, f->stats, f->ssq, f->N,
                          f->p, f->q, f->r, f->ldx, f->ldy, f->Wc, f->Cc, f->sc_cur, f->Wn, f->Cn,
                          f->sc_nxt, f->mom, f->loglik, f->logl_index, f->work, f->status, f->qr, f->mode);

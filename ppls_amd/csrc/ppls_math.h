@@ -271,6 +271,62 @@ PPLS_HD int ppls_small_polar_n(const double* R, int r, double* P) {
   return rc;
 }
 
+// Same algorithm with caller-provided workspace A, V (r*r each; e.g. LDS on the device).
+template <int RC>
+PPLS_HD int ppls_small_polar_ws(const double* R, int r, double* P, double* A, double* V) {
+  for (int i = 0; i < r * r; ++i) A[i] = R[i];
+  for (int j = 0; j < r; ++j)
+    for (int i = 0; i < r; ++i) V[j * r + i] = (i == j) ? 1.0 : 0.0;
+  for (int sweep = 0; sweep < 60; ++sweep) {
+    double off = 0.0;
+    for (int i = 0; i < r - 1; ++i)
+      for (int j = i + 1; j < r; ++j) {
+        double a = 0.0, b = 0.0, g = 0.0;
+        for (int k = 0; k < r; ++k) {
+          a += A[i * r + k] * A[i * r + k];
+          b += A[j * r + k] * A[j * r + k];
+          g += A[i * r + k] * A[j * r + k];
+        }
+        if (g == 0.0) continue;
+        const double rel = fabs(g) / sqrt(a * b);
+        if (rel > off) off = rel;
+        if (rel < 1e-17) continue;
+        const double zeta = (b - a) / (2.0 * g);
+        const double tt = (zeta >= 0.0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
+        const double c = 1.0 / sqrt(1.0 + tt * tt), sn = c * tt;
+        for (int k = 0; k < r; ++k) {
+          const double x = A[i * r + k], y = A[j * r + k];
+          A[i * r + k] = c * x - sn * y;
+          A[j * r + k] = sn * x + c * y;
+          const double vx = V[i * r + k], vy = V[j * r + k];
+          V[i * r + k] = c * vx - sn * vy;
+          V[j * r + k] = sn * vx + c * vy;
+        }
+      }
+    if (off < 1e-15) break;
+  }
+  double smax = 0.0, sv[RC];
+  for (int i = 0; i < r; ++i) {
+    double nrm = 0.0;
+    for (int k = 0; k < r; ++k) nrm += A[i * r + k] * A[i * r + k];
+    sv[i] = sqrt(nrm);
+    if (sv[i] > smax) smax = sv[i];
+  }
+  int rc = 0;
+  for (int i = 0; i < r; ++i) {
+    if (!(sv[i] > smax * 1e-14)) { rc = -1; sv[i] = 1.0; }
+    for (int k = 0; k < r; ++k) A[i * r + k] /= sv[i];   // U_R column i
+  }
+  // P = U V'
+  for (int j = 0; j < r; ++j)
+    for (int i = 0; i < r; ++i) {
+      double acc = 0.0;
+      for (int k = 0; k < r; ++k) acc += A[k * r + i] * V[k * r + j];
+      P[j * r + i] = acc;
+    }
+  return rc;
+}
+
 PPLS_HD int ppls_small_polar(const double* R, int r, double* P) {
   return ppls_small_polar_n<PPLS_RMAX>(R, r, P);
 }
