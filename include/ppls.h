@@ -131,6 +131,11 @@ int ppls_sweep_timing(ppls_ctx* ctx, double* total_ms, int64_t* launches, int re
 /* Shape facts for the roofline: bytes of X and Y one sweep reads (algorithmic), kernel variant. */
 int ppls_sweep_info(ppls_ctx* ctx, int r, int64_t* bytes_per_sweep, int* variant, int* grid);
 
+/* Diagnostics: wall-clock stamps of the last finalize's phases (PPLS_FTRACE_LEN = 3 blocks x 16
+ * slots; 0 = slot not reached) and the tick length in ns.  Requires set_option("ftrace", 1). */
+#define PPLS_FTRACE_LEN 48
+int ppls_finalize_trace(ppls_ctx* ctx, int64_t* stamps, double* tick_ns);
+
 /* ---- host-side algebra (no GPU; the same code the device finalize runs) ------------------------ */
 /* From the all-reduced sufficient statistics of one sweep with theta (stats = [X'mu_T p x r |
  * Y'mu_U q x r | Gram 2r x 2r], all column-major) compute Expect_M's moments, logl_W(theta) and

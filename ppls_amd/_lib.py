@@ -66,6 +66,7 @@ SIGNATURES = {
     "ppls_em_state": (ct.c_int, [ct.c_void_p, ct.POINTER(PplsTheta), _dp, ct.c_int, ct.POINTER(ct.c_int)]),
     "ppls_synchronize": (ct.c_int, [ct.c_void_p]),
     "ppls_sweep_timing": (ct.c_int, [ct.c_void_p, _dp, ct.POINTER(ct.c_int64), ct.c_int]),
+    "ppls_finalize_trace": (ct.c_int, [ct.c_void_p, ct.POINTER(ct.c_int64), _dp]),
     "ppls_sweep_info": (ct.c_int, [ct.c_void_p, ct.c_int, ct.POINTER(ct.c_int64), ct.POINTER(ct.c_int),
                                    ct.POINTER(ct.c_int)]),
     "ppls_finalize_host": (ct.c_int, [_dp, _dp, _dp, ct.c_double, ct.c_double, ct.c_double, ct.c_int,

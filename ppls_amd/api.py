@@ -223,6 +223,20 @@ class Context:
         self._chk(self._L.ppls_sweep_timing(self.h, ct.byref(ms), ct.byref(n), int(reset)))
         return ms.value, n.value
 
+    def finalize_trace(self):
+        """Phase stamps of the last finalize (set_option('ftrace', 1) first): {block: [us since the
+        block's first stamp, ...]} for the slots that were reached."""
+        buf = (ct.c_int64 * 48)()
+        tick = ct.c_double()
+        self._chk(self._L.ppls_finalize_trace(self.h, buf, ct.byref(tick)))
+        out = {}
+        for b in range(3):
+            s = [buf[16 * b + i] for i in range(16)]
+            if s[0]:
+                out[b] = [round((v - s[0]) * tick.value * 1e-3, 3) if v else None for v in s[:10]]
+                out[b] += s[10:]   # raw diagnostics (counts, core clock stamps)
+        return out
+
     def sweep_info(self, r):
         b, v, g = ct.c_int64(), ct.c_int(), ct.c_int()
         self._chk(self._L.ppls_sweep_info(self.h, int(r), ct.byref(b), ct.byref(v), ct.byref(g)))

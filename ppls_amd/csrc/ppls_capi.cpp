@@ -50,6 +50,8 @@ struct ppls_ctx {
   double* W[2] = {nullptr, nullptr};
   double* C[2] = {nullptr, nullptr};
   PplsScalars* sc[2] = {nullptr, nullptr};
+  double* gram[2] = {nullptr, nullptr};   // [W'W | C'C] of W[i], C[i]
+  double* vstate = nullptr;   // polar Jacobi warm start [V_W | V_C], reset on every theta upload
   PplsMoments* mom = nullptr;
   double* stats = nullptr;
   double* part = nullptr;
@@ -61,6 +63,7 @@ struct ppls_ctx {
   int loglik_cap = 0;
   double* work = nullptr;
   int* status = nullptr;
+  long long* ftrace = nullptr;   // finalize phase timestamps (diagnostics)
   double* coefs = nullptr;     // loglC_fast coefficient block (5r)
   double* scratch = nullptr;   // generic device scratch
   size_t scratch_bytes = 0;
@@ -156,8 +159,10 @@ int ensure_r(ppls_ctx* c, int r, int max_steps) {
       if ((rc = dalloc(c, &c->W[i], (size_t)c->ldx * r))) return rc;
       if ((rc = dalloc(c, &c->C[i], (size_t)c->ldy * r))) return rc;
       if ((rc = dalloc(c, &c->sc[i], 1))) return rc;
+      if ((rc = dalloc(c, &c->gram[i], (size_t)2 * r * r))) return rc;
     }
     if ((rc = dalloc(c, &c->mom, 1))) return rc;
+    if ((rc = dalloc(c, &c->vstate, (size_t)2 * r * r))) return rc;
     c->part_ld = (int64_t)r * c->ldx + (int64_t)r * c->ldy + 4 * (int64_t)r * r;
     if ((rc = dalloc(c, &c->stats, (size_t)c->part_ld))) return rc;
     if ((rc = dalloc(c, &c->work, (size_t)2 * (c->p + c->q) * r + 16))) return rc;
@@ -188,6 +193,21 @@ int upload_theta(ppls_ctx* c, const ppls_theta* th, int r, int slot) {
   HIPCHK(c, hipMemcpyAsync(c->C[slot], buf.data(), sizeof(double) * c->ldy * r, hipMemcpyHostToDevice, c->stream));
   PplsScalars s = scalars_of(th, r);
   HIPCHK(c, hipMemcpyAsync(c->sc[slot], &s, sizeof s, hipMemcpyHostToDevice, c->stream));
+  // [W'W | C'C] for the finalize's scalar block (later iterations get it from the polar blocks)
+  std::vector<double> g((size_t)2 * r * r);
+  for (int a = 0; a < r; ++a)
+    for (int b = 0; b < r; ++b) {
+      double w = 0.0, cc = 0.0;
+      for (int i = 0; i < c->p; ++i) w += th->W[(size_t)a * c->p + i] * th->W[(size_t)b * c->p + i];
+      for (int i = 0; i < c->q; ++i) cc += th->C[(size_t)a * c->q + i] * th->C[(size_t)b * c->q + i];
+      g[(size_t)b * r + a] = w;
+      g[(size_t)r * r + (size_t)b * r + a] = cc;
+    }
+  HIPCHK(c, hipMemcpyAsync(c->gram[slot], g.data(), sizeof(double) * g.size(), hipMemcpyHostToDevice, c->stream));
+  // identity warm start for the polar Jacobi: a run's result depends only on its own theta0
+  std::vector<double> eye(g.size());
+  for (size_t e = 0; e < eye.size(); ++e) eye[e] = ((e % ((size_t)r * r)) % (size_t)(r + 1)) == 0 ? 1.0 : 0.0;
+  HIPCHK(c, hipMemcpyAsync(c->vstate, eye.data(), sizeof(double) * eye.size(), hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return PPLS_OK;
 }
@@ -370,6 +390,10 @@ int finalize(ppls_ctx* c, int r, int cur, int nxt, int logl_index, int type) {
   f.status = c->status;
   f.qr = type == PPLS_ORTH_QR ? 1 : 0;
   f.mode = 3 & ~(c->ablate >> 2);   // ablate bit2: skip polar, bit3: skip scalars (timing only)
+  f.trace = c->ftrace;
+  f.gram_cur = c->gram[cur];
+  f.gram_nxt = c->gram[nxt];
+  f.vstate = c->vstate;
   HIPCHK(c, ppls_launch_finalize(&f, c->stream));
   return PPLS_OK;
 }
@@ -528,9 +552,11 @@ void ppls_ctx_destroy(ppls_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->comm) ncclCommDestroy(c->comm);
   dfree(c->X); dfree(c->Y); dfree(c->ssq);
-  for (int i = 0; i < 2; ++i) { dfree(c->W[i]); dfree(c->C[i]); dfree(c->sc[i]); }
+  for (int i = 0; i < 2; ++i) { dfree(c->W[i]); dfree(c->C[i]); dfree(c->sc[i]); dfree(c->gram[i]); }
+  dfree(c->vstate);
   dfree(c->mom); dfree(c->stats); dfree(c->part); dfree(c->Z); dfree(c->mu); dfree(c->loglik);
   dfree(c->work); dfree(c->status); dfree(c->coefs); dfree(c->scratch);
+  if (c->ftrace) (void)hipFree(c->ftrace);
   for (auto& e : c->ev) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
@@ -562,6 +588,15 @@ int ppls_set_option(ppls_ctx* c, const char* key, int64_t value) {
   } else if (!strcmp(key, "ablate")) {
     if (value < 0 || value > 15) return fail(c, PPLS_E_ARG, "ablate must be in [0,15]");
     c->ablate = (int)value;   // timing experiments only: results are wrong while set
+  } else if (!strcmp(key, "ftrace")) {
+    if (value && !c->ftrace) {
+      HIPCHK(c, hipMalloc(&c->ftrace, PPLS_FTRACE_LEN * sizeof(long long)));
+      HIPCHK(c, hipMemset(c->ftrace, 0, PPLS_FTRACE_LEN * sizeof(long long)));
+    } else if (!value && c->ftrace) {
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+      (void)hipFree(c->ftrace);
+      c->ftrace = nullptr;
+    }
   } else if (!strcmp(key, "timing")) {
     c->timing = value ? 1 : 0;
   } else {
@@ -966,6 +1001,19 @@ int ppls_sweep_info(ppls_ctx* c, int r, int64_t* bytes_per_sweep, int* variant, 
   if (bytes_per_sweep) *bytes_per_sweep = (int64_t)8 * c->n_local * ((int64_t)c->p + c->q);
   if (variant) *variant = plan == 3 ? 4 : plan == 1 ? (a.threads == 1024 ? 3 : 1) : 2;
   if (grid) *grid = a.grid;
+  return PPLS_OK;
+}
+
+int ppls_finalize_trace(ppls_ctx* c, int64_t* stamps, double* tick_ns) {
+  if (!c || !stamps) return PPLS_E_ARG;
+  if (!c->ftrace) return fail(c, PPLS_E_STATE, "finalize tracing is off (set_option ftrace 1)");
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  HIPCHK(c, hipMemcpy(stamps, c->ftrace, PPLS_FTRACE_LEN * sizeof(long long), hipMemcpyDeviceToHost));
+  if (tick_ns) {
+    int khz = 0;
+    HIPCHK(c, hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c->device));
+    *tick_ns = khz > 0 ? 1e6 / khz : 0.0;
+  }
   return PPLS_OK;
 }
 

@@ -50,6 +50,10 @@ struct PplsFinalizeArgs {
   int* status;
   int qr;                // orth type: 0 SVD (polar), 1 QR
   int mode;              // bit0: W/C update (polar), bit1: scalars (moments, loglik, M-step)
+  const double* gram_cur;   // [W'W | C'C] (2 r^2) of Wc, Cc, or nullptr (finalize computes it)
+  double* gram_nxt;         // receives [Wn'Wn | Cn'Cn], or nullptr
+  double* vstate;           // [V_W | V_C] (2 r^2) Jacobi warm start carried across iterations, or nullptr
+  long long* trace;      // diagnostics: per-block phase timestamps (16 per block) or nullptr
 };
 
 extern "C" {

@@ -863,7 +863,7 @@ __device__ void ppls_block_sum(double* vals, int nv, double* sh) {
 
 // Polar factor of the p x r matrix S (ld lds): Householder QR S = QR, Jacobi R = U S V',
 // out = Q U V'.  A, E: p x r scratch (ld p).  Returns status through *status.
-__device__ void ppls_block_polar(const double* S, int64_t lds, int p, int r, double* out,
+__device__ __noinline__ void ppls_block_polar(const double* S, int64_t lds, int p, int r, double* out,
                                  int64_t ldo, int ldo_rows, double* A, double* E, int* status, int qr) {
   __shared__ double sh[16 * PPLS_RMAX];
   __shared__ double Rm[PPLS_RMAX * PPLS_RMAX];
@@ -952,178 +952,603 @@ __device__ void ppls_block_polar(const double* S, int64_t lds, int p, int r, dou
     }
 }
 
-// Block-wide sum of NV values per thread with a compile-time count (registers, no scratch).
-template <int NV>
+// Block-wide sum of NV <= 64 values per thread (every thread gets the sums): a wave
+// reduce-scatter (ppls_rs: permlane/DPP, no LDS round trips) leaves each wave sum on one lane,
+// which writes it to LDS; the cross-wave sums are read back by every thread.
+template <int NV, int NW = 0>
 __device__ __forceinline__ void ppls_block_sum_t(double (&vals)[NV], double* sh) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
+  static_assert(NV >= 1 && NV <= 64, "block sum of at most 64 values");
+  constexpr int NB = NV + (NV & 1);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int nwaves = NW > 0 ? NW : (int)(blockDim.x >> 6);
+  double a[NB];
 #pragma unroll
-  for (int k = 0; k < NV; ++k) {
-    const double s = ppls_wave_sum(vals[k]);
-    if (lane == 0) sh[wave * NV + k] = s;
-  }
+  for (int k = 0; k < NV; ++k) a[k] = vals[k];
+  int idx = 0;
+  bool canon = true;
+  ppls_rs<NV, 0, NB>(a, lane, idx, canon);
+  if (canon && idx < NV) sh[wave * NV + idx] = a[0];
   __syncthreads();
 #pragma unroll
   for (int k = 0; k < NV; ++k) {
     double t = 0.0;
-    for (int w = 0; w < nwaves; ++w) t += sh[w * NV + k];
+#pragma unroll
+    for (int w = 0; w < (NW > 0 ? NW : 16); ++w)
+      if (NW > 0 || w < nwaves) t += sh[w * NV + k];
     vals[k] = t;
   }
   __syncthreads();
 }
 
-// Upper Cholesky G = R'R of an r x r SPD matrix (column-major); false if not numerically SPD.
+// Diagnostics stamp (finalize phases; tr == nullptr in production).
+__device__ __forceinline__ void ppls_stamp(long long* tr, int slot) {
+  if (tr && threadIdx.x == 0) tr[slot] = (long long)wall_clock64();
+}
+
+// ---- r x r algebra in registers (compile-time R, fully unrolled; run by one thread) -----------
+// Matrices are T[row][col].
+
+// Upper Cholesky G = U'U; false if a pivot is not positive.
 template <int R>
-__device__ bool ppls_chol_upper(const double* G, double* Rm) {
+__device__ __forceinline__ bool ppls_chol_reg(const double (&G)[R][R], double (&U)[R][R], double (&dinv)[R]) {
+  bool ok = true;
+#pragma unroll
   for (int j = 0; j < R; ++j) {
-    for (int i = 0; i <= j; ++i) {
-      double s = G[j * R + i];
-      for (int k = 0; k < i; ++k) s -= Rm[i * R + k] * Rm[j * R + k];
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      if (i > j) { U[i][j] = 0.0; continue; }
+      double s = G[i][j];
+#pragma unroll
+      for (int k = 0; k < i; ++k) s = fma(-U[k][i], U[k][j], s);
       if (i == j) {
-        if (!(s > 0.0)) return false;
-        Rm[j * R + j] = sqrt(s);
+        ok = ok && (s > 0.0);
+        U[j][j] = sqrt(s > 0.0 ? s : 1.0);
+        dinv[j] = 1.0 / U[j][j];
       } else {
-        Rm[j * R + i] = s / Rm[i * R + i];
+        U[i][j] = s * dinv[i];
       }
     }
-    for (int i = j + 1; i < R; ++i) Rm[j * R + i] = 0.0;
   }
-  return true;
+  return ok;
 }
 
-// inv(U) for upper-triangular U (column-major), into Ui.
+// Ui = inv(U) for upper-triangular U with reciprocal diagonal dinv.
 template <int R>
-__device__ void ppls_inv_upper(const double* U, double* Ui) {
+__device__ __forceinline__ void ppls_inv_upper_reg(const double (&U)[R][R], const double (&dinv)[R],
+                                                   double (&Ui)[R][R]) {
+#pragma unroll
   for (int j = 0; j < R; ++j)
-    for (int i = R - 1; i >= 0; --i) {
+#pragma unroll
+    for (int ii = 0; ii < R; ++ii) {
+      const int i = R - 1 - ii;
+      if (i > j) { Ui[i][j] = 0.0; continue; }
       double s = (i == j) ? 1.0 : 0.0;
-      for (int k = i + 1; k < R; ++k) s -= U[k * R + i] * Ui[j * R + k];
-      Ui[j * R + i] = (i <= j) ? s / U[i * R + i] : 0.0;
+#pragma unroll
+      for (int k = i + 1; k <= j; ++k) s = fma(-U[i][k], Ui[k][j], s);
+      Ui[i][j] = s * dinv[i];
     }
 }
 
-// Polar factor U V' of the p x r matrix S (column-major, ld lds) by Cholesky-QR2:
-//   G1 = S'S = R1'R1, Q1 = S R1^-1, G2 = Q1'Q1 = R2'R2, R = R2 R1 (orthogonality O(eps kappa)),
-//   R = U_R Sigma V_R' (one-sided Jacobi), polar(S) = S R^-1 U_R V_R'.
-// Two block reductions instead of the 3r of Householder.  The r x r algebra runs on one thread
-// with every operand in LDS (sm: >= 10 R^2 doubles).  Returns false when a Cholesky pivot fails
-// (kappa(S) ~> 1e8); the caller then falls back to Householder.
+// 1/x and 1/sqrt(x) from the hardware estimates plus two Newton steps (~1 ulp; x normal, > 0
+// for rsq).  The serial r x r code is latency-bound on one wave, and these are 5-7 dependent
+// instructions against ~12-15 for the IEEE-exact expansions.
+__device__ __forceinline__ double ppls_rcp(double x) {
+  double y = __builtin_amdgcn_rcp(x);
+  double e = fma(-x, y, 1.0);
+  y = fma(y, e, y);
+  e = fma(-x, y, 1.0);
+  return fma(y, e, y);
+}
+__device__ __forceinline__ double ppls_rsq(double x) {
+  double y = __builtin_amdgcn_rsq(x);
+  double r = fma(-x * y, y, 1.0);
+  y = fma(0.5 * y, r, y);
+  r = fma(-x * y, y, 1.0);
+  return fma(0.5 * y, r, y);
+}
+
+// Round-robin (circle method) schedule of the R(R-1)/2 column pairs: N-1 rounds of N/2 disjoint
+// pairs (N = R rounded up to even; pairs with the dummy column R are dropped).
 template <int R>
-__device__ bool ppls_block_polar_cholqr2(const double* S, int64_t lds, int p, double* out, int64_t ldo,
-                                        int ldo_rows, double* sh, double* sm) {
+struct PplsRoundRobin {
+  static constexpr int N = R + (R & 1);
+  int i[N - 1][N / 2], j[N - 1][N / 2];
+  constexpr PplsRoundRobin() : i(), j() {
+    for (int m = 0; m < N - 1; ++m)
+      for (int k = 0; k < N / 2; ++k) {
+        const int pa = k == 0 ? 0 : ((k - 1 + m) % (N - 1)) + 1;
+        const int kb = N - 1 - k;
+        const int pb = ((kb - 1 + m) % (N - 1)) + 1;
+        i[m][k] = pa < pb ? pa : pb;
+        j[m][k] = pa < pb ? pb : pa;
+      }
+  }
+};
+
+// One-sided (Hestenes) Jacobi: A V = U Sigma, warm-started.  On entry V is orthogonal and
+// A = A0 V; on return A = U Sigma, V accumulates the rotations, sv = Sigma.  Sweeps of the
+// round-robin schedule until no pair has |a_i'a_j| >= 1e-15 ||a_i|| ||a_j|| (the stopping rule of
+// ppls_small_polar_n, ppls_math.h).  Branch-free, so the disjoint pairs of a round are
+// independent dependency chains the compiler interleaves.  Returns the sweep count.
+template <int R>
+__device__ __forceinline__ int ppls_jacobi_reg(double (&A)[R][R], double (&V)[R][R], double (&sv)[R]) {
+  constexpr PplsRoundRobin<R> rr;
+  constexpr int N = PplsRoundRobin<R>::N;
+  int sweeps = 0;
+  for (int sweep = 0; sweep < 60; ++sweep) {
+    bool rotated = false;
+    ++sweeps;
+#pragma unroll
+    for (int m = 0; m < N - 1; ++m) {
+      double cs[N / 2], sn[N / 2];
+#pragma unroll
+      for (int k = 0; k < N / 2; ++k) {
+        const int i = rr.i[m][k], j = rr.j[m][k];
+        if (j >= R) continue;
+        double a = 0.0, b = 0.0, g = 0.0;
+#pragma unroll
+        for (int t = 0; t < R; ++t) {
+          a = fma(A[t][i], A[t][i], a);
+          b = fma(A[t][j], A[t][j], b);
+          g = fma(A[t][i], A[t][j], g);
+        }
+        const bool rot = (g * g >= 1e-30 * (a * b)) && g != 0.0;
+        rotated = rotated || rot;
+        // tan = sign(z) / (|z| + sqrt(1 + z^2)), z = (b - a) / 2g;  c = u w, s = sign(z) w
+        const double z = (b - a) * ppls_rcp(rot ? 2.0 * g : 1.0);
+        const double z2 = fma(z, z, 1.0);
+        const double u = fabs(z) + z2 * ppls_rsq(z2);
+        const double w = ppls_rsq(fma(u, u, 1.0));
+        cs[k] = rot ? u * w : 1.0;
+        sn[k] = rot ? (z >= 0.0 ? w : -w) : 0.0;
+      }
+#pragma unroll
+      for (int k = 0; k < N / 2; ++k) {
+        const int i = rr.i[m][k], j = rr.j[m][k];
+        if (j >= R) continue;
+        const double c = cs[k], s = sn[k];
+#pragma unroll
+        for (int t = 0; t < R; ++t) {
+          const double x = A[t][i], y = A[t][j];
+          A[t][i] = fma(c, x, -s * y);
+          A[t][j] = fma(s, x, c * y);
+          const double vx = V[t][i], vy = V[t][j];
+          V[t][i] = fma(c, vx, -s * vy);
+          V[t][j] = fma(s, vx, c * vy);
+        }
+      }
+    }
+    if (!rotated) break;
+  }
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    double nrm = 0.0;
+#pragma unroll
+    for (int k = 0; k < R; ++k) nrm = fma(A[k][i], A[k][i], nrm);
+    sv[i] = sqrt(nrm);
+  }
+  return sweeps;
+}
+
+// Modified Gram-Schmidt on the columns of V (restores orthogonality of a carried warm start).
+template <int R>
+__device__ __forceinline__ void ppls_mgs_reg(double (&V)[R][R]) {
+#pragma unroll
+  for (int j = 0; j < R; ++j) {
+#pragma unroll
+    for (int i = 0; i < j; ++i) {
+      double d = 0.0;
+#pragma unroll
+      for (int k = 0; k < R; ++k) d = fma(V[k][i], V[k][j], d);
+#pragma unroll
+      for (int k = 0; k < R; ++k) V[k][j] = fma(-d, V[k][i], V[k][j]);
+    }
+    double nrm = 0.0;
+#pragma unroll
+    for (int k = 0; k < R; ++k) nrm = fma(V[k][j], V[k][j], nrm);
+    const double inv = 1.0 / sqrt(nrm);
+#pragma unroll
+    for (int k = 0; k < R; ++k) V[k][j] *= inv;
+  }
+}
+
+// Block Gram of rows x (R values per thread) accumulated into the packed upper triangle.
+template <int R>
+__device__ __forceinline__ void ppls_gram_acc(const double (&x)[R], double (&vals)[R * (R + 1) / 2]) {
+  int e = 0;
+#pragma unroll
+  for (int b = 0; b < R; ++b)
+#pragma unroll
+    for (int a = 0; a <= b; ++a) { vals[e] = fma(x[a], x[b], vals[e]); ++e; }
+}
+
+template <int R>
+__device__ __forceinline__ void ppls_gram_unpack(const double (&vals)[R * (R + 1) / 2], double (&G)[R][R]) {
+  int e = 0;
+#pragma unroll
+  for (int b = 0; b < R; ++b)
+#pragma unroll
+    for (int a = 0; a <= b; ++a) { G[a][b] = vals[e]; G[b][a] = vals[e]; ++e; }
+}
+
+// Sum over an aligned group of 8 lanes (DPP quad xor1, quad xor2, half-row mirror); every lane of
+// the group gets the bitwise-same total.  All 64 lanes must be active.
+__device__ __forceinline__ double ppls_group8_sum(double v) {
+  v += ppls_dpp_partner<5>(v);
+  v += ppls_dpp_partner<4>(v);
+  v += ppls_dpp_partner<3>(v);
+  return v;
+}
+
+__device__ __forceinline__ void ppls_wave_lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+// Pair k of round m of the circle-method schedule (PplsRoundRobin), i < j.
+template <int R>
+__device__ __forceinline__ void ppls_rr_pair(int m, int k, int& i, int& j) {
+  constexpr int N = R + (R & 1);
+  const int pa = k == 0 ? 0 : ((k - 1 + m) % (N - 1)) + 1;
+  const int pb = ((N - 2 - k + m) % (N - 1)) + 1;
+  i = pa < pb ? pa : pb;
+  j = pa < pb ? pb : pa;
+}
+
+// One-sided Jacobi on one wave: A V = U Sigma with A, V in LDS as 8 x 8 column blocks
+// (element (row t, col c) at [c * 8 + t], rows >= R zero).  Round m of a sweep rotates the N/2
+// disjoint pairs of the circle-method schedule at once: lane group k = lane / 8 owns pair k, lane
+// t = lane % 8 owns row t, the column dots are 8-lane DPP sums.  Same rotation and stopping rule
+// as ppls_jacobi_reg / ppls_small_polar_n.  Wave-uniform; all 64 lanes of the wave must call.
+template <int R>
+__device__ int ppls_jacobi_wave(double* sA, double* sV) {
+  constexpr int N = R + (R & 1);
+  const int lane = threadIdx.x & 63, k = lane >> 3, t = lane & 7;
+  const bool grp = k < N / 2;
+  int sweeps = 0;
+  for (int sweep = 0; sweep < 60; ++sweep) {
+    ++sweeps;
+    bool rot_any = false;
+#pragma unroll
+    for (int m = 0; m < N - 1; ++m) {
+      int i, j;
+      ppls_rr_pair<R>(m, grp ? k : 0, i, j);
+      const bool act = grp && j < R;
+      const int ci = (act ? i : 0) * 8 + t, cj = (act ? j : 1) * 8 + t;
+      const double x = sA[ci], y = sA[cj], vx = sV[ci], vy = sV[cj];
+      const double a = ppls_group8_sum(x * x), b = ppls_group8_sum(y * y), g = ppls_group8_sum(x * y);
+      const bool rot = act && (g * g >= 1e-30 * (a * b)) && g != 0.0;
+      const double z = (b - a) * ppls_rcp(rot ? 2.0 * g : 1.0);
+      const double z2 = fma(z, z, 1.0);
+      const double u = fabs(z) + z2 * ppls_rsq(z2);
+      const double w = ppls_rsq(fma(u, u, 1.0));
+      const double c = u * w, sn = z >= 0.0 ? w : -w;
+      if (rot) {
+        sA[ci] = fma(c, x, -sn * y);
+        sA[cj] = fma(sn, x, c * y);
+        sV[ci] = fma(c, vx, -sn * vy);
+        sV[cj] = fma(sn, vx, c * vy);
+      }
+      rot_any = rot_any || rot;
+      ppls_wave_lds_fence();
+    }
+    if (!__any(rot_any)) break;
+  }
+  return sweeps;
+}
+
+// Polar factor U V' of the p x R matrix S (column-major, ld lds) = S V Sigma^-1 V', where V and
+// Sigma are the right singular vectors / values of S, obtained accurately by Cholesky-QR2
+// (S = Q R2 R1, orthogonality O(eps kappa(S))) followed by one-sided Jacobi on T = R2 R1 (the
+// left factor is never formed and no triangular inverse is applied to S).  Three block passes
+// over S: the first stages S into LDS (Sl, p*R doubles; nullptr = re-read from global); the last
+// writes out = S F, F = V Sigma^-1 V', and, if gram_out != nullptr, the Gram out'out the next
+// iteration's scalar update needs.  The Jacobi is warm-started from vstate (the previous
+// iteration's V; nullptr = identity) and runs lane-parallel on wave 0.  sm: >= 2 R^2 doubles of
+// LDS.  Returns false when S is numerically rank deficient (a Cholesky pivot fails or
+// sigma_min < 1e-14 sigma_max); the caller then falls back to Householder (which reports it).
+template <int R, int NT>
+__device__ bool ppls_block_polar_fast(const double* __restrict__ S, int64_t lds, int p,
+                                      double* __restrict__ out, int64_t ldo, int ldo_rows, double* Sl,
+                                      double* sh, double* sm, double* __restrict__ gram_out,
+                                      double* __restrict__ vstate, long long* tr) {
   constexpr int NG = R * (R + 1) / 2;
-  constexpr int RR = R * R;
-  const int tid = threadIdx.x, nt = blockDim.x;
-  double* R1 = sm;               // R1, later the final r x r multiplier
-  double* M = sm + RR;           // R1^-1
-  double* Gm = sm + 2 * RR;
-  double* R2 = sm + 3 * RR;
-  double* Rr = sm + 4 * RR;
-  double* R2i = sm + 5 * RR;
-  double* P = sm + 6 * RR;
-  double* T = sm + 7 * RR;
-  double* A = sm + 8 * RR;       // Jacobi workspace (2 RR)
+  constexpr int NW = NT / 64;
+  static_assert(R <= 8, "8 x 8 LDS blocks");
+  const int tid = threadIdx.x;
+  double* sR1 = sm;           // R1 (upper), later F
+  double* sM = sm + R * R;    // R1^-1
+  __shared__ double sA[64], sV[64], sT[64], ssv[8];
   __shared__ int ok;
   double vals[NG];
 #pragma unroll
   for (int e = 0; e < NG; ++e) vals[e] = 0.0;
-  for (int i = tid; i < p; i += nt) {
-    double x[R];
+  // the carried V (wave 0), fetched now so its latency hides under pass 1
+  const int lane = tid & 63, cb = lane >> 3, rt = lane & 7;
+  double vprev = (cb == rt) ? 1.0 : 0.0;
+  if (vstate && tid < 64 && cb < R && rt < R) vprev = vstate[cb * R + rt];
+  // pass 1: G1 = S'S, staging S into LDS; chunks of PU rows per thread with every load of a
+  // chunk issued before the first use
+  constexpr int PU = R >= 6 ? 4 : 8;
+  for (int i0 = 0; i0 < p; i0 += PU * NT) {
+    double x[PU][R];
 #pragma unroll
-    for (int k = 0; k < R; ++k) x[k] = S[(int64_t)k * lds + i];
-    int e = 0;
+    for (int u = 0; u < PU; ++u) {
+      const int i = i0 + u * NT + tid;
 #pragma unroll
-    for (int b = 0; b < R; ++b)
+      for (int k = 0; k < R; ++k) x[u][k] = (i < p) ? S[(int64_t)k * lds + i] : 0.0;
+    }
 #pragma unroll
-      for (int a = 0; a <= b; ++a) { vals[e] = fma(x[a], x[b], vals[e]); ++e; }
+    for (int u = 0; u < PU; ++u) {
+      const int i = i0 + u * NT + tid;
+      if (Sl && i < p) {
+#pragma unroll
+        for (int k = 0; k < R; ++k) Sl[k * p + i] = x[u][k];
+      }
+      ppls_gram_acc<R>(x[u], vals);
+    }
   }
-  ppls_block_sum_t<NG>(vals, sh);
+  ppls_block_sum_t<NG, NW>(vals, sh);
+  ppls_stamp(tr, 1);
   if (tid == 0) {
-    int e = 0;
-    for (int b = 0; b < R; ++b)
-      for (int a = 0; a <= b; ++a) { Gm[b * R + a] = vals[e]; Gm[a * R + b] = vals[e]; ++e; }
-    ok = ppls_chol_upper<R>(Gm, R1);
-    if (ok) ppls_inv_upper<R>(R1, M);
+    double G[R][R], U[R][R], Ui[R][R], dinv[R];
+    ppls_gram_unpack<R>(vals, G);
+    ok = ppls_chol_reg<R>(G, U, dinv);
+    ppls_inv_upper_reg<R>(U, dinv, Ui);
+#pragma unroll
+    for (int a = 0; a < R; ++a)
+#pragma unroll
+      for (int b = 0; b < R; ++b) { sR1[a * R + b] = U[a][b]; sM[a * R + b] = Ui[a][b]; }
   }
   __syncthreads();
+  ppls_stamp(tr, 2);
   if (!ok) return false;
+  const double* Sr = Sl ? Sl : S;
+  const int64_t ldr = Sl ? p : lds;
+  // pass 2: G2 = Q1'Q1, Q1 = S R1^-1
+  {
+    double M[R][R];
+#pragma unroll
+    for (int a = 0; a < R; ++a)
+#pragma unroll
+      for (int b = 0; b < R; ++b) M[a][b] = sM[a * R + b];
+#pragma unroll
+    for (int e = 0; e < NG; ++e) vals[e] = 0.0;
+#pragma unroll 4
+    for (int i = tid; i < p; i += NT) {
+      double x[R], qv[R];
+#pragma unroll
+      for (int k = 0; k < R; ++k) x[k] = Sr[(int64_t)k * ldr + i];
+#pragma unroll
+      for (int j = 0; j < R; ++j) {
+        double s = 0.0;
+#pragma unroll
+        for (int k = 0; k <= j; ++k) s = fma(x[k], M[k][j], s);
+        qv[j] = s;
+      }
+      ppls_gram_acc<R>(qv, vals);
+    }
+  }
+  ppls_block_sum_t<NG, NW>(vals, sh);
+  ppls_stamp(tr, 3);
+  if (tid < 64) {   // wave 0: T = R2 R1, warm start, Jacobi, F
+    // V_prev -> sV (8 x 8 block, zero padding)
+    {
+      sV[lane] = (cb < R && rt < R) ? vprev : 0.0;
+      sA[lane] = 0.0;
+      sT[lane] = 0.0;
+    }
+    ppls_wave_lds_fence();
+    if (lane == 0) {
+      double G[R][R], U2[R][R], dinv[R];
+      ppls_gram_unpack<R>(vals, G);
+      ok = ppls_chol_reg<R>(G, U2, dinv);
+#pragma unroll
+      for (int a = 0; a < R; ++a)                 // T = R2 R1 (upper)
+#pragma unroll
+        for (int b = 0; b < R; ++b) {
+          double s = 0.0;
+#pragma unroll
+          for (int k = 0; k < R; ++k) s = fma(U2[a][k], sR1[k * R + b], s);
+          sT[b * 8 + a] = s;
+        }
+    }
+    ppls_wave_lds_fence();
+    ppls_stamp(tr, 6);
+    // re-orthonormalise the carried V (modified Gram-Schmidt, rows on lanes 0..7)
+    if (vstate) {
+#pragma unroll
+      for (int j = 0; j < R; ++j) {
+        double vj = sV[j * 8 + rt];
+#pragma unroll
+        for (int i = 0; i < j; ++i) {
+          const double vi = sV[i * 8 + rt];
+          vj = fma(-ppls_group8_sum(vi * vj), vi, vj);
+        }
+        vj *= ppls_rsq(ppls_group8_sum(vj * vj));
+        if (lane < 8) sV[j * 8 + rt] = vj;
+        ppls_wave_lds_fence();
+      }
+    }
+    // A = T V (lane (row rt, col cb))
+    if (cb < R && rt < R) {
+      double s = 0.0;
+#pragma unroll
+      for (int k = 0; k < R; ++k) s = fma(sT[k * 8 + rt], sV[cb * 8 + k], s);
+      sA[cb * 8 + rt] = s;
+    }
+    ppls_wave_lds_fence();
+    ppls_stamp(tr, 7);
+    const int sweeps = ppls_jacobi_wave<R>(sA, sV);
+    ppls_stamp(tr, 8);
+    if (tr && lane == 0) tr[10] = sweeps;
+    if (lane < R) {
+      double nrm = 0.0;
+#pragma unroll
+      for (int t = 0; t < R; ++t) nrm = fma(sA[lane * 8 + t], sA[lane * 8 + t], nrm);
+      ssv[lane] = sqrt(nrm);
+    }
+    ppls_wave_lds_fence();
+    double smax = 0.0;
+    bool good = true;
+#pragma unroll
+    for (int i = 0; i < R; ++i) smax = fmax(smax, ssv[i]);
+#pragma unroll
+    for (int i = 0; i < R; ++i) good = good && (ssv[i] > smax * 1e-14);
+    if (lane < R * R) {   // F = V Sigma^-1 V', lane (a, b)
+      const int a = lane % R, b = lane / R;
+      double s = 0.0;
+#pragma unroll
+      for (int k = 0; k < R; ++k) s = fma(sV[k * 8 + a] * (1.0 / ssv[k]), sV[k * 8 + b], s);
+      sR1[b * R + a] = s;
+      if (vstate) vstate[b * R + a] = sV[b * 8 + a];
+    }
+    if (lane == 0) ok = ok && good;
+  }
+  __syncthreads();
+  ppls_stamp(tr, 4);
+  if (!ok) return false;
+  // pass 3: out = S F (+ Gram of out)
+  double F[R][R];
+#pragma unroll
+  for (int a = 0; a < R; ++a)
+#pragma unroll
+    for (int b = 0; b < R; ++b) F[a][b] = sR1[b * R + a];
 #pragma unroll
   for (int e = 0; e < NG; ++e) vals[e] = 0.0;
-  for (int i = tid; i < p; i += nt) {
-    double x[R], qv[R];
+#pragma unroll 4
+  for (int i = tid; i < ldo_rows; i += NT) {
+    double x[R], o[R];
 #pragma unroll
-    for (int k = 0; k < R; ++k) x[k] = S[(int64_t)k * lds + i];
-#pragma unroll
-    for (int j = 0; j < R; ++j) {
-      double s = 0.0;
-#pragma unroll
-      for (int k = 0; k <= j; ++k) s = fma(x[k], M[j * R + k], s);
-      qv[j] = s;
-    }
-    int e = 0;
-#pragma unroll
-    for (int b = 0; b < R; ++b)
-#pragma unroll
-      for (int a = 0; a <= b; ++a) { vals[e] = fma(qv[a], qv[b], vals[e]); ++e; }
-  }
-  ppls_block_sum_t<NG>(vals, sh);
-  if (tid == 0) {
-    int e = 0;
-    for (int b = 0; b < R; ++b)
-      for (int a = 0; a <= b; ++a) { Gm[b * R + a] = vals[e]; Gm[a * R + b] = vals[e]; ++e; }
-    ok = ppls_chol_upper<R>(Gm, R2);
-    if (ok) {
-      for (int j = 0; j < R; ++j)            // R = R2 R1
-        for (int i = 0; i < R; ++i) {
-          double s = 0.0;
-          for (int k = 0; k < R; ++k) s += R2[k * R + i] * R1[j * R + k];
-          Rr[j * R + i] = s;
-        }
-      ok = ppls_small_polar_ws<R>(Rr, R, P, A, A + RR) == 0;
-      ppls_inv_upper<R>(R2, R2i);
-      for (int j = 0; j < R; ++j)            // T = R2^-1 P
-        for (int i = 0; i < R; ++i) {
-          double s = 0.0;
-          for (int k = 0; k < R; ++k) s += R2i[k * R + i] * P[j * R + k];
-          T[j * R + i] = s;
-        }
-      for (int j = 0; j < R; ++j)            // R1 <- R1^-1 R2^-1 P
-        for (int i = 0; i < R; ++i) {
-          double s = 0.0;
-          for (int k = 0; k < R; ++k) s += M[k * R + i] * T[j * R + k];
-          R1[j * R + i] = s;
-        }
-    }
-  }
-  __syncthreads();
-  if (!ok) return false;
-  for (int i = tid; i < ldo_rows; i += nt) {
-    double x[R];
-#pragma unroll
-    for (int k = 0; k < R; ++k) x[k] = (i < p) ? S[(int64_t)k * lds + i] : 0.0;
+    for (int k = 0; k < R; ++k) x[k] = (i < p) ? Sr[(int64_t)k * ldr + i] : 0.0;
 #pragma unroll
     for (int j = 0; j < R; ++j) {
       double s = 0.0;
 #pragma unroll
-      for (int k = 0; k < R; ++k) s = fma(x[k], R1[j * R + k], s);
+      for (int k = 0; k < R; ++k) s = fma(x[k], F[k][j], s);
+      o[j] = s;
       out[(int64_t)j * ldo + i] = s;
+    }
+    ppls_gram_acc<R>(o, vals);
+  }
+  if (gram_out) {
+    ppls_block_sum_t<NG, NW>(vals, sh);
+    if (tid == 0) {
+      double G[R][R];
+      ppls_gram_unpack<R>(vals, G);
+#pragma unroll
+      for (int a = 0; a < R; ++a)
+#pragma unroll
+        for (int b = 0; b < R; ++b) gram_out[b * R + a] = G[a][b];
     }
   }
   return true;
 }
 
-// Block 0: W_next = orth(S_X); block 1: C_next = orth(S_Y); block 2: scalars (moments, loglik,
-// M-step).  stats = [SX ldx*R][SY ldy*R][G 4R^2];  ssq = {||X||^2, ||Y||^2}.  Every sequential
-// working set lives in LDS (no private-memory scratch).
+// Gram out'out of a p x R column-major matrix written earlier by this block (fallback path).
+template <int R, int NT>
+__device__ void ppls_block_gram_of(const double* __restrict__ M, int64_t ld, int p, double* sh,
+                                   double* __restrict__ gram_out) {
+  constexpr int NG = R * (R + 1) / 2;
+  double vals[NG];
+#pragma unroll
+  for (int e = 0; e < NG; ++e) vals[e] = 0.0;
+  for (int i = threadIdx.x; i < p; i += NT) {
+    double x[R];
+#pragma unroll
+    for (int k = 0; k < R; ++k) x[k] = M[(int64_t)k * ld + i];
+    ppls_gram_acc<R>(x, vals);
+  }
+  ppls_block_sum_t<NG>(vals, sh);
+  if (threadIdx.x == 0) {
+    double G[R][R];
+    ppls_gram_unpack<R>(vals, G);
+#pragma unroll
+    for (int a = 0; a < R; ++a)
+#pragma unroll
+      for (int b = 0; b < R; ++b) gram_out[b * R + a] = G[a][b];
+  }
+}
+
+// Sum over the 64 lanes of a wave; every lane gets the bitwise-same total.
+__device__ __forceinline__ double ppls_wave_allsum(double v) {
+  double a[2] = {v, 0.0};
+  int idx = 0;
+  bool canon = true;
+  ppls_rs<1, 0, 2>(a, threadIdx.x & 63, idx, canon);
+  return a[0];
+}
+
+// The finalize's scalar part on one wave: lane k < R evaluates component k (coefficients, diagonal
+// moments, log-likelihood terms, M-step, next mu coefficients), lane k + R l < R^2 the pair
+// (k, l) terms; the O(1) combinations use wave sums.  Same formulas as the serial host form
+// (ppls_estep_moments, ppls_loglik_from_gram, ppls_mstep_scalars in ppls_math.h); only the
+// summation order differs.  sG, sWtW, sCtC, sc, m, nx live in LDS; nx must hold a copy of *sc.
 template <int R>
-__global__ __launch_bounds__(256) void ppls_finalize_kernel(
+__device__ void ppls_scalars_wave(const double* sG, const double* sWtW, const double* sCtC, double ssqX,
+                                  double ssqY, double N, int p, int q, const PplsScalars* sc,
+                                  PplsMoments* m, PplsScalars* nx, double* loglik_out) {
+  const int lane = threadIdx.x & 63;
+  const bool kact = lane < R;
+  const int k = kact ? lane : 0;
+  double c1, c2, c3;
+  ppls_coef_estep(sc->t[k], sc->b[k], sc->sigE, sc->sigF, sc->sigH, &c1, &c2, &c3, nullptr);
+  double Ctt, Cuu, Cut, xk, yk;
+  ppls_moment_diag(sG, R, k, sc, c1, c2, c3, N, &Ctt, &Cuu, &Cut, &xk, &yk);
+  const bool pact = lane < R * R;
+  const int pk = pact ? lane % R : 0, pl = pact ? lane / R : 0;
+  const double c1k = __shfl(c1, pk, 64), c2k = __shfl(c2, pk, 64), c3k = __shfl(c3, pk, 64);
+  const double c1l = __shfl(c1, pl, 64), c2l = __shfl(c2, pl, 64), c3l = __shfl(c3, pl, 64);
+  double z, w, chh;
+  ppls_moment_pair(sG, R, pk, pl, c1k, c2k, c3k, c1l, c2l, c3l, sWtW[pl * R + pk], sCtC[pl * R + pk], sc,
+                   N, &z, &w, &chh);
+  const double xz = ppls_wave_allsum(kact ? xk : 0.0), yz = ppls_wave_allsum(kact ? yk : 0.0);
+  const double sc1 = ppls_wave_allsum(kact ? c1 : 0.0), sc3 = ppls_wave_allsum(kact ? c3 : 0.0);
+  const double zz = ppls_wave_allsum(pact ? z : 0.0), ww = ppls_wave_allsum(pact ? w : 0.0);
+  const double trChh = ppls_wave_allsum(pact && pk == pl ? chh : 0.0);
+  double Cee, Cff;
+  ppls_moment_noise(ssqX, ssqY, N, p, q, sc, xz, yz, zz, ww, sc1, sc3, &Cee, &Cff);
+  if (loglik_out) {
+    double lg, tk;
+    ppls_logl_k(sG, R, k, sc, &lg, &tk);
+    const double LG = ppls_wave_allsum(kact ? lg : 0.0), TK = ppls_wave_allsum(kact ? tk : 0.0);
+    if (lane == 0) *loglik_out = ppls_logl_total(LG, TK, ssqX, ssqY, N, p, q, R, sc);
+  }
+  if (kact) { m->Ctt[k] = Ctt; m->Cuu[k] = Cuu; m->Cut[k] = Cut; }
+  if (pact) m->Chh[pl * R + pk] = chh;
+  // Maximiz_M scalars (EM_W_multi.R:734-738) and the next mu coefficients (:691-694)
+  const double sE = sqrt(Cee / 1.0), sF = sqrt(Cff / 1.0), sH = sqrt(trChh / (double)R);
+  const double bn = Cut * (1.0 / Ctt), tn = sqrt(Ctt);
+  double al, be, ga, de;
+  ppls_mu_coef_k(tn, bn, sE, sF, sH, &al, &be, &ga, &de);
+  if (kact) {
+    nx->b[k] = bn; nx->t[k] = tn;
+    nx->alpha[k] = al; nx->beta[k] = be; nx->gamma[k] = ga; nx->delta[k] = de;
+  }
+  if (lane == 0) {
+    m->Cee = Cee; m->Cff = Cff;
+    nx->sigE = sE; nx->sigF = sF; nx->sigH = sH;
+  }
+}
+
+#define PPLS_FIN_THREADS 256   // 1 wave per SIMD: the r x r code may use all 512 VGPR+AGPRs
+
+// Block 0: W_next = orth(S_X); block 1: C_next = orth(S_Y); block 2: scalars (moments, loglik,
+// M-step).  stats = [SX ldx*R][SY ldy*R][G 4R^2];  ssq = {||X||^2, ||Y||^2}.
+// gram_cur = [W'W | C'C] of the parameters the sweep used (written by the previous finalize or
+// by the host upload); the polar blocks write gram_nxt for the parameters they produce, so the
+// scalar block needs no pass over W and C.  Dynamic LDS (if any) stages S for the polar blocks.
+template <int R>
+__global__ __launch_bounds__(PPLS_FIN_THREADS) void ppls_finalize_kernel(
     const double* __restrict__ stats, const double* __restrict__ ssq, double N, int p, int q, int ldx,
     int ldy, const double* __restrict__ Wc, const double* __restrict__ Cc,
     const PplsScalars* __restrict__ sc_cur, double* __restrict__ Wn, double* __restrict__ Cn,
     PplsScalars* __restrict__ sc_nxt, PplsMoments* __restrict__ mom, double* __restrict__ loglik,
-    int logl_index, double* __restrict__ work, int* __restrict__ status, int qr, int mode) {
+    int logl_index, double* __restrict__ work, int* __restrict__ status, int qr, int mode,
+    const double* __restrict__ gram_cur, double* __restrict__ gram_nxt, double* __restrict__ vstate,
+    int stage_lds, long long* __restrict__ trace) {
+  constexpr int NT = PPLS_FIN_THREADS;
   constexpr int NG = R * (R + 1) / 2;
-  __shared__ double sh[4 * 2 * NG];
-  __shared__ double sm[10 * R * R];
+  extern __shared__ double dyn_lds[];
+  __shared__ double sh[(NT / 64) * 2 * NG];
+  __shared__ double sm[2 * R * R];
   __shared__ PplsScalars s_cur, s_nx;
   __shared__ PplsMoments s_m;
   __shared__ double s_G[4 * R * R], s_WtW[R * R], s_CtC[R * R];
@@ -1131,69 +1556,92 @@ __global__ __launch_bounds__(256) void ppls_finalize_kernel(
   const double* SY = stats + (int64_t)R * ldx;
   const double* G = SY + (int64_t)R * ldy;
   const int tid = threadIdx.x;
+  long long* tr = trace ? trace + 16 * blockIdx.x : nullptr;
+  ppls_stamp(tr, 0);
+  if (tr && tid == 0) tr[11] = (long long)clock64();
   if (blockIdx.x < 2) {
     if (!(mode & 1)) return;
     const bool isx = blockIdx.x == 0;
     const double* S = isx ? SX : SY;
     const int ld = isx ? ldx : ldy, rows = isx ? p : q;
     double* out = isx ? Wn : Cn;
+    double* gout = gram_nxt ? gram_nxt + (isx ? 0 : R * R) : nullptr;
     double* w2 = work + (isx ? 0 : 2 * (int64_t)p * R);
-    if (qr || !ppls_block_polar_cholqr2<R>(S, ld, rows, out, ld, ld, sh, sm))
+    double* vs = vstate ? vstate + (isx ? 0 : R * R) : nullptr;
+    if (qr || !ppls_block_polar_fast<R, NT>(S, ld, rows, out, ld, ld, stage_lds ? dyn_lds : nullptr, sh,
+                                            sm, gout, vs, tr)) {
       ppls_block_polar(S, ld, rows, R, out, ld, ld, w2, w2 + (int64_t)rows * R, status, qr);
+      if (gout) {
+        __syncthreads();
+        ppls_block_gram_of<R, NT>(out, ld, rows, sh, gout);
+      }
+    }
+    ppls_stamp(tr, 5);
+    if (tr && tid == 0) tr[12] = (long long)clock64();
     return;
   }
   if (!(mode & 2)) return;
-  // stage theta's scalars and the Gram in LDS (all threads)
+  // stage theta's scalars, the Gram and W'W, C'C in LDS (all threads)
   {
     const double* src = (const double*)sc_cur;
     double* dst = (double*)&s_cur;
-    for (int i = tid; i < (int)(sizeof(PplsScalars) / 8); i += blockDim.x) dst[i] = src[i];
-    for (int i = tid; i < 4 * R * R; i += blockDim.x) s_G[i] = G[i];
+    for (int i = tid; i < (int)(sizeof(PplsScalars) / 8); i += NT) dst[i] = src[i];
+    for (int i = tid; i < 4 * R * R; i += NT) s_G[i] = G[i];
+    if (gram_cur)
+      for (int i = tid; i < R * R; i += NT) { s_WtW[i] = gram_cur[i]; s_CtC[i] = gram_cur[R * R + i]; }
   }
-  // W'W and C'C of the parameters the sweep used (one batched reduction)
-  double vals[2 * NG];
+  if (!gram_cur) {   // W'W and C'C by a pass over W, C (one batched reduction)
+    double vals[2 * NG];
 #pragma unroll
-  for (int e = 0; e < 2 * NG; ++e) vals[e] = 0.0;
-  for (int i = tid; i < (p > q ? p : q); i += blockDim.x) {
-    double wv[R], cv[R];
+    for (int e = 0; e < 2 * NG; ++e) vals[e] = 0.0;
+    for (int i = tid; i < (p > q ? p : q); i += NT) {
+      double wv[R], cv[R];
 #pragma unroll
-    for (int k = 0; k < R; ++k) {
-      wv[k] = (i < p) ? Wc[(int64_t)k * ldx + i] : 0.0;
-      cv[k] = (i < q) ? Cc[(int64_t)k * ldy + i] : 0.0;
+      for (int k = 0; k < R; ++k) {
+        wv[k] = (i < p) ? Wc[(int64_t)k * ldx + i] : 0.0;
+        cv[k] = (i < q) ? Cc[(int64_t)k * ldy + i] : 0.0;
+      }
+      int e = 0;
+#pragma unroll
+      for (int b = 0; b < R; ++b)
+#pragma unroll
+        for (int a = 0; a <= b; ++a) {
+          vals[e] = fma(wv[a], wv[b], vals[e]);
+          vals[NG + e] = fma(cv[a], cv[b], vals[NG + e]);
+          ++e;
+        }
     }
-    int e = 0;
-#pragma unroll
-    for (int b = 0; b < R; ++b)
-#pragma unroll
-      for (int a = 0; a <= b; ++a) {
-        vals[e] = fma(wv[a], wv[b], vals[e]);
-        vals[NG + e] = fma(cv[a], cv[b], vals[NG + e]);
-        ++e;
-      }
-  }
-  ppls_block_sum_t<2 * NG>(vals, sh);
-  if (tid == 0) {
-    int e = 0;
-    for (int b = 0; b < R; ++b)
-      for (int a = 0; a <= b; ++a) {
-        s_WtW[b * R + a] = s_WtW[a * R + b] = vals[e];
-        s_CtC[b * R + a] = s_CtC[a * R + b] = vals[NG + e];
-        ++e;
-      }
-    const double s0 = ssq[0], s1 = ssq[1];
-    if (logl_index >= 0) loglik[logl_index] = ppls_loglik_from_gram(s_G, s0, s1, N, p, q, R, &s_cur);
-    ppls_estep_moments(s_G, s_WtW, s_CtC, s0, s1, N, p, q, R, &s_cur, &s_m);
-    s_nx = s_cur;
-    ppls_mstep_scalars(&s_m, R, &s_nx);
+    ppls_block_sum_t<2 * NG>(vals, sh);
+    if (tid == 0) {
+      int e = 0;
+      for (int b = 0; b < R; ++b)
+        for (int a = 0; a <= b; ++a) {
+          s_WtW[b * R + a] = s_WtW[a * R + b] = vals[e];
+          s_CtC[b * R + a] = s_CtC[a * R + b] = vals[NG + e];
+          ++e;
+        }
+    }
   }
   __syncthreads();
   {
+    const double* a = (const double*)&s_cur;
+    double* b = (double*)&s_nx;
+    for (int i = tid; i < (int)(sizeof(PplsScalars) / 8); i += NT) b[i] = a[i];
+  }
+  __syncthreads();
+  ppls_stamp(tr, 1);
+  if (tid < 64)
+    ppls_scalars_wave<R>(s_G, s_WtW, s_CtC, ssq[0], ssq[1], N, p, q, &s_cur, &s_m, &s_nx,
+                         logl_index >= 0 ? loglik + logl_index : nullptr);
+  __syncthreads();
+  ppls_stamp(tr, 2);
+  {
     const double* a = (const double*)&s_m;
     double* b = (double*)mom;
-    for (int i = tid; i < (int)(sizeof(PplsMoments) / 8); i += blockDim.x) b[i] = a[i];
+    for (int i = tid; i < (int)(sizeof(PplsMoments) / 8); i += NT) b[i] = a[i];
     const double* c = (const double*)&s_nx;
     double* d = (double*)sc_nxt;
-    for (int i = tid; i < (int)(sizeof(PplsScalars) / 8); i += blockDim.x) d[i] = c[i];
+    for (int i = tid; i < (int)(sizeof(PplsScalars) / 8); i += NT) d[i] = c[i];
   }
 }
 
@@ -1266,11 +1714,24 @@ __global__ void ppls_loglc_kernel(const double* __restrict__ G, const double* __
 
 // ============================================================================ launchers
 namespace {
+#define PPLS_FIN_STAGE_MAX (136 * 1024)   // dynamic LDS for staging S (static use is < 8 KB)
+
 template <int R>
 hipError_t launch_finalize_t(const PplsFinalizeArgs* f, hipStream_t st) {
-  hipLaunchKernelGGL(ppls_finalize_kernel<R>, dim3(3), dim3(256), 0, st, f->stats, f->ssq, f->N, f->p,
-                     f->q, f->ldx, f->ldy, f->Wc, f->Cc, f->sc_cur, f->Wn, f->Cn, f->sc_nxt, f->mom,
-                     f->loglik, f->logl_index, f->work, f->status, f->qr, f->mode);
+  auto kern = ppls_finalize_kernel<R>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       PPLS_FIN_STAGE_MAX);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  const size_t stage = (size_t)R * (f->p > f->q ? f->p : f->q) * sizeof(double);
+  const int use = stage <= PPLS_FIN_STAGE_MAX && !f->qr;
+  hipLaunchKernelGGL(kern, dim3(3), dim3(PPLS_FIN_THREADS), use ? stage : 0, st, f->stats, f->ssq, f->N,
+                     f->p, f->q, f->ldx, f->ldy, f->Wc, f->Cc, f->sc_cur, f->Wn, f->Cn, f->sc_nxt, f->mom,
+                     f->loglik, f->logl_index, f->work, f->status, f->qr, f->mode, f->gram_cur,
+                     f->gram_nxt, f->vstate, use, f->trace);
   return hipGetLastError();
 }
 

@@ -17,7 +17,7 @@
 #include <stdint.h>
 
 #if defined(__HIPCC__)
-#define PPLS_HD __host__ __device__ inline
+#define PPLS_HD __host__ __device__ inline __attribute__((always_inline))
 #else
 #define PPLS_HD inline
 #endif
@@ -77,18 +77,23 @@ PPLS_HD void ppls_coef_logl(double t, double b, double sigX, double sigY, double
 }
 
 // alpha..delta of the per-row posterior means, EM_W_multi.R:691-694 collected per column.
+PPLS_HD void ppls_mu_coef_k(double t, double b, double sigE, double sigF, double sigH, double* al,
+                            double* be, double* ga, double* de) {
+  double c1, c2, c3;
+  ppls_coef_estep(t, b, sigE, sigF, sigH, &c1, &c2, &c3, nullptr);
+  const double t2 = t * t;
+  const double v = t2 * b * b + sigH * sigH;   // varU, :688
+  const double iE = 1.0 / (sigE * sigE), iF = 1.0 / (sigF * sigF);
+  *al = iE * t2 - c1 * t2 - c2 * t2 * b;
+  *be = iF * t2 * b - c2 * t2 - c3 * b * t2;
+  *ga = iE * t2 * b - c1 * t2 * b - c2 * v;
+  *de = iF * v - c2 * t2 * b - c3 * v;
+}
+
 PPLS_HD void ppls_mu_coef(PplsScalars* s, int r) {
-  for (int k = 0; k < r; ++k) {
-    double c1, c2, c3;
-    ppls_coef_estep(s->t[k], s->b[k], s->sigE, s->sigF, s->sigH, &c1, &c2, &c3, nullptr);
-    const double t2 = s->t[k] * s->t[k], b = s->b[k];
-    const double v = t2 * b * b + s->sigH * s->sigH;   // varU, :688
-    const double iE = 1.0 / (s->sigE * s->sigE), iF = 1.0 / (s->sigF * s->sigF);
-    s->alpha[k] = iE * t2 - c1 * t2 - c2 * t2 * b;
-    s->beta[k] = iF * t2 * b - c2 * t2 - c3 * b * t2;
-    s->gamma[k] = iE * t2 * b - c1 * t2 * b - c2 * v;
-    s->delta[k] = iF * v - c2 * t2 * b - c3 * v;
-  }
+  for (int k = 0; k < r; ++k)
+    ppls_mu_coef_k(s->t[k], s->b[k], s->sigE, s->sigF, s->sigH, &s->alpha[k], &s->beta[k],
+                   &s->gamma[k], &s->delta[k]);
 }
 
 // Gram accessors: G is 2r x 2r column-major; A = Xw'Xw, D = Xw'Yc, Bm = Yc'Yc.
@@ -99,86 +104,124 @@ PPLS_HD void ppls_mu_coef(PplsScalars* s, int r) {
 // Expect_M second moments (EM_W_multi.R:696-716) from the sufficient statistics of a sweep that
 // used theta = (W, C, s).  ssq(mu_E) and ssq(mu_F) are expanded exactly:
 //   ||X - sE^2 Z W'||^2 = ||X||^2 - 2 sE^2 tr(Z'Xw) + sE^4 tr(Z'Z W'W),  Z = Xw c1 + Yc c2.
+// The pieces below are shared by the serial form (ppls_estep_moments, host and tests) and the
+// lane-parallel device form (one lane per component / per component pair).
+
+// Component k: diagonal Ctt, Cuu, Cut (:696-701, abs() of :715) and its terms of tr(Z'Xw), tr(Z_F'Yc).
+PPLS_HD void ppls_moment_diag(const double* G, int r, int k, const PplsScalars* s, double c1, double c2,
+                              double c3, double N, double* Ctt_o, double* Cuu_o, double* Cut_o,
+                              double* xz_o, double* yz_o) {
+  const double sE2 = s->sigE * s->sigE, sF2 = s->sigF * s->sigF, sH2 = s->sigH * s->sigH;
+  const double iE = 1.0 / sE2, iF = 1.0 / sF2;
+  const double t2 = s->t[k] * s->t[k], t4 = t2 * t2, b = s->b[k], b2 = b * b;
+  const double v = t2 * b2 + sH2;
+  const double A = PPLS_GA(G, r, k, k), D = PPLS_GD(G, r, k, k), Bm = PPLS_GB(G, r, k, k);
+  const double al = s->alpha[k], be = s->beta[k], ga = s->gamma[k], de = s->delta[k];
+  const double tt = al * al * A + 2.0 * al * be * D + be * be * Bm;   // crossprod(mu_T)_kk
+  const double uu = ga * ga * A + 2.0 * ga * de * D + de * de * Bm;   // crossprod(mu_U)_kk
+  const double ut = ga * al * A + (ga * be + de * al) * D + de * be * Bm;
+  const double Ctt = t2 - iE * t4 - iF * (t4 * b2) + t4 * c1 + 2.0 * (t4 * b * c2) +
+                     t4 * b2 * c3 + tt / N;                                       // :696-697
+  const double Cuu = v - iE * (t4 * b2) - iF * (v * v) + t4 * b2 * c1 +
+                     2.0 * (t2 * b * v * c2) + v * v * c3 + uu / N;            // :698-699
+  const double Cut = t2 * b - iE * (t4 * b) - iF * (t2 * b * v) + t4 * b * c1 +
+                     t2 * v * c2 + t4 * b2 * c2 + t2 * b * v * c3 + ut / N;  // :700-701
+  *Ctt_o = fabs(Ctt);   // abs(Ctt)*I, :715
+  *Cuu_o = fabs(Cuu);
+  *Cut_o = Cut;
+  *xz_o = c1 * A + c2 * D;
+  *yz_o = c3 * Bm + c2 * D;
+}
+
+// Component pair (k, l): (Z'Z)_kl W'W_lk, (Z_F'Z_F)_kl C'C_lk (:703-709) and Chh_kl (:711-712, abs).
+PPLS_HD void ppls_moment_pair(const double* G, int r, int k, int l, double c1k, double c2k, double c3k,
+                              double c1l, double c2l, double c3l, double WtW_lk, double CtC_lk,
+                              const PplsScalars* s, double N, double* zz_o, double* ww_o, double* Chh_o) {
+  const double sF2 = s->sigF * s->sigF, sH2 = s->sigH * s->sigH, iF = 1.0 / sF2;
+  // (Z'Z)_kl with Z_k = c1_k a_k + c2_k b_k ; D(k,l) = sum a_k b_l
+  const double zkl = c1k * c1l * PPLS_GA(G, r, k, l) + c1k * c2l * PPLS_GD(G, r, k, l) +
+                     c2k * c1l * PPLS_GD(G, r, l, k) + c2k * c2l * PPLS_GB(G, r, k, l);
+  // (Z'_F Z_F)_kl with Z_F,k = c3_k b_k + c2_k a_k
+  const double fkl = c3k * c3l * PPLS_GB(G, r, k, l) + c3k * c2l * PPLS_GD(G, r, l, k) +
+                     c2k * c3l * PPLS_GD(G, r, k, l) + c2k * c2l * PPLS_GA(G, r, k, l);
+  *zz_o = zkl * WtW_lk;
+  *ww_o = fkl * CtC_lk;
+  // mu_H,k = h1_k Yc_k + h2_k Xw_k
+  const double h1k = iF * sH2 - sH2 * c3k, h2k = -sH2 * c2k;
+  const double h1l = iF * sH2 - sH2 * c3l, h2l = -sH2 * c2l;
+  const double hh = h1k * h1l * PPLS_GB(G, r, k, l) + h1k * h2l * PPLS_GD(G, r, l, k) +
+                    h2k * h1l * PPLS_GD(G, r, k, l) + h2k * h2l * PPLS_GA(G, r, k, l);
+  double v = hh / N;
+  if (k == l) v = (sH2 - sH2 * sH2 / sF2) + sH2 * sH2 * c3k + v;
+  *Chh_o = fabs(v);   // abs(Chh), :716
+}
+
+// Cee, Cff (:706, :709) from the reduced traces.
+PPLS_HD void ppls_moment_noise(double ssqX, double ssqY, double N, int64_t p, int64_t q, const PplsScalars* s,
+                               double xz, double yz, double zz, double ww, double sc1, double sc3,
+                               double* Cee, double* Cff) {
+  const double sE2 = s->sigE * s->sigE, sF2 = s->sigF * s->sigF;
+  const double ssqE = ssqX - 2.0 * sE2 * xz + sE2 * sE2 * zz;
+  const double ssqF = ssqY - 2.0 * sF2 * yz + sF2 * sF2 * ww;
+  const double pd = (double)p, qd = (double)q;
+  *Cee = (pd * sE2 - pd * sE2 + sE2 * sE2 * sc1 + ssqE / N) / pd;   // :706
+  *Cff = (qd * sF2 - qd * sF2 + sF2 * sF2 * sc3 + ssqF / N) / qd;   // :709
+}
+
 PPLS_HD void ppls_estep_moments(const double* G, const double* WtW, const double* CtC,
                                 double ssqX, double ssqY, double N, int64_t p, int64_t q, int r,
                                 const PplsScalars* s, PplsMoments* m) {
   double c1[PPLS_RMAX], c2[PPLS_RMAX], c3[PPLS_RMAX];
   for (int k = 0; k < r; ++k)
     ppls_coef_estep(s->t[k], s->b[k], s->sigE, s->sigF, s->sigH, &c1[k], &c2[k], &c3[k], nullptr);
-  const double sE2 = s->sigE * s->sigE, sF2 = s->sigF * s->sigF, sH2 = s->sigH * s->sigH;
-  const double iE = 1.0 / sE2, iF = 1.0 / sF2;
-  for (int k = 0; k < r; ++k) {
-    const double t2 = s->t[k] * s->t[k], t4 = t2 * t2, b = s->b[k], b2 = b * b;
-    const double v = t2 * b2 + sH2;
-    const double A = PPLS_GA(G, r, k, k), D = PPLS_GD(G, r, k, k), Bm = PPLS_GB(G, r, k, k);
-    const double al = s->alpha[k], be = s->beta[k], ga = s->gamma[k], de = s->delta[k];
-    const double tt = al * al * A + 2.0 * al * be * D + be * be * Bm;   // crossprod(mu_T)_kk
-    const double uu = ga * ga * A + 2.0 * ga * de * D + de * de * Bm;   // crossprod(mu_U)_kk
-    const double ut = ga * al * A + (ga * be + de * al) * D + de * be * Bm;
-    const double Ctt = t2 - iE * t4 - iF * (t4 * b2) + t4 * c1[k] + 2.0 * (t4 * b * c2[k]) +
-                       t4 * b2 * c3[k] + tt / N;                                       // :696-697
-    const double Cuu = v - iE * (t4 * b2) - iF * (v * v) + t4 * b2 * c1[k] +
-                       2.0 * (t2 * b * v * c2[k]) + v * v * c3[k] + uu / N;            // :698-699
-    const double Cut = t2 * b - iE * (t4 * b) - iF * (t2 * b * v) + t4 * b * c1[k] +
-                       t2 * v * c2[k] + t4 * b2 * c2[k] + t2 * b * v * c3[k] + ut / N;  // :700-701
-    m->Ctt[k] = fabs(Ctt);   // abs(Ctt)*I, :715
-    m->Cuu[k] = fabs(Cuu);
-    m->Cut[k] = Cut;
-  }
-  // ssq(mu_E), ssq(mu_F) (:703-709)
   double xz = 0.0, zz = 0.0, yz = 0.0, ww = 0.0, sc1 = 0.0, sc3 = 0.0;
   for (int k = 0; k < r; ++k) {
-    xz += c1[k] * PPLS_GA(G, r, k, k) + c2[k] * PPLS_GD(G, r, k, k);
-    yz += c3[k] * PPLS_GB(G, r, k, k) + c2[k] * PPLS_GD(G, r, k, k);
+    double xk, yk;
+    ppls_moment_diag(G, r, k, s, c1[k], c2[k], c3[k], N, &m->Ctt[k], &m->Cuu[k], &m->Cut[k], &xk, &yk);
+    xz += xk;
+    yz += yk;
     sc1 += c1[k];
     sc3 += c3[k];
   }
   for (int l = 0; l < r; ++l)
     for (int k = 0; k < r; ++k) {
-      // (Z'Z)_kl with Z_k = c1_k a_k + c2_k b_k ; D(k,l) = sum a_k b_l
-      const double zkl = c1[k] * c1[l] * PPLS_GA(G, r, k, l) + c1[k] * c2[l] * PPLS_GD(G, r, k, l) +
-                         c2[k] * c1[l] * PPLS_GD(G, r, l, k) + c2[k] * c2[l] * PPLS_GB(G, r, k, l);
-      // (Z'_F Z_F)_kl with Z_F,k = c3_k b_k + c2_k a_k
-      const double fkl = c3[k] * c3[l] * PPLS_GB(G, r, k, l) + c3[k] * c2[l] * PPLS_GD(G, r, l, k) +
-                         c2[k] * c3[l] * PPLS_GD(G, r, k, l) + c2[k] * c2[l] * PPLS_GA(G, r, k, l);
-      zz += zkl * WtW[l * r + k];
-      ww += fkl * CtC[l * r + k];
+      double z, w;
+      ppls_moment_pair(G, r, k, l, c1[k], c2[k], c3[k], c1[l], c2[l], c3[l], WtW[l * r + k],
+                       CtC[l * r + k], s, N, &z, &w, &m->Chh[l * r + k]);
+      zz += z;
+      ww += w;
     }
-  const double ssqE = ssqX - 2.0 * sE2 * xz + sE2 * sE2 * zz;
-  const double ssqF = ssqY - 2.0 * sF2 * yz + sF2 * sF2 * ww;
-  const double pd = (double)p, qd = (double)q;
-  m->Cee = (pd * sE2 - pd * sE2 + sE2 * sE2 * sc1 + ssqE / N) / pd;   // :706
-  m->Cff = (qd * sF2 - qd * sF2 + sF2 * sF2 * sc3 + ssqF / N) / qd;   // :709
-  // Chh (:711-712): mu_H,k = h1_k Yc_k + h2_k Xw_k
-  for (int l = 0; l < r; ++l)
-    for (int k = 0; k < r; ++k) {
-      const double h1k = iF * sH2 - sH2 * c3[k], h2k = -sH2 * c2[k];
-      const double h1l = iF * sH2 - sH2 * c3[l], h2l = -sH2 * c2[l];
-      const double hh = h1k * h1l * PPLS_GB(G, r, k, l) + h1k * h2l * PPLS_GD(G, r, l, k) +
-                        h2k * h1l * PPLS_GD(G, r, k, l) + h2k * h2l * PPLS_GA(G, r, k, l);
-      double v = hh / N;
-      if (k == l) v = (sH2 - sH2 * sH2 / sF2) + sH2 * sH2 * c3[k] + v;
-      m->Chh[l * r + k] = fabs(v);   // abs(Chh), :716
-    }
+  ppls_moment_noise(ssqX, ssqY, N, p, q, s, xz, yz, zz, ww, sc1, sc3, &m->Cee, &m->Cff);
 }
 
 // loglC_fast (loglC.cpp:318-338) for theta = (W, C, s) from the Gram of the sweep that used W, C.
+// Component k's log-determinant terms (:331) and trace term (:335).
+PPLS_HD void ppls_logl_k(const double* G, int r, int k, const PplsScalars* s, double* logs, double* trk) {
+  const double sX2 = s->sigE * s->sigE, sY2 = s->sigF * s->sigF;
+  double c1, c2, c3, Kc;
+  ppls_coef_logl(s->t[k], s->b[k], s->sigE, s->sigF, s->sigH, &c1, &c2, &c3, &Kc);
+  *logs = log(sX2 + s->t[k] * s->t[k]) + log(sY2 + Kc);
+  *trk = -c1 * PPLS_GA(G, r, k, k) - 2.0 * c2 * PPLS_GD(G, r, k, k) - c3 * PPLS_GB(G, r, k, k);
+}
+
+PPLS_HD double ppls_logl_total(double logs, double trk, double ssqX, double ssqY, double N, int64_t p,
+                               int64_t q, int r, const PplsScalars* s) {
+  const double sX2 = s->sigE * s->sigE, sY2 = s->sigF * s->sigF;
+  const double logdet = logs + (double)(p - r) * log(sX2) + (double)(q - r) * log(sY2);   // :331
+  const double traceL = 1.0 / sX2 * ssqX + 1.0 / sY2 * ssqY + trk;                       // :334-335
+  return -0.5 * N * (double)(p + q) * log(2.0 * M_PI) - 0.5 * N * logdet - 0.5 * traceL;  // :336
+}
+
 PPLS_HD double ppls_loglik_from_gram(const double* G, double ssqX, double ssqY, double N, int64_t p,
                                      int64_t q, int r, const PplsScalars* s) {
-  const double sX2 = s->sigE * s->sigE, sY2 = s->sigF * s->sigF;
-  double logdet = 0.0, a1 = 0.0, a2 = 0.0;
-  double c1[PPLS_RMAX], c2[PPLS_RMAX], c3[PPLS_RMAX], Kc[PPLS_RMAX];
+  double logs = 0.0, trk = 0.0;
   for (int k = 0; k < r; ++k) {
-    ppls_coef_logl(s->t[k], s->b[k], s->sigE, s->sigF, s->sigH, &c1[k], &c2[k], &c3[k], &Kc[k]);
-    a1 += log(sX2 + s->t[k] * s->t[k]);
-    a2 += log(sY2 + Kc[k]);
+    double a, b;
+    ppls_logl_k(G, r, k, s, &a, &b);
+    logs += a;
+    trk += b;
   }
-  logdet = a1 + (double)(p - r) * log(sX2) + a2 + (double)(q - r) * log(sY2);   // :331
-  double traceL = 1.0 / sX2 * ssqX + 1.0 / sY2 * ssqY;                          // :334
-  for (int k = 0; k < r; ++k)                                                   // :335
-    traceL += -c1[k] * PPLS_GA(G, r, k, k) - 2.0 * c2[k] * PPLS_GD(G, r, k, k) -
-              c3[k] * PPLS_GB(G, r, k, k);
-  return -0.5 * N * (double)(p + q) * log(2.0 * M_PI) - 0.5 * N * logdet - 0.5 * traceL;  // :336
+  return ppls_logl_total(logs, trk, ssqX, ssqY, N, p, q, r, s);
 }
 
 // Generic loglC_fast from explicit coefficient vectors (the drop-in for the .Call boundary).

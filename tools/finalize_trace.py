@@ -1,0 +1,38 @@
+"""Phase timeline of the finalize kernel (wall-clock stamps written by the kernel itself)."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from bench import CONFIGS, make_truth_and_theta0  # noqa: E402
+from ppls_amd import Context  # noqa: E402
+
+SLOTS = {0: "start", 1: "gram1/WtW summed", 2: "chol1+inv / serial scalars", 3: "gram2 summed",
+         4: "serial r x r (chol2, Jacobi, products)", 5: "output written"}
+
+
+def main():
+    for cfgname in sys.argv[1:] or ["c3"]:
+        cfg = CONFIGS[cfgname]
+        n, p, q, r = cfg["n"], cfg["p"], cfg["q"], cfg["r"]
+        ctx = Context(0)
+        truth, th0 = make_truth_and_theta0(p, q, r)
+        ctx.generate_synthetic(min(n, 200_000), p, q, truth, seed=20261015)
+        ctx.set_option("ftrace", 1)
+        ctx.em_begin(th0)
+        for it in range(4):
+            ctx.em_iterate(1)
+            tr = ctx.finalize_trace()
+            raw = tr[0][10:]
+            if raw[1] and raw[2]:
+                us = tr[0][5]
+                print(f"  block 0: jacobi sweeps {raw[0]}, core clock {(raw[2] - raw[1]) / (us * 1e3):.2f} GHz")
+            print(f"{cfgname} iter {it}: " + "; ".join(
+                f"block {b}: " + " ".join(f"{s}={v}" for s, v in enumerate(ts) if v is not None)
+                for b, ts in tr.items()), flush=True)
+        ctx.set_option("ftrace", 0)
+        ctx.close()
+
+
+if __name__ == "__main__":
+    main()
