@@ -69,16 +69,16 @@ def cpu_baseline(ctx, th0, cfg, seconds_target=15.0):
     from ppls_amd import Context
     th = th0.as_dict()
     cores = cpu_ref.load().cpu_ref_max_threads()
-    n_probe = min(ctx.n_local, 5000)
-    X, Y = ctx.get_data(0, n_probe)
-    t0 = time.perf_counter()
-    cpu_ref.em_steps(np.ascontiguousarray(X), np.ascontiguousarray(Y), th, 1)
-    per_row_iter = (time.perf_counter() - t0) / n_probe
     n_s = int(min(ctx.n_local, 150_000))
-    steps = int(min(200, max(2, seconds_target / (n_s * per_row_iter))))
     X, Y = ctx.get_data(0, n_s)
     Xs, Ys = np.ascontiguousarray(X), np.ascontiguousarray(Y)
     del X, Y
+    # calibrate on the sample itself (a small probe fits in cache and overstates the rate);
+    # this untimed pass also faults the pages in and spins up the OpenMP pool
+    t0 = time.perf_counter()
+    cpu_ref.em_steps(Xs, Ys, th, 1)
+    per_iter = time.perf_counter() - t0
+    steps = int(min(200, max(2, round(seconds_target / per_iter))))
     t0 = time.perf_counter()
     th_cpu, ll_cpu = cpu_ref.em_steps(Xs, Ys, th, steps)
     dt = time.perf_counter() - t0
@@ -114,6 +114,8 @@ def main():
     ap.add_argument("--threads", type=int, default=0, help="fused workgroup size: 0 auto, 512, 1024")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--timing-every", type=int, default=4,
+                    help="bracket every N-th sweep of the timed region with HIP events")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -155,7 +157,7 @@ def main():
     ctx.em_begin(th0)
     ctx.em_iterate(args.warmup)
     barrier()
-    ctx.set_option("timing", 1)
+    ctx.set_option("timing", args.timing_every)
     ctx.sweep_timing(reset=True)
     t0 = time.perf_counter()
     ctx.em_iterate(args.steps)

@@ -76,7 +76,9 @@ int ppls_ctx_create(int device, ppls_ctx** out);
 void ppls_ctx_destroy(ppls_ctx* ctx);
 const char* ppls_last_error(const ppls_ctx* ctx);
 /* keys: "sweep" (0 auto, 1 fused single-pass, 2 generic two-pass), "grid" (workgroups, 0 = auto),
- *       "timing" (1: record HIP events around every sweep launch) */
+ *       "nt" (sweep loads with the non-temporal cache policy: -1 auto (default: when X, Y exceed
+ *             the 256 MB MALL), 0 off, 1 on),
+ *       "timing" (N > 0: record HIP events around every N-th sweep launch; 0 off) */
 int ppls_set_option(ppls_ctx* ctx, const char* key, int64_t value);
 
 /* ---- multi-GPU: samples are sharded over ranks; one RCCL all-reduce per EM iteration ---- */

@@ -284,6 +284,10 @@ __device__ __forceinline__ void ppls_wait_vmcnt(int n) {
 // put vmcnt(0) in front of every ds_read of the ring (it cannot prove the slots do not alias);
 // the ring's completion is waited for explicitly with ppls_wait_vmcnt.  Invisible VMEM ops can
 // only make the compiler's own vmcnt waits stricter, never unsafe.
+__device__ __forceinline__ void ppls_dma16_nt(const void* gptr, uint32_t lds_addr) {
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt"
+               :: "s"(lds_addr), "v"(gptr) : "memory", "m0");
+}
 __device__ __forceinline__ void ppls_dma16(const void* gptr, uint32_t lds_addr) {
   asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off"
                :: "s"(lds_addr), "v"(gptr) : "memory", "m0");
@@ -310,6 +314,7 @@ __global__ __launch_bounds__(NT, 2 * NT / 512) void ppls_sweep_fused_kernel(
     const double* __restrict__ X, const double* __restrict__ Y, int64_t n_local, int ldx, int ldy,
     const double* __restrict__ Wp, const double* __restrict__ Cp, const PplsScalars* __restrict__ sc,
     double* __restrict__ part, int64_t part_ld, double* __restrict__ mu, int write_mu, int ablate) {
+  // ablate bit4: LDS-DMA with the non-temporal policy (a cache hint; results unchanged).
   // ablate (timing experiments only; results are garbage): bit0 skips the per-row compute,
   // bit1 skips the HBM->LDS copies.
   static_assert(SLOTS >= 2 * RP, "ring must hold the group being read and the group in flight");
@@ -383,7 +388,8 @@ __global__ __launch_bounds__(NT, 2 * NT / 512) void ppls_sweep_fused_kernel(
       const char* src;
       if (ch < nchx) src = xr + min(ch * 1024 + lane * 16, ldx * 8 - 16);
       else src = yr + min((ch - nchx) * 1024 + lane * 16, ldy * 8 - 16);
-      ppls_dma16(src, sb + (uint32_t)(ch * 1024));
+      if (ablate & 16) ppls_dma16_nt(src, sb + (uint32_t)(ch * 1024));
+      else ppls_dma16(src, sb + (uint32_t)(ch * 1024));
     }
   };
   auto issue_group = [&](int grp) {
@@ -609,7 +615,8 @@ __global__ __launch_bounds__(NT, 2 * NT / 512) void ppls_sweep_split_kernel(
       const char* src;
       if (ch < nchx) src = xr + min(ch * 1024 + lane * 16, ldx * 8 - 16);
       else src = yr + min((ch - nchx) * 1024 + lane * 16, ldy * 8 - 16);
-      ppls_dma16(src, sb + (uint32_t)(ch * 1024));
+      if (ablate & 16) ppls_dma16_nt(src, sb + (uint32_t)(ch * 1024));
+      else ppls_dma16(src, sb + (uint32_t)(ch * 1024));
     }
   };
   auto issue_group = [&](int grp) {
