@@ -117,6 +117,29 @@ int ppls_em_run(ppls_ctx* ctx, ppls_theta* th, int r, int max_steps, double atol
 int ppls_em_begin(ppls_ctx* ctx, const ppls_theta* theta0, int r);
 int ppls_em_iterate(ppls_ctx* ctx, int nsteps, int type);
 int ppls_em_state(ppls_ctx* ctx, ppls_theta* out, double* loglik, int loglik_cap, int* n_loglik);
+
+/* ---- sequential initialiser: PPLS(X, Y, a, EMsteps, atol, initialGuess) -------------------------
+ * Replaces the R functions PPLS (Package/PPLS/R/EM_W_multi.R:229-279), PPLSi (:116-180) and
+ * EMstep_W (:51-73) -> .Call('PPLS_EMstepC_fast') (R/RcppExports.R:36-38, src/loglC.cpp:340-397),
+ * i.e. the f0 = PPLS(X, Y, a, 20, 1e-4, 'random') that PPLS_simult starts from (:762).
+ * a rank-1 EM fits, component k on X, Y deflated by components 1..k-1 (:270-271; implicit here).
+ * init: a starting values (theta with r = 1: W p, C q, B[1], sigT[1], sigE, sigF, sigH), i.e. the
+ * initialGuess draws the R side makes (:126-145).  Stop rule per component: increment < atol
+ * (critfunc = identity), no constraints.  If a component's sigE or sigF falls below
+ * 100 * DBL_EPSILON the fit stops there (:152-154, :258-263): ncomp < a. */
+typedef struct {
+  double* W;               /* p x a, column-major (R's W) */
+  double* C;               /* q x a */
+  double* B;               /* a */
+  double* sig;             /* a x 4, column-major: sigX, sigY, sigH, sigT (R's sig) */
+  double* logvalue;        /* nullable: a x (EMsteps + 1), row k = component k's logvalue, NaN padded */
+  double* last_increment;  /* nullable: a (Other_output$Last_increment) */
+  int* number_steps;       /* nullable: a (Other_output$Number_steps) */
+  double* loglikelihoods;  /* nullable: a (Other_output$Loglikelihoods: logl_W of X, Y, comps 1..k) */
+  int ncomp;               /* out: components fitted */
+  int not_monotone;        /* out: bit k set if component k's logvalue decreased (warning, :177) */
+} ppls_seq_fit;
+int ppls_ppls(ppls_ctx* ctx, int a, int max_steps, double atol, const ppls_theta* init, ppls_seq_fit* out);
 int ppls_synchronize(ppls_ctx* ctx);
 
 /* loglC_fast (src/loglC.cpp:318-338) with the reference's argument list.  X, Y (column-major

@@ -11,7 +11,13 @@ Every function cites the reference line it restates (paths relative to /root/ref
 * ``maximiz_m``          Package/PPLS/R/EM_W_multi.R:729-742, tr() Package/PPLS/R/PJSC.R:1-5
 * ``logl_w``             Package/PPLS/R/EM_W_multi.R:297-323
 * ``loglc_fast``         Package/PPLS/src/loglC.cpp:318-338 (the ``src/`` copy; src-x64 has p, not p+q)
-* ``ppls_simult``        Package/PPLS/R/EM_W_multi.R:758-807 (init :762-771 replaced by an explicit theta0)
+* ``ppls_simult``        Package/PPLS/R/EM_W_multi.R:758-807 (init :762-771 replaced by an explicit theta0,
+                         or by ``ppls`` below with explicit per-component starting values)
+* ``emstepc_fast``       Package/PPLS/src/loglC.cpp:340-397 (one rank-1 EM step)
+* ``emstep_w``           Package/PPLS/R/EM_W_multi.R:51-73
+* ``pplsi``              Package/PPLS/R/EM_W_multi.R:116-180 (one direction; no constraints, critfunc = I)
+* ``ppls``               Package/PPLS/R/EM_W_multi.R:229-279 (sequential fit with deflation)
+* ``initial_guess``      Package/PPLS/R/EM_W_multi.R:126-140 ('equal'; 'random' with numpy draws)
 * ``orth``               OmicsPLS::orth (not vendored); semantics Package/functions.R:252-260
 * ``ssq``                OmicsPLS::ssq (not vendored); semantics Package/functions.R:380-385
 
@@ -348,3 +354,136 @@ def mu_coefficients(B, sigE, sigF, sigH, sigT):
     gamma = t2 * b / sigE ** 2 - cf["c1"] * t2 * b - cf["c2"] * v
     delta = v / sigF ** 2 - cf["c2"] * t2 * b - cf["c3"] * v
     return dict(alpha=alpha, beta=beta, gamma=gamma, delta=delta, **cf)
+
+
+# ----------------------------------------------------------------------------- sequential init (PPLS)
+
+def emstepc_fast(W, C, B, X, Y, sigX, sigY, sigH, sigT, c1, c2, c3):
+    """EMstepC_fast -- Package/PPLS/src/loglC.cpp:340-397 (W, C vectors; scalars)."""
+    sig2X, sig2Y, sig2H, sig2T = sigX * sigX, sigY * sigY, sigH * sigH, sigT * sigT
+    N = X.shape[0]
+    p, q = W.shape[0], C.shape[0]
+    Xw = X @ W                                                                    # :351
+    Yc = Y @ C
+    mu_T = Xw * sig2T * (-c1 + -c2 * B + 1 / sig2X) + Yc * sig2T * (-c2 + -c3 * B + 1 / sig2Y * B)   # :354
+    Cxt = X.T @ mu_T / N                                                          # :355
+    Ctt = sig2T - sig2T * sig2T * (-c1 - 2 * B * c2 - B * B * (c3 - 1 / sig2Y) + 1 / sig2X) + mu_T @ mu_T / N
+    v = sig2T * B * B + sig2H
+    mu_U = Xw * (-sig2T * B * c1 + -c2 * v + 1 / sig2X * B * sig2T) + Yc * (-c2 * B * sig2T + -c3 * v + 1 / sig2Y * v)
+    Cyu = Y.T @ mu_U / N                                                          # :360
+    Cuu = v - (-(c1 - 1 / sig2X) * sig2T * sig2T * B * B - 2 * sig2T * B * v * c2 - v ** 2 * (c3 - 1 / sig2Y)) \
+        + mu_U @ mu_U / N                                                         # :361
+    Cut = sig2T * B - (-sig2T * sig2T * B * (c1 - 1 / sig2X) - sig2T * sig2T * B * B * c2 - sig2T * v * c2
+                       - v * sig2T * B * (c3 - 1 / sig2Y)) + mu_U @ mu_T / N       # :363
+    xw2, yc2, xy = Xw @ Xw, Yc @ Yc, Xw @ Yc
+    Ceetmp = (c1 * c1 * sig2X * sig2X * xw2 + ssq(X) + c2 * c2 * sig2X * sig2X * yc2 - 2 * c1 * sig2X * xw2
+              + 2 * c1 * c2 * sig2X * sig2X * xy - 2 * c2 * sig2X * xy)           # :365-366
+    Cee = sig2X - (-sig2X * sig2X * c1 + p * sig2X) / p + Ceetmp / N / p          # :367
+    Cfftmp = (c3 * c3 * sig2Y * sig2Y * yc2 + ssq(Y) + c2 * c2 * sig2Y * sig2Y * xw2 - 2 * c3 * sig2Y * yc2
+              + 2 * c3 * c2 * sig2Y * sig2Y * xy - 2 * c2 * sig2Y * xy)           # :369-370
+    Cff = sig2Y - (-sig2Y * sig2Y * c3 + q * sig2Y) / q + Cfftmp / N / q          # :371
+    mh = -c2 * sig2H * Xw - (c3 - 1 / sig2Y) * sig2H * Yc
+    Chh = sig2H - (-sig2H * sig2H * (c3 - 1 / sig2Y)) + mh @ mh / N               # :373
+    return dict(mu_T=mu_T, mu_U=mu_U, W=Cxt / np.linalg.norm(Cxt), C=Cyu / np.linalg.norm(Cyu),
+                B=Cut / Ctt, sighat=np.array([math.sqrt(Cee), math.sqrt(Cff)]),
+                siglathat=np.array([math.sqrt(Chh), math.sqrt(Ctt)]),
+                Cut=Cut, Ctt=Ctt, Cuu=Cuu, Cee=Cee, Cff=Cff, Chh=Chh)            # :377-396
+
+
+def emstep_w(X, Y, W, C, B_T, sigX, sigY, sigH, sigT):
+    """EMstep_W -- Package/PPLS/R/EM_W_multi.R:51-73 (coefficients with g = t^2 b^2 + sigH^2)."""
+    W = np.ravel(W)
+    C = np.ravel(C)
+    B_T, sigX, sigY, sigH, sigT = (float(np.ravel(v)[0]) for v in (B_T, sigX, sigY, sigH, sigT))
+    g = sigT ** 2 * B_T ** 2 + sigH ** 2
+    Kw = sigT ** 2 - sigT ** 4 * B_T ** 2 / sigY ** 2 + sigT ** 4 * B_T ** 2 * g / (sigY ** 2 * (g + sigY ** 2))
+    Kc = g - sigT ** 4 * B_T ** 2 / sigX ** 2 + sigT ** 6 * B_T ** 2 / (sigX ** 2 * (sigT ** 2 + sigX ** 2))
+    Kwc = (sigT ** 2 * B_T / (sigX ** 2 * sigY ** 2) - Kc * sigT ** 2 * B_T / (sigX ** 2 * sigY ** 2 * (Kc + sigY ** 2))
+           - sigT ** 4 * B_T / (sigX ** 2 * sigY ** 2 * (sigT ** 2 + sigX ** 2))
+           + Kc * sigT ** 4 * B_T / (sigX ** 2 * sigY ** 2 * (Kc + sigY ** 2) * (sigT ** 2 + sigX ** 2)))
+    c1 = Kw / (sigX ** 2 * (Kw + sigX ** 2))
+    c3 = Kc / (sigY ** 2 * (Kc + sigY ** 2))
+    return emstepc_fast(W, C, B_T, X, Y, sigX, sigY, sigH, sigT, c1, Kwc, c3)
+
+
+def initial_guess(p, q, kind="equal", rng=None):
+    """PPLSi starting values -- EM_W_multi.R:126-140.  'equal' is deterministic; 'random' uses the
+    reference's distributions (orth(runif), rchisq(1,1), rchisq(2,100)/100, rchisq(2,10)/100) drawn
+    from numpy, since R's RNG stream is not reproducible here."""
+    if kind == "equal":
+        return dict(W=np.ones(p) / math.sqrt(p), C=np.ones(q) / math.sqrt(q), B=1.0,
+                    sigE=1.0 / p, sigF=1.0 / q, sigH=1.0, sigT=1.0)
+    if kind == "random":
+        rng = rng if rng is not None else np.random.default_rng()
+        W = rng.uniform(size=p)
+        C = rng.uniform(size=q)
+        B = rng.chisquare(1)
+        siglat = rng.chisquare(100, size=2) / 100
+        sig = rng.chisquare(10, size=2) / 100
+        return dict(W=W / np.linalg.norm(W), C=C / np.linalg.norm(C), B=float(B), sigE=float(sig[0]),
+                    sigF=float(sig[1]), sigH=float(siglat[0]), sigT=float(siglat[1]))
+    raise ValueError(kind)
+
+
+def pplsi(X, Y, EMsteps=100, atol=1e-4, theta0=None):
+    """PPLSi -- Package/PPLS/R/EM_W_multi.R:116-180 with critfunc = identity and no constraints;
+    theta0 = initial_guess(...) (or a customGuess).  Returns the reference's list; NA fit -> W None."""
+    W = np.ravel(np.asarray(theta0["W"], dtype=np.float64))
+    C = np.ravel(np.asarray(theta0["C"], dtype=np.float64))
+    B, sigE, sigF = float(theta0["B"]), float(theta0["sigE"]), float(theta0["sigF"])
+    sigH, sigT = float(theta0["sigH"]), float(theta0["sigT"])
+
+    def ll(W, C, B, sigE, sigF, sigH, sigT):
+        return logl_w(X, Y, W.reshape(-1, 1), C.reshape(-1, 1), np.array([[B]]), sigE, sigF, sigH,
+                      np.array([[sigT]]))
+
+    logvalue = [ll(W, C, B, sigE, sigF, sigH, sigT)]                               # :149
+    i = 0
+    for i in range(1, EMsteps + 1):                                                 # :151
+        if sigE < 100 * np.finfo(float).eps or sigF < 100 * np.finfo(float).eps:   # :152-154
+            return dict(W=None, C=None, B=None, sig=None, logvalue=None, Last_increment=None, Number_steps=i)
+        fit = emstep_w(X, Y, W, C, B, sigE, sigF, sigH, sigT)                        # :156
+        B, W, C = float(fit["B"]), fit["W"], fit["C"]
+        sigE, sigF = fit["sighat"]
+        sigH, sigT = fit["siglathat"]
+        logvalue.append(ll(W, C, B, sigE, sigF, sigH, sigT))                         # :172
+        if logvalue[i] - logvalue[i - 1] < atol:                                    # :173
+            break
+    last = logvalue[i] - logvalue[i - 1]                                            # :176
+    return dict(W=W, C=C, B=B, sig=np.array([sigE, sigF, sigH, sigT]), logvalue=np.array(logvalue),
+                Last_increment=last, Number_steps=i, not_monotone=bool(np.any(np.diff(logvalue) < 0)))
+
+
+def ppls(X, Y, nr_comp=1, EMsteps=100, atol=1e-4, theta0s=None):
+    """PPLS -- Package/PPLS/R/EM_W_multi.R:229-279: nr_comp PPLSi fits on successively deflated
+    X, Y (:270-271).  theta0s: one starting-value dict per component (initial_guess)."""
+    X = np.asarray(X, dtype=np.float64)
+    Y = np.asarray(Y, dtype=np.float64)
+    a = nr_comp
+    p, q = X.shape[1], Y.shape[1]
+    Wn, Cn = np.full((p, a), np.nan), np.full((q, a), np.nan)
+    Bn, sig = np.full(a, np.nan), np.full((a, 4), np.nan)
+    other = dict(Last_increment=[], Number_steps=[], Loglikelihoods=[], logvalue=[])
+    Xc, Yc = X, Y
+    done = 0
+    for i in range(a):                                                              # :254
+        fit = pplsi(Xc, Yc, EMsteps, atol, theta0s[i])                              # :256-257
+        if fit["B"] is None:                                                        # :258-263
+            break
+        Wn[:, i], Cn[:, i], Bn[i], sig[i] = fit["W"], fit["C"], fit["B"], fit["sig"]
+        Xc = Xc - np.outer(Xc @ fit["W"], fit["W"])                                 # :270
+        Yc = Yc - np.outer(Yc @ fit["C"], fit["C"])                                 # :271
+        other["Last_increment"].append(fit["Last_increment"])
+        other["Number_steps"].append(fit["Number_steps"])
+        other["logvalue"].append(fit["logvalue"])
+        other["Loglikelihoods"].append(logl_w(X, Y, Wn[:, :i + 1], Cn[:, :i + 1], np.diag(Bn[:i + 1]),
+                                              sig[i, 0], sig[i, 1], sig[i, 2], np.diag(sig[:i + 1, 3])))  # :274
+        done = i + 1
+    return dict(W=Wn[:, :done], C=Cn[:, :done], B=Bn[:done], sig=sig[:done], Other_output=other)
+
+
+def simult_theta0_from_ppls(f0):
+    """PPLS_simult's use of the sequential fit -- EM_W_multi.R:764-770."""
+    a = f0["W"].shape[1]
+    return dict(W=f0["W"], C=f0["C"], B=np.diag(f0["B"]), sigE=f0["sig"][a - 1, 0],
+                sigF=f0["sig"][a - 1, 1], sigH=f0["sig"][a - 1, 2], sigT=np.diag(f0["sig"][:, 3]))

@@ -32,6 +32,12 @@ class PplsExpect(ct.Structure):
                 ("Cee", ct.c_double), ("Cff", ct.c_double), ("Chh", _dp)]
 
 
+class PplsSeqFit(ct.Structure):
+    _fields_ = [("W", _dp), ("C", _dp), ("B", _dp), ("sig", _dp), ("logvalue", _dp),
+                ("last_increment", _dp), ("number_steps", ct.POINTER(ct.c_int)),
+                ("loglikelihoods", _dp), ("ncomp", ct.c_int), ("not_monotone", ct.c_int)]
+
+
 # name -> (restype, argtypes); every symbol declared in include/ppls.h
 SIGNATURES = {
     "ppls_version": (ct.c_int, []),
@@ -65,6 +71,8 @@ SIGNATURES = {
     "ppls_em_iterate": (ct.c_int, [ct.c_void_p, ct.c_int, ct.c_int]),
     "ppls_em_state": (ct.c_int, [ct.c_void_p, ct.POINTER(PplsTheta), _dp, ct.c_int, ct.POINTER(ct.c_int)]),
     "ppls_synchronize": (ct.c_int, [ct.c_void_p]),
+    "ppls_ppls": (ct.c_int, [ct.c_void_p, ct.c_int, ct.c_int, ct.c_double, ct.POINTER(PplsTheta),
+                             ct.POINTER(PplsSeqFit)]),
     "ppls_sweep_timing": (ct.c_int, [ct.c_void_p, _dp, ct.POINTER(ct.c_int64), ct.c_int]),
     "ppls_finalize_trace": (ct.c_int, [ct.c_void_p, ct.POINTER(ct.c_int64), _dp]),
     "ppls_sweep_info": (ct.c_int, [ct.c_void_p, ct.c_int, ct.POINTER(ct.c_int64), ct.POINTER(ct.c_int),

@@ -193,6 +193,34 @@ class Context:
         out.pull(o)
         return out, ll[: n.value].copy()
 
+    def ppls(self, a: int, max_steps: int, atol: float, inits):
+        """Sequential PPLS fit (EM_W_multi.R:229-279) from a list of ``a`` rank-1 starting values
+        (dicts W, C, B, sigE, sigF, sigH, sigT).  Returns the reference's list (W, C, B, sig,
+        Other_output) plus the per-component logvalue traces."""
+        p, q = self.p, self.q
+        ths = [Theta(np.reshape(t["W"], (p, 1)), np.reshape(t["C"], (q, 1)), float(np.ravel(t["B"])[0]),
+                     t["sigE"], t["sigF"], t["sigH"], float(np.ravel(t["sigT"])[0])) for t in inits]
+        if len(ths) != a:
+            raise ValueError(f"{len(ths)} starting values for nr_comp = {a}")
+        arr = (_lib.PplsTheta * a)(*[t.struct() for t in ths])
+        W = np.zeros((p, a), order="F")
+        C = np.zeros((q, a), order="F")
+        B = np.zeros(a)
+        sig = np.zeros((a, 4), order="F")
+        lv = np.full((a, max_steps + 1), np.nan)
+        last = np.zeros(a)
+        nst = np.zeros(a, dtype=np.int32)
+        lls = np.zeros(a)
+        fit = _lib.PplsSeqFit(dptr(W), dptr(C), dptr(B), dptr(sig), dptr(lv), dptr(last),
+                              nst.ctypes.data_as(ct.POINTER(ct.c_int)), dptr(lls), 0, 0)
+        self._chk(self._L.ppls_ppls(self.h, int(a), int(max_steps), float(atol), arr, ct.byref(fit)))
+        k = fit.ncomp
+        return dict(W=W[:, :k].copy(), C=C[:, :k].copy(), B=B[:k].copy(), sig=sig[:k].copy(),
+                    Other_output=dict(Last_increment=last[:k].copy(), Number_steps=nst[:k].copy(),
+                                      Loglikelihoods=lls[:k].copy(),
+                                      logvalue=[lv[i, :nst[i] + 1].copy() for i in range(k)]),
+                    not_monotone=[bool(fit.not_monotone >> i & 1) for i in range(k)], ncomp=k)
+
     def synchronize(self):
         self._chk(self._L.ppls_synchronize(self.h))
 
@@ -333,19 +361,96 @@ def random_theta0(p, q, a, seed=0):
                 B=np.eye(a), sigE=1.0, sigF=1.0, sigH=1.0, sigT=np.eye(a))
 
 
+def initial_guess(p, q, kind="equal", rng=None):
+    """PPLSi's starting values (EM_W_multi.R:126-140): 'equal' (deterministic) or 'random' with the
+    reference's distributions -- orth(runif(p)), orth(runif(q)), rchisq(1,1), rchisq(2,100)/100
+    (sigH, sigT), rchisq(2,10)/100 (sigE, sigF) -- drawn from numpy (R's RNG stream cannot be
+    reproduced; pass customGuess for exact starting values).  'o2m' needs OmicsPLS: not provided."""
+    if kind == "equal":
+        return dict(W=np.ones(p) / np.sqrt(p), C=np.ones(q) / np.sqrt(q), B=1.0, sigE=1.0 / p,
+                    sigF=1.0 / q, sigH=1.0, sigT=1.0)
+    if kind == "random":
+        rng = rng if rng is not None else np.random.default_rng()
+        W = rng.uniform(size=p)
+        C = rng.uniform(size=q)
+        B = rng.chisquare(1)
+        siglat = rng.chisquare(100, size=2) / 100
+        sig = rng.chisquare(10, size=2) / 100
+        return dict(W=W / np.linalg.norm(W), C=C / np.linalg.norm(C), B=float(B), sigE=float(sig[0]),
+                    sigF=float(sig[1]), sigH=float(siglat[0]), sigT=float(siglat[1]))
+    if kind == "o2m":
+        raise NotImplementedError("initialGuess='o2m' needs OmicsPLS::o2m (out of scope)")
+    raise ValueError(f"unknown initialGuess {kind!r}")
+
+
+def PPLS(X, Y, nr_comp=1, EMsteps=100, atol=1e-4, initialGuess=("equal", "o2m", "random", "custom"),
+         customGuess=None, rng=None, ctx=None):
+    """PPLS (EM_W_multi.R:229-279) on the GPU: nr_comp sequential rank-1 EM fits on deflated data.
+    Same return list (W, C, B, sig, Other_output); class "PPLS".  customGuess: one dict (used for
+    every component, as in R) or a list of per-component dicts."""
+    ctx = _ctx_with(X, Y, ctx)
+    kind = initialGuess if isinstance(initialGuess, str) else initialGuess[0]
+    if customGuess is not None:
+        kind = "custom"
+    if kind == "custom":
+        inits = list(customGuess) if isinstance(customGuess, (list, tuple)) else [customGuess] * nr_comp
+    else:
+        rng = rng if rng is not None else np.random.default_rng()
+        inits = [initial_guess(ctx.p, ctx.q, kind, rng) for _ in range(nr_comp)]
+    out = ctx.ppls(int(nr_comp), int(EMsteps), float(atol), inits)
+    if out["ncomp"] < nr_comp:
+        warnings.warn(f"From component {out['ncomp'] + 1} on the residuals are of rank < 1e-14 and "
+                      "calculations are stopped.")
+    for k, bad in enumerate(out.pop("not_monotone")):
+        if bad:
+            warnings.warn(f"Not monotone (component {k + 1})")
+    out.pop("ncomp")
+    out["class"] = "PPLS"
+    return out
+
+
+def PPLSi(X, Y, EMsteps=100, atol=1e-4, initialGuess=("equal", "o2m", "random", "custom"),
+          customGuess=None, rng=None, ctx=None):
+    """PPLSi (EM_W_multi.R:116-180): one direction; returns W, C, B, sig, logvalue, Last_increment,
+    Number_steps (W = NA when sigE or sigF collapse, :152-154)."""
+    fit = PPLS(X, Y, 1, EMsteps, atol, initialGuess, customGuess, rng, ctx)
+    if len(fit["B"]) == 0:
+        return dict(W=None, C=None, B=None, sig=None, logvalue=None, Last_increment=None, Number_steps=None)
+    oo = fit["Other_output"]
+    return dict(W=fit["W"][:, 0], C=fit["C"][:, 0], B=fit["B"][0], sig=fit["sig"][0],
+                logvalue=oo["logvalue"][0], Last_increment=oo["Last_increment"][0],
+                Number_steps=int(oo["Number_steps"][0]))
+
+
 def PPLS_simult(X, Y, a, EMsteps=10, atol=1e-4, type=("SVD", "QR"), init=None, ctx=None, **kw):
     """PPLS_simult (EM_W_multi.R:758-807) on the GPU.
 
-    ``init``: dict(W, C, B, sigE, sigF, sigH, sigT) used as theta0 (the reference's f0); default
-    ``random_theta0``.  Returns dict(Expectations, loglik, estimates) like the R list of class
-    "PPLS_simult"; warns "Negative increments of likelihood" where the reference does (:801).
+    ``init``: dict(W, C, B, sigE, sigF, sigH, sigT) used as theta0.  Default: the reference's own
+    f0 = PPLS(X, Y, a, 20, 1e-4, 'random') (:762-770, retried up to three times), computed on the
+    device with numpy draws (``seed`` keyword).  Returns dict(Expectations, loglik, estimates) like
+    the R list of class "PPLS_simult"; warns "Negative increments of likelihood" where the
+    reference does (:801).
     """
     if kw.get("debug"):
         raise NotImplementedError("debug=TRUE is an oracle-only cross-check")
     ctx = _ctx_with(X, Y, ctx)
     t = _orth_type(type)
     if init is None:
-        init = random_theta0(ctx.p, ctx.q, a, kw.get("seed", 0))
+        rng = np.random.default_rng(kw.get("seed"))
+        f0 = None
+        for _ in range(3):   # f0 = try(PPLS(...)) three times (:762-764)
+            try:
+                with warnings.catch_warnings():
+                    warnings.simplefilter("ignore")
+                    f0 = PPLS(None, None, a, 20, 1e-4, "random", rng=rng, ctx=ctx)
+                if len(f0["B"]) == a:
+                    break
+            except PplsError:
+                f0 = None
+        if f0 is None or len(f0["B"]) < a:
+            raise PplsError(-5, "PPLS initialisation failed three times")
+        init = dict(W=f0["W"], C=f0["C"], B=np.diag(f0["B"]), sigE=f0["sig"][a - 1, 0],
+                    sigF=f0["sig"][a - 1, 1], sigH=f0["sig"][a - 1, 2], sigT=np.diag(f0["sig"][:, 3]))
     th = Theta(init["W"], init["C"], init["B"], init["sigE"], init["sigF"], init["sigH"], init["sigT"])
     if th.r != a:
         raise ValueError(f"init has {th.r} components, a = {a}")

@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -902,6 +903,264 @@ int ppls_em_run(ppls_ctx* c, ppls_theta* th, int r, int max_steps, double atol, 
   canonicalize(th, c->p, c->q, r);   // :794-799
   if ((rc = download_moments(c, r, eout))) return rc;
   return download_mu(c, r, eout);
+}
+
+// ============================================================================ sequential initialiser
+// PPLS (EM_W_multi.R:229-279) -> PPLSi (:116-180) -> EMstep_W (:51-73) -> EMstepC_fast
+// (loglC.cpp:340-397).  Component k is fitted on Xc = X P_1 ... P_{k-1}, P_j = I - w_j w_j'
+// (:270-271; Yc likewise with c_j) without forming Xc: the r = 1 sweep runs on X with the weight
+// P_1..P_{k-1} w (so Xw of the sweep is Xc w), Xc' mu_T = P_{k-1}..P_1 X' mu_T, and
+// ||Xc||^2 = ||X||^2 - sum_j ||Xc_j w_j||^2 (w_j unit).  The sweeps (all the data traffic) run on
+// the device; the O((p+q) k) rank-1 update between them runs here on the host.
+}  // extern "C"
+
+namespace {
+
+// v <- P_{m-1} ... P_0 v (first_last = true: P_0 applied first) or P_0 ... P_{m-1} v.
+void deflate(const std::vector<double>& Wp, int m, int n, double* v, bool first_last) {
+  for (int jj = 0; jj < m; ++jj) {
+    const int j = first_last ? jj : m - 1 - jj;
+    const double* w = Wp.data() + (size_t)j * n;
+    double d = 0.0;
+    for (int i = 0; i < n; ++i) d += w[i] * v[i];
+    for (int i = 0; i < n; ++i) v[i] -= d * w[i];
+  }
+}
+
+struct Rank1 {
+  std::vector<double> w, c;   // unit loadings (the estimates)
+  double B, sigE, sigF, sigH, sigT;
+};
+
+// EMstep_W's coefficients (:60-70) and EMstepC_fast's mu coefficients (:354, :358).
+void rank1_coefs(const Rank1& t, double* c1, double* c2, double* c3, double* al, double* be, double* ga,
+                 double* de) {
+  ppls_coef_estep(t.sigT, t.B, t.sigE, t.sigF, t.sigH, c1, c2, c3, nullptr);
+  const double s2X = t.sigE * t.sigE, s2Y = t.sigF * t.sigF, s2H = t.sigH * t.sigH, s2T = t.sigT * t.sigT;
+  const double B = t.B, v = s2T * B * B + s2H;
+  *al = s2T * (-*c1 + -*c2 * B + 1 / s2X);
+  *be = s2T * (-*c2 + -*c3 * B + 1 / s2Y * B);
+  *ga = -s2T * B * *c1 + -*c2 * v + 1 / s2X * B * s2T;
+  *de = -*c2 * B * s2T + -*c3 * v + 1 / s2Y * v;
+}
+
+// One r = 1 sweep of theta t over the deflated data: stats -> host (SX p, SY q, G 2 x 2).
+int rank1_sweep(ppls_ctx* c, const Rank1& t, const std::vector<double>& Wp, const std::vector<double>& Cp,
+                int m, std::vector<double>& SX, std::vector<double>& SY, double G[4]) {
+  int rc;
+  std::vector<double> wv(c->ldx, 0.0), cv(c->ldy, 0.0);
+  std::copy(t.w.begin(), t.w.end(), wv.begin());
+  std::copy(t.c.begin(), t.c.end(), cv.begin());
+  deflate(Wp, m, c->p, wv.data(), false);   // X P_0 .. P_{m-1} w
+  deflate(Cp, m, c->q, cv.data(), false);
+  PplsScalars s;
+  memset(&s, 0, sizeof s);
+  s.b[0] = t.B;
+  s.t[0] = t.sigT;
+  s.sigE = t.sigE;
+  s.sigF = t.sigF;
+  s.sigH = t.sigH;
+  double c1, c2, c3;
+  rank1_coefs(t, &c1, &c2, &c3, &s.alpha[0], &s.beta[0], &s.gamma[0], &s.delta[0]);
+  HIPCHK(c, hipMemcpyAsync(c->W[0], wv.data(), sizeof(double) * c->ldx, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->C[0], cv.data(), sizeof(double) * c->ldy, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->sc[0], &s, sizeof s, hipMemcpyHostToDevice, c->stream));
+  if ((rc = sweep(c, 1, 0, false))) return rc;
+  std::vector<double> st((size_t)c->part_ld);
+  HIPCHK(c, hipMemcpyAsync(st.data(), c->stats, sizeof(double) * c->part_ld, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  SX.assign(st.begin(), st.begin() + c->p);
+  SY.assign(st.begin() + c->ldx, st.begin() + c->ldx + c->q);
+  for (int e = 0; e < 4; ++e) G[e] = st[(size_t)c->ldx + c->ldy + e];
+  return PPLS_OK;
+}
+
+// logl_W(Xc, Yc, w, c, B, sigE, sigF, sigH, sigT) from the sweep's Gram (:297-323, r = 1).
+double rank1_loglik(const Rank1& t, const double G[4], double ssqX, double ssqY, double N, int p, int q) {
+  PplsScalars s;
+  memset(&s, 0, sizeof s);
+  s.b[0] = t.B;
+  s.t[0] = t.sigT;
+  s.sigE = t.sigE;
+  s.sigF = t.sigF;
+  s.sigH = t.sigH;
+  return ppls_loglik_from_gram(G, ssqX, ssqY, N, p, q, 1, &s);
+}
+
+// EMstepC_fast (loglC.cpp:340-397) from the sweep of t; SX, SY are X'mu_T, Y'mu_U of the full
+// data, projected here onto the deflated column spaces.
+Rank1 rank1_update(const Rank1& t, std::vector<double> SX, std::vector<double> SY, const double G[4],
+                   double ssqX, double ssqY, double N, int p, int q, const std::vector<double>& Wp,
+                   const std::vector<double>& Cp, int m) {
+  double c1, c2, c3, al, be, ga, de;
+  rank1_coefs(t, &c1, &c2, &c3, &al, &be, &ga, &de);
+  const double s2X = t.sigE * t.sigE, s2Y = t.sigF * t.sigF, s2H = t.sigH * t.sigH, s2T = t.sigT * t.sigT;
+  const double B = t.B, v = s2T * B * B + s2H;
+  const double A = G[0], D = G[1], Bm = G[3];   // ||Xw||^2, <Xw, Yc>, ||Yc||^2
+  const double mt2 = al * al * A + 2.0 * al * be * D + be * be * Bm;
+  const double mu2 = ga * ga * A + 2.0 * ga * de * D + de * de * Bm;
+  const double mut = ga * al * A + (ga * be + de * al) * D + de * be * Bm;
+  const double Ctt = s2T - s2T * s2T * (-c1 - 2 * B * c2 - B * B * (c3 - 1 / s2Y) + 1 / s2X) + mt2 / N;   // :356
+  const double Cut = s2T * B - (-s2T * s2T * B * (c1 - 1 / s2X) - s2T * s2T * B * B * c2 - s2T * v * c2 -
+                                v * s2T * B * (c3 - 1 / s2Y)) + mut / N;                              // :363
+  (void)mu2;   // Cuu (:361) is not needed by the update
+  const double Ceetmp = c1 * c1 * s2X * s2X * A + ssqX + c2 * c2 * s2X * s2X * Bm - 2 * c1 * s2X * A +
+                        2 * c1 * c2 * s2X * s2X * D - 2 * c2 * s2X * D;                                // :365-366
+  const double Cee = s2X - (-s2X * s2X * c1 + p * s2X) / p + Ceetmp / N / p;                            // :367
+  const double Cfftmp = c3 * c3 * s2Y * s2Y * Bm + ssqY + c2 * c2 * s2Y * s2Y * A - 2 * c3 * s2Y * Bm +
+                        2 * c3 * c2 * s2Y * s2Y * D - 2 * c2 * s2Y * D;                                // :369-370
+  const double Cff = s2Y - (-s2Y * s2Y * c3 + q * s2Y) / q + Cfftmp / N / q;                            // :371
+  const double hx = -c2 * s2H, hy = -(c3 - 1 / s2Y) * s2H;
+  const double Chh = s2H - (-s2H * s2H * (c3 - 1 / s2Y)) + (hx * hx * A + 2 * hx * hy * D + hy * hy * Bm) / N;  // :373
+  deflate(Wp, m, p, SX.data(), true);   // Xc' mu_T = P_{m-1}..P_0 X' mu_T
+  deflate(Cp, m, q, SY.data(), true);
+  Rank1 n;
+  double nx = 0.0, ny = 0.0;
+  for (int i = 0; i < p; ++i) { SX[i] /= N; nx += SX[i] * SX[i]; }   // Cxt = Xc' mu_T / N (:355)
+  for (int i = 0; i < q; ++i) { SY[i] /= N; ny += SY[i] * SY[i]; }
+  nx = std::sqrt(nx);
+  ny = std::sqrt(ny);
+  n.w.resize(p);
+  n.c.resize(q);
+  for (int i = 0; i < p; ++i) n.w[i] = SX[i] / nx;   // Cxt.normalized() (:383)
+  for (int i = 0; i < q; ++i) n.c[i] = SY[i] / ny;
+  n.B = Cut / Ctt;                                   // :385
+  n.sigE = std::sqrt(Cee);                           // sighat (:376)
+  n.sigF = std::sqrt(Cff);
+  n.sigH = std::sqrt(Chh);                           // siglathat (:377)
+  n.sigT = std::sqrt(Ctt);
+  return n;
+}
+
+// ||X P_0..P_{m-1}||^2 (and the Y analogue) by an exact residual pass over the resident data,
+// all-reduced over ranks.  Used when the running ||X||^2 - sum ||Xc_j w_j||^2 has cancelled to
+// below 1e-6 ||X||^2, where its absolute error (~eps ||X||^2) would hide a rank collapse.
+int deflated_ssq(ppls_ctx* c, const std::vector<double>& Wp, int m, bool isx, double* out) {
+  int rc;
+  const int n = isx ? c->p : c->q;
+  const int nb = 1024;
+  double* Wd = nullptr;
+  double* buf = nullptr;
+  if ((rc = dalloc(c, &Wd, (size_t)n * std::max(m, 1)))) return rc;
+  if ((rc = dalloc(c, &buf, (size_t)nb + 1))) { dfree(Wd); return rc; }
+  double res = 0.0;
+  hipError_t e = hipMemcpyAsync(Wd, Wp.data(), sizeof(double) * n * m, hipMemcpyHostToDevice, c->stream);
+  if (e == hipSuccess)
+    e = ppls_launch_deflated_ssq(isx ? c->X : c->Y, c->n_local, isx ? c->ldx : c->ldy, n, Wd, m, buf, nb,
+                                 buf + nb, c->stream);
+  if (e == hipSuccess && c->n_local == 0) e = hipMemsetAsync(buf + nb, 0, sizeof(double), c->stream);
+  rc = e == hipSuccess ? allreduce(c, buf + nb, 1) : fail(c, PPLS_E_HIP, "deflated ssq: %s", hipGetErrorString(e));
+  if (!rc) {
+    e = hipMemcpyAsync(&res, buf + nb, sizeof(double), hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) rc = fail(c, PPLS_E_HIP, "deflated ssq: %s", hipGetErrorString(e));
+  }
+  dfree(Wd);
+  dfree(buf);
+  *out = res;
+  return rc;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ppls_ppls(ppls_ctx* c, int a, int max_steps, double atol, const ppls_theta* init, ppls_seq_fit* out) {
+  if (!c) return PPLS_E_ARG;
+  if (!c->have_data) return fail(c, PPLS_E_STATE, "no data");
+  if (!init || !out || !out->W || !out->C || !out->B || !out->sig) return fail(c, PPLS_E_ARG, "NULL argument");
+  if (a < 1 || a > PPLS_RMAX) return fail(c, PPLS_E_ARG, "nr_comp=%d outside [1,%d]", a, PPLS_RMAX);
+  if (c->p < a || c->q < a)   // stopifnot(ncol(X) >= nr_comp, ncol(Y) >= nr_comp) (:245)
+    return fail(c, PPLS_E_ARG, "ncol(X)=%d, ncol(Y)=%d must be >= number of components %d", c->p, c->q, a);
+  if (max_steps < 1) return fail(c, PPLS_E_ARG, "EMsteps must be >= 1");
+  for (int k = 0; k < a; ++k)
+    if (!init[k].W || !init[k].C || !init[k].B || !init[k].sigT)
+      return fail(c, PPLS_E_ARG, "init[%d] has NULL fields", k);
+  HIPCHK(c, hipSetDevice(c->device));
+  int rc;
+  if ((rc = ensure_r(c, 1, max_steps))) return rc;
+  const int p = c->p, q = c->q;
+  const double N = (double)c->n_total;
+  double ssqX = c->ssq_host[0], ssqY = c->ssq_host[1];   // ||Xc||^2, ||Yc||^2 of the current deflation
+  std::vector<double> Wp, Cp;                            // w_1..w_k, c_1..c_k (column-major)
+  std::vector<double> gA, gD, gB;                        // ||X w_j||^2, <X w_j, Y c_j>, ||Y c_j||^2
+  std::vector<double> SX, SY;
+  const double tiny = 100.0 * 2.220446049250313e-16;     // 100 * .Machine$double.eps
+  out->ncomp = 0;
+  out->not_monotone = 0;
+  if (out->logvalue)
+    for (size_t e = 0; e < (size_t)a * (max_steps + 1); ++e) out->logvalue[e] = NAN;
+  for (int k = 0; k < a; ++k) {
+    Rank1 t;
+    t.w.assign(init[k].W, init[k].W + p);
+    t.c.assign(init[k].C, init[k].C + q);
+    t.B = init[k].B[0];
+    t.sigT = init[k].sigT[0];
+    t.sigE = init[k].sigE;
+    t.sigF = init[k].sigF;
+    t.sigH = init[k].sigH;
+    double G[4];
+    if ((rc = rank1_sweep(c, t, Wp, Cp, k, SX, SY, G))) return rc;
+    std::vector<double> lv(1, rank1_loglik(t, G, ssqX, ssqY, N, p, q));   // logvalue[1] (:149)
+    int i = 0;
+    bool na = false;
+    for (i = 1; i <= max_steps; ++i) {                                    // :151
+      if (t.sigE < tiny || t.sigF < tiny) { na = true; break; }           // :152-154
+      t = rank1_update(t, SX, SY, G, ssqX, ssqY, N, p, q, Wp, Cp, k);     // :156-170
+      if ((rc = rank1_sweep(c, t, Wp, Cp, k, SX, SY, G))) return rc;
+      lv.push_back(rank1_loglik(t, G, ssqX, ssqY, N, p, q));              // :172
+      if (lv[i] - lv[i - 1] < atol) break;                                // :173
+    }
+    if (na) break;   // PPLS: "residuals are of rank < 1e-14", keep components 1..k-1 (:258-263)
+    if (i > max_steps) i = max_steps;
+    for (int e = 0; e < p; ++e) out->W[(size_t)k * p + e] = t.w[e];
+    for (int e = 0; e < q; ++e) out->C[(size_t)k * q + e] = t.c[e];
+    out->B[k] = t.B;
+    out->sig[k] = t.sigE;             // cbind(sigX, sigY, sigH, sigT), a x 4
+    out->sig[a + k] = t.sigF;
+    out->sig[2 * a + k] = t.sigH;
+    out->sig[3 * a + k] = t.sigT;
+    if (out->logvalue)
+      for (int e = 0; e <= i; ++e) out->logvalue[(size_t)k * (max_steps + 1) + e] = lv[e];
+    if (out->last_increment) out->last_increment[k] = lv[i] - lv[i - 1];   // :176
+    if (out->number_steps) out->number_steps[k] = i;
+    for (int e = 1; e <= i; ++e)
+      if (lv[e] - lv[e - 1] < 0) out->not_monotone |= 1 << k;              // warning("Not monotone") :177
+    // deflation (:270-271): the last sweep used theta_final, so its Gram holds ||Xc_k w_k||^2
+    gA.push_back(G[0]);
+    gD.push_back(G[1]);
+    gB.push_back(G[3]);
+    ssqX -= G[0];
+    ssqY -= G[3];
+    Wp.insert(Wp.end(), t.w.begin(), t.w.end());
+    Cp.insert(Cp.end(), t.c.begin(), t.c.end());
+    if (k + 1 < a && ssqX < 1e-6 * c->ssq_host[0])
+      if ((rc = deflated_ssq(c, Wp, k + 1, true, &ssqX))) return rc;
+    if (k + 1 < a && ssqY < 1e-6 * c->ssq_host[1])
+      if ((rc = deflated_ssq(c, Cp, k + 1, false, &ssqY))) return rc;
+    out->ncomp = k + 1;
+    // Other_output$Loglikelihoods[k] = logl_W(X, Y, W[,1:k], C[,1:k], diag(B[1:k]), sigX_k, sigY_k,
+    // sigH_k, diag(sigT[1:k])) (:274).  loglC_fast only reads the Gram diagonal, and X w_j = Xc_j w_j
+    // because w_j is orthogonal to w_1..w_{j-1}, so the per-component Grams above suffice.
+    if (out->loglikelihoods) {
+      const int r = k + 1;
+      std::vector<double> Gf((size_t)4 * r * r, 0.0);
+      PplsScalars s;
+      memset(&s, 0, sizeof s);
+      for (int j = 0; j < r; ++j) {
+        PPLS_GA(Gf.data(), r, j, j) = gA[j];
+        PPLS_GD(Gf.data(), r, j, j) = gD[j];
+        PPLS_GB(Gf.data(), r, j, j) = gB[j];
+        s.b[j] = out->B[j];
+        s.t[j] = out->sig[3 * a + j];
+      }
+      s.sigE = t.sigE;
+      s.sigF = t.sigF;
+      s.sigH = t.sigH;
+      out->loglikelihoods[k] = ppls_loglik_from_gram(Gf.data(), c->ssq_host[0], c->ssq_host[1], N, p, q, r, &s);
+    }
+  }
+  return PPLS_OK;
 }
 
 int ppls_em_begin(ppls_ctx* c, const ppls_theta* th, int r) {

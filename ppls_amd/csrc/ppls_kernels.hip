@@ -141,6 +141,40 @@ __device__ inline double ppls_wave_sum(double v) {
   return v;
 }
 
+// ||X P_0 .. P_{m-1}||^2 row by row, P_j = I - w_j w_j' (w_j: columns of Wd, p x m, ld p): the
+// residual x P is formed before squaring, so there is no cancellation when X is nearly
+// spanned by the w_j (sequential initialiser's rank-collapse test).  One wave per row; m <= 16.
+__global__ __launch_bounds__(256) void ppls_deflated_ssq_kernel(const double* __restrict__ X, int64_t n,
+                                                                int ld, int p, const double* __restrict__ Wd,
+                                                                int m, double* __restrict__ part) {
+  __shared__ double sh[4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  double acc = 0.0;
+  for (int64_t row = (int64_t)blockIdx.x * 4 + wave; row < n; row += (int64_t)gridDim.x * 4) {
+    const double* x = X + row * ld;
+    double d[16];
+    for (int j = 0; j < m; ++j) {   // x P_0 .. P_{m-1}: apply P_0 first
+      double s = 0.0;
+      for (int i = lane; i < p; i += 64) {
+        double v = x[i];
+        for (int l = 0; l < j; ++l) v -= d[l] * Wd[(int64_t)l * p + i];
+        s = fma(v, Wd[(int64_t)j * p + i], s);
+      }
+      d[j] = ppls_wave_sum(s);
+    }
+    double s = 0.0;
+    for (int i = lane; i < p; i += 64) {
+      double v = x[i];
+      for (int l = 0; l < m; ++l) v -= d[l] * Wd[(int64_t)l * p + i];
+      s = fma(v, v, s);
+    }
+    acc += ppls_wave_sum(s);
+  }
+  if (lane == 0) sh[wave] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = (sh[0] + sh[1]) + (sh[2] + sh[3]);
+}
+
 // Sum of squares of a contiguous buffer; per-block partials (deterministic two-stage).
 __global__ void ppls_sumsq_partial_kernel(const double* __restrict__ a, int64_t len,
                                           double* __restrict__ part) {
@@ -2008,6 +2042,14 @@ hipError_t ppls_launch_sumsq(const double* a, int64_t len, double* part, int nbl
   hipLaunchKernelGGL(ppls_sumsq_partial_kernel, dim3(nblocks), dim3(256), 0, st, a, len, part);
   hipLaunchKernelGGL(ppls_reduce_partials_kernel, dim3(1), dim3(64), 0, st, part, nblocks, 1, 1, out,
                      out_accumulate);
+  return hipGetLastError();
+}
+
+hipError_t ppls_launch_deflated_ssq(const double* X, int64_t n, int ld, int p, const double* Wd, int m,
+                                    double* part, int nblocks, double* out, hipStream_t st) {
+  if (m < 0 || m > 16) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(ppls_deflated_ssq_kernel, dim3(nblocks), dim3(256), 0, st, X, n, ld, p, Wd, m, part);
+  hipLaunchKernelGGL(ppls_reduce_partials_kernel, dim3(1), dim3(64), 0, st, part, nblocks, 1, 1, out, 0);
   return hipGetLastError();
 }
 

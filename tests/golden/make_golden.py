@@ -27,8 +27,42 @@ CASES = [
 ]
 
 
+# sequential initialiser PPLS(X, Y, a, EMsteps, atol, initialGuess) and the PPLS_simult run it seeds
+SEQ_CASES = [
+    # name, n, p, q, a, EMsteps, atol, initialGuess, seed (data) , init seed ('random')
+    ("seq_equal_n200_p30_q25_a3", 200, 30, 25, 3, 20, 1e-4, "equal", 11, None),
+    ("seq_random_n240_p36_q20_a2", 240, 36, 20, 2, 20, 1e-4, "random", 12, 99),
+    ("seq_equal_atol_n150_p16_q12_a2", 150, 16, 12, 2, 100, 1e-2, "equal", 13, None),
+]
+
+
+def seq_fixtures(here):
+    for name, n, p, q, a, steps, atol, kind, seed, iseed in SEQ_CASES:
+        X, Y, _ = make_problem(n, p, q, a, seed=seed)
+        rng = np.random.default_rng(iseed) if iseed is not None else None
+        inits = [o.initial_guess(p, q, kind, rng) for _ in range(a)]
+        f = o.ppls(X, Y, a, steps, atol, inits)
+        oo = f["Other_output"]
+        lv = np.full((a, steps + 1), np.nan)
+        for k, v in enumerate(oo["logvalue"]):
+            lv[k, :len(v)] = v
+        sim = o.ppls_simult(X, Y, a, EMsteps=10, atol=1e-4, theta0=o.simult_theta0_from_ppls(f))
+        meta = dict(n=n, p=p, q=q, a=a, EMsteps=steps, atol=atol, initialGuess=kind, seed=seed,
+                    init_seed=iseed)
+        np.savez_compressed(
+            os.path.join(here, name + ".npz"), meta=json.dumps(meta), X=X, Y=Y,
+            init_W=np.stack([t["W"] for t in inits], 1), init_C=np.stack([t["C"] for t in inits], 1),
+            init_s=np.array([[t["B"], t["sigE"], t["sigF"], t["sigH"], t["sigT"]] for t in inits]),
+            W=f["W"], C=f["C"], B=f["B"], sig=f["sig"], logvalue=lv,
+            last_increment=np.array(oo["Last_increment"]), number_steps=np.array(oo["Number_steps"]),
+            loglikelihoods=np.array(oo["Loglikelihoods"]), simult_loglik=sim["loglik"],
+            simult_W=sim["estimates"]["W"], simult_C=sim["estimates"]["C"])
+        print(name, "steps", oo["Number_steps"], "logliks", oo["Loglikelihoods"])
+
+
 def main():
     here = os.path.dirname(os.path.abspath(__file__))
+    seq_fixtures(here)
     for name, n, p, q, r, steps, atol, typ, seed in CASES:
         X, Y, th0 = make_problem(n, p, q, r, seed=seed)
         res = o.ppls_simult(X, Y, r, EMsteps=steps, atol=atol, type=typ, theta0=th0)

@@ -1,9 +1,13 @@
 """The CPU oracle pinned against the reference's own known-answer checks (no GPU)."""
+import os
+
 import numpy as np
 import pytest
 
 from conftest import make_problem
 from oracle import ppls_oracle as o
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 
 @pytest.mark.parametrize("r", [1, 2, 3])
@@ -67,7 +71,7 @@ def test_golden_fixtures_reproduce():
     import json, os
     here = os.path.join(os.path.dirname(__file__), "golden")
     for name in sorted(os.listdir(here)):
-        if not name.endswith(".npz"):
+        if not name.endswith(".npz") or name.startswith("seq_"):
             continue
         g = np.load(os.path.join(here, name))
         meta = json.loads(str(g["meta"]))
@@ -77,3 +81,59 @@ def test_golden_fixtures_reproduce():
                             theta0=th0, type=meta["type"])
         assert np.allclose(res["loglik"], g["loglik"], rtol=1e-12, atol=0), name
         assert np.allclose(res["estimates"]["W"], g["W"], atol=1e-10), name
+
+
+# ----------------------------------------------------------------------------- sequential initialiser
+
+def test_emstepc_fast_equals_expect_m_rank1():
+    """EMstepC_fast (loglC.cpp:340-397) and the closed-form Expect_M (EM_W_multi.R:668-716) are two
+    independent statements of the same rank-1 E-step: they must agree (abs() masks inactive)."""
+    X, Y, _ = make_problem(180, 12, 9, 1, seed=21)
+    rng = np.random.default_rng(2)
+    w = rng.standard_normal(12); w /= np.linalg.norm(w)
+    c = rng.standard_normal(9); c /= np.linalg.norm(c)
+    B, sE, sF, sH, sT = 0.8, 0.7, 0.6, 0.4, 1.1
+    f = o.emstep_w(X, Y, w, c, B, sE, sF, sH, sT)
+    e = o.expect_m(X, Y, w[:, None], c[:, None], np.array([[B]]), sE, sF, sH, np.array([[sT]]))
+    for k in ("Ctt", "Cuu", "Cut", "Cee", "Cff", "Chh"):
+        assert np.isclose(f[k], np.ravel(e[k])[0], rtol=1e-12, atol=0), k
+    assert np.allclose(f["mu_T"], e["mu_T"][:, 0], rtol=1e-12, atol=1e-12)
+    m = o.maximiz_m(e, X, Y)
+    assert np.allclose(f["W"], m["W"][:, 0], atol=1e-13)    # orth(v) of a vector = v / ||v||
+
+
+def test_implicit_deflation_equals_explicit():
+    """The device path never forms Xc = X (I - w1 w1'): its sweep uses the weight P w on X and
+    projects X' mu_T.  Check that algebra against the explicit deflation of EM_W_multi.R:270-271."""
+    X, Y, _ = make_problem(160, 14, 11, 2, seed=22)
+    f1 = o.pplsi(X, Y, 20, 1e-4, o.initial_guess(14, 11, "equal"))
+    w1, c1 = f1["W"], f1["C"]
+    Xc = X - np.outer(X @ w1, w1)
+    Yc = Y - np.outer(Y @ c1, c1)
+    th = o.initial_guess(14, 11, "random", np.random.default_rng(5))
+    ref = o.emstep_w(Xc, Yc, th["W"], th["C"], th["B"], th["sigE"], th["sigF"], th["sigH"], th["sigT"])
+    Pw = th["W"] - w1 * (w1 @ th["W"])
+    Pc = th["C"] - c1 * (c1 @ th["C"])
+    assert np.allclose(Xc @ th["W"], X @ Pw, atol=1e-12)
+    # X'mu_T projected == Xc'mu_T ; ||Xc||^2 == ||X||^2 - ||Xc w1||^2
+    mu = ref["mu_T"]
+    SX = X.T @ mu
+    assert np.allclose(SX - w1 * (w1 @ SX), Xc.T @ mu, atol=1e-10)
+    assert np.isclose(o.ssq(Xc), o.ssq(X) - np.sum((X @ w1) ** 2), rtol=1e-12)
+
+
+def test_ppls_loadings_orthonormal_and_golden_reproduced():
+    import json
+    for name in ("seq_equal_n200_p30_q25_a3", "seq_random_n240_p36_q20_a2", "seq_equal_atol_n150_p16_q12_a2"):
+        g = np.load(os.path.join(GOLDEN, name + ".npz"))
+        meta = json.loads(str(g["meta"]))
+        a = meta["a"]
+        inits = [dict(W=g["init_W"][:, k], C=g["init_C"][:, k], B=g["init_s"][k, 0], sigE=g["init_s"][k, 1],
+                      sigF=g["init_s"][k, 2], sigH=g["init_s"][k, 3], sigT=g["init_s"][k, 4]) for k in range(a)]
+        f = o.ppls(g["X"], g["Y"], a, meta["EMsteps"], meta["atol"], inits)
+        assert np.array_equal(f["W"], g["W"]) and np.array_equal(f["sig"], g["sig"])
+        assert list(f["Other_output"]["Number_steps"]) == list(g["number_steps"])
+        assert np.allclose(f["W"].T @ f["W"], np.eye(a), atol=1e-12)
+        assert np.allclose(f["C"].T @ f["C"], np.eye(a), atol=1e-12)
+        for lv in f["Other_output"]["logvalue"]:
+            assert np.all(np.diff(lv) > -1e-8 * np.abs(lv[:-1]))      # EM monotone
