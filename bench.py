@@ -24,9 +24,11 @@ sys.path.insert(0, ROOT)
 CONFIGS = {
     "c3": dict(n=1_000_000, p=2000, q=2000, r=5, name="C3: n=1e6, p=q=2000, r=5, fp64 (headline)"),
     "c2": dict(n=100_000, p=1000, q=1000, r=3, name="C2: n=1e5, p=q=1000, r=3, fp64"),
+    "c5": dict(n=500_000, p=10_000, q=500, r=10, name="C5: n=5e5, p=1e4, q=500, r=10 (wide-p omics case)"),
 }
 METRIC = "EM iterations/sec + log-lik rel-err vs CPU ref, n=1e6 p=q=2000 r=5"
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+FP64_PEAK_TF = 78.6     # MI355X fp64 vector (= fp64 MFMA) dense peak, TFLOP/s
 
 
 def polar(M):
@@ -177,11 +179,16 @@ def main():
         avg_kernel_ms = kern_ms / max(launches, 1)
         achieved = info["bytes_per_sweep"] / (avg_kernel_ms * 1e-3) / 1e9 if launches else None
         wl = f"{args.config}_{'dp%d' % world}"
+        # compute side: 2r fp64 FMAs per element (r for the dots, r for the rank-1 update), on
+        # VALU (no fp64 MFMA shape fits r <= 8 better, and its rate equals the VALU rate)
+        flops = 4.0 * (info["bytes_per_sweep"] / 8) * r
+        tflops = flops / (avg_kernel_ms * 1e-3) / 1e12 if launches else None
         roofline = dict(bound="hbm", achieved=achieved, peak=HBM_PEAK_GBS, unit="GB/s",
                         frac=(achieved / HBM_PEAK_GBS) if achieved else None,
                         traffic=load_traffic(wl), kernel=f"ppls_sweep ({info['variant']})",
                         avg_kernel_ms=avg_kernel_ms, bytes_per_launch=info["bytes_per_sweep"],
-                        grid=info["grid"])
+                        grid=info["grid"], fp64_valu_tflops=tflops, fp64_valu_peak_tflops=FP64_PEAK_TF,
+                        fp64_valu_frac=(tflops / FP64_PEAK_TF) if tflops else None)
         out = dict(metric=METRIC, value=its, unit="EM iterations/s", n_gpus=world, steps=args.steps,
                    warmup=args.warmup, ms_per_step=1e3 * dt / args.steps, higher_is_better=True,
                    scaling="strong", vs_baseline=None, dtype="f64",

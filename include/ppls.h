@@ -75,7 +75,7 @@ const char* ppls_strerror(int code);
 int ppls_ctx_create(int device, ppls_ctx** out);
 void ppls_ctx_destroy(ppls_ctx* ctx);
 const char* ppls_last_error(const ppls_ctx* ctx);
-/* keys: "sweep" (0 auto, 1 fused single-pass, 2 generic two-pass), "grid" (workgroups, 0 = auto),
+/* keys: "sweep" (0 auto, 1 fused single-pass, 2 generic two-pass, 3 panel (wide p)), "grid" (workgroups, 0 = auto),
  *       "nt" (sweep loads with the non-temporal cache policy: -1 auto (default: when X, Y exceed
  *             the 256 MB MALL), 0 off, 1 on),
  *       "timing" (N > 0: record HIP events around every N-th sweep launch; 0 off) */

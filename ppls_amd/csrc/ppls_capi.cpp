@@ -61,6 +61,7 @@ struct ppls_ctx {
   int64_t part_ld = 0;
   int part_groups = 0;
   double* Z = nullptr;
+  int z_cols = 0;          // columns allocated in Z (2r two-pass, 4r panel)
   double* mu = nullptr;
   double* loglik = nullptr;
   int loglik_cap = 0;
@@ -173,6 +174,7 @@ int ensure_r(ppls_ctx* c, int r, int max_steps) {
     if ((rc = dalloc(c, &c->coefs, (size_t)5 * r))) return rc;
     dfree(c->part);
     dfree(c->Z);
+    c->z_cols = 0;
     dfree(c->mu);
     c->part_groups = 0;
     c->r_alloc = r;
@@ -299,8 +301,14 @@ int sweep_plan(ppls_ctx* c, int r, PplsSweepArgs* a) {
   memset(a, 0, sizeof *a);
   a->ldx = c->ldx;
   a->ldy = c->ldy;
+  a->p = c->p;
+  a->q = c->q;
   a->r = r;
   a->threads = threads;
+  if (c->sweep_mode == 3) {        // forced panel sweep
+    a->grid = ppls_panel_chunks(c->n_local, c->ldx, c->ldy, c->num_cus);
+    return 4;
+  }
   if (c->sweep_mode != 2 && nsplit > 0 && c->kernel_opt != 2) {
     a->ns = nsplit;
     a->pipe = c->pipe_opt;
@@ -318,6 +326,10 @@ int sweep_plan(ppls_ctx* c, int r, PplsSweepArgs* a) {
     a->grid = grid_of(c);
     return 1;
   }
+  if (c->sweep_mode != 2) {        // wide p / large r: panel sweep (two GEMM-shaped passes)
+    a->grid = ppls_panel_chunks(c->n_local, c->ldx, c->ldy, c->num_cus);
+    return 4;
+  }
   a->grid = grid_of(c);
   return 2;
 }
@@ -331,8 +343,14 @@ int sweep(ppls_ctx* c, int r, int slot, bool write_mu) {
   if ((rc = ensure_part(c, groups))) return rc;
   if (write_mu && !c->mu)
     if ((rc = dalloc(c, &c->mu, (size_t)std::max<int64_t>(c->n_local, 1) * 2 * r))) return rc;
-  if (plan == 2 && !c->Z)
-    if ((rc = dalloc(c, &c->Z, (size_t)std::max<int64_t>(c->n_local, 1) * 2 * r))) return rc;
+  if ((plan == 2 || plan == 4) && c->z_cols < (plan == 4 ? 4 : 2) * r) {
+    dfree(c->Z);
+    c->z_cols = 0;
+    const size_t len = plan == 4 ? (size_t)ppls_panel_z_len(c->n_local, c->ldx, c->ldy, r)
+                                 : (size_t)std::max<int64_t>(c->n_local, 1) * 2 * r;
+    if ((rc = dalloc(c, &c->Z, len))) return rc;
+    c->z_cols = (plan == 4 ? 4 : 2) * r;
+  }
   if (c->n_local == 0) {
     HIPCHK(c, hipMemsetAsync(c->stats, 0, sizeof(double) * c->part_ld, c->stream));
   } else {
@@ -367,6 +385,7 @@ int sweep(ppls_ctx* c, int r, int slot, bool write_mu) {
     }
     if (plan == 3) HIPCHK(c, ppls_launch_sweep_split(&a, c->stream));
     else if (plan == 1) HIPCHK(c, ppls_launch_sweep_fused(&a, c->stream));
+    else if (plan == 4) HIPCHK(c, ppls_launch_sweep_panel(&a, 0, c->Z, a.grid, c->stream));
     else HIPCHK(c, ppls_launch_sweep_twopass(&a, c->Z, c->stream));
     if (timed) HIPCHK(c, hipEventRecord(e1, c->stream));
     HIPCHK(c, ppls_launch_reduce2(c->part, groups, c->part_ld, c->part_ld, c->stats,
@@ -444,6 +463,7 @@ int alloc_data(ppls_ctx* c, int64_t n_local, int p, int q, int64_t n_total) {
   c->r_alloc = 0;   // force per-r buffers to be re-sized for the new shape
   dfree(c->part);
   dfree(c->Z);
+  c->z_cols = 0;
   dfree(c->mu);
   c->part_groups = 0;
   c->have_data = false;
@@ -563,6 +583,7 @@ void ppls_ctx_destroy(ppls_ctx* c) {
   for (int i = 0; i < 2; ++i) { dfree(c->W[i]); dfree(c->C[i]); dfree(c->sc[i]); dfree(c->gram[i]); }
   dfree(c->vstate);
   dfree(c->mom); dfree(c->stats); dfree(c->part); dfree(c->Z); dfree(c->mu); dfree(c->loglik);
+  c->z_cols = 0;
   dfree(c->work); dfree(c->status); dfree(c->coefs); dfree(c->scratch);
   if (c->ftrace) (void)hipFree(c->ftrace);
   for (auto& e : c->ev) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
@@ -575,7 +596,7 @@ const char* ppls_last_error(const ppls_ctx* c) { return c ? c->err.c_str() : "nu
 int ppls_set_option(ppls_ctx* c, const char* key, int64_t value) {
   if (!c || !key) return PPLS_E_ARG;
   if (!strcmp(key, "sweep")) {
-    if (value < 0 || value > 2) return fail(c, PPLS_E_ARG, "sweep must be 0, 1 or 2");
+    if (value < 0 || value > 3) return fail(c, PPLS_E_ARG, "sweep must be 0 (auto), 1 (fused), 2 (two-pass) or 3 (panel)");
     c->sweep_mode = (int)value;
   } else if (!strcmp(key, "grid")) {
     if (value < 0 || value > 65535) return fail(c, PPLS_E_ARG, "grid out of range");
@@ -785,7 +806,11 @@ int ppls_mstep(ppls_ctx* c, const ppls_expect* fit, int r, int type, ppls_theta*
   const int grid = grid_of(c);
   const int groups = ppls_twopass_groups(std::max<int64_t>(c->n_local, 1), grid);
   if ((rc = ensure_part(c, groups))) return rc;
-  if (!c->Z && (rc = dalloc(c, &c->Z, (size_t)std::max<int64_t>(c->n_local, 1) * 2 * r))) return rc;
+  if (c->z_cols < 2 * r) {
+    dfree(c->Z);
+    c->z_cols = 2 * r;
+    if ((rc = dalloc(c, &c->Z, (size_t)std::max<int64_t>(c->n_local, 1) * 2 * r))) return rc;
+  }
   // Z = [mu_T | mu_U] row-major, coefficients alpha = delta = 1, beta = gamma = 0:
   // the accumulate pass then computes exactly X'mu_T and Y'mu_U (EM_W_multi.R:732-733).
   PplsScalars s;
@@ -1270,7 +1295,7 @@ int ppls_sweep_info(ppls_ctx* c, int r, int64_t* bytes_per_sweep, int* variant, 
   PplsSweepArgs a;
   const int plan = sweep_plan(c, r, &a);
   if (bytes_per_sweep) *bytes_per_sweep = (int64_t)8 * c->n_local * ((int64_t)c->p + c->q);
-  if (variant) *variant = plan == 3 ? 4 : plan == 1 ? (a.threads == 1024 ? 3 : 1) : 2;
+  if (variant) *variant = plan == 4 ? 5 : plan == 3 ? 4 : plan == 1 ? (a.threads == 1024 ? 3 : 1) : 2;
   if (grid) *grid = a.grid;
   return PPLS_OK;
 }

@@ -14,6 +14,7 @@ struct PplsSweepArgs {
   const double* X;
   const double* Y;
   int64_t n_local;
+  int p, q;               // columns of X, Y (ldx, ldy include padding)
   int ldx, ldy;          // leading dimensions (doubles, even)
   const double* Wp;      // ldx x r column-major (padded rows are 0)
   const double* Cp;      // ldy x r
@@ -65,6 +66,10 @@ hipError_t ppls_launch_sweep_split(const PplsSweepArgs* a, hipStream_t st);
 hipError_t ppls_launch_sweep_twopass(const PplsSweepArgs* a, double* Z, hipStream_t st);
 hipError_t ppls_launch_accumulate(const PplsSweepArgs* a, const double* Z, hipStream_t st);
 int ppls_twopass_groups(int64_t n_local, int grid);
+// Wide-p panel sweep (two GEMM-shaped passes); Z: n_local x 4r doubles; chunks = partial groups.
+int ppls_panel_chunks(int64_t n_local, int ldx, int ldy, int num_cus);
+int64_t ppls_panel_z_len(int64_t n_local, int ldx, int ldy, int r);   // doubles of Z (+ transposed W, C)
+hipError_t ppls_launch_sweep_panel(const PplsSweepArgs* a, int dtype_f32, double* Z, int chunks, hipStream_t st);
 hipError_t ppls_launch_reduce(const double* part, int ngroups, int64_t ld, int64_t len, double* out,
                               int accumulate, hipStream_t st);
 hipError_t ppls_launch_finalize(const PplsFinalizeArgs* f, hipStream_t st);

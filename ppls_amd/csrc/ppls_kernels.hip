@@ -885,6 +885,228 @@ __global__ __launch_bounds__(256) void ppls_acc_kernel(
   }
 }
 
+// ============================================================================ panel sweep (wide p)
+// When p r is too large for per-thread column ownership (C5: p = 1e4, r = 10 -> 1e5 accumulators
+// per matrix), the sweep is two GEMM-shaped passes over X and Y:
+//   dots: Z_i = [x_i W | y_i C | mu_T,i | mu_U,i] (n x 4R fp64) -- 64-row tiles per workgroup,
+//         W staged transposed in LDS, 16-B coalesced loads of X, fp64 FMA, 16-lane DPP sums;
+//   acc : [X' mu_T | Y' mu_U] partials per row chunk -- each thread owns one 16-B column vector
+//         with R fp64 accumulators per element and streams the chunk's rows; mu_T / mu_U are
+//         wave-uniform (scalar loads); the first column tile also accumulates the 2R x 2R Gram
+//         of [Xw Yc].
+// T is the storage type of X, Y (double or float); arithmetic is fp64.  Algorithmic bytes:
+// 2 sizeof(T) n (p + q) (two HBM passes) + 64 R n (Z written and read twice).
+__device__ __forceinline__ double ppls_group16_sum(double v) {
+  v += ppls_dpp_partner<5>(v);   // quad xor 1
+  v += ppls_dpp_partner<4>(v);   // quad xor 2
+  v += ppls_dpp_partner<3>(v);   // half-row mirror: lane l <-> 7 - l
+  v += ppls_dpp_partner<2>(v);   // row mirror: lane l <-> 15 - l
+  return v;
+}
+
+template <typename T>
+struct PplsVec16 {   // one 16-B load of T
+  static constexpr int N = 16 / sizeof(T);
+  T v[N];
+};
+
+template <typename T>
+__device__ __forceinline__ PplsVec16<T> ppls_load16(const T* p) {
+  PplsVec16<T> r;
+  if constexpr (sizeof(T) == 8) {
+    const double2 d = *(const double2*)p;
+    r.v[0] = d.x;
+    r.v[1] = d.y;
+  } else {
+    const float4 f = *(const float4*)p;
+    r.v[0] = f.x;
+    r.v[1] = f.y;
+    r.v[2] = f.z;
+    r.v[3] = f.w;
+  }
+  return r;
+}
+
+#define PPLS_PANEL_ROWS 64
+
+// Wt, Ct: W, C transposed to row-major [ld x R] (ppls_transpose_wc_kernel), so a column's R
+// weights are contiguous; they are read straight from L1/L2 (W is 8 p R bytes, resident) -- no LDS
+// staging and no barrier in the column loop, so the X loads of consecutive steps overlap.
+template <typename T, int R>
+__global__ __launch_bounds__(256) void ppls_panel_dots_kernel(
+    const T* __restrict__ X, const T* __restrict__ Y, int64_t n, int ldx, int ldy,
+    const double* __restrict__ Wt, const double* __restrict__ Ct, const PplsScalars* __restrict__ sc,
+    double* __restrict__ Z, double* __restrict__ mu) {
+  constexpr int VEC = PplsVec16<T>::N;
+  constexpr int RT = 4, CL = 16, ROWS = PPLS_PANEL_ROWS;   // 16 row groups x 4 rows
+  constexpr int KS = CL * VEC;                             // columns per step
+  constexpr int V4 = 4 * R;
+  __shared__ double sZ[ROWS * 2 * R];
+  __shared__ double sco[4 * R];
+  const int tid = threadIdx.x, cl = tid % CL, rg = tid / CL;
+  for (int e = tid; e < R; e += 256) {
+    sco[e] = sc->alpha[e];
+    sco[R + e] = sc->beta[e];
+    sco[2 * R + e] = sc->gamma[e];
+    sco[3 * R + e] = sc->delta[e];
+  }
+  for (int64_t tile = blockIdx.x; tile * ROWS < n; tile += gridDim.x) {
+    const int64_t rbase = tile * ROWS + rg * RT;
+    for (int mat = 0; mat < 2; ++mat) {
+      const T* M = mat ? Y : X;
+      const int ld = mat ? ldy : ldx;
+      const double* Wm = mat ? Ct : Wt;
+      const T* rows[RT];
+      bool ok[RT];
+#pragma unroll
+      for (int j = 0; j < RT; ++j) {
+        ok[j] = rbase + j < n;
+        rows[j] = M + (ok[j] ? rbase + j : 0) * ld;
+      }
+      double acc[RT][R];
+#pragma unroll
+      for (int j = 0; j < RT; ++j)
+#pragma unroll
+        for (int k = 0; k < R; ++k) acc[j][k] = 0.0;
+#pragma unroll 2
+      for (int c0 = cl * VEC; c0 < ld; c0 += KS) {   // ld is a multiple of VEC (zero padding)
+        PplsVec16<T> xv[RT];
+#pragma unroll
+        for (int j = 0; j < RT; ++j) xv[j] = ppls_load16(rows[j] + c0);
+#pragma unroll
+        for (int v = 0; v < VEC; ++v) {
+          const double* wr = Wm + (int64_t)(c0 + v) * R;
+          double w[R];
+#pragma unroll
+          for (int k = 0; k < R; ++k) w[k] = wr[k];
+#pragma unroll
+          for (int j = 0; j < RT; ++j) {
+            const double x = ok[j] ? (double)xv[j].v[v] : 0.0;
+#pragma unroll
+            for (int k = 0; k < R; ++k) acc[j][k] = fma(x, w[k], acc[j][k]);
+          }
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < RT; ++j)
+#pragma unroll
+        for (int k = 0; k < R; ++k) acc[j][k] = ppls_group16_sum(acc[j][k]);
+      if (cl == 0)
+#pragma unroll
+        for (int j = 0; j < RT; ++j)
+#pragma unroll
+          for (int k = 0; k < R; ++k) sZ[(rg * RT + j) * 2 * R + mat * R + k] = acc[j][k];
+    }
+    __syncthreads();
+    for (int e = tid; e < ROWS * V4; e += 256) {   // Z rows [a | b | mu_T | mu_U], coalesced
+      const int rr = e / V4, f = e - rr * V4;
+      const int64_t row = tile * ROWS + rr;
+      if (row >= n) continue;
+      double val;
+      if (f < 2 * R) {
+        val = sZ[rr * 2 * R + f];
+      } else {
+        const int k = (f - 2 * R) % R, u = f >= 3 * R;
+        const double a = sZ[rr * 2 * R + k], b = sZ[rr * 2 * R + R + k];
+        val = u ? sco[2 * R + k] * a + sco[3 * R + k] * b : sco[k] * a + sco[R + k] * b;
+        if (mu) mu[(int64_t)(u * R + k) * n + row] = val;
+      }
+      Z[row * V4 + f] = val;
+    }
+    __syncthreads();
+  }
+}
+
+// W (ldx x R, column-major) -> Wt (ldx x R, row-major); same for C.
+__global__ void ppls_transpose_wc_kernel(const double* __restrict__ W, const double* __restrict__ C,
+                                         int ldx, int ldy, int r, double* __restrict__ Wt,
+                                         double* __restrict__ Ct) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t nx = (int64_t)ldx * r;
+  if (e < nx) {
+    const int i = (int)(e / r), k = (int)(e % r);
+    Wt[e] = W[(int64_t)k * ldx + i];
+  } else if (e < nx + (int64_t)ldy * r) {
+    const int64_t f = e - nx;
+    const int i = (int)(f / r), k = (int)(f % r);
+    Ct[f] = C[(int64_t)k * ldy + i];
+  }
+}
+
+template <typename T, int R>
+__global__ __launch_bounds__(256) void ppls_panel_acc_kernel(
+    const T* __restrict__ X, const T* __restrict__ Y, int64_t n, int ldx, int ldy,
+    const double* __restrict__ Z, int64_t rows_per_chunk, double* __restrict__ part, int64_t part_ld) {
+  constexpr int VEC = PplsVec16<T>::N;
+  constexpr int V4 = 4 * R;
+  const int tid = threadIdx.x;
+  const int ntx = (ldx + 256 * VEC - 1) / (256 * VEC);
+  const bool isx = (int)blockIdx.x < ntx;
+  const int col = (isx ? blockIdx.x : blockIdx.x - ntx) * 256 * VEC + tid * VEC;
+  const int ld = isx ? ldx : ldy;
+  const T* M = isx ? X : Y;
+  const int off = isx ? 2 * R : 3 * R;
+  const int64_t r0 = (int64_t)blockIdx.y * rows_per_chunk;
+  const int64_t r1 = min(n, r0 + rows_per_chunk);
+  double* pg = part + (int64_t)blockIdx.y * part_ld;
+  if (col < ld) {
+    double acc[VEC][R];
+#pragma unroll
+    for (int v = 0; v < VEC; ++v)
+#pragma unroll
+      for (int k = 0; k < R; ++k) acc[v][k] = 0.0;
+#pragma unroll 8
+    for (int64_t row = r0; row < r1; ++row) {
+      const PplsVec16<T> xv = ppls_load16(M + row * ld + col);
+      const double* zr = Z + row * V4 + off;   // wave-uniform
+#pragma unroll
+      for (int k = 0; k < R; ++k) {
+        const double m = zr[k];
+#pragma unroll
+        for (int v = 0; v < VEC; ++v) acc[v][k] = fma((double)xv.v[v], m, acc[v][k]);
+      }
+    }
+    double* dst = isx ? pg : pg + (int64_t)R * ldx;
+#pragma unroll
+    for (int k = 0; k < R; ++k)
+#pragma unroll
+      for (int v = 0; v < VEC; ++v) dst[(int64_t)k * ld + col + v] = acc[v][k];
+  }
+  if (blockIdx.x == 0) {   // Gram of [Xw Yc] over the chunk (2R x 2R, column-major)
+    constexpr int V2 = 2 * R, NP = V2 * (V2 + 1) / 2, BR = 64;
+    __shared__ double sz[BR * V2];
+    double* G2 = pg + (int64_t)R * ldx + (int64_t)R * ldy;
+    double gs[(NP + 255) / 256];
+    int pi[(NP + 255) / 256], pj[(NP + 255) / 256];
+#pragma unroll
+    for (int u = 0; u < (NP + 255) / 256; ++u) {
+      gs[u] = 0.0;
+      int e = tid + 256 * u, i = 0;   // packed upper triangle: e -> (i <= j)
+      while (e >= V2 - i && i < V2) { e -= V2 - i; ++i; }
+      pi[u] = i;
+      pj[u] = i + e;
+    }
+    for (int64_t b0 = r0; b0 < r1; b0 += BR) {   // stage BR rows of [a | b], then sum from LDS
+      __syncthreads();
+      for (int e = tid; e < BR * V2; e += 256) {
+        const int rr = e / V2, f = e - rr * V2;
+        sz[e] = (b0 + rr < r1) ? Z[(b0 + rr) * V4 + f] : 0.0;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int u = 0; u < (NP + 255) / 256; ++u)
+        if (tid + 256 * u < NP)
+          for (int rr = 0; rr < BR; ++rr) gs[u] = fma(sz[rr * V2 + pi[u]], sz[rr * V2 + pj[u]], gs[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < (NP + 255) / 256; ++u)
+      if (tid + 256 * u < NP) {
+        G2[pj[u] * V2 + pi[u]] = gs[u];
+        G2[pi[u] * V2 + pj[u]] = gs[u];
+      }
+  }
+}
+
 // ============================================================================ finalize
 // Block-wide sum of nv values per thread (blockDim.x <= 1024); result broadcast to all threads.
 __device__ void ppls_block_sum(double* vals, int nv, double* sh) {
@@ -1233,42 +1455,130 @@ __device__ __forceinline__ void ppls_rr_pair(int m, int k, int& i, int& j) {
   j = pa < pb ? pb : pa;
 }
 
-// One-sided Jacobi on one wave: A V = U Sigma with A, V in LDS as 8 x 8 column blocks
-// (element (row t, col c) at [c * 8 + t], rows >= R zero).  Round m of a sweep rotates the N/2
-// disjoint pairs of the circle-method schedule at once: lane group k = lane / 8 owns pair k, lane
-// t = lane % 8 owns row t, the column dots are 8-lane DPP sums.  Same rotation and stopping rule
-// as ppls_jacobi_reg / ppls_small_polar_n.  Wave-uniform; all 64 lanes of the wave must call.
+// Small dense algebra on one wave with R x R matrices in LDS as G x G column blocks
+// (element (row t, col c) at [c * G + t], G = 8 for R <= 8 else 16, rows >= R zero).  All 64
+// lanes of the wave must call (DPP sums); results are wave-uniform.
+template <int R>
+struct PplsWaveBlk {
+  static constexpr int G = R <= 8 ? 8 : 16;
+  static constexpr int SZ = G * G;
+};
+
+template <int G>
+__device__ __forceinline__ double ppls_groupG_sum(double v) {
+  if constexpr (G == 8) return ppls_group8_sum(v);
+  else return ppls_group16_sum(v);
+}
+
+// Upper Cholesky G = U'U (right-looking, lane-parallel updates); ok = false if a pivot <= 0.
+// sW: G x G scratch (destroyed); sU receives U (zero below the diagonal).
+template <int R>
+__device__ bool ppls_chol_wave(double* sW, double* sU) {
+  constexpr int G = PplsWaveBlk<R>::G;
+  const int lane = threadIdx.x & 63;
+  bool ok = true;
+  for (int e = lane; e < G * G; e += 64) sU[e] = 0.0;
+  ppls_wave_lds_fence();
+  for (int j = 0; j < R; ++j) {
+    const double piv = sW[j * G + j];
+    ok = ok && (piv > 0.0);
+    const double d = sqrt(piv > 0.0 ? piv : 1.0);
+    const double di = 1.0 / d;
+    if (lane == 0) sU[j * G + j] = d;
+    if (lane > j && lane < R) sU[lane * G + j] = sW[lane * G + j] * di;   // U[j][lane]
+    ppls_wave_lds_fence();
+    for (int e = lane; e < G * G; e += 64) {   // W[a][b] -= U[j][a] U[j][b], j < a, b < R
+      const int a = e % G, b = e / G;
+      if (a > j && b > j && a < R && b < R) sW[b * G + a] -= sU[a * G + j] * sU[b * G + j];
+    }
+    ppls_wave_lds_fence();
+  }
+  return ok;
+}
+
+// sUi = inv(U), U upper triangular: lane c < R back-substitutes column c.
+template <int R>
+__device__ void ppls_inv_upper_wave(const double* sU, double* sUi) {
+  constexpr int G = PplsWaveBlk<R>::G;
+  const int lane = threadIdx.x & 63;
+  for (int e = lane; e < G * G; e += 64) sUi[e] = 0.0;
+  ppls_wave_lds_fence();
+  if (lane < R) {
+    const int c = lane;
+    double col[R];
+#pragma unroll
+    for (int ii = 0; ii < R; ++ii) {
+      const int i = R - 1 - ii;
+      double s = (i == c) ? 1.0 : 0.0;
+#pragma unroll
+      for (int kk = i + 1; kk < R; ++kk) s = fma(-sU[kk * G + i], col[kk], s);
+      col[i] = (i <= c) ? s / sU[i * G + i] : 0.0;
+    }
+#pragma unroll
+    for (int i = 0; i < R; ++i) sUi[c * G + i] = col[i];
+  }
+  ppls_wave_lds_fence();
+}
+
+// sC = op(A) sB with A transposed if TA; entries (a, b) on lanes.
+template <int R, bool TA>
+__device__ void ppls_matmul_wave(const double* sA, const double* sB, double* sC) {
+  constexpr int G = PplsWaveBlk<R>::G;
+  const int lane = threadIdx.x & 63;
+  for (int e = lane; e < G * G; e += 64) {
+    const int a = e % G, b = e / G;
+    double s = 0.0;
+    if (a < R && b < R)
+#pragma unroll
+      for (int kk = 0; kk < R; ++kk) s = fma(TA ? sA[a * G + kk] : sA[kk * G + a], sB[b * G + kk], s);
+    sC[e] = s;
+  }
+  ppls_wave_lds_fence();
+}
+
+// One-sided Jacobi on one wave: A V = U Sigma with A, V in LDS (G x G blocks).  Round m of a
+// sweep rotates the N/2 disjoint pairs of the circle-method schedule: lane group g = lane / G owns
+// pair g (+ 64/G per pass), lane t = lane % G owns row t, the column dots are G-lane DPP sums.
+// Same rotation and stopping rule as ppls_jacobi_reg / ppls_small_polar_n.  Wave-uniform.
 template <int R>
 __device__ int ppls_jacobi_wave(double* sA, double* sV) {
   constexpr int N = R + (R & 1);
-  const int lane = threadIdx.x & 63, k = lane >> 3, t = lane & 7;
-  const bool grp = k < N / 2;
+  constexpr int G = PplsWaveBlk<R>::G;
+  constexpr int PPW = 64 / G;                       // pairs per pass
+  constexpr int PASSES = (N / 2 + PPW - 1) / PPW;
+  const int lane = threadIdx.x & 63, t = lane % G;
   int sweeps = 0;
   for (int sweep = 0; sweep < 60; ++sweep) {
     ++sweeps;
     bool rot_any = false;
 #pragma unroll
     for (int m = 0; m < N - 1; ++m) {
-      int i, j;
-      ppls_rr_pair<R>(m, grp ? k : 0, i, j);
-      const bool act = grp && j < R;
-      const int ci = (act ? i : 0) * 8 + t, cj = (act ? j : 1) * 8 + t;
-      const double x = sA[ci], y = sA[cj], vx = sV[ci], vy = sV[cj];
-      const double a = ppls_group8_sum(x * x), b = ppls_group8_sum(y * y), g = ppls_group8_sum(x * y);
-      const bool rot = act && (g * g >= 1e-30 * (a * b)) && g != 0.0;
-      const double z = (b - a) * ppls_rcp(rot ? 2.0 * g : 1.0);
-      const double z2 = fma(z, z, 1.0);
-      const double u = fabs(z) + z2 * ppls_rsq(z2);
-      const double w = ppls_rsq(fma(u, u, 1.0));
-      const double c = u * w, sn = z >= 0.0 ? w : -w;
-      if (rot) {
-        sA[ci] = fma(c, x, -sn * y);
-        sA[cj] = fma(sn, x, c * y);
-        sV[ci] = fma(c, vx, -sn * vy);
-        sV[cj] = fma(sn, vx, c * vy);
+#pragma unroll
+      for (int ps = 0; ps < PASSES; ++ps) {
+        const int k = ps * PPW + lane / G;
+        const bool grp = k < N / 2;
+        int i, j;
+        ppls_rr_pair<R>(m, grp ? k : 0, i, j);
+        const bool act = grp && j < R;
+        const int ci = (act ? i : 0) * G + t, cj = (act ? j : 1) * G + t;
+        const double x = sA[ci], y = sA[cj], vx = sV[ci], vy = sV[cj];
+        const double a = ppls_groupG_sum<G>(x * x), b = ppls_groupG_sum<G>(y * y);
+        const double g = ppls_groupG_sum<G>(x * y);
+        const bool rot = act && (g * g >= 1e-30 * (a * b)) && g != 0.0;
+        const double z = (b - a) * ppls_rcp(rot ? 2.0 * g : 1.0);
+        const double z2 = fma(z, z, 1.0);
+        const double u = fabs(z) + z2 * ppls_rsq(z2);
+        const double w = ppls_rsq(fma(u, u, 1.0));
+        const double c = u * w, sn = z >= 0.0 ? w : -w;
+        if (rot) {
+          sA[ci] = fma(c, x, -sn * y);
+          sA[cj] = fma(sn, x, c * y);
+          sV[ci] = fma(c, vx, -sn * vy);
+          sV[cj] = fma(sn, vx, c * vy);
+        }
+        rot_any = rot_any || rot;
+        ppls_wave_lds_fence();
       }
-      rot_any = rot_any || rot;
-      ppls_wave_lds_fence();
     }
     if (!__any(rot_any)) break;
   }
@@ -1281,9 +1591,9 @@ __device__ int ppls_jacobi_wave(double* sA, double* sV) {
 // left factor is never formed and no triangular inverse is applied to S).  Three block passes
 // over S: the first stages S into LDS (Sl, p*R doubles; nullptr = re-read from global); the last
 // writes out = S F, F = V Sigma^-1 V', and, if gram_out != nullptr, the Gram out'out the next
-// iteration's scalar update needs.  The Jacobi is warm-started from vstate (the previous
-// iteration's V; nullptr = identity) and runs lane-parallel on wave 0.  sm: >= 2 R^2 doubles of
-// LDS.  Returns false when S is numerically rank deficient (a Cholesky pivot fails or
+// iteration's scalar update needs.  All R x R algebra runs on wave 0 in LDS; the Jacobi is
+// warm-started from vstate (the previous iteration's V; nullptr = identity).  sm: >= 2 R^2
+// doubles of LDS.  Returns false when S is numerically rank deficient (a Cholesky pivot fails or
 // sigma_min < 1e-14 sigma_max); the caller then falls back to Householder (which reports it).
 template <int R, int NT>
 __device__ bool ppls_block_polar_fast(const double* __restrict__ S, int64_t lds, int p,
@@ -1292,19 +1602,23 @@ __device__ bool ppls_block_polar_fast(const double* __restrict__ S, int64_t lds,
                                       double* __restrict__ vstate, long long* tr) {
   constexpr int NG = R * (R + 1) / 2;
   constexpr int NW = NT / 64;
-  static_assert(R <= 8, "8 x 8 LDS blocks");
-  const int tid = threadIdx.x;
-  double* sR1 = sm;           // R1 (upper), later F
-  double* sM = sm + R * R;    // R1^-1
-  __shared__ double sA[64], sV[64], sT[64], ssv[8];
+  constexpr int G = PplsWaveBlk<R>::G, GG = G * G;
+  static_assert(R <= 16 && NG <= 64, "block sums of at most 64 values");
+  const int tid = threadIdx.x, lane = tid & 63;
+  double* sF = sm;            // R x R (column-major, ld R): R1^-1 for pass 2, then F for pass 3
+  __shared__ double sA[GG], sV[GG], sT[GG], sU[GG], ssv[16];
   __shared__ int ok;
+  // the carried V (wave 0), fetched now so its latency hides under pass 1
+  double vprev[(GG + 63) / 64];
+#pragma unroll
+  for (int u = 0; u < (GG + 63) / 64; ++u) {
+    const int e = lane + 64 * u, cb = e / G, rt = e % G;
+    vprev[u] = (cb == rt && cb < R) ? 1.0 : 0.0;
+    if (vstate && tid < 64 && cb < R && rt < R) vprev[u] = vstate[cb * R + rt];
+  }
   double vals[NG];
 #pragma unroll
   for (int e = 0; e < NG; ++e) vals[e] = 0.0;
-  // the carried V (wave 0), fetched now so its latency hides under pass 1
-  const int lane = tid & 63, cb = lane >> 3, rt = lane & 7;
-  double vprev = (cb == rt) ? 1.0 : 0.0;
-  if (vstate && tid < 64 && cb < R && rt < R) vprev = vstate[cb * R + rt];
   // pass 1: G1 = S'S, staging S into LDS; chunks of PU rows per thread with every load of a
   // chunk issued before the first use
   constexpr int PU = R >= 6 ? 4 : 8;
@@ -1328,15 +1642,33 @@ __device__ bool ppls_block_polar_fast(const double* __restrict__ S, int64_t lds,
   }
   ppls_block_sum_t<NG, NW>(vals, sh);
   ppls_stamp(tr, 1);
-  if (tid == 0) {
-    double G[R][R], U[R][R], Ui[R][R], dinv[R];
-    ppls_gram_unpack<R>(vals, G);
-    ok = ppls_chol_reg<R>(G, U, dinv);
-    ppls_inv_upper_reg<R>(U, dinv, Ui);
+  if constexpr (R <= 6) {   // small R: one thread in registers is faster than the wave form
+    if (tid == 0) {
+      double Gm[R][R], U[R][R], Ui[R][R], dinv[R];
+      ppls_gram_unpack<R>(vals, Gm);
+      ok = ppls_chol_reg<R>(Gm, U, dinv);
+      ppls_inv_upper_reg<R>(U, dinv, Ui);
+      for (int e = 0; e < GG; ++e) sT[e] = 0.0;
 #pragma unroll
-    for (int a = 0; a < R; ++a)
+      for (int a = 0; a < R; ++a)
 #pragma unroll
-      for (int b = 0; b < R; ++b) { sR1[a * R + b] = U[a][b]; sM[a * R + b] = Ui[a][b]; }
+        for (int b = 0; b < R; ++b) { sT[b * G + a] = U[a][b]; sF[b * R + a] = Ui[a][b]; }
+    }
+  } else if (tid < 64) {   // R1 = chol(G1) -> sT, R1^-1 -> sF (ld R)
+    for (int e = lane; e < GG; e += 64) {
+      const int a = e % G, b = e / G;
+      double v = 0.0;
+      if (a < R && b < R) {
+        const int lo = a < b ? a : b, hi = a < b ? b : a;
+        v = vals[hi * (hi + 1) / 2 + lo];
+      }
+      sA[e] = v;
+    }
+    ppls_wave_lds_fence();
+    const bool good = ppls_chol_wave<R>(sA, sT);
+    ppls_inv_upper_wave<R>(sT, sU);
+    for (int e = lane; e < R * R; e += 64) sF[e] = sU[(e / R) * G + e % R];
+    if (lane == 0) ok = good;
   }
   __syncthreads();
   ppls_stamp(tr, 2);
@@ -1349,19 +1681,19 @@ __device__ bool ppls_block_polar_fast(const double* __restrict__ S, int64_t lds,
 #pragma unroll
     for (int a = 0; a < R; ++a)
 #pragma unroll
-      for (int b = 0; b < R; ++b) M[a][b] = sM[a * R + b];
+      for (int b = 0; b < R; ++b) M[a][b] = sF[b * R + a];
 #pragma unroll
     for (int e = 0; e < NG; ++e) vals[e] = 0.0;
-#pragma unroll 4
+#pragma unroll 2
     for (int i = tid; i < p; i += NT) {
-      double x[R], qv[R];
+      double xq[R], qv[R];
 #pragma unroll
-      for (int k = 0; k < R; ++k) x[k] = Sr[(int64_t)k * ldr + i];
+      for (int k = 0; k < R; ++k) xq[k] = Sr[(int64_t)k * ldr + i];
 #pragma unroll
       for (int j = 0; j < R; ++j) {
         double s = 0.0;
 #pragma unroll
-        for (int k = 0; k <= j; ++k) s = fma(x[k], M[k][j], s);
+        for (int k = 0; k <= j; ++k) s = fma(xq[k], M[k][j], s);
         qv[j] = s;
       }
       ppls_gram_acc<R>(qv, vals);
@@ -1369,78 +1701,84 @@ __device__ bool ppls_block_polar_fast(const double* __restrict__ S, int64_t lds,
   }
   ppls_block_sum_t<NG, NW>(vals, sh);
   ppls_stamp(tr, 3);
-  if (tid < 64) {   // wave 0: T = R2 R1, warm start, Jacobi, F
-    // V_prev -> sV (8 x 8 block, zero padding)
-    {
-      sV[lane] = (cb < R && rt < R) ? vprev : 0.0;
-      sA[lane] = 0.0;
-      sT[lane] = 0.0;
-    }
-    ppls_wave_lds_fence();
-    if (lane == 0) {
-      double G[R][R], U2[R][R], dinv[R];
-      ppls_gram_unpack<R>(vals, G);
-      ok = ppls_chol_reg<R>(G, U2, dinv);
-#pragma unroll
-      for (int a = 0; a < R; ++a)                 // T = R2 R1 (upper)
-#pragma unroll
-        for (int b = 0; b < R; ++b) {
-          double s = 0.0;
-#pragma unroll
-          for (int k = 0; k < R; ++k) s = fma(U2[a][k], sR1[k * R + b], s);
-          sT[b * 8 + a] = s;
+  if (tid < 64) {   // wave 0: R2 = chol(G2), T = R2 R1, warm start, Jacobi, F
+    for (int e = lane; e < GG; e += 64) {
+      if constexpr (R > 6) {
+        const int a = e % G, b = e / G;
+        double v = 0.0;
+        if (a < R && b < R) {
+          const int lo = a < b ? a : b, hi = a < b ? b : a;
+          v = vals[hi * (hi + 1) / 2 + lo];
         }
+        sA[e] = v;
+      }
+#pragma unroll
+      for (int u = 0; u < (GG + 63) / 64; ++u)
+        if (e == lane + 64 * u) sV[e] = vprev[u];
     }
     ppls_wave_lds_fence();
+    bool good = true;
+    if constexpr (R <= 6) {
+      if (lane == 0) {
+        double Gm[R][R], U2[R][R], dinv[R];
+        ppls_gram_unpack<R>(vals, Gm);
+        good = ppls_chol_reg<R>(Gm, U2, dinv);
+        for (int e = 0; e < GG; ++e) sA[e] = 0.0;
+#pragma unroll
+        for (int a = 0; a < R; ++a)                 // T = R2 R1 (upper)
+#pragma unroll
+          for (int b = 0; b < R; ++b) {
+            double sacc = 0.0;
+#pragma unroll
+            for (int kk = 0; kk < R; ++kk) sacc = fma(U2[a][kk], sT[b * G + kk], sacc);
+            sA[b * G + a] = sacc;
+          }
+      }
+      ppls_wave_lds_fence();
+    } else {
+      good = ppls_chol_wave<R>(sA, sU);                     // sU = R2
+      ppls_matmul_wave<R, false>(sU, sT, sA);               // sA = R2 R1 = T
+    }
     ppls_stamp(tr, 6);
-    // re-orthonormalise the carried V (modified Gram-Schmidt, rows on lanes 0..7)
-    if (vstate) {
-#pragma unroll
+    if (vstate) {   // re-orthonormalise the carried V (modified Gram-Schmidt, rows on lanes)
+      const int rt = lane % G;
       for (int j = 0; j < R; ++j) {
-        double vj = sV[j * 8 + rt];
-#pragma unroll
+        double vj = sV[j * G + rt];
         for (int i = 0; i < j; ++i) {
-          const double vi = sV[i * 8 + rt];
-          vj = fma(-ppls_group8_sum(vi * vj), vi, vj);
+          const double vi = sV[i * G + rt];
+          vj = fma(-ppls_groupG_sum<G>(vi * vj), vi, vj);
         }
-        vj *= ppls_rsq(ppls_group8_sum(vj * vj));
-        if (lane < 8) sV[j * 8 + rt] = vj;
+        vj *= ppls_rsq(ppls_groupG_sum<G>(vj * vj));
+        if (lane < G) sV[j * G + rt] = vj;
         ppls_wave_lds_fence();
       }
     }
-    // A = T V (lane (row rt, col cb))
-    if (cb < R && rt < R) {
-      double s = 0.0;
-#pragma unroll
-      for (int k = 0; k < R; ++k) s = fma(sT[k * 8 + rt], sV[cb * 8 + k], s);
-      sA[cb * 8 + rt] = s;
-    }
-    ppls_wave_lds_fence();
+    ppls_matmul_wave<R, false>(sA, sV, sT);                // sT = T V (A of the Jacobi)
     ppls_stamp(tr, 7);
-    const int sweeps = ppls_jacobi_wave<R>(sA, sV);
+    const int sweeps = ppls_jacobi_wave<R>(sT, sV);
     ppls_stamp(tr, 8);
     if (tr && lane == 0) tr[10] = sweeps;
     if (lane < R) {
       double nrm = 0.0;
 #pragma unroll
-      for (int t = 0; t < R; ++t) nrm = fma(sA[lane * 8 + t], sA[lane * 8 + t], nrm);
+      for (int t = 0; t < R; ++t) nrm = fma(sT[lane * G + t], sT[lane * G + t], nrm);
       ssv[lane] = sqrt(nrm);
     }
     ppls_wave_lds_fence();
     double smax = 0.0;
-    bool good = true;
 #pragma unroll
     for (int i = 0; i < R; ++i) smax = fmax(smax, ssv[i]);
 #pragma unroll
     for (int i = 0; i < R; ++i) good = good && (ssv[i] > smax * 1e-14);
-    if (lane < R * R) {   // F = V Sigma^-1 V', lane (a, b)
-      const int a = lane % R, b = lane / R;
+    for (int e = lane; e < R * R; e += 64) {   // F = V Sigma^-1 V', entry (a, b)
+      const int a = e % R, b = e / R;
       double s = 0.0;
 #pragma unroll
-      for (int k = 0; k < R; ++k) s = fma(sV[k * 8 + a] * (1.0 / ssv[k]), sV[k * 8 + b], s);
-      sR1[b * R + a] = s;
-      if (vstate) vstate[b * R + a] = sV[b * 8 + a];
+      for (int kk = 0; kk < R; ++kk) s = fma(sV[kk * G + a] * (1.0 / ssv[kk]), sV[kk * G + b], s);
+      sF[b * R + a] = s;
+      if (vstate) vstate[b * R + a] = sV[b * G + a];
     }
+    good = __shfl(good ? 1 : 0, 0, 64) != 0 && good;   // lane 0 holds the chol2 verdict for small R
     if (lane == 0) ok = ok && good;
   }
   __syncthreads();
@@ -1451,19 +1789,19 @@ __device__ bool ppls_block_polar_fast(const double* __restrict__ S, int64_t lds,
 #pragma unroll
   for (int a = 0; a < R; ++a)
 #pragma unroll
-    for (int b = 0; b < R; ++b) F[a][b] = sR1[b * R + a];
+    for (int b = 0; b < R; ++b) F[a][b] = sF[b * R + a];
 #pragma unroll
   for (int e = 0; e < NG; ++e) vals[e] = 0.0;
-#pragma unroll 4
+#pragma unroll 2
   for (int i = tid; i < ldo_rows; i += NT) {
-    double x[R], o[R];
+    double xq[R], o[R];
 #pragma unroll
-    for (int k = 0; k < R; ++k) x[k] = (i < p) ? Sr[(int64_t)k * ldr + i] : 0.0;
+    for (int k = 0; k < R; ++k) xq[k] = (i < p) ? Sr[(int64_t)k * ldr + i] : 0.0;
 #pragma unroll
     for (int j = 0; j < R; ++j) {
       double s = 0.0;
 #pragma unroll
-      for (int k = 0; k < R; ++k) s = fma(x[k], F[k][j], s);
+      for (int k = 0; k < R; ++k) s = fma(xq[k], F[k][j], s);
       o[j] = s;
       out[(int64_t)j * ldo + i] = s;
     }
@@ -1472,12 +1810,12 @@ __device__ bool ppls_block_polar_fast(const double* __restrict__ S, int64_t lds,
   if (gram_out) {
     ppls_block_sum_t<NG, NW>(vals, sh);
     if (tid == 0) {
-      double G[R][R];
-      ppls_gram_unpack<R>(vals, G);
+      double Gm[R][R];
+      ppls_gram_unpack<R>(vals, Gm);
 #pragma unroll
       for (int a = 0; a < R; ++a)
 #pragma unroll
-        for (int b = 0; b < R; ++b) gram_out[b * R + a] = G[a][b];
+        for (int b = 0; b < R; ++b) gram_out[b * R + a] = Gm[a][b];
     }
   }
   return true;
@@ -1533,17 +1871,28 @@ __device__ void ppls_scalars_wave(const double* sG, const double* sWtW, const do
   ppls_coef_estep(sc->t[k], sc->b[k], sc->sigE, sc->sigF, sc->sigH, &c1, &c2, &c3, nullptr);
   double Ctt, Cuu, Cut, xk, yk;
   ppls_moment_diag(sG, R, k, sc, c1, c2, c3, N, &Ctt, &Cuu, &Cut, &xk, &yk);
-  const bool pact = lane < R * R;
-  const int pk = pact ? lane % R : 0, pl = pact ? lane / R : 0;
-  const double c1k = __shfl(c1, pk, 64), c2k = __shfl(c2, pk, 64), c3k = __shfl(c3, pk, 64);
-  const double c1l = __shfl(c1, pl, 64), c2l = __shfl(c2, pl, 64), c3l = __shfl(c3, pl, 64);
-  double z, w, chh;
-  ppls_moment_pair(sG, R, pk, pl, c1k, c2k, c3k, c1l, c2l, c3l, sWtW[pl * R + pk], sCtC[pl * R + pk], sc,
-                   N, &z, &w, &chh);
+  double zsum = 0.0, wsum = 0.0, hsum = 0.0;
+#pragma unroll
+  for (int u = 0; u < (R * R + 63) / 64; ++u) {   // component pairs (k, l) on lanes
+    const int e = lane + 64 * u;
+    const bool pact = e < R * R;
+    const int pk = pact ? e % R : 0, pl = pact ? e / R : 0;
+    const double c1k = __shfl(c1, pk, 64), c2k = __shfl(c2, pk, 64), c3k = __shfl(c3, pk, 64);
+    const double c1l = __shfl(c1, pl, 64), c2l = __shfl(c2, pl, 64), c3l = __shfl(c3, pl, 64);
+    double z, w, chh;
+    ppls_moment_pair(sG, R, pk, pl, c1k, c2k, c3k, c1l, c2l, c3l, sWtW[pl * R + pk], sCtC[pl * R + pk],
+                     sc, N, &z, &w, &chh);
+    if (pact) {
+      zsum += z;
+      wsum += w;
+      if (pk == pl) hsum += chh;
+      m->Chh[pl * R + pk] = chh;
+    }
+  }
   const double xz = ppls_wave_allsum(kact ? xk : 0.0), yz = ppls_wave_allsum(kact ? yk : 0.0);
   const double sc1 = ppls_wave_allsum(kact ? c1 : 0.0), sc3 = ppls_wave_allsum(kact ? c3 : 0.0);
-  const double zz = ppls_wave_allsum(pact ? z : 0.0), ww = ppls_wave_allsum(pact ? w : 0.0);
-  const double trChh = ppls_wave_allsum(pact && pk == pl ? chh : 0.0);
+  const double zz = ppls_wave_allsum(zsum), ww = ppls_wave_allsum(wsum);
+  const double trChh = ppls_wave_allsum(hsum);
   double Cee, Cff;
   ppls_moment_noise(ssqX, ssqY, N, p, q, sc, xz, yz, zz, ww, sc1, sc3, &Cee, &Cff);
   if (loglik_out) {
@@ -1553,7 +1902,6 @@ __device__ void ppls_scalars_wave(const double* sG, const double* sWtW, const do
     if (lane == 0) *loglik_out = ppls_logl_total(LG, TK, ssqX, ssqY, N, p, q, R, sc);
   }
   if (kact) { m->Ctt[k] = Ctt; m->Cuu[k] = Cuu; m->Cut[k] = Cut; }
-  if (pact) m->Chh[pl * R + pk] = chh;
   // Maximiz_M scalars (EM_W_multi.R:734-738) and the next mu coefficients (:691-694)
   const double sE = sqrt(Cee / 1.0), sF = sqrt(Cff / 1.0), sH = sqrt(trChh / (double)R);
   const double bn = Cut * (1.0 / Ctt), tn = sqrt(Ctt);
@@ -1631,36 +1979,29 @@ __global__ __launch_bounds__(PPLS_FIN_THREADS) void ppls_finalize_kernel(
     if (gram_cur)
       for (int i = tid; i < R * R; i += NT) { s_WtW[i] = gram_cur[i]; s_CtC[i] = gram_cur[R * R + i]; }
   }
-  if (!gram_cur) {   // W'W and C'C by a pass over W, C (one batched reduction)
-    double vals[2 * NG];
+  if (!gram_cur) {   // W'W and C'C by a pass over W, then one over C
+    for (int mat = 0; mat < 2; ++mat) {
+      const double* M = mat ? Cc : Wc;
+      const int ld = mat ? ldy : ldx, rows = mat ? q : p;
+      double* dst = mat ? s_CtC : s_WtW;
+      double vals[NG];
 #pragma unroll
-    for (int e = 0; e < 2 * NG; ++e) vals[e] = 0.0;
-    for (int i = tid; i < (p > q ? p : q); i += NT) {
-      double wv[R], cv[R];
+      for (int e = 0; e < NG; ++e) vals[e] = 0.0;
+      for (int i = tid; i < rows; i += NT) {
+        double wv[R];
 #pragma unroll
-      for (int k = 0; k < R; ++k) {
-        wv[k] = (i < p) ? Wc[(int64_t)k * ldx + i] : 0.0;
-        cv[k] = (i < q) ? Cc[(int64_t)k * ldy + i] : 0.0;
+        for (int k = 0; k < R; ++k) wv[k] = M[(int64_t)k * ld + i];
+        ppls_gram_acc<R>(wv, vals);
       }
-      int e = 0;
-#pragma unroll
-      for (int b = 0; b < R; ++b)
-#pragma unroll
-        for (int a = 0; a <= b; ++a) {
-          vals[e] = fma(wv[a], wv[b], vals[e]);
-          vals[NG + e] = fma(cv[a], cv[b], vals[NG + e]);
-          ++e;
-        }
-    }
-    ppls_block_sum_t<2 * NG>(vals, sh);
-    if (tid == 0) {
-      int e = 0;
-      for (int b = 0; b < R; ++b)
-        for (int a = 0; a <= b; ++a) {
-          s_WtW[b * R + a] = s_WtW[a * R + b] = vals[e];
-          s_CtC[b * R + a] = s_CtC[a * R + b] = vals[NG + e];
-          ++e;
-        }
+      ppls_block_sum_t<NG, NT / 64>(vals, sh);
+      if (tid == 0) {
+        int e = 0;
+        for (int b = 0; b < R; ++b)
+          for (int a = 0; a <= b; ++a) {
+            dst[b * R + a] = dst[a * R + b] = vals[e];
+            ++e;
+          }
+      }
     }
   }
   __syncthreads();
@@ -1760,15 +2101,20 @@ namespace {
 template <int R>
 hipError_t launch_finalize_t(const PplsFinalizeArgs* f, hipStream_t st) {
   auto kern = ppls_finalize_kernel<R>;
+  static size_t dyn_max = 0;   // dynamic LDS left next to the kernel's static LDS (160 KB per WG)
   static bool attr_set = false;
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       PPLS_FIN_STAGE_MAX);
+    hipFuncAttributes fa;
+    hipError_t e = hipFuncGetAttributes(&fa, (const void*)kern);
+    if (e != hipSuccess) return e;
+    const size_t budget = 160 * 1024 - fa.sharedSizeBytes - 1024;
+    dyn_max = budget < PPLS_FIN_STAGE_MAX ? budget : PPLS_FIN_STAGE_MAX;
+    e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn_max);
     if (e != hipSuccess) return e;
     attr_set = true;
   }
   const size_t stage = (size_t)R * (f->p > f->q ? f->p : f->q) * sizeof(double);
-  const int use = stage <= PPLS_FIN_STAGE_MAX && !f->qr;
+  const int use = stage <= dyn_max && !f->qr;
   hipLaunchKernelGGL(kern, dim3(3), dim3(PPLS_FIN_THREADS), use ? stage : 0, st, f->stats, f->ssq, f->N,
                      f->p, f->q, f->ldx, f->ldy, f->Wc, f->Cc, f->sc_cur, f->Wn, f->Cn, f->sc_nxt, f->mom,
                      f->loglik, f->logl_index, f->work, f->status, f->qr, f->mode, f->gram_cur,
@@ -1978,6 +2324,75 @@ hipError_t ppls_launch_accumulate(const PplsSweepArgs* a, const double* Z, hipSt
   return hipGetLastError();
 }
 
+// ---- panel sweep launchers
+}  // extern "C"
+namespace {
+template <typename T, int R>
+hipError_t launch_panel_t(const PplsSweepArgs* a, const T* X, const T* Y, double* Z, int chunks, hipStream_t st) {
+  const int64_t tiles = (a->n_local + PPLS_PANEL_ROWS - 1) / PPLS_PANEL_ROWS;
+  const int blocks = (int)(tiles < 8192 ? tiles : 8192);
+  double* Wt = Z + a->n_local * 4 * R;   // transposed W, C behind Z (see ppls_panel_z_len)
+  double* Ct = Wt + (int64_t)a->ldx * R;
+  const int64_t ne = (int64_t)(a->ldx + a->ldy) * R;
+  hipLaunchKernelGGL(ppls_transpose_wc_kernel, dim3((unsigned)((ne + 255) / 256)), dim3(256), 0, st, a->Wp,
+                     a->Cp, a->ldx, a->ldy, R, Wt, Ct);
+  hipLaunchKernelGGL((ppls_panel_dots_kernel<T, R>), dim3(blocks), dim3(256), 0, st, X, Y, a->n_local,
+                     a->ldx, a->ldy, Wt, Ct, a->sc, Z, a->write_mu ? a->mu : nullptr);
+  constexpr int VEC = PplsVec16<T>::N;
+  const int ntx = (a->ldx + 256 * VEC - 1) / (256 * VEC), nty = (a->ldy + 256 * VEC - 1) / (256 * VEC);
+  const int64_t rpc = (a->n_local + chunks - 1) / chunks;
+  hipLaunchKernelGGL((ppls_panel_acc_kernel<T, R>), dim3(ntx + nty, chunks), dim3(256), 0, st, X, Y,
+                     a->n_local, a->ldx, a->ldy, Z, rpc, a->part, a->part_ld);
+  return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_panel_dt(const PplsSweepArgs* a, const T* X, const T* Y, double* Z, int chunks, hipStream_t st) {
+  switch (a->r) {
+    case 1: return launch_panel_t<T, 1>(a, X, Y, Z, chunks, st);
+    case 2: return launch_panel_t<T, 2>(a, X, Y, Z, chunks, st);
+    case 3: return launch_panel_t<T, 3>(a, X, Y, Z, chunks, st);
+    case 4: return launch_panel_t<T, 4>(a, X, Y, Z, chunks, st);
+    case 5: return launch_panel_t<T, 5>(a, X, Y, Z, chunks, st);
+    case 6: return launch_panel_t<T, 6>(a, X, Y, Z, chunks, st);
+    case 7: return launch_panel_t<T, 7>(a, X, Y, Z, chunks, st);
+    case 8: return launch_panel_t<T, 8>(a, X, Y, Z, chunks, st);
+    case 9: return launch_panel_t<T, 9>(a, X, Y, Z, chunks, st);
+    case 10: return launch_panel_t<T, 10>(a, X, Y, Z, chunks, st);
+    case 11: return launch_panel_t<T, 11>(a, X, Y, Z, chunks, st);
+    case 12: return launch_panel_t<T, 12>(a, X, Y, Z, chunks, st);
+    case 13: return launch_panel_t<T, 13>(a, X, Y, Z, chunks, st);
+    case 14: return launch_panel_t<T, 14>(a, X, Y, Z, chunks, st);
+    case 15: return launch_panel_t<T, 15>(a, X, Y, Z, chunks, st);
+    case 16: return launch_panel_t<T, 16>(a, X, Y, Z, chunks, st);
+    default: return hipErrorInvalidValue;
+  }
+}
+}  // namespace
+extern "C" {
+
+int64_t ppls_panel_z_len(int64_t n_local, int ldx, int ldy, int r) {
+  return (n_local > 0 ? n_local : 1) * 4 * r + (int64_t)(ldx + ldy) * r;
+}
+
+int ppls_panel_chunks(int64_t n_local, int ldx, int ldy, int num_cus) {
+  // enough workgroups for memory-level parallelism (>= 16 per CU) as column tiles x row chunks
+  const int tiles = (ldx + 511) / 512 + (ldy + 511) / 512;
+  int64_t ch = (16LL * num_cus + tiles - 1) / tiles;
+  const int64_t maxch = (n_local + 255) / 256;   // at least 256 rows per chunk
+  if (ch > maxch) ch = maxch;
+  if (ch < 1) ch = 1;
+  if (ch > 1024) ch = 1024;
+  return (int)ch;
+}
+
+hipError_t ppls_launch_sweep_panel(const PplsSweepArgs* a, int dtype_f32, double* Z, int chunks, hipStream_t st) {
+  if (a->n_local <= 0) return hipSuccess;
+  if (dtype_f32)
+    return launch_panel_dt<float>(a, (const float*)a->X, (const float*)a->Y, Z, chunks, st);
+  return launch_panel_dt<double>(a, a->X, a->Y, Z, chunks, st);
+}
+
 int ppls_twopass_groups(int64_t n_local, int grid) {
   const int64_t rpc = (n_local + grid - 1) / grid;
   return (int)((n_local + rpc - 1) / rpc);
@@ -2021,7 +2436,11 @@ hipError_t ppls_launch_finalize(const PplsFinalizeArgs* f, hipStream_t st) {
     case 4: return launch_finalize_t<4>(f, st);
     case 5: return launch_finalize_t<5>(f, st);
     case 6: return launch_finalize_t<6>(f, st);
-    default:   // r = 7..16: runtime-r finalize (the unrolled batched reductions would spill)
+    case 7: return launch_finalize_t<7>(f, st);
+    case 8: return launch_finalize_t<8>(f, st);
+    case 9: return launch_finalize_t<9>(f, st);
+    case 10: return launch_finalize_t<10>(f, st);
+    default:   // r = 11..16: runtime-r finalize (R(R+1)/2 > 64 block-sum values)
       hipLaunchKernelGGL(ppls_finalize_generic_kernel, dim3(3), dim3(256), 0, st, f->stats, f->ssq, f->N,
                          f->p, f->q, f->r, f->ldx, f->ldy, f->Wc, f->Cc, f->sc_cur, f->Wn, f->Cn,
                          f->sc_nxt, f->mom, f->loglik, f->logl_index, f->work, f->status, f->qr, f->mode);

@@ -21,8 +21,8 @@ GOLD = os.path.join(os.path.dirname(__file__), "golden")
 # threads, 1 or 2 rows per step), generic two-pass
 SWEEPS = [dict(), dict(kernel=3, rows_per_step=1, pipe=1), dict(kernel=3, rows_per_step=1, pipe=0),
           dict(kernel=2, threads=512, rows_per_step=1), dict(kernel=2, threads=512, rows_per_step=2),
-          dict(kernel=2, threads=1024), dict(sweep=2)]
-SWEEP_IDS = ["split", "split_rp1", "split_rp1_nopipe", "v2_512", "v2_512_rp2", "v2_1024", "twopass"]
+          dict(kernel=2, threads=1024), dict(sweep=2), dict(sweep=3)]
+SWEEP_IDS = ["split", "split_rp1", "split_rp1_nopipe", "v2_512", "v2_512_rp2", "v2_1024", "twopass", "panel"]
 DEFAULTS = dict(sweep=0, threads=0, grid=0, rows_per_step=0, kernel=0, pipe=1)
 
 

@@ -13,7 +13,7 @@ def main():
     rows = list(csv.DictReader(open(sys.argv[1])))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     # keep the EM loop: from the first sweep launch on
-    first = next(i for i, r in enumerate(rows) if "sweep" in r["Kernel_Name"])
+    first = next(i for i, r in enumerate(rows) if "sweep" in r["Kernel_Name"] or "panel" in r["Kernel_Name"])
     rows = rows[first:]
     dur = defaultdict(list)
     gap = defaultdict(list)
