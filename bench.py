@@ -24,7 +24,9 @@ sys.path.insert(0, ROOT)
 CONFIGS = {
     "c3": dict(n=1_000_000, p=2000, q=2000, r=5, name="C3: n=1e6, p=q=2000, r=5, fp64 (headline)"),
     "c2": dict(n=100_000, p=1000, q=1000, r=3, name="C2: n=1e5, p=q=1000, r=3, fp64"),
-    "c5": dict(n=500_000, p=10_000, q=500, r=10, name="C5: n=5e5, p=1e4, q=500, r=10 (wide-p omics case)"),
+    "c5": dict(n=500_000, p=10_000, q=500, r=10, storage="f32",
+               name="C5: n=5e5, p=1e4, q=500, r=10, fp32 storage / fp64 arithmetic (wide-p omics case)"),
+    "c5d": dict(n=500_000, p=10_000, q=500, r=10, name="C5 shape in fp64 storage"),
 }
 METRIC = "EM iterations/sec + log-lik rel-err vs CPU ref, n=1e6 p=q=2000 r=5"
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
@@ -112,7 +114,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
-    ap.add_argument("--sweep", type=int, default=0, help="0 auto, 1 fused, 2 two-pass")
+    ap.add_argument("--sweep", type=int, default=0, help="0 auto, 1 fused, 2 two-pass, 3 panel")
     ap.add_argument("--threads", type=int, default=0, help="fused workgroup size: 0 auto, 512, 1024")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
@@ -139,6 +141,8 @@ def main():
     device = local % ndev
     ctx = Context(device)
     _DEVICE[id(ctx)] = device
+    if cfg.get("storage") == "f32":
+        ctx.set_option("dtype", 1)
     ctx.set_option("sweep", args.sweep)
     ctx.set_option("threads", args.threads)
     if world > 1:
@@ -181,7 +185,7 @@ def main():
         wl = f"{args.config}_{'dp%d' % world}"
         # compute side: 2r fp64 FMAs per element (r for the dots, r for the rank-1 update), on
         # VALU (no fp64 MFMA shape fits r <= 8 better, and its rate equals the VALU rate)
-        flops = 4.0 * (info["bytes_per_sweep"] / 8) * r
+        flops = 4.0 * (n_local * (p + q)) * r
         tflops = flops / (avg_kernel_ms * 1e-3) / 1e12 if launches else None
         roofline = dict(bound="hbm", achieved=achieved, peak=HBM_PEAK_GBS, unit="GB/s",
                         frac=(achieved / HBM_PEAK_GBS) if achieved else None,
@@ -192,6 +196,7 @@ def main():
         out = dict(metric=METRIC, value=its, unit="EM iterations/s", n_gpus=world, steps=args.steps,
                    warmup=args.warmup, ms_per_step=1e3 * dt / args.steps, higher_is_better=True,
                    scaling="strong", vs_baseline=None, dtype="f64",
+                   storage=cfg.get("storage", "f64"),
                    data="synthetic (simulC model: X=TW'+sigE E, Y=UC'+sigF F; Philox normals on device)",
                    config=dict(workload=cfg["name"], n=n, p=p, q=q, r=r,
                                parallelism=f"dp{world} (rows sharded, 1 RCCL all-reduce/iteration)"),

@@ -34,6 +34,7 @@ struct ppls_ctx {
   int kernel_opt = 0;   // fused sweep kernel: 0 auto, 2 = shared ownership (v2), 3 = split ownership
   int pipe_opt = 1;     // split kernel: software-pipelined order
   int ablate = 0;
+  int dtype = 0;           // storage of X, Y: 0 fp64, 1 fp32 (arithmetic is fp64 either way)
   int nt_loads = -1;       // sweep LDS-DMA non-temporal: -1 auto (when X, Y exceed the MALL), 0 off, 1 on
   int timing = 0;          // 0 off; N > 0: bracket every N-th sweep launch with HIP events
   int64_t sweep_count = 0;
@@ -129,7 +130,7 @@ void dfree(T*& p) {
   p = nullptr;
 }
 
-int ld_of(int p) { return (p + 1) & ~1; }
+int ld_of(int p, int f32 = 0) { return f32 ? (p + 3) & ~3 : (p + 1) & ~1; }   // 16-B rows
 
 int check_theta(ppls_ctx* c, const ppls_theta* th, int r) {
   if (!th || !th->W || !th->C || !th->B || !th->sigT) return fail(c, PPLS_E_ARG, "theta has NULL fields");
@@ -305,7 +306,7 @@ int sweep_plan(ppls_ctx* c, int r, PplsSweepArgs* a) {
   a->q = c->q;
   a->r = r;
   a->threads = threads;
-  if (c->sweep_mode == 3) {        // forced panel sweep
+  if (c->sweep_mode == 3 || c->dtype) {   // forced panel sweep (the only fp32-storage sweep)
     a->grid = ppls_panel_chunks(c->n_local, c->ldx, c->ldy, c->num_cus);
     return 4;
   }
@@ -385,7 +386,7 @@ int sweep(ppls_ctx* c, int r, int slot, bool write_mu) {
     }
     if (plan == 3) HIPCHK(c, ppls_launch_sweep_split(&a, c->stream));
     else if (plan == 1) HIPCHK(c, ppls_launch_sweep_fused(&a, c->stream));
-    else if (plan == 4) HIPCHK(c, ppls_launch_sweep_panel(&a, 0, c->Z, a.grid, c->stream));
+    else if (plan == 4) HIPCHK(c, ppls_launch_sweep_panel(&a, c->dtype, c->Z, a.grid, c->stream));
     else HIPCHK(c, ppls_launch_sweep_twopass(&a, c->Z, c->stream));
     if (timed) HIPCHK(c, hipEventRecord(e1, c->stream));
     HIPCHK(c, ppls_launch_reduce2(c->part, groups, c->part_ld, c->part_ld, c->stats,
@@ -437,7 +438,10 @@ int compute_ssq(ppls_ctx* c) {
   const int nb = 1024;
   if ((rc = dalloc(c, &c->scratch, nb + 8))) return rc;
   HIPCHK(c, hipMemsetAsync(c->ssq, 0, 2 * sizeof(double), c->stream));
-  if (c->n_local > 0) {
+  if (c->n_local > 0 && c->dtype) {
+    HIPCHK(c, ppls_launch_sumsq_f32((const float*)c->X, c->n_local * c->ldx, c->scratch, nb, c->ssq, c->stream));
+    HIPCHK(c, ppls_launch_sumsq_f32((const float*)c->Y, c->n_local * c->ldy, c->scratch, nb, c->ssq + 1, c->stream));
+  } else if (c->n_local > 0) {
     HIPCHK(c, ppls_launch_sumsq(c->X, c->n_local * c->ldx, c->scratch, nb, c->ssq, 0, c->stream));
     HIPCHK(c, ppls_launch_sumsq(c->Y, c->n_local * c->ldy, c->scratch, nb, c->ssq + 1, 0, c->stream));
   }
@@ -455,10 +459,12 @@ int alloc_data(ppls_ctx* c, int64_t n_local, int p, int q, int64_t n_total) {
   c->n_total = n_total > 0 ? n_total : n_local;
   c->p = p;
   c->q = q;
-  c->ldx = ld_of(p);
-  c->ldy = ld_of(q);
-  if ((rc = dalloc(c, &c->X, (size_t)std::max<int64_t>(n_local, 1) * c->ldx))) return rc;
-  if ((rc = dalloc(c, &c->Y, (size_t)std::max<int64_t>(n_local, 1) * c->ldy))) return rc;
+  c->ldx = ld_of(p, c->dtype);
+  c->ldy = ld_of(q, c->dtype);
+  // X, Y storage (fp64, or fp32 packed into the double allocation)
+  const size_t es = c->dtype ? 4 : 8;
+  if ((rc = dalloc(c, &c->X, ((size_t)std::max<int64_t>(n_local, 1) * c->ldx * es + 7) / 8))) return rc;
+  if ((rc = dalloc(c, &c->Y, ((size_t)std::max<int64_t>(n_local, 1) * c->ldy * es + 7) / 8))) return rc;
   if (!c->ssq && (rc = dalloc(c, &c->ssq, 2))) return rc;
   c->r_alloc = 0;   // force per-r buffers to be re-sized for the new shape
   dfree(c->part);
@@ -615,7 +621,7 @@ int ppls_set_option(ppls_ctx* c, const char* key, int64_t value) {
   } else if (!strcmp(key, "pipe")) {
     c->pipe_opt = value ? 1 : 0;
   } else if (!strcmp(key, "ablate")) {
-    if (value < 0 || value > 15) return fail(c, PPLS_E_ARG, "ablate must be in [0,15]");
+    if (value < 0 || value > 63) return fail(c, PPLS_E_ARG, "ablate must be in [0,63]");
     c->ablate = (int)value;   // timing experiments only: results are wrong while set
   } else if (!strcmp(key, "ftrace")) {
     if (value && !c->ftrace) {
@@ -625,6 +631,12 @@ int ppls_set_option(ppls_ctx* c, const char* key, int64_t value) {
       HIPCHK(c, hipStreamSynchronize(c->stream));
       (void)hipFree(c->ftrace);
       c->ftrace = nullptr;
+    }
+  } else if (!strcmp(key, "dtype")) {
+    if (value != 0 && value != 1) return fail(c, PPLS_E_ARG, "dtype must be 0 (fp64) or 1 (fp32 storage)");
+    if (c->dtype != (int)value) {
+      c->dtype = (int)value;
+      c->have_data = false;   // the data must be (re)loaded in the new storage type
     }
   } else if (!strcmp(key, "nt")) {
     if (value < -1 || value > 1) return fail(c, PPLS_E_ARG, "nt must be -1 (auto), 0 or 1");
@@ -677,7 +689,38 @@ int ppls_set_data(ppls_ctx* c, const double* X, const double* Y, int64_t n_local
   HIPCHK(c, hipSetDevice(c->device));
   int rc = alloc_data(c, n_local, p, q, n_total);
   if (rc) return rc;
-  if (n_local > 0) {
+  if (n_local > 0 && c->dtype) {   // fp32 storage: build fp64 row-major chunks, then convert
+    const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(n_local, (int64_t)(256 << 20) / (8LL * (c->ldx + p))));
+    double *tmp = nullptr, *tcm = nullptr;
+    const int wmax = std::max(c->ldx, c->ldy), cmax = std::max(p, q);
+    if ((rc = dalloc(c, &tmp, (size_t)chunk * wmax))) return rc;
+    if ((rc = dalloc(c, &tcm, (size_t)chunk * cmax))) { dfree(tmp); return rc; }
+    for (int m = 0; m < 2 && !rc; ++m) {
+      const double* src = m == 0 ? X : Y;
+      const int cols = m == 0 ? p : q, ld = m == 0 ? c->ldx : c->ldy;
+      float* dst = (float*)(m == 0 ? c->X : c->Y);
+      for (int64_t r0 = 0; r0 < n_local && !rc; r0 += chunk) {
+        const int64_t nc = std::min(chunk, n_local - r0);
+        hipError_t e;
+        if (layout == PPLS_LAYOUT_ROWMAJOR) {
+          e = hipMemset2DAsync(tmp, sizeof(double) * ld, 0, sizeof(double) * ld, nc, c->stream);
+          if (e == hipSuccess)
+            e = hipMemcpy2DAsync(tmp, sizeof(double) * ld, src + r0 * cols, sizeof(double) * cols,
+                                 sizeof(double) * cols, nc, hipMemcpyHostToDevice, c->stream);
+        } else {   // column-major n_local x cols: rows [r0, r0 + nc) of every column
+          e = hipMemcpy2DAsync(tcm, sizeof(double) * nc, src + r0, sizeof(double) * n_local, sizeof(double) * nc,
+                               cols, hipMemcpyHostToDevice, c->stream);
+          if (e == hipSuccess) e = ppls_launch_to_rowmajor(tcm, nc, cols, ld, tmp, c->stream);
+        }
+        if (e == hipSuccess) e = ppls_launch_convert(tmp, 0, dst + r0 * ld, 1, nc * ld, c->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+        if (e != hipSuccess) rc = fail(c, PPLS_E_HIP, "fp32 upload: %s", hipGetErrorString(e));
+      }
+    }
+    dfree(tmp);
+    dfree(tcm);
+    if (rc) return rc;
+  } else if (n_local > 0) {
     for (int m = 0; m < 2; ++m) {
       const double* src = m == 0 ? X : Y;
       const int cols = m == 0 ? p : q, ld = m == 0 ? c->ldx : c->ldy;
@@ -716,8 +759,23 @@ int ppls_generate_synthetic(ppls_ctx* c, int64_t n_total, int64_t row0, int64_t 
   PplsScalars s = scalars_of(truth, r);
   hipError_t e = hipMemcpy(Wt, truth->W, sizeof(double) * p * r, hipMemcpyHostToDevice);
   if (e == hipSuccess) e = hipMemcpy(Ct, truth->C, sizeof(double) * q * r, hipMemcpyHostToDevice);
-  if (e == hipSuccess)
+  if (e == hipSuccess && !c->dtype)
     e = ppls_launch_generate(n_local, row0, p, q, c->ldx, c->ldy, r, &s, Wt, Ct, seed, TU, c->X, c->Y, c->stream);
+  if (e == hipSuccess && c->dtype) {   // fp32 storage: generate fp64 row chunks, convert
+    const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(std::max<int64_t>(n_local, 1),
+                                                                 (int64_t)(512 << 20) / (8LL * (c->ldx + c->ldy))));
+    double *gx = nullptr, *gy = nullptr;
+    if (dalloc(c, &gx, (size_t)chunk * c->ldx) || dalloc(c, &gy, (size_t)chunk * c->ldy)) e = hipErrorOutOfMemory;
+    for (int64_t o = 0; o < n_local && e == hipSuccess; o += chunk) {
+      const int64_t nc = std::min(chunk, n_local - o);
+      e = ppls_launch_generate(nc, row0 + o, p, q, c->ldx, c->ldy, r, &s, Wt, Ct, seed, TU, gx, gy, c->stream);
+      if (e == hipSuccess) e = ppls_launch_convert(gx, 0, (float*)c->X + o * c->ldx, 1, nc * c->ldx, c->stream);
+      if (e == hipSuccess) e = ppls_launch_convert(gy, 0, (float*)c->Y + o * c->ldy, 1, nc * c->ldy, c->stream);
+      if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    }
+    dfree(gx);
+    dfree(gy);
+  }
   if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
   dfree(Wt); dfree(Ct); dfree(TU);
   if (e != hipSuccess) return fail(c, PPLS_E_HIP, "synthetic generation: %s", hipGetErrorString(e));
@@ -737,12 +795,19 @@ int ppls_get_data(ppls_ctx* c, double* X, double* Y, int64_t row_begin, int64_t 
     if (!dst) continue;
     const int cols = m == 0 ? c->p : c->q, ld = m == 0 ? c->ldx : c->ldy;
     const double* src = (m == 0 ? c->X : c->Y) + row_begin * ld;
-    double* tmp = nullptr;
+    double *tmp = nullptr, *wide = nullptr;
     if ((rc = dalloc(c, &tmp, (size_t)nrows * cols))) return rc;
+    if (c->dtype) {   // fp32 storage: widen the rows first
+      if ((rc = dalloc(c, &wide, (size_t)nrows * ld))) { dfree(tmp); return rc; }
+      HIPCHK(c, ppls_launch_convert((const float*)(m == 0 ? c->X : c->Y) + row_begin * ld, 1, wide, 0, nrows * ld,
+                                    c->stream));
+      src = wide;
+    }
     HIPCHK(c, ppls_launch_to_colmajor(src, nrows, cols, ld, tmp, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     hipError_t e = hipMemcpy(dst, tmp, sizeof(double) * nrows * cols, hipMemcpyDeviceToHost);
     dfree(tmp);
+    dfree(wide);
     if (e != hipSuccess) return fail(c, PPLS_E_HIP, "copy back: %s", hipGetErrorString(e));
   }
   return PPLS_OK;
@@ -800,6 +865,7 @@ int ppls_mstep(ppls_ctx* c, const ppls_expect* fit, int r, int type, ppls_theta*
     return fail(c, PPLS_E_ARG, "Maximiz_M needs mu_T, mu_U, Ctt, Cut, Cee, Cff, Chh");
   if (!out || !out->W || !out->C || !out->B || !out->sigT) return fail(c, PPLS_E_ARG, "NULL output theta");
   if (r < 1 || r > PPLS_RMAX) return fail(c, PPLS_E_ARG, "bad r");
+  if (c->dtype) return fail(c, PPLS_E_ARG, "Maximiz_M from caller-supplied moments needs fp64 storage (dtype 0)");
   HIPCHK(c, hipSetDevice(c->device));
   int rc;
   if ((rc = ensure_r(c, r, 1))) return rc;
@@ -1071,8 +1137,8 @@ int deflated_ssq(ppls_ctx* c, const std::vector<double>& Wp, int m, bool isx, do
   double res = 0.0;
   hipError_t e = hipMemcpyAsync(Wd, Wp.data(), sizeof(double) * n * m, hipMemcpyHostToDevice, c->stream);
   if (e == hipSuccess)
-    e = ppls_launch_deflated_ssq(isx ? c->X : c->Y, c->n_local, isx ? c->ldx : c->ldy, n, Wd, m, buf, nb,
-                                 buf + nb, c->stream);
+    e = ppls_launch_deflated_ssq(isx ? c->X : c->Y, c->dtype, c->n_local, isx ? c->ldx : c->ldy, n, Wd, m, buf,
+                                 nb, buf + nb, c->stream);
   if (e == hipSuccess && c->n_local == 0) e = hipMemsetAsync(buf + nb, 0, sizeof(double), c->stream);
   rc = e == hipSuccess ? allreduce(c, buf + nb, 1) : fail(c, PPLS_E_HIP, "deflated ssq: %s", hipGetErrorString(e));
   if (!rc) {
@@ -1294,7 +1360,7 @@ int ppls_sweep_info(ppls_ctx* c, int r, int64_t* bytes_per_sweep, int* variant, 
   if (!c) return PPLS_E_ARG;
   PplsSweepArgs a;
   const int plan = sweep_plan(c, r, &a);
-  if (bytes_per_sweep) *bytes_per_sweep = (int64_t)8 * c->n_local * ((int64_t)c->p + c->q);
+  if (bytes_per_sweep) *bytes_per_sweep = (int64_t)(c->dtype ? 4 : 8) * c->n_local * ((int64_t)c->p + c->q);
   if (variant) *variant = plan == 4 ? 5 : plan == 3 ? 4 : plan == 1 ? (a.threads == 1024 ? 3 : 1) : 2;
   if (grid) *grid = a.grid;
   return PPLS_OK;

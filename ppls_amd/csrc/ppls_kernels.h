@@ -80,8 +80,12 @@ hipError_t ppls_launch_loglc(const double* G, const double* ssq, double N, int p
                              double sigX, double sigY, const double* coefs, double* out, hipStream_t st);
 hipError_t ppls_launch_sumsq(const double* a, int64_t len, double* part, int nblocks, double* out,
                              int out_accumulate, hipStream_t st);
-hipError_t ppls_launch_deflated_ssq(const double* X, int64_t n, int ld, int p, const double* Wd, int m,
+hipError_t ppls_launch_deflated_ssq(const void* X, int f32, int64_t n, int ld, int p, const double* Wd, int m,
                                     double* part, int nblocks, double* out, hipStream_t st);
+hipError_t ppls_launch_sumsq_f32(const float* a, int64_t len, double* part, int nblocks, double* out,
+                                 hipStream_t st);
+// element conversion fp64 <-> fp32 (same type: device copy)
+hipError_t ppls_launch_convert(const void* src, int src_f32, void* dst, int dst_f32, int64_t len, hipStream_t st);
 hipError_t ppls_launch_generate(int64_t n_local, int64_t row0, int p, int q, int ldx, int ldy, int r,
                                 const PplsScalars* truth, const double* Wt, const double* Ct,
                                 uint64_t seed, double* TU, double* X, double* Y, hipStream_t st);

@@ -144,14 +144,15 @@ __device__ inline double ppls_wave_sum(double v) {
 // ||X P_0 .. P_{m-1}||^2 row by row, P_j = I - w_j w_j' (w_j: columns of Wd, p x m, ld p): the
 // residual x P is formed before squaring, so there is no cancellation when X is nearly
 // spanned by the w_j (sequential initialiser's rank-collapse test).  One wave per row; m <= 16.
-__global__ __launch_bounds__(256) void ppls_deflated_ssq_kernel(const double* __restrict__ X, int64_t n,
+template <typename T>
+__global__ __launch_bounds__(256) void ppls_deflated_ssq_kernel(const T* __restrict__ X, int64_t n,
                                                                 int ld, int p, const double* __restrict__ Wd,
                                                                 int m, double* __restrict__ part) {
   __shared__ double sh[4];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   double acc = 0.0;
   for (int64_t row = (int64_t)blockIdx.x * 4 + wave; row < n; row += (int64_t)gridDim.x * 4) {
-    const double* x = X + row * ld;
+    const T* x = X + row * ld;
     double d[16];
     for (int j = 0; j < m; ++j) {   // x P_0 .. P_{m-1}: apply P_0 first
       double s = 0.0;
@@ -198,6 +199,31 @@ __global__ void ppls_sumsq_partial_kernel(const double* __restrict__ a, int64_t 
     part[blockIdx.x] = t;
   }
 }
+
+// fp32-storage helpers: sum of squares in fp64, and element conversions.
+__global__ void ppls_sumsq_f32_kernel(const float* __restrict__ a, int64_t len, double* __restrict__ part) {
+  __shared__ double sh[16];
+  double s = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < len; i += (int64_t)gridDim.x * blockDim.x) {
+    const double v = a[i];
+    s = fma(v, v, s);
+  }
+  s = ppls_wave_sum(s);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = 0.0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += sh[w];
+    part[blockIdx.x] = t;
+  }
+}
+
+template <typename TI, typename TO>
+__global__ void ppls_convert_kernel(const TI* __restrict__ src, TO* __restrict__ dst, int64_t len) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < len; i += (int64_t)gridDim.x * blockDim.x)
+    dst[i] = (TO)src[i];
+}
+
 
 // out[j] (+)= sum_g part[g*ld + j], fixed order -> deterministic.
 __global__ void ppls_reduce_partials_kernel(const double* __restrict__ part, int ngroups, int64_t ld,
@@ -1017,19 +1043,123 @@ __global__ __launch_bounds__(256) void ppls_panel_dots_kernel(
   }
 }
 
-// W (ldx x R, column-major) -> Wt (ldx x R, row-major); same for C.
+// Row-per-lane dots (the default panel dots): each wave owns 64 rows, one per lane, and walks the
+// columns in 128-B tiles (KT = 128 / sizeof(T) columns).  A tile (64 rows x 128 B) is loaded with
+// 16-B coalesced loads (8 lanes per row), transposed through a padded per-wave LDS buffer
+// (row stride 144 B: conflict-free row reads), and then each lane applies its row's KT values to
+// the R weights of each column -- the weights are wave-uniform (scalar loads, SGPR operands), so
+// no per-lane weight traffic at all.  The next tile's global loads are in flight while the
+// current one is computed.  Waves are independent (no workgroup barrier).
+template <typename T, int R>
+__global__ __launch_bounds__(256) void ppls_panel_rowdots_kernel(
+    const T* __restrict__ X, const T* __restrict__ Y, int64_t n, int ldx, int ldy,
+    const double* __restrict__ Wt, const double* __restrict__ Ct, const PplsScalars* __restrict__ sc,
+    double* __restrict__ Z, double* __restrict__ mu) {
+  constexpr int KT = 128 / (int)sizeof(T);   // columns per tile
+  constexpr int RS = 144;                    // padded LDS row stride (bytes)
+  constexpr int V4 = 4 * R;
+  __shared__ __attribute__((aligned(16))) char lds[4 * 64 * RS];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  char* wl = lds + wave * 64 * RS;
+  const int lrow = lane >> 3, lchunk = lane & 7;   // tile loading: 8 lanes per row, 8 rows per load
+  double al[R], be[R], ga[R], de[R];
+#pragma unroll
+  for (int k = 0; k < R; ++k) {
+    al[k] = sc->alpha[k];
+    be[k] = sc->beta[k];
+    ga[k] = sc->gamma[k];
+    de[k] = sc->delta[k];
+  }
+  const int64_t ntiles = (n + 63) / 64;
+  for (int64_t tile = (int64_t)blockIdx.x * 4 + wave; tile < ntiles; tile += (int64_t)gridDim.x * 4) {
+    const int64_t row0 = tile * 64;
+    const int64_t myrow = row0 + lane;
+    double ab[2][R];
+#pragma unroll
+    for (int mat = 0; mat < 2; ++mat) {
+      const T* M = mat ? Y : X;
+      const int ld = mat ? ldy : ldx;
+      const double* Wm = mat ? Ct : Wt;
+      double acc[R];
+#pragma unroll
+      for (int k = 0; k < R; ++k) acc[k] = 0.0;
+      // rows this lane loads (clamped; rows >= n contribute zeros through their lane)
+      const T* src[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        int64_t rr = row0 + lrow + 8 * i;
+        if (rr >= n) rr = n - 1;
+        src[i] = M + rr * ld + lchunk * (16 / (int)sizeof(T));
+      }
+      const int ntile_c = (ld + KT - 1) / KT;
+      float4 buf[8];
+      auto load_tile = [&](int tc) {
+        const int c0 = tc * KT + lchunk * (16 / (int)sizeof(T));
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          buf[i] = (c0 < ld) ? *(const float4*)(src[i] + tc * KT) : make_float4(0.f, 0.f, 0.f, 0.f);
+      };
+      load_tile(0);
+      for (int tc = 0; tc < ntile_c; ++tc) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) *(float4*)(wl + (lrow + 8 * i) * RS + lchunk * 16) = buf[i];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (tc + 1 < ntile_c) load_tile(tc + 1);   // next tile's loads overlap this tile's FMAs
+        T xr[KT];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float4 v = *(const float4*)(wl + lane * RS + j * 16);
+          const T* pv = (const T*)&v;
+#pragma unroll
+          for (int u = 0; u < 16 / (int)sizeof(T); ++u) xr[j * (16 / (int)sizeof(T)) + u] = pv[u];
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // reads done before the next writes
+        // whole tile, static trip count: Wt is zero-padded to whole tiles and X columns >= ld
+        // were loaded as zeros, so no bound check (the loop unrolls and the scalar weight loads
+        // of later columns are issued ahead of the FMAs of earlier ones)
+        const double* wt = Wm + (int64_t)tc * KT * R;   // wave-uniform
+#pragma unroll
+        for (int c = 0; c < KT; ++c) {
+          const double x = (double)xr[c];
+#pragma unroll
+          for (int k = 0; k < R; ++k) acc[k] = fma(x, wt[c * R + k], acc[k]);
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < R; ++k) ab[mat][k] = acc[k];
+    }
+    if (myrow < n) {
+      double* zr = Z + myrow * V4;
+#pragma unroll
+      for (int k = 0; k < R; ++k) {
+        const double a = ab[0][k], b = ab[1][k];
+        const double mt = al[k] * a + be[k] * b, mu_u = ga[k] * a + de[k] * b;
+        zr[k] = a;
+        zr[R + k] = b;
+        zr[2 * R + k] = mt;
+        zr[3 * R + k] = mu_u;
+        if (mu) {
+          mu[(int64_t)k * n + myrow] = mt;
+          mu[(int64_t)(R + k) * n + myrow] = mu_u;
+        }
+      }
+    }
+  }
+}
+
+// W (ldx x R, column-major) -> Wt (ldxp x R, row-major, rows >= ldx zero); same for C.
 __global__ void ppls_transpose_wc_kernel(const double* __restrict__ W, const double* __restrict__ C,
-                                         int ldx, int ldy, int r, double* __restrict__ Wt,
+                                         int ldx, int ldy, int ldxp, int ldyp, int r, double* __restrict__ Wt,
                                          double* __restrict__ Ct) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t nx = (int64_t)ldx * r;
+  const int64_t nx = (int64_t)ldxp * r;
   if (e < nx) {
     const int i = (int)(e / r), k = (int)(e % r);
-    Wt[e] = W[(int64_t)k * ldx + i];
-  } else if (e < nx + (int64_t)ldy * r) {
+    Wt[e] = i < ldx ? W[(int64_t)k * ldx + i] : 0.0;
+  } else if (e < nx + (int64_t)ldyp * r) {
     const int64_t f = e - nx;
     const int i = (int)(f / r), k = (int)(f % r);
-    Ct[f] = C[(int64_t)k * ldy + i];
+    Ct[f] = i < ldy ? C[(int64_t)k * ldy + i] : 0.0;
   }
 }
 
@@ -1049,23 +1179,52 @@ __global__ __launch_bounds__(256) void ppls_panel_acc_kernel(
   const int64_t r0 = (int64_t)blockIdx.y * rows_per_chunk;
   const int64_t r1 = min(n, r0 + rows_per_chunk);
   double* pg = part + (int64_t)blockIdx.y * part_ld;
-  if (col < ld) {
-    double acc[VEC][R];
+  // mu (mu_T for X tiles, mu_U for Y tiles) of BR rows at a time in LDS: every lane reads the same
+  // address (broadcast), and the X loads of a batch are issued together
+  constexpr int BR = 64;
+  __shared__ double smu[BR * R];
+  double acc[VEC][R];
 #pragma unroll
-    for (int v = 0; v < VEC; ++v)
+  for (int v = 0; v < VEC; ++v)
 #pragma unroll
-      for (int k = 0; k < R; ++k) acc[v][k] = 0.0;
-#pragma unroll 8
-    for (int64_t row = r0; row < r1; ++row) {
-      const PplsVec16<T> xv = ppls_load16(M + row * ld + col);
-      const double* zr = Z + row * V4 + off;   // wave-uniform
+    for (int k = 0; k < R; ++k) acc[v][k] = 0.0;
+  const bool act = col < ld;
+  const T* base = M + (act ? col : 0);
+  for (int64_t b0 = r0; b0 < r1; b0 += BR) {
+    const int nb = (int)(r1 - b0 < BR ? r1 - b0 : BR);
+    __syncthreads();
+    for (int e = tid; e < BR * R; e += 256) {
+      const int rr = e / R, k = e - rr * R;
+      smu[e] = rr < nb ? Z[(b0 + rr) * V4 + off + k] : 0.0;
+    }
+    __syncthreads();
+    if (act) {
+      int rr = 0;
+      for (; rr + 8 <= nb; rr += 8) {
+        PplsVec16<T> xv[8];
 #pragma unroll
-      for (int k = 0; k < R; ++k) {
-        const double m = zr[k];
+        for (int u = 0; u < 8; ++u) xv[u] = ppls_load16(base + (b0 + rr + u) * ld);
 #pragma unroll
-        for (int v = 0; v < VEC; ++v) acc[v][k] = fma((double)xv.v[v], m, acc[v][k]);
+        for (int u = 0; u < 8; ++u)
+#pragma unroll
+          for (int k = 0; k < R; ++k) {
+            const double m = smu[(rr + u) * R + k];
+#pragma unroll
+            for (int v = 0; v < VEC; ++v) acc[v][k] = fma((double)xv[u].v[v], m, acc[v][k]);
+          }
+      }
+      for (; rr < nb; ++rr) {
+        const PplsVec16<T> xv = ppls_load16(base + (b0 + rr) * ld);
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
+          const double m = smu[rr * R + k];
+#pragma unroll
+          for (int v = 0; v < VEC; ++v) acc[v][k] = fma((double)xv.v[v], m, acc[v][k]);
+        }
       }
     }
+  }
+  if (act) {
     double* dst = isx ? pg : pg + (int64_t)R * ldx;
 #pragma unroll
     for (int k = 0; k < R; ++k)
@@ -2331,13 +2490,25 @@ template <typename T, int R>
 hipError_t launch_panel_t(const PplsSweepArgs* a, const T* X, const T* Y, double* Z, int chunks, hipStream_t st) {
   const int64_t tiles = (a->n_local + PPLS_PANEL_ROWS - 1) / PPLS_PANEL_ROWS;
   const int blocks = (int)(tiles < 8192 ? tiles : 8192);
-  double* Wt = Z + a->n_local * 4 * R;   // transposed W, C behind Z (see ppls_panel_z_len)
-  double* Ct = Wt + (int64_t)a->ldx * R;
-  const int64_t ne = (int64_t)(a->ldx + a->ldy) * R;
+  // transposed W, C behind Z (see ppls_panel_z_len), rows padded to whole 32-column tiles
+  const int ldxp = (a->ldx + 31) & ~31, ldyp = (a->ldy + 31) & ~31;
+  double* Wt = Z + a->n_local * 4 * R;
+  double* Ct = Wt + (int64_t)ldxp * R;
+  const int64_t ne = (int64_t)(ldxp + ldyp) * R;
   hipLaunchKernelGGL(ppls_transpose_wc_kernel, dim3((unsigned)((ne + 255) / 256)), dim3(256), 0, st, a->Wp,
-                     a->Cp, a->ldx, a->ldy, R, Wt, Ct);
-  hipLaunchKernelGGL((ppls_panel_dots_kernel<T, R>), dim3(blocks), dim3(256), 0, st, X, Y, a->n_local,
-                     a->ldx, a->ldy, Wt, Ct, a->sc, Z, a->write_mu ? a->mu : nullptr);
+                     a->Cp, a->ldx, a->ldy, ldxp, ldyp, R, Wt, Ct);
+  // measured at the C5 shape (tools/panel_experiment.py): tiled dots is faster for fp64 storage
+  // (8.6 vs 13.1 ms), row-per-lane dots for fp32 storage (6.7 vs 7.5 ms); ablate bit 5 flips it
+  const bool tiled = (sizeof(T) == 8) != ((a->ablate & 32) != 0);
+  if (tiled) {
+    hipLaunchKernelGGL((ppls_panel_dots_kernel<T, R>), dim3(blocks), dim3(256), 0, st, X, Y, a->n_local,
+                       a->ldx, a->ldy, Wt, Ct, a->sc, Z, a->write_mu ? a->mu : nullptr);
+  } else {
+    const int64_t wtiles = (a->n_local + 63) / 64;
+    const int rblocks = (int)((wtiles + 3) / 4 < 16384 ? (wtiles + 3) / 4 : 16384);
+    hipLaunchKernelGGL((ppls_panel_rowdots_kernel<T, R>), dim3(rblocks), dim3(256), 0, st, X, Y,
+                       a->n_local, a->ldx, a->ldy, Wt, Ct, a->sc, Z, a->write_mu ? a->mu : nullptr);
+  }
   constexpr int VEC = PplsVec16<T>::N;
   const int ntx = (a->ldx + 256 * VEC - 1) / (256 * VEC), nty = (a->ldy + 256 * VEC - 1) / (256 * VEC);
   const int64_t rpc = (a->n_local + chunks - 1) / chunks;
@@ -2372,7 +2543,7 @@ hipError_t launch_panel_dt(const PplsSweepArgs* a, const T* X, const T* Y, doubl
 extern "C" {
 
 int64_t ppls_panel_z_len(int64_t n_local, int ldx, int ldy, int r) {
-  return (n_local > 0 ? n_local : 1) * 4 * r + (int64_t)(ldx + ldy) * r;
+  return (n_local > 0 ? n_local : 1) * 4 * r + (int64_t)(((ldx + 31) & ~31) + ((ldy + 31) & ~31)) * r;
 }
 
 int ppls_panel_chunks(int64_t n_local, int ldx, int ldy, int num_cus) {
@@ -2456,6 +2627,27 @@ hipError_t ppls_launch_loglc(const double* G, const double* ssq, double N, int p
   return hipGetLastError();
 }
 
+hipError_t ppls_launch_sumsq_f32(const float* a, int64_t len, double* part, int nblocks, double* out,
+                                 hipStream_t st) {
+  hipLaunchKernelGGL(ppls_sumsq_f32_kernel, dim3(nblocks), dim3(256), 0, st, a, len, part);
+  hipLaunchKernelGGL(ppls_reduce_partials_kernel, dim3(1), dim3(64), 0, st, part, nblocks, 1, 1, out, 0);
+  return hipGetLastError();
+}
+
+hipError_t ppls_launch_convert(const void* src, int src_f32, void* dst, int dst_f32, int64_t len, hipStream_t st) {
+  if (len <= 0) return hipSuccess;
+  const int blocks = (int)((len + 255) / 256 < 16384 ? (len + 255) / 256 : 16384);
+  if (!src_f32 && dst_f32)
+    hipLaunchKernelGGL((ppls_convert_kernel<double, float>), dim3(blocks), dim3(256), 0, st, (const double*)src,
+                       (float*)dst, len);
+  else if (src_f32 && !dst_f32)
+    hipLaunchKernelGGL((ppls_convert_kernel<float, double>), dim3(blocks), dim3(256), 0, st, (const float*)src,
+                       (double*)dst, len);
+  else
+    return hipMemcpyAsync(dst, src, (size_t)len * (src_f32 ? 4 : 8), hipMemcpyDeviceToDevice, st);
+  return hipGetLastError();
+}
+
 hipError_t ppls_launch_sumsq(const double* a, int64_t len, double* part, int nblocks, double* out,
                              int out_accumulate, hipStream_t st) {
   hipLaunchKernelGGL(ppls_sumsq_partial_kernel, dim3(nblocks), dim3(256), 0, st, a, len, part);
@@ -2464,10 +2656,15 @@ hipError_t ppls_launch_sumsq(const double* a, int64_t len, double* part, int nbl
   return hipGetLastError();
 }
 
-hipError_t ppls_launch_deflated_ssq(const double* X, int64_t n, int ld, int p, const double* Wd, int m,
+hipError_t ppls_launch_deflated_ssq(const void* X, int f32, int64_t n, int ld, int p, const double* Wd, int m,
                                     double* part, int nblocks, double* out, hipStream_t st) {
   if (m < 0 || m > 16) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(ppls_deflated_ssq_kernel, dim3(nblocks), dim3(256), 0, st, X, n, ld, p, Wd, m, part);
+  if (f32)
+    hipLaunchKernelGGL(ppls_deflated_ssq_kernel<float>, dim3(nblocks), dim3(256), 0, st, (const float*)X, n, ld,
+                       p, Wd, m, part);
+  else
+    hipLaunchKernelGGL(ppls_deflated_ssq_kernel<double>, dim3(nblocks), dim3(256), 0, st, (const double*)X, n,
+                       ld, p, Wd, m, part);
   hipLaunchKernelGGL(ppls_reduce_partials_kernel, dim3(1), dim3(64), 0, st, part, nblocks, 1, 1, out, 0);
   return hipGetLastError();
 }

@@ -1,0 +1,79 @@
+"""fp32 storage of X, Y (context option dtype = 1; C5's "fp32" configuration) on the GPU.
+
+X and Y are held in HBM as fp32 (half the bytes per sweep); every product and statistic is
+accumulated in fp64.  So the GPU fit on fp32-stored data must match the fp64 oracle run on the
+same fp32-rounded data to the fp64 tolerances (loglik 1e-10 relative, loadings 1e-8 absolute):
+the only fp32 effect is the rounding of the data itself, which these tests apply to the oracle's
+input as well.
+"""
+import numpy as np
+import pytest
+
+from conftest import make_problem
+from oracle import ppls_oracle as o
+
+pytestmark = pytest.mark.gpu
+
+
+def _ctx32():
+    from ppls_amd import Context
+    c = Context(0)
+    c.set_option("dtype", 1)
+    return c
+
+
+def _round32(A):
+    return np.asarray(A, dtype=np.float32).astype(np.float64)
+
+
+def _theta(th):
+    from ppls_amd import Theta
+    return Theta(th["W"], th["C"], th["B"], th["sigE"], th["sigF"], th["sigH"], th["sigT"])
+
+
+def _relerr(a, b):
+    a, b = np.asarray(a, dtype=float), np.asarray(b, dtype=float)
+    return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-300))
+
+
+@pytest.mark.parametrize("p,q,r", [(37, 23, 3), (700, 41, 10), (130, 96, 1)])
+def test_fp32_storage_em_matches_oracle_on_rounded_data(p, q, r):
+    X, Y, th0 = make_problem(333, p, q, r, seed=40 + r)
+    X32, Y32 = _round32(X), _round32(Y)
+    with _ctx32() as c:
+        c.set_data(X, Y)
+        Xb, Yb = c.get_data()
+        assert np.array_equal(Xb, X32) and np.array_equal(Yb, Y32)
+        sx, sy = c.ssq()
+        assert np.isclose(sx, np.sum(X32 * X32), rtol=1e-13)
+        est, ll, _, _ = c.em_run(_theta(th0), 6, -np.inf, 0, want_eout=False)
+    ref = o.ppls_simult(X32, Y32, r, EMsteps=6, atol=-np.inf, theta0=th0)
+    assert _relerr(ll, ref["loglik"]) < 1e-10
+    assert np.abs(est.W - ref["estimates"]["W"]).max() < 1e-8
+    assert _relerr([est.sigE, est.sigF, est.sigH], [ref["estimates"][k] for k in ("sigE", "sigF", "sigH")]) < 1e-8
+
+
+def test_fp32_synthetic_equals_rounded_fp64_synthetic():
+    from ppls_amd import Context, Theta
+    rng = np.random.default_rng(3)
+    W = np.linalg.qr(rng.standard_normal((45, 2)))[0]
+    C = np.linalg.qr(rng.standard_normal((31, 2)))[0]
+    truth = Theta(W, C, [1.2, 0.8], 0.5, 0.5, 0.1, [1.0, 0.9])
+    with Context(0) as c64, _ctx32() as c32:
+        c64.generate_synthetic(5000, 45, 31, truth, seed=77)
+        c32.generate_synthetic(5000, 45, 31, truth, seed=77)
+        X64, Y64 = c64.get_data()
+        X32, Y32 = c32.get_data()
+    assert np.array_equal(X32, _round32(X64)) and np.array_equal(Y32, _round32(Y64))
+
+
+def test_fp32_sequential_init_matches_oracle():
+    X, Y, _ = make_problem(260, 28, 19, 2, seed=44)
+    X32, Y32 = _round32(X), _round32(Y)
+    inits = [o.initial_guess(28, 19, "equal")] * 2
+    with _ctx32() as c:
+        c.set_data(X, Y)
+        f = c.ppls(2, 20, 1e-4, inits)
+    ref = o.ppls(X32, Y32, 2, 20, 1e-4, inits)
+    assert np.abs(f["W"] - ref["W"]).max() < 1e-8
+    assert _relerr(f["Other_output"]["Loglikelihoods"], ref["Other_output"]["Loglikelihoods"]) < 1e-10
