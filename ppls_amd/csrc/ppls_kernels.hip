@@ -1147,6 +1147,118 @@ __global__ __launch_bounds__(256) void ppls_panel_rowdots_kernel(
   }
 }
 
+// MFMA dots (default panel dots): Z_tile = X_tile (16 rows x K) . W (K x 16, R columns used) on
+// v_mfma_f64_16x16x4_f64.  Each wave owns 32 rows (two 16-row blocks sharing the B operand) and
+// walks the columns in 128-B tiles: a tile (32 rows x 128 B) is loaded with 16-B coalesced loads,
+// transposed through padded per-wave LDS, and each lane reads its A operands for several MFMA
+// steps with one ds_read_b128 -- the k order is permuted so that lane group g = lane >> 4 owns the
+// contiguous columns [g KT/4, (g+1) KT/4) of the tile, step s using column g KT/4 + s; the B
+// operand (lane l: W[that column][l & 15]) is a plain per-lane load of the transposed, zero-padded
+// W.  The next tile's global loads are in flight during the MFMAs.  Result lane map (f64 MFMA):
+// row (l >> 4) + 4 reg, component l & 15 -- the same for the X and the Y product, so mu_T/mu_U are
+// formed in registers.
+template <typename T, int R>
+__global__ __launch_bounds__(256) void ppls_panel_mfmadots_kernel(
+    const T* __restrict__ X, const T* __restrict__ Y, int64_t n, int ldx, int ldy,
+    const double* __restrict__ Wt, const double* __restrict__ Ct, const PplsScalars* __restrict__ sc,
+    double* __restrict__ Z, double* __restrict__ mu) {
+  typedef double d4 __attribute__((ext_vector_type(4)));
+  constexpr int ES = (int)sizeof(T);
+  constexpr int KT = 128 / ES;        // columns per tile
+  constexpr int KQ = KT / 4;          // MFMA steps per tile (columns per lane group)
+  constexpr int RB = 32;              // rows per wave
+  constexpr int RS = 144;             // padded LDS row stride (bytes)
+  constexpr int V4 = 4 * R;
+  static_assert(R <= 16, "one 16-wide MFMA tile of components");
+  __shared__ __attribute__((aligned(16))) char lds[4 * 2 * RB * RS];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int i16 = lane & 15, kq = lane >> 4;
+  const int lrow = lane >> 3, lchunk = lane & 7;   // loading: 8 lanes per row, 8 rows per load
+  const int comp = i16 < R ? i16 : 0;
+  const double al = sc->alpha[comp], be = sc->beta[comp], ga = sc->gamma[comp], de = sc->delta[comp];
+  const int64_t ntiles = (n + RB - 1) / RB;
+  for (int64_t t = (int64_t)blockIdx.x * 4 + wave; t < ntiles; t += (int64_t)gridDim.x * 4) {
+    const int64_t row0 = t * RB;
+    d4 res[2][2];   // [mat][block]
+#pragma unroll
+    for (int mat = 0; mat < 2; ++mat) {
+      const T* M = mat ? Y : X;
+      const int ld = mat ? ldy : ldx;
+      const double* Wm = mat ? Ct : Wt;
+      d4 acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
+      const T* src[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        int64_t rr = row0 + lrow + 8 * u;
+        if (rr >= n) rr = n - 1;
+        src[u] = M + rr * ld + lchunk * (16 / ES);
+      }
+      const int ntc = (ld + KT - 1) / KT;
+      float4 buf[4];
+      auto load_tile = [&](int tc) {
+        const int c0 = tc * KT + lchunk * (16 / ES);
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          buf[u] = (c0 < ld) ? *(const float4*)(src[u] + tc * KT) : make_float4(0.f, 0.f, 0.f, 0.f);
+      };
+      load_tile(0);
+      for (int tc = 0; tc < ntc; ++tc) {
+        char* wl = lds + (wave * 2 + (tc & 1)) * RB * RS;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) *(float4*)(wl + (lrow + 8 * u) * RS + lchunk * 16) = buf[u];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (tc + 1 < ntc) load_tile(tc + 1);
+        // A operands: rows i16 and 16 + i16, columns [kq KQ, kq KQ + KQ) of the tile
+        T a0[KQ], a1[KQ];
+#pragma unroll
+        for (int h = 0; h < KQ * ES / 16; ++h) {
+          const float4 v0 = *(const float4*)(wl + i16 * RS + kq * KQ * ES + h * 16);
+          const float4 v1 = *(const float4*)(wl + (16 + i16) * RS + kq * KQ * ES + h * 16);
+          const T* p0 = (const T*)&v0;
+          const T* p1 = (const T*)&v1;
+#pragma unroll
+          for (int u = 0; u < 16 / ES; ++u) {
+            a0[h * (16 / ES) + u] = p0[u];
+            a1[h * (16 / ES) + u] = p1[u];
+          }
+        }
+        // B operands: W[tile column kq KQ + s][i16] (zero for i16 >= R; Wt rows padded)
+        const double* wb = Wm + ((int64_t)tc * KT + kq * KQ) * R + comp;
+        double b[KQ];
+#pragma unroll
+        for (int s2 = 0; s2 < KQ; ++s2) b[s2] = i16 < R ? wb[s2 * R] : 0.0;
+#pragma unroll
+        for (int s2 = 0; s2 < KQ; ++s2) {
+          acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64((double)a0[s2], b[s2], acc0, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64((double)a1[s2], b[s2], acc1, 0, 0, 0);
+        }
+      }
+      res[mat][0] = acc0;
+      res[mat][1] = acc1;
+    }
+    if (i16 < R) {
+#pragma unroll
+      for (int blk = 0; blk < 2; ++blk)
+#pragma unroll
+        for (int reg = 0; reg < 4; ++reg) {
+          const int64_t row = row0 + 16 * blk + kq + 4 * reg;
+          if (row >= n) continue;
+          const double a = res[0][blk][reg], bb = res[1][blk][reg];
+          const double mt = al * a + be * bb, mu_u = ga * a + de * bb;
+          double* zr = Z + row * V4;
+          zr[i16] = a;
+          zr[R + i16] = bb;
+          zr[2 * R + i16] = mt;
+          zr[3 * R + i16] = mu_u;
+          if (mu) {
+            mu[(int64_t)i16 * n + row] = mt;
+            mu[(int64_t)(R + i16) * n + row] = mu_u;
+          }
+        }
+    }
+  }
+}
+
 // W (ldx x R, column-major) -> Wt (ldxp x R, row-major, rows >= ldx zero); same for C.
 __global__ void ppls_transpose_wc_kernel(const double* __restrict__ W, const double* __restrict__ C,
                                          int ldx, int ldy, int ldxp, int ldyp, int r, double* __restrict__ Wt,
@@ -2499,8 +2611,13 @@ hipError_t launch_panel_t(const PplsSweepArgs* a, const T* X, const T* Y, double
                      a->Cp, a->ldx, a->ldy, ldxp, ldyp, R, Wt, Ct);
   // measured at the C5 shape (tools/panel_experiment.py): tiled dots is faster for fp64 storage
   // (8.6 vs 13.1 ms), row-per-lane dots for fp32 storage (6.7 vs 7.5 ms); ablate bit 5 flips it
-  const bool tiled = (sizeof(T) == 8) != ((a->ablate & 32) != 0);
-  if (tiled) {
+  const int dots = (a->ablate >> 5) & 3;   // 0 MFMA (default), 1 tiled VALU, 2 row-per-lane VALU
+  if (dots == 0) {
+    const int64_t wtiles = (a->n_local + 31) / 32;
+    const int mblocks = (int)((wtiles + 3) / 4 < 16384 ? (wtiles + 3) / 4 : 16384);
+    hipLaunchKernelGGL((ppls_panel_mfmadots_kernel<T, R>), dim3(mblocks), dim3(256), 0, st, X, Y,
+                       a->n_local, a->ldx, a->ldy, Wt, Ct, a->sc, Z, a->write_mu ? a->mu : nullptr);
+  } else if (dots == 1) {
     hipLaunchKernelGGL((ppls_panel_dots_kernel<T, R>), dim3(blocks), dim3(256), 0, st, X, Y, a->n_local,
                        a->ldx, a->ldy, Wt, Ct, a->sc, Z, a->write_mu ? a->mu : nullptr);
   } else {

@@ -1,4 +1,4 @@
-"""Panel sweep variants on the C5 shape (timing only): row-per-lane dots (default) vs tiled dots."""
+"""Panel sweep dots variants on the C5 shape (timing only): MFMA (default), tiled VALU, row-per-lane VALU."""
 import os
 import sys
 import time
@@ -21,7 +21,7 @@ def main():
     ctx.set_option("sweep", 3)
     ctx.em_begin(th0)
     for rep in range(2):
-        for ab, name in ((0, "rowdots"), (32, "tiled")):
+        for ab, name in ((0, "mfma"), (32, "tiled"), (64, "rowdots")):
             ctx.set_option("ablate", ab)
             ctx.em_iterate(1)
             ctx.synchronize()
