@@ -621,7 +621,7 @@ int ppls_set_option(ppls_ctx* c, const char* key, int64_t value) {
   } else if (!strcmp(key, "pipe")) {
     c->pipe_opt = value ? 1 : 0;
   } else if (!strcmp(key, "ablate")) {
-    if (value < 0 || value > 127) return fail(c, PPLS_E_ARG, "ablate must be in [0,127]");
+    if (value < 0 || value > 255) return fail(c, PPLS_E_ARG, "ablate must be in [0,255]");
     c->ablate = (int)value;   // timing experiments only: results are wrong while set
   } else if (!strcmp(key, "ftrace")) {
     if (value && !c->ftrace) {

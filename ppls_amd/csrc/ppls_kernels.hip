@@ -2597,6 +2597,108 @@ hipError_t ppls_launch_accumulate(const PplsSweepArgs* a, const double* Z, hipSt
 
 // ---- panel sweep launchers
 }  // extern "C"
+// MFMA accumulation (experimental panel acc, see the launcher): S = X' mu over a row chunk on v_mfma_f64_16x16x4_f64,
+// A = X' (16 columns x 4 rows), B = mu (4 rows x 16 components, R used).  Each wave owns 64
+// columns as 4 MFMA blocks with the column assignment permuted (block b, A-row i <-> column
+// 4 i + b), so one lane's 4 consecutive columns of a row -- one 16-B (fp32) or two 16-B (fp64)
+// coalesced loads -- are its A operands for all 4 blocks; the B operand (lane l: mu[row l >> 4]
+// [component l & 15]) is shared by the blocks.  Result (f64 MFMA lane map): column
+// 4 ((l >> 4) + 4 reg) + b, component l & 15.  Gram of [Xw Yc] as in ppls_panel_acc_kernel.
+template <typename T, int R>
+__global__ __launch_bounds__(256) void ppls_panel_mfmaacc_kernel(
+    const T* __restrict__ X, const T* __restrict__ Y, int64_t n, int ldx, int ldy,
+    const double* __restrict__ Z, int64_t rows_per_chunk, double* __restrict__ part, int64_t part_ld) {
+  typedef double d4 __attribute__((ext_vector_type(4)));
+  constexpr int V4 = 4 * R;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int i16 = lane & 15, kq = lane >> 4;
+  const int ntx = (ldx + 255) / 256;   // 256 columns per workgroup
+  const bool isx = (int)blockIdx.x < ntx;
+  const int ld = isx ? ldx : ldy;
+  const int cbase = (isx ? blockIdx.x : blockIdx.x - ntx) * 256 + wave * 64;
+  const int mycol = cbase + 4 * i16;   // this lane's 4 columns
+  const T* M = isx ? X : Y;
+  const int off = isx ? 2 * R : 3 * R;
+  const int64_t r0 = (int64_t)blockIdx.y * rows_per_chunk;
+  const int64_t r1 = min(n, r0 + rows_per_chunk);
+  double* pg = part + (int64_t)blockIdx.y * part_ld;
+  const bool colok = mycol < ld;   // ld is a multiple of 4 (fp32) / 2 (fp64): whole vectors
+  const bool colok2 = mycol + 2 < ld;
+  d4 acc[4];
+#pragma unroll
+  for (int b = 0; b < 4; ++b) acc[b] = (d4){0.0, 0.0, 0.0, 0.0};
+  if (cbase < ld) {
+    const T* base = M + mycol;
+    auto ldx4 = [&](int64_t row, double (&v)[4]) {
+      if (sizeof(T) == 4) {
+        const float4 f = (colok && row < r1) ? *(const float4*)(base + row * ld) : make_float4(0.f, 0.f, 0.f, 0.f);
+        v[0] = f.x; v[1] = f.y; v[2] = f.z; v[3] = f.w;
+      } else {
+        const double2 d0 = (colok && row < r1) ? *(const double2*)(base + row * ld) : make_double2(0.0, 0.0);
+        const double2 d1 = (colok2 && row < r1) ? *(const double2*)(base + row * ld + 2) : make_double2(0.0, 0.0);
+        v[0] = d0.x; v[1] = d0.y; v[2] = d1.x; v[3] = d1.y;
+      }
+    };
+    for (int64_t rb = r0; rb < r1; rb += 16) {   // 4 MFMA steps of 4 rows, loads issued together
+      double xv[4][4], mv[4];
+#pragma unroll
+      for (int st = 0; st < 4; ++st) {
+        const int64_t row = rb + 4 * st + kq;
+        ldx4(row, xv[st]);
+        mv[st] = (i16 < R && row < r1) ? Z[row * V4 + off + i16] : 0.0;
+      }
+#pragma unroll
+      for (int st = 0; st < 4; ++st)
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+          acc[b] = __builtin_amdgcn_mfma_f64_16x16x4f64(xv[st][b], mv[st], acc[b], 0, 0, 0);
+    }
+    if (i16 < R) {
+      double* dst = (isx ? pg : pg + (int64_t)R * ldx) + (int64_t)i16 * ld;
+#pragma unroll
+      for (int b = 0; b < 4; ++b)
+#pragma unroll
+        for (int reg = 0; reg < 4; ++reg) {
+          const int col = cbase + 4 * (kq + 4 * reg) + b;
+          if (col < ld) dst[col] = acc[b][reg];
+        }
+    }
+  }
+  if (blockIdx.x == 0) {   // Gram of [Xw Yc] over the chunk (2R x 2R, column-major)
+    constexpr int V2 = 2 * R, NP = V2 * (V2 + 1) / 2, BR = 64;
+    __shared__ double sz[BR * V2];
+    double* G2 = pg + (int64_t)R * ldx + (int64_t)R * ldy;
+    double gs[(NP + 255) / 256];
+    int pi[(NP + 255) / 256], pj[(NP + 255) / 256];
+#pragma unroll
+    for (int u = 0; u < (NP + 255) / 256; ++u) {
+      gs[u] = 0.0;
+      int e = tid + 256 * u, i = 0;
+      while (e >= V2 - i && i < V2) { e -= V2 - i; ++i; }
+      pi[u] = i;
+      pj[u] = i + e;
+    }
+    for (int64_t b0 = r0; b0 < r1; b0 += BR) {
+      __syncthreads();
+      for (int e = tid; e < BR * V2; e += 256) {
+        const int rr = e / V2, f = e - rr * V2;
+        sz[e] = (b0 + rr < r1) ? Z[(b0 + rr) * V4 + f] : 0.0;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int u = 0; u < (NP + 255) / 256; ++u)
+        if (tid + 256 * u < NP)
+          for (int rr = 0; rr < BR; ++rr) gs[u] = fma(sz[rr * V2 + pi[u]], sz[rr * V2 + pj[u]], gs[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < (NP + 255) / 256; ++u)
+      if (tid + 256 * u < NP) {
+        G2[pj[u] * V2 + pi[u]] = gs[u];
+        G2[pi[u] * V2 + pj[u]] = gs[u];
+      }
+  }
+}
+
 namespace {
 template <typename T, int R>
 hipError_t launch_panel_t(const PplsSweepArgs* a, const T* X, const T* Y, double* Z, int chunks, hipStream_t st) {
@@ -2627,10 +2729,19 @@ hipError_t launch_panel_t(const PplsSweepArgs* a, const T* X, const T* Y, double
                        a->n_local, a->ldx, a->ldy, Wt, Ct, a->sc, Z, a->write_mu ? a->mu : nullptr);
   }
   constexpr int VEC = PplsVec16<T>::N;
-  const int ntx = (a->ldx + 256 * VEC - 1) / (256 * VEC), nty = (a->ldy + 256 * VEC - 1) / (256 * VEC);
   const int64_t rpc = (a->n_local + chunks - 1) / chunks;
-  hipLaunchKernelGGL((ppls_panel_acc_kernel<T, R>), dim3(ntx + nty, chunks), dim3(256), 0, st, X, Y,
-                     a->n_local, a->ldx, a->ldy, Z, rpc, a->part, a->part_ld);
+  // VALU accumulation is the default: measured at C5 (profiles/r1_c5_*_acc_variants.txt) the MFMA
+  // form is no faster in fp64 storage (7.7 vs 7.5 ms) and slower in fp32 (6.0 vs 4.5 ms), since the
+  // pass is bound by its load stream, not by FMA issue; ablate bit 7 selects the MFMA form
+  if (!(a->ablate & 128)) {
+    const int ntx = (a->ldx + 256 * VEC - 1) / (256 * VEC), nty = (a->ldy + 256 * VEC - 1) / (256 * VEC);
+    hipLaunchKernelGGL((ppls_panel_acc_kernel<T, R>), dim3(ntx + nty, chunks), dim3(256), 0, st, X, Y,
+                       a->n_local, a->ldx, a->ldy, Z, rpc, a->part, a->part_ld);
+  } else {
+    const int ntx = (a->ldx + 255) / 256, nty = (a->ldy + 255) / 256;
+    hipLaunchKernelGGL((ppls_panel_mfmaacc_kernel<T, R>), dim3(ntx + nty, chunks), dim3(256), 0, st, X, Y,
+                       a->n_local, a->ldx, a->ldy, Z, rpc, a->part, a->part_ld);
+  }
   return hipGetLastError();
 }
 

@@ -21,7 +21,7 @@ def main():
     ctx.set_option("sweep", 3)
     ctx.em_begin(th0)
     for rep in range(2):
-        for ab, name in ((0, "mfma"), (32, "tiled"), (64, "rowdots")):
+        for ab, name in ((0, "mfma dots + valu acc"), (128, "mfma dots + mfma acc"), (32, "tiled dots + valu acc")):
             ctx.set_option("ablate", ab)
             ctx.em_iterate(1)
             ctx.synchronize()
