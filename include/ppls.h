@@ -128,6 +128,10 @@ int ppls_em_state(ppls_ctx* ctx, ppls_theta* out, double* loglik, int loglik_cap
  * initialGuess draws the R side makes (:126-145).  Stop rule per component: increment < atol
  * (critfunc = identity), no constraints.  If a component's sigE or sigF falls below
  * 100 * DBL_EPSILON the fit stops there (:152-154, :258-263): ncomp < a. */
+/* scores.PPLS (Package/PPLS/R/EM_W_multi.R:411-420): T = X W (n_local x k), U = Y C (n_local x k),
+ * column-major, for this rank's rows; one pass over the resident data.  T or U may be NULL. */
+int ppls_scores(ppls_ctx* ctx, const double* W, const double* C, int k, double* T, double* U);
+
 typedef struct {
   double* W;               /* p x a, column-major (R's W) */
   double* C;               /* q x a */

@@ -18,6 +18,8 @@ Every function cites the reference line it restates (paths relative to /root/ref
 * ``pplsi``              Package/PPLS/R/EM_W_multi.R:116-180 (one direction; no constraints, critfunc = I)
 * ``ppls``               Package/PPLS/R/EM_W_multi.R:229-279 (sequential fit with deflation)
 * ``initial_guess``      Package/PPLS/R/EM_W_multi.R:126-140 ('equal'; 'random' with numpy draws)
+* ``scores_ppls``        Package/PPLS/R/EM_W_multi.R:411-420
+* ``ppls_simult_to_o2m`` Package/PPLS/R/PPLS_to_o2m.R:82-140
 * ``orth``               OmicsPLS::orth (not vendored); semantics Package/functions.R:252-260
 * ``ssq``                OmicsPLS::ssq (not vendored); semantics Package/functions.R:380-385
 
@@ -487,3 +489,29 @@ def simult_theta0_from_ppls(f0):
     a = f0["W"].shape[1]
     return dict(W=f0["W"], C=f0["C"], B=np.diag(f0["B"]), sigE=f0["sig"][a - 1, 0],
                 sigF=f0["sig"][a - 1, 1], sigH=f0["sig"][a - 1, 2], sigT=np.diag(f0["sig"][:, 3]))
+
+
+# ----------------------------------------------------------------------------- outputs after the path
+
+def scores_ppls(W, C, X, Y, subset=None):
+    """scores.PPLS -- Package/PPLS/R/EM_W_multi.R:411-420 (subset: 1-based component indices)."""
+    cols = list(range(W.shape[1])) if subset is None else [int(s) - 1 for s in np.atleast_1d(subset)]
+    if len(cols) == 1:
+        return np.concatenate([X @ W[:, cols[0]], Y @ C[:, cols[0]]])
+    return np.vstack([X @ W[:, cols], Y @ C[:, cols]])
+
+
+def ppls_simult_to_o2m(X, Y, fit):
+    """PPLS_simult_to_o2m -- Package/PPLS/R/PPLS_to_o2m.R:82-140 (the numeric fields)."""
+    est, E = fit["estimates"], fit["Expectations"]
+    W, C, B_T = est["W"], est["C"], est["B"]
+    p, q, r = X.shape[1], Y.shape[1], W.shape[1]
+    Tt, U = E["mu_T"], E["mu_U"]
+    sT, B, sE, sF, sH = est["sigT"], est["B"], est["sigE"], est["sigF"], est["sigH"]
+    R2Xcorr = ssq(sT @ sT) / (ssq(sT @ sT) + p * sE ** 2)                       # :109
+    v = sT @ sT @ B @ B + np.diag(np.full(r, sH ** 2))
+    R2Ycorr = ssq(v) / (ssq(v) + q * sF ** 2)                                    # :110
+    R2Yhat = ssq(sT @ sT @ B) / (ssq(sT @ sT @ B @ B) + r * sH ** 2 + q * sF ** 2)   # :114
+    return dict(Tt=Tt, U=U, W_=W, C_=C, B_T_=B_T, B_U=np.linalg.inv(B_T), H_UT=U - Tt @ B_T,
+                R2X=R2Xcorr, R2Y=R2Ycorr, R2Xcorr=R2Xcorr, R2Ycorr=R2Ycorr, R2Yhat=R2Yhat,
+                ssqX=ssq(X), ssqY=ssq(Y), varXjoint=np.sum(Tt * Tt, axis=0), varYjoint=np.sum(U * U, axis=0))

@@ -71,6 +71,7 @@ SIGNATURES = {
     "ppls_em_iterate": (ct.c_int, [ct.c_void_p, ct.c_int, ct.c_int]),
     "ppls_em_state": (ct.c_int, [ct.c_void_p, ct.POINTER(PplsTheta), _dp, ct.c_int, ct.POINTER(ct.c_int)]),
     "ppls_synchronize": (ct.c_int, [ct.c_void_p]),
+    "ppls_scores": (ct.c_int, [ct.c_void_p, _dp, _dp, ct.c_int, _dp, _dp]),
     "ppls_ppls": (ct.c_int, [ct.c_void_p, ct.c_int, ct.c_int, ct.c_double, ct.POINTER(PplsTheta),
                              ct.POINTER(PplsSeqFit)]),
     "ppls_sweep_timing": (ct.c_int, [ct.c_void_p, _dp, ct.POINTER(ct.c_int64), ct.c_int]),

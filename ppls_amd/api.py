@@ -221,6 +221,18 @@ class Context:
                                       logvalue=[lv[i, :nst[i] + 1].copy() for i in range(k)]),
                     not_monotone=[bool(fit.not_monotone >> i & 1) for i in range(k)], ncomp=k)
 
+    def scores(self, W, C):
+        """scores.PPLS (EM_W_multi.R:411-420) on the resident rows: (X W, Y C), n_local x k each."""
+        W = np.asfortranarray(np.array(W, dtype=np.float64, ndmin=2).reshape(self.p, -1))
+        C = np.asfortranarray(np.array(C, dtype=np.float64, ndmin=2).reshape(self.q, -1))
+        k = W.shape[1]
+        if C.shape[1] != k:
+            raise ValueError("W and C need the same number of components")
+        T = np.zeros((self.n_local, k), order="F")
+        U = np.zeros((self.n_local, k), order="F")
+        self._chk(self._L.ppls_scores(self.h, dptr(W), dptr(C), int(k), dptr(T), dptr(U)))
+        return T, U
+
     def synchronize(self):
         self._chk(self._L.ppls_synchronize(self.h))
 
@@ -420,6 +432,56 @@ def PPLSi(X, Y, EMsteps=100, atol=1e-4, initialGuess=("equal", "o2m", "random", 
     return dict(W=fit["W"][:, 0], C=fit["C"][:, 0], B=fit["B"][0], sig=fit["sig"][0],
                 logvalue=oo["logvalue"][0], Last_increment=oo["Last_increment"][0],
                 Number_steps=int(oo["Number_steps"][0]))
+
+
+def scores_PPLS(fit, X, Y, subset=None, ctx=None):
+    """scores.PPLS (EM_W_multi.R:411-420): rbind(X W[, subset], Y C[, subset]) (a vector when one
+    component is selected); X W and Y C are computed on the GPU in one pass.  ``fit``: a PPLS list
+    (W, C) or a PPLS_simult list (estimates$W, estimates$C)."""
+    ctx = _ctx_with(X, Y, ctx)
+    est = fit.get("estimates", fit)
+    W, C = np.asarray(est["W"]), np.asarray(est["C"])
+    cols = list(range(W.shape[1])) if subset is None else [int(s) - 1 for s in np.atleast_1d(subset)]
+    T, U = ctx.scores(W[:, cols], C[:, cols])
+    if len(cols) == 1:
+        return np.concatenate([T[:, 0], U[:, 0]])
+    return np.vstack([T, U])
+
+
+def PPLS_simult_to_o2m(X_true, Y_true, fit_PPLS, ctx=None):
+    """PPLS_simult_to_o2m (PPLS_to_o2m.R:82-140): the fit as an OmicsPLS "o2m" list.  Host-side
+    bookkeeping on the fit's Expectations (mu_T, mu_U from the device Eout) and estimates; the
+    only data terms, ssq(X) and ssq(Y), come from the context (computed on the device at load)."""
+    ctx = _ctx_with(X_true, Y_true, ctx)
+    est, E = fit_PPLS["estimates"], fit_PPLS["Expectations"]
+    W, C = np.asarray(est["W"]), np.asarray(est["C"])
+    r = W.shape[1]
+    B_T = np.asarray(est["B"])
+    Tt, U = np.asarray(E["mu_T"]), np.asarray(E["mu_U"])
+    p, q = W.shape[0], C.shape[0]
+    sT, B = np.asarray(est["sigT"]), np.asarray(est["B"])
+    sE, sF, sH = float(est["sigE"]), float(est["sigF"]), float(est["sigH"])
+
+    def ssq(A):
+        A = np.asarray(A, dtype=np.float64)
+        return float(np.sum(A * A))
+    ssqX, ssqY = ctx.ssq()
+    R2Xcorr = ssq(sT @ sT) / (ssq(sT @ sT) + p * sE ** 2)
+    v = sT @ sT @ B @ B + np.diag(np.full(r, sH ** 2))
+    R2Ycorr = ssq(v) / (ssq(v) + q * sF ** 2)
+    R2Yhat = ssq(sT @ sT @ B) / (ssq(sT @ sT @ B @ B) + r * sH ** 2 + q * sF ** 2)
+    P_Yosc = np.zeros((p, 1))
+    P_Xosc = np.zeros((q, 1))
+    model = dict(Tt=Tt, U=U, W_=W, C_=C, P_Yosc_=P_Yosc, P_Xosc_=P_Xosc, T_Yosc_=np.zeros((Tt.shape[0], 1)),
+                 U_Xosc_=np.zeros((Tt.shape[0], 1)), W_Yosc=np.zeros((p, 1)), C_Xosc=np.zeros((q, 1)),
+                 B_T_=B_T, B_U=np.linalg.inv(B_T), H_TU=0 * Tt, H_UT=U - Tt @ B_T,
+                 R2X=R2Xcorr + 0, R2Y=R2Ycorr + 0, R2Xcorr=R2Xcorr, R2Ycorr=R2Ycorr, R2Xhat=float("nan"),
+                 R2Yhat=R2Yhat)
+    model["flags"] = dict(time=float("nan"), n=r, nx=0, ny=0, stripped=True, highd=False, ssqX=ssqX, ssqY=ssqY,
+                          varXjoint=np.sum(Tt * Tt, axis=0), varYjoint=np.sum(U * U, axis=0),
+                          varXorth=np.zeros(1), varYorth=np.zeros(1))
+    model["class"] = ["o2m", "o2m_stripped"]
+    return model
 
 
 def PPLS_simult(X, Y, a, EMsteps=10, atol=1e-4, type=("SVD", "QR"), init=None, ctx=None, **kw):

@@ -159,6 +159,7 @@ PplsScalars scalars_of(const ppls_theta* th, int r) {
 
 int ensure_r(ppls_ctx* c, int r, int max_steps) {
   int rc;
+  c->em_active = false;   // every entry point that (re)stages theta ends an ppls_em_begin session
   if (r != c->r_alloc) {
     for (int i = 0; i < 2; ++i) {
       if ((rc = dalloc(c, &c->W[i], (size_t)c->ldx * r))) return rc;
@@ -1251,6 +1252,44 @@ int ppls_ppls(ppls_ctx* c, int a, int max_steps, double atol, const ppls_theta* 
       out->loglikelihoods[k] = ppls_loglik_from_gram(Gf.data(), c->ssq_host[0], c->ssq_host[1], N, p, q, r, &s);
     }
   }
+  return PPLS_OK;
+}
+
+// scores.PPLS (EM_W_multi.R:411-420): T = X W, U = Y C (local rows, column-major n_local x k) in
+// one pass -- the panel dots kernel with mu coefficients (1, 0; 0, 1), whose mu write-out is then
+// exactly [X W | Y C].
+int ppls_scores(ppls_ctx* c, const double* W, const double* C, int k, double* T, double* U) {
+  if (!c) return PPLS_E_ARG;
+  if (!c->have_data) return fail(c, PPLS_E_STATE, "no data");
+  if (!W || !C || k < 1 || k > PPLS_RMAX) return fail(c, PPLS_E_ARG, "W, C must be given with 1 <= k <= %d", PPLS_RMAX);
+  HIPCHK(c, hipSetDevice(c->device));
+  int rc;
+  if ((rc = ensure_r(c, k, 1))) return rc;
+  std::vector<double> B(k, 1.0), sT(k, 1.0);
+  ppls_theta th = {const_cast<double*>(W), const_cast<double*>(C), B.data(), sT.data(), 1.0, 1.0, 1.0};
+  if ((rc = upload_theta(c, &th, k, 0))) return rc;
+  PplsScalars s;
+  memset(&s, 0, sizeof s);
+  for (int j = 0; j < k; ++j) { s.alpha[j] = 1.0; s.delta[j] = 1.0; }
+  HIPCHK(c, hipMemcpyAsync(c->sc[0], &s, sizeof s, hipMemcpyHostToDevice, c->stream));
+  if (c->z_cols < 4 * k) {
+    dfree(c->Z);
+    c->z_cols = 0;
+    if ((rc = dalloc(c, &c->Z, (size_t)ppls_panel_z_len(c->n_local, c->ldx, c->ldy, k)))) return rc;
+    c->z_cols = 4 * k;
+  }
+  dfree(c->mu);
+  if ((rc = dalloc(c, &c->mu, (size_t)std::max<int64_t>(c->n_local, 1) * 2 * k))) return rc;
+  PplsSweepArgs a;
+  memset(&a, 0, sizeof a);
+  a.X = c->X; a.Y = c->Y; a.n_local = c->n_local; a.p = c->p; a.q = c->q; a.ldx = c->ldx; a.ldy = c->ldy;
+  a.Wp = c->W[0]; a.Cp = c->C[0]; a.sc = c->sc[0]; a.mu = c->mu; a.write_mu = 1; a.r = k;
+  HIPCHK(c, ppls_launch_panel_dots(&a, c->dtype, c->Z, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  const size_t blk = sizeof(double) * (size_t)c->n_local * k;
+  if (c->n_local > 0 && T) HIPCHK(c, hipMemcpy(T, c->mu, blk, hipMemcpyDeviceToHost));
+  if (c->n_local > 0 && U) HIPCHK(c, hipMemcpy(U, c->mu + (size_t)c->n_local * k, blk, hipMemcpyDeviceToHost));
+  dfree(c->mu);   // sized for this k; the EM path re-allocates its own
   return PPLS_OK;
 }
 

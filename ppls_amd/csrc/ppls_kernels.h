@@ -70,6 +70,8 @@ int ppls_twopass_groups(int64_t n_local, int grid);
 int ppls_panel_chunks(int64_t n_local, int ldx, int ldy, int num_cus);
 int64_t ppls_panel_z_len(int64_t n_local, int ldx, int ldy, int r);   // doubles of Z (+ transposed W, C)
 hipError_t ppls_launch_sweep_panel(const PplsSweepArgs* a, int dtype_f32, double* Z, int chunks, hipStream_t st);
+// dots pass only: Z = [Xw | Yc | mu_T | mu_U] and (if a->write_mu) mu (n x 2r column-major)
+hipError_t ppls_launch_panel_dots(const PplsSweepArgs* a, int dtype_f32, double* Z, hipStream_t st);
 hipError_t ppls_launch_reduce(const double* part, int ngroups, int64_t ld, int64_t len, double* out,
                               int accumulate, hipStream_t st);
 hipError_t ppls_launch_finalize(const PplsFinalizeArgs* f, hipStream_t st);

@@ -2729,6 +2729,7 @@ hipError_t launch_panel_t(const PplsSweepArgs* a, const T* X, const T* Y, double
                        a->n_local, a->ldx, a->ldy, Wt, Ct, a->sc, Z, a->write_mu ? a->mu : nullptr);
   }
   constexpr int VEC = PplsVec16<T>::N;
+  if (a->ablate & 256) return hipGetLastError();   // dots only (scores)
   const int64_t rpc = (a->n_local + chunks - 1) / chunks;
   // VALU accumulation is the default: measured at C5 (profiles/r1_c5_*_acc_variants.txt) the MFMA
   // form is no faster in fp64 storage (7.7 vs 7.5 ms) and slower in fp32 (6.0 vs 4.5 ms), since the
@@ -2783,6 +2784,14 @@ int ppls_panel_chunks(int64_t n_local, int ldx, int ldy, int num_cus) {
   if (ch < 1) ch = 1;
   if (ch > 1024) ch = 1024;
   return (int)ch;
+}
+
+hipError_t ppls_launch_panel_dots(const PplsSweepArgs* a, int dtype_f32, double* Z, hipStream_t st) {
+  if (a->n_local <= 0) return hipSuccess;
+  PplsSweepArgs b = *a;
+  b.ablate = a->ablate | 256;   // dots only
+  if (dtype_f32) return launch_panel_dt<float>(&b, (const float*)a->X, (const float*)a->Y, Z, 0, st);
+  return launch_panel_dt<double>(&b, a->X, a->Y, Z, 0, st);
 }
 
 hipError_t ppls_launch_sweep_panel(const PplsSweepArgs* a, int dtype_f32, double* Z, int chunks, hipStream_t st) {

@@ -122,3 +122,36 @@ def test_ppls_multi_component_shapes_and_orthogonality(ctx):
     assert np.allclose(f["W"].T @ f["W"], np.eye(5), atol=1e-12)
     assert np.abs(f["W"] - ref["W"]).max() < 1e-8
     assert _relerr(f["Other_output"]["Loglikelihoods"], ref["Other_output"]["Loglikelihoods"]) < 1e-10
+
+
+def test_scores_and_to_o2m_match_oracle(ctx):
+    """scores.PPLS (:411-420) through the one-pass device kernel and PPLS_simult_to_o2m
+    (PPLS_to_o2m.R:82-140) on a device fit, against the oracle restatements."""
+    from ppls_amd import PPLS_simult, PPLS_simult_to_o2m, scores_PPLS
+    X, Y, th0 = make_problem(350, 26, 21, 3, seed=51)
+    fit = PPLS_simult(X, Y, 3, EMsteps=8, atol=-np.inf, init=th0, ctx=ctx)
+    sc = scores_PPLS(fit, X, Y, ctx=ctx)
+    ref = o.scores_ppls(fit["estimates"]["W"], fit["estimates"]["C"], X, Y)
+    assert sc.shape == (700, 3) and np.abs(sc - ref).max() < 1e-11 * np.abs(ref).max()
+    one = scores_PPLS(fit, None, None, subset=2, ctx=ctx)
+    assert np.allclose(one, o.scores_ppls(fit["estimates"]["W"], fit["estimates"]["C"], X, Y, subset=2),
+                       rtol=1e-12, atol=1e-12)
+    m = PPLS_simult_to_o2m(None, None, fit, ctx=ctx)
+    r = o.ppls_simult_to_o2m(X, Y, fit)
+    for key in ("R2Xcorr", "R2Ycorr", "R2Yhat"):
+        assert np.isclose(m[key], r[key], rtol=1e-13), key
+    assert np.allclose(m["H_UT"], r["H_UT"], atol=1e-12)
+    assert np.isclose(m["flags"]["ssqX"], r["ssqX"], rtol=1e-12)
+
+
+def test_scores_fp32_storage(ctx):
+    from ppls_amd import Context
+    X, Y, th0 = make_problem(300, 33, 17, 2, seed=52)
+    with Context(0) as c32:
+        c32.set_option("dtype", 1)
+        c32.set_data(X, Y)
+        T, U = c32.scores(th0["W"], th0["C"])
+    X32 = X.astype(np.float32).astype(np.float64)
+    Y32 = Y.astype(np.float32).astype(np.float64)
+    assert np.allclose(T, X32 @ th0["W"], rtol=1e-12, atol=1e-12)
+    assert np.allclose(U, Y32 @ th0["C"], rtol=1e-12, atol=1e-12)
