@@ -1043,110 +1043,6 @@ __global__ __launch_bounds__(256) void ppls_panel_dots_kernel(
   }
 }
 
-// Row-per-lane dots (the default panel dots): each wave owns 64 rows, one per lane, and walks the
-// columns in 128-B tiles (KT = 128 / sizeof(T) columns).  A tile (64 rows x 128 B) is loaded with
-// 16-B coalesced loads (8 lanes per row), transposed through a padded per-wave LDS buffer
-// (row stride 144 B: conflict-free row reads), and then each lane applies its row's KT values to
-// the R weights of each column -- the weights are wave-uniform (scalar loads, SGPR operands), so
-// no per-lane weight traffic at all.  The next tile's global loads are in flight while the
-// current one is computed.  Waves are independent (no workgroup barrier).
-template <typename T, int R>
-__global__ __launch_bounds__(256) void ppls_panel_rowdots_kernel(
-    const T* __restrict__ X, const T* __restrict__ Y, int64_t n, int ldx, int ldy,
-    const double* __restrict__ Wt, const double* __restrict__ Ct, const PplsScalars* __restrict__ sc,
-    double* __restrict__ Z, double* __restrict__ mu) {
-  constexpr int KT = 128 / (int)sizeof(T);   // columns per tile
-  constexpr int RS = 144;                    // padded LDS row stride (bytes)
-  constexpr int V4 = 4 * R;
-  __shared__ __attribute__((aligned(16))) char lds[4 * 64 * RS];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  char* wl = lds + wave * 64 * RS;
-  const int lrow = lane >> 3, lchunk = lane & 7;   // tile loading: 8 lanes per row, 8 rows per load
-  double al[R], be[R], ga[R], de[R];
-#pragma unroll
-  for (int k = 0; k < R; ++k) {
-    al[k] = sc->alpha[k];
-    be[k] = sc->beta[k];
-    ga[k] = sc->gamma[k];
-    de[k] = sc->delta[k];
-  }
-  const int64_t ntiles = (n + 63) / 64;
-  for (int64_t tile = (int64_t)blockIdx.x * 4 + wave; tile < ntiles; tile += (int64_t)gridDim.x * 4) {
-    const int64_t row0 = tile * 64;
-    const int64_t myrow = row0 + lane;
-    double ab[2][R];
-#pragma unroll
-    for (int mat = 0; mat < 2; ++mat) {
-      const T* M = mat ? Y : X;
-      const int ld = mat ? ldy : ldx;
-      const double* Wm = mat ? Ct : Wt;
-      double acc[R];
-#pragma unroll
-      for (int k = 0; k < R; ++k) acc[k] = 0.0;
-      // rows this lane loads (clamped; rows >= n contribute zeros through their lane)
-      const T* src[8];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        int64_t rr = row0 + lrow + 8 * i;
-        if (rr >= n) rr = n - 1;
-        src[i] = M + rr * ld + lchunk * (16 / (int)sizeof(T));
-      }
-      const int ntile_c = (ld + KT - 1) / KT;
-      float4 buf[8];
-      auto load_tile = [&](int tc) {
-        const int c0 = tc * KT + lchunk * (16 / (int)sizeof(T));
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-          buf[i] = (c0 < ld) ? *(const float4*)(src[i] + tc * KT) : make_float4(0.f, 0.f, 0.f, 0.f);
-      };
-      load_tile(0);
-      for (int tc = 0; tc < ntile_c; ++tc) {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) *(float4*)(wl + (lrow + 8 * i) * RS + lchunk * 16) = buf[i];
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if (tc + 1 < ntile_c) load_tile(tc + 1);   // next tile's loads overlap this tile's FMAs
-        T xr[KT];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float4 v = *(const float4*)(wl + lane * RS + j * 16);
-          const T* pv = (const T*)&v;
-#pragma unroll
-          for (int u = 0; u < 16 / (int)sizeof(T); ++u) xr[j * (16 / (int)sizeof(T)) + u] = pv[u];
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // reads done before the next writes
-        // whole tile, static trip count: Wt is zero-padded to whole tiles and X columns >= ld
-        // were loaded as zeros, so no bound check (the loop unrolls and the scalar weight loads
-        // of later columns are issued ahead of the FMAs of earlier ones)
-        const double* wt = Wm + (int64_t)tc * KT * R;   // wave-uniform
-#pragma unroll
-        for (int c = 0; c < KT; ++c) {
-          const double x = (double)xr[c];
-#pragma unroll
-          for (int k = 0; k < R; ++k) acc[k] = fma(x, wt[c * R + k], acc[k]);
-        }
-      }
-#pragma unroll
-      for (int k = 0; k < R; ++k) ab[mat][k] = acc[k];
-    }
-    if (myrow < n) {
-      double* zr = Z + myrow * V4;
-#pragma unroll
-      for (int k = 0; k < R; ++k) {
-        const double a = ab[0][k], b = ab[1][k];
-        const double mt = al[k] * a + be[k] * b, mu_u = ga[k] * a + de[k] * b;
-        zr[k] = a;
-        zr[R + k] = b;
-        zr[2 * R + k] = mt;
-        zr[3 * R + k] = mu_u;
-        if (mu) {
-          mu[(int64_t)k * n + myrow] = mt;
-          mu[(int64_t)(R + k) * n + myrow] = mu_u;
-        }
-      }
-    }
-  }
-}
-
 // MFMA dots (default panel dots): Z_tile = X_tile (16 rows x K) . W (K x 16, R columns used) on
 // v_mfma_f64_16x16x4_f64.  Each wave owns 32 rows (two 16-row blocks sharing the B operand) and
 // walks the columns in 128-B tiles: a tile (32 rows x 128 B) is loaded with 16-B coalesced loads,
@@ -1581,111 +1477,6 @@ __device__ __forceinline__ double ppls_rsq(double x) {
   return fma(0.5 * y, r, y);
 }
 
-// Round-robin (circle method) schedule of the R(R-1)/2 column pairs: N-1 rounds of N/2 disjoint
-// pairs (N = R rounded up to even; pairs with the dummy column R are dropped).
-template <int R>
-struct PplsRoundRobin {
-  static constexpr int N = R + (R & 1);
-  int i[N - 1][N / 2], j[N - 1][N / 2];
-  constexpr PplsRoundRobin() : i(), j() {
-    for (int m = 0; m < N - 1; ++m)
-      for (int k = 0; k < N / 2; ++k) {
-        const int pa = k == 0 ? 0 : ((k - 1 + m) % (N - 1)) + 1;
-        const int kb = N - 1 - k;
-        const int pb = ((kb - 1 + m) % (N - 1)) + 1;
-        i[m][k] = pa < pb ? pa : pb;
-        j[m][k] = pa < pb ? pb : pa;
-      }
-  }
-};
-
-// One-sided (Hestenes) Jacobi: A V = U Sigma, warm-started.  On entry V is orthogonal and
-// A = A0 V; on return A = U Sigma, V accumulates the rotations, sv = Sigma.  Sweeps of the
-// round-robin schedule until no pair has |a_i'a_j| >= 1e-15 ||a_i|| ||a_j|| (the stopping rule of
-// ppls_small_polar_n, ppls_math.h).  Branch-free, so the disjoint pairs of a round are
-// independent dependency chains the compiler interleaves.  Returns the sweep count.
-template <int R>
-__device__ __forceinline__ int ppls_jacobi_reg(double (&A)[R][R], double (&V)[R][R], double (&sv)[R]) {
-  constexpr PplsRoundRobin<R> rr;
-  constexpr int N = PplsRoundRobin<R>::N;
-  int sweeps = 0;
-  for (int sweep = 0; sweep < 60; ++sweep) {
-    bool rotated = false;
-    ++sweeps;
-#pragma unroll
-    for (int m = 0; m < N - 1; ++m) {
-      double cs[N / 2], sn[N / 2];
-#pragma unroll
-      for (int k = 0; k < N / 2; ++k) {
-        const int i = rr.i[m][k], j = rr.j[m][k];
-        if (j >= R) continue;
-        double a = 0.0, b = 0.0, g = 0.0;
-#pragma unroll
-        for (int t = 0; t < R; ++t) {
-          a = fma(A[t][i], A[t][i], a);
-          b = fma(A[t][j], A[t][j], b);
-          g = fma(A[t][i], A[t][j], g);
-        }
-        const bool rot = (g * g >= 1e-30 * (a * b)) && g != 0.0;
-        rotated = rotated || rot;
-        // tan = sign(z) / (|z| + sqrt(1 + z^2)), z = (b - a) / 2g;  c = u w, s = sign(z) w
-        const double z = (b - a) * ppls_rcp(rot ? 2.0 * g : 1.0);
-        const double z2 = fma(z, z, 1.0);
-        const double u = fabs(z) + z2 * ppls_rsq(z2);
-        const double w = ppls_rsq(fma(u, u, 1.0));
-        cs[k] = rot ? u * w : 1.0;
-        sn[k] = rot ? (z >= 0.0 ? w : -w) : 0.0;
-      }
-#pragma unroll
-      for (int k = 0; k < N / 2; ++k) {
-        const int i = rr.i[m][k], j = rr.j[m][k];
-        if (j >= R) continue;
-        const double c = cs[k], s = sn[k];
-#pragma unroll
-        for (int t = 0; t < R; ++t) {
-          const double x = A[t][i], y = A[t][j];
-          A[t][i] = fma(c, x, -s * y);
-          A[t][j] = fma(s, x, c * y);
-          const double vx = V[t][i], vy = V[t][j];
-          V[t][i] = fma(c, vx, -s * vy);
-          V[t][j] = fma(s, vx, c * vy);
-        }
-      }
-    }
-    if (!rotated) break;
-  }
-#pragma unroll
-  for (int i = 0; i < R; ++i) {
-    double nrm = 0.0;
-#pragma unroll
-    for (int k = 0; k < R; ++k) nrm = fma(A[k][i], A[k][i], nrm);
-    sv[i] = sqrt(nrm);
-  }
-  return sweeps;
-}
-
-// Modified Gram-Schmidt on the columns of V (restores orthogonality of a carried warm start).
-template <int R>
-__device__ __forceinline__ void ppls_mgs_reg(double (&V)[R][R]) {
-#pragma unroll
-  for (int j = 0; j < R; ++j) {
-#pragma unroll
-    for (int i = 0; i < j; ++i) {
-      double d = 0.0;
-#pragma unroll
-      for (int k = 0; k < R; ++k) d = fma(V[k][i], V[k][j], d);
-#pragma unroll
-      for (int k = 0; k < R; ++k) V[k][j] = fma(-d, V[k][i], V[k][j]);
-    }
-    double nrm = 0.0;
-#pragma unroll
-    for (int k = 0; k < R; ++k) nrm = fma(V[k][j], V[k][j], nrm);
-    const double inv = 1.0 / sqrt(nrm);
-#pragma unroll
-    for (int k = 0; k < R; ++k) V[k][j] *= inv;
-  }
-}
-
 // Block Gram of rows x (R values per thread) accumulated into the packed upper triangle.
 template <int R>
 __device__ __forceinline__ void ppls_gram_acc(const double (&x)[R], double (&vals)[R * (R + 1) / 2]) {
@@ -1716,7 +1507,9 @@ __device__ __forceinline__ double ppls_group8_sum(double v) {
 
 __device__ __forceinline__ void ppls_wave_lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
-// Pair k of round m of the circle-method schedule (PplsRoundRobin), i < j.
+// Pair k of round m of the circle-method (round-robin) schedule of the R(R-1)/2 column pairs:
+// N-1 rounds of N/2 disjoint pairs, N = R rounded up to even, pairs with the dummy column R
+// dropped by the caller; i < j.
 template <int R>
 __device__ __forceinline__ void ppls_rr_pair(int m, int k, int& i, int& j) {
   constexpr int N = R + (R & 1);
@@ -1810,7 +1603,7 @@ __device__ void ppls_matmul_wave(const double* sA, const double* sB, double* sC)
 // One-sided Jacobi on one wave: A V = U Sigma with A, V in LDS (G x G blocks).  Round m of a
 // sweep rotates the N/2 disjoint pairs of the circle-method schedule: lane group g = lane / G owns
 // pair g (+ 64/G per pass), lane t = lane % G owns row t, the column dots are G-lane DPP sums.
-// Same rotation and stopping rule as ppls_jacobi_reg / ppls_small_polar_n.  Wave-uniform.
+// Same rotation and stopping rule as ppls_small_polar_n (ppls_math.h).  Wave-uniform.
 template <int R>
 __device__ int ppls_jacobi_wave(double* sA, double* sV) {
   constexpr int N = R + (R & 1);
@@ -2713,7 +2506,7 @@ hipError_t launch_panel_t(const PplsSweepArgs* a, const T* X, const T* Y, double
                      a->Cp, a->ldx, a->ldy, ldxp, ldyp, R, Wt, Ct);
   // measured at the C5 shape (tools/panel_experiment.py): tiled dots is faster for fp64 storage
   // (8.6 vs 13.1 ms), row-per-lane dots for fp32 storage (6.7 vs 7.5 ms); ablate bit 5 flips it
-  const int dots = (a->ablate >> 5) & 3;   // 0 MFMA (default), 1 tiled VALU, 2 row-per-lane VALU
+  const int dots = (a->ablate >> 5) & 1;   // 0 MFMA (default), 1 tiled VALU (experiments)
   if (dots == 0) {
     const int64_t wtiles = (a->n_local + 31) / 32;
     const int mblocks = (int)((wtiles + 3) / 4 < 16384 ? (wtiles + 3) / 4 : 16384);
@@ -2722,11 +2515,6 @@ hipError_t launch_panel_t(const PplsSweepArgs* a, const T* X, const T* Y, double
   } else if (dots == 1) {
     hipLaunchKernelGGL((ppls_panel_dots_kernel<T, R>), dim3(blocks), dim3(256), 0, st, X, Y, a->n_local,
                        a->ldx, a->ldy, Wt, Ct, a->sc, Z, a->write_mu ? a->mu : nullptr);
-  } else {
-    const int64_t wtiles = (a->n_local + 63) / 64;
-    const int rblocks = (int)((wtiles + 3) / 4 < 16384 ? (wtiles + 3) / 4 : 16384);
-    hipLaunchKernelGGL((ppls_panel_rowdots_kernel<T, R>), dim3(rblocks), dim3(256), 0, st, X, Y,
-                       a->n_local, a->ldx, a->ldy, Wt, Ct, a->sc, Z, a->write_mu ? a->mu : nullptr);
   }
   constexpr int VEC = PplsVec16<T>::N;
   if (a->ablate & 256) return hipGetLastError();   // dots only (scores)

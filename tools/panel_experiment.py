@@ -1,4 +1,6 @@
-"""Panel sweep dots variants on the C5 shape (timing only): MFMA (default), tiled VALU, row-per-lane VALU."""
+"""Panel sweep variants on the C5 shape (timing only): MFMA dots (default) vs tiled VALU dots, VALU
+accumulation (default) vs MFMA accumulation.  (A row-per-lane VALU dots form, removed in round 1,
+measured 13.1 ms fp64 / 6.7 ms fp32 per dots pass: profiles/r1_c5_*_dots_variants.txt.)"""
 import os
 import sys
 import time
