@@ -147,6 +147,32 @@ typedef struct {
 int ppls_ppls(ppls_ctx* ctx, int a, int max_steps, double atol, const ppls_theta* init, ppls_seq_fit* out);
 int ppls_synchronize(ppls_ctx* ctx);
 
+/* ---- multi-population rank-1 fits: meta_EMstep / meta_PPLSi ----------------------------------
+ * Replace the R functions meta_EMstep (Package/PPLS/R/EM_W_multi.R:446-485) -> .Call meta_Estep /
+ * meta_Mstep (R/RcppExports.R:40-46, src/loglC.cpp:399-474) and meta_PPLSi (:509-589): one shared
+ * loading pair (W., C.) and per-population scalars (B_T, sigX, sigY, sigH, sigT).
+ * Populations are contiguous row blocks in level order: population j is global rows
+ * [N_1 + .. + N_{j-1}, N_1 + .. + N_j), exactly the reference's X[popui, ] with popui from
+ * cumsum(table(Ipopu)) (:451-458, :537-541).  pop_local[j] = rows of population j in this rank's
+ * shard (contiguous, in order; they sum to n_local), pop_total[j] = N_j over all ranks.
+ * params: npop x 5 column-major, columns B_T, sigX, sigY, sigH, sigT (params[[j]] of the reference).
+ * Each population is one r = 1 sweep over its rows (one all-reduce when sharded). */
+int ppls_meta_emstep(ppls_ctx* ctx, int npop, const int64_t* pop_local, const int64_t* pop_total,
+                     const double* W, const double* C, const double* params_in, double* W_out,
+                     double* C_out, double* params_out, double* Cxt /* p x npop, nullable */,
+                     double* Cyu /* q x npop, nullable */);
+typedef struct {
+  double* W;       /* p (out): c(Wnw) */
+  double* C;       /* q (out) */
+  double* params;  /* npop x 5 (out) */
+  double* log;     /* nullable: (EMsteps + 1) x npop column-major logvalue; row 0 = the initial
+                      rep(logl_W(X, Y, theta0), npop) (:544), rows 1..steps the EM steps; NaN padded */
+  int steps;       /* out: EM steps made (the reference's i) */
+} ppls_meta_fit;
+/* crit_abs: 0 critfunc = identity (default), 1 critfunc = abs.  init: theta with r = 1. */
+int ppls_meta_ppls(ppls_ctx* ctx, int npop, const int64_t* pop_local, const int64_t* pop_total,
+                   int max_steps, double atol, int crit_abs, const ppls_theta* init, ppls_meta_fit* out);
+
 /* loglC_fast (src/loglC.cpp:318-338) with the reference's argument list.  X, Y (column-major
  * n x p / n x q host matrices) are uploaded into ctx like Rcpp's input_parameter copies them;
  * pass X = Y = NULL to evaluate on the data already resident in ctx (zero-copy). */

@@ -20,6 +20,10 @@ Every function cites the reference line it restates (paths relative to /root/ref
 * ``initial_guess``      Package/PPLS/R/EM_W_multi.R:126-140 ('equal'; 'random' with numpy draws)
 * ``scores_ppls``        Package/PPLS/R/EM_W_multi.R:411-420
 * ``ppls_simult_to_o2m`` Package/PPLS/R/PPLS_to_o2m.R:82-140
+* ``meta_estep``         Package/PPLS/src/loglC.cpp:399-448 (one population's rank-1 E-step)
+* ``meta_mstep``         Package/PPLS/src/loglC.cpp:452-474
+* ``meta_emstep``        Package/PPLS/R/EM_W_multi.R:446-485 (populations = contiguous blocks :451-458)
+* ``meta_pplsi``         Package/PPLS/R/EM_W_multi.R:509-589 (critfunc = identity, no sigma check)
 * ``orth``               OmicsPLS::orth (not vendored); semantics Package/functions.R:252-260
 * ``ssq``                OmicsPLS::ssq (not vendored); semantics Package/functions.R:380-385
 
@@ -515,3 +519,88 @@ def ppls_simult_to_o2m(X, Y, fit):
     return dict(Tt=Tt, U=U, W_=W, C_=C, B_T_=B_T, B_U=np.linalg.inv(B_T), H_UT=U - Tt @ B_T,
                 R2X=R2Xcorr, R2Y=R2Ycorr, R2Xcorr=R2Xcorr, R2Ycorr=R2Ycorr, R2Yhat=R2Yhat,
                 ssqX=ssq(X), ssqY=ssq(Y), varXjoint=np.sum(Tt * Tt, axis=0), varYjoint=np.sum(U * U, axis=0))
+
+
+# ----------------------------------------------------------------------------- multi-population (meta_*)
+
+def meta_estep(W, C, B, X, Y, sigX, sigY, sigH, sigT, c1, c2, c3):
+    """meta_Estep -- Package/PPLS/src/loglC.cpp:399-448.  The same arithmetic as EMstepC_fast
+    (:340-397) but Cxt, Cyu are returned un-normalised, with mu_T, mu_U, Vt, Vu."""
+    e = emstepc_fast(W, C, B, X, Y, sigX, sigY, sigH, sigT, c1, c2, c3)
+    N = X.shape[0]
+    sig2X, sig2Y, sig2H, sig2T = sigX * sigX, sigY * sigY, sigH * sigH, sigT * sigT
+    v = sig2T * B * B + sig2H
+    return dict(Cxt=X.T @ e["mu_T"] / N, Cyu=Y.T @ e["mu_U"] / N, mu_T=e["mu_T"], mu_U=e["mu_U"],   # :416, :421
+                Vt=sig2T - sig2T * sig2T * (-c1 - 2 * B * c2 - B * B * (c3 - 1 / sig2Y) + 1 / sig2X),   # :441
+                Vu=v - (-(c1 - 1 / sig2X) * sig2T * sig2T * B * B - 2 * sig2T * B * v * c2
+                        - v ** 2 * (c3 - 1 / sig2Y)),                                                    # :442
+                Cut=e["Cut"], Ctt=e["Ctt"], Cee=e["Cee"], Cff=e["Cff"], Chh=e["Chh"])
+
+
+def meta_mstep(e):
+    """meta_Mstep -- Package/PPLS/src/loglC.cpp:452-474."""
+    return dict(B=e["Cut"] / e["Ctt"], sighat=np.array([math.sqrt(e["Cee"]), math.sqrt(e["Cff"])]),
+                siglathat=np.array([math.sqrt(e["Chh"]), math.sqrt(e["Ctt"])]), Cxt=e["Cxt"], Cyu=e["Cyu"])
+
+
+def _vec_orth(v):
+    """orth() of one column: v / ||v|| (Package/functions.R:252-260 semantics; OmicsPLS unpinned)."""
+    return v / np.linalg.norm(v)
+
+
+def meta_emstep(X, Y, W, C, pop_sizes, params):
+    """meta_EMstep -- Package/PPLS/R/EM_W_multi.R:446-485.  pop_sizes = table(Ipopu) in level order;
+    population j is the contiguous row block X[(1+Ni[j]):Ni[j+1], ] (:455-458).  params[j]: dict
+    B_T, sigX, sigY, sigH, sigT.  Returns dict(pops=[meta_Mstep list per population], W, C)."""
+    W, C = np.ravel(W), np.ravel(C)
+    Ni = np.concatenate([[0], np.cumsum(pop_sizes)])
+    ret = []
+    for j in range(len(pop_sizes)):                                                  # :453
+        Xj, Yj = X[Ni[j]:Ni[j + 1]], Y[Ni[j]:Ni[j + 1]]
+        pp = params[j]
+        B, sX, sY, sH, sT = (float(np.ravel(pp[k])[0]) for k in ("B_T", "sigX", "sigY", "sigH", "sigT"))
+        g = sT ** 2 * B ** 2 + sH ** 2                                               # :466-474
+        Kw = sT ** 2 - sT ** 4 * B ** 2 / sY ** 2 + sT ** 4 * B ** 2 * g / (sY ** 2 * (g + sY ** 2))
+        Kc = g - sT ** 4 * B ** 2 / sX ** 2 + sT ** 6 * B ** 2 / (sX ** 2 * (sT ** 2 + sX ** 2))
+        Kwc = (sT ** 2 * B / (sX ** 2 * sY ** 2) - Kc * sT ** 2 * B / (sX ** 2 * sY ** 2 * (Kc + sY ** 2))
+               - sT ** 4 * B / (sX ** 2 * sY ** 2 * (sT ** 2 + sX ** 2))
+               + Kc * sT ** 4 * B / (sX ** 2 * sY ** 2 * (Kc + sY ** 2) * (sT ** 2 + sX ** 2)))
+        c1 = Kw / (sX ** 2 * (Kw + sX ** 2))
+        c3 = Kc / (sY ** 2 * (Kc + sY ** 2))
+        e = meta_estep(W, C, B, Xj, Yj, sX, sY, sH, sT, c1, Kwc, c3)                  # :475
+        ret.append(meta_mstep(e))                                                     # :477
+    sg = [float(np.sign(ret[0]["Cxt"] @ e["Cxt"])) for e in ret]
+    Wn = _vec_orth(sum(s * e["Cxt"] for s, e in zip(sg, ret)))                        # :481
+    Cn = _vec_orth(sum(s * e["Cyu"] for s, e in zip(sg, ret)))                        # :482
+    return dict(pops=ret, W=Wn, C=Cn)
+
+
+def meta_pplsi(X, Y, pop_sizes, EMsteps=100, atol=1e-4, theta0=None):
+    """meta_PPLSi -- Package/PPLS/R/EM_W_multi.R:509-589 (critfunc = identity, no constraints).
+    theta0: initial_guess(...)-style dict.  Returns dict(W, C, params, log = logvalue[1:i+1, ],
+    logvalue = the whole trace incl. the initial row)."""
+    W = np.ravel(np.asarray(theta0["W"], dtype=np.float64))
+    C = np.ravel(np.asarray(theta0["C"], dtype=np.float64))
+    B, sigE, sigF = float(theta0["B"]), float(theta0["sigE"]), float(theta0["sigF"])
+    sigH, sigT = float(theta0["sigH"]), float(theta0["sigT"])
+    K = len(pop_sizes)
+    Ni = np.concatenate([[0], np.cumsum(pop_sizes)])
+
+    def ll(Xd, Yd, W, C, pp):
+        return logl_w(Xd, Yd, W.reshape(-1, 1), C.reshape(-1, 1), np.array([[pp["B_T"]]]), pp["sigX"],
+                      pp["sigY"], pp["sigH"], np.array([[pp["sigT"]]]))
+
+    params = [dict(B_T=B, sigX=sigE, sigY=sigF, sigH=sigH, sigT=sigT) for _ in range(K)]   # :545
+    logvalue = [np.full(K, ll(X, Y, W, C, params[0]))]                                     # :544
+    i = 0
+    for i in range(1, EMsteps + 1):                                                         # :551
+        fit = meta_emstep(X, Y, W, C, pop_sizes, params)                                    # :555
+        params = [dict(B_T=float(e["B"]), sigX=float(e["sighat"][0]), sigY=float(e["sighat"][1]),
+                       sigH=float(e["siglathat"][0]), sigT=float(e["siglathat"][1])) for e in fit["pops"]]
+        W, C = fit["W"], fit["C"]                                                           # :556-570
+        logvalue.append(np.array([ll(X[Ni[j]:Ni[j + 1]], Y[Ni[j]:Ni[j + 1]], W, C, params[j])
+                                  for j in range(K)]))                                      # :571-573
+        if np.sum(logvalue[i]) - np.sum(logvalue[i - 1]) < atol:                           # :575
+            break
+    lv = np.array(logvalue)
+    return dict(W=W, C=C, params=params, log=lv[1:i + 1], logvalue=lv)

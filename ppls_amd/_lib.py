@@ -38,6 +38,12 @@ class PplsSeqFit(ct.Structure):
                 ("loglikelihoods", _dp), ("ncomp", ct.c_int), ("not_monotone", ct.c_int)]
 
 
+class PplsMetaFit(ct.Structure):
+    _fields_ = [("W", _dp), ("C", _dp), ("params", _dp), ("log", _dp), ("steps", ct.c_int)]
+
+
+_i64p = ct.POINTER(ct.c_int64)
+
 # name -> (restype, argtypes); every symbol declared in include/ppls.h
 SIGNATURES = {
     "ppls_version": (ct.c_int, []),
@@ -74,6 +80,10 @@ SIGNATURES = {
     "ppls_scores": (ct.c_int, [ct.c_void_p, _dp, _dp, ct.c_int, _dp, _dp]),
     "ppls_ppls": (ct.c_int, [ct.c_void_p, ct.c_int, ct.c_int, ct.c_double, ct.POINTER(PplsTheta),
                              ct.POINTER(PplsSeqFit)]),
+    "ppls_meta_emstep": (ct.c_int, [ct.c_void_p, ct.c_int, _i64p, _i64p, _dp, _dp, _dp, _dp, _dp, _dp,
+                                    _dp, _dp]),
+    "ppls_meta_ppls": (ct.c_int, [ct.c_void_p, ct.c_int, _i64p, _i64p, ct.c_int, ct.c_double, ct.c_int,
+                                  ct.POINTER(PplsTheta), ct.POINTER(PplsMetaFit)]),
     "ppls_sweep_timing": (ct.c_int, [ct.c_void_p, _dp, ct.POINTER(ct.c_int64), ct.c_int]),
     "ppls_finalize_trace": (ct.c_int, [ct.c_void_p, ct.POINTER(ct.c_int64), _dp]),
     "ppls_sweep_info": (ct.c_int, [ct.c_void_p, ct.c_int, ct.POINTER(ct.c_int64), ct.POINTER(ct.c_int),

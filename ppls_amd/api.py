@@ -8,6 +8,8 @@ Same names, argument meaning, return structure and error behaviour as the R func
 * ``Maximiz_M``    Package/PPLS/R/EM_W_multi.R:729-742
 * ``logl_W``       Package/PPLS/R/EM_W_multi.R:297-323
 * ``loglC_fast``   Package/PPLS/src/loglC.cpp:318-338 (via RcppExports.R:32-34)
+* ``meta_EMstep``  Package/PPLS/R/EM_W_multi.R:446-485 (meta_Estep/meta_Mstep, src/loglC.cpp:399-474)
+* ``meta_PPLSi``   Package/PPLS/R/EM_W_multi.R:509-589
 
 Every call goes through the C ABI (include/ppls.h) into the HIP kernels on the GPU; matrices
 are numpy arrays, R lists are dicts.  Passing ``X=None, Y=None`` uses the data already resident
@@ -23,6 +25,17 @@ import numpy as np
 
 from . import _lib
 from ._lib import Expect, PplsError, Theta, dptr
+
+
+def pop_rows(pop_sizes, row0, n_local):
+    """(local, total) rows per population for the shard [row0, row0 + n_local): population j is the
+    global row block [N_1 + .. + N_{j-1}, N_1 + .. + N_j) (EM_W_multi.R:451-458, :537-541)."""
+    sizes = np.asarray(pop_sizes, dtype=np.int64)
+    ends = np.cumsum(sizes)
+    begins = ends - sizes
+    lo, hi = int(row0), int(row0) + int(n_local)
+    local = np.clip(np.minimum(ends, hi) - np.maximum(begins, lo), 0, None).astype(np.int64)
+    return np.ascontiguousarray(local), np.ascontiguousarray(sizes)
 
 
 class Context:
@@ -220,6 +233,46 @@ class Context:
                                       Loglikelihoods=lls[:k].copy(),
                                       logvalue=[lv[i, :nst[i] + 1].copy() for i in range(k)]),
                     not_monotone=[bool(fit.not_monotone >> i & 1) for i in range(k)], ncomp=k)
+
+    def pop_rows(self, pop_sizes):
+        return pop_rows(pop_sizes, self.row0, self.n_local)
+
+    def meta_emstep(self, W, C, pop_sizes, params):
+        """meta_EMstep (EM_W_multi.R:446-485) on the resident rows: per-population E- and M-step
+        (meta_Estep / meta_Mstep, src/loglC.cpp:399-474) and the shared W., C.  params: npop x 5
+        (B_T, sigX, sigY, sigH, sigT).  Returns (W, C, params_out, Cxt p x npop, Cyu q x npop)."""
+        loc, tot = self.pop_rows(pop_sizes)
+        npop = len(tot)
+        W = np.ascontiguousarray(np.ravel(W), dtype=np.float64)
+        C = np.ascontiguousarray(np.ravel(C), dtype=np.float64)
+        pin = np.asfortranarray(np.asarray(params, dtype=np.float64).reshape(npop, 5))
+        Wo, Co = np.zeros(self.p), np.zeros(self.q)
+        po = np.zeros((npop, 5), order="F")
+        cxt, cyu = np.zeros((self.p, npop), order="F"), np.zeros((self.q, npop), order="F")
+        i64 = ct.POINTER(ct.c_int64)
+        self._chk(self._L.ppls_meta_emstep(self.h, npop, loc.ctypes.data_as(i64), tot.ctypes.data_as(i64),
+                                           dptr(W), dptr(C), dptr(pin), dptr(Wo), dptr(Co), dptr(po),
+                                           dptr(cxt), dptr(cyu)))
+        return Wo, Co, po, cxt, cyu
+
+    def meta_ppls(self, pop_sizes, max_steps, atol, init, crit_abs=False):
+        """meta_PPLSi's loop (EM_W_multi.R:544-578) from the starting values ``init`` (dict W, C, B,
+        sigE, sigF, sigH, sigT, r = 1).  Returns (W, C, params npop x 5, logvalue (steps+1) x npop)."""
+        loc, tot = self.pop_rows(pop_sizes)
+        npop = len(tot)
+        th = Theta(np.reshape(init["W"], (self.p, 1)), np.reshape(init["C"], (self.q, 1)),
+                   float(np.ravel(init["B"])[0]), init["sigE"], init["sigF"], init["sigH"],
+                   float(np.ravel(init["sigT"])[0]))
+        t = th.struct()
+        Wo, Co = np.zeros(self.p), np.zeros(self.q)
+        po = np.zeros((npop, 5), order="F")
+        lg = np.full((max_steps + 1, npop), np.nan, order="F")
+        fit = _lib.PplsMetaFit(dptr(Wo), dptr(Co), dptr(po), dptr(lg), 0)
+        i64 = ct.POINTER(ct.c_int64)
+        self._chk(self._L.ppls_meta_ppls(self.h, npop, loc.ctypes.data_as(i64), tot.ctypes.data_as(i64),
+                                         int(max_steps), float(atol), int(bool(crit_abs)), ct.byref(t),
+                                         ct.byref(fit)))
+        return Wo, Co, po, lg[: fit.steps + 1].copy()
 
     def scores(self, W, C):
         """scores.PPLS (EM_W_multi.R:411-420) on the resident rows: (X W, Y C), n_local x k each."""
@@ -482,6 +535,74 @@ def PPLS_simult_to_o2m(X_true, Y_true, fit_PPLS, ctx=None):
                           varXorth=np.zeros(1), varYorth=np.zeros(1))
     model["class"] = ["o2m", "o2m_stripped"]
     return model
+
+
+def _populations(Ipopu, n):
+    """as.factor(Ipopu) -> level counts in level order (table(Ipopu)); R sorts the levels."""
+    Ipopu = np.asarray(Ipopu)
+    if Ipopu.ndim != 1 or Ipopu.shape[0] != n:
+        raise ValueError("nrow(X) == length(Ipopu) is not TRUE")   # stopifnot (:448, :511)
+    levels, counts = np.unique(Ipopu, return_counts=True)
+    return levels, counts.astype(np.int64)
+
+
+def _params_list(levels, P):
+    return [dict(B_T=float(P[j, 0]), sigX=float(P[j, 1]), sigY=float(P[j, 2]), sigH=float(P[j, 3]),
+                 sigT=float(P[j, 4])) for j in range(len(levels))]
+
+
+def _params_matrix(params):
+    return np.array([[float(np.ravel(pp[k])[0]) for k in ("B_T", "sigX", "sigY", "sigH", "sigT")]
+                     for pp in params])
+
+
+def meta_EMstep(X, Y, W, C, Ipopu, params, ctx=None):
+    """meta_EMstep (EM_W_multi.R:446-485) on the GPU: one EM step of the multi-population rank-1
+    model.  ``params``: one dict per population (B_T, sigX, sigY, sigH, sigT), in level order.
+    Returns the reference's list: per population dict(B, sighat, siglathat, Cxt, Cyu), plus
+    ``W.`` and ``C.`` (shared loadings, orth of the sign-aligned sums, :481-482)."""
+    ctx = _ctx_with(X, Y, ctx)
+    levels, counts = _populations(Ipopu, ctx.n_total)
+    if len(params) != len(levels):
+        raise ValueError(f"{len(params)} parameter sets for {len(levels)} populations")
+    Wo, Co, P, cxt, cyu = ctx.meta_emstep(W, C, counts, _params_matrix(params))
+    out = [dict(B=P[j, 0], sighat=P[j, 1:3].copy(), siglathat=P[j, 3:5].copy(), Cxt=cxt[:, j].copy(),
+                Cyu=cyu[:, j].copy()) for j in range(len(levels))]
+    return dict(pops=out, **{"W.": Wo.reshape(-1, 1), "C.": Co.reshape(-1, 1)})
+
+
+def meta_PPLSi(X, Y, Ipopu, EMsteps=100, atol=1e-4, initialGuess=("equal", "o2m", "random", "custom"),
+               customGuess=None, critfunc=None, constraints=None, rng=None, ctx=None):
+    """meta_PPLSi (EM_W_multi.R:509-589) on the GPU: a rank-1 PPLS fit with loadings shared across
+    populations and per-population scalars.  Returns the reference's list (W, C, params, log) where
+    ``log`` is logvalue[1:i+1, ] (rows 2..i+1 of the trace: the per-population log-likelihoods after
+    each step; kept 2-D) and, additionally, ``logvalue`` (the full trace incl. the initial row).
+    critfunc: None/identity or abs.  constraints: dict with numeric "W" / "C" (the only constraints
+    the reference applies, :543-544)."""
+    ctx = _ctx_with(X, Y, ctx)
+    levels, counts = _populations(Ipopu, ctx.n_total)
+    kind = initialGuess if isinstance(initialGuess, str) else initialGuess[0]
+    if customGuess is not None:
+        kind = "custom"
+    if kind == "custom":
+        g = customGuess
+        init = dict(W=np.ravel(g["W"]), C=np.ravel(g["C"]), B=g["B"], sigE=g["sigE"], sigF=g["sigF"],
+                    sigH=g["sigH"], sigT=g["sigT"])
+    else:
+        init = initial_guess(ctx.p, ctx.q, kind, rng if rng is not None else np.random.default_rng())
+    if constraints:
+        if constraints.get("W") is not None:
+            init["W"] = np.ravel(np.asarray(constraints["W"], dtype=np.float64))
+        if constraints.get("C") is not None:
+            init["C"] = np.ravel(np.asarray(constraints["C"], dtype=np.float64))
+    if critfunc is None or critfunc is (lambda x: x) or getattr(critfunc, "__name__", "") == "identity":
+        crit_abs = False
+    elif critfunc in (abs, np.abs):
+        crit_abs = True
+    else:
+        raise NotImplementedError("critfunc must be the identity (default) or abs")
+    W, C, P, lg = ctx.meta_ppls(counts, int(EMsteps), float(atol), init, crit_abs)
+    return dict(W=W, C=C, params=_params_list(levels, P), log=lg[1:], logvalue=lg)
 
 
 def PPLS_simult(X, Y, a, EMsteps=10, atol=1e-4, type=("SVD", "QR"), init=None, ctx=None, **kw):

@@ -38,6 +38,8 @@ struct ppls_ctx {
   int nt_loads = -1;       // sweep LDS-DMA non-temporal: -1 auto (when X, Y exceed the MALL), 0 off, 1 on
   int timing = 0;          // 0 off; N > 0: bracket every N-th sweep launch with HIP events
   int64_t sweep_count = 0;
+  // row segment the next sweeps cover (meta_* per-population sweeps); seg_rows < 0 = all rows
+  int64_t seg_row0 = 0, seg_rows = -1;
   // communicator
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0;
@@ -296,8 +298,11 @@ int ensure_part(ppls_ctx* c, int groups) {
 
 // Which sweep kernel runs for this shape: 3 = split ownership (default), 1 = shared ownership
 // (v2, option kernel=2), 2 = generic two-pass; *grid is the workgroup count.
+int64_t sweep_rows(const ppls_ctx* c) { return c->seg_rows >= 0 ? c->seg_rows : c->n_local; }
+
 int sweep_plan(ppls_ctx* c, int r, PplsSweepArgs* a) {
   int ns = 0, threads = 512;
+  const int64_t nrows = sweep_rows(c);
   const bool fused = use_fused(c, r, &ns, &threads);
   const int nsplit = ppls_split_supported(r, c->ldx, c->ldy);
   memset(a, 0, sizeof *a);
@@ -308,7 +313,7 @@ int sweep_plan(ppls_ctx* c, int r, PplsSweepArgs* a) {
   a->r = r;
   a->threads = threads;
   if (c->sweep_mode == 3 || c->dtype) {   // forced panel sweep (the only fp32-storage sweep)
-    a->grid = ppls_panel_chunks(c->n_local, c->ldx, c->ldy, c->num_cus);
+    a->grid = ppls_panel_chunks(nrows, c->ldx, c->ldy, c->num_cus);
     return 4;
   }
   if (c->sweep_mode != 2 && nsplit > 0 && c->kernel_opt != 2) {
@@ -329,7 +334,7 @@ int sweep_plan(ppls_ctx* c, int r, PplsSweepArgs* a) {
     return 1;
   }
   if (c->sweep_mode != 2) {        // wide p / large r: panel sweep (two GEMM-shaped passes)
-    a->grid = ppls_panel_chunks(c->n_local, c->ldx, c->ldy, c->num_cus);
+    a->grid = ppls_panel_chunks(nrows, c->ldx, c->ldy, c->num_cus);
     return 4;
   }
   a->grid = grid_of(c);
@@ -341,7 +346,9 @@ int sweep(ppls_ctx* c, int r, int slot, bool write_mu) {
   int rc;
   PplsSweepArgs a;
   const int plan = sweep_plan(c, r, &a);
-  const int groups = plan == 2 ? ppls_twopass_groups(std::max<int64_t>(c->n_local, 1), a.grid) : a.grid;
+  const int64_t nrows = sweep_rows(c);
+  if (c->seg_rows >= 0 && write_mu) return fail(c, PPLS_E_STATE, "mu write-out is not available for row segments");
+  const int groups = plan == 2 ? ppls_twopass_groups(std::max<int64_t>(nrows, 1), a.grid) : a.grid;
   if ((rc = ensure_part(c, groups))) return rc;
   if (write_mu && !c->mu)
     if ((rc = dalloc(c, &c->mu, (size_t)std::max<int64_t>(c->n_local, 1) * 2 * r))) return rc;
@@ -353,12 +360,13 @@ int sweep(ppls_ctx* c, int r, int slot, bool write_mu) {
     if ((rc = dalloc(c, &c->Z, len))) return rc;
     c->z_cols = (plan == 4 ? 4 : 2) * r;
   }
-  if (c->n_local == 0) {
+  if (nrows == 0) {
     HIPCHK(c, hipMemsetAsync(c->stats, 0, sizeof(double) * c->part_ld, c->stream));
   } else {
-    a.X = c->X;
-    a.Y = c->Y;
-    a.n_local = c->n_local;
+    const size_t esz = c->dtype ? sizeof(float) : sizeof(double);
+    a.X = (const double*)((const char*)c->X + (size_t)c->seg_row0 * c->ldx * esz);
+    a.Y = (const double*)((const char*)c->Y + (size_t)c->seg_row0 * c->ldy * esz);
+    a.n_local = nrows;
     a.Wp = c->W[slot];
     a.Cp = c->C[slot];
     a.sc = c->sc[slot];
@@ -369,7 +377,7 @@ int sweep(ppls_ctx* c, int r, int slot, bool write_mu) {
     // once-read streams bigger than the 256 MB MALL: the non-temporal policy lands 3-9 % faster
     // (6.53 vs 6.34 TB/s at C3); smaller X, Y stay MALL-resident across iterations by default
     const bool nt = c->nt_loads > 0 ||
-                    (c->nt_loads < 0 && 8.0 * c->n_local * (double)(c->ldx + c->ldy) > 256.0 * (1 << 20));
+                    (c->nt_loads < 0 && 8.0 * nrows * (double)(c->ldx + c->ldy) > 256.0 * (1 << 20));
     a.ablate = c->ablate | (nt ? 16 : 0);
     hipEvent_t e0 = nullptr, e1 = nullptr;
     const bool timed = c->timing > 0 && (c->sweep_count++ % c->timing) == 0;
@@ -1079,11 +1087,11 @@ double rank1_loglik(const Rank1& t, const double G[4], double ssqX, double ssqY,
   return ppls_loglik_from_gram(G, ssqX, ssqY, N, p, q, 1, &s);
 }
 
-// EMstepC_fast (loglC.cpp:340-397) from the sweep of t; SX, SY are X'mu_T, Y'mu_U of the full
-// data, projected here onto the deflated column spaces.
-Rank1 rank1_update(const Rank1& t, std::vector<double> SX, std::vector<double> SY, const double G[4],
-                   double ssqX, double ssqY, double N, int p, int q, const std::vector<double>& Wp,
-                   const std::vector<double>& Cp, int m) {
+// The rank-1 E-step moments and M-step scalars from one sweep's Gram -- the arithmetic shared by
+// EMstepC_fast (loglC.cpp:354-385) and meta_Estep / meta_Mstep (loglC.cpp:399-474), which restate
+// the same formulas: B = Cut/Ctt, sighat = (sqrt(Cee), sqrt(Cff)), siglathat = (sqrt(Chh), sqrt(Ctt)).
+void rank1_scalars(const Rank1& t, const double G[4], double ssqX, double ssqY, double N, int p, int q,
+                   Rank1* n) {
   double c1, c2, c3, al, be, ga, de;
   rank1_coefs(t, &c1, &c2, &c3, &al, &be, &ga, &de);
   const double s2X = t.sigE * t.sigE, s2Y = t.sigF * t.sigF, s2H = t.sigH * t.sigH, s2T = t.sigT * t.sigT;
@@ -1104,9 +1112,22 @@ Rank1 rank1_update(const Rank1& t, std::vector<double> SX, std::vector<double> S
   const double Cff = s2Y - (-s2Y * s2Y * c3 + q * s2Y) / q + Cfftmp / N / q;                            // :371
   const double hx = -c2 * s2H, hy = -(c3 - 1 / s2Y) * s2H;
   const double Chh = s2H - (-s2H * s2H * (c3 - 1 / s2Y)) + (hx * hx * A + 2 * hx * hy * D + hy * hy * Bm) / N;  // :373
+  n->B = Cut / Ctt;                                  // :385
+  n->sigE = std::sqrt(Cee);                          // sighat (:376)
+  n->sigF = std::sqrt(Cff);
+  n->sigH = std::sqrt(Chh);                          // siglathat (:377)
+  n->sigT = std::sqrt(Ctt);
+}
+
+// EMstepC_fast (loglC.cpp:340-397) from the sweep of t; SX, SY are X'mu_T, Y'mu_U of the full
+// data, projected here onto the deflated column spaces.
+Rank1 rank1_update(const Rank1& t, std::vector<double> SX, std::vector<double> SY, const double G[4],
+                   double ssqX, double ssqY, double N, int p, int q, const std::vector<double>& Wp,
+                   const std::vector<double>& Cp, int m) {
+  Rank1 n;
+  rank1_scalars(t, G, ssqX, ssqY, N, p, q, &n);
   deflate(Wp, m, p, SX.data(), true);   // Xc' mu_T = P_{m-1}..P_0 X' mu_T
   deflate(Cp, m, q, SY.data(), true);
-  Rank1 n;
   double nx = 0.0, ny = 0.0;
   for (int i = 0; i < p; ++i) { SX[i] /= N; nx += SX[i] * SX[i]; }   // Cxt = Xc' mu_T / N (:355)
   for (int i = 0; i < q; ++i) { SY[i] /= N; ny += SY[i] * SY[i]; }
@@ -1116,11 +1137,6 @@ Rank1 rank1_update(const Rank1& t, std::vector<double> SX, std::vector<double> S
   n.c.resize(q);
   for (int i = 0; i < p; ++i) n.w[i] = SX[i] / nx;   // Cxt.normalized() (:383)
   for (int i = 0; i < q; ++i) n.c[i] = SY[i] / ny;
-  n.B = Cut / Ctt;                                   // :385
-  n.sigE = std::sqrt(Cee);                           // sighat (:376)
-  n.sigF = std::sqrt(Cff);
-  n.sigH = std::sqrt(Chh);                           // siglathat (:377)
-  n.sigT = std::sqrt(Ctt);
   return n;
 }
 
@@ -1252,6 +1268,237 @@ int ppls_ppls(ppls_ctx* c, int a, int max_steps, double atol, const ppls_theta* 
       out->loglikelihoods[k] = ppls_loglik_from_gram(Gf.data(), c->ssq_host[0], c->ssq_host[1], N, p, q, r, &s);
     }
   }
+  return PPLS_OK;
+}
+
+}  // extern "C"
+
+namespace {
+
+// Sums of squares of the rows [row0, row0 + nrows) of X and Y on this rank, all-reduced -> out[2].
+int segment_ssq(ppls_ctx* c, int64_t row0, int64_t nrows, double out[2]) {
+  int rc;
+  const int nb = 1024;
+  double* buf = nullptr;
+  if ((rc = dalloc(c, &buf, (size_t)nb + 2))) return rc;
+  hipError_t e = hipMemsetAsync(buf + nb, 0, 2 * sizeof(double), c->stream);
+  for (int m = 0; m < 2 && e == hipSuccess && nrows > 0; ++m) {
+    const int64_t ld = m ? c->ldy : c->ldx;
+    const void* base = m ? (const void*)c->Y : (const void*)c->X;
+    if (c->dtype)
+      e = ppls_launch_sumsq_f32((const float*)base + row0 * ld, nrows * ld, buf, nb, buf + nb + m, c->stream);
+    else
+      e = ppls_launch_sumsq((const double*)base + row0 * ld, nrows * ld, buf, nb, buf + nb + m, 0, c->stream);
+  }
+  rc = e == hipSuccess ? allreduce(c, buf + nb, 2) : fail(c, PPLS_E_HIP, "segment ssq: %s", hipGetErrorString(e));
+  if (!rc) {
+    e = hipMemcpyAsync(out, buf + nb, 2 * sizeof(double), hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) rc = fail(c, PPLS_E_HIP, "segment ssq: %s", hipGetErrorString(e));
+  }
+  dfree(buf);
+  return rc;
+}
+
+// rank1_sweep restricted to this rank's rows of one population.
+int segment_sweep(ppls_ctx* c, int64_t row0, int64_t nrows, const Rank1& t, std::vector<double>& SX,
+                  std::vector<double>& SY, double G[4]) {
+  static const std::vector<double> none;
+  c->seg_row0 = row0;
+  c->seg_rows = nrows;
+  const int rc = rank1_sweep(c, t, none, none, 0, SX, SY, G);
+  c->seg_row0 = 0;
+  c->seg_rows = -1;
+  return rc;
+}
+
+struct MetaPop {
+  int64_t row0 = 0, nloc = 0;   // this rank's rows of the population
+  double N = 0.0;               // rows over all ranks (nrow(X[popui, ]))
+  double ssq[2] = {0.0, 0.0};   // ssq(X[popui, ]), ssq(Y[popui, ])
+  Rank1 t;                      // params[[j]] with the shared W., C.
+  std::vector<double> SX, SY;   // X[popui, ]' mu_T, Y[popui, ]' mu_U of the last sweep
+  double G[4] = {0, 0, 0, 0};
+};
+
+int meta_setup(ppls_ctx* c, int npop, const int64_t* pop_local, const int64_t* pop_total,
+               std::vector<MetaPop>& pops) {
+  if (npop < 1 || !pop_local || !pop_total) return fail(c, PPLS_E_ARG, "need npop >= 1 populations with row counts");
+  pops.assign(npop, MetaPop());
+  int64_t r0 = 0, tot = 0;
+  for (int j = 0; j < npop; ++j) {
+    if (pop_local[j] < 0 || pop_total[j] < 1) return fail(c, PPLS_E_ARG, "population %d has no rows", j + 1);
+    pops[j].row0 = r0;
+    pops[j].nloc = pop_local[j];
+    pops[j].N = (double)pop_total[j];
+    r0 += pop_local[j];
+    tot += pop_total[j];
+  }
+  if (r0 != c->n_local) return fail(c, PPLS_E_ARG, "population rows on this rank sum to %lld, not n_local = %lld",
+                                    (long long)r0, (long long)c->n_local);
+  if (tot != c->n_total)   // stopifnot(nrow(X) == length(Ipopu)) (:448, :511)
+    return fail(c, PPLS_E_ARG, "population sizes sum to %lld, not nrow(X) = %lld", (long long)tot,
+                (long long)c->n_total);
+  int rc;
+  for (auto& pp : pops)
+    if ((rc = segment_ssq(c, pp.row0, pp.nloc, pp.ssq))) return rc;
+  return PPLS_OK;
+}
+
+// The M-step half of meta_EMstep (:453-484) from each population's last sweep: meta_Mstep per
+// population, then W. = orth(sum_j sign(<Cxt_1, Cxt_j>) Cxt_j), C. likewise with Cyu_j.  orth of one
+// column is v / ||v|| (OmicsPLS::orth semantics of Package/functions.R:252-260; unpinned).
+void meta_mstep(std::vector<MetaPop>& pops, int p, int q, std::vector<double>& w, std::vector<double>& cv,
+                std::vector<double>* Cxt, std::vector<double>* Cyu) {
+  const int npop = (int)pops.size();
+  std::vector<Rank1> nt(npop);
+  for (int j = 0; j < npop; ++j) rank1_scalars(pops[j].t, pops[j].G, pops[j].ssq[0], pops[j].ssq[1], pops[j].N, p, q, &nt[j]);
+  w.assign(p, 0.0);
+  cv.assign(q, 0.0);
+  if (Cxt) Cxt->assign((size_t)p * npop, 0.0);
+  if (Cyu) Cyu->assign((size_t)q * npop, 0.0);
+  const std::vector<double>& x1 = pops[0].SX;
+  const double N1 = pops[0].N;
+  for (int j = 0; j < npop; ++j) {
+    const MetaPop& pp = pops[j];
+    double d = 0.0;   // crossprod(Cxt_1, Cxt_j) = <SX_1, SX_j> / (N_1 N_j)
+    for (int i = 0; i < p; ++i) d += (x1[i] / N1) * (pp.SX[i] / pp.N);
+    const double sg = d > 0 ? 1.0 : (d < 0 ? -1.0 : 0.0);   // R's sign()
+    for (int i = 0; i < p; ++i) w[i] += sg * (pp.SX[i] / pp.N);     // Cxt = X' mu_T / N (loglC.cpp:416)
+    for (int i = 0; i < q; ++i) cv[i] += sg * (pp.SY[i] / pp.N);    // Cyu (:421)
+    if (Cxt) for (int i = 0; i < p; ++i) (*Cxt)[(size_t)j * p + i] = pp.SX[i] / pp.N;
+    if (Cyu) for (int i = 0; i < q; ++i) (*Cyu)[(size_t)j * q + i] = pp.SY[i] / pp.N;
+  }
+  double nw = 0.0, nc = 0.0;
+  for (double v : w) nw += v * v;
+  for (double v : cv) nc += v * v;
+  nw = std::sqrt(nw);
+  nc = std::sqrt(nc);
+  for (double& v : w) v /= nw;
+  for (double& v : cv) v /= nc;
+  for (int j = 0; j < npop; ++j) {
+    pops[j].t.B = nt[j].B;
+    pops[j].t.sigE = nt[j].sigE;
+    pops[j].t.sigF = nt[j].sigF;
+    pops[j].t.sigH = nt[j].sigH;
+    pops[j].t.sigT = nt[j].sigT;
+  }
+}
+
+void meta_params_out(const std::vector<MetaPop>& pops, double* params) {
+  const int npop = (int)pops.size();
+  for (int j = 0; j < npop; ++j) {
+    params[j] = pops[j].t.B;
+    params[npop + j] = pops[j].t.sigE;
+    params[2 * npop + j] = pops[j].t.sigF;
+    params[3 * npop + j] = pops[j].t.sigH;
+    params[4 * npop + j] = pops[j].t.sigT;
+  }
+}
+
+int meta_sweep_all(ppls_ctx* c, std::vector<MetaPop>& pops, const std::vector<double>& w,
+                   const std::vector<double>& cv) {
+  int rc;
+  for (auto& pp : pops) {
+    pp.t.w = w;
+    pp.t.c = cv;
+    if ((rc = segment_sweep(c, pp.row0, pp.nloc, pp.t, pp.SX, pp.SY, pp.G))) return rc;
+  }
+  return PPLS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ppls_meta_emstep(ppls_ctx* c, int npop, const int64_t* pop_local, const int64_t* pop_total, const double* W,
+                     const double* C, const double* params_in, double* W_out, double* C_out, double* params_out,
+                     double* Cxt, double* Cyu) {
+  if (!c) return PPLS_E_ARG;
+  if (!c->have_data) return fail(c, PPLS_E_STATE, "no data");
+  if (!W || !C || !params_in || !W_out || !C_out || !params_out) return fail(c, PPLS_E_ARG, "NULL argument");
+  HIPCHK(c, hipSetDevice(c->device));
+  int rc;
+  if ((rc = ensure_r(c, 1, 1))) return rc;
+  std::vector<MetaPop> pops;
+  if ((rc = meta_setup(c, npop, pop_local, pop_total, pops))) return rc;
+  std::vector<double> w(W, W + c->p), cv(C, C + c->q);
+  for (int j = 0; j < npop; ++j) {
+    Rank1& t = pops[j].t;
+    t.B = params_in[j];
+    t.sigE = params_in[npop + j];
+    t.sigF = params_in[2 * npop + j];
+    t.sigH = params_in[3 * npop + j];
+    t.sigT = params_in[4 * npop + j];
+  }
+  if ((rc = meta_sweep_all(c, pops, w, cv))) return rc;
+  std::vector<double> cx, cy;
+  meta_mstep(pops, c->p, c->q, w, cv, Cxt ? &cx : nullptr, Cyu ? &cy : nullptr);
+  std::copy(w.begin(), w.end(), W_out);
+  std::copy(cv.begin(), cv.end(), C_out);
+  meta_params_out(pops, params_out);
+  if (Cxt) std::copy(cx.begin(), cx.end(), Cxt);
+  if (Cyu) std::copy(cy.begin(), cy.end(), Cyu);
+  return PPLS_OK;
+}
+
+int ppls_meta_ppls(ppls_ctx* c, int npop, const int64_t* pop_local, const int64_t* pop_total, int max_steps,
+                   double atol, int crit_abs, const ppls_theta* init, ppls_meta_fit* out) {
+  if (!c) return PPLS_E_ARG;
+  if (!c->have_data) return fail(c, PPLS_E_STATE, "no data");
+  if (!init || !init->W || !init->C || !init->B || !init->sigT || !out || !out->W || !out->C || !out->params)
+    return fail(c, PPLS_E_ARG, "NULL argument");
+  if (max_steps < 1) return fail(c, PPLS_E_ARG, "EMsteps must be >= 1");
+  HIPCHK(c, hipSetDevice(c->device));
+  int rc;
+  if ((rc = ensure_r(c, 1, max_steps))) return rc;
+  std::vector<MetaPop> pops;
+  if ((rc = meta_setup(c, npop, pop_local, pop_total, pops))) return rc;
+  const int p = c->p, q = c->q;
+  std::vector<double> w(init->W, init->W + p), cv(init->C, init->C + q);
+  Rank1 t0;
+  t0.w = w;
+  t0.c = cv;
+  t0.B = init->B[0];
+  t0.sigE = init->sigE;
+  t0.sigF = init->sigF;
+  t0.sigH = init->sigH;
+  t0.sigT = init->sigT[0];
+  for (auto& pp : pops) pp.t = t0;   // params = lapply(.., list(B_T = Bnw, sigX = signw[1], ...)) (:545)
+  auto crit = [&](double x) { return crit_abs ? std::fabs(x) : x; };
+  const size_t ld = (size_t)max_steps + 1;
+  if (out->log)
+    for (size_t e = 0; e < ld * npop; ++e) out->log[e] = NAN;
+  // logvalue[1, ] = rep(logl_W(X, Y, Wnw, Cnw, Bnw, ...), K) (:544): one full-data sweep
+  {
+    std::vector<double> SX, SY;
+    double G[4];
+    if ((rc = rank1_sweep(c, t0, std::vector<double>(), std::vector<double>(), 0, SX, SY, G))) return rc;
+    const double l0 = rank1_loglik(t0, G, c->ssq_host[0], c->ssq_host[1], (double)c->n_total, p, q);
+    if (out->log)
+      for (int j = 0; j < npop; ++j) out->log[(size_t)j * ld] = l0;
+    out->steps = 0;
+    std::vector<double> prev(npop, l0);
+    if ((rc = meta_sweep_all(c, pops, w, cv))) return rc;   // meta_EMstep's E-step of step 1
+    int i;
+    for (i = 1; i <= max_steps; ++i) {                           // :551
+      meta_mstep(pops, p, q, w, cv, nullptr, nullptr);         // fit = meta_EMstep(...) (:555-570)
+      if ((rc = meta_sweep_all(c, pops, w, cv))) return rc;   // next E-step; its Gram gives logl_W
+      double s_new = 0.0, s_old = 0.0;
+      for (int j = 0; j < npop; ++j) {                          // logvalue[i+1, j] (:571-573)
+        const double lj = rank1_loglik(pops[j].t, pops[j].G, pops[j].ssq[0], pops[j].ssq[1], pops[j].N, p, q);
+        if (out->log) out->log[(size_t)j * ld + i] = lj;
+        s_old += prev[j];
+        s_new += lj;
+        prev[j] = lj;
+      }
+      out->steps = i;
+      if (crit(s_new - s_old) < atol) break;                    // :575-578
+    }
+  }
+  std::copy(w.begin(), w.end(), out->W);
+  std::copy(cv.begin(), cv.end(), out->C);
+  meta_params_out(pops, out->params);
   return PPLS_OK;
 }
 

@@ -60,8 +60,60 @@ def seq_fixtures(here):
         print(name, "steps", oo["Number_steps"], "logliks", oo["Loglikelihoods"])
 
 
+# multi-population meta_PPLSi(X, Y, Ipopu, EMsteps, atol, initialGuess): shared W, C, per-population
+# scalars (B, t, sigE, sigF) -- populations are contiguous row blocks in level order
+META_CASES = [
+    # name, pop sizes, p, q, EMsteps, atol, initialGuess, data seed, init seed ('random')
+    ("meta_equal_k2_p30_q20", (120, 80), 30, 20, 100, 5e-3, "equal", 21, None),
+    ("meta_random_k3_p24_q18", (100, 60, 90), 24, 18, 25, 1e-6, "random", 22, 7),
+]
+
+
+def meta_problem(sizes, p, q, seed):
+    rng = np.random.default_rng(seed)
+    w = rng.standard_normal(p)
+    c = rng.standard_normal(q)
+    w, c = w / np.linalg.norm(w), c / np.linalg.norm(c)
+    Xs, Ys = [], []
+    for j, nj in enumerate(sizes):
+        t, b, sE, sF, sH = 1.0 + 0.3 * j, 1.5 - 0.4 * j, 0.5 + 0.1 * j, 0.6 - 0.05 * j, 0.2
+        T = t * rng.standard_normal(nj)
+        U = b * T + sH * rng.standard_normal(nj)
+        Xs.append(np.outer(T, w) + sE * rng.standard_normal((nj, p)))
+        Ys.append(np.outer(U, c) + sF * rng.standard_normal((nj, q)))
+    return np.vstack(Xs), np.vstack(Ys)
+
+
+def meta_fixtures(here):
+    for name, sizes, p, q, steps, atol, kind, seed, iseed in META_CASES:
+        X, Y = meta_problem(sizes, p, q, seed)
+        rng = np.random.default_rng(iseed) if iseed is not None else None
+        init = o.initial_guess(p, q, kind, rng)
+        f = o.meta_pplsi(X, Y, list(sizes), steps, atol, init)
+        P = np.array([[pp[k] for k in ("B_T", "sigX", "sigY", "sigH", "sigT")] for pp in f["params"]])
+        one = o.meta_emstep(X, Y, init["W"], init["C"], list(sizes),
+                            [dict(B_T=init["B"], sigX=init["sigE"], sigY=init["sigF"], sigH=init["sigH"],
+                                  sigT=init["sigT"])] * len(sizes))
+        meta = dict(sizes=list(sizes), p=p, q=q, EMsteps=steps, atol=atol, initialGuess=kind, seed=seed,
+                    init_seed=iseed, steps=int(f["logvalue"].shape[0] - 1))
+        np.savez_compressed(
+            os.path.join(here, name + ".npz"), meta=json.dumps(meta), X=X, Y=Y, init_W=init["W"],
+            init_C=init["C"],
+            init_s=np.array([init["B"], init["sigE"], init["sigF"], init["sigH"], init["sigT"]]),
+            W=f["W"], C=f["C"], params=P, logvalue=f["logvalue"],
+            step1_W=one["W"], step1_C=one["C"],
+            step1_params=np.array([[e["B"], *e["sighat"], *e["siglathat"]] for e in one["pops"]]),
+            step1_Cxt=np.stack([e["Cxt"] for e in one["pops"]], 1),
+            step1_Cyu=np.stack([e["Cyu"] for e in one["pops"]], 1))
+        print(name, "steps", meta["steps"], "log", f["logvalue"][-1])
+
+
 def main():
     here = os.path.dirname(os.path.abspath(__file__))
+    if "--meta" in sys.argv:   # only the meta_* fixtures (the others are unchanged)
+        meta_fixtures(here)
+        return
+    meta_fixtures(here)
     seq_fixtures(here)
     for name, n, p, q, r, steps, atol, typ, seed in CASES:
         X, Y, th0 = make_problem(n, p, q, r, seed=seed)

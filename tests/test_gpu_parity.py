@@ -57,7 +57,7 @@ def _relerr(a, b):
 
 
 def _golden():
-    return sorted(f for f in os.listdir(GOLD) if f.endswith(".npz") and not f.startswith("seq_"))
+    return sorted(f for f in os.listdir(GOLD) if f.endswith(".npz") and not f.startswith(("seq_", "meta_")))
 
 
 @pytest.mark.parametrize("sweep", SWEEPS, ids=SWEEP_IDS)

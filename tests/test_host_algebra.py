@@ -102,3 +102,19 @@ def test_context_without_gpu_fails_loudly():
     from ppls_amd import Context, PplsError
     with pytest.raises(PplsError):
         Context(0)
+
+
+def test_population_rows_per_shard():
+    # population j = global rows [N_1+..+N_{j-1}, N_1+..+N_j) intersected with each rank's shard
+    from ppls_amd.api import pop_rows
+    sizes = [7, 0, 5, 9]
+    for nranks in (1, 2, 3, 4):
+        tot = np.zeros(4, dtype=np.int64)
+        for rank in range(nranks):
+            r0 = 21 * rank // nranks
+            nl = 21 * (rank + 1) // nranks - r0
+            loc, t = pop_rows(sizes, r0, nl)
+            assert loc.sum() == nl and list(t) == sizes
+            tot += loc
+        assert list(tot) == sizes
+    assert list(pop_rows([10, 10], 5, 10)[0]) == [5, 5]

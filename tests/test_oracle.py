@@ -71,7 +71,7 @@ def test_golden_fixtures_reproduce():
     import json, os
     here = os.path.join(os.path.dirname(__file__), "golden")
     for name in sorted(os.listdir(here)):
-        if not name.endswith(".npz") or name.startswith("seq_"):
+        if not name.endswith(".npz") or name.startswith(("seq_", "meta_")):
             continue
         g = np.load(os.path.join(here, name))
         meta = json.loads(str(g["meta"]))
@@ -137,3 +137,54 @@ def test_ppls_loadings_orthonormal_and_golden_reproduced():
         assert np.allclose(f["C"].T @ f["C"], np.eye(a), atol=1e-12)
         for lv in f["Other_output"]["logvalue"]:
             assert np.all(np.diff(lv) > -1e-8 * np.abs(lv[:-1]))      # EM monotone
+
+
+# ----------------------------------------------------------------------------- meta_* (multi-population)
+
+def _meta_fixture(name):
+    import json
+    g = np.load(os.path.join(GOLDEN, name))
+    return g, json.loads(str(g["meta"]))
+
+
+def _meta_init(g):
+    s = g["init_s"]
+    return dict(W=g["init_W"], C=g["init_C"], B=s[0], sigE=s[1], sigF=s[2], sigH=s[3], sigT=s[4])
+
+
+def test_meta_single_population_equals_pplsi():
+    # with one population meta_EMstep's orth(sum) is EMstepC_fast's Cxt.normalized() and the stop rule is
+    # PPLSi's: the two independent reference code paths must agree
+    X, Y, _ = make_problem(150, 14, 11, 1, seed=31)
+    init = o.initial_guess(14, 11, "equal")
+    a = o.pplsi(X, Y, 40, 1e-5, init)
+    m = o.meta_pplsi(X, Y, [150], 40, 1e-5, init)
+    assert m["logvalue"].shape[0] - 1 == a["Number_steps"]
+    assert np.abs(m["logvalue"][:, 0] - a["logvalue"]).max() / abs(a["logvalue"][-1]) < 1e-13
+    assert np.abs(m["W"] - a["W"]).max() < 1e-12 and np.abs(m["C"] - a["C"]).max() < 1e-12
+    p0 = m["params"][0]
+    assert np.allclose([p0["B_T"], p0["sigX"], p0["sigY"], p0["sigH"], p0["sigT"]],
+                       [a["B"], *a["sig"]], rtol=1e-12, atol=0)
+
+
+def test_meta_estep_matches_closed_form_expect_m_rank1():
+    # meta_Estep (loglC.cpp:399-448) vs the independent closed-form Expect_M at r = 1 (EM_W_multi.R:668-716)
+    X, Y, th = make_problem(90, 12, 10, 1, seed=32)
+    B, sE, sF, sH, sT = th["B"][0, 0], th["sigE"], th["sigF"], th["sigH"], th["sigT"][0, 0]
+    cf = o.coefficients(np.array([B]), sE, sF, sH, np.array([sT]))
+    e = o.meta_estep(th["W"][:, 0], th["C"][:, 0], B, X, Y, sE, sF, sH, sT, cf["c1"][0], cf["c2"][0], cf["c3"][0])
+    E = o.expect_m(X, Y, th["W"], th["C"], th["B"], sE, sF, sH, th["sigT"])
+    assert np.abs(e["mu_T"] - E["mu_T"][:, 0]).max() < 1e-12
+    assert abs(e["Ctt"] - E["Ctt"][0, 0]) < 1e-12 and abs(e["Cut"] - E["Cut"][0, 0]) < 1e-12
+    assert abs(e["Cee"] - E["Cee"][0, 0]) < 1e-12 and abs(e["Chh"] - E["Chh"][0, 0]) < 1e-12
+    assert np.abs(e["Cxt"] - X.T @ E["mu_T"][:, 0] / 90).max() < 1e-12
+
+
+@pytest.mark.parametrize("name", ["meta_equal_k2_p30_q20.npz", "meta_random_k3_p24_q18.npz"])
+def test_meta_golden_reproduces(name):
+    g, meta = _meta_fixture(name)
+    f = o.meta_pplsi(g["X"], g["Y"], meta["sizes"], meta["EMsteps"], meta["atol"], _meta_init(g))
+    assert f["logvalue"].shape[0] - 1 == meta["steps"]
+    assert np.array_equal(f["logvalue"], g["logvalue"]) and np.array_equal(f["W"], g["W"])
+    # the EM never decreases the summed log-likelihood after the first step (row 0 is rep(full, K))
+    assert np.all(np.diff(g["logvalue"][1:].sum(1)) > -1e-9)
