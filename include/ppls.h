@@ -181,6 +181,20 @@ int ppls_loglC_fast(ppls_ctx* ctx, const double* W, const double* C, const doubl
                     const double* c1, const double* c2, const double* c3, const double* Kc,
                     double* out);
 
+/* ---- variances.PPLS_simult(fit, data, XorY) (Package/PPLS/R/EM_W_multi.R:830-860) ---------------
+ * mu: this rank's rows of fit$Expectations$mu_T (xory 0, "X") or $mu_U (xory 1, "Y"), n_local x a
+ * column-major; Cdiag: diag of $Ctt (or $Cuu), a; sigE: fit$estimates$sigE (the reference uses sigE
+ * for both XorY).  Outputs (p = ncol(data)): W = orth(t(data) %*% mu, "SVD") p x a; B_exp[i]: the
+ * reference's B_exp of component i is B_exp[i] * diag(p); varMatrix, SSt_exp, SSt_star (each a
+ * consecutive p x p column-major matrices, nullable) and seLoad (p x a).  t(data) diag(Ctt) data is
+ * Ctt * data'data: one MFMA Gram for all components. */
+int ppls_variances(ppls_ctx* ctx, const double* mu, const double* Cdiag, double sigE, int a, int xory,
+                   double* W, double* B_exp, double* varMatrix, double* SSt_exp, double* SSt_star,
+                   double* seLoad);
+/* The Gram D'D alone (D = X for xory 0, Y for 1; nsplit 0 = auto), for tests and benchmarks:
+ * G (p x p, column-major, nullable), *ms = the MFMA kernel's duration. */
+int ppls_gram(ppls_ctx* ctx, int xory, int nsplit, double* G, double* ms);
+
 /* ---- measurement ---------------------------------------------------------------------------- */
 /* Sum of HIP-event durations of the sweep kernel launches recorded since the last reset. */
 int ppls_sweep_timing(ppls_ctx* ctx, double* total_ms, int64_t* launches, int reset);

@@ -24,6 +24,7 @@ Every function cites the reference line it restates (paths relative to /root/ref
 * ``meta_mstep``         Package/PPLS/src/loglC.cpp:452-474
 * ``meta_emstep``        Package/PPLS/R/EM_W_multi.R:446-485 (populations = contiguous blocks :451-458)
 * ``meta_pplsi``         Package/PPLS/R/EM_W_multi.R:509-589 (critfunc = identity, no sigma check)
+* ``variances_ppls_simult`` Package/PPLS/R/EM_W_multi.R:830-860
 * ``orth``               OmicsPLS::orth (not vendored); semantics Package/functions.R:252-260
 * ``ssq``                OmicsPLS::ssq (not vendored); semantics Package/functions.R:380-385
 
@@ -604,3 +605,38 @@ def meta_pplsi(X, Y, pop_sizes, EMsteps=100, atol=1e-4, theta0=None):
             break
     lv = np.array(logvalue)
     return dict(W=W, C=C, params=params, log=lv[1:i + 1], logvalue=lv)
+
+
+# ----------------------------------------------------------------------------- variances.PPLS_simult
+
+def variances_ppls_simult(fit, data, XorY):
+    """variances.PPLS_simult -- Package/PPLS/R/EM_W_multi.R:830-860 (dense, literal: the N x N
+    diag(Ctt) product is written as Ctt * X'X, which is the same matrix).  fit: a ppls_simult() list.
+    Note the reference uses fit$estimates$sigE for XorY = "Y" too (kept)."""
+    X = np.asarray(data, dtype=np.float64)
+    E = fit["Expectations"]
+    mu_all = E["mu_T"] if XorY == "X" else E["mu_U"]                                  # :837
+    Cm = E["Ctt"] if XorY == "X" else E["Cuu"]                                         # :836
+    W = orth(X.T @ mu_all, type="SVD")                                                 # :831-832
+    N, p = X.shape
+    a = W.shape[1]
+    sigE = float(np.ravel(fit["estimates"]["sigE"])[0])
+    XtX = X.T @ X
+    outp = []
+    for i in range(a):                                                                 # :838
+        w = W[:, [i]]
+        Ctt = N * Cm[i, i]
+        mu = mu_all[:, i]
+        mu2 = float(mu @ mu)
+        Vt = Ctt - mu2                                                                 # :842
+        Cxt = (X.T @ mu)[:, None]                                                      # :843
+        B_star = Ctt / sigE ** 2 * np.eye(p) / N                                       # :844
+        SSt_expec = (Ctt * XtX - Cxt * (Ctt + 2 * Vt) @ w.T - w * (Ctt + 2 * Vt) @ Cxt.T
+                     + w * (Ctt ** 2 + 4 * mu2 * Vt + 2 * Vt * Vt) @ w.T)               # :846-847
+        SSt_expec = SSt_expec / sigE ** 4 / N                                          # :848
+        d = Cxt - w * Ctt
+        SSt_star = (d @ d.T) / sigE ** 4                                               # :850-851
+        outp.append(dict(B_exp=B_star, SSt_exp=SSt_expec, SSt_star=SSt_star))
+    varMatrix = [-np.linalg.solve(e["B_exp"] - e["SSt_exp"], np.eye(p)) for e in outp]   # :856
+    seLoad = np.stack([np.sqrt(np.diag(v)) for v in varMatrix], 1)                     # :857
+    return dict(components=outp, varMatrix=varMatrix, seLoad=seLoad, W=W)

@@ -84,6 +84,9 @@ SIGNATURES = {
                                     _dp, _dp]),
     "ppls_meta_ppls": (ct.c_int, [ct.c_void_p, ct.c_int, _i64p, _i64p, ct.c_int, ct.c_double, ct.c_int,
                                   ct.POINTER(PplsTheta), ct.POINTER(PplsMetaFit)]),
+    "ppls_variances": (ct.c_int, [ct.c_void_p, _dp, _dp, ct.c_double, ct.c_int, ct.c_int, _dp, _dp, _dp, _dp,
+                                  _dp, _dp]),
+    "ppls_gram": (ct.c_int, [ct.c_void_p, ct.c_int, ct.c_int, _dp, _dp]),
     "ppls_sweep_timing": (ct.c_int, [ct.c_void_p, _dp, ct.POINTER(ct.c_int64), ct.c_int]),
     "ppls_finalize_trace": (ct.c_int, [ct.c_void_p, ct.POINTER(ct.c_int64), _dp]),
     "ppls_sweep_info": (ct.c_int, [ct.c_void_p, ct.c_int, ct.POINTER(ct.c_int64), ct.POINTER(ct.c_int),

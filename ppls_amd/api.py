@@ -10,6 +10,7 @@ Same names, argument meaning, return structure and error behaviour as the R func
 * ``loglC_fast``   Package/PPLS/src/loglC.cpp:318-338 (via RcppExports.R:32-34)
 * ``meta_EMstep``  Package/PPLS/R/EM_W_multi.R:446-485 (meta_Estep/meta_Mstep, src/loglC.cpp:399-474)
 * ``meta_PPLSi``   Package/PPLS/R/EM_W_multi.R:509-589
+* ``variances_PPLS_simult``  Package/PPLS/R/EM_W_multi.R:830-860 (variances.PPLS_simult)
 
 Every call goes through the C ABI (include/ppls.h) into the HIP kernels on the GPU; matrices
 are numpy arrays, R lists are dicts.  Passing ``X=None, Y=None`` uses the data already resident
@@ -273,6 +274,38 @@ class Context:
                                          int(max_steps), float(atol), int(bool(crit_abs)), ct.byref(t),
                                          ct.byref(fit)))
         return Wo, Co, po, lg[: fit.steps + 1].copy()
+
+    def variances(self, mu, Cdiag, sigE, xory, full=True):
+        """variances.PPLS_simult (EM_W_multi.R:830-860) on the resident X (xory 0) or Y (xory 1):
+        mu = this rank's rows of Expectations$mu_T / mu_U (n_local x a), Cdiag = diag(Ctt / Cuu).
+        Returns (W, B_exp scalars, varMatrix a x p x p, seLoad p x a, SSt_exp, SSt_star) -- the
+        last two (a x p x p) only with full=True."""
+        mu = np.asfortranarray(np.array(mu, dtype=np.float64, ndmin=2).reshape(self.n_local, -1))
+        a = mu.shape[1]
+        p = self.q if xory else self.p
+        Cd = np.ascontiguousarray(np.ravel(Cdiag), dtype=np.float64)
+        if Cd.shape[0] != a:
+            raise ValueError(f"{Cd.shape[0]} variances for {a} components")
+        W = np.zeros((p, a), order="F")
+        Bx = np.zeros(a)
+        V = np.zeros((a, p, p))            # component i: V[i] holds the column-major p x p as its transpose
+        se = np.zeros((p, a), order="F")
+        SE = np.zeros((a, p, p)) if full else None
+        SS = np.zeros((a, p, p)) if full else None
+        self._chk(self._L.ppls_variances(self.h, dptr(mu), dptr(Cd), float(sigE), int(a), int(xory), dptr(W),
+                                         dptr(Bx), dptr(V), dptr(SE), dptr(SS), dptr(se)))
+        # buffers hold consecutive column-major matrices: transpose each back (all are symmetric up to
+        # rounding except where the inverse is not exactly symmetric)
+        tr = (lambda A: None if A is None else np.ascontiguousarray(np.transpose(A, (0, 2, 1))))
+        return W, Bx, tr(V), se, tr(SE), tr(SS)
+
+    def gram(self, xory=0, nsplit=0, want=True):
+        """D'D (D = X or Y) on the MFMA Gram kernel alone -> (G or None, kernel ms)."""
+        p = self.q if xory else self.p
+        G = np.zeros((p, p), order="F") if want else None
+        ms = ct.c_double()
+        self._chk(self._L.ppls_gram(self.h, int(xory), int(nsplit), dptr(G), ct.byref(ms)))
+        return G, ms.value
 
     def scores(self, W, C):
         """scores.PPLS (EM_W_multi.R:411-420) on the resident rows: (X W, Y C), n_local x k each."""
@@ -603,6 +636,43 @@ def meta_PPLSi(X, Y, Ipopu, EMsteps=100, atol=1e-4, initialGuess=("equal", "o2m"
         raise NotImplementedError("critfunc must be the identity (default) or abs")
     W, C, P, lg = ctx.meta_ppls(counts, int(EMsteps), float(atol), init, crit_abs)
     return dict(W=W, C=C, params=_params_list(levels, P), log=lg[1:], logvalue=lg)
+
+
+def variances_PPLS_simult(fit, data, XorY=("X", "Y"), ctx=None, full=True):
+    """variances.PPLS_simult (EM_W_multi.R:830-860) on the GPU: asymptotic standard errors of the
+    loadings.  ``fit``: a PPLS_simult list (Expectations, estimates); ``data``: X (XorY = "X") or Y
+    (XorY = "Y"), or None to use the context's resident X / Y.  Returns the reference's list: per
+    component dict(B_exp, SSt_exp, SSt_star), then varMatrix (list of p x p) and seLoad (p x a);
+    full=False skips the p x p B_exp / SSt_exp / SSt_star matrices (B_exp is then its scalar).
+    The reference's t(X) %*% diag(Ctt, N) %*% X is Ctt X'X, computed once on MFMA; like the reference
+    it uses estimates$sigE for XorY = "Y" as well."""
+    if isinstance(XorY, (list, tuple)):
+        raise ValueError("the condition has length > 1")   # if(XorY=="X") with the default c("X","Y")
+    if XorY not in ("X", "Y"):
+        return None                                        # neither branch: W undefined in R
+    xory = 0 if XorY == "X" else 1
+    E = fit["Expectations"]
+    mu = np.asarray(E["mu_T"] if xory == 0 else E["mu_U"])
+    Cd = np.diag(np.asarray(E["Ctt"] if xory == 0 else E["Cuu"]))
+    sigE = float(np.ravel(fit["estimates"]["sigE"])[0])
+    own = None
+    if data is not None:
+        D = np.asarray(data, dtype=np.float64)
+        own = Context(0) if ctx is None else ctx
+        dummy = np.zeros((D.shape[0], 1))
+        own.set_data(D, dummy) if xory == 0 else own.set_data(dummy, D)
+        c = own
+    else:
+        c = ctx or default_context()
+    try:
+        W, Bx, V, se, SE, SS = c.variances(mu, Cd, sigE, xory, full)
+    finally:
+        if own is not None and ctx is None:
+            own.close()
+    p = W.shape[0]
+    comps = [dict(B_exp=(Bx[i] * np.eye(p) if full else float(Bx[i])),
+                  SSt_exp=(SE[i] if full else None), SSt_star=(SS[i] if full else None)) for i in range(len(Bx))]
+    return dict(components=comps, varMatrix=[V[i] for i in range(len(Bx))], seLoad=se, W=W)
 
 
 def PPLS_simult(X, Y, a, EMsteps=10, atol=1e-4, type=("SVD", "QR"), init=None, ctx=None, **kw):

@@ -16,7 +16,7 @@ LIB = os.path.join(HERE, "libppls_amd.so")
 ARCH = os.environ.get("PPLS_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
-SOURCES = ["ppls_kernels.hip", "ppls_capi.cpp"]
+SOURCES = ["ppls_kernels.hip", "ppls_variances.hip", "ppls_capi.cpp"]
 HEADERS = ["ppls_kernels.h", "ppls_math.h"]
 CFLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function", "-Wno-inline-asm",
           "-I" + os.path.join(ROOT, "include"), "-I" + CSRC]
@@ -42,7 +42,7 @@ def build(force: bool = False, verbose: bool = True) -> str:
             subprocess.run(cmd, check=True)
     if force or _mtime(LIB) < max(_mtime(o) for o in objs):
         cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB, *objs,
-               "-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"]
+               "-L/opt/rocm/lib", "-lrccl", "-lrocsolver", "-lrocblas", "-Wl,-rpath,/opt/rocm/lib"]
         if verbose:
             print(" ".join(cmd), flush=True)
         subprocess.run(cmd, check=True)

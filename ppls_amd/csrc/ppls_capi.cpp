@@ -7,6 +7,8 @@
 // when the convergence test of PPLS_simult (EM_W_multi.R:792) needs it.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
+#include <rocblas/rocblas.h>
+#include <rocsolver/rocsolver.h>
 
 #include <algorithm>
 #include <cmath>
@@ -77,6 +79,7 @@ struct ppls_ctx {
   // device-resident iteration state (ppls_em_begin / ppls_em_iterate)
   int em_r = 0, em_cur = 0, em_iter = 0;
   bool em_active = false;
+  rocblas_handle blas = nullptr;   // rocSOLVER (variances.PPLS_simult's p x p inverse), created lazily
   // timing
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;
   size_t ev_used = 0;
@@ -602,6 +605,7 @@ void ppls_ctx_destroy(ppls_ctx* c) {
   dfree(c->work); dfree(c->status); dfree(c->coefs); dfree(c->scratch);
   if (c->ftrace) (void)hipFree(c->ftrace);
   for (auto& e : c->ev) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
+  if (c->blas) (void)rocblas_destroy_handle(c->blas);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -1499,6 +1503,189 @@ int ppls_meta_ppls(ppls_ctx* c, int npop, const int64_t* pop_local, const int64_
   std::copy(w.begin(), w.end(), out->W);
   std::copy(cv.begin(), cv.end(), out->C);
   meta_params_out(pops, out->params);
+  return PPLS_OK;
+}
+
+// variances.PPLS_simult (EM_W_multi.R:830-860).  X'X (or Y'Y) once on MFMA for all components,
+// Cxt = X' mu in one HBM pass, then per component the p x p B_exp - SSt_exp on the device and its
+// inverse by rocSOLVER getrf/getri (R's solve()).  Data-dependent sums are all-reduced over ranks.
+int ppls_variances(ppls_ctx* c, const double* mu, const double* Cdiag, double sigE, int a, int xory, double* W,
+                   double* B_exp, double* varMatrix, double* SSt_exp, double* SSt_star, double* seLoad) {
+  if (!c) return PPLS_E_ARG;
+  if (!c->have_data) return fail(c, PPLS_E_STATE, "no data");
+  if ((!mu && c->n_local > 0) || !Cdiag || !W || !B_exp || !seLoad) return fail(c, PPLS_E_ARG, "NULL argument");
+  if (a < 1 || a > 16) return fail(c, PPLS_E_ARG, "number of components %d outside [1, 16]", a);
+  if (xory != 0 && xory != 1) return fail(c, PPLS_E_ARG, "XorY must be 0 (\"X\") or 1 (\"Y\")");
+  HIPCHK(c, hipSetDevice(c->device));
+  const int f32 = c->dtype;
+  const int p = xory ? c->q : c->p, ld = xory ? c->ldy : c->ldx;
+  const void* D = xory ? (const void*)c->Y : (const void*)c->X;
+  const int64_t n = c->n_local;
+  const double N = (double)c->n_total;
+  if (a > p) return fail(c, PPLS_E_ARG, "more components (%d) than columns (%d)", a, p);
+  int rc = PPLS_OK;
+  double *dmu = nullptr, *dpart = nullptr, *dS = nullptr, *dG = nullptr, *dM = nullptr, *dv = nullptr;
+  double *dexp = nullptr, *dstar = nullptr, *dse = nullptr;
+  rocblas_int *ipiv = nullptr, *info = nullptr;
+  auto done = [&](int code) {
+    dfree(dmu); dfree(dpart); dfree(dS); dfree(dG); dfree(dM); dfree(dv); dfree(dexp); dfree(dstar); dfree(dse);
+    if (ipiv) (void)hipFree(ipiv);
+    if (info) (void)hipFree(info);
+    return code;
+  };
+#define VCHK(call)                                                                              \
+  do {                                                                                          \
+    hipError_t e_ = (call);                                                                     \
+    if (e_ != hipSuccess) return done(fail(c, PPLS_E_HIP, "%s: %s", #call, hipGetErrorString(e_))); \
+  } while (0)
+#define VRC(call)                  \
+  do {                             \
+    if ((rc = (call))) return done(rc); \
+  } while (0)
+  const size_t pp = (size_t)p * p;
+  // ---- Cxt = D' mu (a x ld, column k contiguous) and ||mu_k||^2 (all-reduced) ----------------
+  const int chunks = ppls_xtmu_chunks(std::max<int64_t>(n, 1), ld, f32);
+  const int64_t sld = (int64_t)a * ld;
+  VRC(dalloc(c, &dS, (size_t)sld + 16));
+  std::vector<double> mu2(a, 0.0);
+  if (n > 0) {
+    VRC(dalloc(c, &dmu, (size_t)n * a));
+    VRC(dalloc(c, &dpart, (size_t)chunks * sld + (size_t)ppls_reduce_tmp_len(chunks, sld)));
+    VCHK(hipMemcpyAsync(dmu, mu, sizeof(double) * n * a, hipMemcpyHostToDevice, c->stream));
+    VCHK(ppls_launch_xtmu(D, f32, n, ld, dmu, a, chunks, dpart, sld, c->stream));
+    VCHK(ppls_launch_reduce2(dpart, chunks, sld, sld, dS, dpart + (size_t)chunks * sld, c->stream));
+    for (int k = 0; k < a; ++k)
+      for (int64_t i = 0; i < n; ++i) mu2[k] += mu[(size_t)k * n + i] * mu[(size_t)k * n + i];   // crossprod(mu_T)
+    dfree(dpart);
+  } else {
+    VCHK(hipMemsetAsync(dS, 0, sizeof(double) * sld, c->stream));
+  }
+  VCHK(hipMemcpyAsync(dS + sld, mu2.data(), sizeof(double) * a, hipMemcpyHostToDevice, c->stream));
+  VRC(allreduce(c, dS, (size_t)sld + a));
+  std::vector<double> S((size_t)sld + a);
+  VCHK(hipMemcpyAsync(S.data(), dS, sizeof(double) * S.size(), hipMemcpyDeviceToHost, c->stream));
+  VCHK(hipStreamSynchronize(c->stream));
+  std::vector<double> Sp((size_t)p * a);   // t(data) %*% mu (p x a, column-major)
+  for (int k = 0; k < a; ++k)
+    for (int i = 0; i < p; ++i) Sp[(size_t)k * p + i] = S[(size_t)k * ld + i];
+  for (int k = 0; k < a; ++k) mu2[k] = S[(size_t)sld + k];
+  // W = orth(t(data) %*% mu, type = "SVD") (:831-832)
+  if ((rc = host_orth(Sp.data(), p, a, PPLS_ORTH_SVD, W)))
+    return done(fail(c, rc, "orth(t(data) %%*%% mu): rank-deficient"));
+  // ---- G = D'D on MFMA, split over row ranges, all-reduced ----------------------------------
+  VRC(dalloc(c, &dG, pp));
+  if (n > 0) {
+    const int ntiles = ppls_gram_tiles(p);
+    const int64_t slots = (int64_t)c->num_cus * ppls_gram_occupancy(f32);
+    int nsplit = 1;
+    double best = -1.0;
+    for (int sp = 1; sp <= 32; ++sp) {
+      if (sp > 1 && ((int64_t)sp * 512 > n || (double)sp * pp * 8.0 > 4.0e9)) break;
+      const int64_t w = (int64_t)ntiles * sp;
+      const double eff = (double)w / (double)(((w + slots - 1) / slots) * slots);
+      if (eff > best + 1e-9) { best = eff; nsplit = sp; }
+      if (eff >= 0.95) break;
+    }
+    VRC(dalloc(c, &dpart, (size_t)nsplit * pp));
+    VCHK(ppls_launch_gram(D, f32, n, ld, p, nsplit, dpart, (int64_t)pp, c->stream));
+    VCHK(ppls_launch_gram_finish(dpart, nsplit, (int64_t)pp, p, dG, c->stream));
+    dfree(dpart);
+  } else {
+    VCHK(hipMemsetAsync(dG, 0, sizeof(double) * pp, c->stream));
+  }
+  VRC(allreduce(c, dG, pp));
+  // ---- per component: M = B_exp - SSt_exp, varMatrix = -solve(M), seLoad --------------------
+  if (!c->blas) {
+    if (rocblas_create_handle(&c->blas) != rocblas_status_success) return done(fail(c, PPLS_E_HIP, "rocblas_create_handle failed"));
+  }
+  if (rocblas_set_stream(c->blas, c->stream) != rocblas_status_success) return done(fail(c, PPLS_E_HIP, "rocblas_set_stream failed"));
+  VRC(dalloc(c, &dM, pp));
+  VRC(dalloc(c, &dv, (size_t)2 * p));
+  VRC(dalloc(c, &dse, (size_t)p));
+  if (SSt_exp) VRC(dalloc(c, &dexp, pp));
+  if (SSt_star) VRC(dalloc(c, &dstar, pp));
+  VCHK(hipMalloc((void**)&ipiv, sizeof(rocblas_int) * p));
+  VCHK(hipMalloc((void**)&info, sizeof(rocblas_int)));
+  const double s2 = sigE * sigE, s4 = s2 * s2;
+  std::vector<double> v2((size_t)2 * p);
+  for (int i = 0; i < a; ++i) {
+    const double ctt = N * Cdiag[i];                         // Ctt = N * t(Ctt[i, i]) (:840)
+    const double Vt = ctt - mu2[i];                          // Vt = Ctt - crossprod(mu_T) (:842)
+    const double k1 = ctt + 2.0 * Vt;
+    const double k2 = ctt * ctt + 4.0 * mu2[i] * Vt + 2.0 * Vt * Vt;
+    const double bstar = ctt / s2 / N;                       // B_star = c(Ctt)/(sigE^2) * I / nrow(X) (:844)
+    B_exp[i] = bstar;
+    for (int e = 0; e < p; ++e) {
+      v2[e] = Sp[(size_t)i * p + e];                         // Cxt = t(X) %*% mu_T (:843)
+      v2[(size_t)p + e] = W[(size_t)i * p + e];
+    }
+    VCHK(hipMemcpyAsync(dv, v2.data(), sizeof(double) * 2 * p, hipMemcpyHostToDevice, c->stream));
+    VCHK(ppls_launch_varmat(dG, dv, dv + p, p, ctt, k1, k2, bstar, s4, N, dM, dexp, dstar, c->stream));
+    if (SSt_exp) VCHK(hipMemcpyAsync(SSt_exp + (size_t)i * pp, dexp, sizeof(double) * pp, hipMemcpyDeviceToHost, c->stream));
+    if (SSt_star) VCHK(hipMemcpyAsync(SSt_star + (size_t)i * pp, dstar, sizeof(double) * pp, hipMemcpyDeviceToHost, c->stream));
+    if (rocsolver_dgetrf(c->blas, p, p, dM, p, ipiv, info) != rocblas_status_success ||
+        rocsolver_dgetri(c->blas, p, dM, p, ipiv, info) != rocblas_status_success)
+      return done(fail(c, PPLS_E_HIP, "rocsolver getrf/getri failed"));
+    rocblas_int inf = 0;
+    VCHK(hipMemcpyAsync(&inf, info, sizeof inf, hipMemcpyDeviceToHost, c->stream));
+    VCHK(hipStreamSynchronize(c->stream));
+    if (inf != 0)   // solve(): "Lapack routine dgesv: system is exactly singular"
+      return done(fail(c, PPLS_E_NUMERIC, "component %d: B_exp - SSt_exp is exactly singular (U[%d,%d] = 0)", i + 1,
+                       (int)inf, (int)inf));
+    VCHK(ppls_launch_negdiag(dM, p, dse, c->stream));
+    if (varMatrix) VCHK(hipMemcpyAsync(varMatrix + (size_t)i * pp, dM, sizeof(double) * pp, hipMemcpyDeviceToHost, c->stream));
+    VCHK(hipMemcpyAsync(seLoad + (size_t)i * p, dse, sizeof(double) * p, hipMemcpyDeviceToHost, c->stream));
+  }
+  VCHK(hipStreamSynchronize(c->stream));
+#undef VCHK
+#undef VRC
+  return done(PPLS_OK);
+}
+
+// Diagnostics / benchmark: G = D'D (D = X for xory 0, Y for 1) on the MFMA Gram kernel only, with an
+// explicit split count (0 = auto as in ppls_variances); G (p x p, column-major) may be NULL.
+// *ms receives the Gram kernel's duration (HIP events on the context stream).
+int ppls_gram(ppls_ctx* c, int xory, int nsplit, double* G, double* ms) {
+  if (!c) return PPLS_E_ARG;
+  if (!c->have_data) return fail(c, PPLS_E_STATE, "no data");
+  HIPCHK(c, hipSetDevice(c->device));
+  const int p = xory ? c->q : c->p, ld = xory ? c->ldy : c->ldx;
+  const void* D = xory ? (const void*)c->Y : (const void*)c->X;
+  const size_t pp = (size_t)p * p;
+  if (c->n_local <= 0) return fail(c, PPLS_E_STATE, "no rows on this rank");
+  if (nsplit <= 0) {
+    const int ntiles = ppls_gram_tiles(p);
+    const int64_t slots = (int64_t)c->num_cus * ppls_gram_occupancy(c->dtype);
+    double best = -1.0;
+    for (int sp = 1; sp <= 32; ++sp) {
+      if (sp > 1 && ((int64_t)sp * 512 > c->n_local || (double)sp * pp * 8.0 > 4.0e9)) break;
+      const int64_t w = (int64_t)ntiles * sp;
+      const double eff = (double)w / (double)(((w + slots - 1) / slots) * slots);
+      if (eff > best + 1e-9) { best = eff; nsplit = sp; }
+      if (eff >= 0.95) break;
+    }
+  }
+  int rc;
+  double *dpart = nullptr, *dG = nullptr;
+  if ((rc = dalloc(c, &dpart, (size_t)nsplit * pp))) return rc;
+  if ((rc = dalloc(c, &dG, pp))) { dfree(dpart); return rc; }
+  hipEvent_t e0, e1;
+  HIPCHK(c, hipEventCreate(&e0));
+  HIPCHK(c, hipEventCreate(&e1));
+  hipError_t e = hipEventRecord(e0, c->stream);
+  if (e == hipSuccess) e = ppls_launch_gram(D, c->dtype, c->n_local, ld, p, nsplit, dpart, (int64_t)pp, c->stream);
+  if (e == hipSuccess) e = hipEventRecord(e1, c->stream);
+  if (e == hipSuccess) e = ppls_launch_gram_finish(dpart, nsplit, (int64_t)pp, p, dG, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  float t = 0.f;
+  if (e == hipSuccess) e = hipEventElapsedTime(&t, e0, e1);
+  if (e == hipSuccess && G) e = hipMemcpy(G, dG, sizeof(double) * pp, hipMemcpyDeviceToHost);
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  dfree(dpart);
+  dfree(dG);
+  if (e != hipSuccess) return fail(c, PPLS_E_HIP, "gram: %s", hipGetErrorString(e));
+  if (ms) *ms = t;
   return PPLS_OK;
 }
 

@@ -93,6 +93,20 @@ hipError_t ppls_launch_generate(int64_t n_local, int64_t row0, int p, int q, int
                                 uint64_t seed, double* TU, double* X, double* Y, hipStream_t st);
 hipError_t ppls_launch_to_rowmajor(const double* src, int64_t n, int p, int ld, double* dst,
                                    hipStream_t st);
+// variances.PPLS_simult (ppls_variances.hip)
+int ppls_gram_tiles(int p);
+int ppls_gram_occupancy(int f32);
+hipError_t ppls_launch_gram(const void* X, int f32, int64_t n, int ld, int p, int nsplit, double* part,
+                            int64_t part_stride, hipStream_t st);
+hipError_t ppls_launch_gram_finish(const double* part, int nsplit, int64_t part_stride, int p, double* G,
+                                   hipStream_t st);
+int ppls_xtmu_chunks(int64_t n, int ld, int f32);
+hipError_t ppls_launch_xtmu(const void* X, int f32, int64_t n, int ld, const double* mu, int a, int chunks,
+                            double* part, int64_t part_ld, hipStream_t st);
+hipError_t ppls_launch_varmat(const double* G, const double* cxt, const double* w, int p, double ctt, double k1,
+                              double k2, double bstar, double s4, double N, double* M, double* sst_exp,
+                              double* sst_star, hipStream_t st);
+hipError_t ppls_launch_negdiag(double* M, int p, double* se, hipStream_t st);
 hipError_t ppls_launch_to_colmajor(const double* src, int64_t n, int p, int ld, double* dst,
                                    hipStream_t st);
 }

@@ -188,3 +188,26 @@ def test_meta_golden_reproduces(name):
     assert np.array_equal(f["logvalue"], g["logvalue"]) and np.array_equal(f["W"], g["W"])
     # the EM never decreases the summed log-likelihood after the first step (row 0 is rep(full, K))
     assert np.all(np.diff(g["logvalue"][1:].sum(1)) > -1e-9)
+
+
+def test_variances_restatement_equals_literal_nxn_form():
+    # variances.PPLS_simult (EM_W_multi.R:846) forms t(X) %*% diag(c(Ctt), N) %*% X with an N x N
+    # diagonal; the oracle (and the device) use Ctt * X'X -- the same matrix
+    X, Y, th0 = make_problem(60, 7, 5, 2, seed=51)
+    fit = o.ppls_simult(X, Y, 2, EMsteps=5, atol=-np.inf, theta0=th0)
+    v = o.variances_ppls_simult(fit, X, "X")
+    N = X.shape[0]
+    E, sE = fit["Expectations"], fit["estimates"]["sigE"]
+    for i in range(2):
+        Ctt = N * E["Ctt"][i, i]
+        mu = E["mu_T"][:, i]
+        w = v["W"][:, [i]]
+        Vt = Ctt - mu @ mu
+        Cxt = (X.T @ mu)[:, None]
+        lit = (X.T @ np.diag(np.full(N, Ctt)) @ X - Cxt * (Ctt + 2 * Vt) @ w.T - w * (Ctt + 2 * Vt) @ Cxt.T
+               + w * (Ctt ** 2 + 4 * (mu @ mu) * Vt + 2 * Vt * Vt) @ w.T) / sE ** 4 / N
+        assert np.abs(lit - v["components"][i]["SSt_exp"]).max() < 1e-12 * np.abs(lit).max()
+        # -solve(B_exp - SSt_exp) is a symmetric matrix; its diagonal gives seLoad
+        V = v["varMatrix"][i]
+        assert np.abs(V - V.T).max() < 1e-10 * np.abs(V).max()
+        assert np.allclose(v["seLoad"][:, i] ** 2, np.diag(V), rtol=1e-12)

@@ -1,0 +1,64 @@
+"""variances.PPLS_simult at a BASELINE shape: MFMA Gram X'X rate and the whole call.
+
+    python tools/bench_variances.py [--config c3|c2|c5] [--reps 3] [--no-full]
+
+Data: the bench's synthetic simulC model generated on the device; the fit is a short device
+PPLS_simult run (its Expectations feed variances).  Prints one JSON line: Gram kernel time and
+fp64 MFMA TFLOP/s (executed tile flops and the useful n p (p + 1) SYRK flops) against the 78.6 TF
+fp64 matrix peak, and the wall time of the whole variances call (Cxt pass, Gram, per-component
+p x p build + rocSOLVER inverse + copies).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from bench import CONFIGS, FP64_PEAK_TF, make_truth_and_theta0  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--nsplit", type=int, default=0)
+    ap.add_argument("--em-steps", type=int, default=3)
+    ap.add_argument("--no-full", action="store_true", help="skip the whole variances call")
+    args = ap.parse_args()
+    from ppls_amd import Context
+    cfg = CONFIGS[args.config]
+    n, p, q, r = cfg["n"], cfg["p"], cfg["q"], cfg["r"]
+    ctx = Context(0)
+    if cfg.get("storage") == "f32":
+        ctx.set_option("dtype", 1)
+    truth, th0 = make_truth_and_theta0(p, q, r)
+    ctx.generate_synthetic(n, p, q, truth, seed=20261015)
+    ctx.gram(0, args.nsplit, want=False)   # warm-up (code object load, allocations)
+    times = [ctx.gram(0, args.nsplit, want=False)[1] for _ in range(args.reps)]
+    ms = float(np.median(times))
+    nb = (p + 127) // 128
+    tiles = nb * (nb + 1) // 2
+    exec_flops = 2.0 * n * tiles * 128 * 128
+    useful = float(n) * p * (p + 1)
+    out = dict(config=cfg["name"], gram_kernel_ms=ms, gram_kernel_ms_all=times,
+               gram_exec_tflops=exec_flops / ms / 1e9, gram_useful_tflops=useful / ms / 1e9,
+               fp64_mfma_peak_tflops=FP64_PEAK_TF, mfma_frac=exec_flops / ms / 1e9 / FP64_PEAK_TF,
+               tiles=tiles)
+    if not args.no_full:
+        est, ll, eout, _ = ctx.em_run(th0, args.em_steps, -np.inf, 0, want_eout=True, want_mu=True)
+        t0 = time.perf_counter()
+        W, Bx, V, se, _, _ = ctx.variances(eout.mu_T, eout.Ctt, est.sigE, 0, full=False)
+        out["variances_s"] = time.perf_counter() - t0
+        out["seLoad_median"] = float(np.median(se))
+        out["seLoad_finite"] = bool(np.all(np.isfinite(se)))
+    ctx.close()
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
