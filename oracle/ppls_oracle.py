@@ -20,6 +20,7 @@ Every function cites the reference line it restates (paths relative to /root/ref
 * ``initial_guess``      Package/PPLS/R/EM_W_multi.R:126-140 ('equal'; 'random' with numpy draws)
 * ``scores_ppls``        Package/PPLS/R/EM_W_multi.R:411-420
 * ``ppls_simult_to_o2m`` Package/PPLS/R/PPLS_to_o2m.R:82-140
+* ``ppls_to_o2m``        Package/PPLS/R/PPLS_to_o2m.R:28-80 (literal, with the n x p products)
 * ``meta_estep``         Package/PPLS/src/loglC.cpp:399-448 (one population's rank-1 E-step)
 * ``meta_mstep``         Package/PPLS/src/loglC.cpp:452-474
 * ``meta_emstep``        Package/PPLS/R/EM_W_multi.R:446-485 (populations = contiguous blocks :451-458)
@@ -504,6 +505,19 @@ def scores_ppls(W, C, X, Y, subset=None):
     if len(cols) == 1:
         return np.concatenate([X @ W[:, cols[0]], Y @ C[:, cols[0]]])
     return np.vstack([X @ W[:, cols], Y @ C[:, cols]])
+
+
+def ppls_to_o2m(X, Y, fit):
+    """PPLS_to_o2m -- Package/PPLS/R/PPLS_to_o2m.R:28-80 (the numeric fields), literal."""
+    W, C = np.asarray(fit["W"]), np.asarray(fit["C"])
+    B_T = np.diag(np.ravel(fit["B"]))                                             # :33
+    B_U = np.linalg.solve(B_T, np.eye(B_T.shape[0]))                               # :34
+    Tt, U = X @ W, Y @ C                                                          # :35-36
+    ssqX, ssqY = ssq(X), ssq(Y)                                                   # :44-45
+    return dict(Tt=Tt, U=U, B_T_=B_T, B_U=B_U, H_UT=U - Tt @ B_T,
+                R2Xcorr=ssq(Tt) / ssqX, R2Ycorr=ssq(U) / ssqY,                     # :47-48
+                R2Xhat=ssq(U @ B_U @ W.T) / ssqX, R2Yhat=ssq(Tt @ B_T @ C.T) / ssqY,  # :51-52
+                ssqX=ssqX, ssqY=ssqY, varXjoint=np.sum(Tt * Tt, axis=0), varYjoint=np.sum(U * U, axis=0))
 
 
 def ppls_simult_to_o2m(X, Y, fit):

@@ -10,6 +10,7 @@ Same names, argument meaning, return structure and error behaviour as the R func
 * ``loglC_fast``   Package/PPLS/src/loglC.cpp:318-338 (via RcppExports.R:32-34)
 * ``meta_EMstep``  Package/PPLS/R/EM_W_multi.R:446-485 (meta_Estep/meta_Mstep, src/loglC.cpp:399-474)
 * ``meta_PPLSi``   Package/PPLS/R/EM_W_multi.R:509-589
+* ``PPLS_to_o2m``  Package/PPLS/R/PPLS_to_o2m.R:28-80
 * ``variances_PPLS_simult``  Package/PPLS/R/EM_W_multi.R:830-860 (variances.PPLS_simult)
 
 Every call goes through the C ABI (include/ppls.h) into the HIP kernels on the GPU; matrices
@@ -532,6 +533,42 @@ def scores_PPLS(fit, X, Y, subset=None, ctx=None):
     if len(cols) == 1:
         return np.concatenate([T[:, 0], U[:, 0]])
     return np.vstack([T, U])
+
+
+def PPLS_to_o2m(X_true, Y_true, fit_PPLS, ctx=None):
+    """PPLS_to_o2m (PPLS_to_o2m.R:28-80): a sequential PPLS fit as an OmicsPLS "o2m" list.  The
+    scores Tt = X W, U = Y C come from one device pass (ppls_scores); ssq(X), ssq(Y) from the
+    context; ssq(U B_U W'), ssq(Tt B_T C') are evaluated as r x r traces (no n x p product)."""
+    ctx = _ctx_with(X_true, Y_true, ctx)
+    W = np.asarray(fit_PPLS["W"], dtype=np.float64).reshape(ctx.p, -1)
+    C = np.asarray(fit_PPLS["C"], dtype=np.float64).reshape(ctx.q, -1)
+    b = np.ravel(np.asarray(fit_PPLS["B"], dtype=np.float64))
+    B_T = np.diag(b)                                          # diag(fit_PPLS$B, length(fit_PPLS$B)) (:33)
+    B_U = np.linalg.inv(B_T)                                  # solve(B_T) (:34)
+    Tt, U = ctx.scores(W, C)                                  # :35-36
+    n = Tt.shape[0]
+    ssqX, ssqY = ctx.ssq()                                    # :44-45
+
+    def ssq(A):
+        A = np.asarray(A, dtype=np.float64)
+        return float(np.sum(A * A))
+
+    def ssq_prod(S, M, L):   # ssq(S M L') = tr(M' S'S M L'L)
+        return float(np.trace(M.T @ (S.T @ S) @ M @ (L.T @ L)))
+    R2Xcorr, R2Ycorr = ssq(Tt) / ssqX, ssq(U) / ssqY          # :47-48
+    R2Xhat = ssq_prod(U, B_U, W) / ssqX                       # :51
+    R2Yhat = ssq_prod(Tt, B_T, C) / ssqY                      # :52
+    z = lambda r, c: np.zeros((r, c))
+    model = dict(Tt=Tt, U=U, W_=W, C_=C, P_Yosc_=z(W.shape[0], 1), P_Xosc_=z(C.shape[0], 1),
+                 T_Yosc_=z(n, 1), U_Xosc_=z(n, 1), W_Yosc=z(W.shape[0], 1), C_Xosc=z(C.shape[0], 1),
+                 B_T_=B_T, B_U=B_U, H_TU=0 * Tt, H_UT=U - Tt @ B_T,
+                 R2X=R2Xcorr + 0.0, R2Y=R2Ycorr + 0.0, R2Xcorr=R2Xcorr, R2Ycorr=R2Ycorr, R2Xhat=R2Xhat,
+                 R2Yhat=R2Yhat)                               # :60-64 (R2X_YO = R2Y_XO = 0)
+    model["flags"] = dict(time=float("nan"), n=W.shape[1], nx=0, ny=0, stripped=True, highd=False, ssqX=ssqX,
+                          ssqY=ssqY, varXjoint=np.sum(Tt * Tt, axis=0), varYjoint=np.sum(U * U, axis=0),
+                          varXorth=np.zeros(1), varYorth=np.zeros(1))
+    model["class"] = ["o2m", "o2m_stripped"]
+    return model
 
 
 def PPLS_simult_to_o2m(X_true, Y_true, fit_PPLS, ctx=None):

@@ -99,3 +99,68 @@ def test_sharded_em_equals_unsharded_oracle(world):
     W, C, B, T = o.canonicalize(res[0][1], res[0][2], np.diag(res[0][3]), np.diag(res[0][4]))
     assert np.abs(W - ref["estimates"]["W"]).max() < 1e-10
     assert np.abs(C - ref["estimates"]["C"]).max() < 1e-10
+
+
+def _meta_worker(rank, world, port, q_out):
+    import sys
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import torch
+    import torch.distributed as dist
+    from oracle import ppls_oracle as o
+    from ppls_amd.api import pop_rows
+    from ppls_amd import Context
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    g = np.load(os.path.join(ROOT, "tests", "golden", "meta_random_k3_p24_q18.npz"))
+    import json
+    sizes = json.loads(str(g["meta"]))["sizes"]
+    X, Y = g["X"], g["Y"]
+    n = X.shape[0]
+    row0, nl = Context.shard_range(n, world, rank)
+    loc, tot = pop_rows(sizes, row0, nl)
+    cf = o.mu_coefficients(np.eye(1) * 1.2, 0.7, 0.6, 0.3, np.eye(1) * 0.9)
+    w, c = g["init_W"].reshape(-1, 1), g["init_C"].reshape(-1, 1)
+    out = []
+    r0 = row0
+    for j in range(len(sizes)):   # this rank's rows of population j: one segment sweep + all-reduce
+        Xj, Yj = X[r0:r0 + loc[j]], Y[r0:r0 + loc[j]]
+        st = o.sweep_stats(Xj, Yj, w, c, cf)
+        buf = torch.from_numpy(np.concatenate([st["SX"].ravel(), st["SY"].ravel(), st["G"].ravel(),
+                                               [np.sum(Xj * Xj), np.sum(Yj * Yj)]]))
+        dist.all_reduce(buf)
+        out.append(buf.numpy().copy())
+        r0 += loc[j]
+    q_out.put((rank, out))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_meta_population_statistics(world):
+    """meta_* on sharded rows: each rank sweeps the intersection of its shard with each population
+    block; the all-reduced per-population statistics equal the unsharded ones."""
+    import json
+    from oracle import ppls_oracle as o
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_meta_worker, args=(r, world, port, q)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    res = sorted([q.get(timeout=300) for _ in range(world)], key=lambda t: t[0])
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    g = np.load(os.path.join(ROOT, "tests", "golden", "meta_random_k3_p24_q18.npz"))
+    sizes = json.loads(str(g["meta"]))["sizes"]
+    X, Y = g["X"], g["Y"]
+    cf = o.mu_coefficients(np.eye(1) * 1.2, 0.7, 0.6, 0.3, np.eye(1) * 0.9)
+    w, c = g["init_W"].reshape(-1, 1), g["init_C"].reshape(-1, 1)
+    Ni = np.concatenate([[0], np.cumsum(sizes)])
+    for j in range(len(sizes)):
+        Xj, Yj = X[Ni[j]:Ni[j + 1]], Y[Ni[j]:Ni[j + 1]]
+        st = o.sweep_stats(Xj, Yj, w, c, cf)
+        ref = np.concatenate([st["SX"].ravel(), st["SY"].ravel(), st["G"].ravel(), [np.sum(Xj * Xj), np.sum(Yj * Yj)]])
+        for rk in range(world):
+            assert np.allclose(res[rk][1][j], ref, rtol=1e-12, atol=1e-10)

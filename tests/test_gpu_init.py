@@ -144,6 +144,21 @@ def test_scores_and_to_o2m_match_oracle(ctx):
     assert np.isclose(m["flags"]["ssqX"], r["ssqX"], rtol=1e-12)
 
 
+def test_ppls_to_o2m_matches_oracle(ctx):
+    """PPLS_to_o2m (PPLS_to_o2m.R:28-80) on a device sequential fit: scores from one device pass,
+    R2 terms as r x r traces, against the literal n x p restatement."""
+    from ppls_amd import PPLS, PPLS_to_o2m
+    X, Y, _ = make_problem(330, 24, 19, 2, seed=53)
+    f = PPLS(X, Y, 2, EMsteps=30, atol=1e-6, initialGuess="equal", ctx=ctx)
+    m = PPLS_to_o2m(None, None, f, ctx=ctx)
+    r = o.ppls_to_o2m(X, Y, f)
+    for key in ("R2Xcorr", "R2Ycorr", "R2Xhat", "R2Yhat"):
+        assert np.isclose(m[key], r[key], rtol=1e-12), key
+    assert np.allclose(m["Tt"], r["Tt"], rtol=1e-12, atol=1e-12)
+    assert np.allclose(m["H_UT"], r["H_UT"], rtol=1e-12, atol=1e-12)
+    assert np.allclose(m["B_U"], r["B_U"], rtol=1e-14)
+
+
 def test_scores_fp32_storage(ctx):
     from ppls_amd import Context
     X, Y, th0 = make_problem(300, 33, 17, 2, seed=52)
