@@ -75,7 +75,9 @@ const char* ppls_strerror(int code);
 int ppls_ctx_create(int device, ppls_ctx** out);
 void ppls_ctx_destroy(ppls_ctx* ctx);
 const char* ppls_last_error(const ppls_ctx* ctx);
-/* keys: "sweep" (0 auto, 1 fused single-pass, 2 generic two-pass, 3 panel (wide p)), "grid" (workgroups, 0 = auto),
+/* keys: "sweep" (0 auto, 1 fused single-pass, 2 generic two-pass, 3 panel (wide p, two passes),
+ *                4 team (wide p, single pass; falls back to panel where no team plan exists)),
+ *       "grid" (workgroups, 0 = auto),
  *       "dtype" (storage of X, Y: 0 fp64, 1 fp32; arithmetic stays fp64; set before loading data),
  *       "nt" (sweep loads with the non-temporal cache policy: -1 auto (default: when X, Y exceed
  *             the 256 MB MALL), 0 off, 1 on),

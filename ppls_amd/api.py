@@ -367,7 +367,7 @@ class Context:
     def sweep_info(self, r):
         b, v, g = ct.c_int64(), ct.c_int(), ct.c_int()
         self._chk(self._L.ppls_sweep_info(self.h, int(r), ct.byref(b), ct.byref(v), ct.byref(g)))
-        return dict(bytes_per_sweep=b.value, variant={1: "fused512", 2: "twopass", 3: "fused1024", 4: "split512", 5: "panel"}[v.value], grid=g.value)
+        return dict(bytes_per_sweep=b.value, variant={1: "fused512", 2: "twopass", 3: "fused1024", 4: "split512", 5: "panel", 6: "team"}[v.value], grid=g.value)
 
 
 # ================================================================================ R mirror

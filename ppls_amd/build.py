@@ -16,8 +16,8 @@ LIB = os.path.join(HERE, "libppls_amd.so")
 ARCH = os.environ.get("PPLS_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
-SOURCES = ["ppls_kernels.hip", "ppls_variances.hip", "ppls_capi.cpp"]
-HEADERS = ["ppls_kernels.h", "ppls_math.h"]
+SOURCES = ["ppls_kernels.hip", "ppls_variances.hip", "ppls_team.hip", "ppls_capi.cpp"]
+HEADERS = ["ppls_kernels.h", "ppls_math.h", "ppls_device.h"]
 CFLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function", "-Wno-inline-asm",
           "-I" + os.path.join(ROOT, "include"), "-I" + CSRC]
 
@@ -30,8 +30,8 @@ def build(force: bool = False, verbose: bool = True) -> str:
     os.makedirs(BUILD, exist_ok=True)
     deps = [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(ROOT, "include", "ppls.h")]
     newest_dep = max(_mtime(d) for d in deps)
-    objs = []
-    for src in SOURCES:
+    objs, procs = [], []
+    for src in SOURCES:   # the translation units compile in parallel
         s = os.path.join(CSRC, src)
         o = os.path.join(BUILD, os.path.splitext(src)[0] + ".o")
         objs.append(o)
@@ -39,7 +39,15 @@ def build(force: bool = False, verbose: bool = True) -> str:
             cmd = [HIPCC, *CFLAGS, "-x", "hip", "-c", s, "-o", o]
             if verbose:
                 print(" ".join(cmd), flush=True)
-            subprocess.run(cmd, check=True)
+            procs.append((subprocess.Popen(cmd), o))
+    failed = False
+    for pr, o in procs:
+        if pr.wait() != 0:
+            failed = True
+            if os.path.exists(o):
+                os.remove(o)
+    if failed:
+        raise subprocess.CalledProcessError(1, "hipcc")
     if force or _mtime(LIB) < max(_mtime(o) for o in objs):
         cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB, *objs,
                "-L/opt/rocm/lib", "-lrccl", "-lrocsolver", "-lrocblas", "-Wl,-rpath,/opt/rocm/lib"]

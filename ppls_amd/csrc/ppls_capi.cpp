@@ -42,6 +42,13 @@ struct ppls_ctx {
   int64_t sweep_count = 0;
   // row segment the next sweeps cover (meta_* per-population sweeps); seg_rows < 0 = all rows
   int64_t seg_row0 = 0, seg_rows = -1;
+  // team single-pass sweep (wide data): exchange buffer, launch epoch, device status, current plan
+  uint64_t* team_xch = nullptr;
+  int64_t team_xch_words = 0;
+  uint32_t team_epoch = 0;
+  int* team_status = nullptr;
+  bool team_disabled = false;   // a cooperative launch was refused: panel sweep from then on
+  PplsTeamPlan tplan{};
   // communicator
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0;
@@ -315,10 +322,18 @@ int sweep_plan(ppls_ctx* c, int r, PplsSweepArgs* a) {
   a->q = c->q;
   a->r = r;
   a->threads = threads;
-  if (c->sweep_mode == 3 || c->dtype) {   // forced panel sweep (the only fp32-storage sweep)
+  // wide data / fp32 storage: the panel sweep (two GEMM-shaped passes, 4), or with sweep = 4 the
+  // team single-pass sweep (5) where a team plan exists (measured slower at C5)
+  auto wide = [&]() {
+    if (c->sweep_mode == 4 && !c->team_disabled &&
+        ppls_team_plan(r, c->ldx, c->ldy, c->dtype, c->num_cus, nrows, &c->tplan)) {
+      a->grid = c->tplan.nteams;
+      return 5;
+    }
     a->grid = ppls_panel_chunks(nrows, c->ldx, c->ldy, c->num_cus);
     return 4;
-  }
+  };
+  if (c->sweep_mode == 3 || c->sweep_mode == 4 || c->dtype) return wide();
   if (c->sweep_mode != 2 && nsplit > 0 && c->kernel_opt != 2) {
     a->ns = nsplit;
     a->pipe = c->pipe_opt;
@@ -336,12 +351,23 @@ int sweep_plan(ppls_ctx* c, int r, PplsSweepArgs* a) {
     a->grid = grid_of(c);
     return 1;
   }
-  if (c->sweep_mode != 2) {        // wide p / large r: panel sweep (two GEMM-shaped passes)
-    a->grid = ppls_panel_chunks(nrows, c->ldx, c->ldy, c->num_cus);
-    return 4;
-  }
+  if (c->sweep_mode != 2) return wide();   // wide p / large r
   a->grid = grid_of(c);
   return 2;
+}
+
+int ensure_team(ppls_ctx* c) {
+  int rc;
+  if (!c->team_status) {
+    if ((rc = dalloc(c, &c->team_status, 1))) return rc;
+    HIPCHK(c, hipMemset(c->team_status, 0, sizeof(int)));
+  }
+  if (c->tplan.xch_words > c->team_xch_words) {
+    if ((rc = dalloc(c, &c->team_xch, (size_t)c->tplan.xch_words))) return rc;
+    HIPCHK(c, hipMemset(c->team_xch, 0, sizeof(uint64_t) * (size_t)c->tplan.xch_words));
+    c->team_xch_words = c->tplan.xch_words;
+  }
+  return PPLS_OK;
 }
 
 // One sweep with theta[slot] -> c->stats (all-reduced).
@@ -399,6 +425,17 @@ int sweep(ppls_ctx* c, int r, int slot, bool write_mu) {
     if (plan == 3) HIPCHK(c, ppls_launch_sweep_split(&a, c->stream));
     else if (plan == 1) HIPCHK(c, ppls_launch_sweep_fused(&a, c->stream));
     else if (plan == 4) HIPCHK(c, ppls_launch_sweep_panel(&a, c->dtype, c->Z, a.grid, c->stream));
+    else if (plan == 5) {
+      if ((rc = ensure_team(c))) return rc;
+      const hipError_t e = ppls_launch_sweep_team(&c->tplan, &a, c->dtype, c->team_xch, ++c->team_epoch,
+                                                  nt ? 1 : 0, c->team_status, c->stream);
+      if (e != hipSuccess) {   // e.g. cooperative launch refused: the panel sweep from now on
+        (void)hipGetLastError();
+        c->team_disabled = true;
+        if (timed) HIPCHK(c, hipEventRecord(e1, c->stream));
+        return sweep(c, r, slot, write_mu);
+      }
+    }
     else HIPCHK(c, ppls_launch_sweep_twopass(&a, c->Z, c->stream));
     if (timed) HIPCHK(c, hipEventRecord(e1, c->stream));
     HIPCHK(c, ppls_launch_reduce2(c->part, groups, c->part_ld, c->part_ld, c->stats,
@@ -439,6 +476,14 @@ int finalize(ppls_ctx* c, int r, int cur, int nxt, int logl_index, int type) {
 }
 
 int check_status(ppls_ctx* c) {
+  if (c->team_status) {
+    int ts = 0;
+    HIPCHK(c, hipMemcpy(&ts, c->team_status, sizeof ts, hipMemcpyDeviceToHost));
+    if (ts != 0) {
+      HIPCHK(c, hipMemset(c->team_status, 0, sizeof(int)));
+      return fail(c, PPLS_E_HIP, "team sweep: a workgroup's exchange timed out (status %d)", ts);
+    }
+  }
   int st = 0;
   HIPCHK(c, hipMemcpy(&st, c->status, sizeof st, hipMemcpyDeviceToHost));
   if (st != 0) return fail(c, PPLS_E_NUMERIC, "rank-deficient X'mu_T or Y'mu_U in the M-step (status %d)", st);
@@ -606,6 +651,7 @@ void ppls_ctx_destroy(ppls_ctx* c) {
   if (c->ftrace) (void)hipFree(c->ftrace);
   for (auto& e : c->ev) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
   if (c->blas) (void)rocblas_destroy_handle(c->blas);
+  dfree(c->team_xch); dfree(c->team_status);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -615,7 +661,8 @@ const char* ppls_last_error(const ppls_ctx* c) { return c ? c->err.c_str() : "nu
 int ppls_set_option(ppls_ctx* c, const char* key, int64_t value) {
   if (!c || !key) return PPLS_E_ARG;
   if (!strcmp(key, "sweep")) {
-    if (value < 0 || value > 3) return fail(c, PPLS_E_ARG, "sweep must be 0 (auto), 1 (fused), 2 (two-pass) or 3 (panel)");
+    if (value < 0 || value > 4)
+      return fail(c, PPLS_E_ARG, "sweep must be 0 (auto), 1 (fused), 2 (two-pass), 3 (panel) or 4 (team)");
     c->sweep_mode = (int)value;
   } else if (!strcmp(key, "grid")) {
     if (value < 0 || value > 65535) return fail(c, PPLS_E_ARG, "grid out of range");
@@ -1834,7 +1881,7 @@ int ppls_sweep_info(ppls_ctx* c, int r, int64_t* bytes_per_sweep, int* variant, 
   PplsSweepArgs a;
   const int plan = sweep_plan(c, r, &a);
   if (bytes_per_sweep) *bytes_per_sweep = (int64_t)(c->dtype ? 4 : 8) * c->n_local * ((int64_t)c->p + c->q);
-  if (variant) *variant = plan == 4 ? 5 : plan == 3 ? 4 : plan == 1 ? (a.threads == 1024 ? 3 : 1) : 2;
+  if (variant) *variant = plan == 5 ? 6 : plan == 4 ? 5 : plan == 3 ? 4 : plan == 1 ? (a.threads == 1024 ? 3 : 1) : 2;
   if (grid) *grid = a.grid;
   return PPLS_OK;
 }

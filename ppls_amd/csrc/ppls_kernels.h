@@ -33,6 +33,14 @@ struct PplsSweepArgs {
   int ablate;            // timing experiments only (fused): 1 no compute, 2 no HBM copies
 };
 
+// Team single-pass sweep for wide data (ppls_team.hip): teams of S workgroups x (1 comm + wpw data
+// waves); nteams partial rows.
+struct PplsTeamPlan {
+  int S, wpw, nwx, nwy, grid, nteams;
+  double eff;            // lane x CU utilisation of the plan
+  int64_t xch_words;     // uint64 words of the exchange buffer
+};
+
 struct PplsFinalizeArgs {
   const double* stats;   // reduced [SX][SY][G]
   const double* ssq;     // {||X||^2, ||Y||^2}
@@ -93,6 +101,11 @@ hipError_t ppls_launch_generate(int64_t n_local, int64_t row0, int p, int q, int
                                 uint64_t seed, double* TU, double* X, double* Y, hipStream_t st);
 hipError_t ppls_launch_to_rowmajor(const double* src, int64_t n, int p, int ld, double* dst,
                                    hipStream_t st);
+// team sweep (ppls_team.hip)
+size_t ppls_team_lds_bytes(int r, int wpw, int S);
+int ppls_team_plan(int r, int ldx, int ldy, int f32, int num_cus, int64_t n, PplsTeamPlan* tp);
+hipError_t ppls_launch_sweep_team(const PplsTeamPlan* tp, const PplsSweepArgs* a, int f32, uint64_t* xch,
+                                  uint32_t epoch, int nt_loads, int* status, hipStream_t st);
 // variances.PPLS_simult (ppls_variances.hip)
 int ppls_gram_tiles(int p);
 int ppls_gram_occupancy(int f32);
