@@ -153,10 +153,13 @@ def main():
     truth, th0 = make_truth_and_theta0(p, q, r)
     ctx.generate_synthetic(n, p, q, truth, seed=20261015, row0=row0, n_local=n_local)
 
+    if torch.cuda.is_available():
+        torch.cuda.set_device(device)   # torch.cuda.synchronize() below then waits on this rank's GPU
+
     def barrier():
         ctx.synchronize()
         if torch.cuda.is_available():
-            torch.cuda.synchronize()
+            torch.cuda.synchronize(device)
         if dist is not None:
             dist.barrier()
 
