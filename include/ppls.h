@@ -147,6 +147,21 @@ typedef struct {
   int not_monotone;        /* out: bit k set if component k's logvalue decreased (warning, :177) */
 } ppls_seq_fit;
 int ppls_ppls(ppls_ctx* ctx, int a, int max_steps, double atol, const ppls_theta* init, ppls_seq_fit* out);
+/* PPLS / PPLSi with the reference's optional arguments: critfunc (crit_abs 0 = identity, 1 = abs)
+ * and constraints = list(fconstraint(...)) per component (Package/PPLS/R/EM_W_multi.R:85-92,
+ * :141-145, :165-169): each non-NULL pointer fixes that parameter (W: p, C: q, the rest: 1 value)
+ * at the start and after every EM step.  cons: a entries, or NULL (no constraints). */
+typedef struct {
+  const double* W;
+  const double* C;
+  const double* B;
+  const double* sigE;
+  const double* sigF;
+  const double* sigH;
+  const double* sigT;
+} ppls_constraint;
+int ppls_ppls_ex(ppls_ctx* ctx, int a, int max_steps, double atol, int crit_abs, const ppls_theta* init,
+                 const ppls_constraint* cons, ppls_seq_fit* out);
 int ppls_synchronize(ppls_ctx* ctx);
 
 /* ---- multi-population rank-1 fits: meta_EMstep / meta_PPLSi ----------------------------------

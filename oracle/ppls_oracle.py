@@ -15,7 +15,7 @@ Every function cites the reference line it restates (paths relative to /root/ref
                          or by ``ppls`` below with explicit per-component starting values)
 * ``emstepc_fast``       Package/PPLS/src/loglC.cpp:340-397 (one rank-1 EM step)
 * ``emstep_w``           Package/PPLS/R/EM_W_multi.R:51-73
-* ``pplsi``              Package/PPLS/R/EM_W_multi.R:116-180 (one direction; no constraints, critfunc = I)
+* ``pplsi``              Package/PPLS/R/EM_W_multi.R:116-180 (one direction; fconstraint :85-92)
 * ``ppls``               Package/PPLS/R/EM_W_multi.R:229-279 (sequential fit with deflation)
 * ``initial_guess``      Package/PPLS/R/EM_W_multi.R:126-140 ('equal'; 'random' with numpy draws)
 * ``scores_ppls``        Package/PPLS/R/EM_W_multi.R:411-420
@@ -366,6 +366,12 @@ def mu_coefficients(B, sigE, sigF, sigH, sigT):
 
 # ----------------------------------------------------------------------------- sequential init (PPLS)
 
+def _rsqrt(v):
+    """R's sqrt(): NaN (with a warning in R) for negative input."""
+    with np.errstate(invalid="ignore"):
+        return np.sqrt(np.asarray(v, dtype=np.float64))
+
+
 def emstepc_fast(W, C, B, X, Y, sigX, sigY, sigH, sigT, c1, c2, c3):
     """EMstepC_fast -- Package/PPLS/src/loglC.cpp:340-397 (W, C vectors; scalars)."""
     sig2X, sig2Y, sig2H, sig2T = sigX * sigX, sigY * sigY, sigH * sigH, sigT * sigT
@@ -393,8 +399,8 @@ def emstepc_fast(W, C, B, X, Y, sigX, sigY, sigH, sigT, c1, c2, c3):
     mh = -c2 * sig2H * Xw - (c3 - 1 / sig2Y) * sig2H * Yc
     Chh = sig2H - (-sig2H * sig2H * (c3 - 1 / sig2Y)) + mh @ mh / N               # :373
     return dict(mu_T=mu_T, mu_U=mu_U, W=Cxt / np.linalg.norm(Cxt), C=Cyu / np.linalg.norm(Cyu),
-                B=Cut / Ctt, sighat=np.array([math.sqrt(Cee), math.sqrt(Cff)]),
-                siglathat=np.array([math.sqrt(Chh), math.sqrt(Ctt)]),
+                B=Cut / Ctt, sighat=_rsqrt(np.array([Cee, Cff])),
+                siglathat=_rsqrt(np.array([Chh, Ctt])),
                 Cut=Cut, Ctt=Ctt, Cuu=Cuu, Cee=Cee, Cff=Cff, Chh=Chh)            # :377-396
 
 
@@ -433,13 +439,37 @@ def initial_guess(p, q, kind="equal", rng=None):
     raise ValueError(kind)
 
 
-def pplsi(X, Y, EMsteps=100, atol=1e-4, theta0=None):
-    """PPLSi -- Package/PPLS/R/EM_W_multi.R:116-180 with critfunc = identity and no constraints;
-    theta0 = initial_guess(...) (or a customGuess).  Returns the reference's list; NA fit -> W None."""
+def fconstraint(constraints=None):
+    """fconstraint -- Package/PPLS/R/EM_W_multi.R:85-92: the 7 named constraints, None = free."""
+    out = dict(W=None, C=None, B=None, sigE=None, sigF=None, sigH=None, sigT=None)
+    for k, v in (constraints or {}).items():
+        if k in out:
+            out[k] = v
+    return out
+
+
+def _constrain(cs, W, C, B, sigE, sigF, sigH, sigT):
+    """PPLSi's `with(constraints, if(is.numeric(.)) . else .)` -- EM_W_multi.R:141-145, :165-169."""
+    if cs is None:
+        return W, C, B, sigE, sigF, sigH, sigT
+    f = lambda key, cur: cur if cs.get(key) is None else cs[key]   # noqa: E731
+    W = np.ravel(np.asarray(f("W", W), dtype=np.float64))
+    C = np.ravel(np.asarray(f("C", C), dtype=np.float64))
+    return (W, C, float(np.ravel(f("B", B))[0]), float(np.ravel(f("sigE", sigE))[0]),
+            float(np.ravel(f("sigF", sigF))[0]), float(np.ravel(f("sigH", sigH))[0]),
+            float(np.ravel(f("sigT", sigT))[0]))
+
+
+def pplsi(X, Y, EMsteps=100, atol=1e-4, theta0=None, constraints=None, critfunc=None):
+    """PPLSi -- Package/PPLS/R/EM_W_multi.R:116-180; theta0 = initial_guess(...) (or a customGuess),
+    constraints = fconstraint(...)-style dict (None = free), critfunc None = identity.  Returns the
+    reference's list; NA fit -> W None."""
+    crit = critfunc if critfunc is not None else (lambda x: x)
     W = np.ravel(np.asarray(theta0["W"], dtype=np.float64))
     C = np.ravel(np.asarray(theta0["C"], dtype=np.float64))
     B, sigE, sigF = float(theta0["B"]), float(theta0["sigE"]), float(theta0["sigF"])
     sigH, sigT = float(theta0["sigH"]), float(theta0["sigT"])
+    W, C, B, sigE, sigF, sigH, sigT = _constrain(constraints, W, C, B, sigE, sigF, sigH, sigT)   # :141-145
 
     def ll(W, C, B, sigE, sigF, sigH, sigT):
         return logl_w(X, Y, W.reshape(-1, 1), C.reshape(-1, 1), np.array([[B]]), sigE, sigF, sigH,
@@ -454,17 +484,19 @@ def pplsi(X, Y, EMsteps=100, atol=1e-4, theta0=None):
         B, W, C = float(fit["B"]), fit["W"], fit["C"]
         sigE, sigF = fit["sighat"]
         sigH, sigT = fit["siglathat"]
+        W, C, B, sigE, sigF, sigH, sigT = _constrain(constraints, W, C, B, sigE, sigF, sigH, sigT)  # :165-169
         logvalue.append(ll(W, C, B, sigE, sigF, sigH, sigT))                         # :172
-        if logvalue[i] - logvalue[i - 1] < atol:                                    # :173
+        if crit(logvalue[i] - logvalue[i - 1]) < atol:                              # :173
             break
     last = logvalue[i] - logvalue[i - 1]                                            # :176
     return dict(W=W, C=C, B=B, sig=np.array([sigE, sigF, sigH, sigT]), logvalue=np.array(logvalue),
                 Last_increment=last, Number_steps=i, not_monotone=bool(np.any(np.diff(logvalue) < 0)))
 
 
-def ppls(X, Y, nr_comp=1, EMsteps=100, atol=1e-4, theta0s=None):
+def ppls(X, Y, nr_comp=1, EMsteps=100, atol=1e-4, theta0s=None, constraints=None, critfunc=None):
     """PPLS -- Package/PPLS/R/EM_W_multi.R:229-279: nr_comp PPLSi fits on successively deflated
-    X, Y (:270-271).  theta0s: one starting-value dict per component (initial_guess)."""
+    X, Y (:270-271).  theta0s: one starting-value dict per component (initial_guess); constraints:
+    one fconstraint dict per component (:230, :255) or None."""
     X = np.asarray(X, dtype=np.float64)
     Y = np.asarray(Y, dtype=np.float64)
     a = nr_comp
@@ -475,7 +507,8 @@ def ppls(X, Y, nr_comp=1, EMsteps=100, atol=1e-4, theta0s=None):
     Xc, Yc = X, Y
     done = 0
     for i in range(a):                                                              # :254
-        fit = pplsi(Xc, Yc, EMsteps, atol, theta0s[i])                              # :256-257
+        fit = pplsi(Xc, Yc, EMsteps, atol, theta0s[i], None if constraints is None else constraints[i],
+                    critfunc)                                                       # :256-257
         if fit["B"] is None:                                                        # :258-263
             break
         Wn[:, i], Cn[:, i], Bn[i], sig[i] = fit["W"], fit["C"], fit["B"], fit["sig"]

@@ -38,6 +38,11 @@ class PplsSeqFit(ct.Structure):
                 ("loglikelihoods", _dp), ("ncomp", ct.c_int), ("not_monotone", ct.c_int)]
 
 
+class PplsConstraint(ct.Structure):
+    _fields_ = [("W", _dp), ("C", _dp), ("B", _dp), ("sigE", _dp), ("sigF", _dp), ("sigH", _dp),
+                ("sigT", _dp)]
+
+
 class PplsMetaFit(ct.Structure):
     _fields_ = [("W", _dp), ("C", _dp), ("params", _dp), ("log", _dp), ("steps", ct.c_int)]
 
@@ -80,6 +85,8 @@ SIGNATURES = {
     "ppls_scores": (ct.c_int, [ct.c_void_p, _dp, _dp, ct.c_int, _dp, _dp]),
     "ppls_ppls": (ct.c_int, [ct.c_void_p, ct.c_int, ct.c_int, ct.c_double, ct.POINTER(PplsTheta),
                              ct.POINTER(PplsSeqFit)]),
+    "ppls_ppls_ex": (ct.c_int, [ct.c_void_p, ct.c_int, ct.c_int, ct.c_double, ct.c_int, ct.POINTER(PplsTheta),
+                                ct.POINTER(PplsConstraint), ct.POINTER(PplsSeqFit)]),
     "ppls_meta_emstep": (ct.c_int, [ct.c_void_p, ct.c_int, _i64p, _i64p, _dp, _dp, _dp, _dp, _dp, _dp,
                                     _dp, _dp]),
     "ppls_meta_ppls": (ct.c_int, [ct.c_void_p, ct.c_int, _i64p, _i64p, ct.c_int, ct.c_double, ct.c_int,

@@ -208,10 +208,11 @@ class Context:
         out.pull(o)
         return out, ll[: n.value].copy()
 
-    def ppls(self, a: int, max_steps: int, atol: float, inits):
+    def ppls(self, a: int, max_steps: int, atol: float, inits, constraints=None, crit_abs=False):
         """Sequential PPLS fit (EM_W_multi.R:229-279) from a list of ``a`` rank-1 starting values
-        (dicts W, C, B, sigE, sigF, sigH, sigT).  Returns the reference's list (W, C, B, sig,
-        Other_output) plus the per-component logvalue traces."""
+        (dicts W, C, B, sigE, sigF, sigH, sigT); ``constraints``: None or one fconstraint dict per
+        component (fixed values, EM_W_multi.R:85-92); ``crit_abs``: critfunc = abs.  Returns the
+        reference's list (W, C, B, sig, Other_output) plus the per-component logvalue traces."""
         p, q = self.p, self.q
         ths = [Theta(np.reshape(t["W"], (p, 1)), np.reshape(t["C"], (q, 1)), float(np.ravel(t["B"])[0]),
                      t["sigE"], t["sigF"], t["sigH"], float(np.ravel(t["sigT"])[0])) for t in inits]
@@ -228,7 +229,25 @@ class Context:
         lls = np.zeros(a)
         fit = _lib.PplsSeqFit(dptr(W), dptr(C), dptr(B), dptr(sig), dptr(lv), dptr(last),
                               nst.ctypes.data_as(ct.POINTER(ct.c_int)), dptr(lls), 0, 0)
-        self._chk(self._L.ppls_ppls(self.h, int(a), int(max_steps), float(atol), arr, ct.byref(fit)))
+        cons = None
+        keep = []
+        if constraints is not None:
+            if len(constraints) != a:
+                raise ValueError("There should be a list of constraints for each component, see ?PPLS.")
+            cons = (_lib.PplsConstraint * a)()
+            for k, cdict in enumerate(constraints):
+                for key, size in (("W", p), ("C", q), ("B", 1), ("sigE", 1), ("sigF", 1), ("sigH", 1), ("sigT", 1)):
+                    v = (cdict or {}).get(key)
+                    if v is None:
+                        continue
+                    arrv = np.ascontiguousarray(np.ravel(np.asarray(v, dtype=np.float64)))
+                    if arrv.shape[0] != size:
+                        raise ValueError(f"constraint {key} of component {k + 1} has {arrv.shape[0]} values, not {size}")
+                    keep.append(arrv)
+                    setattr(cons[k], key, dptr(arrv))
+        self._chk(self._L.ppls_ppls_ex(self.h, int(a), int(max_steps), float(atol), int(bool(crit_abs)), arr,
+                                       cons, ct.byref(fit)))
+        del keep
         k = fit.ncomp
         return dict(W=W[:, :k].copy(), C=C[:, :k].copy(), B=B[:k].copy(), sig=sig[:k].copy(),
                     Other_output=dict(Last_increment=last[:k].copy(), Number_steps=nst[:k].copy(),
@@ -482,11 +501,30 @@ def initial_guess(p, q, kind="equal", rng=None):
     raise ValueError(f"unknown initialGuess {kind!r}")
 
 
+def fconstraint(constraints=None):
+    """fconstraint (EM_W_multi.R:85-92): the seven named constraints W, C, B, sigE, sigF, sigH, sigT;
+    None = estimated, a number (or vector for W, C) = fixed."""
+    out = dict(W=None, C=None, B=None, sigE=None, sigF=None, sigH=None, sigT=None)
+    for k, v in (constraints or {}).items():
+        if k in out:
+            out[k] = v
+    return out
+
+
+def _crit_abs(critfunc):
+    if critfunc is None or getattr(critfunc, "__name__", "") == "identity":
+        return False
+    if critfunc in (abs, np.abs, np.fabs):
+        return True
+    raise NotImplementedError("critfunc must be the identity (default) or abs")
+
+
 def PPLS(X, Y, nr_comp=1, EMsteps=100, atol=1e-4, initialGuess=("equal", "o2m", "random", "custom"),
-         customGuess=None, rng=None, ctx=None):
+         customGuess=None, critfunc=None, constraints=None, rng=None, ctx=None):
     """PPLS (EM_W_multi.R:229-279) on the GPU: nr_comp sequential rank-1 EM fits on deflated data.
     Same return list (W, C, B, sig, Other_output); class "PPLS".  customGuess: one dict (used for
-    every component, as in R) or a list of per-component dicts."""
+    every component, as in R) or a list of per-component dicts; critfunc: identity (default) or abs;
+    constraints: None or a list of nr_comp fconstraint(...) dicts (:230, :255)."""
     ctx = _ctx_with(X, Y, ctx)
     kind = initialGuess if isinstance(initialGuess, str) else initialGuess[0]
     if customGuess is not None:
@@ -496,7 +534,9 @@ def PPLS(X, Y, nr_comp=1, EMsteps=100, atol=1e-4, initialGuess=("equal", "o2m", 
     else:
         rng = rng if rng is not None else np.random.default_rng()
         inits = [initial_guess(ctx.p, ctx.q, kind, rng) for _ in range(nr_comp)]
-    out = ctx.ppls(int(nr_comp), int(EMsteps), float(atol), inits)
+    if constraints is not None and len(constraints) != nr_comp:
+        raise ValueError("There should be a list of constraints for each component, see ?PPLS.")   # :240
+    out = ctx.ppls(int(nr_comp), int(EMsteps), float(atol), inits, constraints, _crit_abs(critfunc))
     if out["ncomp"] < nr_comp:
         warnings.warn(f"From component {out['ncomp'] + 1} on the residuals are of rank < 1e-14 and "
                       "calculations are stopped.")
@@ -509,10 +549,11 @@ def PPLS(X, Y, nr_comp=1, EMsteps=100, atol=1e-4, initialGuess=("equal", "o2m", 
 
 
 def PPLSi(X, Y, EMsteps=100, atol=1e-4, initialGuess=("equal", "o2m", "random", "custom"),
-          customGuess=None, rng=None, ctx=None):
+          customGuess=None, critfunc=None, constraints=None, rng=None, ctx=None):
     """PPLSi (EM_W_multi.R:116-180): one direction; returns W, C, B, sig, logvalue, Last_increment,
-    Number_steps (W = NA when sigE or sigF collapse, :152-154)."""
-    fit = PPLS(X, Y, 1, EMsteps, atol, initialGuess, customGuess, rng, ctx)
+    Number_steps (W = NA when sigE or sigF collapse, :152-154).  constraints: one fconstraint dict."""
+    fit = PPLS(X, Y, 1, EMsteps, atol, initialGuess, customGuess, critfunc,
+               None if constraints is None else [constraints], rng, ctx)
     if len(fit["B"]) == 0:
         return dict(W=None, C=None, B=None, sig=None, logvalue=None, Last_increment=None, Number_steps=None)
     oo = fit["Other_output"]

@@ -1225,6 +1225,11 @@ int deflated_ssq(ppls_ctx* c, const std::vector<double>& Wp, int m, bool isx, do
 extern "C" {
 
 int ppls_ppls(ppls_ctx* c, int a, int max_steps, double atol, const ppls_theta* init, ppls_seq_fit* out) {
+  return ppls_ppls_ex(c, a, max_steps, atol, 0, init, nullptr, out);
+}
+
+int ppls_ppls_ex(ppls_ctx* c, int a, int max_steps, double atol, int crit_abs, const ppls_theta* init,
+                 const ppls_constraint* cons, ppls_seq_fit* out) {
   if (!c) return PPLS_E_ARG;
   if (!c->have_data) return fail(c, PPLS_E_STATE, "no data");
   if (!init || !out || !out->W || !out->C || !out->B || !out->sig) return fail(c, PPLS_E_ARG, "NULL argument");
@@ -1244,6 +1249,7 @@ int ppls_ppls(ppls_ctx* c, int a, int max_steps, double atol, const ppls_theta* 
   std::vector<double> Wp, Cp;                            // w_1..w_k, c_1..c_k (column-major)
   std::vector<double> gA, gD, gB;                        // ||X w_j||^2, <X w_j, Y c_j>, ||Y c_j||^2
   std::vector<double> SX, SY;
+  bool fixed_wc = false;                                 // some component had W or C fixed
   const double tiny = 100.0 * 2.220446049250313e-16;     // 100 * .Machine$double.eps
   out->ncomp = 0;
   out->not_monotone = 0;
@@ -1258,6 +1264,21 @@ int ppls_ppls(ppls_ctx* c, int a, int max_steps, double atol, const ppls_theta* 
     t.sigE = init[k].sigE;
     t.sigF = init[k].sigF;
     t.sigH = init[k].sigH;
+    // PPLSi's constraints (fconstraint, :85-92): fixed values replace the estimates at the start
+    // (:141-145) and after every EM step (:165-169)
+    const ppls_constraint* ck = cons ? &cons[k] : nullptr;
+    auto constrain = [&](Rank1& u) {
+      if (!ck) return;
+      if (ck->W) u.w.assign(ck->W, ck->W + p);
+      if (ck->C) u.c.assign(ck->C, ck->C + q);
+      if (ck->B) u.B = ck->B[0];
+      if (ck->sigE) u.sigE = ck->sigE[0];
+      if (ck->sigF) u.sigF = ck->sigF[0];
+      if (ck->sigH) u.sigH = ck->sigH[0];
+      if (ck->sigT) u.sigT = ck->sigT[0];
+    };
+    if (ck && (ck->W || ck->C)) fixed_wc = true;
+    constrain(t);
     double G[4];
     if ((rc = rank1_sweep(c, t, Wp, Cp, k, SX, SY, G))) return rc;
     std::vector<double> lv(1, rank1_loglik(t, G, ssqX, ssqY, N, p, q));   // logvalue[1] (:149)
@@ -1265,10 +1286,12 @@ int ppls_ppls(ppls_ctx* c, int a, int max_steps, double atol, const ppls_theta* 
     bool na = false;
     for (i = 1; i <= max_steps; ++i) {                                    // :151
       if (t.sigE < tiny || t.sigF < tiny) { na = true; break; }           // :152-154
-      t = rank1_update(t, SX, SY, G, ssqX, ssqY, N, p, q, Wp, Cp, k);     // :156-170
+      t = rank1_update(t, SX, SY, G, ssqX, ssqY, N, p, q, Wp, Cp, k);     // :156-164
+      constrain(t);                                                       // :165-169
       if ((rc = rank1_sweep(c, t, Wp, Cp, k, SX, SY, G))) return rc;
       lv.push_back(rank1_loglik(t, G, ssqX, ssqY, N, p, q));              // :172
-      if (lv[i] - lv[i - 1] < atol) break;                                // :173
+      const double incr = lv[i] - lv[i - 1];
+      if ((crit_abs ? std::fabs(incr) : incr) < atol) break;              // critfunc(.) < atol (:173)
     }
     if (na) break;   // PPLS: "residuals are of rank < 1e-14", keep components 1..k-1 (:258-263)
     if (i > max_steps) i = max_steps;
@@ -1289,8 +1312,21 @@ int ppls_ppls(ppls_ctx* c, int a, int max_steps, double atol, const ppls_theta* 
     gA.push_back(G[0]);
     gD.push_back(G[1]);
     gB.push_back(G[3]);
-    ssqX -= G[0];
-    ssqY -= G[3];
+    // ||Xc (I - w w')||^2 = ||Xc||^2 - (2 - w'w) ||Xc w||^2 (w'w = 1 unless W is a fixed constraint)
+    if (ck && ck->W) {
+      double ww = 0.0;
+      for (int e = 0; e < p; ++e) ww += t.w[e] * t.w[e];
+      ssqX -= (2.0 - ww) * G[0];
+    } else {
+      ssqX -= G[0];
+    }
+    if (ck && ck->C) {
+      double cc = 0.0;
+      for (int e = 0; e < q; ++e) cc += t.c[e] * t.c[e];
+      ssqY -= (2.0 - cc) * G[3];
+    } else {
+      ssqY -= G[3];
+    }
     Wp.insert(Wp.end(), t.w.begin(), t.w.end());
     Cp.insert(Cp.end(), t.c.begin(), t.c.end());
     if (k + 1 < a && ssqX < 1e-6 * c->ssq_host[0])
@@ -1303,6 +1339,20 @@ int ppls_ppls(ppls_ctx* c, int a, int max_steps, double atol, const ppls_theta* 
     // because w_j is orthogonal to w_1..w_{j-1}, so the per-component Grams above suffice.
     if (out->loglikelihoods) {
       const int r = k + 1;
+      if (fixed_wc) {   // fixed W / C need not be orthogonal: X w_j from undeflated sweeps
+        for (int j = 0; j < r; ++j) {
+          Rank1 u = t;
+          u.w.assign(Wp.begin() + (size_t)j * p, Wp.begin() + (size_t)(j + 1) * p);
+          u.c.assign(Cp.begin() + (size_t)j * q, Cp.begin() + (size_t)(j + 1) * q);
+          double Gj[4];
+          std::vector<double> sx, sy;
+          static const std::vector<double> none;
+          if ((rc = rank1_sweep(c, u, none, none, 0, sx, sy, Gj))) return rc;
+          gA[j] = Gj[0];
+          gD[j] = Gj[1];
+          gB[j] = Gj[3];
+        }
+      }
       std::vector<double> Gf((size_t)4 * r * r, 0.0);
       PplsScalars s;
       memset(&s, 0, sizeof s);

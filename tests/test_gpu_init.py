@@ -170,3 +170,32 @@ def test_scores_fp32_storage(ctx):
     Y32 = Y.astype(np.float32).astype(np.float64)
     assert np.allclose(T, X32 @ th0["W"], rtol=1e-12, atol=1e-12)
     assert np.allclose(U, Y32 @ th0["C"], rtol=1e-12, atol=1e-12)
+
+
+def test_ppls_constraints_and_critfunc_match_oracle(ctx):
+    """PPLS / PPLSi with fconstraint (EM_W_multi.R:85-92, :141-145, :165-169) and critfunc = abs:
+    component 1 fixes B and sigT, component 2 fixes W (not orthogonal to w_1), so the deflation and the
+    Loglikelihoods take the non-orthogonal route; the rest is estimated."""
+    import ppls_amd
+    X, Y, _ = make_problem(260, 21, 17, 2, seed=57)
+    p, q = 21, 17
+    inits = [o.initial_guess(p, q, "equal") for _ in range(2)]
+    wfix = np.linspace(1.0, 2.0, p)
+    wfix /= np.linalg.norm(wfix)                         # a unit vector not orthogonal to w_1
+    cons = [ppls_amd.fconstraint(dict(B=0.8, sigT=1.3)), ppls_amd.fconstraint(dict(W=wfix))]
+    ctx.set_data(X, Y)
+    f = ppls_amd.PPLS(None, None, 2, 25, 1e-6, customGuess=inits, critfunc=abs, constraints=cons, ctx=ctx)
+    ref = o.ppls(X, Y, 2, 25, 1e-6, inits, constraints=cons, critfunc=abs)
+    oo, ro = f["Other_output"], ref["Other_output"]
+    assert list(oo["Number_steps"]) == list(ro["Number_steps"])
+    assert f["B"][0] == 0.8 and f["sig"][0, 3] == 1.3
+    assert np.array_equal(f["W"][:, 1], wfix)
+    assert np.abs(f["W"] - ref["W"]).max() < 1e-8 and np.abs(f["C"] - ref["C"]).max() < 1e-8
+    assert _relerr(f["sig"], ref["sig"]) < 1e-8
+    for k in range(2):
+        assert _relerr(oo["logvalue"][k], ro["logvalue"][k]) < 1e-10
+    assert _relerr(oo["Loglikelihoods"], ro["Loglikelihoods"]) < 1e-10
+    one = ppls_amd.PPLSi(None, None, 25, 1e-6, customGuess=inits[0], constraints=cons[0], ctx=ctx)
+    assert one["B"] == 0.8 and one["sig"][3] == 1.3
+    with pytest.raises(ValueError):
+        ppls_amd.PPLS(None, None, 2, 5, 1e-4, constraints=cons[:1], ctx=ctx)   # one list per component

@@ -211,3 +211,16 @@ def test_variances_restatement_equals_literal_nxn_form():
         V = v["varMatrix"][i]
         assert np.abs(V - V.T).max() < 1e-10 * np.abs(V).max()
         assert np.allclose(v["seLoad"][:, i] ** 2, np.diag(V), rtol=1e-12)
+
+
+def test_pplsi_constraints_hold_and_free_fit_is_unchanged():
+    # fconstraint (EM_W_multi.R:85-92): fixed values persist through every EM step (:165-169);
+    # no constraints (all NULL) is the plain PPLSi
+    X, Y, _ = make_problem(120, 9, 7, 1, seed=58)
+    init = o.initial_guess(9, 7, "equal")
+    free = o.pplsi(X, Y, 30, 1e-6, init)
+    same = o.pplsi(X, Y, 30, 1e-6, init, o.fconstraint())
+    assert np.array_equal(free["logvalue"], same["logvalue"])
+    cfix = np.ones(7) / np.sqrt(7.0)
+    fixed = o.pplsi(X, Y, 30, 1e-6, init, o.fconstraint(dict(sigH=0.25, C=cfix)))
+    assert fixed["sig"][2] == 0.25 and np.array_equal(fixed["C"], cfix)
