@@ -30,6 +30,7 @@ CONFIGS = {
 }
 METRIC = "EM iterations/sec + log-lik rel-err vs CPU ref, n=1e6 p=q=2000 r=5"
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+READ_CEILING_GBS = 6848.0   # measured read-only ceiling, profiles/r1_read_bw_probe.txt (tools/read_bw_probe.hip)
 FP64_PEAK_TF = 78.6     # MI355X fp64 vector (= fp64 MFMA) dense peak, TFLOP/s
 
 
@@ -195,7 +196,9 @@ def main():
                         traffic=load_traffic(wl), kernel=f"ppls_sweep ({info['variant']})",
                         avg_kernel_ms=avg_kernel_ms, bytes_per_launch=info["bytes_per_sweep"],
                         grid=info["grid"], fp64_valu_tflops=tflops, fp64_valu_peak_tflops=FP64_PEAK_TF,
-                        fp64_valu_frac=(tflops / FP64_PEAK_TF) if tflops else None)
+                        fp64_valu_frac=(tflops / FP64_PEAK_TF) if tflops else None,
+                        measured_read_ceiling=READ_CEILING_GBS,
+                        frac_of_measured_ceiling=(achieved / READ_CEILING_GBS) if achieved else None)
         out = dict(metric=METRIC, value=its, unit="EM iterations/s", n_gpus=world, steps=args.steps,
                    warmup=args.warmup, ms_per_step=1e3 * dt / args.steps, higher_is_better=True,
                    scaling="strong", vs_baseline=None, dtype="f64",
