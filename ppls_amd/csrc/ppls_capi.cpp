@@ -330,7 +330,8 @@ int sweep_plan(ppls_ctx* c, int r, PplsSweepArgs* a) {
       a->grid = c->tplan.nteams;
       return 5;
     }
-    a->grid = ppls_panel_chunks(nrows, c->ldx, c->ldy, c->num_cus);
+    a->grid = c->grid_opt > 0 ? c->grid_opt : ppls_panel_chunks(nrows, c->ldx, c->ldy, c->num_cus, c->dtype, r);
+    a->dots_grid = c->grid_opt;   // the grid option also sets the dots grid (tests: grid-stride path)
     return 4;
   };
   if (c->sweep_mode == 3 || c->sweep_mode == 4 || c->dtype) return wide();
@@ -681,7 +682,7 @@ int ppls_set_option(ppls_ctx* c, const char* key, int64_t value) {
   } else if (!strcmp(key, "pipe")) {
     c->pipe_opt = value ? 1 : 0;
   } else if (!strcmp(key, "ablate")) {
-    if (value < 0 || value > 255) return fail(c, PPLS_E_ARG, "ablate must be in [0,255]");
+    if (value < 0 || value > 1023) return fail(c, PPLS_E_ARG, "ablate must be in [0,1023]");
     c->ablate = (int)value;   // timing experiments only: results are wrong while set
   } else if (!strcmp(key, "ftrace")) {
     if (value && !c->ftrace) {

@@ -31,6 +31,7 @@ struct PplsSweepArgs {
   int* occ_out;          // split kernel: if set, report resident WGs per CU instead of launching
   int grid;              // workgroups (fused) / row chunks (two-pass)
   int ablate;            // timing experiments only (fused): 1 no compute, 2 no HBM copies
+  int dots_grid;         // panel dots workgroups (0 = one per 128-row group, capped)
 };
 
 // Team single-pass sweep for wide data (ppls_team.hip): teams of S workgroups x (1 comm + wpw data
@@ -75,7 +76,7 @@ hipError_t ppls_launch_sweep_twopass(const PplsSweepArgs* a, double* Z, hipStrea
 hipError_t ppls_launch_accumulate(const PplsSweepArgs* a, const double* Z, hipStream_t st);
 int ppls_twopass_groups(int64_t n_local, int grid);
 // Wide-p panel sweep (two GEMM-shaped passes); Z: n_local x 4r doubles; chunks = partial groups.
-int ppls_panel_chunks(int64_t n_local, int ldx, int ldy, int num_cus);
+int ppls_panel_chunks(int64_t n_local, int ldx, int ldy, int num_cus, int dtype_f32, int r);
 int64_t ppls_panel_z_len(int64_t n_local, int ldx, int ldy, int r);   // doubles of Z (+ transposed W, C)
 hipError_t ppls_launch_sweep_panel(const PplsSweepArgs* a, int dtype_f32, double* Z, int chunks, hipStream_t st);
 // dots pass only: Z = [Xw | Yc | mu_T | mu_U] and (if a->write_mu) mu (n x 2r column-major)

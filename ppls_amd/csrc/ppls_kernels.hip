@@ -1055,6 +1055,152 @@ __global__ __launch_bounds__(256) void ppls_panel_mfmadots_kernel(
   }
 }
 
+// MFMA dots fed by a workgroup-synchronous LDS-DMA ring (the panel dots default).  The register
+// form above keeps only one tile in flight per wave: its B operand is a per-lane global load issued
+// after the next tile's loads, and VMEM completion is in order, so waiting for B waits for the
+// prefetch too.  Here a stage holds the four waves' row tiles (32 rows x 128 B each) AND the tile's
+// slab of W^T (or C^T), all copied HBM/L2 -> LDS by global_load_lds_dwordx4, so one in-order vmcnt
+// wait covers both and PPLS_DOTS_STAGES - 1 stages stay in flight.  The waves of a workgroup walk
+// the same column tiles (one barrier per tile) and share the slab.  Row tiles are unpadded (128-B
+// rows) with the 16-B chunks swizzled (chunk c of row r at slot c ^ ((r >> 1) & 5)), which makes
+// each 16-lane group of the A-operand ds_read_b128 hit 16 distinct 4-bank groups; the swizzle is
+// applied on the global side, since the DMA writes lane l's 16 B at m0 + 16 l.
+#define PPLS_DOTS_STAGES 4
+
+template <typename T, int R>
+constexpr int ppls_dots_stage_bytes() {
+  return 4 * 32 * 128 + ((128 / (int)sizeof(T)) * R * 8 + 1023) / 1024 * 1024;
+}
+
+template <typename T, int R>
+__global__ __launch_bounds__(256) void ppls_panel_dmadots_kernel(
+    const T* __restrict__ X, const T* __restrict__ Y, int64_t n, int ldx, int ldy,
+    const double* __restrict__ Wt, const double* __restrict__ Ct, const PplsScalars* __restrict__ sc,
+    double* __restrict__ Z, double* __restrict__ mu) {
+  typedef double d4 __attribute__((ext_vector_type(4)));
+  constexpr int ES = (int)sizeof(T);
+  constexpr int CW = 16 / ES;          // columns per 16-B chunk
+  constexpr int KT = 128 / ES;         // columns per tile
+  constexpr int KQ = KT / 4;           // MFMA steps per tile
+  constexpr int RB = 32;               // rows per wave
+  constexpr int D = PPLS_DOTS_STAGES;
+  constexpr int TB = RB * 128;         // one wave's row tile
+  constexpr int SB = KT * R * 8;       // the tile's W^T slab
+  constexpr int NSB = (SB + 1023) / 1024;
+  constexpr int STAGE = ppls_dots_stage_bytes<T, R>();
+  constexpr int V4 = 4 * R;
+  static_assert(R <= 16 && NSB <= 4, "one 16-wide MFMA tile; slab copied by at most 4 waves");
+  __shared__ __attribute__((aligned(1024))) char lds[D * STAGE];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int i16 = lane & 15, kq = lane >> 4;
+  const int lr = lane >> 3, slot = lane & 7;
+  const int comp = i16 < R ? i16 : 0;
+  const double al = sc->alpha[comp], be = sc->beta[comp], ga = sc->gamma[comp], de = sc->delta[comp];
+  const int ntcx = (ldx + KT - 1) / KT, ntcy = (ldy + KT - 1) / KT, nsb = ntcx + ntcy;
+  const int64_t nblk = (n + RB - 1) / RB;
+  const int64_t ngrp = (nblk + 3) / 4;    // groups of four row blocks, one per wave
+  const int64_t K = (int64_t)blockIdx.x < ngrp ? (ngrp - blockIdx.x + gridDim.x - 1) / gridDim.x : 0;
+  const int64_t S = K * nsb;              // steps (tiles) of every wave of this workgroup
+  const int nst = 4 + (wave < NSB ? 1 : 0);   // DMA instructions per stage issued by this wave
+  const uint32_t lds0 = (uint32_t)(uintptr_t)lds;
+
+  // prefetch iterator: step -> (group k, tile j)
+  int64_t pk = 0;
+  int pj = 0;
+  auto issue = [&](int64_t step) {
+    const bool isy = pj >= ntcx;
+    const int tc = isy ? pj - ntcx : pj;
+    const T* M = isy ? Y : X;
+    const int ld = isy ? ldy : ldx;
+    const int64_t t = ((int64_t)blockIdx.x + pk * gridDim.x) * 4 + wave;
+    const uint32_t st = lds0 + (uint32_t)(step % D) * STAGE;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int rl = 8 * u + lr;
+      int64_t row = t * RB + rl;
+      if (row >= n) row = n - 1;
+      int c = tc * KT + (slot ^ ((rl >> 1) & 5)) * CW;
+      if (c >= ld) c = 0;
+      ppls_dma16(M + row * ld + c, __builtin_amdgcn_readfirstlane(st + wave * TB + u * 1024));
+    }
+    if (wave < NSB) {
+      const int off = wave * 1024 + 16 * lane;
+      const char* slab = (const char*)((isy ? Ct : Wt) + (int64_t)tc * KT * R);
+      ppls_dma16(slab + (off < SB ? off : 0), __builtin_amdgcn_readfirstlane(st + 4 * TB + wave * 1024));
+    }
+    if (++pj == nsb) { pj = 0; ++pk; }
+  };
+  for (int64_t s = 0; s < D - 1 && s < S; ++s) issue(s);
+
+  const int swz = (i16 >> 1) & 5;
+  int64_t step = 0;
+  for (int64_t k = 0; k < K; ++k) {
+    const int64_t row0 = (((int64_t)blockIdx.x + k * gridDim.x) * 4 + wave) * RB;
+    d4 res[2][2];
+#pragma unroll
+    for (int mat = 0; mat < 2; ++mat) {
+      d4 acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
+      const int ntc = mat ? ntcy : ntcx;
+      for (int tc = 0; tc < ntc; ++tc, ++step) {
+        // loads complete in order: once at most the later stages' copies are outstanding, this
+        // stage's have landed (Z stores in the count can only make the wait stricter)
+        const int64_t ahead = S - 1 - step;
+        ppls_wait_vmcnt(nst * (int)(ahead < D - 2 ? ahead : D - 2));
+        ppls_lds_barrier();   // every wave's copies of this stage have landed
+        if (step + D - 1 < S) issue(step + D - 1);   // into the stage everyone finished last step
+        const char* st = lds + (step % D) * STAGE;
+        const char* wt = st + wave * TB;
+        // A: rows i16, 16 + i16, columns [kq KQ, kq KQ + KQ) = chunks 2kq, 2kq+1
+        T a0[KQ], a1[KQ];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int sl = (2 * kq + h) ^ swz;
+          const float4 v0 = *(const float4*)(wt + i16 * 128 + sl * 16);
+          const float4 v1 = *(const float4*)(wt + (16 + i16) * 128 + sl * 16);
+          const T* p0 = (const T*)&v0;
+          const T* p1 = (const T*)&v1;
+#pragma unroll
+          for (int u = 0; u < CW; ++u) {
+            a0[h * CW + u] = p0[u];
+            a1[h * CW + u] = p1[u];
+          }
+        }
+        const double* wb = (const double*)(st + 4 * TB) + kq * KQ * R + comp;
+        double b[KQ];
+#pragma unroll
+        for (int s2 = 0; s2 < KQ; ++s2) b[s2] = i16 < R ? wb[s2 * R] : 0.0;
+#pragma unroll
+        for (int s2 = 0; s2 < KQ; ++s2) {
+          acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64((double)a0[s2], b[s2], acc0, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64((double)a1[s2], b[s2], acc1, 0, 0, 0);
+        }
+      }
+      res[mat][0] = acc0;
+      res[mat][1] = acc1;
+    }
+    if (i16 < R && row0 < n) {
+#pragma unroll
+      for (int blk = 0; blk < 2; ++blk)
+#pragma unroll
+        for (int reg = 0; reg < 4; ++reg) {
+          const int64_t row = row0 + 16 * blk + kq + 4 * reg;
+          if (row >= n) continue;
+          const double a = res[0][blk][reg], bb = res[1][blk][reg];
+          const double mt = al * a + be * bb, mu_u = ga * a + de * bb;
+          double* zr = Z + row * V4;
+          zr[i16] = a;
+          zr[R + i16] = bb;
+          zr[2 * R + i16] = mt;
+          zr[3 * R + i16] = mu_u;
+          if (mu) {
+            mu[(int64_t)i16 * n + row] = mt;
+            mu[(int64_t)(R + i16) * n + row] = mu_u;
+          }
+        }
+    }
+  }
+}
+
 // W (ldx x R, column-major) -> Wt (ldxp x R, row-major, rows >= ldx zero); same for C.
 __global__ void ppls_transpose_wc_kernel(const double* __restrict__ W, const double* __restrict__ C,
                                          int ldx, int ldy, int ldxp, int ldyp, int r, double* __restrict__ Wt,
@@ -1087,10 +1233,13 @@ __global__ __launch_bounds__(256) void ppls_panel_acc_kernel(
   const int64_t r0 = (int64_t)blockIdx.y * rows_per_chunk;
   const int64_t r1 = min(n, r0 + rows_per_chunk);
   double* pg = part + (int64_t)blockIdx.y * part_ld;
-  // mu (mu_T for X tiles, mu_U for Y tiles) of BR rows at a time in LDS: every lane reads the same
-  // address (broadcast), and the X loads of a batch are issued together
-  constexpr int BR = 64;
-  __shared__ double smu[BR * R];
+  // mu (mu_T for X tiles, mu_U for Y tiles) of BR rows at a time in LDS (every lane reads the same
+  // address: broadcast).  Software-pipelined: the next batch's mu is loaded into registers while the
+  // current batch is computed (LDS double-buffered, one barrier per batch), and the X rows stream in
+  // groups of 8 with the next group's loads in flight during the current group's FMAs.
+  constexpr int BR = 128;
+  constexpr int MPT = (BR * R + 255) / 256;
+  __shared__ double smu[2][BR * R];
   double acc[VEC][R];
 #pragma unroll
   for (int v = 0; v < VEC; ++v)
@@ -1098,39 +1247,62 @@ __global__ __launch_bounds__(256) void ppls_panel_acc_kernel(
     for (int k = 0; k < R; ++k) acc[v][k] = 0.0;
   const bool act = col < ld;
   const T* base = M + (act ? col : 0);
-  for (int64_t b0 = r0; b0 < r1; b0 += BR) {
-    const int nb = (int)(r1 - b0 < BR ? r1 - b0 : BR);
-    __syncthreads();
-    for (int e = tid; e < BR * R; e += 256) {
+  double mreg[MPT];
+  auto load_mu = [&](int64_t b0) {
+#pragma unroll
+    for (int u = 0; u < MPT; ++u) {
+      const int e = tid + 256 * u;
       const int rr = e / R, k = e - rr * R;
-      smu[e] = rr < nb ? Z[(b0 + rr) * V4 + off + k] : 0.0;
+      mreg[u] = (e < BR * R && b0 + rr < r1) ? Z[(b0 + rr) * V4 + off + k] : 0.0;
     }
-    __syncthreads();
+  };
+  auto store_mu = [&](int buf) {
+#pragma unroll
+    for (int u = 0; u < MPT; ++u) {
+      const int e = tid + 256 * u;
+      if (e < BR * R) smu[buf][e] = mreg[u];
+    }
+  };
+  const int64_t nbatch = (r1 - r0 + BR - 1) / BR;
+  if (nbatch > 0) {
+    load_mu(r0);
+    store_mu(0);
+  }
+  __syncthreads();
+  for (int64_t bt = 0; bt < nbatch; ++bt) {
+    const int64_t b0 = r0 + bt * BR;
+    const int nb = (int)(r1 - b0 < BR ? r1 - b0 : BR);
+    if (bt + 1 < nbatch) load_mu(b0 + BR);
+    const double* sm = smu[bt & 1];
     if (act) {
-      int rr = 0;
-      for (; rr + 8 <= nb; rr += 8) {
-        PplsVec16<T> xv[8];
+      PplsVec16<T> xa[8], xb[8];
+      auto load8 = [&](int rr, PplsVec16<T> (&xv)[8]) {
 #pragma unroll
-        for (int u = 0; u < 8; ++u) xv[u] = ppls_load16(base + (b0 + rr + u) * ld);
+        for (int u = 0; u < 8; ++u) xv[u] = ppls_load16(base + (b0 + min(rr + u, nb - 1)) * ld);
+      };
+      auto fma8 = [&](int rr, const PplsVec16<T> (&xv)[8]) {
 #pragma unroll
-        for (int u = 0; u < 8; ++u)
+        for (int u = 0; u < 8; ++u) {
+          if (rr + u >= nb) break;
 #pragma unroll
           for (int k = 0; k < R; ++k) {
-            const double m = smu[(rr + u) * R + k];
+            const double m = sm[(rr + u) * R + k];
 #pragma unroll
             for (int v = 0; v < VEC; ++v) acc[v][k] = fma((double)xv[u].v[v], m, acc[v][k]);
           }
-      }
-      for (; rr < nb; ++rr) {
-        const PplsVec16<T> xv = ppls_load16(base + (b0 + rr) * ld);
-#pragma unroll
-        for (int k = 0; k < R; ++k) {
-          const double m = smu[rr * R + k];
-#pragma unroll
-          for (int v = 0; v < VEC; ++v) acc[v][k] = fma((double)xv.v[v], m, acc[v][k]);
         }
+      };
+      load8(0, xa);
+      for (int rr = 0; rr < nb; rr += 16) {
+        if (rr + 8 < nb) load8(rr + 8, xb);
+        fma8(rr, xa);
+        if (rr + 8 >= nb) break;
+        if (rr + 16 < nb) load8(rr + 16, xa);
+        fma8(rr + 8, xb);
       }
     }
+    if (bt + 1 < nbatch) store_mu((bt + 1) & 1);
+    __syncthreads();
   }
   if (act) {
     double* dst = isx ? pg : pg + (int64_t)R * ldx;
@@ -2407,7 +2579,13 @@ hipError_t launch_panel_t(const PplsSweepArgs* a, const T* X, const T* Y, double
   // measured at the C5 shape (tools/panel_experiment.py): tiled dots is faster for fp64 storage
   // (8.6 vs 13.1 ms), row-per-lane dots for fp32 storage (6.7 vs 7.5 ms); ablate bit 5 flips it
   const int dots = (a->ablate >> 5) & 1;   // 0 MFMA (default), 1 tiled VALU (experiments)
-  if (dots == 0) {
+  if (dots == 0 && (a->ablate & 512)) {   // LDS-DMA ring dots (opt-in until measured)
+    const int64_t ngrp = ((a->n_local + 31) / 32 + 3) / 4;
+    int64_t g = a->dots_grid > 0 ? a->dots_grid : (ngrp < 16384 ? ngrp : 16384);
+    if (g > ngrp) g = ngrp;
+    hipLaunchKernelGGL((ppls_panel_dmadots_kernel<T, R>), dim3((unsigned)g), dim3(256), 0, st, X, Y,
+                       a->n_local, a->ldx, a->ldy, Wt, Ct, a->sc, Z, a->write_mu ? a->mu : nullptr);
+  } else if (dots == 0) {   // register-staged MFMA dots (ablate bit 9, experiments)
     const int64_t wtiles = (a->n_local + 31) / 32;
     const int mblocks = (int)((wtiles + 3) / 4 < 16384 ? (wtiles + 3) / 4 : 16384);
     hipLaunchKernelGGL((ppls_panel_mfmadots_kernel<T, R>), dim3(mblocks), dim3(256), 0, st, X, Y,
@@ -2456,6 +2634,38 @@ hipError_t launch_panel_dt(const PplsSweepArgs* a, const T* X, const T* Y, doubl
     default: return hipErrorInvalidValue;
   }
 }
+
+template <typename T, int R>
+hipError_t acc_occ_t(int* occ) {
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, (const void*)ppls_panel_acc_kernel<T, R>, 256, 0);
+}
+
+template <typename T>
+hipError_t acc_occ_dt(int r, int* occ) {
+  switch (r) {
+    case 1: return acc_occ_t<T, 1>(occ);
+    case 2: return acc_occ_t<T, 2>(occ);
+    case 3: return acc_occ_t<T, 3>(occ);
+    case 4: return acc_occ_t<T, 4>(occ);
+    case 5: return acc_occ_t<T, 5>(occ);
+    case 6: return acc_occ_t<T, 6>(occ);
+    case 7: return acc_occ_t<T, 7>(occ);
+    case 8: return acc_occ_t<T, 8>(occ);
+    case 9: return acc_occ_t<T, 9>(occ);
+    case 10: return acc_occ_t<T, 10>(occ);
+    case 11: return acc_occ_t<T, 11>(occ);
+    case 12: return acc_occ_t<T, 12>(occ);
+    case 13: return acc_occ_t<T, 13>(occ);
+    case 14: return acc_occ_t<T, 14>(occ);
+    case 15: return acc_occ_t<T, 15>(occ);
+    case 16: return acc_occ_t<T, 16>(occ);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+hipError_t panel_acc_occupancy(int dtype_f32, int r, int* occ) {
+  return dtype_f32 ? acc_occ_dt<float>(r, occ) : acc_occ_dt<double>(r, occ);
+}
 }  // namespace
 extern "C" {
 
@@ -2463,14 +2673,22 @@ int64_t ppls_panel_z_len(int64_t n_local, int ldx, int ldy, int r) {
   return (n_local > 0 ? n_local : 1) * 4 * r + (int64_t)(((ldx + 31) & ~31) + ((ldy + 31) & ~31)) * r;
 }
 
-int ppls_panel_chunks(int64_t n_local, int ldx, int ldy, int num_cus) {
-  // enough workgroups for memory-level parallelism (>= 16 per CU) as column tiles x row chunks
-  const int tiles = (ldx + 511) / 512 + (ldy + 511) / 512;
-  int64_t ch = (16LL * num_cus + tiles - 1) / tiles;
+int ppls_panel_chunks(int64_t n_local, int ldx, int ldy, int num_cus, int dtype_f32, int r) {
+  // The accumulation grid is column tiles x row chunks, sized in rounds of the resident slots (CUs x
+  // workgroups per CU at the kernel's register use).
+  const int vec = dtype_f32 ? 4 : 2;
+  const int tiles = (ldx + 256 * vec - 1) / (256 * vec) + (ldy + 256 * vec - 1) / (256 * vec);
+  int occ = 0;
+  if (panel_acc_occupancy(dtype_f32, r, &occ) != hipSuccess || occ < 1) occ = 1;
+  const int64_t slots = (int64_t)num_cus * occ;
   const int64_t maxch = (n_local + 255) / 256;   // at least 256 rows per chunk
+  // about 8 rounds: measured at C5 fp32 (tools/chunk_sweep.py) 93 chunks (2 rounds) 9.08 ms,
+  // 196 8.70, 300 8.65, 450 8.57, 700 8.58, 1024 8.60 -- more rounds shorten the tail, while the
+  // partials the reduction reads grow with the chunk count
+  int64_t ch = (8 * slots + tiles - 1) / tiles;
   if (ch > maxch) ch = maxch;
-  if (ch < 1) ch = 1;
   if (ch > 1024) ch = 1024;
+  if (ch < 1) ch = 1;
   return (int)ch;
 }
 

@@ -1,6 +1,6 @@
 """Timing experiments on the wide-data sweeps (team single pass vs panel two passes).
 
-    python tools/team_ablation.py [c5|c5d]
+    python tools/team_ablation.py [c5|c5d] [r] [--quick]
 
 Team ablate bits (timing only; results garbage while set): 32 = no team exchange, 64 = no dots /
 update arithmetic, 128 = no HBM -> LDS copies.
@@ -27,10 +27,11 @@ def time_sweep(ctx, steps=6):
 
 
 def main():
-    cfgname = sys.argv[1] if len(sys.argv) > 1 else "c5"
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    cfgname = args[0] if args else "c5"
     cfg = dict(CONFIGS[cfgname])
-    if len(sys.argv) > 2:                      # optional r override
-        cfg["r"] = int(sys.argv[2])
+    if len(args) > 1:                          # optional r override
+        cfg["r"] = int(args[1])
         cfgname += f"_r{cfg['r']}"
     n, p, q, r = cfg["n"], cfg["p"], cfg["q"], cfg["r"]
     ctx = Context(0)
