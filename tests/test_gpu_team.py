@@ -73,12 +73,14 @@ def test_team_repeatable_and_small_n_falls_back():
 
 
 def test_team_initialiser_and_meta():
-    """The r = 1 paths (sequential PPLS, meta_* row segments) run the team sweep on wide data."""
+    """The r = 1 paths (sequential PPLS, meta_* row segments) run the team sweep (sweep = 4, opt-in)
+    on wide data."""
     import ppls_amd
     from ppls_amd import Context
     X, Y, _ = make_problem(4000, 2700, 140, 1, seed=83)
     init = o.initial_guess(2700, 140, "equal")
     with Context(0) as c:
+        c.set_option("sweep", 4)
         c.set_data(X, Y)
         assert c.sweep_info(1)["variant"] == "team"
         f = c.ppls(1, 10, 1e-6, [init])
