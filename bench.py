@@ -66,40 +66,58 @@ def load_traffic(workload_key):
         return None
 
 
-def cpu_baseline(ctx, th0, cfg, seconds_target=15.0):
-    """Time the C restatement of the reference path (oracle/cpu_ref.c, OpenMP) on the host cores on
-    a bounded sample of the same rows; compare its log-likelihood trace with the GPU's on the
-    identical sample."""
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(ctx, th0, cfg, iters=3, one_core_rows=100_000):
+    """Time the C restatement of the reference path (oracle/cpu_ref.c: its pass structure, OpenMP
+    over rows) on the host cores, on the SAME rows the GPU holds (full n, >= 3 steady-
+    state iterations after one untimed iteration, all cores; plus 1 core on a row sample, scaled
+    linearly in n), and compare the CPU's log-likelihood trace and loadings with the GPU's first
+    iterations from the same theta0."""
     from oracle import cpu_ref
-    from ppls_amd import Context
+    from oracle.ppls_oracle import canonicalize
     th = th0.as_dict()
     cores = cpu_ref.load().cpu_ref_max_threads()
-    n_s = int(min(ctx.n_local, 150_000))
-    X, Y = ctx.get_data(0, n_s)
-    Xs, Ys = np.ascontiguousarray(X), np.ascontiguousarray(Y)
-    del X, Y
-    # calibrate on the sample itself (a small probe fits in cache and overstates the rate);
-    # this untimed pass also faults the pages in and spins up the OpenMP pool
+    X, Y = ctx.get_data_rows()             # all rows, row-major (what cpu_ref streams)
     t0 = time.perf_counter()
-    cpu_ref.em_steps(Xs, Ys, th, 1)
-    per_iter = time.perf_counter() - t0
-    steps = int(min(200, max(2, round(seconds_target / per_iter))))
+    th1, ll1 = cpu_ref.em_steps(X, Y, th, 1)        # untimed: faults the pages in, spins up OpenMP
+    t_first = time.perf_counter() - t0
     t0 = time.perf_counter()
-    th_cpu, ll_cpu = cpu_ref.em_steps(Xs, Ys, th, steps)
+    th_cpu, ll_cpu = cpu_ref.em_steps(X, Y, th1, iters)
     dt = time.perf_counter() - t0
-    row_iters_per_s = n_s * steps / dt
-    # GPU on the identical sample, same theta0, same number of iterations
-    with Context(ctx_device(ctx)) as c2:
-        c2.set_data(Xs, Ys)
-        est, ll_gpu, _, _ = c2.em_run(th0, steps, -np.inf, 0, want_eout=False)
-    rel = float(np.abs(ll_gpu - ll_cpu).max() / np.abs(ll_cpu).max())
-    from oracle.ppls_oracle import canonicalize   # the GPU estimates are canonicalised (:794-799)
-    Wc, _, _, _ = canonicalize(th_cpu["W"], th_cpu["C"], th_cpu["B"], th_cpu["sigT"])
-    werr = float(np.abs(est.W - Wc).max())
-    return dict(value=row_iters_per_s / cfg["n"], unit="EM iterations/s", cores=int(cores), kind="port",
-                sample=f"{steps} EM iterations on the first {n_s} of n={cfg['n']} rows in {dt:.1f} s "
-                       f"(oracle/cpu_ref.c, reference pass structure, OpenMP {cores} threads, -O3 "
-                       f"-march=native); value = rows*iterations/s / n"), rel, werr
+    ll_all = np.concatenate([ll1, ll_cpu])
+    # 1 core on the first rows (bounded time), per-row rate scaled to the full n
+    ns = int(min(one_core_rows, X.shape[0]))
+    Xs, Ys = X[:ns], Y[:ns]
+    cpu_ref.em_steps(Xs, Ys, th, 1, nthreads=1)
+    t0 = time.perf_counter()
+    cpu_ref.em_steps(Xs, Ys, th, iters, nthreads=1)
+    dt1 = time.perf_counter() - t0
+    cpu_ref.load().cpu_ref_em_step   # noqa: B018 (keep the library loaded)
+    del X, Y, Xs, Ys
+    # GPU on the same resident rows, same theta0, iters + 1 iterations
+    est, ll_gpu, _, _ = ctx.em_run(th0, iters + 1, -np.inf, 0, want_eout=False)
+    rel = float(np.abs(ll_gpu - ll_all).max() / np.abs(ll_all).max())
+    Wc, Cc, _, _ = canonicalize(th_cpu["W"], th_cpu["C"], th_cpu["B"], th_cpu["sigT"])
+    werr = float(max(np.abs(est.W - Wc).max(), np.abs(est.C - Cc).max()))
+    n = cfg["n"]
+    one_core = iters * ns / dt1 / n
+    return dict(value=iters / dt, unit="EM iterations/s", cores=int(cores), kind="port",
+                sample=f"{iters} steady-state EM iterations (after 1 untimed, {t_first:.1f} s) on all n={n} rows "
+                       f"in {dt:.1f} s: oracle/cpu_ref.c (reference pass structure), OpenMP {cores} threads, "
+                       f"-O3 -march=native, {cpu_model()}",
+                one_core=dict(value=one_core, unit="EM iterations/s", cores=1,
+                              sample=f"{iters} EM iterations on the first {ns} rows in {dt1:.1f} s, 1 thread; "
+                                     f"value = rows*iterations/s / n")), rel, werr
 
 
 _DEVICE = {}
@@ -109,16 +127,50 @@ def ctx_device(ctx):
     return _DEVICE.get(id(ctx), 0)
 
 
+def _rank_entry(rank, world, port, argv):
+    """Child rank of spawn_ranks: the launcher's environment, then main() (before any GPU call)."""
+    os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world), LOCAL_WORLD_SIZE=str(world),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    sys.argv = argv
+    main()
+
+
+def spawn_ranks(n):
+    """`bench.py --gpus N` without torchrun: N fresh rank processes (multiprocessing spawn), one per
+    GPU, started before this process touches a GPU; returns the exit status (non-zero if any rank
+    failed or fewer than N GPUs are visible)."""
+    import multiprocessing as mp
+    import socket
+    import torch
+    ndev = torch.cuda.device_count()   # does not initialise the GPU on this image
+    if ndev < n:
+        print(f"error: --gpus {n} but only {ndev} GPU(s) visible", file=sys.stderr)
+        return 2
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    procs = [ctx.Process(target=_rank_entry, args=(r, n, port, list(sys.argv))) for r in range(n)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join()
+    bad = [r for r, p in enumerate(procs) if p.exitcode != 0]
+    if bad:
+        print(f"error: rank(s) {bad} failed", file=sys.stderr)
+        return 1
+    return 0
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
-    ap.add_argument("--sweep", type=int, default=0, help="0 auto, 1 fused, 2 two-pass, 3 panel")
-    ap.add_argument("--threads", type=int, default=0, help="fused workgroup size: 0 auto, 512, 1024")
+    ap.add_argument("--sweep", type=int, default=0, help="0 auto, 2 two-pass, 3 panel")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--cpu-iters", type=int, default=3, help="timed CPU-baseline iterations (full n)")
     ap.add_argument("--timing-every", type=int, default=4,
                     help="bracket every N-th sweep of the timed region with HIP events")
     args = ap.parse_args()
@@ -126,8 +178,11 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and world > 1:
-        print(f"warning: WORLD_SIZE={world} != --gpus {args.gpus}", file=sys.stderr)
+    if world == 1 and args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))   # no launcher: one child process per GPU (spawn, no exec)
+    if world != args.gpus:
+        print(f"error: {world} rank(s) (WORLD_SIZE) but --gpus {args.gpus}", file=sys.stderr)
+        sys.exit(2)
     dist = None
     if world > 1:
         import torch.distributed as dist  # gloo: barriers, max-over-ranks, RCCL id exchange
@@ -145,7 +200,6 @@ def main():
     if cfg.get("storage") == "f32":
         ctx.set_option("dtype", 1)
     ctx.set_option("sweep", args.sweep)
-    ctx.set_option("threads", args.threads)
     if world > 1:
         uid = [Context.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
@@ -193,7 +247,7 @@ def main():
         tflops = flops / (avg_kernel_ms * 1e-3) / 1e12 if launches else None
         roofline = dict(bound="hbm", achieved=achieved, peak=HBM_PEAK_GBS, unit="GB/s",
                         frac=(achieved / HBM_PEAK_GBS) if achieved else None,
-                        traffic=load_traffic(wl), kernel=f"ppls_sweep ({info['variant']})",
+                        traffic=load_traffic(wl), kernel=ctx.sweep_kernel(r),
                         avg_kernel_ms=avg_kernel_ms, bytes_per_launch=info["bytes_per_sweep"],
                         grid=info["grid"], fp64_valu_tflops=tflops, fp64_valu_peak_tflops=FP64_PEAK_TF,
                         fp64_valu_frac=(tflops / FP64_PEAK_TF) if tflops else None,
@@ -209,7 +263,7 @@ def main():
                    roofline=roofline,
                    loglik_last=float(ll[-1]) if len(ll) else None)
         if world == 1 and not args.no_cpu:
-            cb, rel, werr = cpu_baseline(ctx, th0, cfg, args.cpu_seconds)
+            cb, rel, werr = cpu_baseline(ctx, th0, cfg, args.cpu_iters)
             out["cpu_baseline"] = cb
             out["loglik_rel_err_vs_cpu"] = rel
             out["W_abs_err_vs_cpu"] = werr

@@ -75,8 +75,9 @@ const char* ppls_strerror(int code);
 int ppls_ctx_create(int device, ppls_ctx** out);
 void ppls_ctx_destroy(ppls_ctx* ctx);
 const char* ppls_last_error(const ppls_ctx* ctx);
-/* keys: "sweep" (0 auto, 1 fused single-pass, 2 generic two-pass, 3 panel (wide p, two passes),
- *                4 team (wide p, single pass; falls back to panel where no team plan exists)),
+/* keys: "sweep" (0 auto: the single-pass split sweep where W, C and the X'mu accumulators fit in
+ *                registers, else the panel sweep; 2 generic two-pass; 3 panel (wide p, two passes)),
+ *       "rows_per_step" (split sweep: 0 auto, 1, 2), "pipe" (split sweep software pipelining, 0/1),
  *       "grid" (workgroups, 0 = auto),
  *       "dtype" (storage of X, Y: 0 fp64, 1 fp32; arithmetic stays fp64; set before loading data),
  *       "nt" (sweep loads with the non-temporal cache policy: -1 auto (default: when X, Y exceed
@@ -88,6 +89,14 @@ int ppls_set_option(ppls_ctx* ctx, const char* key, int64_t value);
 void ppls_shard_range(int64_t n_total, int nranks, int rank, int64_t* row0, int64_t* n_local);
 int ppls_comm_unique_id(char id[128]);
 int ppls_comm_init(ppls_ctx* ctx, int nranks, int rank, const char id[128]);
+/* Host-side reduction in place of RCCL (MPI, gloo, a test harness, k contexts on one GPU, ...):
+ * fn(user, buf, count) must replace buf[0..count) by its element-wise sum over all ranks and return
+ * 0 (non-zero -> PPLS_E_COMM).  Every collective of the library (per-iteration sufficient statistics,
+ * ||X||^2 and ||Y||^2, population and deflation sums, variances) then runs device -> host -> fn ->
+ * device, synchronously, in the same order on every rank.  fn = NULL restores RCCL (or no
+ * reduction).  Collective when data is resident (||X||^2, ||Y||^2 are re-reduced). */
+typedef int (*ppls_reduce_fn)(void* user, double* buf, int64_t count);
+int ppls_set_reducer(ppls_ctx* ctx, ppls_reduce_fn fn, void* user);
 
 /* ---- data (X: n_local x p, Y: n_local x q; this rank's rows of an n_total-sample problem) ---- */
 int ppls_set_data(ppls_ctx* ctx, const double* X, const double* Y, int64_t n_local, int p, int q,
@@ -98,6 +107,9 @@ int ppls_set_data(ppls_ctx* ctx, const double* X, const double* Y, int64_t n_loc
 int ppls_generate_synthetic(ppls_ctx* ctx, int64_t n_total, int64_t row0, int64_t n_local, int p,
                             int q, int r, const ppls_theta* truth, uint64_t seed);
 int ppls_get_data(ppls_ctx* ctx, double* X, double* Y, int64_t row_begin, int64_t nrows);
+/* The same rows in row-major layout (X: nrows x p, Y: nrows x q, C order), streamed without a
+ * device-side transpose: what a row-oriented host consumer (the CPU baseline) reads. */
+int ppls_get_data_rows(ppls_ctx* ctx, double* X, double* Y, int64_t row_begin, int64_t nrows);
 int ppls_data_ssq(ppls_ctx* ctx, double* ssqX, double* ssqY);   /* global (all ranks) */
 
 /* ---- the hot path ------------------------------------------------------------------------ */
@@ -217,6 +229,9 @@ int ppls_gram(ppls_ctx* ctx, int xory, int nsplit, double* G, double* ms);
 int ppls_sweep_timing(ppls_ctx* ctx, double* total_ms, int64_t* launches, int reset);
 /* Shape facts for the roofline: bytes of X and Y one sweep reads (algorithmic), kernel variant. */
 int ppls_sweep_info(ppls_ctx* ctx, int r, int64_t* bytes_per_sweep, int* variant, int* grid);
+/* The sweep kernel instantiation the next EM iteration with r components launches, as text
+ * (e.g. "split<5,4,512,2,false,4,4> nt"): tests assert the production kernel is the one checked. */
+int ppls_sweep_kernel(ppls_ctx* ctx, int r, char* buf, int len);
 
 /* Diagnostics: wall-clock stamps of the last finalize's phases (PPLS_FTRACE_LEN = 3 blocks x 16
  * slots; 0 = slot not reached) and the tick length in ns.  Requires set_option("ftrace", 1). */

@@ -11,8 +11,8 @@
  * with the coefficient block of EM_W_multi.R:670-686 / :312-320, Chh :711-712, the M-step scalars
  * :734-738 and orth(type="SVD") = U V' by Householder QR + one-sided Jacobi (OmicsPLS::orth,
  * semantics Package/functions.R:252-260).  Row-major X (n x p), Y (n x q); W, C column-major.
- * OpenMP over rows; per-thread partial sums reduced in thread order (deterministic for a fixed
- * thread count).
+ * OpenMP over rows (static schedule); every thread accumulates its own partial sums, which are
+ * then added in thread-index order: the result is deterministic for a fixed thread count.
  */
 #include <math.h>
 #include <stdint.h>
@@ -23,6 +23,21 @@
 #endif
 
 #define RM 16
+
+#ifdef _OPENMP
+static int max_threads(void) { return omp_get_max_threads(); }
+static int thread_id(void) { return omp_get_thread_num(); }
+#else
+static int max_threads(void) { return 1; }
+static int thread_id(void) { return 0; }
+#endif
+
+/* part[T][len] -> out[len]: the per-thread partials summed in thread-index order */
+static void sum_ordered(const double* part, int T, int len, double* out) {
+  for (int j = 0; j < len; ++j) out[j] = 0.0;
+  for (int t = 0; t < T; ++t)
+    for (int j = 0; j < len; ++j) out[j] += part[(size_t)t * len + j];
+}
 
 static void coef_estep(double t, double b, double sE, double sF, double sH, double* c1, double* c2,
                        double* c3, double* Kc_out, int logl_variant) {
@@ -133,24 +148,37 @@ static double loglc(const double* X, const double* Y, int64_t n, int p, int q, i
   double a1 = 0, a2 = 0;
   for (int k = 0; k < r; ++k) { a1 += log(sX2 + t[k] * t[k]); a2 += log(sY2 + Kc[k]); }
   const double logdet = a1 + (p - r) * log(sX2) + a2 + (q - r) * log(sY2);
-  double ssx = 0, ssy = 0, quad = 0;
-#pragma omp parallel for reduction(+ : ssx, ssy, quad) schedule(static)
-  for (int64_t i = 0; i < n; ++i) {
-    const double* x = X + i * p;
-    const double* y = Y + i * q;
-    double xw[RM] = {0}, yc[RM] = {0}, sx = 0, sy = 0;
-    for (int j = 0; j < p; ++j) {
-      sx += x[j] * x[j];
-      for (int k = 0; k < r; ++k) xw[k] += x[j] * W[k * p + j];
+  const int T = max_threads();
+  double* part = (double*)calloc((size_t)T * 3, sizeof(double));
+#pragma omp parallel num_threads(T)
+  {
+    double ssx = 0, ssy = 0, quad = 0;
+#pragma omp for schedule(static)
+    for (int64_t i = 0; i < n; ++i) {
+      const double* x = X + i * p;
+      const double* y = Y + i * q;
+      double xw[RM] = {0}, yc[RM] = {0}, sx = 0, sy = 0;
+      for (int j = 0; j < p; ++j) {
+        sx += x[j] * x[j];
+        for (int k = 0; k < r; ++k) xw[k] += x[j] * W[k * p + j];
+      }
+      for (int j = 0; j < q; ++j) {
+        sy += y[j] * y[j];
+        for (int k = 0; k < r; ++k) yc[k] += y[j] * C[k * q + j];
+      }
+      ssx += sx;
+      ssy += sy;
+      for (int k = 0; k < r; ++k) quad += c1[k] * xw[k] * xw[k] + 2 * c2[k] * xw[k] * yc[k] + c3[k] * yc[k] * yc[k];
     }
-    for (int j = 0; j < q; ++j) {
-      sy += y[j] * y[j];
-      for (int k = 0; k < r; ++k) yc[k] += y[j] * C[k * q + j];
-    }
-    ssx += sx;
-    ssy += sy;
-    for (int k = 0; k < r; ++k) quad += c1[k] * xw[k] * xw[k] + 2 * c2[k] * xw[k] * yc[k] + c3[k] * yc[k] * yc[k];
+    double* mine = part + 3 * (size_t)thread_id();
+    mine[0] = ssx;
+    mine[1] = ssy;
+    mine[2] = quad;
   }
+  double tot[3];
+  sum_ordered(part, T, 3, tot);
+  free(part);
+  const double ssx = tot[0], ssy = tot[1], quad = tot[2];
   const double traceL = ssx / sX2 + ssy / sY2 - quad;
   return -0.5 * (double)n * (p + q) * log(2 * M_PI) - 0.5 * (double)n * logdet - 0.5 * traceL;
 }
@@ -178,13 +206,18 @@ int cpu_ref_em_step(const double* X, const double* Y, int64_t n, int p, int q, i
   double* muU = (double*)malloc(sizeof(double) * n * r);
   double* Xw = (double*)malloc(sizeof(double) * n * r);
   double* Yc = (double*)malloc(sizeof(double) * n * r);
-  double tt[RM] = {0}, uu[RM] = {0}, ut[RM] = {0}, hh[RM * RM] = {0};
+  double tt[RM] = {0}, uu[RM] = {0}, ut[RM] = {0}, hh[RM * RM] = {0};   /* uu: Cuu, not used by the M-step */
+  (void)uu;
   double h1[RM], h2[RM];
   for (int k = 0; k < r; ++k) { h1[k] = sH2 / sF2 - sH2 * c3[k]; h2[k] = -sH2 * c2[k]; }
   /* pass 1: Xw, Yc, mu_T, mu_U and their crossprods (:689-701), mu_H crossprod (:711-712) */
-#pragma omp parallel
+  const int T = max_threads();
+  const int L1 = 3 * RM + RM * RM;
+  double* part1 = (double*)calloc((size_t)T * L1, sizeof(double));
+#pragma omp parallel num_threads(T)
   {
-    double ltt[RM] = {0}, luu[RM] = {0}, lut[RM] = {0}, lhh[RM * RM] = {0};
+    double* mine = part1 + (size_t)thread_id() * L1;
+    double *ltt = mine, *luu = mine + RM, *lut = mine + 2 * RM, *lhh = mine + 3 * RM;
 #pragma omp for schedule(static)
     for (int64_t i = 0; i < n; ++i) {
       const double* x = X + i * p;
@@ -208,15 +241,20 @@ int cpu_ref_em_step(const double* X, const double* Y, int64_t n, int p, int q, i
       for (int k = 0; k < r; ++k)
         for (int l = 0; l < r; ++l) lhh[l * r + k] += h[k] * h[l];
     }
-#pragma omp critical
-    {
-      for (int k = 0; k < r; ++k) { tt[k] += ltt[k]; uu[k] += luu[k]; ut[k] += lut[k]; }
-      for (int k = 0; k < r * r; ++k) hh[k] += lhh[k];
-    }
+  }
+  {
+    double tot1[3 * RM + RM * RM];
+    sum_ordered(part1, T, L1, tot1);
+    for (int k = 0; k < r; ++k) { tt[k] = tot1[k]; uu[k] = tot1[RM + k]; ut[k] = tot1[2 * RM + k]; }
+    for (int k = 0; k < r * r; ++k) hh[k] = tot1[3 * RM + k];
+    free(part1);
   }
   /* pass 2: ssq(mu_E), ssq(mu_F) streamed (:703-709) */
+  double* part2 = (double*)calloc((size_t)T * 2, sizeof(double));
+#pragma omp parallel num_threads(T)
+  {
   double sse = 0, ssf = 0;
-#pragma omp parallel for reduction(+ : sse, ssf) schedule(static)
+#pragma omp for schedule(static)
   for (int64_t i = 0; i < n; ++i) {
     const double* x = X + i * p;
     const double* y = Y + i * q;
@@ -236,6 +274,13 @@ int cpu_ref_em_step(const double* X, const double* Y, int64_t n, int p, int q, i
       ssf += f * f;
     }
   }
+  part2[2 * (size_t)thread_id()] = sse;
+  part2[2 * (size_t)thread_id() + 1] = ssf;
+  }
+  double tot2[2];
+  sum_ordered(part2, T, 2, tot2);
+  free(part2);
+  const double sse = tot2[0], ssf = tot2[1];
   const double N = (double)n;
   double Ctt[RM], Cut[RM], trChh = 0, sc1 = 0, sc3 = 0;
   for (int k = 0; k < r; ++k) {
@@ -251,10 +296,12 @@ int cpu_ref_em_step(const double* X, const double* Y, int64_t n, int p, int q, i
   /* pass 3: X' mu_T, Y' mu_U (:732-733) */
   double* SX = (double*)calloc((size_t)p * r, sizeof(double));
   double* SY = (double*)calloc((size_t)q * r, sizeof(double));
-#pragma omp parallel
+  const int L3 = (p + q) * r;
+  double* part3 = (double*)calloc((size_t)T * L3, sizeof(double));
+#pragma omp parallel num_threads(T)
   {
-    double* lx = (double*)calloc((size_t)p * r, sizeof(double));
-    double* ly = (double*)calloc((size_t)q * r, sizeof(double));
+    double* lx = part3 + (size_t)thread_id() * L3;
+    double* ly = lx + (size_t)p * r;
 #pragma omp for schedule(static)
     for (int64_t i = 0; i < n; ++i) {
       const double* x = X + i * p;
@@ -265,14 +312,13 @@ int cpu_ref_em_step(const double* X, const double* Y, int64_t n, int p, int q, i
         for (int j = 0; j < q; ++j) ly[k * q + j] += y[j] * mu;
       }
     }
-#pragma omp critical
-    {
-      for (int j = 0; j < p * r; ++j) SX[j] += lx[j];
-      for (int j = 0; j < q * r; ++j) SY[j] += ly[j];
-    }
-    free(lx);
-    free(ly);
   }
+  for (int t = 0; t < T; ++t) {   /* thread-index order */
+    const double* lx = part3 + (size_t)t * L3;
+    for (int j = 0; j < p * r; ++j) SX[j] += lx[j];
+    for (int j = 0; j < q * r; ++j) SY[j] += lx[(size_t)p * r + j];
+  }
+  free(part3);
   int rc = polar(SX, p, r, W);
   if (rc == 0) rc = polar(SY, q, r, C);
   for (int k = 0; k < r; ++k) {

@@ -63,8 +63,10 @@ def orth(X, type="SVD"):
     """OmicsPLS::orth -- semantics Package/functions.R:252-260.
 
     type "SVD": thin SVD X = U S V' -> U V' (the polar factor; R's svd() is LAPACK dgesdd,
-    numpy's svd is LAPACK gesdd as well).  type "QR": qr.Q(qr(X)) -- Householder QR, for which
-    LINPACK dqrdc2 and LAPACK geqrf share the sign convention R[k,k] = -sign(x_kk)*||x||.
+    numpy's svd is LAPACK gesdd as well).  type "QR": e = qr.Q(qr(X)) -- Householder QR, for which
+    LINPACK dqrdc2 and LAPACK geqrf share the sign convention R[k,k] = -sign(x_kk)*||x|| -- then
+    sign_e * e with the scalar sign_e = sign(crossprod(e[,1], X[,1])) (functions.R:257-259), so
+    the first column points along X[,1].
     """
     X = np.asarray(X, dtype=np.float64)
     if X.ndim == 1:
@@ -74,7 +76,7 @@ def orth(X, type="SVD"):
         return U @ Vt
     if type == "QR":
         Q, _ = np.linalg.qr(X, mode="reduced")
-        return Q
+        return np.sign(Q[:, 0] @ X[:, 0]) * Q   # sign_e * e (functions.R:258-259; R's sign(0) = 0)
     raise ValueError("type must be 'SVD' or 'QR'")
 
 

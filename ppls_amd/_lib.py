@@ -49,6 +49,9 @@ class PplsMetaFit(ct.Structure):
 
 _i64p = ct.POINTER(ct.c_int64)
 
+# typedef int (*ppls_reduce_fn)(void* user, double* buf, int64_t count)
+REDUCE_FN = ct.CFUNCTYPE(ct.c_int, ct.c_void_p, _dp, ct.c_int64)
+
 # name -> (restype, argtypes); every symbol declared in include/ppls.h
 SIGNATURES = {
     "ppls_version": (ct.c_int, []),
@@ -61,11 +64,13 @@ SIGNATURES = {
                                 ct.POINTER(ct.c_int64)]),
     "ppls_comm_unique_id": (ct.c_int, [ct.c_char_p]),
     "ppls_comm_init": (ct.c_int, [ct.c_void_p, ct.c_int, ct.c_int, ct.c_char_p]),
+    "ppls_set_reducer": (ct.c_int, [ct.c_void_p, ct.c_void_p, ct.c_void_p]),
     "ppls_set_data": (ct.c_int, [ct.c_void_p, _dp, _dp, ct.c_int64, ct.c_int, ct.c_int, ct.c_int,
                                  ct.c_int64]),
     "ppls_generate_synthetic": (ct.c_int, [ct.c_void_p, ct.c_int64, ct.c_int64, ct.c_int64, ct.c_int,
                                            ct.c_int, ct.c_int, ct.POINTER(PplsTheta), ct.c_uint64]),
     "ppls_get_data": (ct.c_int, [ct.c_void_p, _dp, _dp, ct.c_int64, ct.c_int64]),
+    "ppls_get_data_rows": (ct.c_int, [ct.c_void_p, _dp, _dp, ct.c_int64, ct.c_int64]),
     "ppls_data_ssq": (ct.c_int, [ct.c_void_p, _dp, _dp]),
     "ppls_estep": (ct.c_int, [ct.c_void_p, ct.POINTER(PplsTheta), ct.c_int, ct.POINTER(PplsExpect)]),
     "ppls_mstep": (ct.c_int, [ct.c_void_p, ct.POINTER(PplsExpect), ct.c_int, ct.c_int,
@@ -98,6 +103,7 @@ SIGNATURES = {
     "ppls_finalize_trace": (ct.c_int, [ct.c_void_p, ct.POINTER(ct.c_int64), _dp]),
     "ppls_sweep_info": (ct.c_int, [ct.c_void_p, ct.c_int, ct.POINTER(ct.c_int64), ct.POINTER(ct.c_int),
                                    ct.POINTER(ct.c_int)]),
+    "ppls_sweep_kernel": (ct.c_int, [ct.c_void_p, ct.c_int, ct.c_char_p, ct.c_int]),
     "ppls_finalize_host": (ct.c_int, [_dp, _dp, _dp, ct.c_double, ct.c_double, ct.c_double, ct.c_int,
                                       ct.c_int, ct.c_int, ct.POINTER(PplsTheta), ct.c_int,
                                       ct.POINTER(PplsTheta), ct.POINTER(PplsExpect), _dp]),

@@ -100,6 +100,28 @@ class Context:
         assert len(uid) == 128
         self._chk(self._L.ppls_comm_init(self.h, int(nranks), int(rank), uid))
 
+    def set_reducer(self, fn):
+        """Host-side reduction in place of RCCL (ppls_set_reducer): ``fn(buf)`` receives a float64
+        numpy view of the buffer and must overwrite it in place with its sum over all ranks (e.g.
+        ``torch.distributed.all_reduce`` on gloo).  ``None`` restores RCCL.  Collective when data
+        is resident."""
+        if fn is None:
+            self._reducer_cb = None
+            self._chk(self._L.ppls_set_reducer(self.h, None, None))
+            return
+
+        def _cb(_user, buf, count):
+            try:
+                fn(np.ctypeslib.as_array(buf, shape=(int(count),)))
+                return 0
+            except Exception:   # noqa: BLE001 -- reported to the library as a reduction failure
+                import traceback
+                traceback.print_exc()
+                return 1
+
+        self._reducer_cb = _lib.REDUCE_FN(_cb)   # kept alive as long as the context
+        self._chk(self._L.ppls_set_reducer(self.h, ct.cast(self._reducer_cb, ct.c_void_p), None))
+
     # -- data
     def set_data(self, X, Y, n_total=None):
         X = np.asarray(X, dtype=np.float64)
@@ -130,6 +152,14 @@ class Context:
         X = np.zeros((nrows, self.p), order="F")
         Y = np.zeros((nrows, self.q), order="F")
         self._chk(self._L.ppls_get_data(self.h, dptr(X), dptr(Y), int(row_begin), int(nrows)))
+        return X, Y
+
+    def get_data_rows(self, row_begin=0, nrows=None):
+        """Rows [row_begin, row_begin + nrows) of X, Y as C-ordered (row-major) float64 arrays."""
+        nrows = self.n_local - row_begin if nrows is None else nrows
+        X = np.empty((nrows, self.p))
+        Y = np.empty((nrows, self.q))
+        self._chk(self._L.ppls_get_data_rows(self.h, dptr(X), dptr(Y), int(row_begin), int(nrows)))
         return X, Y
 
     def ssq(self):
@@ -386,7 +416,13 @@ class Context:
     def sweep_info(self, r):
         b, v, g = ct.c_int64(), ct.c_int(), ct.c_int()
         self._chk(self._L.ppls_sweep_info(self.h, int(r), ct.byref(b), ct.byref(v), ct.byref(g)))
-        return dict(bytes_per_sweep=b.value, variant={1: "fused512", 2: "twopass", 3: "fused1024", 4: "split512", 5: "panel", 6: "team"}[v.value], grid=g.value)
+        return dict(bytes_per_sweep=b.value, variant={2: "twopass", 4: "split512", 5: "panel"}[v.value], grid=g.value)
+
+    def sweep_kernel(self, r):
+        """The sweep kernel instantiation an EM iteration with r components launches (text)."""
+        buf = ct.create_string_buffer(256)
+        self._chk(self._L.ppls_sweep_kernel(self.h, int(r), buf, 256))
+        return buf.value.decode()
 
 
 # ================================================================================ R mirror

@@ -16,7 +16,7 @@ LIB = os.path.join(HERE, "libppls_amd.so")
 ARCH = os.environ.get("PPLS_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
-SOURCES = ["ppls_kernels.hip", "ppls_variances.hip", "ppls_team.hip", "ppls_capi.cpp"]
+SOURCES = ["ppls_kernels.hip", "ppls_variances.hip", "ppls_capi.cpp"]
 HEADERS = ["ppls_kernels.h", "ppls_math.h", "ppls_device.h"]
 CFLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function", "-Wno-inline-asm",
           "-I" + os.path.join(ROOT, "include"), "-I" + CSRC]

@@ -29,11 +29,9 @@ struct ppls_ctx {
   std::string err;
   int num_cus = 256;
   // options
-  int sweep_mode = 0;
+  int sweep_mode = 0;      // 0 auto, 2 generic two-pass, 3 panel
   int grid_opt = 0;
-  int threads_opt = 0;
   int rp_opt = 0;   // rows per pipeline step: 0 auto (2 where the kernel fits in registers)
-  int kernel_opt = 0;   // fused sweep kernel: 0 auto, 2 = shared ownership (v2), 3 = split ownership
   int pipe_opt = 1;     // split kernel: software-pipelined order
   int ablate = 0;
   int dtype = 0;           // storage of X, Y: 0 fp64, 1 fp32 (arithmetic is fp64 either way)
@@ -42,16 +40,12 @@ struct ppls_ctx {
   int64_t sweep_count = 0;
   // row segment the next sweeps cover (meta_* per-population sweeps); seg_rows < 0 = all rows
   int64_t seg_row0 = 0, seg_rows = -1;
-  // team single-pass sweep (wide data): exchange buffer, launch epoch, device status, current plan
-  uint64_t* team_xch = nullptr;
-  int64_t team_xch_words = 0;
-  uint32_t team_epoch = 0;
-  int* team_status = nullptr;
-  bool team_disabled = false;   // a cooperative launch was refused: panel sweep from then on
-  PplsTeamPlan tplan{};
-  // communicator
+  // communicator: RCCL, or a caller-supplied host reduction (ppls_set_reducer)
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0;
+  ppls_reduce_fn reducer = nullptr;
+  void* reducer_user = nullptr;
+  std::vector<double> reduce_host;
   // data
   bool have_data = false;
   int64_t n_local = 0, n_total = 0;
@@ -276,21 +270,22 @@ int download_mu(ppls_ctx* c, int r, ppls_expect* e) {
   return PPLS_OK;
 }
 
-// Fused workgroup size: option "threads" (512 / 1024) is a preference that falls back to the other
-// size when unsupported; auto = 512 (measured faster than 1024 at every shape tried).
-bool use_fused(ppls_ctx* c, int r, int* ns, int* threads) {
-  int t = c->threads_opt ? c->threads_opt : 512;
-  if (!ppls_fused_supported(r, c->ldx, c->ldy, t)) t = (t == 512) ? 1024 : 512;
-  *threads = t;
-  *ns = ppls_fused_supported(r, c->ldx, c->ldy, t);
-  if (c->sweep_mode == 2) return false;
-  return *ns > 0;
-}
-
 int grid_of(ppls_ctx* c) { return c->grid_opt > 0 ? c->grid_opt : c->num_cus; }
 
-// Allreduce in place (sum) over ranks, on the context stream.
+// Allreduce in place (sum) over ranks, on the context stream: RCCL, or the caller's host
+// reduction (ppls_set_reducer: device -> host, fn sums over the caller's ranks, host -> device).
 int allreduce(ppls_ctx* c, double* buf, size_t count) {
+  if (c->reducer) {
+    if (c->reduce_host.size() < count) c->reduce_host.resize(count);
+    double* h = c->reduce_host.data();
+    HIPCHK(c, hipMemcpyAsync(h, buf, sizeof(double) * count, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    const int rc = c->reducer(c->reducer_user, h, (int64_t)count);
+    if (rc != 0) return fail(c, PPLS_E_COMM, "host reducer returned %d", rc);
+    HIPCHK(c, hipMemcpyAsync(buf, h, sizeof(double) * count, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return PPLS_OK;
+  }
   if (!c->comm) return PPLS_OK;   // a 1-rank communicator still takes the RCCL path
   RCCLCHK(c, ncclAllReduce(buf, buf, count, ncclDouble, ncclSum, c->comm, c->stream));
   return PPLS_OK;
@@ -306,14 +301,12 @@ int ensure_part(ppls_ctx* c, int groups) {
   return rc;
 }
 
-// Which sweep kernel runs for this shape: 3 = split ownership (default), 1 = shared ownership
-// (v2, option kernel=2), 2 = generic two-pass; *grid is the workgroup count.
+// Which sweep kernel runs for this shape: 3 = split ownership (default), 4 = panel (wide p, large r
+// or fp32 storage), 2 = generic two-pass (option sweep = 2); a->grid is the workgroup count.
 int64_t sweep_rows(const ppls_ctx* c) { return c->seg_rows >= 0 ? c->seg_rows : c->n_local; }
 
 int sweep_plan(ppls_ctx* c, int r, PplsSweepArgs* a) {
-  int ns = 0, threads = 512;
   const int64_t nrows = sweep_rows(c);
-  const bool fused = use_fused(c, r, &ns, &threads);
   const int nsplit = ppls_split_supported(r, c->ldx, c->ldy);
   memset(a, 0, sizeof *a);
   a->ldx = c->ldx;
@@ -321,21 +314,12 @@ int sweep_plan(ppls_ctx* c, int r, PplsSweepArgs* a) {
   a->p = c->p;
   a->q = c->q;
   a->r = r;
-  a->threads = threads;
-  // wide data / fp32 storage: the panel sweep (two GEMM-shaped passes, 4), or with sweep = 4 the
-  // team single-pass sweep (5) where a team plan exists (measured slower at C5)
-  auto wide = [&]() {
-    if (c->sweep_mode == 4 && !c->team_disabled &&
-        ppls_team_plan(r, c->ldx, c->ldy, c->dtype, c->num_cus, nrows, &c->tplan)) {
-      a->grid = c->tplan.nteams;
-      return 5;
-    }
-    a->grid = c->grid_opt > 0 ? c->grid_opt : ppls_panel_chunks(nrows, c->ldx, c->ldy, c->num_cus, c->dtype, r);
-    a->dots_grid = c->grid_opt;   // the grid option also sets the dots grid (tests: grid-stride path)
-    return 4;
-  };
-  if (c->sweep_mode == 3 || c->sweep_mode == 4 || c->dtype) return wide();
-  if (c->sweep_mode != 2 && nsplit > 0 && c->kernel_opt != 2) {
+  a->threads = 512;
+  if (c->sweep_mode == 2) {
+    a->grid = grid_of(c);
+    return 2;
+  }
+  if (c->sweep_mode != 3 && !c->dtype && nsplit > 0) {
     a->ns = nsplit;
     a->pipe = c->pipe_opt;
     a->rp = c->rp_opt;             // 0 = auto: two rows per step wherever instantiated
@@ -346,29 +330,10 @@ int sweep_plan(ppls_ctx* c, int r, PplsSweepArgs* a) {
     a->grid = c->grid_opt > 0 ? c->grid_opt : c->num_cus * occ;
     return 3;
   }
-  if (fused) {
-    a->ns = ns;
-    a->rp = (c->rp_opt != 1 && ns == 1 && r <= 4 && threads == 512) ? 2 : 1;
-    a->grid = grid_of(c);
-    return 1;
-  }
-  if (c->sweep_mode != 2) return wide();   // wide p / large r
-  a->grid = grid_of(c);
-  return 2;
-}
-
-int ensure_team(ppls_ctx* c) {
-  int rc;
-  if (!c->team_status) {
-    if ((rc = dalloc(c, &c->team_status, 1))) return rc;
-    HIPCHK(c, hipMemset(c->team_status, 0, sizeof(int)));
-  }
-  if (c->tplan.xch_words > c->team_xch_words) {
-    if ((rc = dalloc(c, &c->team_xch, (size_t)c->tplan.xch_words))) return rc;
-    HIPCHK(c, hipMemset(c->team_xch, 0, sizeof(uint64_t) * (size_t)c->tplan.xch_words));
-    c->team_xch_words = c->tplan.xch_words;
-  }
-  return PPLS_OK;
+  // wide data / large r / fp32 storage: the panel sweep (two GEMM-shaped passes)
+  a->grid = c->grid_opt > 0 ? c->grid_opt : ppls_panel_chunks(nrows, c->ldx, c->ldy, c->num_cus, c->dtype, r);
+  a->dots_grid = c->grid_opt;   // the grid option also sets the dots grid (tests: grid-stride path)
+  return 4;
 }
 
 // One sweep with theta[slot] -> c->stats (all-reduced).
@@ -424,19 +389,7 @@ int sweep(ppls_ctx* c, int r, int slot, bool write_mu) {
       HIPCHK(c, hipEventRecord(e0, c->stream));
     }
     if (plan == 3) HIPCHK(c, ppls_launch_sweep_split(&a, c->stream));
-    else if (plan == 1) HIPCHK(c, ppls_launch_sweep_fused(&a, c->stream));
     else if (plan == 4) HIPCHK(c, ppls_launch_sweep_panel(&a, c->dtype, c->Z, a.grid, c->stream));
-    else if (plan == 5) {
-      if ((rc = ensure_team(c))) return rc;
-      const hipError_t e = ppls_launch_sweep_team(&c->tplan, &a, c->dtype, c->team_xch, ++c->team_epoch,
-                                                  nt ? 1 : 0, c->team_status, c->stream);
-      if (e != hipSuccess) {   // e.g. cooperative launch refused: the panel sweep from now on
-        (void)hipGetLastError();
-        c->team_disabled = true;
-        if (timed) HIPCHK(c, hipEventRecord(e1, c->stream));
-        return sweep(c, r, slot, write_mu);
-      }
-    }
     else HIPCHK(c, ppls_launch_sweep_twopass(&a, c->Z, c->stream));
     if (timed) HIPCHK(c, hipEventRecord(e1, c->stream));
     HIPCHK(c, ppls_launch_reduce2(c->part, groups, c->part_ld, c->part_ld, c->stats,
@@ -477,14 +430,6 @@ int finalize(ppls_ctx* c, int r, int cur, int nxt, int logl_index, int type) {
 }
 
 int check_status(ppls_ctx* c) {
-  if (c->team_status) {
-    int ts = 0;
-    HIPCHK(c, hipMemcpy(&ts, c->team_status, sizeof ts, hipMemcpyDeviceToHost));
-    if (ts != 0) {
-      HIPCHK(c, hipMemset(c->team_status, 0, sizeof(int)));
-      return fail(c, PPLS_E_HIP, "team sweep: a workgroup's exchange timed out (status %d)", ts);
-    }
-  }
   int st = 0;
   HIPCHK(c, hipMemcpy(&st, c->status, sizeof st, hipMemcpyDeviceToHost));
   if (st != 0) return fail(c, PPLS_E_NUMERIC, "rank-deficient X'mu_T or Y'mu_U in the M-step (status %d)", st);
@@ -586,8 +531,9 @@ int host_orth(const double* S, int p, int r, int type, double* out) {
       const double f = 2.0 * d / vtv[k];
       for (int i = k; i < p; ++i) E[(size_t)j * p + i] -= f * A[(size_t)k * p + i];
     }
-  if (type == PPLS_ORTH_QR) {
-    memcpy(out, E.data(), sizeof(double) * E.size());
+  if (type == PPLS_ORTH_QR) {   // sign_e * qr.Q(qr(S)), sign_e = sign(<e_1, S_1>) = sign(R_11) (functions.R:257-259)
+    const double sg = R[0] < 0.0 ? -1.0 : 1.0;
+    for (size_t e = 0; e < E.size(); ++e) out[e] = sg * E[e];
     return PPLS_OK;
   }
   if (ppls_small_polar(R, r, P) != 0) return PPLS_E_NUMERIC;
@@ -652,7 +598,6 @@ void ppls_ctx_destroy(ppls_ctx* c) {
   if (c->ftrace) (void)hipFree(c->ftrace);
   for (auto& e : c->ev) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
   if (c->blas) (void)rocblas_destroy_handle(c->blas);
-  dfree(c->team_xch); dfree(c->team_status);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -662,23 +607,17 @@ const char* ppls_last_error(const ppls_ctx* c) { return c ? c->err.c_str() : "nu
 int ppls_set_option(ppls_ctx* c, const char* key, int64_t value) {
   if (!c || !key) return PPLS_E_ARG;
   if (!strcmp(key, "sweep")) {
-    if (value < 0 || value > 4)
-      return fail(c, PPLS_E_ARG, "sweep must be 0 (auto), 1 (fused), 2 (two-pass), 3 (panel) or 4 (team)");
+    if (value != 0 && value != 2 && value != 3)
+      return fail(c, PPLS_E_ARG, "sweep must be 0 (auto), 2 (two-pass) or 3 (panel)");
     c->sweep_mode = (int)value;
   } else if (!strcmp(key, "grid")) {
     if (value < 0 || value > 65535) return fail(c, PPLS_E_ARG, "grid out of range");
     c->grid_opt = (int)value;
     c->part_groups = 0;
     dfree(c->part);
-  } else if (!strcmp(key, "threads")) {
-    if (value != 0 && value != 512 && value != 1024) return fail(c, PPLS_E_ARG, "threads must be 0, 512 or 1024");
-    c->threads_opt = (int)value;
   } else if (!strcmp(key, "rows_per_step")) {
     if (value < 0 || value > 2) return fail(c, PPLS_E_ARG, "rows_per_step must be 0 (auto), 1 or 2");
     c->rp_opt = (int)value;
-  } else if (!strcmp(key, "kernel")) {
-    if (value != 0 && value != 2 && value != 3) return fail(c, PPLS_E_ARG, "kernel must be 0, 2 or 3");
-    c->kernel_opt = (int)value;
   } else if (!strcmp(key, "pipe")) {
     c->pipe_opt = value ? 1 : 0;
   } else if (!strcmp(key, "ablate")) {
@@ -733,12 +672,22 @@ int ppls_comm_init(ppls_ctx* c, int nranks, int rank, const char id[128]) {
   if (c->comm) { ncclCommDestroy(c->comm); c->comm = nullptr; }
   c->nranks = nranks;
   c->rank = rank;
-  if (nranks > 1 || id) {
+  if (nranks > 1 && !id) return fail(c, PPLS_E_ARG, "nranks=%d needs the root's unique id", nranks);
+  if (id) {
     ncclUniqueId u;
     memcpy(u.internal, id, 128);
     RCCLCHK(c, ncclCommInitRank(&c->comm, nranks, u, rank));
   }
   if (c->have_data) return compute_ssq(c);
+  return PPLS_OK;
+}
+
+int ppls_set_reducer(ppls_ctx* c, ppls_reduce_fn fn, void* user) {
+  if (!c) return PPLS_E_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  c->reducer = fn;
+  c->reducer_user = user;
+  if (c->have_data) return compute_ssq(c);   // ||X||^2, ||Y||^2 summed by the new reduction
   return PPLS_OK;
 }
 
@@ -842,6 +791,42 @@ int ppls_generate_synthetic(ppls_ctx* c, int64_t n_total, int64_t row0, int64_t 
   if (e != hipSuccess) return fail(c, PPLS_E_HIP, "synthetic generation: %s", hipGetErrorString(e));
   c->have_data = true;
   return compute_ssq(c);
+}
+
+int ppls_get_data_rows(ppls_ctx* c, double* X, double* Y, int64_t row_begin, int64_t nrows) {
+  if (!c) return PPLS_E_ARG;
+  if (!c->have_data) return fail(c, PPLS_E_STATE, "no data");
+  if (row_begin < 0 || nrows < 0 || row_begin + nrows > c->n_local) return fail(c, PPLS_E_ARG, "bad row range");
+  if (nrows == 0) return PPLS_OK;
+  HIPCHK(c, hipSetDevice(c->device));
+  int rc;
+  const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(nrows, (int64_t)(256 << 20) / (8LL * std::max(c->ldx, c->ldy))));
+  double* wide = nullptr;
+  if (c->dtype && (rc = dalloc(c, &wide, (size_t)chunk * std::max(c->ldx, c->ldy)))) return rc;
+  for (int m = 0; m < 2; ++m) {
+    double* dst = m == 0 ? X : Y;
+    if (!dst) continue;
+    const int cols = m == 0 ? c->p : c->q, ld = m == 0 ? c->ldx : c->ldy;
+    for (int64_t r0 = 0; r0 < nrows; r0 += chunk) {
+      const int64_t nc = std::min(chunk, nrows - r0), g0 = row_begin + r0;
+      const double* src = (m == 0 ? c->X : c->Y) + g0 * ld;
+      hipError_t e = hipSuccess;
+      if (c->dtype) {   // fp32 storage: widen the rows first
+        e = ppls_launch_convert((const float*)(m == 0 ? c->X : c->Y) + g0 * ld, 1, wide, 0, nc * ld, c->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+        src = wide;
+      }
+      if (e == hipSuccess)
+        e = hipMemcpy2D(dst + r0 * cols, sizeof(double) * cols, src, sizeof(double) * ld, sizeof(double) * cols, nc,
+                        hipMemcpyDeviceToHost);
+      if (e != hipSuccess) {
+        dfree(wide);
+        return fail(c, PPLS_E_HIP, "copy back: %s", hipGetErrorString(e));
+      }
+    }
+  }
+  dfree(wide);
+  return PPLS_OK;
 }
 
 int ppls_get_data(ppls_ctx* c, double* X, double* Y, int64_t row_begin, int64_t nrows) {
@@ -1932,8 +1917,27 @@ int ppls_sweep_info(ppls_ctx* c, int r, int64_t* bytes_per_sweep, int* variant, 
   PplsSweepArgs a;
   const int plan = sweep_plan(c, r, &a);
   if (bytes_per_sweep) *bytes_per_sweep = (int64_t)(c->dtype ? 4 : 8) * c->n_local * ((int64_t)c->p + c->q);
-  if (variant) *variant = plan == 5 ? 6 : plan == 4 ? 5 : plan == 3 ? 4 : plan == 1 ? (a.threads == 1024 ? 3 : 1) : 2;
+  if (variant) *variant = plan == 4 ? 5 : plan == 3 ? 4 : 2;
   if (grid) *grid = a.grid;
+  return PPLS_OK;
+}
+
+int ppls_sweep_kernel(ppls_ctx* c, int r, char* buf, int len) {
+  if (!c || !buf || len < 1) return PPLS_E_ARG;
+  if (r < 1 || r > PPLS_RMAX) return fail(c, PPLS_E_ARG, "bad r");
+  PplsSweepArgs a;
+  const int plan = sweep_plan(c, r, &a);
+  const int nt = c->nt_loads > 0 ||
+                 (c->nt_loads < 0 && 8.0 * sweep_rows(c) * (double)(c->ldx + c->ldy) > 256.0 * (1 << 20));
+  char k[128];
+  if (plan == 3) {
+    if (ppls_split_describe(&a, k, sizeof k) != 0) return fail(c, PPLS_E_STATE, "no split instantiation for r=%d", r);
+  } else if (plan == 4) {
+    snprintf(k, sizeof k, "panel<%s,%d> (mfmadots + acc, %d chunks)", c->dtype ? "float" : "double", r, a.grid);
+  } else {
+    snprintf(k, sizeof k, "twopass (dots + acc, %d chunks)", a.grid);
+  }
+  snprintf(buf, (size_t)len, "%s%s", k, plan == 3 && nt ? " nt" : "");
   return PPLS_OK;
 }
 

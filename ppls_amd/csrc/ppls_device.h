@@ -1,4 +1,4 @@
-// ppls_device.h -- device helpers shared by the sweep kernels (ppls_kernels.hip, ppls_team.hip):
+// ppls_device.h -- device helpers shared by the sweep kernels (ppls_kernels.hip):
 // the wave reduce-scatter (permlane / DPP butterflies) and the LDS-DMA ring primitives.
 #pragma once
 
@@ -98,12 +98,6 @@ __device__ __forceinline__ void ppls_dma16_nt(const void* gptr, uint32_t lds_add
 }
 __device__ __forceinline__ void ppls_dma16(const void* gptr, uint32_t lds_addr) {
   asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off"
-               :: "s"(lds_addr), "v"(gptr) : "memory", "m0");
-}
-
-// The same copy with device-scope loads (sc1: past the CU's L1, served by the XCD's L2).
-__device__ __forceinline__ void ppls_dma16_l2(const void* gptr, uint32_t lds_addr) {
-  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off sc1"
                :: "s"(lds_addr), "v"(gptr) : "memory", "m0");
 }
 

@@ -6,7 +6,6 @@
 
 #include "ppls_math.h"
 
-#define PPLS_SWEEP_THREADS 512   // 8 waves, one workgroup per CU
 #define PPLS_SWEEP_SLOTS 4       // LDS-DMA ring depth (rows)
 #define PPLS_FUSED_RMAX 8
 
@@ -24,22 +23,14 @@ struct PplsSweepArgs {
   double* mu;            // n_local x 2r column-major [mu_T | mu_U] or nullptr
   int write_mu;
   int r;
-  int ns;                // column pairs per thread (fused)
-  int threads;           // fused workgroup size: 512 or 1024
-  int rp;                // fused rows per pipeline step (1 or 2)
+  int ns;                // split sweep: column pairs per thread
+  int threads;           // split sweep workgroup size (512)
+  int rp;                // split sweep rows per pipeline step (0 auto, 1 or 2)
   int pipe;              // split kernel: 1 = dots(g+1) before update(g), 0 = after
   int* occ_out;          // split kernel: if set, report resident WGs per CU instead of launching
-  int grid;              // workgroups (fused) / row chunks (two-pass)
-  int ablate;            // timing experiments only (fused): 1 no compute, 2 no HBM copies
+  int grid;              // workgroups (split) / row chunks (two-pass, panel accumulation)
+  int ablate;            // timing experiments only (split): 1 no compute, 2 no HBM copies; 16 = nt loads
   int dots_grid;         // panel dots workgroups (0 = one per 128-row group, capped)
-};
-
-// Team single-pass sweep for wide data (ppls_team.hip): teams of S workgroups x (1 comm + wpw data
-// waves); nteams partial rows.
-struct PplsTeamPlan {
-  int S, wpw, nwx, nwy, grid, nteams;
-  double eff;            // lane x CU utilisation of the plan
-  int64_t xch_words;     // uint64 words of the exchange buffer
 };
 
 struct PplsFinalizeArgs {
@@ -67,11 +58,9 @@ struct PplsFinalizeArgs {
 };
 
 extern "C" {
-int ppls_fused_supported(int r, int ldx, int ldy, int threads);
-size_t ppls_fused_lds_bytes(int r, int ldx, int ldy, int threads);
-hipError_t ppls_launch_sweep_fused(const PplsSweepArgs* a, hipStream_t st);
 int ppls_split_supported(int r, int ldx, int ldy);
 hipError_t ppls_launch_sweep_split(const PplsSweepArgs* a, hipStream_t st);
+int ppls_split_describe(const PplsSweepArgs* a, char* buf, int len);
 hipError_t ppls_launch_sweep_twopass(const PplsSweepArgs* a, double* Z, hipStream_t st);
 hipError_t ppls_launch_accumulate(const PplsSweepArgs* a, const double* Z, hipStream_t st);
 int ppls_twopass_groups(int64_t n_local, int grid);
@@ -102,11 +91,6 @@ hipError_t ppls_launch_generate(int64_t n_local, int64_t row0, int p, int q, int
                                 uint64_t seed, double* TU, double* X, double* Y, hipStream_t st);
 hipError_t ppls_launch_to_rowmajor(const double* src, int64_t n, int p, int ld, double* dst,
                                    hipStream_t st);
-// team sweep (ppls_team.hip)
-size_t ppls_team_lds_bytes(int r, int wpw, int S);
-int ppls_team_plan(int r, int ldx, int ldy, int f32, int num_cus, int64_t n, PplsTeamPlan* tp);
-hipError_t ppls_launch_sweep_team(const PplsTeamPlan* tp, const PplsSweepArgs* a, int f32, uint64_t* xch,
-                                  uint32_t epoch, int nt_loads, int* status, hipStream_t st);
 // variances.PPLS_simult (ppls_variances.hip)
 int ppls_gram_tiles(int p);
 int ppls_gram_occupancy(int f32);

@@ -11,6 +11,11 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <cstdio>
+#include <mutex>
+#include <set>
+#include <tuple>
+
 #include "ppls_kernels.h"
 #include "ppls_math.h"
 
@@ -259,242 +264,14 @@ __global__ void ppls_reduce_chunks_kernel(const double* __restrict__ part, int n
 
 #include "ppls_device.h"
 
-// ============================================================================ fused sweep
-// One workgroup (NT threads, one per CU) owns a contiguous block of rows.  Each thread owns NS
-// column pairs of X and NS of Y for the whole sweep: it keeps W/C for those columns and the
-// X'mu_T / Y'mu_U accumulators in registers.  Rows stream HBM -> LDS through a ring of SLOTS row
-// slots filled by LDS-DMA (global_load_lds_dwordx4; the first ceil(nch/CPW) waves copy CPW 1-KiB
-// chunks of every row, so the steady-state vmcnt is a compile-time immediate).  The loop handles
-// RP rows per step, software-pipelined: step g sums group g's dots (cross-wave, LDS), computes
-// group g+1's dots + wave reduce-scatter, then applies group g's rank-RP update -- ONE workgroup
-// barrier per step (reduction scratch double-buffered).  mu_T / mu_U and [Xw Yc] rows are
-// broadcast through a per-wave LDS scratch (no readlane / SGPR traffic).  X, Y are read once.
-template <int R, int NS, int NT, int RP, int SLOTS, int CPW>
-__global__ __launch_bounds__(NT, 2 * NT / 512) void ppls_sweep_fused_kernel(
-    const double* __restrict__ X, const double* __restrict__ Y, int64_t n_local, int ldx, int ldy,
-    const double* __restrict__ Wp, const double* __restrict__ Cp, const PplsScalars* __restrict__ sc,
-    double* __restrict__ part, int64_t part_ld, double* __restrict__ mu, int write_mu, int ablate) {
-  // ablate bit4: LDS-DMA with the non-temporal policy (a cache hint; results unchanged).
-  // ablate (timing experiments only; results are garbage): bit0 skips the per-row compute,
-  // bit1 skips the HBM->LDS copies.
-  static_assert(SLOTS >= 2 * RP, "ring must hold the group being read and the group in flight");
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  constexpr int V = 2 * R * RP;                       // partial dots per thread per step
-  constexpr int VP = V;                               // reduce-scatter scratch (V is even)
-  constexpr int NWAVES = NT / 64;
-  constexpr int AHEAD = SLOTS / RP - 2;               // groups in flight beyond the next one
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int nchx = (ldx * 8 + 1023) >> 10, nchy = (ldy * 8 + 1023) >> 10;
-  const int nch = nchx + nchy;
-  const int slot_bytes = nch << 10;
-  const bool dma_wave = wave * CPW < nch;
-  double* red = (double*)(smem + (size_t)SLOTS * slot_bytes);          // [2][NWAVES][V]
-  double* bc = red + 2 * NWAVES * V + wave * V;                       // per wave: [Xw Yc] rows
-  double* cf = red + 3 * NWAVES * V;                                  // alpha | beta | gamma | delta
-  const int64_t g = blockIdx.x, G = gridDim.x;
-  const int64_t rb = n_local * g / G, re = n_local * (g + 1) / G;
-  const int nrows = (int)(re - rb);
-  const int ngroups = (nrows + RP - 1) / RP;
-  const int npx = ldx >> 1, npy = ldy >> 1;
-
-  bool vx[NS], vy[NS];
-  double2 w[NS][R], c[NS][R], ax[NS][R], ay[NS][R];
-#pragma unroll
-  for (int s = 0; s < NS; ++s) {
-    const int px = tid + s * NT;
-    vx[s] = px < npx;
-    vy[s] = px < npy;
-#pragma unroll
-    for (int k = 0; k < R; ++k) {
-      w[s][k] = vx[s] ? *(const double2*)(Wp + (int64_t)k * ldx + 2 * px) : make_double2(0.0, 0.0);
-      c[s][k] = vy[s] ? *(const double2*)(Cp + (int64_t)k * ldy + 2 * px) : make_double2(0.0, 0.0);
-      ax[s][k] = make_double2(0.0, 0.0);
-      ay[s][k] = make_double2(0.0, 0.0);
-    }
-  }
-  // lane m < R*RP of every wave turns (a, b) = (Xw, Yc) of row m/R, component m%R into mu_T, mu_U;
-  // the coefficients live in LDS (no registers, no VMEM inside the DMA-counted loop)
-  const int mj = lane / R, mk = lane - (lane / R) * R;
-  if (tid < R) {
-    cf[tid] = sc->alpha[tid];
-    cf[R + tid] = sc->beta[tid];
-    cf[2 * R + tid] = sc->gamma[tid];
-    cf[3 * R + tid] = sc->delta[tid];
-  }
-  // Gram entry owned by this thread (upper triangle of the 2R x 2R Gram, one entry per thread)
-  const int ge = wave * 64 + lane;
-  int gi = 0, gj = 0;
-  const bool has_g = ge < R * (2 * R + 1);
-  if (has_g) {
-    int e = ge, j = 0;
-    while (e >= j + 1) { e -= j + 1; ++j; }
-    gi = e;
-    gj = j;
-  }
-  double gacc = 0.0;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-
-  const uint32_t lds_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
-  auto issue_row = [&](int i) {
-    if ((ablate & 2) || !dma_wave) return;
-    const int64_t row = rb + i;
-    const char* xr = (const char*)(X + row * (int64_t)ldx);
-    const char* yr = (const char*)(Y + row * (int64_t)ldy);
-    const uint32_t sb = lds_base + (uint32_t)((i % SLOTS) * slot_bytes);
-#pragma unroll
-    for (int j = 0; j < CPW; ++j) {
-      const int ch = min(wave * CPW + j, nch - 1);   // surplus issues repeat the last chunk
-      const char* src;
-      if (ch < nchx) src = xr + min(ch * 1024 + lane * 16, ldx * 8 - 16);
-      else src = yr + min((ch - nchx) * 1024 + lane * 16, ldy * 8 - 16);
-      if (ablate & 16) ppls_dma16_nt(src, sb + (uint32_t)(ch * 1024));
-      else ppls_dma16(src, sb + (uint32_t)(ch * 1024));
-    }
-  };
-  auto issue_group = [&](int grp) {
-    for (int j = 0; j < RP; ++j)
-      if (grp * RP + j < nrows) issue_row(grp * RP + j);
-  };
-  // group grp's partial dots -> wave reduce-scatter -> red[grp & 1]; keeps the rows' x/y pairs
-  auto dots_group = [&](int grp, double2 (&xv)[RP][NS], double2 (&yv)[RP][NS]) {
-    if (ablate & 1) return;
-    double v[VP];
-#pragma unroll
-    for (int j = 0; j < RP; ++j) {
-      const int row = min(grp * RP + j, nrows - 1);   // a partial last group repeats its last row
-      const char* sb = smem + (size_t)(row % SLOTS) * slot_bytes;
-#pragma unroll
-      for (int s = 0; s < NS; ++s) {
-        const int px = tid + s * NT;
-        xv[j][s] = vx[s] ? *(const double2*)(sb + px * 16) : make_double2(0.0, 0.0);
-        yv[j][s] = vy[s] ? *(const double2*)(sb + nchx * 1024 + px * 16) : make_double2(0.0, 0.0);
-      }
-#pragma unroll
-      for (int k = 0; k < R; ++k) {
-        double sx = 0.0, sy = 0.0;
-#pragma unroll
-        for (int s = 0; s < NS; ++s) {
-          sx = fma(xv[j][s].x, w[s][k].x, sx);
-          sx = fma(xv[j][s].y, w[s][k].y, sx);
-          sy = fma(yv[j][s].x, c[s][k].x, sy);
-          sy = fma(yv[j][s].y, c[s][k].y, sy);
-        }
-        v[j * 2 * R + k] = sx;
-        v[j * 2 * R + R + k] = sy;
-      }
-    }
-#pragma unroll
-    for (int k = V; k < VP; ++k) v[k] = 0.0;
-    int idx = 0;
-    bool canon = true;
-    ppls_rs<V, 0, VP>(v, lane, idx, canon);
-    if (canon && idx < V) red[((grp & 1) * NWAVES + wave) * V + idx] = v[0];
-  };
-
-  if (ngroups > 0) {
-    const int npro = min(SLOTS, nrows);
-    for (int i = 0; i < npro; ++i) issue_row(i);
-    if (write_mu) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    else ppls_wait_vmcnt((npro - min(RP, nrows)) * CPW);
-    ppls_lds_barrier();
-    double2 xc[RP][NS] = {}, yc[RP][NS] = {};
-    dots_group(0, xc, yc);
-    for (int gg = 0; gg < ngroups; ++gg) {
-      // rows issued after group gg+1: steady state AHEAD groups (compile-time wait)
-      if (write_mu) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      } else if ((gg + 2 + AHEAD) * RP <= nrows && gg >= 1) {
-        if constexpr (AHEAD * RP * CPW == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        else ppls_wait_vmcnt(AHEAD * RP * CPW);
-      } else {
-        const int last_issued = min(gg >= 1 ? (gg - 1) * RP + SLOTS + RP - 1 : SLOTS - 1, nrows - 1);
-        ppls_wait_vmcnt(max(0, last_issued - ((gg + 2) * RP - 1)) * CPW);
-      }
-      ppls_lds_barrier();   // red[gg&1] complete, group gg+1 landed, slots of group gg free
-      if (gg * RP + SLOTS < nrows) issue_group(gg + SLOTS / RP);
-      if (ablate & 1) continue;
-      // cross-wave sums of group gg: lane m < R*RP holds (a, b) = (Xw, Yc)[row m/R][comp m%R]
-      // and its mu_T / mu_U; [Xw Yc] rows go to the per-wave LDS scratch for the Gram
-      double mta = 0.0, mua = 0.0;
-      if (lane < R * RP) {
-        const double* rr = red + (gg & 1) * NWAVES * V;
-        double a = 0.0, b = 0.0;
-#pragma unroll
-        for (int ww = 0; ww < NWAVES; ++ww) {
-          a += rr[ww * V + mj * 2 * R + mk];
-          b += rr[ww * V + mj * 2 * R + R + mk];
-        }
-        bc[mj * 2 * R + mk] = a;
-        bc[mj * 2 * R + R + mk] = b;
-        mta = cf[mk] * a + cf[R + mk] * b;           // mu_T (EM_W_multi.R:691-692)
-        mua = cf[2 * R + mk] * a + cf[3 * R + mk] * b;   // mu_U (EM_W_multi.R:693-694)
-      }
-      double2 xn[RP][NS] = {}, yn[RP][NS] = {};
-      if (gg + 1 < ngroups) dots_group(gg + 1, xn, yn);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's bc writes are visible
-#pragma unroll
-      for (int j = 0; j < RP; ++j) {
-        if (gg * RP + j >= nrows) break;
-        if (has_g) gacc = fma(bc[j * 2 * R + gi], bc[j * 2 * R + gj], gacc);
-        double mt[R], mu_u[R];
-#pragma unroll
-        for (int k = 0; k < R; ++k) {
-          mt[k] = __hiloint2double(__builtin_amdgcn_readlane((int)__double2hiint(mta), j * R + k),
-                                   __builtin_amdgcn_readlane((int)__double2loint(mta), j * R + k));
-          mu_u[k] = __hiloint2double(__builtin_amdgcn_readlane((int)__double2hiint(mua), j * R + k),
-                                     __builtin_amdgcn_readlane((int)__double2loint(mua), j * R + k));
-        }
-        if (write_mu && wave == 0 && lane < R) {
-          const int64_t row = rb + gg * RP + j;
-          double a = 0.0, b = 0.0;
-#pragma unroll
-          for (int k = 0; k < R; ++k)
-            if (lane == k) { a = mt[k]; b = mu_u[k]; }
-          mu[(int64_t)lane * n_local + row] = a;
-          mu[(int64_t)(R + lane) * n_local + row] = b;
-        }
-#pragma unroll
-        for (int s = 0; s < NS; ++s)
-#pragma unroll
-          for (int k = 0; k < R; ++k) {
-            ax[s][k].x = fma(xc[j][s].x, mt[k], ax[s][k].x);
-            ax[s][k].y = fma(xc[j][s].y, mt[k], ax[s][k].y);
-            ay[s][k].x = fma(yc[j][s].x, mu_u[k], ay[s][k].x);
-            ay[s][k].y = fma(yc[j][s].y, mu_u[k], ay[s][k].y);
-          }
-      }
-#pragma unroll
-      for (int j = 0; j < RP; ++j)
-#pragma unroll
-        for (int s = 0; s < NS; ++s) {
-          xc[j][s] = xn[j][s];
-          yc[j][s] = yn[j][s];
-        }
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  // partials: [SX ldx*R][SY ldy*R][G 4R^2]
-  double* pg = part + g * part_ld;
-#pragma unroll
-  for (int s = 0; s < NS; ++s) {
-    const int px = tid + s * NT;
-#pragma unroll
-    for (int k = 0; k < R; ++k) {
-      if (vx[s]) *(double2*)(pg + (int64_t)k * ldx + 2 * px) = ax[s][k];
-      if (vy[s]) *(double2*)(pg + (int64_t)R * ldx + (int64_t)k * ldy + 2 * px) = ay[s][k];
-    }
-  }
-  if (has_g) {
-    double* G2 = pg + (int64_t)R * ldx + (int64_t)R * ldy;
-    G2[gj * 2 * R + gi] = gacc;
-    G2[gi * 2 * R + gj] = gacc;
-  }
-}
-
-// ============================================================================ fused sweep v3
-// Same ring and pipeline as above, but column ownership is split by matrix: threads [0, NT/2) own
-// NSH column pairs of X, threads [NT/2, NT) own NSH pairs of Y.  A wave's partial dots are then
+// ============================================================================ split sweep
+// One workgroup (NT threads, occupancy-sized grid) owns a contiguous block of rows.  Column
+// ownership is split by matrix: threads [0, NT/2) own NSH column pairs of X, threads [NT/2, NT)
+// own NSH pairs of Y, for the whole sweep, and keep W (or C) and the X'mu_T (or Y'mu_U)
+// accumulators for them in VGPRs.  Rows stream HBM -> LDS through a ring of SLOTS row slots filled
+// by LDS-DMA (global_load_lds_dwordx4; the first ceil(nch/CPW) waves copy CPW 1-KiB chunks of
+// every row, so the steady-state vmcnt is a compile-time immediate).  The loop handles RP rows
+// per step, software-pipelined, ONE workgroup barrier per step.  A wave's partial dots are then
 // Xw only or Yc only, so the per-row wave reduce-scatter handles R*RP values (not 2R*RP) and each
 // wave broadcasts only the mu it uses (mu_T for X waves, mu_U for Y waves).
 //   PIPE = true : step g computes group g+1's dots before group g's update (x of both in VGPRs)
@@ -855,94 +632,6 @@ __device__ __forceinline__ PplsVec16<T> ppls_load16(const T* p) {
 
 #define PPLS_PANEL_ROWS 64
 
-// Wt, Ct: W, C transposed to row-major [ld x R] (ppls_transpose_wc_kernel), so a column's R
-// weights are contiguous; they are read straight from L1/L2 (W is 8 p R bytes, resident) -- no LDS
-// staging and no barrier in the column loop, so the X loads of consecutive steps overlap.
-template <typename T, int R>
-__global__ __launch_bounds__(256) void ppls_panel_dots_kernel(
-    const T* __restrict__ X, const T* __restrict__ Y, int64_t n, int ldx, int ldy,
-    const double* __restrict__ Wt, const double* __restrict__ Ct, const PplsScalars* __restrict__ sc,
-    double* __restrict__ Z, double* __restrict__ mu) {
-  constexpr int VEC = PplsVec16<T>::N;
-  constexpr int RT = 4, CL = 16, ROWS = PPLS_PANEL_ROWS;   // 16 row groups x 4 rows
-  constexpr int KS = CL * VEC;                             // columns per step
-  constexpr int V4 = 4 * R;
-  __shared__ double sZ[ROWS * 2 * R];
-  __shared__ double sco[4 * R];
-  const int tid = threadIdx.x, cl = tid % CL, rg = tid / CL;
-  for (int e = tid; e < R; e += 256) {
-    sco[e] = sc->alpha[e];
-    sco[R + e] = sc->beta[e];
-    sco[2 * R + e] = sc->gamma[e];
-    sco[3 * R + e] = sc->delta[e];
-  }
-  for (int64_t tile = blockIdx.x; tile * ROWS < n; tile += gridDim.x) {
-    const int64_t rbase = tile * ROWS + rg * RT;
-    for (int mat = 0; mat < 2; ++mat) {
-      const T* M = mat ? Y : X;
-      const int ld = mat ? ldy : ldx;
-      const double* Wm = mat ? Ct : Wt;
-      const T* rows[RT];
-      bool ok[RT];
-#pragma unroll
-      for (int j = 0; j < RT; ++j) {
-        ok[j] = rbase + j < n;
-        rows[j] = M + (ok[j] ? rbase + j : 0) * ld;
-      }
-      double acc[RT][R];
-#pragma unroll
-      for (int j = 0; j < RT; ++j)
-#pragma unroll
-        for (int k = 0; k < R; ++k) acc[j][k] = 0.0;
-#pragma unroll 2
-      for (int c0 = cl * VEC; c0 < ld; c0 += KS) {   // ld is a multiple of VEC (zero padding)
-        PplsVec16<T> xv[RT];
-#pragma unroll
-        for (int j = 0; j < RT; ++j) xv[j] = ppls_load16(rows[j] + c0);
-#pragma unroll
-        for (int v = 0; v < VEC; ++v) {
-          const double* wr = Wm + (int64_t)(c0 + v) * R;
-          double w[R];
-#pragma unroll
-          for (int k = 0; k < R; ++k) w[k] = wr[k];
-#pragma unroll
-          for (int j = 0; j < RT; ++j) {
-            const double x = ok[j] ? (double)xv[j].v[v] : 0.0;
-#pragma unroll
-            for (int k = 0; k < R; ++k) acc[j][k] = fma(x, w[k], acc[j][k]);
-          }
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < RT; ++j)
-#pragma unroll
-        for (int k = 0; k < R; ++k) acc[j][k] = ppls_group16_sum(acc[j][k]);
-      if (cl == 0)
-#pragma unroll
-        for (int j = 0; j < RT; ++j)
-#pragma unroll
-          for (int k = 0; k < R; ++k) sZ[(rg * RT + j) * 2 * R + mat * R + k] = acc[j][k];
-    }
-    __syncthreads();
-    for (int e = tid; e < ROWS * V4; e += 256) {   // Z rows [a | b | mu_T | mu_U], coalesced
-      const int rr = e / V4, f = e - rr * V4;
-      const int64_t row = tile * ROWS + rr;
-      if (row >= n) continue;
-      double val;
-      if (f < 2 * R) {
-        val = sZ[rr * 2 * R + f];
-      } else {
-        const int k = (f - 2 * R) % R, u = f >= 3 * R;
-        const double a = sZ[rr * 2 * R + k], b = sZ[rr * 2 * R + R + k];
-        val = u ? sco[2 * R + k] * a + sco[3 * R + k] * b : sco[k] * a + sco[R + k] * b;
-        if (mu) mu[(int64_t)(u * R + k) * n + row] = val;
-      }
-      Z[row * V4 + f] = val;
-    }
-    __syncthreads();
-  }
-}
-
 // MFMA dots (default panel dots): Z_tile = X_tile (16 rows x K) . W (K x 16, R columns used) on
 // v_mfma_f64_16x16x4_f64.  Each wave owns 32 rows (two 16-row blocks sharing the B operand) and
 // walks the columns in 128-B tiles: a tile (32 rows x 128 B) is loaded with 16-B coalesced loads,
@@ -1033,152 +722,6 @@ __global__ __launch_bounds__(256) void ppls_panel_mfmadots_kernel(
       res[mat][1] = acc1;
     }
     if (i16 < R) {
-#pragma unroll
-      for (int blk = 0; blk < 2; ++blk)
-#pragma unroll
-        for (int reg = 0; reg < 4; ++reg) {
-          const int64_t row = row0 + 16 * blk + kq + 4 * reg;
-          if (row >= n) continue;
-          const double a = res[0][blk][reg], bb = res[1][blk][reg];
-          const double mt = al * a + be * bb, mu_u = ga * a + de * bb;
-          double* zr = Z + row * V4;
-          zr[i16] = a;
-          zr[R + i16] = bb;
-          zr[2 * R + i16] = mt;
-          zr[3 * R + i16] = mu_u;
-          if (mu) {
-            mu[(int64_t)i16 * n + row] = mt;
-            mu[(int64_t)(R + i16) * n + row] = mu_u;
-          }
-        }
-    }
-  }
-}
-
-// MFMA dots fed by a workgroup-synchronous LDS-DMA ring (the panel dots default).  The register
-// form above keeps only one tile in flight per wave: its B operand is a per-lane global load issued
-// after the next tile's loads, and VMEM completion is in order, so waiting for B waits for the
-// prefetch too.  Here a stage holds the four waves' row tiles (32 rows x 128 B each) AND the tile's
-// slab of W^T (or C^T), all copied HBM/L2 -> LDS by global_load_lds_dwordx4, so one in-order vmcnt
-// wait covers both and PPLS_DOTS_STAGES - 1 stages stay in flight.  The waves of a workgroup walk
-// the same column tiles (one barrier per tile) and share the slab.  Row tiles are unpadded (128-B
-// rows) with the 16-B chunks swizzled (chunk c of row r at slot c ^ ((r >> 1) & 5)), which makes
-// each 16-lane group of the A-operand ds_read_b128 hit 16 distinct 4-bank groups; the swizzle is
-// applied on the global side, since the DMA writes lane l's 16 B at m0 + 16 l.
-#define PPLS_DOTS_STAGES 4
-
-template <typename T, int R>
-constexpr int ppls_dots_stage_bytes() {
-  return 4 * 32 * 128 + ((128 / (int)sizeof(T)) * R * 8 + 1023) / 1024 * 1024;
-}
-
-template <typename T, int R>
-__global__ __launch_bounds__(256) void ppls_panel_dmadots_kernel(
-    const T* __restrict__ X, const T* __restrict__ Y, int64_t n, int ldx, int ldy,
-    const double* __restrict__ Wt, const double* __restrict__ Ct, const PplsScalars* __restrict__ sc,
-    double* __restrict__ Z, double* __restrict__ mu) {
-  typedef double d4 __attribute__((ext_vector_type(4)));
-  constexpr int ES = (int)sizeof(T);
-  constexpr int CW = 16 / ES;          // columns per 16-B chunk
-  constexpr int KT = 128 / ES;         // columns per tile
-  constexpr int KQ = KT / 4;           // MFMA steps per tile
-  constexpr int RB = 32;               // rows per wave
-  constexpr int D = PPLS_DOTS_STAGES;
-  constexpr int TB = RB * 128;         // one wave's row tile
-  constexpr int SB = KT * R * 8;       // the tile's W^T slab
-  constexpr int NSB = (SB + 1023) / 1024;
-  constexpr int STAGE = ppls_dots_stage_bytes<T, R>();
-  constexpr int V4 = 4 * R;
-  static_assert(R <= 16 && NSB <= 4, "one 16-wide MFMA tile; slab copied by at most 4 waves");
-  __shared__ __attribute__((aligned(1024))) char lds[D * STAGE];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int i16 = lane & 15, kq = lane >> 4;
-  const int lr = lane >> 3, slot = lane & 7;
-  const int comp = i16 < R ? i16 : 0;
-  const double al = sc->alpha[comp], be = sc->beta[comp], ga = sc->gamma[comp], de = sc->delta[comp];
-  const int ntcx = (ldx + KT - 1) / KT, ntcy = (ldy + KT - 1) / KT, nsb = ntcx + ntcy;
-  const int64_t nblk = (n + RB - 1) / RB;
-  const int64_t ngrp = (nblk + 3) / 4;    // groups of four row blocks, one per wave
-  const int64_t K = (int64_t)blockIdx.x < ngrp ? (ngrp - blockIdx.x + gridDim.x - 1) / gridDim.x : 0;
-  const int64_t S = K * nsb;              // steps (tiles) of every wave of this workgroup
-  const int nst = 4 + (wave < NSB ? 1 : 0);   // DMA instructions per stage issued by this wave
-  const uint32_t lds0 = (uint32_t)(uintptr_t)lds;
-
-  // prefetch iterator: step -> (group k, tile j)
-  int64_t pk = 0;
-  int pj = 0;
-  auto issue = [&](int64_t step) {
-    const bool isy = pj >= ntcx;
-    const int tc = isy ? pj - ntcx : pj;
-    const T* M = isy ? Y : X;
-    const int ld = isy ? ldy : ldx;
-    const int64_t t = ((int64_t)blockIdx.x + pk * gridDim.x) * 4 + wave;
-    const uint32_t st = lds0 + (uint32_t)(step % D) * STAGE;
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int rl = 8 * u + lr;
-      int64_t row = t * RB + rl;
-      if (row >= n) row = n - 1;
-      int c = tc * KT + (slot ^ ((rl >> 1) & 5)) * CW;
-      if (c >= ld) c = 0;
-      ppls_dma16(M + row * ld + c, __builtin_amdgcn_readfirstlane(st + wave * TB + u * 1024));
-    }
-    if (wave < NSB) {
-      const int off = wave * 1024 + 16 * lane;
-      const char* slab = (const char*)((isy ? Ct : Wt) + (int64_t)tc * KT * R);
-      ppls_dma16(slab + (off < SB ? off : 0), __builtin_amdgcn_readfirstlane(st + 4 * TB + wave * 1024));
-    }
-    if (++pj == nsb) { pj = 0; ++pk; }
-  };
-  for (int64_t s = 0; s < D - 1 && s < S; ++s) issue(s);
-
-  const int swz = (i16 >> 1) & 5;
-  int64_t step = 0;
-  for (int64_t k = 0; k < K; ++k) {
-    const int64_t row0 = (((int64_t)blockIdx.x + k * gridDim.x) * 4 + wave) * RB;
-    d4 res[2][2];
-#pragma unroll
-    for (int mat = 0; mat < 2; ++mat) {
-      d4 acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
-      const int ntc = mat ? ntcy : ntcx;
-      for (int tc = 0; tc < ntc; ++tc, ++step) {
-        // loads complete in order: once at most the later stages' copies are outstanding, this
-        // stage's have landed (Z stores in the count can only make the wait stricter)
-        const int64_t ahead = S - 1 - step;
-        ppls_wait_vmcnt(nst * (int)(ahead < D - 2 ? ahead : D - 2));
-        ppls_lds_barrier();   // every wave's copies of this stage have landed
-        if (step + D - 1 < S) issue(step + D - 1);   // into the stage everyone finished last step
-        const char* st = lds + (step % D) * STAGE;
-        const char* wt = st + wave * TB;
-        // A: rows i16, 16 + i16, columns [kq KQ, kq KQ + KQ) = chunks 2kq, 2kq+1
-        T a0[KQ], a1[KQ];
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int sl = (2 * kq + h) ^ swz;
-          const float4 v0 = *(const float4*)(wt + i16 * 128 + sl * 16);
-          const float4 v1 = *(const float4*)(wt + (16 + i16) * 128 + sl * 16);
-          const T* p0 = (const T*)&v0;
-          const T* p1 = (const T*)&v1;
-#pragma unroll
-          for (int u = 0; u < CW; ++u) {
-            a0[h * CW + u] = p0[u];
-            a1[h * CW + u] = p1[u];
-          }
-        }
-        const double* wb = (const double*)(st + 4 * TB) + kq * KQ * R + comp;
-        double b[KQ];
-#pragma unroll
-        for (int s2 = 0; s2 < KQ; ++s2) b[s2] = i16 < R ? wb[s2 * R] : 0.0;
-#pragma unroll
-        for (int s2 = 0; s2 < KQ; ++s2) {
-          acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64((double)a0[s2], b[s2], acc0, 0, 0, 0);
-          acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64((double)a1[s2], b[s2], acc1, 0, 0, 0);
-        }
-      }
-      res[mat][0] = acc0;
-      res[mat][1] = acc1;
-    }
-    if (i16 < R && row0 < n) {
 #pragma unroll
       for (int blk = 0; blk < 2; ++blk)
 #pragma unroll
@@ -1437,9 +980,10 @@ __device__ __noinline__ void ppls_block_polar(const double* S, int64_t lds, int 
     __syncthreads();
   }
   if (tid == 0) {
-    if (qr) {
+    if (qr) {   // orth(type = "QR") = sign_e * qr.Q(qr(S)), sign_e = sign(<e_1, S_1>) = sign(R_11)
+      const double sg = Rm[0] < 0.0 ? -1.0 : 1.0;   // (Package/functions.R:257-259)
       for (int j = 0; j < r; ++j)
-        for (int i = 0; i < r; ++i) P[j * r + i] = (i == j) ? 1.0 : 0.0;
+        for (int i = 0; i < r; ++i) P[j * r + i] = (i == j) ? sg : 0.0;
     } else if (ppls_small_polar_ws<PPLS_RMAX>(Rm, r, P, jw, jw + r * r) != 0) {
       *status = -3;
     }
@@ -1915,6 +1459,17 @@ __device__ bool ppls_block_polar_fast(const double* __restrict__ S, int64_t lds,
       if (vstate) vstate[b * R + a] = sV[b * G + a];
     }
     good = __shfl(good ? 1 : 0, 0, 64) != 0 && good;   // lane 0 holds the chol2 verdict for small R
+    // Cholesky-QR2 yields an orthonormal factor only while Q1 = S R1^-1 is nearly orthonormal
+    // (||Q1'Q1 - I|| ~ eps kappa(S)^2 small, kappa(S) <~ 1e7): otherwise the Householder fallback
+    {
+      bool orth_ok = true;
+#pragma unroll
+      for (int b = 0; b < R; ++b)
+#pragma unroll
+        for (int a2 = 0; a2 <= b; ++a2)
+          orth_ok = orth_ok && fabs(vals[b * (b + 1) / 2 + a2] - (a2 == b ? 1.0 : 0.0)) <= 0.1;
+      good = good && orth_ok;
+    }
     if (lane == 0) ok = ok && good;
   }
   __syncthreads();
@@ -2234,20 +1789,36 @@ __global__ void ppls_loglc_kernel(const double* __restrict__ G, const double* __
 namespace {
 #define PPLS_FIN_STAGE_MAX (136 * 1024)   // dynamic LDS for staging S (static use is < 8 KB)
 
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per (kernel, device, size): contexts on
+// different devices or host threads each get the attribute set on their own current device.
+hipError_t set_dyn_lds(const void* kern, int bytes) {
+  static std::mutex mu;
+  static std::set<std::tuple<const void*, int, int>> done;
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  std::lock_guard<std::mutex> g(mu);
+  const auto key = std::make_tuple(kern, dev, bytes);
+  if (done.count(key)) return hipSuccess;
+  e = hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+  if (e == hipSuccess) done.insert(key);
+  return e;
+}
+
 template <int R>
 hipError_t launch_finalize_t(const PplsFinalizeArgs* f, hipStream_t st) {
   auto kern = ppls_finalize_kernel<R>;
-  static size_t dyn_max = 0;   // dynamic LDS left next to the kernel's static LDS (160 KB per WG)
-  static bool attr_set = false;
-  if (!attr_set) {
+  // dynamic LDS left next to the kernel's static LDS (160 KB per WG); thread-safe static init
+  static const size_t dyn_max = []() -> size_t {
     hipFuncAttributes fa;
-    hipError_t e = hipFuncGetAttributes(&fa, (const void*)kern);
-    if (e != hipSuccess) return e;
+    if (hipFuncGetAttributes(&fa, (const void*)ppls_finalize_kernel<R>) != hipSuccess) return 0;
     const size_t budget = 160 * 1024 - fa.sharedSizeBytes - 1024;
-    dyn_max = budget < PPLS_FIN_STAGE_MAX ? budget : PPLS_FIN_STAGE_MAX;
-    e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn_max);
+    return budget < PPLS_FIN_STAGE_MAX ? budget : PPLS_FIN_STAGE_MAX;
+  }();
+  if (dyn_max == 0) return hipErrorInvalidDeviceFunction;
+  {
+    const hipError_t e = set_dyn_lds((const void*)kern, (int)dyn_max);
     if (e != hipSuccess) return e;
-    attr_set = true;
   }
   const size_t stage = (size_t)R * (f->p > f->q ? f->p : f->q) * sizeof(double);
   const int use = stage <= dyn_max && !f->qr;
@@ -2259,39 +1830,6 @@ hipError_t launch_finalize_t(const PplsFinalizeArgs* f, hipStream_t st) {
 }
 
 
-size_t fused_lds(int r, int ldx, int ldy, int threads, int rp) {
-  const int nch = ((ldx * 8 + 1023) >> 10) + ((ldy * 8 + 1023) >> 10);
-  const int v = 2 * r * rp, nw = threads / 64;
-  return (size_t)PPLS_SWEEP_SLOTS * (nch << 10) + (size_t)(3 * nw * v + 4 * r) * 8;
-}
-
-template <int R, int NS, int NT, int RP, int CPW>
-hipError_t launch_fused_t(const PplsSweepArgs& a, hipStream_t st) {
-  auto kern = ppls_sweep_fused_kernel<R, NS, NT, RP, PPLS_SWEEP_SLOTS, CPW>;
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       160 * 1024);
-    if (e != hipSuccess) return e;
-    attr_set = true;
-  }
-  hipLaunchKernelGGL(kern, dim3(a.grid), dim3(NT), fused_lds(R, a.ldx, a.ldy, NT, RP), st, a.X, a.Y,
-                     a.n_local, a.ldx, a.ldy, a.Wp, a.Cp, a.sc, a.part, a.part_ld, a.mu, a.write_mu,
-                     a.ablate);
-  return hipGetLastError();
-}
-
-template <int R, int NS, int NT, int RP>
-hipError_t launch_fused_cpw(const PplsSweepArgs& a, hipStream_t st) {
-  const int nch = ((a.ldx * 8 + 1023) >> 10) + ((a.ldy * 8 + 1023) >> 10);
-  const int need = (nch + NT / 64 - 1) / (NT / 64);   // chunks per wave with every wave copying
-  if (need <= 2) return launch_fused_t<R, NS, NT, RP, 2>(a, st);
-  if (need <= 4) return launch_fused_t<R, NS, NT, RP, 4>(a, st);
-  return hipErrorInvalidValue;   // cannot happen: nch <= 16 * NS (ppls_fused_supported)
-}
-
-// Only the (R, NS, NT, RP) combinations ppls_fused_supported admits are instantiated (the others
-// would not fit in 256 VGPRs).
 size_t split_lds(int r, int ldx, int ldy, int threads, int rp) {
   const int nch = ((ldx * 8 + 1023) >> 10) + ((ldy * 8 + 1023) >> 10);
   const int v = r * rp, nw = threads / 64;
@@ -2301,12 +1839,9 @@ size_t split_lds(int r, int ldx, int ldy, int threads, int rp) {
 template <int R, int NSH, int RP, bool PIPE, int CPW>
 hipError_t launch_split_t(const PplsSweepArgs& a, hipStream_t st) {
   auto kern = ppls_sweep_split_kernel<R, NSH, 512, RP, PIPE, PPLS_SWEEP_SLOTS, CPW>;
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       160 * 1024);
+  {
+    const hipError_t e = set_dyn_lds((const void*)kern, 160 * 1024);
     if (e != hipSuccess) return e;
-    attr_set = true;
   }
   if (a.occ_out) {   // query: resident workgroups per CU for this instantiation and shape
     int nb = 0;
@@ -2354,46 +1889,9 @@ hipError_t launch_split_r(const PplsSweepArgs& a, hipStream_t st) {
   return hipErrorInvalidValue;
 }
 
-template <int R>
-hipError_t launch_fused_r(const PplsSweepArgs& a, hipStream_t st) {
-  if (a.threads == 1024) {
-    if constexpr (R <= 3) {
-      if (a.ns == 1) return launch_fused_cpw<R, 1, 1024, 1>(a, st);
-    }
-    return hipErrorInvalidValue;
-  }
-  if constexpr (R <= 4) {
-    if (a.rp == 2 && a.ns == 1) return launch_fused_cpw<R, 1, 512, 2>(a, st);
-  }
-  if (a.ns == 1) return launch_fused_cpw<R, 1, 512, 1>(a, st);
-  if constexpr (2 * R <= 10) {
-    if (a.ns == 2) return launch_fused_cpw<R, 2, 512, 1>(a, st);
-  }
-  return hipErrorInvalidValue;
-}
 }  // namespace
 
 extern "C" {
-
-int ppls_fused_supported(int r, int ldx, int ldy, int threads) {
-  const int npmax = (ldx > ldy ? ldx : ldy) / 2;
-  const int ns = (npmax + threads - 1) / threads;
-  if (r < 1 || r > PPLS_FUSED_RMAX) return 0;
-  if (threads == 1024) {
-    if (ns != 1 || r > 3) return 0;   // 4 waves/SIMD: W, C, accumulators in <= 128 VGPRs
-  } else if (threads == 512) {
-    if (ns < 1 || ns > 2 || ns * r > 10) return 0;   // W, C and accumulators stay in VGPRs
-  } else {
-    return 0;
-  }
-  const int nch = ((ldx * 8 + 1023) >> 10) + ((ldy * 8 + 1023) >> 10);
-  if (nch > 4 * (threads / 64)) return 0;   // at most 4 DMA chunks per wave per row
-  return ppls_fused_lds_bytes(r, ldx, ldy, threads) <= 160 * 1024 ? ns : 0;
-}
-
-size_t ppls_fused_lds_bytes(int r, int ldx, int ldy, int threads) {
-  return fused_lds(r, ldx, ldy, threads, 2);
-}
 
 int ppls_split_supported(int r, int ldx, int ldy) {
   const int npmax = (ldx > ldy ? ldx : ldy) / 2;
@@ -2406,6 +1904,21 @@ int ppls_split_supported(int r, int ldx, int ldy) {
   return split_lds(r, ldx, ldy, 512, 2) <= 160 * 1024 ? ns : 0;
 }
 
+// The split instantiation ppls_launch_sweep_split picks for *a (mirrors launch_split_r and
+// launch_split_cpw): "split<R,NSH,NT,RP,PIPE,SLOTS,CPW>".  Returns 0, or -1 if none fits.
+int ppls_split_describe(const PplsSweepArgs* a, char* buf, int len) {
+  const int R = a->r;
+  int nsh = 0, rp = 1, pipe = 1;
+  if (a->ns <= 1) { nsh = 1; rp = a->rp != 1 ? 2 : 1; }
+  else if (a->ns == 2) { nsh = 2; rp = (R <= 6 && a->rp != 1) ? 2 : 1; }
+  else if (a->ns <= 4 && R <= 5) { nsh = 4; rp = a->rp != 1 ? 2 : 1; pipe = a->rp != 1 ? 0 : (a->pipe ? 1 : 0); }
+  const int nch = ((a->ldx * 8 + 1023) >> 10) + ((a->ldy * 8 + 1023) >> 10);
+  const int need = (nch + 7) / 8, cpw = need <= 2 ? 2 : need <= 4 ? 4 : 0;
+  if (!nsh || !cpw || R < 1 || R > PPLS_FUSED_RMAX) return -1;
+  snprintf(buf, (size_t)len, "split<%d,%d,512,%d,%s,%d,%d>", R, nsh, rp, pipe ? "true" : "false", PPLS_SWEEP_SLOTS, cpw);
+  return 0;
+}
+
 hipError_t ppls_launch_sweep_split(const PplsSweepArgs* a, hipStream_t st) {
   switch (a->r) {
     case 1: return launch_split_r<1>(*a, st);
@@ -2416,20 +1929,6 @@ hipError_t ppls_launch_sweep_split(const PplsSweepArgs* a, hipStream_t st) {
     case 6: return launch_split_r<6>(*a, st);
     case 7: return launch_split_r<7>(*a, st);
     case 8: return launch_split_r<8>(*a, st);
-    default: return hipErrorInvalidValue;
-  }
-}
-
-hipError_t ppls_launch_sweep_fused(const PplsSweepArgs* a, hipStream_t st) {
-  switch (a->r) {
-    case 1: return launch_fused_r<1>(*a, st);
-    case 2: return launch_fused_r<2>(*a, st);
-    case 3: return launch_fused_r<3>(*a, st);
-    case 4: return launch_fused_r<4>(*a, st);
-    case 5: return launch_fused_r<5>(*a, st);
-    case 6: return launch_fused_r<6>(*a, st);
-    case 7: return launch_fused_r<7>(*a, st);
-    case 8: return launch_fused_r<8>(*a, st);
     default: return hipErrorInvalidValue;
   }
 }
@@ -2462,113 +1961,9 @@ hipError_t ppls_launch_accumulate(const PplsSweepArgs* a, const double* Z, hipSt
 
 // ---- panel sweep launchers
 }  // extern "C"
-// MFMA accumulation (experimental panel acc, see the launcher): S = X' mu over a row chunk on v_mfma_f64_16x16x4_f64,
-// A = X' (16 columns x 4 rows), B = mu (4 rows x 16 components, R used).  Each wave owns 64
-// columns as 4 MFMA blocks with the column assignment permuted (block b, A-row i <-> column
-// 4 i + b), so one lane's 4 consecutive columns of a row -- one 16-B (fp32) or two 16-B (fp64)
-// coalesced loads -- are its A operands for all 4 blocks; the B operand (lane l: mu[row l >> 4]
-// [component l & 15]) is shared by the blocks.  Result (f64 MFMA lane map): column
-// 4 ((l >> 4) + 4 reg) + b, component l & 15.  Gram of [Xw Yc] as in ppls_panel_acc_kernel.
-template <typename T, int R>
-__global__ __launch_bounds__(256) void ppls_panel_mfmaacc_kernel(
-    const T* __restrict__ X, const T* __restrict__ Y, int64_t n, int ldx, int ldy,
-    const double* __restrict__ Z, int64_t rows_per_chunk, double* __restrict__ part, int64_t part_ld) {
-  typedef double d4 __attribute__((ext_vector_type(4)));
-  constexpr int V4 = 4 * R;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int i16 = lane & 15, kq = lane >> 4;
-  const int ntx = (ldx + 255) / 256;   // 256 columns per workgroup
-  const bool isx = (int)blockIdx.x < ntx;
-  const int ld = isx ? ldx : ldy;
-  const int cbase = (isx ? blockIdx.x : blockIdx.x - ntx) * 256 + wave * 64;
-  const int mycol = cbase + 4 * i16;   // this lane's 4 columns
-  const T* M = isx ? X : Y;
-  const int off = isx ? 2 * R : 3 * R;
-  const int64_t r0 = (int64_t)blockIdx.y * rows_per_chunk;
-  const int64_t r1 = min(n, r0 + rows_per_chunk);
-  double* pg = part + (int64_t)blockIdx.y * part_ld;
-  const bool colok = mycol < ld;   // ld is a multiple of 4 (fp32) / 2 (fp64): whole vectors
-  const bool colok2 = mycol + 2 < ld;
-  d4 acc[4];
-#pragma unroll
-  for (int b = 0; b < 4; ++b) acc[b] = (d4){0.0, 0.0, 0.0, 0.0};
-  if (cbase < ld) {
-    const T* base = M + mycol;
-    auto ldx4 = [&](int64_t row, double (&v)[4]) {
-      if (sizeof(T) == 4) {
-        const float4 f = (colok && row < r1) ? *(const float4*)(base + row * ld) : make_float4(0.f, 0.f, 0.f, 0.f);
-        v[0] = f.x; v[1] = f.y; v[2] = f.z; v[3] = f.w;
-      } else {
-        const double2 d0 = (colok && row < r1) ? *(const double2*)(base + row * ld) : make_double2(0.0, 0.0);
-        const double2 d1 = (colok2 && row < r1) ? *(const double2*)(base + row * ld + 2) : make_double2(0.0, 0.0);
-        v[0] = d0.x; v[1] = d0.y; v[2] = d1.x; v[3] = d1.y;
-      }
-    };
-    for (int64_t rb = r0; rb < r1; rb += 16) {   // 4 MFMA steps of 4 rows, loads issued together
-      double xv[4][4], mv[4];
-#pragma unroll
-      for (int st = 0; st < 4; ++st) {
-        const int64_t row = rb + 4 * st + kq;
-        ldx4(row, xv[st]);
-        mv[st] = (i16 < R && row < r1) ? Z[row * V4 + off + i16] : 0.0;
-      }
-#pragma unroll
-      for (int st = 0; st < 4; ++st)
-#pragma unroll
-        for (int b = 0; b < 4; ++b)
-          acc[b] = __builtin_amdgcn_mfma_f64_16x16x4f64(xv[st][b], mv[st], acc[b], 0, 0, 0);
-    }
-    if (i16 < R) {
-      double* dst = (isx ? pg : pg + (int64_t)R * ldx) + (int64_t)i16 * ld;
-#pragma unroll
-      for (int b = 0; b < 4; ++b)
-#pragma unroll
-        for (int reg = 0; reg < 4; ++reg) {
-          const int col = cbase + 4 * (kq + 4 * reg) + b;
-          if (col < ld) dst[col] = acc[b][reg];
-        }
-    }
-  }
-  if (blockIdx.x == 0) {   // Gram of [Xw Yc] over the chunk (2R x 2R, column-major)
-    constexpr int V2 = 2 * R, NP = V2 * (V2 + 1) / 2, BR = 64;
-    __shared__ double sz[BR * V2];
-    double* G2 = pg + (int64_t)R * ldx + (int64_t)R * ldy;
-    double gs[(NP + 255) / 256];
-    int pi[(NP + 255) / 256], pj[(NP + 255) / 256];
-#pragma unroll
-    for (int u = 0; u < (NP + 255) / 256; ++u) {
-      gs[u] = 0.0;
-      int e = tid + 256 * u, i = 0;
-      while (e >= V2 - i && i < V2) { e -= V2 - i; ++i; }
-      pi[u] = i;
-      pj[u] = i + e;
-    }
-    for (int64_t b0 = r0; b0 < r1; b0 += BR) {
-      __syncthreads();
-      for (int e = tid; e < BR * V2; e += 256) {
-        const int rr = e / V2, f = e - rr * V2;
-        sz[e] = (b0 + rr < r1) ? Z[(b0 + rr) * V4 + f] : 0.0;
-      }
-      __syncthreads();
-#pragma unroll
-      for (int u = 0; u < (NP + 255) / 256; ++u)
-        if (tid + 256 * u < NP)
-          for (int rr = 0; rr < BR; ++rr) gs[u] = fma(sz[rr * V2 + pi[u]], sz[rr * V2 + pj[u]], gs[u]);
-    }
-#pragma unroll
-    for (int u = 0; u < (NP + 255) / 256; ++u)
-      if (tid + 256 * u < NP) {
-        G2[pj[u] * V2 + pi[u]] = gs[u];
-        G2[pi[u] * V2 + pj[u]] = gs[u];
-      }
-  }
-}
-
 namespace {
 template <typename T, int R>
 hipError_t launch_panel_t(const PplsSweepArgs* a, const T* X, const T* Y, double* Z, int chunks, hipStream_t st) {
-  const int64_t tiles = (a->n_local + PPLS_PANEL_ROWS - 1) / PPLS_PANEL_ROWS;
-  const int blocks = (int)(tiles < 8192 ? tiles : 8192);
   // transposed W, C behind Z (see ppls_panel_z_len), rows padded to whole 32-column tiles
   const int ldxp = (a->ldx + 31) & ~31, ldyp = (a->ldy + 31) & ~31;
   double* Wt = Z + a->n_local * 4 * R;
@@ -2576,39 +1971,20 @@ hipError_t launch_panel_t(const PplsSweepArgs* a, const T* X, const T* Y, double
   const int64_t ne = (int64_t)(ldxp + ldyp) * R;
   hipLaunchKernelGGL(ppls_transpose_wc_kernel, dim3((unsigned)((ne + 255) / 256)), dim3(256), 0, st, a->Wp,
                      a->Cp, a->ldx, a->ldy, ldxp, ldyp, R, Wt, Ct);
-  // measured at the C5 shape (tools/panel_experiment.py): tiled dots is faster for fp64 storage
-  // (8.6 vs 13.1 ms), row-per-lane dots for fp32 storage (6.7 vs 7.5 ms); ablate bit 5 flips it
-  const int dots = (a->ablate >> 5) & 1;   // 0 MFMA (default), 1 tiled VALU (experiments)
-  if (dots == 0 && (a->ablate & 512)) {   // LDS-DMA ring dots (opt-in until measured)
-    const int64_t ngrp = ((a->n_local + 31) / 32 + 3) / 4;
-    int64_t g = a->dots_grid > 0 ? a->dots_grid : (ngrp < 16384 ? ngrp : 16384);
-    if (g > ngrp) g = ngrp;
-    hipLaunchKernelGGL((ppls_panel_dmadots_kernel<T, R>), dim3((unsigned)g), dim3(256), 0, st, X, Y,
-                       a->n_local, a->ldx, a->ldy, Wt, Ct, a->sc, Z, a->write_mu ? a->mu : nullptr);
-  } else if (dots == 0) {   // register-staged MFMA dots (ablate bit 9, experiments)
+  {   // MFMA dots (profiles/r1_c5_*_dots_variants.txt: faster than the VALU and LDS-DMA forms)
     const int64_t wtiles = (a->n_local + 31) / 32;
     const int mblocks = (int)((wtiles + 3) / 4 < 16384 ? (wtiles + 3) / 4 : 16384);
     hipLaunchKernelGGL((ppls_panel_mfmadots_kernel<T, R>), dim3(mblocks), dim3(256), 0, st, X, Y,
                        a->n_local, a->ldx, a->ldy, Wt, Ct, a->sc, Z, a->write_mu ? a->mu : nullptr);
-  } else if (dots == 1) {
-    hipLaunchKernelGGL((ppls_panel_dots_kernel<T, R>), dim3(blocks), dim3(256), 0, st, X, Y, a->n_local,
-                       a->ldx, a->ldy, Wt, Ct, a->sc, Z, a->write_mu ? a->mu : nullptr);
   }
   constexpr int VEC = PplsVec16<T>::N;
   if (a->ablate & 256) return hipGetLastError();   // dots only (scores)
   const int64_t rpc = (a->n_local + chunks - 1) / chunks;
-  // VALU accumulation is the default: measured at C5 (profiles/r1_c5_*_acc_variants.txt) the MFMA
-  // form is no faster in fp64 storage (7.7 vs 7.5 ms) and slower in fp32 (6.0 vs 4.5 ms), since the
-  // pass is bound by its load stream, not by FMA issue; ablate bit 7 selects the MFMA form
-  if (!(a->ablate & 128)) {
-    const int ntx = (a->ldx + 256 * VEC - 1) / (256 * VEC), nty = (a->ldy + 256 * VEC - 1) / (256 * VEC);
-    hipLaunchKernelGGL((ppls_panel_acc_kernel<T, R>), dim3(ntx + nty, chunks), dim3(256), 0, st, X, Y,
-                       a->n_local, a->ldx, a->ldy, Z, rpc, a->part, a->part_ld);
-  } else {
-    const int ntx = (a->ldx + 255) / 256, nty = (a->ldy + 255) / 256;
-    hipLaunchKernelGGL((ppls_panel_mfmaacc_kernel<T, R>), dim3(ntx + nty, chunks), dim3(256), 0, st, X, Y,
-                       a->n_local, a->ldx, a->ldy, Z, rpc, a->part, a->part_ld);
-  }
+  // VALU accumulation: at C5 an MFMA form measured no faster in fp64 storage (7.7 vs 7.5 ms) and
+  // slower in fp32 (6.0 vs 4.5 ms; profiles/r1_c5_*_acc_variants.txt) -- the pass is load-bound
+  const int ntx = (a->ldx + 256 * VEC - 1) / (256 * VEC), nty = (a->ldy + 256 * VEC - 1) / (256 * VEC);
+  hipLaunchKernelGGL((ppls_panel_acc_kernel<T, R>), dim3(ntx + nty, chunks), dim3(256), 0, st, X, Y,
+                     a->n_local, a->ldx, a->ldy, Z, rpc, a->part, a->part_ld);
   return hipGetLastError();
 }
 

@@ -24,7 +24,10 @@ CASES = [
     ("r5_n300_p41_q37", 300, 41, 37, 5, 8, float("-inf"), "SVD", 3),
     ("qr_n200_p24_q18_r3", 200, 24, 18, 3, 6, float("-inf"), "QR", 4),
     ("atol_n250_p20_q16_r2", 250, 20, 16, 2, 300, 5e-3, "SVD", 5),
+    # stress variant of the simulation study's noise level sigE = sigF = 0.05 (Package/EM_Cpp.R:26-28)
+    ("stress_sig005_n300_p40_q30_r3", 300, 40, 30, 3, 12, float("-inf"), "SVD", 6),
 ]
+PROBLEM_KW = {"stress_sig005_n300_p40_q30_r3": dict(sigE=0.05, sigF=0.05, sigH=0.05)}
 
 
 # sequential initialiser PPLS(X, Y, a, EMsteps, atol, initialGuess) and the PPLS_simult run it seeds
@@ -113,10 +116,16 @@ def main():
     if "--meta" in sys.argv:   # only the meta_* fixtures (the others are unchanged)
         meta_fixtures(here)
         return
-    meta_fixtures(here)
-    seq_fixtures(here)
+    only = None
+    if "--cases" in sys.argv:   # only these PPLS_simult fixtures, e.g. --cases qr_n200_p24_q18_r3,...
+        only = set(sys.argv[sys.argv.index("--cases") + 1].split(","))
+    else:
+        meta_fixtures(here)
+        seq_fixtures(here)
     for name, n, p, q, r, steps, atol, typ, seed in CASES:
-        X, Y, th0 = make_problem(n, p, q, r, seed=seed)
+        if only is not None and name not in only:
+            continue
+        X, Y, th0 = make_problem(n, p, q, r, seed=seed, **PROBLEM_KW.get(name, {}))
         res = o.ppls_simult(X, Y, r, EMsteps=steps, atol=atol, type=typ, theta0=th0)
         one = o.ppls_simult(X, Y, r, EMsteps=1, atol=atol, type=typ, theta0=th0)
         two = o.ppls_simult(X, Y, r, EMsteps=2, atol=atol, type=typ, theta0=th0)

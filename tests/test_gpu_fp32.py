@@ -44,6 +44,8 @@ def test_fp32_storage_em_matches_oracle_on_rounded_data(p, q, r):
         c.set_data(X, Y)
         Xb, Yb = c.get_data()
         assert np.array_equal(Xb, X32) and np.array_equal(Yb, Y32)
+        Xr, Yr = c.get_data_rows(5, 300)
+        assert np.array_equal(Xr, X32[5:305]) and np.array_equal(Yr, Y32[5:305])
         sx, sy = c.ssq()
         assert np.isclose(sx, np.sum(X32 * X32), rtol=1e-13)
         est, ll, _, _ = c.em_run(_theta(th0), 6, -np.inf, 0, want_eout=False)

@@ -1,0 +1,210 @@
+"""The N > 1 data-parallel path through the library itself (device sweeps, library reductions).
+
+Rows are sharded over ranks (EM_W_multi.R:689-712 and :732-733 are sums over rows), each rank's
+context sweeps its own rows and every collective of the library -- the per-iteration
+[X'mu_T | Y'mu_U | Gram] statistics, ||X||^2 and ||Y||^2, the initialiser's and meta_*'s sums --
+goes through ppls_set_reducer, the host-side reduction hook:
+
+* k contexts on GPU 0 in one process, one host thread per rank, summing in rank order: the sharded
+  fit must equal the unsharded fit (1e-12) and every rank must hold bit-identical estimates;
+* two processes on GPU 0 with torch.distributed gloo as the reducer (the RCCL path's structure
+  with gloo doing the all-reduce), checked against the CPU oracle.
+"""
+import os
+import socket
+import threading
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, make_problem
+from oracle import ppls_oracle as o
+
+pytestmark = pytest.mark.gpu
+
+
+class ThreadAllReduce:
+    """Sum over k host threads, in rank order (so every rank gets the bitwise-same result)."""
+
+    def __init__(self, k):
+        self.k = k
+        self.bar = threading.Barrier(k, timeout=120)
+        self.bufs = [None] * k
+        self.calls = 0
+
+    def fn(self, rank):
+        def reduce(buf):
+            self.bufs[rank] = buf.copy()
+            self.bar.wait()
+            tot = self.bufs[0].copy()
+            for b in self.bufs[1:]:
+                tot += b
+            self.bar.wait()   # everyone has read the inputs before the next call overwrites them
+            if rank == 0:
+                self.calls += 1
+            buf[:] = tot
+        return reduce
+
+
+def _run_ranks(k, work):
+    """work(rank, ctx) on k threads, each with its own context on GPU 0; returns the results."""
+    from ppls_amd import Context
+    red = ThreadAllReduce(k)
+    out, errs = [None] * k, []
+
+    def body(rank):
+        try:
+            with Context(0) as c:
+                c.set_reducer(red.fn(rank))
+                out[rank] = work(rank, c)
+        except BaseException as e:   # noqa: BLE001
+            errs.append(e)
+            red.bar.abort()
+
+    ths = [threading.Thread(target=body, args=(i,)) for i in range(k)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join(timeout=300)
+    if errs:
+        raise errs[0]
+    assert red.calls > 0
+    return out
+
+
+def _theta(th):
+    from ppls_amd import Theta
+    return Theta(th["W"], th["C"], th["B"], th["sigE"], th["sigF"], th["sigH"], th["sigT"])
+
+
+@pytest.mark.parametrize("k,n,p,q,r,dtype", [(3, 3001, 300, 200, 4, 0), (4, 2000, 700, 90, 10, 0),
+                                             (2, 1500, 260, 130, 3, 1)],
+                         ids=["split_k3", "panel_k4", "panel_fp32_k2"])
+def test_k_contexts_sharded_equal_unsharded(k, n, p, q, r, dtype):
+    from ppls_amd import Context
+    X, Y, th0 = make_problem(n, p, q, r, seed=n + k)
+    steps = 6
+
+    def fit(c, Xs, Ys, n_total):
+        c.set_option("dtype", dtype)
+        c.set_data(Xs, Ys, n_total=n_total)
+        est, ll, eout, _ = c.em_run(_theta(th0), steps, -np.inf, 0)
+        return est, ll, eout, c.sweep_info(r)["variant"]
+
+    with Context(0) as c:
+        ref = fit(c, X, Y, None)
+
+    def work(rank, c):
+        r0, nl = Context.shard_range(n, k, rank)
+        return fit(c, X[r0:r0 + nl], Y[r0:r0 + nl], n)
+
+    res = _run_ranks(k, work)
+    assert res[0][3] == ref[3] == ("split512" if (r <= 8 and not dtype and p <= 2048) else "panel")
+    for est, ll, eout, _ in res:
+        assert np.array_equal(est.W, res[0][0].W) and np.array_equal(est.C, res[0][0].C)
+        assert np.array_equal(ll, res[0][1])
+        assert np.array_equal(eout.Ctt, res[0][2].Ctt) and eout.Cee == res[0][2].Cee
+    est, ll, eout, _ = res[0]
+    assert np.abs(ll - ref[1]).max() / np.abs(ref[1]).max() < 1e-12
+    assert np.abs(est.W - ref[0].W).max() < 1e-12 and np.abs(est.C - ref[0].C).max() < 1e-12
+    assert np.abs(est.B - ref[0].B).max() / np.abs(ref[0].B).max() < 1e-12
+    assert abs(est.sigE - ref[0].sigE) / ref[0].sigE < 1e-12
+    # Eout rows stay sharded: the concatenation is the unsharded mu_T
+    mu = np.vstack([e.mu_T for _, _, e, _ in res])
+    assert np.abs(mu - ref[2].mu_T).max() / np.abs(ref[2].mu_T).max() < 1e-12
+
+
+def test_k_contexts_initialiser_and_meta_sharded():
+    """PPLS (sequential initialiser) and meta_PPLSi on 3 row shards equal the unsharded fits."""
+    from ppls_amd import Context
+    from ppls_amd.api import initial_guess
+    k, n, p, q, a = 3, 900, 60, 40, 2
+    X, Y, _ = make_problem(n, p, q, a, seed=5)
+    inits = [initial_guess(p, q, "equal") for _ in range(a)]
+    sizes = [400, 200, 300]
+    init = initial_guess(p, q, "equal")
+
+    def fits(c):
+        f = c.ppls(a, 20, 1e-4, inits)
+        m = c.meta_ppls(sizes, 30, 1e-6, init)
+        return f, m
+
+    with Context(0) as c:
+        c.set_data(X, Y)
+        ref = fits(c)
+
+    def work(rank, c):
+        r0, nl = Context.shard_range(n, k, rank)
+        c.set_data(X[r0:r0 + nl], Y[r0:r0 + nl], n_total=n)
+        c.row0 = r0
+        return fits(c)
+
+    res = _run_ranks(k, work)
+    for f, m in res:
+        assert np.array_equal(f["W"], res[0][0]["W"]) and np.array_equal(m[0], res[0][1][0])
+    f, m = res[0]
+    assert np.abs(f["W"] - ref[0]["W"]).max() < 1e-12 and np.abs(f["C"] - ref[0]["C"]).max() < 1e-12
+    assert np.abs(f["sig"] - ref[0]["sig"]).max() < 1e-12
+    assert np.abs(m[0] - ref[1][0]).max() < 1e-12 and np.abs(m[2] - ref[1][2]).max() < 1e-11
+    assert np.allclose(m[3], ref[1][3], rtol=1e-12, atol=0, equal_nan=True)
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _gloo_worker(rank, world, port, steps, q_out):
+    import sys
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import torch
+    import torch.distributed as dist
+    from conftest import make_problem as mk
+    from ppls_amd import Context, Theta
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        X, Y, th0 = mk(2501, 120, 80, 3, seed=321)
+        r0, nl = Context.shard_range(X.shape[0], world, rank)
+
+        def allreduce(buf):
+            dist.all_reduce(torch.from_numpy(buf))   # in place on the library's host staging buffer
+
+        with Context(0) as c:
+            c.set_reducer(allreduce)
+            c.set_data(X[r0:r0 + nl], Y[r0:r0 + nl], n_total=X.shape[0])
+            th = Theta(th0["W"], th0["C"], th0["B"], th0["sigE"], th0["sigF"], th0["sigH"], th0["sigT"])
+            est, ll, eout, _ = c.em_run(th, steps, -np.inf, 0)
+            q_out.put((rank, est.W, est.C, est.B, est.sigT, (est.sigE, est.sigF, est.sigH), ll, eout.mu_T))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_two_processes_device_sweep():
+    import torch.multiprocessing as mp
+    world, steps = 2, 8
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gloo_worker, args=(rk, world, port, steps, q)) for rk in range(world)]
+    for pr in procs:
+        pr.start()
+    try:
+        res = sorted([q.get(timeout=240) for _ in range(world)], key=lambda t: t[0])
+    finally:
+        for pr in procs:
+            pr.join(timeout=60)
+    assert all(pr.exitcode == 0 for pr in procs)
+    for other in res[1:]:   # identical finalize on identical reduced statistics
+        for a, b in zip(res[0][1:7], other[1:7]):
+            assert np.array_equal(np.asarray(a), np.asarray(b))
+    X, Y, th0 = make_problem(2501, 120, 80, 3, seed=321)
+    ref = o.ppls_simult(X, Y, 3, EMsteps=steps, atol=-np.inf, theta0=th0)
+    e = ref["estimates"]
+    assert np.abs(res[0][6] - ref["loglik"]).max() / np.abs(ref["loglik"]).max() < 1e-10
+    assert np.abs(res[0][1] - e["W"]).max() < 1e-8 and np.abs(res[0][2] - e["C"]).max() < 1e-8
+    mu = np.vstack([res[0][7], res[1][7]])
+    assert np.abs(mu - ref["Expectations"]["mu_T"]).max() / np.abs(ref["Expectations"]["mu_T"]).max() < 1e-8

@@ -17,13 +17,12 @@ pytestmark = pytest.mark.gpu
 
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
 # sweep-kernel variants (context options): split ownership (default; auto = 2 rows per step,
-# occupancy grid), split 1 row/step pipelined / unpipelined, shared ownership v2 (512 / 1024
-# threads, 1 or 2 rows per step), generic two-pass
-SWEEPS = [dict(), dict(kernel=3, rows_per_step=1, pipe=1), dict(kernel=3, rows_per_step=1, pipe=0),
-          dict(kernel=2, threads=512, rows_per_step=1), dict(kernel=2, threads=512, rows_per_step=2),
-          dict(kernel=2, threads=1024), dict(sweep=2), dict(sweep=3)]
-SWEEP_IDS = ["split", "split_rp1", "split_rp1_nopipe", "v2_512", "v2_512_rp2", "v2_1024", "twopass", "panel"]
-DEFAULTS = dict(sweep=0, threads=0, grid=0, rows_per_step=0, kernel=0, pipe=1)
+# occupancy grid), split 1 row/step pipelined / unpipelined, the same with non-temporal loads,
+# generic two-pass, panel (wide p)
+SWEEPS = [dict(), dict(rows_per_step=1, pipe=1), dict(rows_per_step=1, pipe=0), dict(nt=1), dict(sweep=2),
+          dict(sweep=3)]
+SWEEP_IDS = ["split", "split_rp1", "split_rp1_nopipe", "split_nt", "twopass", "panel"]
+DEFAULTS = dict(sweep=0, grid=0, rows_per_step=0, pipe=1, nt=-1)
 
 
 @pytest.fixture(scope="module")
@@ -152,6 +151,8 @@ def test_colmajor_and_rowmajor_uploads_agree(ctx):
     a = ctx.estep(_theta(th0))
     Xb, Yb = ctx.get_data()
     assert np.array_equal(Xb, X) and np.array_equal(Yb, Y)
+    Xr, Yr = ctx.get_data_rows(17, 100)
+    assert Xr.flags.c_contiguous and np.array_equal(Xr, X[17:117]) and np.array_equal(Yr, Y[17:117])
     ctx.set_data(np.ascontiguousarray(X), np.ascontiguousarray(Y))
     b = ctx.estep(_theta(th0))
     assert np.array_equal(a.mu_T, b.mu_T) and a.Cee == b.Cee
@@ -160,7 +161,7 @@ def test_colmajor_and_rowmajor_uploads_agree(ctx):
 @pytest.mark.parametrize("grid", [1, 7, 256, 1000])
 def test_grid_invariance(ctx, grid):
     X, Y, th0 = make_problem(2000, 130, 90, 3, seed=11)
-    ctx.set_option("sweep", 1)
+    ctx.set_option("sweep", 0)
     ctx.set_data(X, Y)
     ctx.set_option("grid", 0)
     a = ctx.estep(_theta(th0))
@@ -171,7 +172,7 @@ def test_grid_invariance(ctx, grid):
     assert np.array_equal(a.mu_T, b.mu_T)
 
 
-def test_fused_and_twopass_agree_midsize(ctx):
+def test_split_twopass_panel_agree_midsize(ctx):
     from ppls_amd import Theta
     p, q, r = 600, 500, 3
     rng = np.random.default_rng(1)
@@ -182,16 +183,13 @@ def test_fused_and_twopass_agree_midsize(ctx):
     th0 = _theta(dict(W=np.linalg.qr(rng.standard_normal((p, r)))[0], C=np.linalg.qr(rng.standard_normal((q, r)))[0],
                       B=np.eye(r), sigE=1.0, sigF=1.0, sigH=1.0, sigT=np.eye(r)))
     out = {}
-    for sw in (1, 2):
+    for sw in (0, 2, 3):
         ctx.set_option("sweep", sw)
         out[sw] = ctx.em_run(th0, 6, -np.inf, 0)
     ctx.set_option("sweep", 0)
-    ctx.set_option("kernel", 2)
-    out[3] = ctx.em_run(th0, 6, -np.inf, 0)
-    assert _relerr(out[3][1], out[1][1]) < 1e-12
-    (e1, l1, x1, _), (e2, l2, x2, _) = out[1], out[2]
-    assert _relerr(l1, l2) < 1e-12
-    assert np.abs(e1.W - e2.W).max() < 1e-10
+    (e1, l1, x1, _), (e2, l2, x2, _), (e3, l3, _, _) = out[0], out[2], out[3]
+    assert _relerr(l3, l1) < 1e-12 and _relerr(l2, l1) < 1e-12
+    assert np.abs(e1.W - e2.W).max() < 1e-10 and np.abs(e1.W - e3.W).max() < 1e-10
     assert np.all(np.diff(l1) > 0)
     # against the oracle on the same (copied back) data
     X, Y = ctx.get_data()

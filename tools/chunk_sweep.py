@@ -7,10 +7,21 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-sys.path.insert(0, os.path.join(ROOT, "tools"))
 from bench import CONFIGS, make_truth_and_theta0  # noqa: E402
 from ppls_amd import Context  # noqa: E402
-from team_ablation import time_sweep  # noqa: E402
+
+
+def time_sweep(ctx, steps=6):
+    """Average sweep-kernel time (HIP events) over `steps` device-resident EM iterations."""
+    ctx.em_iterate(1)
+    ctx.synchronize()
+    ctx.set_option("timing", 1)
+    ctx.sweep_timing(reset=True)
+    ctx.em_iterate(steps)
+    ctx.synchronize()
+    ms, n = ctx.sweep_timing(reset=True)
+    ctx.set_option("timing", 0)
+    return ms / max(n, 1)
 
 
 def main():
