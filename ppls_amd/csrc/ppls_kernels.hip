@@ -1265,12 +1265,11 @@ __device__ int ppls_jacobi_wave(double* sA, double* sV) {
   return sweeps;
 }
 
-// Polar factor U V' of the p x R matrix S (column-major, ld lds) = S V Sigma^-1 V', where V and
-// Sigma are the right singular vectors / values of S, obtained accurately by Cholesky-QR2
-// (S = Q R2 R1, orthogonality O(eps kappa(S))) followed by one-sided Jacobi on T = R2 R1 (the
-// left factor is never formed and no triangular inverse is applied to S).  Three block passes
-// over S: the first stages S into LDS (Sl, p*R doubles; nullptr = re-read from global); the last
-// writes out = S F, F = V Sigma^-1 V', and, if gram_out != nullptr, the Gram out'out the next
+// Polar factor U V' of the p x R matrix S (column-major, ld lds) by Cholesky-QR2 (S = Q1 R1,
+// Q1 = Q R2) and one-sided Jacobi on T = R2 R1 = U_T Sigma V': U V' = Q1 R2^-1 U_T V'.  Three
+// block passes: the first stages S into LDS (Sl, p*R doubles; nullptr = re-read from global); the
+// second forms Q1 = S R1^-1 (kept in Sl, else in out) and its Gram; the last
+// writes out = Q1 P, P = R2^-1 U_T V', and, if gram_out != nullptr, the Gram out'out the next
 // iteration's scalar update needs.  All R x R algebra runs on wave 0 in LDS; the Jacobi is
 // warm-started from vstate (the previous iteration's V; nullptr = identity).  sm: >= 2 R^2
 // doubles of LDS.  Returns false when S is numerically rank deficient (a Cholesky pivot fails or
@@ -1355,6 +1354,9 @@ __device__ bool ppls_block_polar_fast(const double* __restrict__ S, int64_t lds,
   if (!ok) return false;
   const double* Sr = Sl ? Sl : S;
   const int64_t ldr = Sl ? p : lds;
+  // Q1 is kept where pass 3 reads it back (each thread its own rows): over S in LDS, else in out
+  double* Qs = Sl ? Sl : out;
+  const int64_t ldq = Sl ? p : ldo;
   // pass 2: G2 = Q1'Q1, Q1 = S R1^-1
   {
     double M[R][R];
@@ -1377,6 +1379,8 @@ __device__ bool ppls_block_polar_fast(const double* __restrict__ S, int64_t lds,
         qv[j] = s;
       }
       ppls_gram_acc<R>(qv, vals);
+#pragma unroll
+      for (int j = 0; j < R; ++j) Qs[(int64_t)j * ldq + i] = qv[j];
     }
   }
   ppls_block_sum_t<NG, NW>(vals, sh);
@@ -1403,15 +1407,16 @@ __device__ bool ppls_block_polar_fast(const double* __restrict__ S, int64_t lds,
         double Gm[R][R], U2[R][R], dinv[R];
         ppls_gram_unpack<R>(vals, Gm);
         good = ppls_chol_reg<R>(Gm, U2, dinv);
-        for (int e = 0; e < GG; ++e) sA[e] = 0.0;
+        for (int e = 0; e < GG; ++e) { sA[e] = 0.0; sU[e] = 0.0; }
 #pragma unroll
-        for (int a = 0; a < R; ++a)                 // T = R2 R1 (upper)
+        for (int a = 0; a < R; ++a)                 // T = R2 R1 (upper); sU = R2
 #pragma unroll
           for (int b = 0; b < R; ++b) {
             double sacc = 0.0;
 #pragma unroll
             for (int kk = 0; kk < R; ++kk) sacc = fma(U2[a][kk], sT[b * G + kk], sacc);
             sA[b * G + a] = sacc;
+            sU[b * G + a] = U2[a][b];
           }
       }
       ppls_wave_lds_fence();
@@ -1450,12 +1455,26 @@ __device__ bool ppls_block_polar_fast(const double* __restrict__ S, int64_t lds,
     for (int i = 0; i < R; ++i) smax = fmax(smax, ssv[i]);
 #pragma unroll
     for (int i = 0; i < R; ++i) good = good && (ssv[i] > smax * 1e-14);
-    for (int e = lane; e < R * R; e += 64) {   // F = V Sigma^-1 V', entry (a, b)
+    // P = R2^-1 U_T V' with U_T = (T V) Sigma^-1 (the Jacobi's columns, sT): then the polar factor
+    // is Q1 P.  Q1 is the computed factor whose Gram R2 was taken from and R2^-1, U_T V' are well
+    // conditioned, so out = Q1 P is orthonormal to O(eps) for any kappa(S) CholQR2 accepts (the
+    // one-step form S V Sigma^-1 V' would lose O(eps kappa(S)) of orthogonality).
+    ppls_inv_upper_wave<R>(sU, sA);                        // sA = R2^-1
+    for (int e = lane; e < GG; e += 64) {                  // sU = U_T V'
+      const int a = e % G, b = e / G;
+      double s = 0.0;
+      if (a < R && b < R)
+#pragma unroll
+        for (int kk = 0; kk < R; ++kk) s = fma(sT[kk * G + a] * (1.0 / ssv[kk]), sV[kk * G + b], s);
+      sU[e] = s;
+    }
+    ppls_wave_lds_fence();
+    for (int e = lane; e < R * R; e += 64) {               // P -> sm + R^2 (ld R)
       const int a = e % R, b = e / R;
       double s = 0.0;
 #pragma unroll
-      for (int kk = 0; kk < R; ++kk) s = fma(sV[kk * G + a] * (1.0 / ssv[kk]), sV[kk * G + b], s);
-      sF[b * R + a] = s;
+      for (int kk = 0; kk < R; ++kk) s = fma(sA[kk * G + a], sU[b * G + kk], s);
+      sF[R * R + b * R + a] = s;
       if (vstate) vstate[b * R + a] = sV[b * G + a];
     }
     good = __shfl(good ? 1 : 0, 0, 64) != 0 && good;   // lane 0 holds the chol2 verdict for small R
@@ -1475,19 +1494,19 @@ __device__ bool ppls_block_polar_fast(const double* __restrict__ S, int64_t lds,
   __syncthreads();
   ppls_stamp(tr, 4);
   if (!ok) return false;
-  // pass 3: out = S F (+ Gram of out)
+  // pass 3: out = Q1 P (+ Gram of out)
   double F[R][R];
 #pragma unroll
   for (int a = 0; a < R; ++a)
 #pragma unroll
-    for (int b = 0; b < R; ++b) F[a][b] = sF[b * R + a];
+    for (int b = 0; b < R; ++b) F[a][b] = sF[R * R + b * R + a];
 #pragma unroll
   for (int e = 0; e < NG; ++e) vals[e] = 0.0;
 #pragma unroll 2
   for (int i = tid; i < ldo_rows; i += NT) {
     double xq[R], o[R];
 #pragma unroll
-    for (int k = 0; k < R; ++k) xq[k] = (i < p) ? Sr[(int64_t)k * ldr + i] : 0.0;
+    for (int k = 0; k < R; ++k) xq[k] = (i < p) ? Qs[(int64_t)k * ldq + i] : 0.0;
 #pragma unroll
     for (int j = 0; j < R; ++j) {
       double s = 0.0;
