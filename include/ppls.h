@@ -106,6 +106,10 @@ int ppls_set_data(ppls_ctx* ctx, const double* X, const double* Y, int64_t n_loc
  * counter-based Philox4x32-10 normals keyed by (seed, element index): independent of sharding. */
 int ppls_generate_synthetic(ppls_ctx* ctx, int64_t n_total, int64_t row0, int64_t n_local, int p,
                             int q, int r, const ppls_theta* truth, uint64_t seed);
+/* The generator's Philox4x32-10 block function on the device, for known-answer checks: out[4i..4i+3]
+ * = philox4x32_10(ctr[4i..4i+3], key = {key & 0xffffffff, key >> 32}), i < count (host arrays).
+ * The generator uses ctr = {pair lo, pair hi, stream, 0}, key = seed. */
+int ppls_philox4x32_10(ppls_ctx* ctx, const uint32_t* ctr, int64_t count, uint64_t key, uint32_t* out);
 int ppls_get_data(ppls_ctx* ctx, double* X, double* Y, int64_t row_begin, int64_t nrows);
 /* The same rows in row-major layout (X: nrows x p, Y: nrows x q, C order), streamed without a
  * device-side transpose: what a row-oriented host consumer (the CPU baseline) reads. */

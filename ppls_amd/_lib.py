@@ -71,6 +71,8 @@ SIGNATURES = {
                                            ct.c_int, ct.c_int, ct.POINTER(PplsTheta), ct.c_uint64]),
     "ppls_get_data": (ct.c_int, [ct.c_void_p, _dp, _dp, ct.c_int64, ct.c_int64]),
     "ppls_get_data_rows": (ct.c_int, [ct.c_void_p, _dp, _dp, ct.c_int64, ct.c_int64]),
+    "ppls_philox4x32_10": (ct.c_int, [ct.c_void_p, ct.POINTER(ct.c_uint32), ct.c_int64, ct.c_uint64,
+                                      ct.POINTER(ct.c_uint32)]),
     "ppls_data_ssq": (ct.c_int, [ct.c_void_p, _dp, _dp]),
     "ppls_estep": (ct.c_int, [ct.c_void_p, ct.POINTER(PplsTheta), ct.c_int, ct.POINTER(PplsExpect)]),
     "ppls_mstep": (ct.c_int, [ct.c_void_p, ct.POINTER(PplsExpect), ct.c_int, ct.c_int,

@@ -162,6 +162,15 @@ class Context:
         self._chk(self._L.ppls_get_data_rows(self.h, dptr(X), dptr(Y), int(row_begin), int(nrows)))
         return X, Y
 
+    def philox4x32_10(self, ctr, key: int):
+        """Device Philox4x32-10 block function (the generator's): ctr (count, 4) uint32 -> (count, 4)."""
+        c = np.ascontiguousarray(ctr, dtype=np.uint32).reshape(-1, 4)
+        out = np.empty_like(c)
+        u32p = ct.POINTER(ct.c_uint32)
+        self._chk(self._L.ppls_philox4x32_10(self.h, c.ctypes.data_as(u32p), c.shape[0], ct.c_uint64(int(key)),
+                                             out.ctypes.data_as(u32p)))
+        return out
+
     def ssq(self):
         a, b = ct.c_double(), ct.c_double()
         self._chk(self._L.ppls_data_ssq(self.h, ct.byref(a), ct.byref(b)))

@@ -793,6 +793,22 @@ int ppls_generate_synthetic(ppls_ctx* c, int64_t n_total, int64_t row0, int64_t 
   return compute_ssq(c);
 }
 
+int ppls_philox4x32_10(ppls_ctx* c, const uint32_t* ctr, int64_t count, uint64_t key, uint32_t* out) {
+  if (!c) return PPLS_E_ARG;
+  if (count < 0 || (count > 0 && (!ctr || !out))) return fail(c, PPLS_E_ARG, "bad counter array");
+  if (count == 0) return PPLS_OK;
+  HIPCHK(c, hipSetDevice(c->device));
+  uint32_t* d = nullptr;
+  HIPCHK(c, hipMalloc(&d, sizeof(uint32_t) * 8 * count));
+  hipError_t e = hipMemcpy(d, ctr, sizeof(uint32_t) * 4 * count, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = ppls_launch_philox(d, count, key, d + 4 * count, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  if (e == hipSuccess) e = hipMemcpy(out, d + 4 * count, sizeof(uint32_t) * 4 * count, hipMemcpyDeviceToHost);
+  (void)hipFree(d);
+  if (e != hipSuccess) return fail(c, PPLS_E_HIP, "philox: %s", hipGetErrorString(e));
+  return PPLS_OK;
+}
+
 int ppls_get_data_rows(ppls_ctx* c, double* X, double* Y, int64_t row_begin, int64_t nrows) {
   if (!c) return PPLS_E_ARG;
   if (!c->have_data) return fail(c, PPLS_E_STATE, "no data");

@@ -89,6 +89,7 @@ hipError_t ppls_launch_convert(const void* src, int src_f32, void* dst, int dst_
 hipError_t ppls_launch_generate(int64_t n_local, int64_t row0, int p, int q, int ldx, int ldy, int r,
                                 const PplsScalars* truth, const double* Wt, const double* Ct,
                                 uint64_t seed, double* TU, double* X, double* Y, hipStream_t st);
+hipError_t ppls_launch_philox(const uint32_t* ctr, int64_t count, uint64_t key, uint32_t* out, hipStream_t st);
 hipError_t ppls_launch_to_rowmajor(const double* src, int64_t n, int p, int ld, double* dst,
                                    hipStream_t st);
 // variances.PPLS_simult (ppls_variances.hip)

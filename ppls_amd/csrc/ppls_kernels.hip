@@ -40,6 +40,19 @@ __host__ __device__ inline PplsU4 ppls_philox(PplsU4 c, uint32_t k0, uint32_t k1
   return c;
 }
 
+__global__ void ppls_philox_kernel(const PplsU4* __restrict__ ctr, int64_t count, uint64_t key,
+                                   PplsU4* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < count) out[i] = ppls_philox(ctr[i], (uint32_t)key, (uint32_t)(key >> 32));
+}
+
+hipError_t ppls_launch_philox(const uint32_t* ctr, int64_t count, uint64_t key, uint32_t* out, hipStream_t st) {
+  if (count <= 0) return hipSuccess;
+  hipLaunchKernelGGL(ppls_philox_kernel, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, st,
+                     (const PplsU4*)ctr, count, key, (PplsU4*)out);
+  return hipGetLastError();
+}
+
 // Two standard normals for (seed, stream m, pair index) -- Box-Muller on 53-bit uniforms.
 __device__ inline void ppls_normal2(uint64_t seed, uint32_t m, uint64_t pair, double* z0, double* z1) {
   PplsU4 c = {(uint32_t)pair, (uint32_t)(pair >> 32), m, 0u};

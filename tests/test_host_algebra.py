@@ -19,7 +19,7 @@ def L():
 
 def test_every_declared_symbol_is_exported(L):
     hdr = open(os.path.join(ROOT, "include", "ppls.h")).read()
-    names = set(re.findall(r"\b(ppls_[a-zA-Z_]+)\s*\(", hdr))
+    names = set(re.findall(r"\b(ppls_[a-zA-Z0-9_]+)\s*\(", hdr))
     assert len(names) >= 20
     for n in sorted(names):
         assert hasattr(L, n), n
