@@ -77,6 +77,13 @@ struct ppls_ctx {
   double* coefs = nullptr;     // loglC_fast coefficient block (5r)
   double* scratch = nullptr;   // generic device scratch
   size_t scratch_bytes = 0;
+  // ppls_em_run's device-side stop rule: a device flag every kernel of the run checks, set by the
+  // finalize that sees logl[i] - logl[i-1] < atol, and its host-mapped mirror the host polls
+  int* stop_d = nullptr;
+  int* stop_mirror = nullptr;       // host pointer (hipHostMalloc, mapped, coherent)
+  int* stop_mirror_dev = nullptr;   // its device address
+  const int* sweep_stop = nullptr;  // non-null only inside ppls_em_run with a finite atol
+  double stop_atol = 0.0;
   // device-resident iteration state (ppls_em_begin / ppls_em_iterate)
   int em_r = 0, em_cur = 0, em_iter = 0;
   bool em_active = false;
@@ -374,6 +381,7 @@ int sweep(ppls_ctx* c, int r, int slot, bool write_mu) {
     const bool nt = c->nt_loads > 0 ||
                     (c->nt_loads < 0 && 8.0 * nrows * (double)(c->ldx + c->ldy) > 256.0 * (1 << 20));
     a.ablate = c->ablate | (nt ? 16 : 0);
+    a.stop = c->sweep_stop;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     const bool timed = c->timing > 0 && (c->sweep_count++ % c->timing) == 0;
     if (timed) {
@@ -393,12 +401,12 @@ int sweep(ppls_ctx* c, int r, int slot, bool write_mu) {
     else HIPCHK(c, ppls_launch_sweep_twopass(&a, c->Z, c->stream));
     if (timed) HIPCHK(c, hipEventRecord(e1, c->stream));
     HIPCHK(c, ppls_launch_reduce2(c->part, groups, c->part_ld, c->part_ld, c->stats,
-                                  c->part + (size_t)c->part_groups * c->part_ld, c->stream));
+                                  c->part + (size_t)c->part_groups * c->part_ld, c->sweep_stop, c->stream));
   }
   return allreduce(c, c->stats, (size_t)c->part_ld);
 }
 
-int finalize(ppls_ctx* c, int r, int cur, int nxt, int logl_index, int type) {
+int finalize(ppls_ctx* c, int r, int cur, int nxt, int logl_index, int type, int stop_step = 0) {
   PplsFinalizeArgs f;
   f.stats = c->stats;
   f.ssq = c->ssq;
@@ -425,6 +433,11 @@ int finalize(ppls_ctx* c, int r, int cur, int nxt, int logl_index, int type) {
   f.gram_cur = c->gram[cur];
   f.gram_nxt = c->gram[nxt];
   f.vstate = c->vstate;
+  f.stop = c->sweep_stop ? c->stop_d : nullptr;
+  f.stop_mirror = c->sweep_stop ? c->stop_mirror_dev : nullptr;
+  f.stop_check = stop_step > 0 ? 1 : 0;
+  f.stop_step = stop_step;
+  f.atol = c->stop_atol;
   HIPCHK(c, ppls_launch_finalize(&f, c->stream));
   return PPLS_OK;
 }
@@ -596,6 +609,8 @@ void ppls_ctx_destroy(ppls_ctx* c) {
   c->z_cols = 0;
   dfree(c->work); dfree(c->status); dfree(c->coefs); dfree(c->scratch);
   if (c->ftrace) (void)hipFree(c->ftrace);
+  dfree(c->stop_d);
+  if (c->stop_mirror) (void)hipHostFree(c->stop_mirror);
   for (auto& e : c->ev) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
   if (c->blas) (void)rocblas_destroy_handle(c->blas);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -1022,25 +1037,64 @@ int ppls_em_run(ppls_ctx* c, ppls_theta* th, int r, int max_steps, double atol, 
   HIPCHK(c, hipMemsetAsync(c->status, 0, sizeof(int), c->stream));
   const bool want_mu = eout && (eout->mu_T || eout->mu_U);
   const bool do_check = !(atol == -INFINITY);   // atol = -Inf: the stop rule never fires
-  int cur = 0, i_final = max_steps;
-  std::vector<double> hl(max_steps + 2, NAN);
+  // The stop rule (EM_W_multi.R:792) runs on the device: the finalize that sees
+  // logl[i] - logl[i-1] < atol sets a flag, and every later kernel of the run exits at once, so the
+  // host enqueues iterations without a per-iteration read-back.  It polls the flag's host-mapped
+  // mirror and stays at most EM_LOOKAHEAD iterations ahead of the device (events), so a long
+  // EMsteps stops launching soon after convergence.  With collectives (RCCL or a host reducer)
+  // every rank enqueues every iteration, so the collective sequence is the same on all ranks.
+  if (do_check) {
+    if (!c->stop_d) {
+      int rc2;
+      if ((rc2 = dalloc(c, &c->stop_d, 1))) return rc2;
+      HIPCHK(c, hipHostMalloc((void**)&c->stop_mirror, sizeof(int), hipHostMallocMapped | hipHostMallocCoherent));
+      HIPCHK(c, hipHostGetDevicePointer((void**)&c->stop_mirror_dev, c->stop_mirror, 0));
+    }
+    HIPCHK(c, hipMemsetAsync(c->stop_d, 0, sizeof(int), c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    __atomic_store_n(c->stop_mirror, 0, __ATOMIC_SEQ_CST);
+    c->sweep_stop = c->stop_d;
+    c->stop_atol = atol;
+  }
+  struct StopGuard {   // the flag applies to this run only
+    ppls_ctx* c;
+    std::vector<hipEvent_t> evs;
+    ~StopGuard() {
+      c->sweep_stop = nullptr;
+      for (auto e : evs) (void)hipEventDestroy(e);
+    }
+  } guard{c, {}};
+  constexpr int EM_LOOKAHEAD = 8;
+  std::vector<hipEvent_t>& evs = guard.evs;
+  const bool may_break = c->nranks == 1 && !c->reducer && !c->comm;
+  int cur = 0;
   for (int s = 1; s <= max_steps + 1; ++s) {
+    if (do_check && may_break && s > EM_LOOKAHEAD) {
+      HIPCHK(c, hipEventSynchronize(evs[(size_t)(s - 1 - EM_LOOKAHEAD) % EM_LOOKAHEAD]));
+      if (__atomic_load_n(c->stop_mirror, __ATOMIC_ACQUIRE) != 0) break;   // converged: stop launching
+    }
     const int nxt = cur ^ 1;
     const bool wm = want_mu && (do_check || s == max_steps + 1);
     if ((rc = sweep(c, r, cur, wm))) return rc;
-    if ((rc = finalize(c, r, cur, nxt, s >= 2 ? s - 2 : -1, type))) return rc;
-    if (do_check && s >= 3) {
-      // logl[i] - logl[i-1] < atol with i = s-1 (EM_W_multi.R:792)
-      HIPCHK(c, hipMemcpyAsync(&hl[s - 3], c->loglik + (s - 3), 2 * sizeof(double), hipMemcpyDeviceToHost, c->stream));
-      HIPCHK(c, hipStreamSynchronize(c->stream));
-      if (hl[s - 2] - hl[s - 3] < atol) {
-        i_final = s - 1;
-        break;
+    if ((rc = finalize(c, r, cur, nxt, s >= 2 ? s - 2 : -1, type, do_check && s >= 3 ? s : 0))) return rc;
+    if (do_check && may_break) {
+      const size_t k = (size_t)(s - 1) % EM_LOOKAHEAD;
+      if (evs.size() <= k) {
+        hipEvent_t e;
+        HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        evs.push_back(e);
       }
+      HIPCHK(c, hipEventRecord(evs[k], c->stream));
     }
-    if (s == max_steps + 1) break;
     cur = nxt;
   }
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  // the iteration the run ended at: the finalize of sweep s_stop saw the stop rule fire, so
+  // theta_{s_stop - 1} (slot (s_stop - 1) & 1) is the estimate and logl[1 .. s_stop - 1] the trace
+  int s_stop = 0;
+  if (do_check) HIPCHK(c, hipMemcpy(&s_stop, c->stop_d, sizeof(int), hipMemcpyDeviceToHost));
+  const int i_final = s_stop > 0 ? s_stop - 1 : max_steps;
+  cur = i_final & 1;
   HIPCHK(c, hipStreamSynchronize(c->stream));
   if ((rc = check_status(c))) return rc;
   if (loglik) HIPCHK(c, hipMemcpy(loglik, c->loglik, sizeof(double) * i_final, hipMemcpyDeviceToHost));
@@ -1652,7 +1706,7 @@ int ppls_variances(ppls_ctx* c, const double* mu, const double* Cdiag, double si
     VRC(dalloc(c, &dpart, (size_t)chunks * sld + (size_t)ppls_reduce_tmp_len(chunks, sld)));
     VCHK(hipMemcpyAsync(dmu, mu, sizeof(double) * n * a, hipMemcpyHostToDevice, c->stream));
     VCHK(ppls_launch_xtmu(D, f32, n, ld, dmu, a, chunks, dpart, sld, c->stream));
-    VCHK(ppls_launch_reduce2(dpart, chunks, sld, sld, dS, dpart + (size_t)chunks * sld, c->stream));
+    VCHK(ppls_launch_reduce2(dpart, chunks, sld, sld, dS, dpart + (size_t)chunks * sld, nullptr, c->stream));
     for (int k = 0; k < a; ++k)
       for (int64_t i = 0; i < n; ++i) mu2[k] += mu[(size_t)k * n + i] * mu[(size_t)k * n + i];   // crossprod(mu_T)
     dfree(dpart);

@@ -31,6 +31,7 @@ struct PplsSweepArgs {
   int grid;              // workgroups (split) / row chunks (two-pass, panel accumulation)
   int ablate;            // timing experiments only (split): 1 no compute, 2 no HBM copies; 16 = nt loads
   int dots_grid;         // panel dots workgroups (0 = one per 128-row group, capped)
+  const int* stop;       // device stop flag (em_run's convergence test) or nullptr: kernels exit if set
 };
 
 struct PplsFinalizeArgs {
@@ -55,6 +56,11 @@ struct PplsFinalizeArgs {
   double* gram_nxt;         // receives [Wn'Wn | Cn'Cn], or nullptr
   double* vstate;           // [V_W | V_C] (2 r^2) Jacobi warm start carried across iterations, or nullptr
   long long* trace;      // diagnostics: per-block phase timestamps (16 per block) or nullptr
+  int* stop;             // device stop flag or nullptr: the kernel exits if set; sets it (= stop_step)
+                         // when stop_check and loglik[logl_index] - loglik[logl_index - 1] < atol
+  int* stop_mirror;      // host-mapped copy of the flag the host polls (or nullptr)
+  int stop_check, stop_step;
+  double atol;
 };
 
 extern "C" {
@@ -75,7 +81,7 @@ hipError_t ppls_launch_reduce(const double* part, int ngroups, int64_t ld, int64
 hipError_t ppls_launch_finalize(const PplsFinalizeArgs* f, hipStream_t st);
 int64_t ppls_reduce_tmp_len(int ngroups, int64_t len);
 hipError_t ppls_launch_reduce2(const double* part, int ngroups, int64_t ld, int64_t len, double* out,
-                               double* tmp, hipStream_t st);
+                               double* tmp, const int* stop, hipStream_t st);
 hipError_t ppls_launch_loglc(const double* G, const double* ssq, double N, int p, int q, int r,
                              double sigX, double sigY, const double* coefs, double* out, hipStream_t st);
 hipError_t ppls_launch_sumsq(const double* a, int64_t len, double* part, int nblocks, double* out,

@@ -245,7 +245,9 @@ __global__ void ppls_convert_kernel(const TI* __restrict__ src, TO* __restrict__
 
 // out[j] (+)= sum_g part[g*ld + j], fixed order -> deterministic.
 __global__ void ppls_reduce_partials_kernel(const double* __restrict__ part, int ngroups, int64_t ld,
-                                            int64_t len, double* __restrict__ out, int accumulate) {
+                                            int64_t len, double* __restrict__ out, int accumulate,
+    const int* __restrict__ stop) {
+  if (stop && *stop) return;   // em_run converged earlier (device stop flag)
   const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= len) return;
   double s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -261,7 +263,9 @@ __global__ void ppls_reduce_partials_kernel(const double* __restrict__ part, int
 
 // Stage 1 of the two-stage reduction: tmp[chunk][j] = sum of groups [chunk*32, chunk*32+32).
 __global__ void ppls_reduce_chunks_kernel(const double* __restrict__ part, int ngroups, int64_t ld,
-                                          int64_t len, double* __restrict__ tmp) {
+                                          int64_t len, double* __restrict__ tmp,
+    const int* __restrict__ stop) {
+  if (stop && *stop) return;   // em_run converged earlier (device stop flag)
   const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= len) return;
   const int g0 = blockIdx.y * 32, g1 = min(ngroups, g0 + 32);
@@ -293,7 +297,9 @@ template <int R, int NSH, int NT, int RP, bool PIPE, int SLOTS, int CPW>
 __global__ __launch_bounds__(NT, 2 * NT / 512) void ppls_sweep_split_kernel(
     const double* __restrict__ X, const double* __restrict__ Y, int64_t n_local, int ldx, int ldy,
     const double* __restrict__ Wp, const double* __restrict__ Cp, const PplsScalars* __restrict__ sc,
-    double* __restrict__ part, int64_t part_ld, double* __restrict__ mu, int write_mu, int ablate) {
+    double* __restrict__ part, int64_t part_ld, double* __restrict__ mu, int write_mu, int ablate,
+    const int* __restrict__ stop) {
+  if (stop && *stop) return;   // em_run converged earlier (device stop flag)
   static_assert(SLOTS >= 2 * RP, "ring must hold the group being read and the group in flight");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int V = R * RP;                           // partial dots per thread per step
@@ -515,7 +521,9 @@ __global__ __launch_bounds__(NT, 2 * NT / 512) void ppls_sweep_split_kernel(
 // Pass 1: Z = [X W | Y C] (n_local x 2R row-major), one wave per row.
 __global__ __launch_bounds__(256) void ppls_dots_kernel(
     const double* __restrict__ X, const double* __restrict__ Y, int64_t n_local, int ldx, int ldy,
-    const double* __restrict__ Wp, const double* __restrict__ Cp, int r, double* __restrict__ Z) {
+    const double* __restrict__ Wp, const double* __restrict__ Cp, int r, double* __restrict__ Z,
+    const int* __restrict__ stop) {
+  if (stop && *stop) return;   // em_run converged earlier (device stop flag)
   const int lane = threadIdx.x & 63;
   const int64_t wid = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
@@ -551,7 +559,9 @@ __global__ __launch_bounds__(256) void ppls_dots_kernel(
 __global__ __launch_bounds__(256) void ppls_acc_kernel(
     const double* __restrict__ X, const double* __restrict__ Y, int64_t n_local, int ldx, int ldy,
     const double* __restrict__ Z, int r, const PplsScalars* __restrict__ sc, int64_t rows_per_chunk,
-    double* __restrict__ part, int64_t part_ld, double* __restrict__ mu, int write_mu) {
+    double* __restrict__ part, int64_t part_ld, double* __restrict__ mu, int write_mu,
+    const int* __restrict__ stop) {
+  if (stop && *stop) return;   // em_run converged earlier (device stop flag)
   const int chunk = blockIdx.y;
   const int64_t r0 = (int64_t)chunk * rows_per_chunk;
   const int64_t r1 = min(n_local, r0 + rows_per_chunk);
@@ -659,7 +669,9 @@ template <typename T, int R>
 __global__ __launch_bounds__(256) void ppls_panel_mfmadots_kernel(
     const T* __restrict__ X, const T* __restrict__ Y, int64_t n, int ldx, int ldy,
     const double* __restrict__ Wt, const double* __restrict__ Ct, const PplsScalars* __restrict__ sc,
-    double* __restrict__ Z, double* __restrict__ mu) {
+    double* __restrict__ Z, double* __restrict__ mu,
+    const int* __restrict__ stop) {
+  if (stop && *stop) return;   // em_run converged earlier (device stop flag)
   typedef double d4 __attribute__((ext_vector_type(4)));
   constexpr int ES = (int)sizeof(T);
   constexpr int KT = 128 / ES;        // columns per tile
@@ -760,7 +772,9 @@ __global__ __launch_bounds__(256) void ppls_panel_mfmadots_kernel(
 // W (ldx x R, column-major) -> Wt (ldxp x R, row-major, rows >= ldx zero); same for C.
 __global__ void ppls_transpose_wc_kernel(const double* __restrict__ W, const double* __restrict__ C,
                                          int ldx, int ldy, int ldxp, int ldyp, int r, double* __restrict__ Wt,
-                                         double* __restrict__ Ct) {
+                                         double* __restrict__ Ct,
+    const int* __restrict__ stop) {
+  if (stop && *stop) return;   // em_run converged earlier (device stop flag)
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t nx = (int64_t)ldxp * r;
   if (e < nx) {
@@ -776,7 +790,9 @@ __global__ void ppls_transpose_wc_kernel(const double* __restrict__ W, const dou
 template <typename T, int R>
 __global__ __launch_bounds__(256) void ppls_panel_acc_kernel(
     const T* __restrict__ X, const T* __restrict__ Y, int64_t n, int ldx, int ldy,
-    const double* __restrict__ Z, int64_t rows_per_chunk, double* __restrict__ part, int64_t part_ld) {
+    const double* __restrict__ Z, int64_t rows_per_chunk, double* __restrict__ part, int64_t part_ld,
+    const int* __restrict__ stop) {
+  if (stop && *stop) return;   // em_run converged earlier (device stop flag)
   constexpr int VEC = PplsVec16<T>::N;
   constexpr int V4 = 4 * R;
   const int tid = threadIdx.x;
@@ -1640,6 +1656,18 @@ __device__ void ppls_scalars_wave(const double* sG, const double* sWtW, const do
   }
 }
 
+// The PPLS_simult stop rule on the device (EM_W_multi.R:792: logl[i] - logl[i-1] < atol, i > 1),
+// evaluated by one thread right after it wrote loglik[idx]: sets the stop flag (every later kernel
+// of the run then exits at once) and its host-mapped mirror the host polls.
+__device__ __forceinline__ void ppls_stop_test(const double* loglik, int idx, int* stop, int* stop_mirror,
+                                               int stop_check, int stop_step, double atol) {
+  if (!stop_check || !stop || idx < 1) return;
+  if (loglik[idx] - loglik[idx - 1] < atol) {
+    *stop = stop_step;
+    if (stop_mirror) __hip_atomic_store(stop_mirror, stop_step, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
 #define PPLS_FIN_THREADS 256   // 1 wave per SIMD: the r x r code may use all 512 VGPR+AGPRs
 
 // Block 0: W_next = orth(S_X); block 1: C_next = orth(S_Y); block 2: scalars (moments, loglik,
@@ -1655,7 +1683,9 @@ __global__ __launch_bounds__(PPLS_FIN_THREADS) void ppls_finalize_kernel(
     PplsScalars* __restrict__ sc_nxt, PplsMoments* __restrict__ mom, double* __restrict__ loglik,
     int logl_index, double* __restrict__ work, int* __restrict__ status, int qr, int mode,
     const double* __restrict__ gram_cur, double* __restrict__ gram_nxt, double* __restrict__ vstate,
-    int stage_lds, long long* __restrict__ trace) {
+    int stage_lds, long long* __restrict__ trace,
+    int* __restrict__ stop, int* __restrict__ stop_mirror, int stop_check, int stop_step, double atol) {
+  if (stop && *stop) return;   // em_run converged earlier (device stop flag)
   constexpr int NT = PPLS_FIN_THREADS;
   constexpr int NG = R * (R + 1) / 2;
   extern __shared__ double dyn_lds[];
@@ -1739,6 +1769,7 @@ __global__ __launch_bounds__(PPLS_FIN_THREADS) void ppls_finalize_kernel(
     ppls_scalars_wave<R>(s_G, s_WtW, s_CtC, ssq[0], ssq[1], N, p, q, &s_cur, &s_m, &s_nx,
                          logl_index >= 0 ? loglik + logl_index : nullptr);
   __syncthreads();
+  if (tid == 0) ppls_stop_test(loglik, logl_index, stop, stop_mirror, stop_check, stop_step, atol);
   ppls_stamp(tr, 2);
   {
     const double* a = (const double*)&s_m;
@@ -1758,7 +1789,9 @@ __global__ __launch_bounds__(256) void ppls_finalize_generic_kernel(
     int ldx, int ldy, const double* __restrict__ Wc, const double* __restrict__ Cc,
     const PplsScalars* __restrict__ sc_cur, double* __restrict__ Wn, double* __restrict__ Cn,
     PplsScalars* __restrict__ sc_nxt, PplsMoments* __restrict__ mom, double* __restrict__ loglik,
-    int logl_index, double* __restrict__ work, int* __restrict__ status, int qr, int mode) {
+    int logl_index, double* __restrict__ work, int* __restrict__ status, int qr, int mode,
+    int* __restrict__ stop, int* __restrict__ stop_mirror, int stop_check, int stop_step, double atol) {
+  if (stop && *stop) return;   // em_run converged earlier (device stop flag)
   const double* SX = stats;
   const double* SY = stats + (int64_t)r * ldx;
   const double* G = SY + (int64_t)r * ldy;
@@ -1797,6 +1830,7 @@ __global__ __launch_bounds__(256) void ppls_finalize_generic_kernel(
   if (threadIdx.x == 0) {
     PplsScalars cur = *sc_cur;
     if (logl_index >= 0) loglik[logl_index] = ppls_loglik_from_gram(G, ssq[0], ssq[1], N, p, q, r, &cur);
+    ppls_stop_test(loglik, logl_index, stop, stop_mirror, stop_check, stop_step, atol);
     PplsMoments m;
     ppls_estep_moments(G, WtW, CtC, ssq[0], ssq[1], N, p, q, r, &cur, &m);
     *mom = m;
@@ -1857,7 +1891,8 @@ hipError_t launch_finalize_t(const PplsFinalizeArgs* f, hipStream_t st) {
   hipLaunchKernelGGL(kern, dim3(3), dim3(PPLS_FIN_THREADS), use ? stage : 0, st, f->stats, f->ssq, f->N,
                      f->p, f->q, f->ldx, f->ldy, f->Wc, f->Cc, f->sc_cur, f->Wn, f->Cn, f->sc_nxt, f->mom,
                      f->loglik, f->logl_index, f->work, f->status, f->qr, f->mode, f->gram_cur,
-                     f->gram_nxt, f->vstate, use, f->trace);
+                     f->gram_nxt, f->vstate, use, f->trace, f->stop, f->stop_mirror, f->stop_check,
+                     f->stop_step, f->atol);
   return hipGetLastError();
 }
 
@@ -1884,7 +1919,7 @@ hipError_t launch_split_t(const PplsSweepArgs& a, hipStream_t st) {
   }
   hipLaunchKernelGGL(kern, dim3(a.grid), dim3(512), split_lds(R, a.ldx, a.ldy, 512, RP), st, a.X, a.Y,
                      a.n_local, a.ldx, a.ldy, a.Wp, a.Cp, a.sc, a.part, a.part_ld, a.mu, a.write_mu,
-                     a.ablate);
+                     a.ablate, a.stop);
   return hipGetLastError();
 }
 
@@ -1971,13 +2006,13 @@ hipError_t ppls_launch_sweep_twopass(const PplsSweepArgs* a, double* Z, hipStrea
   int blocks = (int)((nw * 64 + 255) / 256);
   if (blocks > 4096) blocks = 4096;
   hipLaunchKernelGGL(ppls_dots_kernel, dim3(blocks), dim3(256), 0, st, a->X, a->Y, a->n_local,
-                     a->ldx, a->ldy, a->Wp, a->Cp, a->r, Z);
+                     a->ldx, a->ldy, a->Wp, a->Cp, a->r, Z, a->stop);
   const int np = (a->ldx >> 1) + (a->ldy >> 1);
   const int64_t rpc = (a->n_local + a->grid - 1) / a->grid;
   const int chunks = (int)((a->n_local + rpc - 1) / rpc);
   hipLaunchKernelGGL(ppls_acc_kernel, dim3((np + 255) / 256, chunks), dim3(256), 0, st, a->X, a->Y,
                      a->n_local, a->ldx, a->ldy, Z, a->r, a->sc, rpc, a->part, a->part_ld, a->mu,
-                     a->write_mu);
+                     a->write_mu, a->stop);
   return hipGetLastError();
 }
 
@@ -1987,7 +2022,7 @@ hipError_t ppls_launch_accumulate(const PplsSweepArgs* a, const double* Z, hipSt
   const int64_t rpc = (a->n_local + a->grid - 1) / a->grid;
   const int chunks = (int)((a->n_local + rpc - 1) / rpc);
   hipLaunchKernelGGL(ppls_acc_kernel, dim3((np + 255) / 256, chunks), dim3(256), 0, st, a->X, a->Y,
-                     a->n_local, a->ldx, a->ldy, Z, a->r, a->sc, rpc, a->part, a->part_ld, a->mu, 0);
+                     a->n_local, a->ldx, a->ldy, Z, a->r, a->sc, rpc, a->part, a->part_ld, a->mu, 0, a->stop);
   return hipGetLastError();
 }
 
@@ -2002,12 +2037,12 @@ hipError_t launch_panel_t(const PplsSweepArgs* a, const T* X, const T* Y, double
   double* Ct = Wt + (int64_t)ldxp * R;
   const int64_t ne = (int64_t)(ldxp + ldyp) * R;
   hipLaunchKernelGGL(ppls_transpose_wc_kernel, dim3((unsigned)((ne + 255) / 256)), dim3(256), 0, st, a->Wp,
-                     a->Cp, a->ldx, a->ldy, ldxp, ldyp, R, Wt, Ct);
+                     a->Cp, a->ldx, a->ldy, ldxp, ldyp, R, Wt, Ct, a->stop);
   {   // MFMA dots (profiles/r1_c5_*_dots_variants.txt: faster than the VALU and LDS-DMA forms)
     const int64_t wtiles = (a->n_local + 31) / 32;
     const int mblocks = (int)((wtiles + 3) / 4 < 16384 ? (wtiles + 3) / 4 : 16384);
     hipLaunchKernelGGL((ppls_panel_mfmadots_kernel<T, R>), dim3(mblocks), dim3(256), 0, st, X, Y,
-                       a->n_local, a->ldx, a->ldy, Wt, Ct, a->sc, Z, a->write_mu ? a->mu : nullptr);
+                       a->n_local, a->ldx, a->ldy, Wt, Ct, a->sc, Z, a->write_mu ? a->mu : nullptr, a->stop);
   }
   constexpr int VEC = PplsVec16<T>::N;
   if (a->ablate & 256) return hipGetLastError();   // dots only (scores)
@@ -2016,7 +2051,7 @@ hipError_t launch_panel_t(const PplsSweepArgs* a, const T* X, const T* Y, double
   // slower in fp32 (6.0 vs 4.5 ms; profiles/r1_c5_*_acc_variants.txt) -- the pass is load-bound
   const int ntx = (a->ldx + 256 * VEC - 1) / (256 * VEC), nty = (a->ldy + 256 * VEC - 1) / (256 * VEC);
   hipLaunchKernelGGL((ppls_panel_acc_kernel<T, R>), dim3(ntx + nty, chunks), dim3(256), 0, st, X, Y,
-                     a->n_local, a->ldx, a->ldy, Z, rpc, a->part, a->part_ld);
+                     a->n_local, a->ldx, a->ldy, Z, rpc, a->part, a->part_ld, a->stop);
   return hipGetLastError();
 }
 
@@ -2129,24 +2164,24 @@ int64_t ppls_reduce_tmp_len(int ngroups, int64_t len) {
 }
 
 hipError_t ppls_launch_reduce2(const double* part, int ngroups, int64_t ld, int64_t len, double* out,
-                               double* tmp, hipStream_t st) {
+                               double* tmp, const int* stop, hipStream_t st) {
   if (ngroups <= PPLS_RCHUNK || tmp == nullptr) {
     hipLaunchKernelGGL(ppls_reduce_partials_kernel, dim3((unsigned)((len + 255) / 256)), dim3(256), 0,
-                       st, part, ngroups, ld, len, out, 0);
+                       st, part, ngroups, ld, len, out, 0, stop);
     return hipGetLastError();
   }
   const int nch = (ngroups + PPLS_RCHUNK - 1) / PPLS_RCHUNK;
   hipLaunchKernelGGL(ppls_reduce_chunks_kernel, dim3((unsigned)((len + 255) / 256), nch), dim3(256), 0,
-                     st, part, ngroups, ld, len, tmp);
+                     st, part, ngroups, ld, len, tmp, stop);
   hipLaunchKernelGGL(ppls_reduce_partials_kernel, dim3((unsigned)((len + 255) / 256)), dim3(256), 0,
-                     st, tmp, nch, len, len, out, 0);
+                     st, tmp, nch, len, len, out, 0, stop);
   return hipGetLastError();
 }
 
 hipError_t ppls_launch_reduce(const double* part, int ngroups, int64_t ld, int64_t len, double* out,
                               int accumulate, hipStream_t st) {
   hipLaunchKernelGGL(ppls_reduce_partials_kernel, dim3((unsigned)((len + 255) / 256)), dim3(256), 0,
-                     st, part, ngroups, ld, len, out, accumulate);
+                     st, part, ngroups, ld, len, out, accumulate, nullptr);
   return hipGetLastError();
 }
 
@@ -2165,7 +2200,8 @@ hipError_t ppls_launch_finalize(const PplsFinalizeArgs* f, hipStream_t st) {
     default:   // r = 11..16: runtime-r finalize (R(R+1)/2 > 64 block-sum values)
       hipLaunchKernelGGL(ppls_finalize_generic_kernel, dim3(3), dim3(256), 0, st, f->stats, f->ssq, f->N,
                          f->p, f->q, f->r, f->ldx, f->ldy, f->Wc, f->Cc, f->sc_cur, f->Wn, f->Cn,
-                         f->sc_nxt, f->mom, f->loglik, f->logl_index, f->work, f->status, f->qr, f->mode);
+                         f->sc_nxt, f->mom, f->loglik, f->logl_index, f->work, f->status, f->qr, f->mode,
+                         f->stop, f->stop_mirror, f->stop_check, f->stop_step, f->atol);
       return hipGetLastError();
   }
 }
@@ -2181,7 +2217,7 @@ hipError_t ppls_launch_loglc(const double* G, const double* ssq, double N, int p
 hipError_t ppls_launch_sumsq_f32(const float* a, int64_t len, double* part, int nblocks, double* out,
                                  hipStream_t st) {
   hipLaunchKernelGGL(ppls_sumsq_f32_kernel, dim3(nblocks), dim3(256), 0, st, a, len, part);
-  hipLaunchKernelGGL(ppls_reduce_partials_kernel, dim3(1), dim3(64), 0, st, part, nblocks, 1, 1, out, 0);
+  hipLaunchKernelGGL(ppls_reduce_partials_kernel, dim3(1), dim3(64), 0, st, part, nblocks, 1, 1, out, 0, nullptr);
   return hipGetLastError();
 }
 
@@ -2203,7 +2239,7 @@ hipError_t ppls_launch_sumsq(const double* a, int64_t len, double* part, int nbl
                              int out_accumulate, hipStream_t st) {
   hipLaunchKernelGGL(ppls_sumsq_partial_kernel, dim3(nblocks), dim3(256), 0, st, a, len, part);
   hipLaunchKernelGGL(ppls_reduce_partials_kernel, dim3(1), dim3(64), 0, st, part, nblocks, 1, 1, out,
-                     out_accumulate);
+                     out_accumulate, nullptr);
   return hipGetLastError();
 }
 
@@ -2216,7 +2252,7 @@ hipError_t ppls_launch_deflated_ssq(const void* X, int f32, int64_t n, int ld, i
   else
     hipLaunchKernelGGL(ppls_deflated_ssq_kernel<double>, dim3(nblocks), dim3(256), 0, st, (const double*)X, n,
                        ld, p, Wd, m, part);
-  hipLaunchKernelGGL(ppls_reduce_partials_kernel, dim3(1), dim3(64), 0, st, part, nblocks, 1, 1, out, 0);
+  hipLaunchKernelGGL(ppls_reduce_partials_kernel, dim3(1), dim3(64), 0, st, part, nblocks, 1, 1, out, 0, nullptr);
   return hipGetLastError();
 }
 

@@ -208,3 +208,31 @@ def test_gloo_two_processes_device_sweep():
     assert np.abs(res[0][1] - e["W"]).max() < 1e-8 and np.abs(res[0][2] - e["C"]).max() < 1e-8
     mu = np.vstack([res[0][7], res[1][7]])
     assert np.abs(mu - ref["Expectations"]["mu_T"]).max() / np.abs(ref["Expectations"]["mu_T"]).max() < 1e-8
+
+
+def test_k_contexts_device_stop_rule():
+    """A finite atol with sharded ranks: every rank enqueues every iteration (the collective sequence
+    must match), the device stop flag makes them all end at the same iteration as the unsharded fit."""
+    from ppls_amd import Context
+    k, n, p, q, r = 3, 1200, 80, 50, 3
+    X, Y, th0 = make_problem(n, p, q, r, seed=77)
+
+    def fit(c, Xs, Ys, n_total):
+        c.set_data(Xs, Ys, n_total=n_total)
+        est, ll, eout, _ = c.em_run(_theta(th0), 120, 0.5, 0)
+        return est, ll
+
+    with Context(0) as c:
+        ref = fit(c, X, Y, None)
+    assert 2 < len(ref[1]) < 120
+
+    def work(rank, c):
+        r0, nl = Context.shard_range(n, k, rank)
+        return fit(c, X[r0:r0 + nl], Y[r0:r0 + nl], n)
+
+    res = _run_ranks(k, work)
+    for est, ll in res:
+        assert len(ll) == len(ref[1]) and np.array_equal(ll, res[0][1])
+        assert np.array_equal(est.W, res[0][0].W)
+    assert np.abs(res[0][1] - ref[1]).max() / np.abs(ref[1]).max() < 1e-12
+    assert np.abs(res[0][0].W - ref[0].W).max() < 1e-12

@@ -261,3 +261,26 @@ def test_rccl_single_rank_communicator_path():
     rb = b.em_run(_theta(th0), 5, -np.inf, 0)
     b.close()
     assert np.array_equal(ra[1], rb[1]) and np.array_equal(ra[0].W, rb[0].W)
+
+
+@pytest.mark.parametrize("n,p,q,r,steps,atol", [(400, 60, 40, 3, 400, 1e-3), (300, 90, 30, 10, 300, 1e-2),
+                                                (500, 40, 30, 2, 5, 1e-12), (250, 30, 20, 4, 50, 1e6)])
+def test_device_stop_rule_matches_oracle(ctx, n, p, q, r, steps, atol):
+    """The device-side stop rule (EM_W_multi.R:792, evaluated in the finalize, later kernels exit):
+    same number of steps, trace, estimates and Eout as the oracle's host loop, for long EMsteps
+    (stops after a few iterations), an atol never reached, and an atol reached at once (i = 2)."""
+    X, Y, th0 = make_problem(n, p, q, r, seed=n + r)
+    ctx.set_data(X, Y)
+    est, ll, eout, neg = ctx.em_run(_theta(th0), steps, atol, 0)
+    ref = o.ppls_simult(X, Y, r, EMsteps=steps, atol=atol, theta0=th0)
+    e = ref["estimates"]
+    assert len(ll) == len(ref["loglik"]), (len(ll), len(ref["loglik"]))
+    assert _relerr(ll, ref["loglik"]) < 1e-10
+    assert np.abs(est.W - e["W"]).max() < 1e-8 and np.abs(est.C - e["C"]).max() < 1e-8
+    assert _relerr(est.B, np.diag(e["B"])) < 1e-8
+    assert _relerr(eout.mu_T, ref["Expectations"]["mu_T"]) < 1e-8
+    assert _relerr(eout.Ctt, np.diag(ref["Expectations"]["Ctt"])) < 1e-8
+    # a following run on the same context is unaffected by the previous run's stop flag
+    est2, ll2, _, _ = ctx.em_run(_theta(th0), 3, -np.inf, 0)
+    ref3 = o.ppls_simult(X, Y, r, EMsteps=3, atol=-np.inf, theta0=th0)
+    assert len(ll2) == 3 and _relerr(ll2, ref3["loglik"]) < 1e-10
