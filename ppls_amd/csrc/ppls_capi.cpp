@@ -442,6 +442,23 @@ int finalize(ppls_ctx* c, int r, int cur, int nxt, int logl_index, int type, int
   return PPLS_OK;
 }
 
+// The device stop flag (2 ints) and its host-mapped mirror, allocated on first use.
+int ensure_stop(ppls_ctx* c) {
+  if (c->stop_d) return PPLS_OK;
+  int rc;
+  if ((rc = dalloc(c, &c->stop_d, 2))) return rc;
+  HIPCHK(c, hipHostMalloc((void**)&c->stop_mirror, sizeof(int), hipHostMallocMapped | hipHostMallocCoherent));
+  HIPCHK(c, hipHostGetDevicePointer((void**)&c->stop_mirror_dev, c->stop_mirror, 0));
+  return PPLS_OK;
+}
+
+int reset_stop(ppls_ctx* c) {
+  HIPCHK(c, hipMemsetAsync(c->stop_d, 0, 2 * sizeof(int), c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  __atomic_store_n(c->stop_mirror, 0, __ATOMIC_SEQ_CST);
+  return PPLS_OK;
+}
+
 int check_status(ppls_ctx* c) {
   int st = 0;
   HIPCHK(c, hipMemcpy(&st, c->status, sizeof st, hipMemcpyDeviceToHost));
@@ -1044,15 +1061,7 @@ int ppls_em_run(ppls_ctx* c, ppls_theta* th, int r, int max_steps, double atol, 
   // EMsteps stops launching soon after convergence.  With collectives (RCCL or a host reducer)
   // every rank enqueues every iteration, so the collective sequence is the same on all ranks.
   if (do_check) {
-    if (!c->stop_d) {
-      int rc2;
-      if ((rc2 = dalloc(c, &c->stop_d, 1))) return rc2;
-      HIPCHK(c, hipHostMalloc((void**)&c->stop_mirror, sizeof(int), hipHostMallocMapped | hipHostMallocCoherent));
-      HIPCHK(c, hipHostGetDevicePointer((void**)&c->stop_mirror_dev, c->stop_mirror, 0));
-    }
-    HIPCHK(c, hipMemsetAsync(c->stop_d, 0, sizeof(int), c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    __atomic_store_n(c->stop_mirror, 0, __ATOMIC_SEQ_CST);
+    if ((rc = ensure_stop(c)) || (rc = reset_stop(c))) return rc;
     c->sweep_stop = c->stop_d;
     c->stop_atol = atol;
   }
@@ -1139,39 +1148,38 @@ struct Rank1 {
   double B, sigE, sigF, sigH, sigT;
 };
 
-// EMstep_W's coefficients (:60-70) and EMstepC_fast's mu coefficients (:354, :358).
+PplsRank1 r1_of(const Rank1& t) { return PplsRank1{t.B, t.sigE, t.sigF, t.sigH, t.sigT}; }
+
+// EMstep_W's coefficients (:60-70) and EMstepC_fast's mu coefficients (:354, :358) (ppls_math.h).
 void rank1_coefs(const Rank1& t, double* c1, double* c2, double* c3, double* al, double* be, double* ga,
                  double* de) {
-  ppls_coef_estep(t.sigT, t.B, t.sigE, t.sigF, t.sigH, c1, c2, c3, nullptr);
-  const double s2X = t.sigE * t.sigE, s2Y = t.sigF * t.sigF, s2H = t.sigH * t.sigH, s2T = t.sigT * t.sigT;
-  const double B = t.B, v = s2T * B * B + s2H;
-  *al = s2T * (-*c1 + -*c2 * B + 1 / s2X);
-  *be = s2T * (-*c2 + -*c3 * B + 1 / s2Y * B);
-  *ga = -s2T * B * *c1 + -*c2 * v + 1 / s2X * B * s2T;
-  *de = -*c2 * B * s2T + -*c3 * v + 1 / s2Y * v;
+  const PplsRank1 s = r1_of(t);
+  ppls_rank1_coefs(&s, c1, c2, c3, al, be, ga, de);
 }
 
-// One r = 1 sweep of theta t over the deflated data: stats -> host (SX p, SY q, G 2 x 2).
-int rank1_sweep(ppls_ctx* c, const Rank1& t, const std::vector<double>& Wp, const std::vector<double>& Cp,
-                int m, std::vector<double>& SX, std::vector<double>& SY, double G[4]) {
-  int rc;
+// Stage component t for an r = 1 sweep over the deflated data: weights P_0..P_{m-1} w, P_0..P_{m-1} c
+// (so the sweep over X, Y computes Xc w, Yc c) and the sweep scalars.
+int rank1_stage(ppls_ctx* c, const Rank1& t, const std::vector<double>& Wp, const std::vector<double>& Cp, int m) {
   std::vector<double> wv(c->ldx, 0.0), cv(c->ldy, 0.0);
   std::copy(t.w.begin(), t.w.end(), wv.begin());
   std::copy(t.c.begin(), t.c.end(), cv.begin());
   deflate(Wp, m, c->p, wv.data(), false);   // X P_0 .. P_{m-1} w
   deflate(Cp, m, c->q, cv.data(), false);
   PplsScalars s;
-  memset(&s, 0, sizeof s);
-  s.b[0] = t.B;
-  s.t[0] = t.sigT;
-  s.sigE = t.sigE;
-  s.sigF = t.sigF;
-  s.sigH = t.sigH;
-  double c1, c2, c3;
-  rank1_coefs(t, &c1, &c2, &c3, &s.alpha[0], &s.beta[0], &s.gamma[0], &s.delta[0]);
+  const PplsRank1 r1 = r1_of(t);
+  ppls_rank1_sweep_scalars(&r1, &s);
   HIPCHK(c, hipMemcpyAsync(c->W[0], wv.data(), sizeof(double) * c->ldx, hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipMemcpyAsync(c->C[0], cv.data(), sizeof(double) * c->ldy, hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipMemcpyAsync(c->sc[0], &s, sizeof s, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));   // the host vectors go out of scope
+  return PPLS_OK;
+}
+
+// One r = 1 sweep of theta t over the deflated data: stats -> host (SX p, SY q, G 2 x 2).
+int rank1_sweep(ppls_ctx* c, const Rank1& t, const std::vector<double>& Wp, const std::vector<double>& Cp,
+                int m, std::vector<double>& SX, std::vector<double>& SY, double G[4]) {
+  int rc;
+  if ((rc = rank1_stage(c, t, Wp, Cp, m))) return rc;
   if ((rc = sweep(c, 1, 0, false))) return rc;
   std::vector<double> st((size_t)c->part_ld);
   HIPCHK(c, hipMemcpyAsync(st.data(), c->stats, sizeof(double) * c->part_ld, hipMemcpyDeviceToHost, c->stream));
@@ -1184,67 +1192,121 @@ int rank1_sweep(ppls_ctx* c, const Rank1& t, const std::vector<double>& Wp, cons
 
 // logl_W(Xc, Yc, w, c, B, sigE, sigF, sigH, sigT) from the sweep's Gram (:297-323, r = 1).
 double rank1_loglik(const Rank1& t, const double G[4], double ssqX, double ssqY, double N, int p, int q) {
-  PplsScalars s;
-  memset(&s, 0, sizeof s);
-  s.b[0] = t.B;
-  s.t[0] = t.sigT;
-  s.sigE = t.sigE;
-  s.sigF = t.sigF;
-  s.sigH = t.sigH;
-  return ppls_loglik_from_gram(G, ssqX, ssqY, N, p, q, 1, &s);
+  const PplsRank1 s = r1_of(t);
+  return ppls_rank1_loglik(&s, G, ssqX, ssqY, N, p, q);
 }
 
-// The rank-1 E-step moments and M-step scalars from one sweep's Gram -- the arithmetic shared by
-// EMstepC_fast (loglC.cpp:354-385) and meta_Estep / meta_Mstep (loglC.cpp:399-474), which restate
-// the same formulas: B = Cut/Ctt, sighat = (sqrt(Cee), sqrt(Cff)), siglathat = (sqrt(Chh), sqrt(Ctt)).
+// The rank-1 E-step moments and M-step scalars from one sweep's Gram (ppls_rank1_scalars, shared
+// with the device step kernel): the arithmetic of EMstepC_fast (loglC.cpp:354-385) and meta_Estep /
+// meta_Mstep (loglC.cpp:399-474).
 void rank1_scalars(const Rank1& t, const double G[4], double ssqX, double ssqY, double N, int p, int q,
                    Rank1* n) {
-  double c1, c2, c3, al, be, ga, de;
-  rank1_coefs(t, &c1, &c2, &c3, &al, &be, &ga, &de);
-  const double s2X = t.sigE * t.sigE, s2Y = t.sigF * t.sigF, s2H = t.sigH * t.sigH, s2T = t.sigT * t.sigT;
-  const double B = t.B, v = s2T * B * B + s2H;
-  const double A = G[0], D = G[1], Bm = G[3];   // ||Xw||^2, <Xw, Yc>, ||Yc||^2
-  const double mt2 = al * al * A + 2.0 * al * be * D + be * be * Bm;
-  const double mu2 = ga * ga * A + 2.0 * ga * de * D + de * de * Bm;
-  const double mut = ga * al * A + (ga * be + de * al) * D + de * be * Bm;
-  const double Ctt = s2T - s2T * s2T * (-c1 - 2 * B * c2 - B * B * (c3 - 1 / s2Y) + 1 / s2X) + mt2 / N;   // :356
-  const double Cut = s2T * B - (-s2T * s2T * B * (c1 - 1 / s2X) - s2T * s2T * B * B * c2 - s2T * v * c2 -
-                                v * s2T * B * (c3 - 1 / s2Y)) + mut / N;                              // :363
-  (void)mu2;   // Cuu (:361) is not needed by the update
-  const double Ceetmp = c1 * c1 * s2X * s2X * A + ssqX + c2 * c2 * s2X * s2X * Bm - 2 * c1 * s2X * A +
-                        2 * c1 * c2 * s2X * s2X * D - 2 * c2 * s2X * D;                                // :365-366
-  const double Cee = s2X - (-s2X * s2X * c1 + p * s2X) / p + Ceetmp / N / p;                            // :367
-  const double Cfftmp = c3 * c3 * s2Y * s2Y * Bm + ssqY + c2 * c2 * s2Y * s2Y * A - 2 * c3 * s2Y * Bm +
-                        2 * c3 * c2 * s2Y * s2Y * D - 2 * c2 * s2Y * D;                                // :369-370
-  const double Cff = s2Y - (-s2Y * s2Y * c3 + q * s2Y) / q + Cfftmp / N / q;                            // :371
-  const double hx = -c2 * s2H, hy = -(c3 - 1 / s2Y) * s2H;
-  const double Chh = s2H - (-s2H * s2H * (c3 - 1 / s2Y)) + (hx * hx * A + 2 * hx * hy * D + hy * hy * Bm) / N;  // :373
-  n->B = Cut / Ctt;                                  // :385
-  n->sigE = std::sqrt(Cee);                          // sighat (:376)
-  n->sigF = std::sqrt(Cff);
-  n->sigH = std::sqrt(Chh);                          // siglathat (:377)
-  n->sigT = std::sqrt(Ctt);
+  const PplsRank1 s = r1_of(t);
+  PplsRank1 o;
+  ppls_rank1_scalars(&s, G, ssqX, ssqY, N, p, q, &o);
+  n->B = o.B;
+  n->sigE = o.sigE;
+  n->sigF = o.sigF;
+  n->sigH = o.sigH;
+  n->sigT = o.sigT;
 }
 
-// EMstepC_fast (loglC.cpp:340-397) from the sweep of t; SX, SY are X'mu_T, Y'mu_U of the full
-// data, projected here onto the deflated column spaces.
-Rank1 rank1_update(const Rank1& t, std::vector<double> SX, std::vector<double> SY, const double G[4],
-                   double ssqX, double ssqY, double N, int p, int q, const std::vector<double>& Wp,
-                   const std::vector<double>& Cp, int m) {
-  Rank1 n;
-  rank1_scalars(t, G, ssqX, ssqY, N, p, q, &n);
-  deflate(Wp, m, p, SX.data(), true);   // Xc' mu_T = P_{m-1}..P_0 X' mu_T
-  deflate(Cp, m, q, SY.data(), true);
-  double nx = 0.0, ny = 0.0;
-  for (int i = 0; i < p; ++i) { SX[i] /= N; nx += SX[i] * SX[i]; }   // Cxt = Xc' mu_T / N (:355)
-  for (int i = 0; i < q; ++i) { SY[i] /= N; ny += SY[i] * SY[i]; }
-  nx = std::sqrt(nx);
-  ny = std::sqrt(ny);
-  n.w.resize(p);
-  n.c.resize(q);
-  for (int i = 0; i < p; ++i) n.w[i] = SX[i] / nx;   // Cxt.normalized() (:383)
-  for (int i = 0; i < q; ++i) n.c[i] = SY[i] / ny;
-  return n;
+// Device buffers of one PPLSi fit (ppls_rank1_step_kernel's state).
+struct Rank1Dev {
+  double* Wp = nullptr;   // deflation vectors (p x a), (q x a)
+  double* Cp = nullptr;
+  double* tw = nullptr;   // the component's loadings (p), (q)
+  double* tc = nullptr;
+  double* consW = nullptr;
+  double* consC = nullptr;
+  double* lv = nullptr;   // logvalue (EMsteps + 1) and the last Gram (4)
+  PplsRank1* st = nullptr;
+  ~Rank1Dev() { dfree(Wp); dfree(Cp); dfree(tw); dfree(tc); dfree(consW); dfree(consC); dfree(lv); dfree(st); }
+};
+
+// PPLSi's EM loop for component m (EM_W_multi.R:147-173) entirely on the device: per step one r = 1
+// sweep and one ppls_rank1_step_kernel (loglik, stop rule, EMstepC_fast update, constraints, next
+// weights), no host round trip.  The host enqueues up to EMsteps steps, at most EM_LOOKAHEAD ahead
+// of the device, and stops launching once the step kernel reports the end of the fit (host-mapped
+// flag; with collectives every rank enqueues every step so the collective sequence matches).
+// t: in = the constrained initial component, out = the fit.  lv: logvalue[0..i]; G: the last Gram.
+int rank1_fit_device(ppls_ctx* c, Rank1Dev& d, Rank1& t, const ppls_constraint* ck, int m, double ssqX,
+                     double ssqY, int max_steps, double atol, int crit_abs, const std::vector<double>& Wp,
+                     const std::vector<double>& Cp, std::vector<double>& lv, int* steps, bool* na, double G[4]) {
+  int rc;
+  const int p = c->p, q = c->q;
+  if ((rc = rank1_stage(c, t, Wp, Cp, m))) return rc;
+  const PplsRank1 r1 = r1_of(t);
+  HIPCHK(c, hipMemcpyAsync(d.tw, t.w.data(), sizeof(double) * p, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(d.tc, t.c.data(), sizeof(double) * q, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(d.st, &r1, sizeof r1, hipMemcpyHostToDevice, c->stream));
+  PplsRank1StepArgs a;
+  memset(&a, 0, sizeof a);
+  if (ck) {
+    if (ck->W) HIPCHK(c, hipMemcpyAsync(d.consW, ck->W, sizeof(double) * p, hipMemcpyHostToDevice, c->stream));
+    if (ck->C) HIPCHK(c, hipMemcpyAsync(d.consC, ck->C, sizeof(double) * q, hipMemcpyHostToDevice, c->stream));
+    a.consW = ck->W ? d.consW : nullptr;
+    a.consC = ck->C ? d.consC : nullptr;
+    if (ck->B) { a.cons_mask |= 1; a.cons_val.B = ck->B[0]; }
+    if (ck->sigE) { a.cons_mask |= 2; a.cons_val.sigE = ck->sigE[0]; }
+    if (ck->sigF) { a.cons_mask |= 4; a.cons_val.sigF = ck->sigF[0]; }
+    if (ck->sigH) { a.cons_mask |= 8; a.cons_val.sigH = ck->sigH[0]; }
+    if (ck->sigT) { a.cons_mask |= 16; a.cons_val.sigT = ck->sigT[0]; }
+  }
+  if ((rc = ensure_stop(c)) || (rc = reset_stop(c))) return rc;
+  a.stats = c->stats;
+  a.p = p; a.q = q; a.ldx = c->ldx; a.ldy = c->ldy;
+  a.N = (double)c->n_total; a.ssqX = ssqX; a.ssqY = ssqY;
+  a.Wp = d.Wp; a.Cp = d.Cp; a.m = m;
+  a.st = d.st; a.tw = d.tw; a.tc = d.tc;
+  a.Wdst = c->W[0]; a.Cdst = c->C[0]; a.scdst = c->sc[0];
+  a.lv = d.lv; a.Gkeep = d.lv + max_steps + 1;
+  a.max_steps = max_steps; a.crit_abs = crit_abs; a.atol = atol;
+  a.stop = c->stop_d; a.stop_mirror = c->stop_mirror_dev;
+  struct Guard {
+    ppls_ctx* c;
+    std::vector<hipEvent_t> evs;
+    ~Guard() {
+      c->sweep_stop = nullptr;
+      for (auto e : evs) (void)hipEventDestroy(e);
+    }
+  } guard{c, {}};
+  c->sweep_stop = c->stop_d;
+  constexpr int LOOKAHEAD = 8;
+  const bool may_break = c->nranks == 1 && !c->reducer && !c->comm;
+  for (int step = 0; step <= max_steps; ++step) {
+    if (may_break && step >= LOOKAHEAD) {
+      HIPCHK(c, hipEventSynchronize(guard.evs[(size_t)(step - LOOKAHEAD) % LOOKAHEAD]));
+      if (__atomic_load_n(c->stop_mirror, __ATOMIC_ACQUIRE) != 0) break;   // the fit ended
+    }
+    if ((rc = sweep(c, 1, 0, false))) return rc;
+    a.step = step;
+    HIPCHK(c, ppls_launch_rank1_step(&a, c->stream));
+    if (may_break) {
+      const size_t k = (size_t)step % LOOKAHEAD;
+      if (guard.evs.size() <= k) {
+        hipEvent_t e;
+        HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        guard.evs.push_back(e);
+      }
+      HIPCHK(c, hipEventRecord(guard.evs[k], c->stream));
+    }
+  }
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  int stop[2] = {0, 0};
+  HIPCHK(c, hipMemcpy(stop, c->stop_d, sizeof stop, hipMemcpyDeviceToHost));
+  *na = stop[1] != 0;
+  *steps = stop[0] > 0 ? stop[0] : max_steps;
+  std::vector<double> buf((size_t)max_steps + 5);
+  HIPCHK(c, hipMemcpy(buf.data(), d.lv, sizeof(double) * buf.size(), hipMemcpyDeviceToHost));
+  lv.assign(buf.begin(), buf.begin() + (*steps + 1));
+  for (int e = 0; e < 4; ++e) G[e] = buf[(size_t)max_steps + 1 + e];
+  PplsRank1 o;
+  HIPCHK(c, hipMemcpy(&o, d.st, sizeof o, hipMemcpyDeviceToHost));
+  t.B = o.B; t.sigE = o.sigE; t.sigF = o.sigF; t.sigH = o.sigH; t.sigT = o.sigT;
+  HIPCHK(c, hipMemcpy(t.w.data(), d.tw, sizeof(double) * p, hipMemcpyDeviceToHost));
+  HIPCHK(c, hipMemcpy(t.c.data(), d.tc, sizeof(double) * q, hipMemcpyDeviceToHost));
+  return PPLS_OK;
 }
 
 // ||X P_0..P_{m-1}||^2 (and the Y analogue) by an exact residual pass over the resident data,
@@ -1304,9 +1366,13 @@ int ppls_ppls_ex(ppls_ctx* c, int a, int max_steps, double atol, int crit_abs, c
   double ssqX = c->ssq_host[0], ssqY = c->ssq_host[1];   // ||Xc||^2, ||Yc||^2 of the current deflation
   std::vector<double> Wp, Cp;                            // w_1..w_k, c_1..c_k (column-major)
   std::vector<double> gA, gD, gB;                        // ||X w_j||^2, <X w_j, Y c_j>, ||Y c_j||^2
-  std::vector<double> SX, SY;
   bool fixed_wc = false;                                 // some component had W or C fixed
-  const double tiny = 100.0 * 2.220446049250313e-16;     // 100 * .Machine$double.eps
+  Rank1Dev dev;
+  if ((rc = dalloc(c, &dev.Wp, (size_t)p * a)) || (rc = dalloc(c, &dev.Cp, (size_t)q * a)) ||
+      (rc = dalloc(c, &dev.tw, (size_t)p)) || (rc = dalloc(c, &dev.tc, (size_t)q)) ||
+      (rc = dalloc(c, &dev.consW, (size_t)p)) || (rc = dalloc(c, &dev.consC, (size_t)q)) ||
+      (rc = dalloc(c, &dev.lv, (size_t)max_steps + 5)) || (rc = dalloc(c, &dev.st, 1)))
+    return rc;
   out->ncomp = 0;
   out->not_monotone = 0;
   if (out->logvalue)
@@ -1335,20 +1401,17 @@ int ppls_ppls_ex(ppls_ctx* c, int a, int max_steps, double atol, int crit_abs, c
     };
     if (ck && (ck->W || ck->C)) fixed_wc = true;
     constrain(t);
+    if (k > 0) {   // deflation vectors w_1..w_k, c_1..c_k on the device
+      HIPCHK(c, hipMemcpyAsync(dev.Wp, Wp.data(), sizeof(double) * Wp.size(), hipMemcpyHostToDevice, c->stream));
+      HIPCHK(c, hipMemcpyAsync(dev.Cp, Cp.data(), sizeof(double) * Cp.size(), hipMemcpyHostToDevice, c->stream));
+    }
+    // PPLSi's EM loop (:147-173) on the device; i = the reference's final i (steps made)
     double G[4];
-    if ((rc = rank1_sweep(c, t, Wp, Cp, k, SX, SY, G))) return rc;
-    std::vector<double> lv(1, rank1_loglik(t, G, ssqX, ssqY, N, p, q));   // logvalue[1] (:149)
+    std::vector<double> lv;
     int i = 0;
     bool na = false;
-    for (i = 1; i <= max_steps; ++i) {                                    // :151
-      if (t.sigE < tiny || t.sigF < tiny) { na = true; break; }           // :152-154
-      t = rank1_update(t, SX, SY, G, ssqX, ssqY, N, p, q, Wp, Cp, k);     // :156-164
-      constrain(t);                                                       // :165-169
-      if ((rc = rank1_sweep(c, t, Wp, Cp, k, SX, SY, G))) return rc;
-      lv.push_back(rank1_loglik(t, G, ssqX, ssqY, N, p, q));              // :172
-      const double incr = lv[i] - lv[i - 1];
-      if ((crit_abs ? std::fabs(incr) : incr) < atol) break;              // critfunc(.) < atol (:173)
-    }
+    if ((rc = rank1_fit_device(c, dev, t, ck, k, ssqX, ssqY, max_steps, atol, crit_abs, Wp, Cp, lv, &i, &na, G)))
+      return rc;
     if (na) break;   // PPLS: "residuals are of rank < 1e-14", keep components 1..k-1 (:258-263)
     if (i > max_steps) i = max_steps;
     for (int e = 0; e < p; ++e) out->W[(size_t)k * p + e] = t.w[e];

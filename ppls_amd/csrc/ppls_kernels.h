@@ -63,6 +63,32 @@ struct PplsFinalizeArgs {
   double atol;
 };
 
+// One EM step of the sequential initialiser's rank-1 fit on the device (ppls_rank1_step_kernel).
+struct PplsRank1StepArgs {
+  const double* stats;     // the sweep's reduced statistics [SX ldx][SY ldy][G 4]
+  int p, q, ldx, ldy;
+  double N, ssqX, ssqY;    // ssq of the deflated data
+  const double* Wp;        // deflation vectors w_1..w_m (p x m) and c_1..c_m (q x m)
+  const double* Cp;
+  int m;
+  PplsRank1* st;           // the component's scalars (in/out)
+  double* tw;              // its unit loadings w (p), c (q) (in/out)
+  double* tc;
+  const double* consW;     // fixed loadings (fconstraint) or nullptr
+  const double* consC;
+  PplsRank1 cons_val;      // fixed scalars, selected by cons_mask bits 0 B, 1 sigE, 2 sigF, 3 sigH, 4 sigT
+  int cons_mask;
+  double* Wdst;            // the next sweep's weight P_0..P_{m-1} w (ldx), P_0..P_{m-1} c (ldy), scalars
+  double* Cdst;
+  PplsScalars* scdst;
+  double* lv;              // logvalue[0..max_steps]
+  double* Gkeep;           // 4: the Gram of the last sweep that was not skipped
+  int step, max_steps, crit_abs;
+  double atol;
+  int* stop;               // [0] step the stop rule fired at, [1] rank collapse (sigma < 100 eps)
+  int* stop_mirror;        // host-mapped: nonzero once the fit ended
+};
+
 extern "C" {
 int ppls_split_supported(int r, int ldx, int ldy);
 hipError_t ppls_launch_sweep_split(const PplsSweepArgs* a, hipStream_t st);
@@ -95,6 +121,7 @@ hipError_t ppls_launch_convert(const void* src, int src_f32, void* dst, int dst_
 hipError_t ppls_launch_generate(int64_t n_local, int64_t row0, int p, int q, int ldx, int ldy, int r,
                                 const PplsScalars* truth, const double* Wt, const double* Ct,
                                 uint64_t seed, double* TU, double* X, double* Y, hipStream_t st);
+hipError_t ppls_launch_rank1_step(const PplsRank1StepArgs* a, hipStream_t st);
 hipError_t ppls_launch_philox(const uint32_t* ctr, int64_t count, uint64_t key, uint32_t* out, hipStream_t st);
 hipError_t ppls_launch_to_rowmajor(const double* src, int64_t n, int p, int ld, double* dst,
                                    hipStream_t st);

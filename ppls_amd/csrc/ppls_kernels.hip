@@ -1840,6 +1840,105 @@ __global__ __launch_bounds__(256) void ppls_finalize_generic_kernel(
   }
 }
 
+// ============================================================================ initialiser step
+// Loading update of one rank-1 EM step (EMstepC_fast, src/loglC.cpp:355, :383): t = S (the sweep's
+// X'mu_T over the undeflated data), deflated t = P_{m-1}..P_0 t (= Xc'mu_T), t /= N, normalised --
+// or the fixed loading of an fconstraint -- then the next sweep's weight dst = P_0..P_{m-1} t
+// (so the sweep over X computes Xc t).  Every thread keeps its own indices i = tid + k * nt, so
+// only the block sums synchronise.
+__device__ void ppls_rank1_loading(const double* __restrict__ S, int n, double* __restrict__ t,
+                                   const double* __restrict__ Wp, int m, double N, const double* __restrict__ fixed,
+                                   double* __restrict__ dst, int ld, double* sh) {
+  const int tid = threadIdx.x, nt = blockDim.x;
+  double v[1];
+  if (fixed) {
+    for (int i = tid; i < n; i += nt) t[i] = fixed[i];
+  } else {
+    for (int i = tid; i < n; i += nt) t[i] = S[i];
+    for (int j = 0; j < m; ++j) {
+      const double* w = Wp + (int64_t)j * n;
+      v[0] = 0.0;
+      for (int i = tid; i < n; i += nt) v[0] = fma(w[i], t[i], v[0]);
+      ppls_block_sum(v, 1, sh);
+      const double d = v[0];
+      for (int i = tid; i < n; i += nt) t[i] -= d * w[i];
+    }
+    v[0] = 0.0;
+    for (int i = tid; i < n; i += nt) {
+      t[i] /= N;
+      v[0] = fma(t[i], t[i], v[0]);
+    }
+    ppls_block_sum(v, 1, sh);
+    const double nrm = sqrt(v[0]);
+    for (int i = tid; i < n; i += nt) t[i] /= nrm;
+  }
+  for (int i = tid; i < ld; i += nt) dst[i] = i < n ? t[i] : 0.0;
+  for (int jj = 0; jj < m; ++jj) {
+    const double* w = Wp + (int64_t)(m - 1 - jj) * n;
+    v[0] = 0.0;
+    for (int i = tid; i < n; i += nt) v[0] = fma(w[i], dst[i], v[0]);
+    ppls_block_sum(v, 1, sh);
+    const double d = v[0];
+    for (int i = tid; i < n; i += nt) dst[i] -= d * w[i];
+  }
+}
+
+// One EM step of PPLSi (EM_W_multi.R:151-173) on the device, after the sweep of the current
+// component t: logvalue[step] = logl_W(t) from the sweep's Gram (:149, :172); the stop rule
+// critfunc(logvalue[i] - logvalue[i-1]) < atol (:173); the sigma < 100 eps guard (:152-154); then
+// EMstepC_fast's update (scalars ppls_rank1_scalars, loadings above), the constraints (:165-169)
+// and the next sweep's weights and scalars.  Once the fit has ended, every later sweep and step
+// kernel of it exits at once (the stop flag).
+__global__ __launch_bounds__(1024) void ppls_rank1_step_kernel(PplsRank1StepArgs a) {
+  __shared__ double sh[16 * PPLS_RMAX];
+  __shared__ int s_exit;
+  __shared__ PplsRank1 s_new;
+  const int tid = threadIdx.x;
+  if (a.stop[0] || a.stop[1]) return;
+  if (tid == 0) {
+    const double* Gs = a.stats + a.ldx + a.ldy;
+    const double G[4] = {Gs[0], Gs[1], Gs[2], Gs[3]};
+    const PplsRank1 t = *a.st;
+    const double l = ppls_rank1_loglik(&t, G, a.ssqX, a.ssqY, a.N, a.p, a.q);
+    a.lv[a.step] = l;
+    for (int e = 0; e < 4; ++e) a.Gkeep[e] = G[e];
+    int ex = 0;
+    if (a.step >= 1) {
+      const double incr = l - a.lv[a.step - 1];
+      if ((a.crit_abs ? fabs(incr) : incr) < a.atol) {
+        a.stop[0] = a.step;
+        ex = 1;
+      }
+    }
+    if (!ex && a.step >= a.max_steps) ex = 1;
+    const double tiny = 100.0 * 2.220446049250313e-16;   // 100 * .Machine$double.eps
+    if (!ex && (t.sigE < tiny || t.sigF < tiny)) {
+      a.stop[1] = 1;
+      ex = 1;
+    }
+    if (ex && a.stop_mirror) __hip_atomic_store(a.stop_mirror, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (!ex) {
+      PplsRank1 n;
+      ppls_rank1_scalars(&t, G, a.ssqX, a.ssqY, a.N, a.p, a.q, &n);
+      if (a.cons_mask & 1) n.B = a.cons_val.B;
+      if (a.cons_mask & 2) n.sigE = a.cons_val.sigE;
+      if (a.cons_mask & 4) n.sigF = a.cons_val.sigF;
+      if (a.cons_mask & 8) n.sigH = a.cons_val.sigH;
+      if (a.cons_mask & 16) n.sigT = a.cons_val.sigT;
+      s_new = n;
+    }
+    s_exit = ex;
+  }
+  __syncthreads();
+  if (s_exit) return;
+  ppls_rank1_loading(a.stats, a.p, a.tw, a.Wp, a.m, a.N, a.consW, a.Wdst, a.ldx, sh);
+  ppls_rank1_loading(a.stats + a.ldx, a.q, a.tc, a.Cp, a.m, a.N, a.consC, a.Cdst, a.ldy, sh);
+  if (tid == 0) {
+    *a.st = s_new;
+    ppls_rank1_sweep_scalars(&s_new, a.scdst);
+  }
+}
+
 // loglC_fast from explicit coefficients (the drop-in of src/loglC.cpp:318-338).
 __global__ void ppls_loglc_kernel(const double* __restrict__ G, const double* __restrict__ ssq, double N,
                                   int p, int q, int r, double sigX, double sigY,
@@ -2204,6 +2303,11 @@ hipError_t ppls_launch_finalize(const PplsFinalizeArgs* f, hipStream_t st) {
                          f->stop, f->stop_mirror, f->stop_check, f->stop_step, f->atol);
       return hipGetLastError();
   }
+}
+
+hipError_t ppls_launch_rank1_step(const PplsRank1StepArgs* a, hipStream_t st) {
+  hipLaunchKernelGGL(ppls_rank1_step_kernel, dim3(1), dim3(1024), 0, st, *a);
+  return hipGetLastError();
 }
 
 hipError_t ppls_launch_loglc(const double* G, const double* ssq, double N, int p, int q, int r,

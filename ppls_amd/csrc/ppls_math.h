@@ -254,6 +254,75 @@ PPLS_HD void ppls_mstep_scalars(const PplsMoments* m, int r, PplsScalars* nx) {
   ppls_mu_coef(nx, r);
 }
 
+// ---- rank-1 EM step of the sequential initialiser (EMstep_W EM_W_multi.R:51-73 ->
+// EMstepC_fast src/loglC.cpp:340-397; meta_Estep / meta_Mstep loglC.cpp:399-474 restate the same
+// formulas).  Scalars of one component; the loadings live beside them.
+struct PplsRank1 {
+  double B, sigE, sigF, sigH, sigT;
+};
+
+// EMstep_W's coefficients (:60-70) and EMstepC_fast's mu coefficients (:354, :358).
+PPLS_HD void ppls_rank1_coefs(const PplsRank1* t, double* c1, double* c2, double* c3, double* al, double* be,
+                              double* ga, double* de) {
+  ppls_coef_estep(t->sigT, t->B, t->sigE, t->sigF, t->sigH, c1, c2, c3, nullptr);
+  const double s2X = t->sigE * t->sigE, s2Y = t->sigF * t->sigF, s2H = t->sigH * t->sigH;
+  const double s2T = t->sigT * t->sigT, B = t->B, v = s2T * B * B + s2H;
+  *al = s2T * (-*c1 + -*c2 * B + 1 / s2X);
+  *be = s2T * (-*c2 + -*c3 * B + 1 / s2Y * B);
+  *ga = -s2T * B * *c1 + -*c2 * v + 1 / s2X * B * s2T;
+  *de = -*c2 * B * s2T + -*c3 * v + 1 / s2Y * v;
+}
+
+// PplsScalars (r = 1) the sweep consumes for component t.
+PPLS_HD void ppls_rank1_sweep_scalars(const PplsRank1* t, PplsScalars* s) {
+  for (int k = 0; k < PPLS_RMAX; ++k) s->b[k] = s->t[k] = s->alpha[k] = s->beta[k] = s->gamma[k] = s->delta[k] = 0.0;
+  s->b[0] = t->B;
+  s->t[0] = t->sigT;
+  s->sigE = t->sigE;
+  s->sigF = t->sigF;
+  s->sigH = t->sigH;
+  s->pad0 = 0.0;
+  double c1, c2, c3;
+  ppls_rank1_coefs(t, &c1, &c2, &c3, &s->alpha[0], &s->beta[0], &s->gamma[0], &s->delta[0]);
+}
+
+// logl_W(Xc, Yc, w, c, B, sigE, sigF, sigH, sigT) from the sweep's 2 x 2 Gram (:297-323, r = 1).
+PPLS_HD double ppls_rank1_loglik(const PplsRank1* t, const double G[4], double ssqX, double ssqY, double N,
+                                 int64_t p, int64_t q) {
+  PplsScalars s;
+  ppls_rank1_sweep_scalars(t, &s);
+  return ppls_loglik_from_gram(G, ssqX, ssqY, N, p, q, 1, &s);
+}
+
+// The rank-1 E-step moments and M-step scalars from one sweep's Gram G = [||Xw||^2, <Xw,Yc>, ., ||Yc||^2]:
+// B = Cut/Ctt, sighat = (sqrt(Cee), sqrt(Cff)), siglathat = (sqrt(Chh), sqrt(Ctt)).
+PPLS_HD void ppls_rank1_scalars(const PplsRank1* t, const double G[4], double ssqX, double ssqY, double N,
+                                int64_t p, int64_t q, PplsRank1* n) {
+  double c1, c2, c3, al, be, ga, de;
+  ppls_rank1_coefs(t, &c1, &c2, &c3, &al, &be, &ga, &de);
+  const double s2X = t->sigE * t->sigE, s2Y = t->sigF * t->sigF, s2H = t->sigH * t->sigH;
+  const double s2T = t->sigT * t->sigT, B = t->B, v = s2T * B * B + s2H;
+  const double A = G[0], D = G[1], Bm = G[3];   // ||Xw||^2, <Xw, Yc>, ||Yc||^2
+  const double mt2 = al * al * A + 2.0 * al * be * D + be * be * Bm;
+  const double mut = ga * al * A + (ga * be + de * al) * D + de * be * Bm;
+  const double Ctt = s2T - s2T * s2T * (-c1 - 2 * B * c2 - B * B * (c3 - 1 / s2Y) + 1 / s2X) + mt2 / N;   // :356
+  const double Cut = s2T * B - (-s2T * s2T * B * (c1 - 1 / s2X) - s2T * s2T * B * B * c2 - s2T * v * c2 -
+                                v * s2T * B * (c3 - 1 / s2Y)) + mut / N;                              // :363
+  const double Ceetmp = c1 * c1 * s2X * s2X * A + ssqX + c2 * c2 * s2X * s2X * Bm - 2 * c1 * s2X * A +
+                        2 * c1 * c2 * s2X * s2X * D - 2 * c2 * s2X * D;                                // :365-366
+  const double Cee = s2X - (-s2X * s2X * c1 + (double)p * s2X) / (double)p + Ceetmp / N / (double)p;   // :367
+  const double Cfftmp = c3 * c3 * s2Y * s2Y * Bm + ssqY + c2 * c2 * s2Y * s2Y * A - 2 * c3 * s2Y * Bm +
+                        2 * c3 * c2 * s2Y * s2Y * D - 2 * c2 * s2Y * D;                                // :369-370
+  const double Cff = s2Y - (-s2Y * s2Y * c3 + (double)q * s2Y) / (double)q + Cfftmp / N / (double)q;   // :371
+  const double hx = -c2 * s2H, hy = -(c3 - 1 / s2Y) * s2H;
+  const double Chh = s2H - (-s2H * s2H * (c3 - 1 / s2Y)) + (hx * hx * A + 2 * hx * hy * D + hy * hy * Bm) / N;  // :373
+  n->B = Cut / Ctt;         // :385
+  n->sigE = sqrt(Cee);      // sighat (:376)
+  n->sigF = sqrt(Cff);
+  n->sigH = sqrt(Chh);      // siglathat (:377)
+  n->sigT = sqrt(Ctt);
+}
+
 // Polar factor U_R V_R' of a small r x r matrix R (column-major, ld r) by one-sided (Hestenes)
 // Jacobi: R V = U S.  Returns 0 on success, -1 if R is numerically rank deficient.
 // P (r x r, column-major) receives U_R V_R'.
