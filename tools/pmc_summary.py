@@ -1,6 +1,10 @@
 """HBM traffic per sweep launch from the rocprofv3 PMC passes written by tools/profile.sh.
 
-    python tools/pmc_summary.py <tag> <workload> <algorithmic_bytes_per_launch> [note]
+    python tools/pmc_summary.py <tag> <workload> <algorithmic_bytes_per_launch> [note] [--kernels a,b]
+
+--kernels: substrings of the kernels that make up one sweep (default "sweep"); the per-launch
+traffic of each is averaged over its dispatches and the sweep's traffic is their sum (the wide-p
+panel sweep is two kernels: panel_mfmadots + panel_acc).
 
 Reads gpurun_out/prof_<tag>/pmc_{FETCH_SIZE,WRITE_SIZE}/run_counter_collection.csv and writes
 profiles/pmc_sweep_<workload>.json.  gfx950 correction (MI355X_MICROARCH.md, HBM section):
@@ -16,23 +20,36 @@ from collections import defaultdict
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def per_launch(path, counter):
-    acc = defaultdict(float)
-    for r in csv.DictReader(open(path)):
-        if "sweep" in r["Kernel_Name"] and r["Counter_Name"] == counter:
-            acc[(r["Kernel_Name"], r["Dispatch_Id"])] += float(r["Counter_Value"])
-    names = {k[0] for k in acc}
-    return names, len(acc), sum(acc.values()) / max(len(acc), 1)
+def per_launch(path, counter, subs=("sweep",)):
+    """Sum over the kernels matching subs of the kernel's average counter value per dispatch."""
+    total, names, launches = 0.0, set(), 0
+    for sub in subs:
+        acc = defaultdict(float)
+        for r in csv.DictReader(open(path)):
+            if sub in r["Kernel_Name"] and r["Counter_Name"] == counter:
+                acc[(r["Kernel_Name"], r["Dispatch_Id"])] += float(r["Counter_Value"])
+        names |= {k[0] for k in acc}
+        launches = max(launches, len(acc))
+        total += sum(acc.values()) / max(len(acc), 1)
+    return names, launches, total
 
 
 def main():
-    tag, workload, alg = sys.argv[1], sys.argv[2], int(float(sys.argv[3]))
-    note = sys.argv[4] if len(sys.argv) > 4 else ""
+    args = list(sys.argv[1:])
+    subs = ("sweep",)
+    if "--kernels" in args:
+        i = args.index("--kernels")
+        subs = tuple(args[i + 1].split(","))
+        del args[i:i + 2]
+    tag, workload, alg = args[0], args[1], int(float(args[2]))
+    note = args[3] if len(args) > 3 else ""
     base = os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
-    names, n, fetch = per_launch(os.path.join(base, "pmc_FETCH_SIZE", "run_counter_collection.csv"), "FETCH_SIZE")
-    _, _, write = per_launch(os.path.join(base, "pmc_WRITE_SIZE", "run_counter_collection.csv"), "WRITE_SIZE")
+    names, n, fetch = per_launch(os.path.join(base, "pmc_FETCH_SIZE", "run_counter_collection.csv"), "FETCH_SIZE",
+                                 subs)
+    _, _, write = per_launch(os.path.join(base, "pmc_WRITE_SIZE", "run_counter_collection.csv"), "WRITE_SIZE", subs)
     hbm = 2.0 * fetch * 1024 + write * 1024
-    out = dict(workload=workload, kernel=sorted(names)[0].split("(")[0] if names else None, launches=n,
+    out = dict(workload=workload, kernel=" + ".join(sorted(k.split("(")[0] for k in names)) if names else None,
+               launches=n,
                FETCH_SIZE_kB_per_launch=fetch, WRITE_SIZE_kB_per_launch=write,
                correction="gfx950: FETCH_SIZE counts half the bytes of 16 B/lane streaming reads "
                           "(MI355X_MICROARCH.md, HBM): read bytes = 2 x FETCH_SIZE x 1024; WRITE_SIZE exact",
