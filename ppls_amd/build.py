@@ -17,6 +17,9 @@ ARCH = os.environ.get("PPLS_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 SOURCES = ["ppls_kernels.hip", "ppls_variances.hip", "ppls_capi.cpp"]
+# Per-file flags.  ppls_kernels.hip: the panel dots kernel keeps its MFMA accumulators in VGPRs
+# (the default AGPR form copied them VGPR <-> AGPR on every tile; its only MFMA user).
+FILE_FLAGS = {"ppls_kernels.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"]}
 HEADERS = ["ppls_kernels.h", "ppls_math.h", "ppls_device.h"]
 CFLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function", "-Wno-inline-asm",
           "-I" + os.path.join(ROOT, "include"), "-I" + CSRC]
@@ -36,7 +39,7 @@ def build(force: bool = False, verbose: bool = True) -> str:
         o = os.path.join(BUILD, os.path.splitext(src)[0] + ".o")
         objs.append(o)
         if force or _mtime(o) < max(_mtime(s), newest_dep):
-            cmd = [HIPCC, *CFLAGS, "-x", "hip", "-c", s, "-o", o]
+            cmd = [HIPCC, *CFLAGS, *FILE_FLAGS.get(src, []), "-x", "hip", "-c", s, "-o", o]
             if verbose:
                 print(" ".join(cmd), flush=True)
             procs.append((subprocess.Popen(cmd), o))

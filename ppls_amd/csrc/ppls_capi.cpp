@@ -496,8 +496,10 @@ int alloc_data(ppls_ctx* c, int64_t n_local, int p, int q, int64_t n_total) {
   c->ldy = ld_of(q, c->dtype);
   // X, Y storage (fp64, or fp32 packed into the double allocation)
   const size_t es = c->dtype ? 4 : 8;
-  if ((rc = dalloc(c, &c->X, ((size_t)std::max<int64_t>(n_local, 1) * c->ldx * es + 7) / 8))) return rc;
-  if ((rc = dalloc(c, &c->Y, ((size_t)std::max<int64_t>(n_local, 1) * c->ldy * es + 7) / 8))) return rc;
+  // + 64 doubles of slack: the panel dots kernel reads whole 128-B column tiles, so the last row's
+  // partial tile may run past the end (those values meet zero rows of the transposed W)
+  if ((rc = dalloc(c, &c->X, ((size_t)std::max<int64_t>(n_local, 1) * c->ldx * es + 7) / 8 + 64))) return rc;
+  if ((rc = dalloc(c, &c->Y, ((size_t)std::max<int64_t>(n_local, 1) * c->ldy * es + 7) / 8 + 64))) return rc;
   if (!c->ssq && (rc = dalloc(c, &c->ssq, 2))) return rc;
   c->r_alloc = 0;   // force per-r buffers to be re-sized for the new shape
   dfree(c->part);
@@ -653,8 +655,8 @@ int ppls_set_option(ppls_ctx* c, const char* key, int64_t value) {
   } else if (!strcmp(key, "pipe")) {
     c->pipe_opt = value ? 1 : 0;
   } else if (!strcmp(key, "ablate")) {
-    if (value < 0 || value > 1023) return fail(c, PPLS_E_ARG, "ablate must be in [0,1023]");
-    c->ablate = (int)value;   // timing experiments only: results are wrong while set
+    if (value < 0 || value > 65535) return fail(c, PPLS_E_ARG, "ablate must be in [0,65535]");
+    c->ablate = (int)value;   // timing experiments (bits 0-9 break results; 10+ select equivalent variants)
   } else if (!strcmp(key, "ftrace")) {
     if (value && !c->ftrace) {
       HIPCHK(c, hipMalloc(&c->ftrace, PPLS_FTRACE_LEN * sizeof(long long)));

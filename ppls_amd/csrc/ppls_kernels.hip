@@ -636,15 +636,17 @@ struct PplsVec16 {   // one 16-B load of T
   T v[N];
 };
 
-template <typename T>
+template <typename T, bool NT = false>
 __device__ __forceinline__ PplsVec16<T> ppls_load16(const T* p) {
   PplsVec16<T> r;
   if constexpr (sizeof(T) == 8) {
-    const double2 d = *(const double2*)p;
+    typedef double d2v __attribute__((ext_vector_type(2)));
+    const d2v d = NT ? __builtin_nontemporal_load((const d2v*)p) : *(const d2v*)p;
     r.v[0] = d.x;
     r.v[1] = d.y;
   } else {
-    const float4 f = *(const float4*)p;
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    const f4v f = NT ? __builtin_nontemporal_load((const f4v*)p) : *(const f4v*)p;
     r.v[0] = f.x;
     r.v[1] = f.y;
     r.v[2] = f.z;
@@ -673,6 +675,7 @@ __global__ __launch_bounds__(256) void ppls_panel_mfmadots_kernel(
     const int* __restrict__ stop) {
   if (stop && *stop) return;   // em_run converged earlier (device stop flag)
   typedef double d4 __attribute__((ext_vector_type(4)));
+  typedef float f4 __attribute__((ext_vector_type(4)));
   constexpr int ES = (int)sizeof(T);
   constexpr int KT = 128 / ES;        // columns per tile
   constexpr int KQ = KT / 4;          // MFMA steps per tile (columns per lane group)
@@ -704,20 +707,41 @@ __global__ __launch_bounds__(256) void ppls_panel_mfmadots_kernel(
         src[u] = M + rr * ld + lchunk * (16 / ES);
       }
       const int ntc = (ld + KT - 1) / KT;
-      float4 buf[4];
-      auto load_tile = [&](int tc) {
-        const int c0 = tc * KT + lchunk * (16 / ES);
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-          buf[u] = (c0 < ld) ? *(const float4*)(src[u] + tc * KT) : make_float4(0.f, 0.f, 0.f, 0.f);
+      // Loads are unconditional (no exec-mask branches, so the waitcnts stay precise): a partial
+      // last tile reads past the row end into the next row (or the allocation's slack after the
+      // last row), which meets the zero rows of Wt beyond ld and adds exactly 0; prefetches past
+      // the last tile re-read it.  Issue order per tile: this tile's B operands, then the next
+      // tile's X loads, so the MFMAs wait only for B while the next tile streams in.
+      f4 xa0, xa1, xa2, xa3;
+      auto ld4 = [&](const T* p) -> f4 { return *(const f4*)p; };   // (non-temporal: 16 % slower here)
+      auto load_tile = [&](int tc, f4& b0, f4& b1, f4& b2, f4& b3) {
+        const int c = tc < ntc ? tc : ntc - 1;
+        b0 = ld4(src[0] + c * KT);
+        b1 = ld4(src[1] + c * KT);
+        b2 = ld4(src[2] + c * KT);
+        b3 = ld4(src[3] + c * KT);
       };
-      load_tile(0);
-      for (int tc = 0; tc < ntc; ++tc) {
+      // B operand of lane l at k-step s: W[tile column kq KQ + s][i16] (Wt: 16 zero-padded columns,
+      // k-steps in pairs: one 16-B load per two steps)
+      const double* wb0 = Wm + (int64_t)kq * KQ * 16 + 2 * i16;   // pair layout (transpose kernel)
+      auto step = [&](int tc, f4& b0, f4& b1, f4& b2, f4& b3) {
         char* wl = lds + (wave * 2 + (tc & 1)) * RB * RS;
+        *(f4*)(wl + lrow * RS + lchunk * 16) = b0;
+        *(f4*)(wl + (lrow + 8) * RS + lchunk * 16) = b1;
+        *(f4*)(wl + (lrow + 16) * RS + lchunk * 16) = b2;
+        *(f4*)(wl + (lrow + 24) * RS + lchunk * 16) = b3;
+        asm volatile("" ::: "memory");   // keep the loads below after the stores (buf is reused)
+        double b[KQ];
+        const double* wb = wb0 + (int64_t)tc * KT * 16;
 #pragma unroll
-        for (int u = 0; u < 4; ++u) *(float4*)(wl + (lrow + 8 * u) * RS + lchunk * 16) = buf[u];
+        for (int s2 = 0; s2 < KQ; s2 += 2) {
+          const double2 w2 = *(const double2*)(wb + s2 * 16);
+          b[s2] = w2.x;
+          b[s2 + 1] = w2.y;
+        }
+        asm volatile("" ::: "memory");   // B before the next tiles' X in the vmcnt order
+        load_tile(tc + 1, b0, b1, b2, b3);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if (tc + 1 < ntc) load_tile(tc + 1);
         // A operands: rows i16 and 16 + i16, columns [kq KQ, kq KQ + KQ) of the tile
         T a0[KQ], a1[KQ];
 #pragma unroll
@@ -732,17 +756,14 @@ __global__ __launch_bounds__(256) void ppls_panel_mfmadots_kernel(
             a1[h * (16 / ES) + u] = p1[u];
           }
         }
-        // B operands: W[tile column kq KQ + s][i16] (zero for i16 >= R; Wt rows padded)
-        const double* wb = Wm + ((int64_t)tc * KT + kq * KQ) * R + comp;
-        double b[KQ];
-#pragma unroll
-        for (int s2 = 0; s2 < KQ; ++s2) b[s2] = i16 < R ? wb[s2 * R] : 0.0;
 #pragma unroll
         for (int s2 = 0; s2 < KQ; ++s2) {
           acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64((double)a0[s2], b[s2], acc0, 0, 0, 0);
           acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64((double)a1[s2], b[s2], acc1, 0, 0, 0);
         }
-      }
+      };
+      load_tile(0, xa0, xa1, xa2, xa3);
+      for (int tc = 0; tc < ntc; ++tc) step(tc, xa0, xa1, xa2, xa3);
       res[mat][0] = acc0;
       res[mat][1] = acc1;
     }
@@ -769,25 +790,27 @@ __global__ __launch_bounds__(256) void ppls_panel_mfmadots_kernel(
   }
 }
 
-// W (ldx x R, column-major) -> Wt (ldxp x R, row-major, rows >= ldx zero); same for C.
+// W (ldx x r, column-major) -> Wt (ldxp x rs: rows >= ldx and columns >= r zero, pair layout below); C alike.
 __global__ void ppls_transpose_wc_kernel(const double* __restrict__ W, const double* __restrict__ C,
-                                         int ldx, int ldy, int ldxp, int ldyp, int r, double* __restrict__ Wt,
+                                         int ldx, int ldy, int ldxp, int ldyp, int r, int rs, double* __restrict__ Wt,
                                          double* __restrict__ Ct,
     const int* __restrict__ stop) {
   if (stop && *stop) return;   // em_run converged earlier (device stop flag)
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t nx = (int64_t)ldxp * r;
+  const int64_t nx = (int64_t)ldxp * rs;
+  // pair layout: rows 2m, 2m + 1 interleaved per component, element (i, k) at
+  // (i >> 1) * 2 rs + 2 k + (i & 1), so one 16-B load gives a lane two consecutive k-steps
   if (e < nx) {
-    const int i = (int)(e / r), k = (int)(e % r);
-    Wt[e] = i < ldx ? W[(int64_t)k * ldx + i] : 0.0;
-  } else if (e < nx + (int64_t)ldyp * r) {
+    const int i = (int)(e / rs), k = (int)(e % rs);
+    Wt[(int64_t)(i >> 1) * 2 * rs + 2 * k + (i & 1)] = (i < ldx && k < r) ? W[(int64_t)k * ldx + i] : 0.0;
+  } else if (e < nx + (int64_t)ldyp * rs) {
     const int64_t f = e - nx;
-    const int i = (int)(f / r), k = (int)(f % r);
-    Ct[f] = i < ldy ? C[(int64_t)k * ldy + i] : 0.0;
+    const int i = (int)(f / rs), k = (int)(f % rs);
+    Ct[(int64_t)(i >> 1) * 2 * rs + 2 * k + (i & 1)] = (i < ldy && k < r) ? C[(int64_t)k * ldy + i] : 0.0;
   }
 }
 
-template <typename T, int R>
+template <typename T, int R, bool NT>
 __global__ __launch_bounds__(256) void ppls_panel_acc_kernel(
     const T* __restrict__ X, const T* __restrict__ Y, int64_t n, int ldx, int ldy,
     const double* __restrict__ Z, int64_t rows_per_chunk, double* __restrict__ part, int64_t part_ld,
@@ -850,7 +873,7 @@ __global__ __launch_bounds__(256) void ppls_panel_acc_kernel(
       PplsVec16<T> xa[8], xb[8];
       auto load8 = [&](int rr, PplsVec16<T> (&xv)[8]) {
 #pragma unroll
-        for (int u = 0; u < 8; ++u) xv[u] = ppls_load16(base + (b0 + min(rr + u, nb - 1)) * ld);
+        for (int u = 0; u < 8; ++u) xv[u] = ppls_load16<T, NT>(base + (b0 + min(rr + u, nb - 1)) * ld);
       };
       auto fma8 = [&](int rr, const PplsVec16<T> (&xv)[8]) {
 #pragma unroll
@@ -2132,11 +2155,12 @@ template <typename T, int R>
 hipError_t launch_panel_t(const PplsSweepArgs* a, const T* X, const T* Y, double* Z, int chunks, hipStream_t st) {
   // transposed W, C behind Z (see ppls_panel_z_len), rows padded to whole 32-column tiles
   const int ldxp = (a->ldx + 31) & ~31, ldyp = (a->ldy + 31) & ~31;
+  const int rs = 16;   // the MFMA's B operand: 16 component columns, zero beyond R
   double* Wt = Z + a->n_local * 4 * R;
-  double* Ct = Wt + (int64_t)ldxp * R;
-  const int64_t ne = (int64_t)(ldxp + ldyp) * R;
+  double* Ct = Wt + (int64_t)ldxp * rs;
+  const int64_t ne = (int64_t)(ldxp + ldyp) * rs;
   hipLaunchKernelGGL(ppls_transpose_wc_kernel, dim3((unsigned)((ne + 255) / 256)), dim3(256), 0, st, a->Wp,
-                     a->Cp, a->ldx, a->ldy, ldxp, ldyp, R, Wt, Ct, a->stop);
+                     a->Cp, a->ldx, a->ldy, ldxp, ldyp, R, rs, Wt, Ct, a->stop);
   {   // MFMA dots (profiles/r1_c5_*_dots_variants.txt: faster than the VALU and LDS-DMA forms)
     const int64_t wtiles = (a->n_local + 31) / 32;
     const int mblocks = (int)((wtiles + 3) / 4 < 16384 ? (wtiles + 3) / 4 : 16384);
@@ -2149,8 +2173,14 @@ hipError_t launch_panel_t(const PplsSweepArgs* a, const T* X, const T* Y, double
   // VALU accumulation: at C5 an MFMA form measured no faster in fp64 storage (7.7 vs 7.5 ms) and
   // slower in fp32 (6.0 vs 4.5 ms; profiles/r1_c5_*_acc_variants.txt) -- the pass is load-bound
   const int ntx = (a->ldx + 256 * VEC - 1) / (256 * VEC), nty = (a->ldy + 256 * VEC - 1) / (256 * VEC);
-  hipLaunchKernelGGL((ppls_panel_acc_kernel<T, R>), dim3(ntx + nty, chunks), dim3(256), 0, st, X, Y,
-                     a->n_local, a->ldx, a->ldy, Z, rpc, a->part, a->part_ld, a->stop);
+  // the accumulation pass's once-read stream: non-temporal loads where X, Y exceed the MALL (the
+  // sweep's nt policy, ablate bit 16): C5 fp32 4.05 -> 3.89 ms (profiles/r2_c5_nt_policy.txt)
+  if (a->ablate & 16)
+    hipLaunchKernelGGL((ppls_panel_acc_kernel<T, R, true>), dim3(ntx + nty, chunks), dim3(256), 0, st, X, Y,
+                       a->n_local, a->ldx, a->ldy, Z, rpc, a->part, a->part_ld, a->stop);
+  else
+    hipLaunchKernelGGL((ppls_panel_acc_kernel<T, R, false>), dim3(ntx + nty, chunks), dim3(256), 0, st, X, Y,
+                       a->n_local, a->ldx, a->ldy, Z, rpc, a->part, a->part_ld, a->stop);
   return hipGetLastError();
 }
 
@@ -2179,7 +2209,7 @@ hipError_t launch_panel_dt(const PplsSweepArgs* a, const T* X, const T* Y, doubl
 
 template <typename T, int R>
 hipError_t acc_occ_t(int* occ) {
-  return hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, (const void*)ppls_panel_acc_kernel<T, R>, 256, 0);
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(occ, (const void*)ppls_panel_acc_kernel<T, R, false>, 256, 0);
 }
 
 template <typename T>
@@ -2212,7 +2242,7 @@ hipError_t panel_acc_occupancy(int dtype_f32, int r, int* occ) {
 extern "C" {
 
 int64_t ppls_panel_z_len(int64_t n_local, int ldx, int ldy, int r) {
-  return (n_local > 0 ? n_local : 1) * 4 * r + (int64_t)(((ldx + 31) & ~31) + ((ldy + 31) & ~31)) * r;
+  return (n_local > 0 ? n_local : 1) * 4 * r + (int64_t)(((ldx + 31) & ~31) + ((ldy + 31) & ~31)) * 16;
 }
 
 int ppls_panel_chunks(int64_t n_local, int ldx, int ldy, int num_cus, int dtype_f32, int r) {

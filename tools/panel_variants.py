@@ -1,0 +1,48 @@
+"""Time the wide-p panel sweep under experiment switches (set_option("ablate", bits)).
+
+    python tools/panel_variants.py [c5|c5d] bits [bits ...]
+
+For each bits value: 2 warm-up EM iterations, then 8 timed ones; prints the average sweep time
+(HIP events around every sweep launch) and the EM iterations/s.  Run it under
+rocprofv3 --kernel-trace --stats for the per-kernel split."""
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from bench import CONFIGS, make_truth_and_theta0  # noqa: E402
+from ppls_amd import Context  # noqa: E402
+
+
+def main():
+    cfgname = sys.argv[1]
+    bits = [int(b, 0) for b in sys.argv[2:]] or [0]
+    cfg = CONFIGS[cfgname]
+    n, p, q, r = cfg["n"], cfg["p"], cfg["q"], cfg["r"]
+    ctx = Context(0)
+    if cfg.get("storage") == "f32":
+        ctx.set_option("dtype", 1)
+    truth, th0 = make_truth_and_theta0(p, q, r)
+    ctx.generate_synthetic(n, p, q, truth, seed=20261015)
+    for b in bits + bits:   # each variant twice, interleaved (clock drift)
+        ctx.set_option("ablate", b)
+        ctx.em_begin(th0)
+        ctx.em_iterate(2)
+        ctx.synchronize()
+        ctx.set_option("timing", 1)
+        ctx.sweep_timing(reset=True)
+        t0 = time.perf_counter()
+        ctx.em_iterate(8)
+        ctx.synchronize()
+        dt = time.perf_counter() - t0
+        ms, launches = ctx.sweep_timing(reset=True)
+        ctx.set_option("timing", 0)
+        _, ll = ctx.em_state()
+        print(f"{cfgname} ablate={b:#x}: sweep {ms / max(launches, 1):.3f} ms, {8 / dt:.1f} it/s, "
+              f"loglik[-1] {ll[-1]:.10e}", flush=True)
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()
