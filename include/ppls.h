@@ -241,6 +241,11 @@ int ppls_sweep_kernel(ppls_ctx* ctx, int r, char* buf, int len);
  * slots; 0 = slot not reached) and the tick length in ns.  Requires set_option("ftrace", 1). */
 #define PPLS_FTRACE_LEN 48
 int ppls_finalize_trace(ppls_ctx* ctx, int64_t* stamps, double* tick_ns);
+/* Diagnostics: wall-clock stamps of the last split sweep per workgroup (entry, ring prologue done,
+ * row loop done, partials written; 4 per workgroup, row-major), up to PPLS_STRACE_MAX_WG workgroups;
+ * *n = workgroups copied.  Requires set_option("strace", 1). */
+#define PPLS_STRACE_MAX_WG 4096
+int ppls_sweep_trace(ppls_ctx* ctx, int64_t* stamps, int cap, int* n, double* tick_ns);
 
 /* ---- host-side algebra (no GPU; the same code the device finalize runs) ------------------------ */
 /* From the all-reduced sufficient statistics of one sweep with theta (stats = [X'mu_T p x r |

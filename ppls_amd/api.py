@@ -408,6 +408,15 @@ class Context:
         self._chk(self._L.ppls_sweep_timing(self.h, ct.byref(ms), ct.byref(n), int(reset)))
         return ms.value, n.value
 
+    def sweep_trace(self, grid):
+        """Per-workgroup wall-clock stamps (us, relative to the earliest entry) of the last split
+        sweep: (grid, 4) = entry, ring prologue done, row loop done, partials written."""
+        buf = (ct.c_int64 * (4 * grid))()
+        n, tick = ct.c_int(), ct.c_double()
+        self._chk(self._L.ppls_sweep_trace(self.h, buf, int(grid), ct.byref(n), ct.byref(tick)))
+        a = np.array(buf[:4 * n.value], dtype=np.int64).reshape(n.value, 4)
+        return (a - a[:, 0].min()) * tick.value / 1e3
+
     def finalize_trace(self):
         """Phase stamps of the last finalize (set_option('ftrace', 1) first): {block: [us since the
         block's first stamp, ...]} for the slots that were reached."""

@@ -74,6 +74,7 @@ struct ppls_ctx {
   double* work = nullptr;
   int* status = nullptr;
   long long* ftrace = nullptr;   // finalize phase timestamps (diagnostics)
+  long long* strace = nullptr;   // split sweep per-workgroup stamps (diagnostics, PPLS_STRACE_MAX_WG x 4)
   double* coefs = nullptr;     // loglC_fast coefficient block (5r)
   double* scratch = nullptr;   // generic device scratch
   size_t scratch_bytes = 0;
@@ -382,6 +383,7 @@ int sweep(ppls_ctx* c, int r, int slot, bool write_mu) {
                     (c->nt_loads < 0 && 8.0 * nrows * (double)(c->ldx + c->ldy) > 256.0 * (1 << 20));
     a.ablate = c->ablate | (nt ? 16 : 0);
     a.stop = c->sweep_stop;
+    a.trace = (plan == 3 && a.grid <= PPLS_STRACE_MAX_WG) ? c->strace : nullptr;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     const bool timed = c->timing > 0 && (c->sweep_count++ % c->timing) == 0;
     if (timed) {
@@ -628,6 +630,7 @@ void ppls_ctx_destroy(ppls_ctx* c) {
   c->z_cols = 0;
   dfree(c->work); dfree(c->status); dfree(c->coefs); dfree(c->scratch);
   if (c->ftrace) (void)hipFree(c->ftrace);
+  if (c->strace) (void)hipFree(c->strace);
   dfree(c->stop_d);
   if (c->stop_mirror) (void)hipHostFree(c->stop_mirror);
   for (auto& e : c->ev) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
@@ -657,6 +660,15 @@ int ppls_set_option(ppls_ctx* c, const char* key, int64_t value) {
   } else if (!strcmp(key, "ablate")) {
     if (value < 0 || value > 65535) return fail(c, PPLS_E_ARG, "ablate must be in [0,65535]");
     c->ablate = (int)value;   // timing experiments (bits 0-9 break results; 10+ select equivalent variants)
+  } else if (!strcmp(key, "strace")) {
+    if (value && !c->strace) {
+      HIPCHK(c, hipMalloc(&c->strace, (size_t)PPLS_STRACE_MAX_WG * 4 * sizeof(long long)));
+      HIPCHK(c, hipMemset(c->strace, 0, (size_t)PPLS_STRACE_MAX_WG * 4 * sizeof(long long)));
+    } else if (!value && c->strace) {
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+      (void)hipFree(c->strace);
+      c->strace = nullptr;
+    }
   } else if (!strcmp(key, "ftrace")) {
     if (value && !c->ftrace) {
       HIPCHK(c, hipMalloc(&c->ftrace, PPLS_FTRACE_LEN * sizeof(long long)));
@@ -2081,6 +2093,21 @@ int ppls_finalize_trace(ppls_ctx* c, int64_t* stamps, double* tick_ns) {
   if (!c->ftrace) return fail(c, PPLS_E_STATE, "finalize tracing is off (set_option ftrace 1)");
   HIPCHK(c, hipStreamSynchronize(c->stream));
   HIPCHK(c, hipMemcpy(stamps, c->ftrace, PPLS_FTRACE_LEN * sizeof(long long), hipMemcpyDeviceToHost));
+  if (tick_ns) {
+    int khz = 0;
+    HIPCHK(c, hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c->device));
+    *tick_ns = khz > 0 ? 1e6 / khz : 0.0;
+  }
+  return PPLS_OK;
+}
+
+int ppls_sweep_trace(ppls_ctx* c, int64_t* stamps, int cap, int* n, double* tick_ns) {
+  if (!c || !stamps || !n) return PPLS_E_ARG;
+  if (!c->strace) return fail(c, PPLS_E_STATE, "sweep tracing is off (set_option strace 1)");
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  const int m = std::min(cap, PPLS_STRACE_MAX_WG);
+  HIPCHK(c, hipMemcpy(stamps, c->strace, (size_t)m * 4 * sizeof(long long), hipMemcpyDeviceToHost));
+  *n = m;
   if (tick_ns) {
     int khz = 0;
     HIPCHK(c, hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, c->device));

@@ -32,6 +32,7 @@ struct PplsSweepArgs {
   int ablate;            // timing experiments only (split): 1 no compute, 2 no HBM copies; 16 = nt loads
   int dots_grid;         // panel dots workgroups (0 = one per 128-row group, capped)
   const int* stop;       // device stop flag (em_run's convergence test) or nullptr: kernels exit if set
+  long long* trace;      // split sweep diagnostics: 4 wall-clock stamps per workgroup, or nullptr
 };
 
 struct PplsFinalizeArgs {

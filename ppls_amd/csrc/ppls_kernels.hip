@@ -298,9 +298,13 @@ __global__ __launch_bounds__(NT, 2 * NT / 512) void ppls_sweep_split_kernel(
     const double* __restrict__ X, const double* __restrict__ Y, int64_t n_local, int ldx, int ldy,
     const double* __restrict__ Wp, const double* __restrict__ Cp, const PplsScalars* __restrict__ sc,
     double* __restrict__ part, int64_t part_ld, double* __restrict__ mu, int write_mu, int ablate,
-    const int* __restrict__ stop) {
+    const int* __restrict__ stop, long long* __restrict__ trace) {
   if (stop && *stop) return;   // em_run converged earlier (device stop flag)
   static_assert(SLOTS >= 2 * RP, "ring must hold the group being read and the group in flight");
+  // diagnostics (set_option "strace"): per workgroup wall-clock stamps at entry, after the ring
+  // prologue, after the row loop and after the partial write-out
+  long long* tr = (trace && threadIdx.x == 0) ? trace + 4 * blockIdx.x : nullptr;
+  if (tr) tr[0] = (long long)wall_clock64();
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int V = R * RP;                           // partial dots per thread per step
   constexpr int VP = V + (V & 1);                     // reduce-scatter scratch
@@ -356,8 +360,8 @@ __global__ __launch_bounds__(NT, 2 * NT / 512) void ppls_sweep_split_kernel(
     gj = j;
   }
   double gacc = 0.0;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-
+  // no wait here: the W / C loads (issued first) complete before the ring prologue's first group,
+  // which the prologue waits for, so their latency overlaps the first rows' DMA
   const uint32_t lds_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
   auto issue_row = [&](int i) {
     if ((ablate & 2) || !dma_wave) return;
@@ -462,6 +466,7 @@ __global__ __launch_bounds__(NT, 2 * NT / 512) void ppls_sweep_split_kernel(
     if (write_mu) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     else ppls_wait_vmcnt((npro - min(RP, nrows)) * CPW);
     ppls_lds_barrier();
+    if (tr) tr[1] = (long long)wall_clock64();
     double2 xc[RP][NSH] = {};
     load_x(0, xc);
     if (!(ablate & 1)) dots(0, xc);
@@ -501,6 +506,7 @@ __global__ __launch_bounds__(NT, 2 * NT / 512) void ppls_sweep_split_kernel(
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (tr) tr[2] = (long long)wall_clock64();
   double* pg = part + g * part_ld;
   double* po = pg + (isx ? 0 : (int64_t)R * ldx);
 #pragma unroll
@@ -514,6 +520,11 @@ __global__ __launch_bounds__(NT, 2 * NT / 512) void ppls_sweep_split_kernel(
     double* G2 = pg + (int64_t)R * ldx + (int64_t)R * ldy;
     G2[gj * 2 * R + gi] = gacc;
     G2[gi * 2 * R + gj] = gacc;
+  }
+  if (trace) {
+    __syncthreads();   // every thread's stores issued
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (tr) tr[3] = (long long)wall_clock64();
   }
 }
 
@@ -2041,7 +2052,7 @@ hipError_t launch_split_t(const PplsSweepArgs& a, hipStream_t st) {
   }
   hipLaunchKernelGGL(kern, dim3(a.grid), dim3(512), split_lds(R, a.ldx, a.ldy, 512, RP), st, a.X, a.Y,
                      a.n_local, a.ldx, a.ldy, a.Wp, a.Cp, a.sc, a.part, a.part_ld, a.mu, a.write_mu,
-                     a.ablate, a.stop);
+                     a.ablate, a.stop, a.trace);
   return hipGetLastError();
 }
 
