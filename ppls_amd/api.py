@@ -427,8 +427,10 @@ class Context:
         for b in range(3):
             s = [buf[16 * b + i] for i in range(16)]
             if s[0]:
-                out[b] = [round((v - s[0]) * tick.value * 1e-3, 3) if v else None for v in s[:10]]
-                out[b] += s[10:]   # raw diagnostics (counts, core clock stamps)
+                us = [round((v - s[0]) * tick.value * 1e-3, 3) if v else None for v in s]
+                # 10-12 raw (Jacobi sweeps, core clock stamps); a polar team's member 0 stamps its
+                # first barrier in 9 (arrived) and 10 (all arrived)
+                out[b] = us[:10] + ([us[10]] if s[10] > 1000 else [s[10]]) + s[11:13] + us[13:]
         return out
 
     def sweep_info(self, r):

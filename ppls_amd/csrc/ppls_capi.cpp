@@ -74,6 +74,8 @@ struct ppls_ctx {
   double* work = nullptr;
   int* status = nullptr;
   long long* ftrace = nullptr;   // finalize phase timestamps (diagnostics)
+  unsigned* team_bar = nullptr;  // finalize polar teams (wide p): counters (self-resetting) + partials
+  double* team_part = nullptr;
   long long* strace = nullptr;   // split sweep per-workgroup stamps (diagnostics, PPLS_STRACE_MAX_WG x 4)
   double* coefs = nullptr;     // loglC_fast coefficient block (5r)
   double* scratch = nullptr;   // generic device scratch
@@ -435,6 +437,14 @@ int finalize(ppls_ctx* c, int r, int cur, int nxt, int logl_index, int type, int
   f.gram_cur = c->gram[cur];
   f.gram_nxt = c->gram[nxt];
   f.vstate = c->vstate;
+  if (!c->team_bar) {
+    int rc;
+    if ((rc = dalloc(c, &c->team_bar, 8)) || (rc = dalloc(c, &c->team_part, (size_t)2 * 3 * PPLS_TEAM_MAX * 64)))
+      return rc;
+    HIPCHK(c, hipMemsetAsync(c->team_bar, 0, 8 * sizeof(unsigned), c->stream));
+  }
+  f.team_bar = c->team_bar;
+  f.team_part = c->team_part;
   f.stop = c->sweep_stop ? c->stop_d : nullptr;
   f.stop_mirror = c->sweep_stop ? c->stop_mirror_dev : nullptr;
   f.stop_check = stop_step > 0 ? 1 : 0;
@@ -464,6 +474,10 @@ int reset_stop(ppls_ctx* c) {
 int check_status(ppls_ctx* c) {
   int st = 0;
   HIPCHK(c, hipMemcpy(&st, c->status, sizeof st, hipMemcpyDeviceToHost));
+  if (st == -7) {   // a polar team member waited too long: clear the team counters, report
+    if (c->team_bar) HIPCHK(c, hipMemset(c->team_bar, 0, 8 * sizeof(unsigned)));
+    return fail(c, PPLS_E_HIP, "finalize polar team barrier timed out (status -7)");
+  }
   if (st != 0) return fail(c, PPLS_E_NUMERIC, "rank-deficient X'mu_T or Y'mu_U in the M-step (status %d)", st);
   return PPLS_OK;
 }
@@ -632,6 +646,8 @@ void ppls_ctx_destroy(ppls_ctx* c) {
   if (c->ftrace) (void)hipFree(c->ftrace);
   if (c->strace) (void)hipFree(c->strace);
   dfree(c->stop_d);
+  dfree(c->team_bar);
+  dfree(c->team_part);
   if (c->stop_mirror) (void)hipHostFree(c->stop_mirror);
   for (auto& e : c->ev) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
   if (c->blas) (void)rocblas_destroy_handle(c->blas);

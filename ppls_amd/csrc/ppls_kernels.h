@@ -62,7 +62,12 @@ struct PplsFinalizeArgs {
   int* stop_mirror;      // host-mapped copy of the flag the host polls (or nullptr)
   int stop_check, stop_step;
   double atol;
+  unsigned* team_bar;    // wide-p polar teams: 8 zero-initialised counters, or nullptr (one block each)
+  double* team_part;     // 2 x 3 x PPLS_TEAM_MAX x 64 doubles
 };
+
+#define PPLS_TEAM_ROWS 1024   // rows of S per polar team member
+#define PPLS_TEAM_MAX 32
 
 // One EM step of the sequential initialiser's rank-1 fit on the device (ppls_rank1_step_kernel).
 struct PplsRank1StepArgs {

@@ -1280,52 +1280,133 @@ __device__ void ppls_matmul_wave(const double* sA, const double* sB, double* sC)
 }
 
 // One-sided Jacobi on one wave: A V = U Sigma with A, V in LDS (G x G blocks).  Round m of a
-// sweep rotates the N/2 disjoint pairs of the circle-method schedule: lane group g = lane / G owns
-// pair g (+ 64/G per pass), lane t = lane % G owns row t, the column dots are G-lane DPP sums.
-// Same rotation and stopping rule as ppls_small_polar_n (ppls_math.h).  Wave-uniform.
+// sweep rotates the N/2 (<= 8) disjoint pairs of the circle-method schedule at once: lane group
+// g = lane / 8 owns pair g, lane t = lane % 8 owns rows t and t + 8 (R > 8) of its two columns,
+// the column dots are 8-lane DPP sums.  Same rotation and stopping rule as ppls_small_polar_n
+// (ppls_math.h).  Wave-uniform.
 template <int R>
 __device__ int ppls_jacobi_wave(double* sA, double* sV) {
   constexpr int N = R + (R & 1);
   constexpr int G = PplsWaveBlk<R>::G;
-  constexpr int PPW = 64 / G;                       // pairs per pass
-  constexpr int PASSES = (N / 2 + PPW - 1) / PPW;
-  const int lane = threadIdx.x & 63, t = lane % G;
+  constexpr int RPL = (R + 7) / 8;                  // rows per lane (G = 16 layout for R > 8)
+  static_assert(N / 2 <= 8, "one pass of 8-lane groups per round");
+  const int lane = threadIdx.x & 63, t = lane & 7;
   int sweeps = 0;
   for (int sweep = 0; sweep < 60; ++sweep) {
     ++sweeps;
     bool rot_any = false;
 #pragma unroll
     for (int m = 0; m < N - 1; ++m) {
+      const int k = lane >> 3;
+      const bool grp = k < N / 2;
+      int i, j;
+      ppls_rr_pair<R>(m, grp ? k : 0, i, j);
+      const bool act = grp && j < R;
+      const int ci = (act ? i : 0) * G + t, cj = (act ? j : 1) * G + t;
+      double x[RPL], y[RPL], vx[RPL], vy[RPL];
+      double aa = 0.0, bb = 0.0, gg = 0.0;
 #pragma unroll
-      for (int ps = 0; ps < PASSES; ++ps) {
-        const int k = ps * PPW + lane / G;
-        const bool grp = k < N / 2;
-        int i, j;
-        ppls_rr_pair<R>(m, grp ? k : 0, i, j);
-        const bool act = grp && j < R;
-        const int ci = (act ? i : 0) * G + t, cj = (act ? j : 1) * G + t;
-        const double x = sA[ci], y = sA[cj], vx = sV[ci], vy = sV[cj];
-        const double a = ppls_groupG_sum<G>(x * x), b = ppls_groupG_sum<G>(y * y);
-        const double g = ppls_groupG_sum<G>(x * y);
-        const bool rot = act && (g * g >= 1e-30 * (a * b)) && g != 0.0;
-        const double z = (b - a) * ppls_rcp(rot ? 2.0 * g : 1.0);
-        const double z2 = fma(z, z, 1.0);
-        const double u = fabs(z) + z2 * ppls_rsq(z2);
-        const double w = ppls_rsq(fma(u, u, 1.0));
-        const double c = u * w, sn = z >= 0.0 ? w : -w;
-        if (rot) {
-          sA[ci] = fma(c, x, -sn * y);
-          sA[cj] = fma(sn, x, c * y);
-          sV[ci] = fma(c, vx, -sn * vy);
-          sV[cj] = fma(sn, vx, c * vy);
-        }
-        rot_any = rot_any || rot;
-        ppls_wave_lds_fence();
+      for (int u = 0; u < RPL; ++u) {
+        x[u] = sA[ci + 8 * u];
+        y[u] = sA[cj + 8 * u];
+        vx[u] = sV[ci + 8 * u];
+        vy[u] = sV[cj + 8 * u];
+        aa = fma(x[u], x[u], aa);
+        bb = fma(y[u], y[u], bb);
+        gg = fma(x[u], y[u], gg);
       }
+      const double a = ppls_group8_sum(aa), b = ppls_group8_sum(bb), g = ppls_group8_sum(gg);
+      const bool rot = act && (g * g >= 1e-30 * (a * b)) && g != 0.0;
+      const double z = (b - a) * ppls_rcp(rot ? 2.0 * g : 1.0);
+      const double z2 = fma(z, z, 1.0);
+      const double uu = fabs(z) + z2 * ppls_rsq(z2);
+      const double w = ppls_rsq(fma(uu, uu, 1.0));
+      const double c = uu * w, sn = z >= 0.0 ? w : -w;
+      if (rot) {
+#pragma unroll
+        for (int u = 0; u < RPL; ++u) {
+          sA[ci + 8 * u] = fma(c, x[u], -sn * y[u]);
+          sA[cj + 8 * u] = fma(sn, x[u], c * y[u]);
+          sV[ci + 8 * u] = fma(c, vx[u], -sn * vy[u]);
+          sV[cj + 8 * u] = fma(sn, vx[u], c * vy[u]);
+        }
+      }
+      rot_any = rot_any || rot;
+      ppls_wave_lds_fence();
     }
     if (!__any(rot_any)) break;
   }
   return sweeps;
+}
+
+// A team of K workgroups computing one polar factor together (wide p): each owns rows
+// [p rank / K, p (rank + 1) / K); the R x R Grams of passes 1-2 are exchanged through `part` (one
+// 64-double slot per rank and phase, summed in rank order by every member, so all members hold
+// bitwise-identical values and run the identical small algebra) at a counter barrier; the Gram
+// of the result is summed by the last member to finish.  K = 1 is the single-block form (no
+// exchange).  Barrier waits are bounded: a member that waits longer than ~100 ms sets status -7
+// and carries on, so a missing member can never hang the GPU.
+struct PplsTeam {
+  int rank, K;
+  unsigned* bar;    // [0] barrier arrivals, [1] members done, [2] result-Gram arrivals (per matrix)
+  double* part;     // 3 phases x K x 64 doubles
+  int* status;
+  long long* tr;    // diagnostics (member 0): stamps inside the first barrier
+};
+
+// Members publish with plain stores and one agent-scope release fence, wait with relaxed polling of
+// the arrival counter and one acquire fence (measured: memory-side atomic swaps for the values
+// instead cost more, profiles/r2_finalize_team.txt).
+__device__ void ppls_team_barrier(const PplsTeam& tm, unsigned target) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();   // release this member's partials
+    atomicAdd(&tm.bar[0], 1u);
+    if (tm.tr && target == (unsigned)tm.K) tm.tr[9] = (long long)wall_clock64();
+    long spins = 0;
+    // relaxed polling (no cache invalidation per poll); one acquire fence after the wait
+    while (__hip_atomic_load(&tm.bar[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      if (++spins > (1L << 21)) {
+        atomicExch(tm.status, -7);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    if (tm.tr && target == (unsigned)tm.K) tm.tr[10] = (long long)wall_clock64();
+    __threadfence();   // acquire the others' partials
+  }
+  __syncthreads();
+}
+
+// After a member's last barrier: the last member to leave resets the counters for the next launch.
+__device__ void ppls_team_leave(const PplsTeam& tm) {
+  if (tm.K <= 1 || threadIdx.x != 0) return;
+  if (atomicAdd(&tm.bar[1], 1u) == (unsigned)tm.K - 1) {
+    atomicExch(&tm.bar[0], 0u);
+    atomicExch(&tm.bar[1], 0u);
+  }
+}
+
+// vals (NG per thread, identical in every thread of the block) -> the team's sum over members.
+template <int NG>
+__device__ void ppls_team_sum(const PplsTeam& tm, int phase, double (&vals)[NG], double* sh) {
+  if (tm.K <= 1) return;
+  double* slot = tm.part + ((int64_t)phase * tm.K) * 64;
+  if (threadIdx.x < NG) {
+#pragma unroll
+    for (int e = 0; e < NG; ++e)
+      if ((int)threadIdx.x == e) slot[(int64_t)tm.rank * 64 + e] = vals[e];
+  }
+  ppls_team_barrier(tm, (unsigned)(phase + 1) * tm.K);
+  if (threadIdx.x < NG) {
+    double t = 0.0;
+    for (int k = 0; k < tm.K; ++k) t += __builtin_nontemporal_load(slot + (int64_t)k * 64 + threadIdx.x);
+    sh[threadIdx.x] = t;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int e = 0; e < NG; ++e) vals[e] = sh[e];
+  __syncthreads();
 }
 
 // Polar factor U V' of the p x R matrix S (column-major, ld lds) by Cholesky-QR2 (S = Q1 R1,
@@ -1341,12 +1422,15 @@ template <int R, int NT>
 __device__ bool ppls_block_polar_fast(const double* __restrict__ S, int64_t lds, int p,
                                       double* __restrict__ out, int64_t ldo, int ldo_rows, double* Sl,
                                       double* sh, double* sm, double* __restrict__ gram_out,
-                                      double* __restrict__ vstate, long long* tr) {
+                                      double* __restrict__ vstate, long long* tr, const PplsTeam& tm) {
   constexpr int NG = R * (R + 1) / 2;
   constexpr int NW = NT / 64;
   constexpr int G = PplsWaveBlk<R>::G, GG = G * G;
   static_assert(R <= 16 && NG <= 64, "block sums of at most 64 values");
   const int tid = threadIdx.x, lane = tid & 63;
+  const int i0 = (int)((int64_t)p * tm.rank / tm.K), i1 = (int)((int64_t)p * (tm.rank + 1) / tm.K);
+  const int nr = i1 - i0;                                     // this member's rows
+  const int o1 = tm.rank == tm.K - 1 ? ldo_rows : i1;        // output rows (the last takes the padding)
   double* sF = sm;            // R x R (column-major, ld R): R1^-1 for pass 2, then F for pass 3
   __shared__ double sA[GG], sV[GG], sT[GG], sU[GG], ssv[16];
   __shared__ int ok;
@@ -1364,25 +1448,28 @@ __device__ bool ppls_block_polar_fast(const double* __restrict__ S, int64_t lds,
   // pass 1: G1 = S'S, staging S into LDS; chunks of PU rows per thread with every load of a
   // chunk issued before the first use
   constexpr int PU = R >= 6 ? 4 : 8;
-  for (int i0 = 0; i0 < p; i0 += PU * NT) {
+  for (int c0 = i0; c0 < i1; c0 += PU * NT) {
     double x[PU][R];
 #pragma unroll
     for (int u = 0; u < PU; ++u) {
-      const int i = i0 + u * NT + tid;
+      const int i = c0 + u * NT + tid;
 #pragma unroll
-      for (int k = 0; k < R; ++k) x[u][k] = (i < p) ? S[(int64_t)k * lds + i] : 0.0;
+      for (int k = 0; k < R; ++k) x[u][k] = (i < i1) ? S[(int64_t)k * lds + i] : 0.0;
     }
 #pragma unroll
     for (int u = 0; u < PU; ++u) {
-      const int i = i0 + u * NT + tid;
-      if (Sl && i < p) {
+      const int i = c0 + u * NT + tid;
+      if (Sl && i < i1) {
 #pragma unroll
-        for (int k = 0; k < R; ++k) Sl[k * p + i] = x[u][k];
+        for (int k = 0; k < R; ++k) Sl[k * nr + (i - i0)] = x[u][k];
       }
       ppls_gram_acc<R>(x[u], vals);
     }
   }
+  ppls_stamp(tr, 13);
   ppls_block_sum_t<NG, NW>(vals, sh);
+  ppls_stamp(tr, 14);
+  ppls_team_sum<NG>(tm, 0, vals, sh);
   ppls_stamp(tr, 1);
   if constexpr (R <= 6) {   // small R: one thread in registers is faster than the wave form
     if (tid == 0) {
@@ -1414,12 +1501,18 @@ __device__ bool ppls_block_polar_fast(const double* __restrict__ S, int64_t lds,
   }
   __syncthreads();
   ppls_stamp(tr, 2);
-  if (!ok) return false;
+  if (!ok) {   // identical verdict in every member
+    ppls_team_leave(tm);
+    return false;
+  }
+  // row i of S / Q1 at Sr[k * ldr + i - sro]: own rows staged in LDS, else S in global memory
   const double* Sr = Sl ? Sl : S;
-  const int64_t ldr = Sl ? p : lds;
+  const int64_t ldr = Sl ? nr : lds;
+  const int sro = Sl ? i0 : 0;
   // Q1 is kept where pass 3 reads it back (each thread its own rows): over S in LDS, else in out
   double* Qs = Sl ? Sl : out;
-  const int64_t ldq = Sl ? p : ldo;
+  const int64_t ldq = Sl ? nr : ldo;
+  const int qo = Sl ? i0 : 0;
   // pass 2: G2 = Q1'Q1, Q1 = S R1^-1
   {
     double M[R][R];
@@ -1430,10 +1523,10 @@ __device__ bool ppls_block_polar_fast(const double* __restrict__ S, int64_t lds,
 #pragma unroll
     for (int e = 0; e < NG; ++e) vals[e] = 0.0;
 #pragma unroll 2
-    for (int i = tid; i < p; i += NT) {
+    for (int i = i0 + tid; i < i1; i += NT) {
       double xq[R], qv[R];
 #pragma unroll
-      for (int k = 0; k < R; ++k) xq[k] = Sr[(int64_t)k * ldr + i];
+      for (int k = 0; k < R; ++k) xq[k] = Sr[(int64_t)k * ldr + i - sro];
 #pragma unroll
       for (int j = 0; j < R; ++j) {
         double s = 0.0;
@@ -1443,10 +1536,13 @@ __device__ bool ppls_block_polar_fast(const double* __restrict__ S, int64_t lds,
       }
       ppls_gram_acc<R>(qv, vals);
 #pragma unroll
-      for (int j = 0; j < R; ++j) Qs[(int64_t)j * ldq + i] = qv[j];
+      for (int j = 0; j < R; ++j) Qs[(int64_t)j * ldq + i - qo] = qv[j];
     }
   }
+  ppls_stamp(tr, 15);
   ppls_block_sum_t<NG, NW>(vals, sh);
+  ppls_team_sum<NG>(tm, 1, vals, sh);
+  ppls_team_leave(tm);   // the last barrier of this member
   ppls_stamp(tr, 3);
   if (tid < 64) {   // wave 0: R2 = chol(G2), T = R2 R1, warm start, Jacobi, F
     for (int e = lane; e < GG; e += 64) {
@@ -1505,7 +1601,7 @@ __device__ bool ppls_block_polar_fast(const double* __restrict__ S, int64_t lds,
     ppls_stamp(tr, 7);
     const int sweeps = ppls_jacobi_wave<R>(sT, sV);
     ppls_stamp(tr, 8);
-    if (tr && lane == 0) tr[10] = sweeps;
+    if (tr && lane == 0 && tm.K <= 1) tr[10] = sweeps;
     if (lane < R) {
       double nrm = 0.0;
 #pragma unroll
@@ -1538,7 +1634,7 @@ __device__ bool ppls_block_polar_fast(const double* __restrict__ S, int64_t lds,
 #pragma unroll
       for (int kk = 0; kk < R; ++kk) s = fma(sA[kk * G + a], sU[b * G + kk], s);
       sF[R * R + b * R + a] = s;
-      if (vstate) vstate[b * R + a] = sV[b * G + a];
+      if (vstate && tm.rank == 0) vstate[b * R + a] = sV[b * G + a];   // every member's V is identical
     }
     good = __shfl(good ? 1 : 0, 0, 64) != 0 && good;   // lane 0 holds the chol2 verdict for small R
     // Cholesky-QR2 yields an orthonormal factor only while Q1 = S R1^-1 is nearly orthonormal
@@ -1566,10 +1662,10 @@ __device__ bool ppls_block_polar_fast(const double* __restrict__ S, int64_t lds,
 #pragma unroll
   for (int e = 0; e < NG; ++e) vals[e] = 0.0;
 #pragma unroll 2
-  for (int i = tid; i < ldo_rows; i += NT) {
+  for (int i = i0 + tid; i < o1; i += NT) {
     double xq[R], o[R];
 #pragma unroll
-    for (int k = 0; k < R; ++k) xq[k] = (i < p) ? Qs[(int64_t)k * ldq + i] : 0.0;
+    for (int k = 0; k < R; ++k) xq[k] = (i < p) ? Qs[(int64_t)k * ldq + i - qo] : 0.0;
 #pragma unroll
     for (int j = 0; j < R; ++j) {
       double s = 0.0;
@@ -1582,6 +1678,34 @@ __device__ bool ppls_block_polar_fast(const double* __restrict__ S, int64_t lds,
   }
   if (gram_out) {
     ppls_block_sum_t<NG, NW>(vals, sh);
+    if (tm.K > 1) {   // the last member to finish sums the members' Grams in rank order
+      __shared__ int last;
+      double* slot = tm.part + ((int64_t)2 * tm.K) * 64;
+      if (tid < NG) {
+#pragma unroll
+        for (int e = 0; e < NG; ++e)
+          if (tid == e) slot[(int64_t)tm.rank * 64 + e] = vals[e];
+      }
+      __syncthreads();
+      if (tid == 0) {
+        __threadfence();
+        last = atomicAdd(&tm.bar[2], 1u) == (unsigned)tm.K - 1;
+        if (last) {
+          __threadfence();
+          atomicExch(&tm.bar[2], 0u);
+        }
+      }
+      __syncthreads();
+      if (!last) return true;
+      if (tid < NG) {
+        double t = 0.0;
+        for (int k = 0; k < tm.K; ++k) t += __builtin_nontemporal_load(slot + (int64_t)k * 64 + tid);
+        sh[tid] = t;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int e = 0; e < NG; ++e) vals[e] = sh[e];
+    }
     if (tid == 0) {
       double Gm[R][R];
       ppls_gram_unpack<R>(vals, Gm);
@@ -1718,7 +1842,8 @@ __global__ __launch_bounds__(PPLS_FIN_THREADS) void ppls_finalize_kernel(
     int logl_index, double* __restrict__ work, int* __restrict__ status, int qr, int mode,
     const double* __restrict__ gram_cur, double* __restrict__ gram_nxt, double* __restrict__ vstate,
     int stage_lds, long long* __restrict__ trace,
-    int* __restrict__ stop, int* __restrict__ stop_mirror, int stop_check, int stop_step, double atol) {
+    int* __restrict__ stop, int* __restrict__ stop_mirror, int stop_check, int stop_step, double atol,
+    int KX, int KY, unsigned* __restrict__ team_bar, double* __restrict__ team_part) {
   if (stop && *stop) return;   // em_run converged earlier (device stop flag)
   constexpr int NT = PPLS_FIN_THREADS;
   constexpr int NG = R * (R + 1) / 2;
@@ -1732,20 +1857,32 @@ __global__ __launch_bounds__(PPLS_FIN_THREADS) void ppls_finalize_kernel(
   const double* SY = stats + (int64_t)R * ldx;
   const double* G = SY + (int64_t)R * ldy;
   const int tid = threadIdx.x;
-  long long* tr = trace ? trace + 16 * blockIdx.x : nullptr;
+  const int b = blockIdx.x;
+  // blocks [0, KX): the team computing W_next; [KX, KX + KY): C_next; the last block: scalars
+  const int slot = b < KX ? 0 : b < KX + KY ? 1 : 2;
+  const bool lead = b == 0 || b == KX || b == KX + KY;   // member 0 of its team / the scalar block
+  long long* tr = (trace && lead) ? trace + 16 * slot : nullptr;
   ppls_stamp(tr, 0);
   if (tr && tid == 0) tr[11] = (long long)clock64();
-  if (blockIdx.x < 2) {
+  if (slot < 2) {
     if (!(mode & 1)) return;
-    const bool isx = blockIdx.x == 0;
+    const bool isx = slot == 0;
     const double* S = isx ? SX : SY;
     const int ld = isx ? ldx : ldy, rows = isx ? p : q;
     double* out = isx ? Wn : Cn;
     double* gout = gram_nxt ? gram_nxt + (isx ? 0 : R * R) : nullptr;
     double* w2 = work + (isx ? 0 : 2 * (int64_t)p * R);
     double* vs = vstate ? vstate + (isx ? 0 : R * R) : nullptr;
+    PplsTeam tm;
+    tm.K = isx ? KX : KY;
+    tm.rank = isx ? b : b - KX;
+    tm.bar = team_bar + (isx ? 0 : 4);
+    tm.part = team_part + (isx ? 0 : (int64_t)3 * PPLS_TEAM_MAX * 64);
+    tm.status = status;
+    tm.tr = tr;
     if (qr || !ppls_block_polar_fast<R, NT>(S, ld, rows, out, ld, ld, stage_lds ? dyn_lds : nullptr, sh,
-                                            sm, gout, vs, tr)) {
+                                            sm, gout, vs, tr, tm)) {
+      if (tm.rank != 0) return;   // the Householder fallback runs on one block
       ppls_block_polar(S, ld, rows, R, out, ld, ld, w2, w2 + (int64_t)rows * R, status, qr);
       if (gout) {
         __syncthreads();
@@ -2019,13 +2156,21 @@ hipError_t launch_finalize_t(const PplsFinalizeArgs* f, hipStream_t st) {
     const hipError_t e = set_dyn_lds((const void*)kern, (int)dyn_max);
     if (e != hipSuccess) return e;
   }
-  const size_t stage = (size_t)R * (f->p > f->q ? f->p : f->q) * sizeof(double);
+  // teams for wide p: one member per PPLS_TEAM_ROWS rows (QR: one block, Householder)
+  auto team = [&](int rows) {
+    if (f->qr || !f->team_bar) return 1;
+    const int k = (rows + PPLS_TEAM_ROWS - 1) / PPLS_TEAM_ROWS;
+    return k < 1 ? 1 : k > PPLS_TEAM_MAX ? PPLS_TEAM_MAX : k;
+  };
+  const int KX = team(f->p), KY = team(f->q);
+  const int mrows = (f->p + KX - 1) / KX > (f->q + KY - 1) / KY ? (f->p + KX - 1) / KX : (f->q + KY - 1) / KY;
+  const size_t stage = (size_t)R * mrows * sizeof(double);   // a member stages its own rows
   const int use = stage <= dyn_max && !f->qr;
-  hipLaunchKernelGGL(kern, dim3(3), dim3(PPLS_FIN_THREADS), use ? stage : 0, st, f->stats, f->ssq, f->N,
-                     f->p, f->q, f->ldx, f->ldy, f->Wc, f->Cc, f->sc_cur, f->Wn, f->Cn, f->sc_nxt, f->mom,
+  hipLaunchKernelGGL(kern, dim3(KX + KY + 1), dim3(PPLS_FIN_THREADS), use ? stage : 0, st, f->stats, f->ssq,
+                     f->N, f->p, f->q, f->ldx, f->ldy, f->Wc, f->Cc, f->sc_cur, f->Wn, f->Cn, f->sc_nxt, f->mom,
                      f->loglik, f->logl_index, f->work, f->status, f->qr, f->mode, f->gram_cur,
                      f->gram_nxt, f->vstate, use, f->trace, f->stop, f->stop_mirror, f->stop_check,
-                     f->stop_step, f->atol);
+                     f->stop_step, f->atol, KX, KY, f->team_bar, f->team_part);
   return hipGetLastError();
 }
 

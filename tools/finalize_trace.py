@@ -7,8 +7,9 @@ sys.path.insert(0, ROOT)
 from bench import CONFIGS, make_truth_and_theta0  # noqa: E402
 from ppls_amd import Context  # noqa: E402
 
-SLOTS = {0: "start", 1: "gram1/WtW summed", 2: "chol1+inv / serial scalars", 3: "gram2 summed",
-         4: "serial r x r (chol2, Jacobi, products)", 5: "output written"}
+SLOTS = {0: "start", 1: "gram1 summed over the team", 2: "chol1+inv / serial scalars", 3: "gram2 summed",
+         4: "serial r x r (chol2, Jacobi, products)", 5: "output written", 6: "chol2", 7: "T V",
+         8: "Jacobi", 13: "pass-1 rows", 14: "gram1 block sum", 15: "pass-2 rows"}
 
 
 def main():
@@ -28,7 +29,7 @@ def main():
                 us = tr[0][5]
                 print(f"  block 0: jacobi sweeps {raw[0]}, core clock {(raw[2] - raw[1]) / (us * 1e3):.2f} GHz")
             print(f"{cfgname} iter {it}: " + "; ".join(
-                f"block {b}: " + " ".join(f"{s}={v}" for s, v in enumerate(ts) if v is not None)
+                f"block {b}: " + " ".join(f"{s}={v}" for s, v in enumerate(ts) if v is not None and s not in (10, 11, 12))
                 for b, ts in tr.items()), flush=True)
         ctx.set_option("ftrace", 0)
         ctx.close()
