@@ -27,6 +27,9 @@ CONFIGS = {
     "c5": dict(n=500_000, p=10_000, q=500, r=10, storage="f32",
                name="C5: n=5e5, p=1e4, q=500, r=10, fp32 storage / fp64 arithmetic (wide-p omics case)"),
     "c5d": dict(n=500_000, p=10_000, q=500, r=10, name="C5 shape in fp64 storage"),
+    # one GPU's share of C5 over 8 GPUs (n = 6.25e4 of 5e5), fp32 storage, no all-reduce
+    "c5s": dict(n=62_500, p=10_000, q=500, r=10, storage="f32",
+                name="C5 per-GPU shard (n=6.25e4 of 5e5), fp32 storage, no all-reduce"),
     # one GPU's share of C4 (C3 over 8 GPUs): the per-GPU sweep + fixed per-iteration costs, no all-reduce
     "c4s": dict(n=125_000, p=2000, q=2000, r=5, name="C4 per-GPU shard (n=1.25e5 of C3's 1e6), fp64, no all-reduce"),
 }
