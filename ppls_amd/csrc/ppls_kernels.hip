@@ -678,7 +678,7 @@ __device__ __forceinline__ PplsVec16<T> ppls_load16(const T* p) {
 // W.  The next tile's global loads are in flight during the MFMAs.  Result lane map (f64 MFMA):
 // row (l >> 4) + 4 reg, component l & 15 -- the same for the X and the Y product, so mu_T/mu_U are
 // formed in registers.
-template <typename T, int R>
+template <typename T, int R, int NB>
 __global__ __launch_bounds__(256) void ppls_panel_mfmadots_kernel(
     const T* __restrict__ X, const T* __restrict__ Y, int64_t n, int ldx, int ldy,
     const double* __restrict__ Wt, const double* __restrict__ Ct, const PplsScalars* __restrict__ sc,
@@ -690,7 +690,8 @@ __global__ __launch_bounds__(256) void ppls_panel_mfmadots_kernel(
   constexpr int ES = (int)sizeof(T);
   constexpr int KT = 128 / ES;        // columns per tile
   constexpr int KQ = KT / 4;          // MFMA steps per tile (columns per lane group)
-  constexpr int RB = 32;              // rows per wave
+  constexpr int RB = 16 * NB;         // rows per wave: NB 16-row blocks sharing the B operand
+  constexpr int NL = RB / 8;          // 16-B loads per lane per tile
   constexpr int RS = 144;             // padded LDS row stride (bytes)
   constexpr int V4 = 4 * R;
   static_assert(R <= 16, "one 16-wide MFMA tile of components");
@@ -703,16 +704,18 @@ __global__ __launch_bounds__(256) void ppls_panel_mfmadots_kernel(
   const int64_t ntiles = (n + RB - 1) / RB;
   for (int64_t t = (int64_t)blockIdx.x * 4 + wave; t < ntiles; t += (int64_t)gridDim.x * 4) {
     const int64_t row0 = t * RB;
-    d4 res[2][2];   // [mat][block]
+    d4 res[2][NB];   // [mat][block]
 #pragma unroll
     for (int mat = 0; mat < 2; ++mat) {
       const T* M = mat ? Y : X;
       const int ld = mat ? ldy : ldx;
       const double* Wm = mat ? Ct : Wt;
-      d4 acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
-      const T* src[4];
+      d4 acc[NB];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int bk = 0; bk < NB; ++bk) acc[bk] = d4{0.0, 0.0, 0.0, 0.0};
+      const T* src[NL];
+#pragma unroll
+      for (int u = 0; u < NL; ++u) {
         int64_t rr = row0 + lrow + 8 * u;
         if (rr >= n) rr = n - 1;
         src[u] = M + rr * ld + lchunk * (16 / ES);
@@ -723,64 +726,56 @@ __global__ __launch_bounds__(256) void ppls_panel_mfmadots_kernel(
       // last row), which meets the zero rows of Wt beyond ld and adds exactly 0; prefetches past
       // the last tile re-read it.  Issue order per tile: this tile's B operands, then the next
       // tile's X loads, so the MFMAs wait only for B while the next tile streams in.
-      f4 xa0, xa1, xa2, xa3;
+      f4 xa[NL];
       auto ld4 = [&](const T* p) -> f4 { return *(const f4*)p; };   // (non-temporal: 16 % slower here)
-      auto load_tile = [&](int tc, f4& b0, f4& b1, f4& b2, f4& b3) {
+      auto load_tile = [&](int tc, f4 (&b)[NL]) {
         const int c = tc < ntc ? tc : ntc - 1;
-        b0 = ld4(src[0] + c * KT);
-        b1 = ld4(src[1] + c * KT);
-        b2 = ld4(src[2] + c * KT);
-        b3 = ld4(src[3] + c * KT);
+#pragma unroll
+        for (int u = 0; u < NL; ++u) b[u] = ld4(src[u] + c * KT);
       };
       // B operand of lane l at k-step s: W[tile column kq KQ + s][i16] (Wt: 16 zero-padded columns,
       // k-steps in pairs: one 16-B load per two steps)
       const double* wb0 = Wm + (int64_t)kq * KQ * 16 + 2 * i16;   // pair layout (transpose kernel)
-      auto step = [&](int tc, f4& b0, f4& b1, f4& b2, f4& b3) {
+      auto step = [&](int tc, f4 (&b)[NL]) {
         char* wl = lds + (wave * 2 + (tc & 1)) * RB * RS;
-        *(f4*)(wl + lrow * RS + lchunk * 16) = b0;
-        *(f4*)(wl + (lrow + 8) * RS + lchunk * 16) = b1;
-        *(f4*)(wl + (lrow + 16) * RS + lchunk * 16) = b2;
-        *(f4*)(wl + (lrow + 24) * RS + lchunk * 16) = b3;
+#pragma unroll
+        for (int u = 0; u < NL; ++u) *(f4*)(wl + (lrow + 8 * u) * RS + lchunk * 16) = b[u];
         asm volatile("" ::: "memory");   // keep the loads below after the stores (buf is reused)
-        double b[KQ];
+        double bw[KQ];
         const double* wb = wb0 + (int64_t)tc * KT * 16;
 #pragma unroll
         for (int s2 = 0; s2 < KQ; s2 += 2) {
           const double2 w2 = *(const double2*)(wb + s2 * 16);
-          b[s2] = w2.x;
-          b[s2 + 1] = w2.y;
+          bw[s2] = w2.x;
+          bw[s2 + 1] = w2.y;
         }
         asm volatile("" ::: "memory");   // B before the next tiles' X in the vmcnt order
-        load_tile(tc + 1, b0, b1, b2, b3);
+        load_tile(tc + 1, b);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        // A operands: rows i16 and 16 + i16, columns [kq KQ, kq KQ + KQ) of the tile
-        T a0[KQ], a1[KQ];
+        // A operands: rows 16 bk + i16, columns [kq KQ, kq KQ + KQ) of the tile
 #pragma unroll
-        for (int h = 0; h < KQ * ES / 16; ++h) {
-          const float4 v0 = *(const float4*)(wl + i16 * RS + kq * KQ * ES + h * 16);
-          const float4 v1 = *(const float4*)(wl + (16 + i16) * RS + kq * KQ * ES + h * 16);
-          const T* p0 = (const T*)&v0;
-          const T* p1 = (const T*)&v1;
+        for (int bk = 0; bk < NB; ++bk) {
+          T a[KQ];
 #pragma unroll
-          for (int u = 0; u < 16 / ES; ++u) {
-            a0[h * (16 / ES) + u] = p0[u];
-            a1[h * (16 / ES) + u] = p1[u];
+          for (int h = 0; h < KQ * ES / 16; ++h) {
+            const float4 v = *(const float4*)(wl + (16 * bk + i16) * RS + kq * KQ * ES + h * 16);
+            const T* pv = (const T*)&v;
+#pragma unroll
+            for (int u = 0; u < 16 / ES; ++u) a[h * (16 / ES) + u] = pv[u];
           }
-        }
 #pragma unroll
-        for (int s2 = 0; s2 < KQ; ++s2) {
-          acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64((double)a0[s2], b[s2], acc0, 0, 0, 0);
-          acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64((double)a1[s2], b[s2], acc1, 0, 0, 0);
+          for (int s2 = 0; s2 < KQ; ++s2)
+            acc[bk] = __builtin_amdgcn_mfma_f64_16x16x4f64((double)a[s2], bw[s2], acc[bk], 0, 0, 0);
         }
       };
-      load_tile(0, xa0, xa1, xa2, xa3);
-      for (int tc = 0; tc < ntc; ++tc) step(tc, xa0, xa1, xa2, xa3);
-      res[mat][0] = acc0;
-      res[mat][1] = acc1;
+      load_tile(0, xa);
+      for (int tc = 0; tc < ntc; ++tc) step(tc, xa);
+#pragma unroll
+      for (int bk = 0; bk < NB; ++bk) res[mat][bk] = acc[bk];
     }
     if (i16 < R) {
 #pragma unroll
-      for (int blk = 0; blk < 2; ++blk)
+      for (int blk = 0; blk < NB; ++blk)
 #pragma unroll
         for (int reg = 0; reg < 4; ++reg) {
           const int64_t row = row0 + 16 * blk + kq + 4 * reg;
@@ -881,14 +876,15 @@ __global__ __launch_bounds__(256) void ppls_panel_acc_kernel(
     if (bt + 1 < nbatch) load_mu(b0 + BR);
     const double* sm = smu[bt & 1];
     if (act) {
-      PplsVec16<T> xa[8], xb[8];
-      auto load8 = [&](int rr, PplsVec16<T> (&xv)[8]) {
+      constexpr int G = 8;   // rows per load group (4: 168 VGPRs, 3 waves/SIMD, no faster at C5)
+      PplsVec16<T> xa[G], xb[G];
+      auto load8 = [&](int rr, PplsVec16<T> (&xv)[G]) {
 #pragma unroll
-        for (int u = 0; u < 8; ++u) xv[u] = ppls_load16<T, NT>(base + (b0 + min(rr + u, nb - 1)) * ld);
+        for (int u = 0; u < G; ++u) xv[u] = ppls_load16<T, NT>(base + (b0 + min(rr + u, nb - 1)) * ld);
       };
-      auto fma8 = [&](int rr, const PplsVec16<T> (&xv)[8]) {
+      auto fma8 = [&](int rr, const PplsVec16<T> (&xv)[G]) {
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
+        for (int u = 0; u < G; ++u) {
           if (rr + u >= nb) break;
 #pragma unroll
           for (int k = 0; k < R; ++k) {
@@ -899,12 +895,12 @@ __global__ __launch_bounds__(256) void ppls_panel_acc_kernel(
         }
       };
       load8(0, xa);
-      for (int rr = 0; rr < nb; rr += 16) {
-        if (rr + 8 < nb) load8(rr + 8, xb);
+      for (int rr = 0; rr < nb; rr += 2 * G) {
+        if (rr + G < nb) load8(rr + G, xb);
         fma8(rr, xa);
-        if (rr + 8 >= nb) break;
-        if (rr + 16 < nb) load8(rr + 16, xa);
-        fma8(rr + 8, xb);
+        if (rr + G >= nb) break;
+        if (rr + 2 * G < nb) load8(rr + 2 * G, xa);
+        fma8(rr + G, xb);
       }
     }
     if (bt + 1 < nbatch) store_mu((bt + 1) & 1);
@@ -2318,10 +2314,19 @@ hipError_t launch_panel_t(const PplsSweepArgs* a, const T* X, const T* Y, double
   hipLaunchKernelGGL(ppls_transpose_wc_kernel, dim3((unsigned)((ne + 255) / 256)), dim3(256), 0, st, a->Wp,
                      a->Cp, a->ldx, a->ldy, ldxp, ldyp, R, rs, Wt, Ct, a->stop);
   {   // MFMA dots (profiles/r1_c5_*_dots_variants.txt: faster than the VALU and LDS-DMA forms)
-    const int64_t wtiles = (a->n_local + 31) / 32;
+    // rows per wave: 64 (four 16-row blocks per B load: half the B traffic of 32 rows; 246 VGPRs,
+    // 2 waves/SIMD) once there are enough rows to fill the chip, else 32 (146 VGPRs, 3 waves/SIMD).
+    // C5 fp32: 8.28 -> 7.80 ms per sweep (profiles/r2_c5_dots_rows.txt); ablate bit 12 flips it.
+    const bool big = a->n_local >= 65536;
+    const int rb = (big != ((a->ablate & 4096) != 0)) ? 64 : 32;
+    const int64_t wtiles = (a->n_local + rb - 1) / rb;
     const int mblocks = (int)((wtiles + 3) / 4 < 16384 ? (wtiles + 3) / 4 : 16384);
-    hipLaunchKernelGGL((ppls_panel_mfmadots_kernel<T, R>), dim3(mblocks), dim3(256), 0, st, X, Y,
-                       a->n_local, a->ldx, a->ldy, Wt, Ct, a->sc, Z, a->write_mu ? a->mu : nullptr, a->stop);
+    if (rb == 64)
+      hipLaunchKernelGGL((ppls_panel_mfmadots_kernel<T, R, 4>), dim3(mblocks), dim3(256), 0, st, X, Y,
+                         a->n_local, a->ldx, a->ldy, Wt, Ct, a->sc, Z, a->write_mu ? a->mu : nullptr, a->stop);
+    else
+      hipLaunchKernelGGL((ppls_panel_mfmadots_kernel<T, R, 2>), dim3(mblocks), dim3(256), 0, st, X, Y,
+                         a->n_local, a->ldx, a->ldy, Wt, Ct, a->sc, Z, a->write_mu ? a->mu : nullptr, a->stop);
   }
   constexpr int VEC = PplsVec16<T>::N;
   if (a->ablate & 256) return hipGetLastError();   // dots only (scores)
@@ -2413,7 +2418,7 @@ int ppls_panel_chunks(int64_t n_local, int ldx, int ldy, int num_cus, int dtype_
   // about 8 rounds: measured at C5 fp32 (tools/chunk_sweep.py) 93 chunks (2 rounds) 9.08 ms,
   // 196 8.70, 300 8.65, 450 8.57, 700 8.58, 1024 8.60 -- more rounds shorten the tail, while the
   // partials the reduction reads grow with the chunk count
-  int64_t ch = (8 * slots + tiles - 1) / tiles;
+  int64_t ch = 8 * slots / tiles;   // (rounding up left a 9th round of a few workgroups; no measurable cost)
   if (ch > maxch) ch = maxch;
   if (ch > 1024) ch = 1024;
   if (ch < 1) ch = 1;

@@ -29,6 +29,28 @@ __global__ __launch_bounds__(256) void rate_kernel(double* out, double seed) {
       c3 = __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, c3, 0, 0, 0);
     }
     s = c0 + c1 + c2 + c3;
+  } else if constexpr (MODE == 3) {   // interleaved: 4 MFMA 16x16x4 chains + 16 VALU FMA per round
+    d4 c0 = {0, 0, 0, 0}, c1 = c0, c2 = c0, c3 = c0;
+    double v[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) v[u] = 0.0;
+    for (int i = 0; i < ITER; ++i) {
+      c0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c0, 0, 0, 0);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = fma(a, b + u, v[u]);
+      c1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c1, 0, 0, 0);
+#pragma unroll
+      for (int u = 4; u < 8; ++u) v[u] = fma(a, b + u, v[u]);
+      c2 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c2, 0, 0, 0);
+#pragma unroll
+      for (int u = 8; u < 12; ++u) v[u] = fma(a, b + u, v[u]);
+      c3 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c3, 0, 0, 0);
+#pragma unroll
+      for (int u = 12; u < 16; ++u) v[u] = fma(a, b + u, v[u]);
+    }
+    s = c0[0] + c1[1] + c2[2] + c3[3];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) s += v[u];
   } else {   // fp64 VALU FMA, 8 chains: 128 flops per wave instruction
     double c[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     for (int i = 0; i < ITER; ++i)
@@ -71,5 +93,9 @@ int main() {
   run<0>("mfma_f64_16x16x4", 2048.0, 4);
   run<1>("mfma_f64_4x4x4_4b", 512.0, 4);
   run<2>("valu fma_f64", 128.0, 8);
+  // 4 MFMA (2048 flops) + 16 VALU FMA (128 flops) per round: if the pipes overlap, the time per round
+  // is max(4 x MFMA, 16 x FMA) instead of their sum (report: ns per round per SIMD)
+  run<3>("mfma 16x16x4 + valu fma", (4 * 2048.0 + 16 * 128.0) / 20.0, 20);
+  run<0>("mfma_f64_16x16x4 (again)", 2048.0, 4);
   return 0;
 }

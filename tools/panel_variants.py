@@ -1,6 +1,6 @@
 """Time the wide-p panel sweep under experiment switches (set_option("ablate", bits)).
 
-    python tools/panel_variants.py <config> bits [bits ...]
+    python tools/panel_variants.py <config> bits[@grid] [bits[@grid] ...]
 
 (config: a bench.py CONFIGS key; split-sweep timing ablations: 1 no compute, 2 no HBM copies,
 4 skip the polar, 8 skip the scalar finalize)
@@ -20,7 +20,7 @@ from ppls_amd import Context  # noqa: E402
 
 def main():
     cfgname = sys.argv[1]
-    bits = [int(b, 0) for b in sys.argv[2:]] or [0]
+    specs = [(int(b.split("@")[0], 0), int(b.split("@")[1]) if "@" in b else 0) for b in sys.argv[2:]] or [(0, 0)]
     cfg = CONFIGS[cfgname]
     n, p, q, r = cfg["n"], cfg["p"], cfg["q"], cfg["r"]
     ctx = Context(0)
@@ -28,8 +28,9 @@ def main():
         ctx.set_option("dtype", 1)
     truth, th0 = make_truth_and_theta0(p, q, r)
     ctx.generate_synthetic(n, p, q, truth, seed=20261015)
-    for b in bits + bits:   # each variant twice, interleaved (clock drift)
+    for b, g in specs + specs:   # each variant twice, interleaved (clock drift)
         ctx.set_option("ablate", b)
+        ctx.set_option("grid", g)   # panel: accumulation row chunks (0 = auto)
         ctx.em_begin(th0)
         ctx.em_iterate(2)
         ctx.synchronize()
@@ -46,7 +47,7 @@ def main():
             tail = f"loglik[-1] {ll[-1]:.10e}"
         except Exception as e:   # noqa: BLE001 (timing ablations that break the results)
             tail = f"(no valid state: {e})"
-        print(f"{cfgname} ablate={b:#x}: sweep {ms / max(launches, 1):.3f} ms, {8 / dt:.1f} it/s, {tail}",
+        print(f"{cfgname} ablate={b:#x} grid={g}: sweep {ms / max(launches, 1):.3f} ms, {8 / dt:.1f} it/s, {tail}",
               flush=True)
     ctx.close()
 
