@@ -513,9 +513,13 @@ int alloc_data(ppls_ctx* c, int64_t n_local, int p, int q, int64_t n_total) {
   // X, Y storage (fp64, or fp32 packed into the double allocation)
   const size_t es = c->dtype ? 4 : 8;
   // + 64 doubles of slack: the panel dots kernel reads whole 128-B column tiles, so the last row's
-  // partial tile may run past the end (those values meet zero rows of the transposed W)
-  if ((rc = dalloc(c, &c->X, ((size_t)std::max<int64_t>(n_local, 1) * c->ldx * es + 7) / 8 + 64))) return rc;
-  if ((rc = dalloc(c, &c->Y, ((size_t)std::max<int64_t>(n_local, 1) * c->ldy * es + 7) / 8 + 64))) return rc;
+  // partial tile may run past the end (those values meet zero rows of the transposed W, so the
+  // slack must hold finite values: it is zeroed here -- reused device memory can hold NaN patterns)
+  const size_t xb = (size_t)std::max<int64_t>(n_local, 1) * c->ldx * es, yb = (size_t)std::max<int64_t>(n_local, 1) * c->ldy * es;
+  if ((rc = dalloc(c, &c->X, (xb + 7) / 8 + 64))) return rc;
+  if ((rc = dalloc(c, &c->Y, (yb + 7) / 8 + 64))) return rc;
+  HIPCHK(c, hipMemsetAsync((char*)c->X + xb, 0, ((xb + 7) / 8 + 64) * 8 - xb, c->stream));
+  HIPCHK(c, hipMemsetAsync((char*)c->Y + yb, 0, ((yb + 7) / 8 + 64) * 8 - yb, c->stream));
   if (!c->ssq && (rc = dalloc(c, &c->ssq, 2))) return rc;
   c->r_alloc = 0;   // force per-r buffers to be re-sized for the new shape
   dfree(c->part);

@@ -2331,6 +2331,8 @@ hipError_t launch_panel_t(const PplsSweepArgs* a, const T* X, const T* Y, double
     const int rb = (big != ((a->ablate & 4096) != 0)) ? 64 : 32;
     const int64_t wtiles = (a->n_local + rb - 1) / rb;
     const int mblocks = (int)((wtiles + 3) / 4 < 16384 ? (wtiles + 3) / 4 : 16384);
+    // (also measured: the B operands prefetched a tile ahead, 256 VGPRs -- no faster, 7.70-7.88 vs
+    // 7.69-7.78 ms; profiles/r2_c5_dots_rows.txt)
     if (rb == 64)
       hipLaunchKernelGGL((ppls_panel_mfmadots_kernel<T, R, 4>), dim3(mblocks), dim3(256), 0, st, X, Y,
                          a->n_local, a->ldx, a->ldy, Wt, Ct, a->sc, Z, a->write_mu ? a->mu : nullptr, a->stop);
