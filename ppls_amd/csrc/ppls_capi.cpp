@@ -2100,7 +2100,7 @@ int ppls_sweep_kernel(ppls_ctx* c, int r, char* buf, int len) {
   if (plan == 3) {
     if (ppls_split_describe(&a, k, sizeof k) != 0) return fail(c, PPLS_E_STATE, "no split instantiation for r=%d", r);
   } else if (plan == 4) {
-    const bool rows64 = (sweep_rows(c) >= 65536) != ((c->ablate & 4096) != 0);   // ppls_kernels.hip launch_panel_t
+    const bool rows64 = (sweep_rows(c) >= 32768) != ((c->ablate & 4096) != 0);   // ppls_kernels.hip launch_panel_t
     snprintf(k, sizeof k, "panel<%s,%d> (mfmadots %d rows/wave + acc, %d chunks)", c->dtype ? "float" : "double", r,
              rows64 ? 64 : 32, a.grid);
   } else {

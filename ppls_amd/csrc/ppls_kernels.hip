@@ -2325,9 +2325,10 @@ hipError_t launch_panel_t(const PplsSweepArgs* a, const T* X, const T* Y, double
                      a->Cp, a->ldx, a->ldy, ldxp, ldyp, R, rs, Wt, Ct, a->stop);
   {   // MFMA dots (profiles/r1_c5_*_dots_variants.txt: faster than the VALU and LDS-DMA forms)
     // rows per wave: 64 (four 16-row blocks per B load: half the B traffic of 32 rows; 246 VGPRs,
-    // 2 waves/SIMD) once there are enough rows to fill the chip, else 32 (146 VGPRs, 3 waves/SIMD).
-    // C5 fp32: 8.28 -> 7.80 ms per sweep (profiles/r2_c5_dots_rows.txt); ablate bit 12 flips it.
-    const bool big = a->n_local >= 65536;
+    // 2 waves/SIMD) from 32768 rows per shard, else 32 (146 VGPRs, 3 waves/SIMD).  C5 fp32: 8.28 ->
+    // 7.80 ms per sweep; C5's 8-GPU share (62,500 rows): 1.125 -> 1.09 ms (profiles/r2_c5_dots_rows.txt).
+    // ablate bit 12 flips it.
+    const bool big = a->n_local >= 32768;
     const int rb = (big != ((a->ablate & 4096) != 0)) ? 64 : 32;
     const int64_t wtiles = (a->n_local + rb - 1) / rb;
     const int mblocks = (int)((wtiles + 3) / 4 < 16384 ? (wtiles + 3) / 4 : 16384);

@@ -121,7 +121,7 @@ def test_c3_full_size_properties(ctx):
 def test_c5_kernel_parity_vs_oracle(ctx, rows64):
     """The C5 panel sweep (fp32 storage) on n = 5,000 rows of the C5 model vs the fp64 oracle on the
     fp32-rounded data (the data as stored); dots64 = the 64-rows-per-wave dots kernel the full-size
-    C5 run uses (ablate bit 12 selects it below 65536 rows)."""
+    C5 run uses (ablate bit 12 selects it below 32768 rows)."""
     n, p, q, r, steps = 5_000, 10_000, 500, 10, 3
     truth, th0 = _truth_theta0(p, q, r)
     ctx.set_option("dtype", 1)

@@ -18,7 +18,7 @@ pytestmark = pytest.mark.gpu
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
 # sweep-kernel variants (context options): split ownership (default; auto = 2 rows per step,
 # occupancy grid), split 1 row/step pipelined / unpipelined, the same with non-temporal loads,
-# generic two-pass, panel (wide p) with 32 and (ablate bit 12 below 65536 rows) 64 rows per dots wave
+# generic two-pass, panel (wide p) with 32 and (ablate bit 12 below 32768 rows) 64 rows per dots wave
 SWEEPS = [dict(), dict(rows_per_step=1, pipe=1), dict(rows_per_step=1, pipe=0), dict(nt=1), dict(sweep=2),
           dict(sweep=3), dict(sweep=3, ablate=4096)]
 SWEEP_IDS = ["split", "split_rp1", "split_rp1_nopipe", "split_nt", "twopass", "panel", "panel_rows64"]
