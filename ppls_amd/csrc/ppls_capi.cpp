@@ -34,6 +34,7 @@ struct ppls_ctx {
   int rp_opt = 0;   // rows per pipeline step: 0 auto (2 where the kernel fits in registers)
   int pipe_opt = 1;     // split kernel: software-pipelined order
   int ablate = 0;
+  int ldpad = 1;   // row padding of the panel sweep's rows (ld_of); 0 = 16-B rows (experiment)
   int dtype = 0;           // storage of X, Y: 0 fp64, 1 fp32 (arithmetic is fp64 either way)
   int nt_loads = -1;       // sweep LDS-DMA non-temporal: -1 auto (when X, Y exceed the MALL), 0 off, 1 on
   int timing = 0;          // 0 off; N > 0: bracket every N-th sweep launch with HIP events
@@ -146,7 +147,20 @@ void dfree(T*& p) {
   p = nullptr;
 }
 
-int ld_of(int p, int f32 = 0) { return f32 ? (p + 3) & ~3 : (p + 1) & ~1; }   // 16-B rows
+// Row stride (elements) of the resident X or Y.  16-B rows for narrow data and for the fp64 rows of
+// the split sweep (p <= 2048: its DMA ring streams whole row ranges, alignment beyond 16 B is moot,
+// and C3's 16,000-B rows stay unpadded).  Rows the panel sweep reads (fp32 storage, wider fp64) are
+// padded to 128 B (one cache line per dots tile) and from 16 KB to 4 KB: the accumulation pass reads
+// 4-KB column segments of every row, and 4-KB-aligned segments stream faster -- 5e5 x 40 KB rows,
+// no arithmetic: 16-B-aligned stride 3.24 ms, 128-B 3.07 ms, 4-KB 2.93 ms
+// (tools/acc_pattern_probe.hip, profiles/r2_row_alignment_probe.txt).  Padding columns are zero.
+int ld_of(int p, int f32 = 0, int pad = 1) {
+  const int es = f32 ? 4 : 8;
+  const long bytes = (long)p * es;
+  if (!pad || bytes < 1024 || (!f32 && p <= 2048)) return f32 ? (p + 3) & ~3 : (p + 1) & ~1;
+  const long al = bytes >= 16384 ? 4096 : 128;
+  return (int)(((bytes + al - 1) / al * al) / es);
+}
 
 int check_theta(ppls_ctx* c, const ppls_theta* th, int r) {
   if (!th || !th->W || !th->C || !th->B || !th->sigT) return fail(c, PPLS_E_ARG, "theta has NULL fields");
@@ -508,8 +522,8 @@ int alloc_data(ppls_ctx* c, int64_t n_local, int p, int q, int64_t n_total) {
   c->n_total = n_total > 0 ? n_total : n_local;
   c->p = p;
   c->q = q;
-  c->ldx = ld_of(p, c->dtype);
-  c->ldy = ld_of(q, c->dtype);
+  c->ldx = ld_of(p, c->dtype, c->ldpad);
+  c->ldy = ld_of(q, c->dtype, c->ldpad);
   // X, Y storage (fp64, or fp32 packed into the double allocation)
   const size_t es = c->dtype ? 4 : 8;
   // + 64 doubles of slack: the panel dots kernel reads whole 128-B column tiles, so the last row's
@@ -677,6 +691,8 @@ int ppls_set_option(ppls_ctx* c, const char* key, int64_t value) {
     c->rp_opt = (int)value;
   } else if (!strcmp(key, "pipe")) {
     c->pipe_opt = value ? 1 : 0;
+  } else if (!strcmp(key, "ldpad")) {   // applies to data set or generated afterwards
+    c->ldpad = value ? 1 : 0;
   } else if (!strcmp(key, "ablate")) {
     if (value < 0 || value > 65535) return fail(c, PPLS_E_ARG, "ablate must be in [0,65535]");
     c->ablate = (int)value;   // timing experiments (bits 0-9 break results; 10+ select equivalent variants)

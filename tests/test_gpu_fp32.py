@@ -79,3 +79,33 @@ def test_fp32_sequential_init_matches_oracle():
     ref = o.ppls(X32, Y32, 2, 20, 1e-4, inits)
     assert np.abs(f["W"] - ref["W"]).max() < 1e-8
     assert _relerr(f["Other_output"]["Loglikelihoods"], ref["Other_output"]["Loglikelihoods"]) < 1e-10
+
+
+@pytest.mark.parametrize("dtype,p,q", [(1, 4100, 300), (1, 700, 41), (0, 2600, 9)])
+def test_row_padding_is_invisible(dtype, p, q):
+    """Panel-path rows are padded to 128 B / 4 KB (ldpad, ppls_capi.cpp ld_of); the padding
+    columns are zero, so a fit on padded rows equals the 16-B-row fit (the E-step and one EM step
+    bitwise; over several iterations to rounding, since the grid partition of the ||X||^2 and
+    reduction kernels follows the row stride), and get_data returns the unpadded matrices.
+    (4100 fp32 = 16,400 B -> 4-KB padding; 700 fp32 -> 128 B; 2600 fp64 = 20,800 B -> 4 KB.)"""
+    from ppls_amd import Context
+    r = 3
+    X, Y, th0 = make_problem(700, p, q, r, seed=p + q)
+    out = []
+    for pad in (0, 1):
+        with Context(0) as c:
+            c.set_option("dtype", dtype)
+            c.set_option("ldpad", pad)
+            c.set_data(X, Y)
+            Xb, Yb = c.get_data()
+            mu = c.estep(_theta(th0)).mu_T
+            one, _ = c.em_step(_theta(th0))
+            est, ll, _, _ = c.em_run(_theta(th0), 3, -np.inf, 0, want_eout=False)
+            out.append((Xb, Yb, mu, one, est, ll))
+    (X0, Y0, m0, o0, e0, l0), (X1, Y1, m1, o1, e1, l1) = out
+    assert X1.shape == (700, p) and Y1.shape == (700, q)
+    assert np.array_equal(X0, X1) and np.array_equal(Y0, Y1)
+    assert np.array_equal(m0, m1)
+    assert np.array_equal(o0.W, o1.W) and np.array_equal(o0.C, o1.C)
+    assert _relerr(l1, l0) < 1e-14
+    assert np.abs(e0.W - e1.W).max() < 1e-14 and np.abs(e0.C - e1.C).max() < 1e-14

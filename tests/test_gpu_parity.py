@@ -90,7 +90,7 @@ def test_em_run_matches_golden(ctx, name, sweep):
 @pytest.mark.parametrize("sweep", SWEEPS, ids=SWEEP_IDS)
 @pytest.mark.parametrize("n,p,q,r", [(200, 50, 50, 2), (97, 33, 7, 1), (301, 64, 31, 5), (50, 9, 12, 8),
                                      (3, 5, 4, 2), (1, 6, 3, 1), (700, 1025, 3, 2), (400, 3, 1500, 3),
-                                     (150, 17, 14, 10), (90, 24, 20, 16)])
+                                     (150, 17, 14, 10), (90, 24, 20, 16), (120, 2600, 9, 3)])
 def test_estep_mstep_loglik_vs_oracle(ctx, sweep, n, p, q, r):
     X, Y, th0 = make_problem(n, p, q, r, seed=n + p + q + r)
     _apply(ctx, sweep)
