@@ -12,11 +12,13 @@ typedef float f4 __attribute__((ext_vector_type(4)));
 template <int MODE>
 __global__ __launch_bounds__(256) void probe(const char* __restrict__ X, long n, long ldb, long rpc, int nch,
                                              double* out) {
+  extern __shared__ char pad_lds[];   // dynamic LDS only to cap the workgroups per CU
+  if (out == nullptr) pad_lds[threadIdx.x] = 0;
   const int tile = blockIdx.x, chunk = blockIdx.y;
   const char* base = X + (long)tile * 4096 + threadIdx.x * 16;
   double s = 0.0;
   long r0, r1, step;
-  if (MODE == 0) { r0 = (long)chunk * rpc; r1 = r0 + rpc < n ? r0 + rpc : n; step = 1; }
+  if (MODE != 1) { r0 = (long)chunk * rpc; r1 = r0 + rpc < n ? r0 + rpc : n; step = 1; }
   else { r0 = chunk; r1 = n; step = nch; }
   for (long r = r0; r < r1; r += 8 * step) {
     f4 v[8];
@@ -28,6 +30,7 @@ __global__ __launch_bounds__(256) void probe(const char* __restrict__ X, long n,
     }
 #pragma unroll
     for (int u = 0; u < 8; ++u) s += (double)v[u].x + (double)v[u].w;
+    if (MODE == 2 && ((r - r0) & 127) == 120) __syncthreads();   // a barrier per 128 rows (mu batches)
   }
   if (s == 12345.678) out[0] = s;
 }
@@ -41,22 +44,24 @@ int main(int argc, char** argv) {
   hipEvent_t e0, e1;
   (void)hipEventCreate(&e0); (void)hipEventCreate(&e1);
   printf("row stride %ld B\n", ldb);
+  for (int lds : {0, 72 * 1024}) {   // 8+, 2 workgroups per CU
   for (int nch : {372}) {
     const long rpc = (n + nch - 1) / nch;
-    for (int mode = 0; mode < 2; ++mode) {
+    for (int mode = 0; mode < 3; mode += 2) {
       float best = 1e30f;
       for (int rep = 0; rep < 5; ++rep) {
         (void)hipEventRecord(e0);
-        if (mode == 0) hipLaunchKernelGGL(probe<0>, dim3(10, nch), dim3(256), 0, 0, X, n, ldb, rpc, nch, out);
-        else hipLaunchKernelGGL(probe<1>, dim3(10, nch), dim3(256), 0, 0, X, n, ldb, rpc, nch, out);
+        if (mode == 0) hipLaunchKernelGGL(probe<0>, dim3(10, nch), dim3(256), lds, 0, X, n, ldb, rpc, nch, out);
+        else hipLaunchKernelGGL(probe<2>, dim3(10, nch), dim3(256), lds, 0, X, n, ldb, rpc, nch, out);
         (void)hipEventRecord(e1);
         (void)hipEventSynchronize(e1);
         float ms; (void)hipEventElapsedTime(&ms, e0, e1);
         if (rep > 0 && ms < best) best = ms;
       }
-      printf("chunks %4d mode %d (%s): %.3f ms  %.0f GB/s\n", nch, mode, mode ? "interleaved rows" : "row ranges",
-             best, bytes / 1e6 / best);
+      printf("lds %6d B/WG chunks %4d mode %d (%s): %.3f ms  %.0f GB/s\n", lds, nch, mode,
+             mode ? "row ranges, barrier per 128 rows" : "row ranges", best, bytes / 1e6 / best);
     }
+  }
   }
   return 0;
 }
