@@ -178,6 +178,9 @@ def main():
     ap.add_argument("--cpu-iters", type=int, default=3, help="timed CPU-baseline iterations (full n)")
     ap.add_argument("--timing-every", type=int, default=4,
                     help="bracket every N-th sweep of the timed region with HIP events")
+    ap.add_argument("--comm", default="rccl", choices=["rccl", "host"],
+                    help="N>1 statistics all-reduce: RCCL (default) or the host reducer hook over gloo "
+                         "(ppls_set_reducer; rehearses the multi-rank bench with several ranks on one GPU)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -205,10 +208,14 @@ def main():
     if cfg.get("storage") == "f32":
         ctx.set_option("dtype", 1)
     ctx.set_option("sweep", args.sweep)
-    if world > 1:
+    if world > 1 and args.comm == "rccl":
         uid = [Context.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         ctx.comm_init(world, rank, uid[0])
+    elif world > 1:
+        def host_allreduce(buf):   # the library's host staging buffer, summed in place over gloo
+            dist.all_reduce(torch.from_numpy(buf))
+        ctx.set_reducer(host_allreduce)
     row0, n_local = Context.shard_range(n, world, rank)
     truth, th0 = make_truth_and_theta0(p, q, r)
     ctx.generate_synthetic(n, p, q, truth, seed=20261015, row0=row0, n_local=n_local)
@@ -264,7 +271,8 @@ def main():
                    storage=cfg.get("storage", "f64"),
                    data="synthetic (simulC model: X=TW'+sigE E, Y=UC'+sigF F; Philox normals on device)",
                    config=dict(workload=cfg["name"], n=n, p=p, q=q, r=r,
-                               parallelism=f"dp{world} (rows sharded, 1 RCCL all-reduce/iteration)"),
+                               parallelism=f"dp{world} (rows sharded, 1 {'RCCL' if args.comm == 'rccl' else 'host (gloo)'} "
+                                           f"all-reduce/iteration)"),
                    roofline=roofline,
                    loglik_last=float(ll[-1]) if len(ll) else None)
         if world == 1 and not args.no_cpu:
