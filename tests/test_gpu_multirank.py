@@ -78,8 +78,10 @@ def _theta(th):
 
 
 @pytest.mark.parametrize("k,n,p,q,r,dtype", [(3, 3001, 300, 200, 4, 0), (4, 2000, 700, 90, 10, 0),
-                                             (2, 1500, 260, 130, 3, 1)],
-                         ids=["split_k3", "panel_k4", "panel_fp32_k2"])
+                                             (2, 1500, 260, 130, 3, 1), (4, 3, 20, 12, 2, 0),
+                                             (4, 3, 20, 12, 2, 1)],
+                         ids=["split_k3", "panel_k4", "panel_fp32_k2", "split_empty_shard",
+                              "panel_fp32_empty_shard"])
 def test_k_contexts_sharded_equal_unsharded(k, n, p, q, r, dtype):
     from ppls_amd import Context
     X, Y, th0 = make_problem(n, p, q, r, seed=n + k)
@@ -99,19 +101,22 @@ def test_k_contexts_sharded_equal_unsharded(k, n, p, q, r, dtype):
         return fit(c, X[r0:r0 + nl], Y[r0:r0 + nl], n)
 
     res = _run_ranks(k, work)
+    assert min(Context.shard_range(n, k, rk)[1] for rk in range(k)) >= (0 if n < k else 1)
     assert res[0][3] == ref[3] == ("split512" if (r <= 8 and not dtype and p <= 2048) else "panel")
     for est, ll, eout, _ in res:
         assert np.array_equal(est.W, res[0][0].W) and np.array_equal(est.C, res[0][0].C)
         assert np.array_equal(ll, res[0][1])
         assert np.array_equal(eout.Ctt, res[0][2].Ctt) and eout.Cee == res[0][2].Cee
     est, ll, eout, _ = res[0]
-    assert np.abs(ll - ref[1]).max() / np.abs(ref[1]).max() < 1e-12
-    assert np.abs(est.W - ref[0].W).max() < 1e-12 and np.abs(est.C - ref[0].C).max() < 1e-12
-    assert np.abs(est.B - ref[0].B).max() / np.abs(ref[0].B).max() < 1e-12
-    assert abs(est.sigE - ref[0].sigE) / ref[0].sigE < 1e-12
-    # Eout rows stay sharded: the concatenation is the unsharded mu_T
-    mu = np.vstack([e.mu_T for _, _, e, _ in res])
-    assert np.abs(mu - ref[2].mu_T).max() / np.abs(ref[2].mu_T).max() < 1e-12
+    # (3 rows with p >> n: an ill-posed fit that amplifies the sharded sums' rounding ~100x)
+    tol = 1e-12 if n >= 100 else 1e-10
+    assert np.abs(ll - ref[1]).max() / np.abs(ref[1]).max() < tol
+    assert np.abs(est.W - ref[0].W).max() < tol and np.abs(est.C - ref[0].C).max() < tol
+    assert np.abs(est.B - ref[0].B).max() / np.abs(ref[0].B).max() < tol
+    assert abs(est.sigE - ref[0].sigE) / ref[0].sigE < tol
+    # Eout rows stay sharded: the concatenation is the unsharded mu_T (a rank with no rows holds none)
+    mu = np.vstack([e.mu_T.reshape(-1, r) for _, _, e, _ in res])
+    assert np.abs(mu - ref[2].mu_T).max() / np.abs(ref[2].mu_T).max() < tol
 
 
 def test_k_contexts_initialiser_and_meta_sharded():
