@@ -921,7 +921,8 @@ __global__ __launch_bounds__(256) void ppls_panel_acc_kernel(
 #pragma unroll
     for (int k = 0; k < R; ++k)
 #pragma unroll
-      for (int v = 0; v < VEC; ++v) dst[(int64_t)k * ld + col + v] = acc[v][k];
+      for (int v = 0; v < VEC; ++v)   // streaming stores: the partials are read once, by the reduce
+        __builtin_nontemporal_store(acc[v][k], dst + (int64_t)k * ld + col + v);
   }
   if (blockIdx.x == 0) {   // Gram of [Xw Yc] over the chunk (2R x 2R, column-major)
     constexpr int V2 = 2 * R, NP = V2 * (V2 + 1) / 2, BR = 64;
