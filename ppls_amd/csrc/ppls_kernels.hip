@@ -816,10 +816,25 @@ __global__ void ppls_transpose_wc_kernel(const double* __restrict__ W, const dou
   }
 }
 
+// Row chunks of the accumulation grid: chunks [0, nbig) hold `big` rows each, the rest `small`
+// rows (a guided static schedule: workgroups are dispatched in chunk order, so the large chunks run
+// first and the small ones fill the tail; fewer partials to write and reduce than equal chunks with
+// the same tail).  Fixed by (n, chunk count), so results stay deterministic.
+struct PplsChunks {
+  int64_t big, small;
+  int nbig;
+  __host__ __device__ void range(int c, int64_t n, int64_t& r0, int64_t& r1) const {
+    r0 = c < nbig ? (int64_t)c * big : (int64_t)nbig * big + (int64_t)(c - nbig) * small;
+    const int64_t len = c < nbig ? big : small;
+    if (r0 > n) r0 = n;
+    r1 = r0 + len < n ? r0 + len : n;
+  }
+};
+
 template <typename T, int R, bool NT>
 __global__ __launch_bounds__(256) void ppls_panel_acc_kernel(
     const T* __restrict__ X, const T* __restrict__ Y, int64_t n, int ldx, int ldy,
-    const double* __restrict__ Z, int64_t rows_per_chunk, double* __restrict__ part, int64_t part_ld,
+    const double* __restrict__ Z, PplsChunks ck, double* __restrict__ part, int64_t part_ld,
     const int* __restrict__ stop) {
   if (stop && *stop) return;   // em_run converged earlier (device stop flag)
   constexpr int VEC = PplsVec16<T>::N;
@@ -831,8 +846,8 @@ __global__ __launch_bounds__(256) void ppls_panel_acc_kernel(
   const int ld = isx ? ldx : ldy;
   const T* M = isx ? X : Y;
   const int off = isx ? 2 * R : 3 * R;
-  const int64_t r0 = (int64_t)blockIdx.y * rows_per_chunk;
-  const int64_t r1 = min(n, r0 + rows_per_chunk);
+  int64_t r0, r1;
+  ck.range(blockIdx.y, n, r0, r1);
   double* pg = part + (int64_t)blockIdx.y * part_ld;
   // mu (mu_T for X tiles, mu_U for Y tiles) of BR rows at a time in LDS (every lane reads the same
   // address: broadcast).  Software-pipelined: the next batch's mu is loaded into registers while the
@@ -2344,7 +2359,17 @@ hipError_t launch_panel_t(const PplsSweepArgs* a, const T* X, const T* Y, double
   }
   constexpr int VEC = PplsVec16<T>::N;
   if (a->ablate & 256) return hipGetLastError();   // dots only (scores)
-  const int64_t rpc = (a->n_local + chunks - 1) / chunks;
+  PplsChunks ck;
+  if (a->ablate & 1024) {   // experiment: equal chunks
+    ck.big = ck.small = (a->n_local + chunks - 1) / chunks;
+    ck.nbig = chunks;
+  } else {   // half the chunks at 4x the rows of the other half
+    ck.nbig = chunks / 2;
+    const int nsmall = chunks - ck.nbig;
+    ck.big = (4 * a->n_local + 4 * ck.nbig + nsmall - 1) / (4 * ck.nbig + nsmall);
+    ck.small = (ck.big + 3) / 4;
+    if (ck.small < 1) ck.small = 1;
+  }
   // VALU accumulation: at C5 an MFMA form measured no faster in fp64 storage (7.7 vs 7.5 ms) and
   // slower in fp32 (6.0 vs 4.5 ms; profiles/r1_c5_*_acc_variants.txt) -- the pass is load-bound
   const int ntx = (a->ldx + 256 * VEC - 1) / (256 * VEC), nty = (a->ldy + 256 * VEC - 1) / (256 * VEC);
@@ -2352,10 +2377,10 @@ hipError_t launch_panel_t(const PplsSweepArgs* a, const T* X, const T* Y, double
   // sweep's nt policy, ablate bit 16): C5 fp32 4.05 -> 3.89 ms (profiles/r2_c5_nt_policy.txt)
   if (a->ablate & 16)
     hipLaunchKernelGGL((ppls_panel_acc_kernel<T, R, true>), dim3(ntx + nty, chunks), dim3(256), 0, st, X, Y,
-                       a->n_local, a->ldx, a->ldy, Z, rpc, a->part, a->part_ld, a->stop);
+                       a->n_local, a->ldx, a->ldy, Z, ck, a->part, a->part_ld, a->stop);
   else
     hipLaunchKernelGGL((ppls_panel_acc_kernel<T, R, false>), dim3(ntx + nty, chunks), dim3(256), 0, st, X, Y,
-                       a->n_local, a->ldx, a->ldy, Z, rpc, a->part, a->part_ld, a->stop);
+                       a->n_local, a->ldx, a->ldy, Z, ck, a->part, a->part_ld, a->stop);
   return hipGetLastError();
 }
 
@@ -2429,10 +2454,11 @@ int ppls_panel_chunks(int64_t n_local, int ldx, int ldy, int num_cus, int dtype_
   if (panel_acc_occupancy(dtype_f32, r, &occ) != hipSuccess || occ < 1) occ = 1;
   const int64_t slots = (int64_t)num_cus * occ;
   const int64_t maxch = (n_local + 255) / 256;   // at least 256 rows per chunk
-  // about 8 rounds: measured at C5 fp32 (tools/chunk_sweep.py) 93 chunks (2 rounds) 9.08 ms,
-  // 196 8.70, 300 8.65, 450 8.57, 700 8.58, 1024 8.60 -- more rounds shorten the tail, while the
-  // partials the reduction reads grow with the chunk count
-  int64_t ch = 8 * slots / tiles;   // (rounding up left a 9th round of a few workgroups; no measurable cost)
+  // Equal chunks needed about 8 rounds (round 1, C5 fp32: 93 chunks 9.08 ms, 196 8.70, 450 8.57):
+  // more rounds shorten the tail, while the partials written and reduced grow with the chunk count
+  // (profiles/r2_row_alignment_probe.txt: the write-out is the kernel's largest overhead).  Now 4
+  // rounds, half of them large chunks (PplsChunks): half the partials, about the same tail.
+  int64_t ch = 4 * slots / tiles;
   if (ch > maxch) ch = maxch;
   if (ch > 1024) ch = 1024;
   if (ch < 1) ch = 1;
