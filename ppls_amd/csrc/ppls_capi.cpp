@@ -34,6 +34,7 @@ struct ppls_ctx {
   int rp_opt = 0;   // rows per pipeline step: 0 auto (2 where the kernel fits in registers)
   int pipe_opt = 1;     // split kernel: software-pipelined order
   int ablate = 0;
+  int polar1 = 1;   // finalize polar: Cholesky-QR1 fast path when kappa(X'mu) <= PPLS_POLAR1_KAPPA
   int ldpad = 1;   // row padding of the panel sweep's rows (ld_of); 0 = 16-B rows (experiment)
   int dtype = 0;           // storage of X, Y: 0 fp64, 1 fp32 (arithmetic is fp64 either way)
   int nt_loads = -1;       // sweep LDS-DMA non-temporal: -1 auto (when X, Y exceed the MALL), 0 off, 1 on
@@ -446,7 +447,7 @@ int finalize(ppls_ctx* c, int r, int cur, int nxt, int logl_index, int type, int
   f.work = c->work;
   f.status = c->status;
   f.qr = type == PPLS_ORTH_QR ? 1 : 0;
-  f.mode = 3 & ~(c->ablate >> 2);   // ablate bit2: skip polar, bit3: skip scalars (timing only)
+  f.mode = (3 & ~(c->ablate >> 2)) | (c->polar1 ? 4 : 0);   // ablate bit2: skip polar, bit3: skip scalars
   f.trace = c->ftrace;
   f.gram_cur = c->gram[cur];
   f.gram_nxt = c->gram[nxt];
@@ -689,6 +690,8 @@ int ppls_set_option(ppls_ctx* c, const char* key, int64_t value) {
   } else if (!strcmp(key, "rows_per_step")) {
     if (value < 0 || value > 2) return fail(c, PPLS_E_ARG, "rows_per_step must be 0 (auto), 1 or 2");
     c->rp_opt = (int)value;
+  } else if (!strcmp(key, "polar1")) {
+    c->polar1 = value ? 1 : 0;
   } else if (!strcmp(key, "pipe")) {
     c->pipe_opt = value ? 1 : 0;
   } else if (!strcmp(key, "ldpad")) {   // applies to data set or generated afterwards
@@ -1050,7 +1053,7 @@ int ppls_mstep(ppls_ctx* c, const ppls_expect* fit, int r, int type, ppls_theta*
   memset(&f, 0, sizeof f);
   f.stats = c->stats; f.ssq = c->ssq; f.N = (double)c->n_total; f.p = c->p; f.q = c->q; f.r = r;
   f.ldx = c->ldx; f.ldy = c->ldy; f.Wn = c->W[1]; f.Cn = c->C[1]; f.work = c->work; f.status = c->status;
-  f.logl_index = -1; f.qr = type == PPLS_ORTH_QR ? 1 : 0; f.mode = 1;   // polar only
+  f.logl_index = -1; f.qr = type == PPLS_ORTH_QR ? 1 : 0; f.mode = 1 | (c->polar1 ? 4 : 0);   // polar only
   HIPCHK(c, ppls_launch_finalize(&f, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   if ((rc = check_status(c))) return rc;

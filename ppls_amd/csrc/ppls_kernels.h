@@ -52,7 +52,8 @@ struct PplsFinalizeArgs {
   double* work;          // 2 (p+q) r doubles
   int* status;
   int qr;                // orth type: 0 SVD (polar), 1 QR
-  int mode;              // bit0: W/C update (polar), bit1: scalars (moments, loglik, M-step)
+  int mode;              // bit0: W/C update (polar), bit1: scalars (moments, loglik, M-step),
+                         // bit2: Cholesky-QR1 fast path allowed for well-conditioned X'mu
   const double* gram_cur;   // [W'W | C'C] (2 r^2) of Wc, Cc, or nullptr (finalize computes it)
   double* gram_nxt;         // receives [Wn'Wn | Cn'Cn], or nullptr
   double* vstate;           // [V_W | V_C] (2 r^2) Jacobi warm start carried across iterations, or nullptr
@@ -68,6 +69,8 @@ struct PplsFinalizeArgs {
 
 #define PPLS_TEAM_ROWS 1024   // rows of S per polar team member
 #define PPLS_TEAM_MAX 32
+// finalize polar: Cholesky-QR1 (one pass, no second team barrier) when kappa(X'mu) <= this
+#define PPLS_POLAR1_KAPPA 8.0
 
 // One EM step of the sequential initialiser's rank-1 fit on the device (ppls_rank1_step_kernel).
 struct PplsRank1StepArgs {

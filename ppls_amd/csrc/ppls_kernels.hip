@@ -1444,7 +1444,8 @@ template <int R, int NT>
 __device__ bool ppls_block_polar_fast(const double* __restrict__ S, int64_t lds, int p,
                                       double* __restrict__ out, int64_t ldo, int ldo_rows, double* Sl,
                                       double* sh, double* sm, double* __restrict__ gram_out,
-                                      double* __restrict__ vstate, long long* tr, const PplsTeam& tm) {
+                                      double* __restrict__ vstate, long long* tr, const PplsTeam& tm,
+                                      bool polar1) {
   constexpr int NG = R * (R + 1) / 2;
   constexpr int NW = NT / 64;
   constexpr int G = PplsWaveBlk<R>::G, GG = G * G;
@@ -1531,10 +1532,84 @@ __device__ bool ppls_block_polar_fast(const double* __restrict__ S, int64_t lds,
   const double* Sr = Sl ? Sl : S;
   const int64_t ldr = Sl ? nr : lds;
   const int sro = Sl ? i0 : 0;
-  // Q1 is kept where pass 3 reads it back (each thread its own rows): over S in LDS, else in out
-  double* Qs = Sl ? Sl : out;
-  const int64_t ldq = Sl ? nr : ldo;
-  const int qo = Sl ? i0 : 0;
+  // re-orthonormalise the carried V in sV (modified Gram-Schmidt, rows on lanes; wave 0)
+  auto load_vprev = [&]() {
+    for (int e = lane; e < GG; e += 64) {
+#pragma unroll
+      for (int u = 0; u < (GG + 63) / 64; ++u)
+        if (e == lane + 64 * u) sV[e] = vprev[u];
+    }
+    ppls_wave_lds_fence();
+    if (vstate) {
+      const int rt = lane % G;
+      for (int j = 0; j < R; ++j) {
+        double vj = sV[j * G + rt];
+        for (int i = 0; i < j; ++i) {
+          const double vi = sV[i * G + rt];
+          vj = fma(-ppls_groupG_sum<G>(vi * vj), vi, vj);
+        }
+        vj *= ppls_rsq(ppls_groupG_sum<G>(vj * vj));
+        if (lane < G) sV[j * G + rt] = vj;
+        ppls_wave_lds_fence();
+      }
+    }
+  };
+  // Cholesky-QR1 fast path (polar1): T = R1 = U_T Sigma V' by the Jacobi; when kappa(S) = kappa(R1)
+  // <= PPLS_POLAR1_KAPPA, Q1 = S R1^-1 is already orthonormal to O(eps kappa^2) (~1e-14), so pass 2,
+  // its team barrier and chol(G2) are skipped: out = S F, F = R1^-1 U_T V'.  Every member decides
+  // on the bitwise-identical G1, so a team takes one path.
+  __shared__ int fast;
+  if (tid < 64) {
+    bool fst = false;
+    if (polar1) {
+      load_vprev();
+      ppls_matmul_wave<R, false>(sT, sV, sA);                // sA = R1 V (sT keeps R1)
+      ppls_jacobi_wave<R>(sA, sV);
+      if (lane < R) {
+        double nrm = 0.0;
+#pragma unroll
+        for (int t = 0; t < R; ++t) nrm = fma(sA[lane * G + t], sA[lane * G + t], nrm);
+        ssv[lane] = sqrt(nrm);
+      }
+      ppls_wave_lds_fence();
+      double smax = 0.0, smin = ssv[0];
+#pragma unroll
+      for (int i = 0; i < R; ++i) { smax = fmax(smax, ssv[i]); smin = fmin(smin, ssv[i]); }
+      fst = smin > 0.0 && smin * PPLS_POLAR1_KAPPA >= smax;
+      if (fst) {
+        for (int e = lane; e < GG; e += 64) {                  // sU = U_T V'
+          const int a = e % G, b = e / G;
+          double s = 0.0;
+          if (a < R && b < R)
+#pragma unroll
+            for (int kk = 0; kk < R; ++kk) s = fma(sA[kk * G + a] * (1.0 / ssv[kk]), sV[kk * G + b], s);
+          sU[e] = s;
+        }
+        ppls_wave_lds_fence();
+        for (int e = lane; e < R * R; e += 64) {               // F = R1^-1 U_T V' -> sm + R^2 (ld R)
+          const int a = e % R, b = e / R;
+          double s = 0.0;
+#pragma unroll
+          for (int kk = 0; kk < R; ++kk) s = fma(sF[kk * R + a], sU[b * G + kk], s);
+          sF[R * R + b * R + a] = s;
+          if (vstate && tm.rank == 0) vstate[b * R + a] = sV[b * G + a];   // every member's V is identical
+        }
+      }
+    }
+    if (lane == 0) fast = fst;
+  }
+  __syncthreads();
+  const bool use1 = fast != 0;
+  // the rows pass 3 multiplies: S itself (fast path), else Q1, kept where pass 3 reads it back
+  // (each thread its own rows): over S in LDS, else in out
+  const double* Qs = use1 ? Sr : (Sl ? Sl : out);
+  const int64_t ldq = use1 ? ldr : (Sl ? nr : ldo);
+  const int qo = use1 ? sro : (Sl ? i0 : 0);
+  if (use1) {
+    ppls_team_leave(tm);   // no further barrier on this path
+    ppls_stamp(tr, 4);
+  } else {
+  double* Qw = Sl ? Sl : out;
   // pass 2: G2 = Q1'Q1, Q1 = S R1^-1
   {
     double M[R][R];
@@ -1558,7 +1633,7 @@ __device__ bool ppls_block_polar_fast(const double* __restrict__ S, int64_t lds,
       }
       ppls_gram_acc<R>(qv, vals);
 #pragma unroll
-      for (int j = 0; j < R; ++j) Qs[(int64_t)j * ldq + i - qo] = qv[j];
+      for (int j = 0; j < R; ++j) Qw[(int64_t)j * ldq + i - qo] = qv[j];
     }
   }
   ppls_stamp(tr, 15);
@@ -1567,8 +1642,8 @@ __device__ bool ppls_block_polar_fast(const double* __restrict__ S, int64_t lds,
   ppls_team_leave(tm);   // the last barrier of this member
   ppls_stamp(tr, 3);
   if (tid < 64) {   // wave 0: R2 = chol(G2), T = R2 R1, warm start, Jacobi, F
-    for (int e = lane; e < GG; e += 64) {
-      if constexpr (R > 6) {
+    if constexpr (R > 6) {
+      for (int e = lane; e < GG; e += 64) {
         const int a = e % G, b = e / G;
         double v = 0.0;
         if (a < R && b < R) {
@@ -1577,9 +1652,6 @@ __device__ bool ppls_block_polar_fast(const double* __restrict__ S, int64_t lds,
         }
         sA[e] = v;
       }
-#pragma unroll
-      for (int u = 0; u < (GG + 63) / 64; ++u)
-        if (e == lane + 64 * u) sV[e] = vprev[u];
     }
     ppls_wave_lds_fence();
     bool good = true;
@@ -1606,19 +1678,7 @@ __device__ bool ppls_block_polar_fast(const double* __restrict__ S, int64_t lds,
       ppls_matmul_wave<R, false>(sU, sT, sA);               // sA = R2 R1 = T
     }
     ppls_stamp(tr, 6);
-    if (vstate) {   // re-orthonormalise the carried V (modified Gram-Schmidt, rows on lanes)
-      const int rt = lane % G;
-      for (int j = 0; j < R; ++j) {
-        double vj = sV[j * G + rt];
-        for (int i = 0; i < j; ++i) {
-          const double vi = sV[i * G + rt];
-          vj = fma(-ppls_groupG_sum<G>(vi * vj), vi, vj);
-        }
-        vj *= ppls_rsq(ppls_groupG_sum<G>(vj * vj));
-        if (lane < G) sV[j * G + rt] = vj;
-        ppls_wave_lds_fence();
-      }
-    }
+    load_vprev();                                          // sV = the carried V, re-orthonormalised
     ppls_matmul_wave<R, false>(sA, sV, sT);                // sT = T V (A of the Jacobi)
     ppls_stamp(tr, 7);
     const int sweeps = ppls_jacobi_wave<R>(sT, sV);
@@ -1675,7 +1735,8 @@ __device__ bool ppls_block_polar_fast(const double* __restrict__ S, int64_t lds,
   __syncthreads();
   ppls_stamp(tr, 4);
   if (!ok) return false;
-  // pass 3: out = Q1 P (+ Gram of out)
+  }   // CholQR2 path
+  // pass 3: out = Q1 P, or S F on the fast path (+ Gram of out)
   double F[R][R];
 #pragma unroll
   for (int a = 0; a < R; ++a)
@@ -1903,7 +1964,7 @@ __global__ __launch_bounds__(PPLS_FIN_THREADS) void ppls_finalize_kernel(
     tm.status = status;
     tm.tr = tr;
     if (qr || !ppls_block_polar_fast<R, NT>(S, ld, rows, out, ld, ld, stage_lds ? dyn_lds : nullptr, sh,
-                                            sm, gout, vs, tr, tm)) {
+                                            sm, gout, vs, tr, tm, (mode & 4) != 0)) {
       if (tm.rank != 0) return;   // the Householder fallback runs on one block
       ppls_block_polar(S, ld, rows, R, out, ld, ld, w2, w2 + (int64_t)rows * R, status, qr);
       if (gout) {

@@ -67,3 +67,40 @@ def test_orth_ill_conditioned(ctx, kappa, p, q, r, typ):
         else:              # QR: W'S upper triangular, first column along S[:, 0] (functions.R:257-259)
             assert np.abs(np.tril(H, -1)).max() < 1e-12 * np.abs(S).max()
             assert H[0, 0] > 0
+
+
+@pytest.mark.parametrize("kappa", [1.0001, 3.0, 7.5, 9.0, 50.0])
+@pytest.mark.parametrize("p,q,r", [(400, 300, 5), (5000, 120, 10), (2500, 64, 3)])
+def test_orth_cholqr1_fast_path(ctx, kappa, p, q, r):
+    """The finalize's Cholesky-QR1 fast path (option polar1, taken when kappa(S) <= 8; wide p runs it
+    as a team) against numpy's SVD polar and against the Cholesky-QR2 path (polar1 = 0)."""
+    from ppls_amd import Expect
+    rng = np.random.default_rng(int(kappa * 10) + p + r)
+    n = max(p, q) + 3
+    X = np.zeros((n, p))
+    X[:p, :p] = np.eye(p)
+    Y = np.zeros((n, q))
+    Y[:q, :q] = np.eye(q)
+    SX = _with_condition(rng, p, r, kappa)
+    SY = _with_condition(rng, q, r, kappa)
+    ctx.set_data(X, Y)
+    fit = Expect(r, n, want_mu=True)
+    fit.mu_T[:p] = SX
+    fit.mu_U[:q] = SY
+    fit.Ctt[:] = 1.0 + np.arange(r)
+    fit.Cuu[:] = 1.0
+    fit.Cut[:] = 0.5
+    fit.Chh[:] = np.eye(r) * 0.1
+    fit.Cee, fit.Cff = 0.3, 0.2
+    out = {}
+    try:
+        for fast in (1, 0):
+            ctx.set_option("polar1", fast)
+            out[fast] = ctx.mstep(fit, 0)
+    finally:
+        ctx.set_option("polar1", 1)
+    for a, b, S in ((out[1].W, out[0].W, SX), (out[1].C, out[0].C, SY)):
+        assert np.abs(a.T @ a - np.eye(r)).max() < 1e-13
+        ref = o.orth(S, "SVD")
+        assert np.abs(a - ref).max() < 1e-13
+        assert np.abs(a - b).max() < 1e-13

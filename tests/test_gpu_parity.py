@@ -284,3 +284,26 @@ def test_device_stop_rule_matches_oracle(ctx, n, p, q, r, steps, atol):
     est2, ll2, _, _ = ctx.em_run(_theta(th0), 3, -np.inf, 0)
     ref3 = o.ppls_simult(X, Y, r, EMsteps=3, atol=-np.inf, theta0=th0)
     assert len(ll2) == 3 and _relerr(ll2, ref3["loglik"]) < 1e-10
+
+
+@pytest.mark.parametrize("n,p,q,r", [(500, 60, 40, 3), (400, 3000, 200, 5), (300, 2100, 90, 10)])
+def test_polar1_fast_path_em_agrees(ctx, n, p, q, r):
+    """EM with the finalize's Cholesky-QR1 fast path (default) equals EM with Cholesky-QR2 only
+    (polar1 = 0) and the oracle; wide p exercises polar teams."""
+    X, Y, th0 = make_problem(n, p, q, r, seed=7 * n + r)
+    ctx.set_data(X, Y)
+    res = {}
+    try:
+        for fast in (1, 0):
+            ctx.set_option("polar1", fast)
+            res[fast] = ctx.em_run(_theta(th0), 12, -np.inf, 0)
+    finally:
+        ctx.set_option("polar1", 1)
+    ref = o.ppls_simult(X, Y, r, EMsteps=12, atol=-np.inf, theta0=th0)
+    for fast in (1, 0):
+        est, ll = res[fast][0], res[fast][1]
+        assert _relerr(ll, ref["loglik"]) < 1e-10
+        assert np.abs(est.W - ref["estimates"]["W"]).max() < 1e-8
+    a, b = res[1][0], res[0][0]
+    assert _relerr(res[1][1], res[0][1]) < 1e-13
+    assert np.abs(a.W - b.W).max() < 1e-11 and np.abs(a.C - b.C).max() < 1e-11
