@@ -15,6 +15,7 @@
 #include <mutex>
 #include <set>
 #include <tuple>
+#include <type_traits>
 
 #include "ppls_kernels.h"
 #include "ppls_math.h"
@@ -363,6 +364,17 @@ __global__ __launch_bounds__(NT, 2 * NT / 512) void ppls_sweep_split_kernel(
   // no wait here: the W / C loads (issued first) complete before the ring prologue's first group,
   // which the prologue waits for, so their latency overlaps the first rows' DMA
   const uint32_t lds_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)smem;
+  // chunk j of this wave: matrix (wave-uniform) and the lane's clamped byte offset in the row, fixed
+  // for the sweep, so a row's copies need only its scalar base address (saddr-form DMA)
+  uint32_t coff[CPW];
+  bool cinx[CPW];
+#pragma unroll
+  for (int j = 0; j < CPW; ++j) {
+    const int ch = min(wave * CPW + j, nch - 1);
+    cinx[j] = ch < nchx;
+    coff[j] = cinx[j] ? (uint32_t)min(ch * 1024 + lane * 16, ldx * 8 - 16)
+                      : (uint32_t)min((ch - nchx) * 1024 + lane * 16, ldy * 8 - 16);
+  }
   auto issue_row = [&](int i) {
     if ((ablate & 2) || !dma_wave) return;
     const int64_t row = rb + i;
@@ -372,25 +384,28 @@ __global__ __launch_bounds__(NT, 2 * NT / 512) void ppls_sweep_split_kernel(
 #pragma unroll
     for (int j = 0; j < CPW; ++j) {
       const int ch = min(wave * CPW + j, nch - 1);
-      const char* src;
-      if (ch < nchx) src = xr + min(ch * 1024 + lane * 16, ldx * 8 - 16);
-      else src = yr + min((ch - nchx) * 1024 + lane * 16, ldy * 8 - 16);
-      if (ablate & 16) ppls_dma16_nt(src, sb + (uint32_t)(ch * 1024));
-      else ppls_dma16(src, sb + (uint32_t)(ch * 1024));
+      const char* base = cinx[j] ? xr : yr;
+      if (ablate & 16) ppls_dma16s_nt(base, coff[j], sb + (uint32_t)(ch * 1024));
+      else ppls_dma16s(base, coff[j], sb + (uint32_t)(ch * 1024));
     }
   };
   auto issue_group = [&](int grp) {
     for (int j = 0; j < RP; ++j)
       if (grp * RP + j < nrows) issue_row(grp * RP + j);
   };
-  auto load_x = [&](int grp, double2 (&xv)[RP][NSH]) {
+  // FULL: this thread's NSH column pairs all lie inside the matrix's 1-KiB-aligned part of a slot,
+  // which the DMA fills completely (lanes past the row's end copy its last 16 B), so the reads need
+  // no guard: a pair past the row reads finite data and meets zero weights (w = 0 there)
+  auto load_x = [&](int grp, double2 (&xv)[RP][NSH], auto full) {
 #pragma unroll
     for (int j = 0; j < RP; ++j) {
       const int row = min(grp * RP + j, nrows - 1);
       const char* sb = smem + (size_t)(row % SLOTS) * slot_bytes + xoff;
 #pragma unroll
-      for (int s = 0; s < NSH; ++s)
-        xv[j][s] = vs[s] ? *(const double2*)(sb + (th + s * HT) * 16) : make_double2(0.0, 0.0);
+      for (int s = 0; s < NSH; ++s) {
+        if constexpr (decltype(full)::value) xv[j][s] = *(const double2*)(sb + (th + s * HT) * 16);
+        else xv[j][s] = vs[s] ? *(const double2*)(sb + (th + s * HT) * 16) : make_double2(0.0, 0.0);
+      }
     }
   };
   // partial dots of group grp (x already loaded) -> reduce-scatter -> red[grp & 1]
@@ -460,51 +475,55 @@ __global__ __launch_bounds__(NT, 2 * NT / 512) void ppls_sweep_split_kernel(
     }
   };
 
-  if (ngroups > 0) {
-    const int npro = min(SLOTS, nrows);
-    for (int i = 0; i < npro; ++i) issue_row(i);
-    if (write_mu) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    else ppls_wait_vmcnt((npro - min(RP, nrows)) * CPW);
-    ppls_lds_barrier();
-    if (tr) tr[1] = (long long)wall_clock64();
-    double2 xc[RP][NSH] = {};
-    load_x(0, xc);
-    if (!(ablate & 1)) dots(0, xc);
-    for (int gg = 0; gg < ngroups; ++gg) {
-      if (write_mu) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      } else if ((gg + 2 + AHEAD) * RP <= nrows && gg >= 1) {
-        if constexpr (AHEAD * RP * CPW == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        else ppls_wait_vmcnt(AHEAD * RP * CPW);
-      } else {
-        const int last_issued = min(gg >= 1 ? (gg - 1) * RP + SLOTS + RP - 1 : SLOTS - 1, nrows - 1);
-        ppls_wait_vmcnt(max(0, last_issued - ((gg + 2) * RP - 1)) * CPW);
-      }
-      ppls_lds_barrier();   // red[gg&1] complete, group gg+1 landed, slots of group gg free
-      if (gg * RP + SLOTS < nrows) issue_group(gg + SLOTS / RP);
-      if (ablate & 1) continue;
-      double mta = 0.0, mua = 0.0;
-      zsum(gg, mta, mua);
-      if constexpr (PIPE) {
-        double2 xn[RP][NSH] = {};
-        if (gg + 1 < ngroups) {
-          load_x(gg + 1, xn);
-          dots(gg + 1, xn);
+  auto run = [&](auto full) {
+    if (ngroups > 0) {
+      const int npro = min(SLOTS, nrows);
+      for (int i = 0; i < npro; ++i) issue_row(i);
+      if (write_mu) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      else ppls_wait_vmcnt((npro - min(RP, nrows)) * CPW);
+      ppls_lds_barrier();
+      if (tr) tr[1] = (long long)wall_clock64();
+      double2 xc[RP][NSH] = {};
+      load_x(0, xc, full);
+      if (!(ablate & 1)) dots(0, xc);
+      for (int gg = 0; gg < ngroups; ++gg) {
+        if (write_mu) {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        } else if ((gg + 2 + AHEAD) * RP <= nrows && gg >= 1) {
+          if constexpr (AHEAD * RP * CPW == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          else ppls_wait_vmcnt(AHEAD * RP * CPW);
+        } else {
+          const int last_issued = min(gg >= 1 ? (gg - 1) * RP + SLOTS + RP - 1 : SLOTS - 1, nrows - 1);
+          ppls_wait_vmcnt(max(0, last_issued - ((gg + 2) * RP - 1)) * CPW);
         }
-        update(gg, mta, mua, xc);
-#pragma unroll
-        for (int j = 0; j < RP; ++j)
-#pragma unroll
-          for (int s = 0; s < NSH; ++s) xc[j][s] = xn[j][s];
-      } else {
-        update(gg, mta, mua, xc);
-        if (gg + 1 < ngroups) {
-          load_x(gg + 1, xc);
-          dots(gg + 1, xc);
+        ppls_lds_barrier();   // red[gg&1] complete, group gg+1 landed, slots of group gg free
+        if (gg * RP + SLOTS < nrows) issue_group(gg + SLOTS / RP);
+        if (ablate & 1) continue;
+        double mta = 0.0, mua = 0.0;
+        zsum(gg, mta, mua);
+        if constexpr (PIPE) {
+          double2 xn[RP][NSH] = {};
+          if (gg + 1 < ngroups) {
+            load_x(gg + 1, xn, full);
+            dots(gg + 1, xn);
+          }
+          update(gg, mta, mua, xc);
+  #pragma unroll
+          for (int j = 0; j < RP; ++j)
+  #pragma unroll
+            for (int s = 0; s < NSH; ++s) xc[j][s] = xn[j][s];
+        } else {
+          update(gg, mta, mua, xc);
+          if (gg + 1 < ngroups) {
+            load_x(gg + 1, xc, full);
+            dots(gg + 1, xc);
+          }
         }
       }
     }
-  }
+  };
+  if (NSH * HT * 16 <= nchx * 1024 && NSH * HT * 16 <= nchy * 1024) run(std::true_type{});
+  else run(std::false_type{});
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (tr) tr[2] = (long long)wall_clock64();
   double* pg = part + g * part_ld;
