@@ -69,8 +69,9 @@ struct PplsFinalizeArgs {
 
 #define PPLS_TEAM_ROWS 1024   // rows of S per polar team member
 #define PPLS_TEAM_MAX 32
-// finalize polar: Cholesky-QR1 (one pass, no second team barrier) when kappa(X'mu) <= this
-#define PPLS_POLAR1_KAPPA 8.0
+// finalize polar: Cholesky-QR1 (one pass, no second team barrier) when ||R1||_F ||R1^-1||_F <= this x r
+// (a bound on kappa_2(X'mu); ||R||_F ||R^-1||_F >= r for any R)
+#define PPLS_POLAR1_KAPPA 2.0
 
 // One EM step of the sequential initialiser's rank-1 fit on the device (ppls_rank1_step_kernel).
 struct PplsRank1StepArgs {

@@ -1573,14 +1573,27 @@ __device__ bool ppls_block_polar_fast(const double* __restrict__ S, int64_t lds,
       }
     }
   };
-  // Cholesky-QR1 fast path (polar1): T = R1 = U_T Sigma V' by the Jacobi; when kappa(S) = kappa(R1)
-  // <= PPLS_POLAR1_KAPPA, Q1 = S R1^-1 is already orthonormal to O(eps kappa^2) (~1e-14), so pass 2,
-  // its team barrier and chol(G2) are skipped: out = S F, F = R1^-1 U_T V'.  Every member decides
-  // on the bitwise-identical G1, so a team takes one path.
+  // Cholesky-QR1 fast path (polar1): when kappa(S) = kappa(R1) is small, Q1 = S R1^-1 is already
+  // orthonormal to O(eps kappa^2) (~1e-14), so pass 2, its team barrier and chol(G2) are skipped:
+  // T = R1 = U_T Sigma V' by the Jacobi, out = S F, F = R1^-1 U_T V'.  The test is the bound
+  // kappa_2(R1) <= ||R1||_F ||R1^-1||_F <= PPLS_POLAR1_KAPPA * R (no Jacobi is spent on a matrix
+  // that then takes the Cholesky-QR2 path).  Every member decides on the bitwise-identical G1, so
+  // a team takes one path.
   __shared__ int fast;
   if (tid < 64) {
     bool fst = false;
     if (polar1) {
+      double fr = 0.0, fi = 0.0;
+      for (int e = lane; e < R * R; e += 64) {
+        const double t = sT[(e / R) * G + e % R], u = sF[e];
+        fr = fma(t, t, fr);
+        fi = fma(u, u, fi);
+      }
+      fr = ppls_wave_sum(fr);
+      fi = ppls_wave_sum(fi);
+      fst = __shfl(fr * fi <= (PPLS_POLAR1_KAPPA * R) * (PPLS_POLAR1_KAPPA * R) ? 1 : 0, 0, 64) != 0;
+    }
+    if (fst) {
       load_vprev();
       ppls_matmul_wave<R, false>(sT, sV, sA);                // sA = R1 V (sT keeps R1)
       ppls_jacobi_wave<R>(sA, sV);
@@ -1591,11 +1604,7 @@ __device__ bool ppls_block_polar_fast(const double* __restrict__ S, int64_t lds,
         ssv[lane] = sqrt(nrm);
       }
       ppls_wave_lds_fence();
-      double smax = 0.0, smin = ssv[0];
-#pragma unroll
-      for (int i = 0; i < R; ++i) { smax = fmax(smax, ssv[i]); smin = fmin(smin, ssv[i]); }
-      fst = smin > 0.0 && smin * PPLS_POLAR1_KAPPA >= smax;
-      if (fst) {
+      {
         for (int e = lane; e < GG; e += 64) {                  // sU = U_T V'
           const int a = e % G, b = e / G;
           double s = 0.0;

@@ -72,7 +72,7 @@ def test_orth_ill_conditioned(ctx, kappa, p, q, r, typ):
 @pytest.mark.parametrize("kappa", [1.0001, 3.0, 7.5, 9.0, 50.0])
 @pytest.mark.parametrize("p,q,r", [(400, 300, 5), (5000, 120, 10), (2500, 64, 3)])
 def test_orth_cholqr1_fast_path(ctx, kappa, p, q, r):
-    """The finalize's Cholesky-QR1 fast path (option polar1, taken when kappa(S) <= 8; wide p runs it
+    """The finalize's Cholesky-QR1 fast path (option polar1, taken when ||R1||_F ||R1^-1||_F <= 2r; wide p runs it
     as a team) against numpy's SVD polar and against the Cholesky-QR2 path (polar1 = 0)."""
     from ppls_amd import Expect
     rng = np.random.default_rng(int(kappa * 10) + p + r)

@@ -20,6 +20,7 @@ def main():
         truth, th0 = make_truth_and_theta0(p, q, r)
         ctx.generate_synthetic(min(n, 200_000), p, q, truth, seed=20261015)
         ctx.set_option("ftrace", 1)
+        ctx.set_option("polar1", int(os.environ.get("POLAR1", "1")))
         ctx.em_begin(th0)
         for it in range(4):
             ctx.em_iterate(1)
@@ -28,7 +29,7 @@ def main():
             if raw[1] and raw[2]:
                 us = tr[0][5]
                 print(f"  block 0: jacobi sweeps {raw[0]}, core clock {(raw[2] - raw[1]) / (us * 1e3):.2f} GHz")
-            print(f"{cfgname} iter {it}: " + "; ".join(
+            print(f"{cfgname} polar1={os.environ.get('POLAR1', '1')} iter {it}: " + "; ".join(
                 f"block {b}: " + " ".join(f"{s}={v}" for s, v in enumerate(ts) if v is not None and s not in (10, 11, 12))
                 for b, ts in tr.items()), flush=True)
         ctx.set_option("ftrace", 0)
