@@ -34,6 +34,7 @@ struct ppls_ctx {
   int rp_opt = 0;   // rows per pipeline step: 0 auto (2 where the kernel fits in registers)
   int pipe_opt = 1;     // split kernel: software-pipelined order
   int ablate = 0;
+  int team_rows = 0;   // finalize polar team: rows of S per member (0: PPLS_TEAM_ROWS)
   int polar1 = 1;   // finalize polar: Cholesky-QR1 fast path when kappa(X'mu) <= PPLS_POLAR1_KAPPA
   int ldpad = 1;   // row padding of the panel sweep's rows (ld_of); 0 = 16-B rows (experiment)
   int dtype = 0;           // storage of X, Y: 0 fp64, 1 fp32 (arithmetic is fp64 either way)
@@ -459,6 +460,7 @@ int finalize(ppls_ctx* c, int r, int cur, int nxt, int logl_index, int type, int
     HIPCHK(c, hipMemsetAsync(c->team_bar, 0, 8 * sizeof(unsigned), c->stream));
   }
   f.team_bar = c->team_bar;
+  f.team_rows = c->team_rows;
   f.team_part = c->team_part;
   f.stop = c->sweep_stop ? c->stop_d : nullptr;
   f.stop_mirror = c->sweep_stop ? c->stop_mirror_dev : nullptr;
@@ -690,6 +692,9 @@ int ppls_set_option(ppls_ctx* c, const char* key, int64_t value) {
   } else if (!strcmp(key, "rows_per_step")) {
     if (value < 0 || value > 2) return fail(c, PPLS_E_ARG, "rows_per_step must be 0 (auto), 1 or 2");
     c->rp_opt = (int)value;
+  } else if (!strcmp(key, "team_rows")) {
+    if (value < 0 || value > (1 << 30)) return fail(c, PPLS_E_ARG, "team_rows must be >= 0");
+    c->team_rows = (int)value;
   } else if (!strcmp(key, "polar1")) {
     c->polar1 = value ? 1 : 0;
   } else if (!strcmp(key, "pipe")) {

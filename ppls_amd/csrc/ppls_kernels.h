@@ -65,9 +65,10 @@ struct PplsFinalizeArgs {
   double atol;
   unsigned* team_bar;    // wide-p polar teams: 8 zero-initialised counters, or nullptr (one block each)
   double* team_part;     // 2 x 3 x PPLS_TEAM_MAX x 64 doubles
+  int team_rows;         // rows of S per team member (0: PPLS_TEAM_ROWS)
 };
 
-#define PPLS_TEAM_ROWS 1024   // rows of S per polar team member
+#define PPLS_TEAM_ROWS 2048   // rows of S per polar team member (tools/team_rows_ab.py: p = 2000 in one block is 4 us faster than a team of 2; C5 equal at 1024 and 2048)
 #define PPLS_TEAM_MAX 32
 // finalize polar: Cholesky-QR1 (one pass, no second team barrier) when ||R1||_F ||R1^-1||_F <= this x r
 // (a bound on kappa_2(X'mu); ||R||_F ||R^-1||_F >= r for any R)

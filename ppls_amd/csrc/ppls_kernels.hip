@@ -2270,7 +2270,8 @@ hipError_t launch_finalize_t(const PplsFinalizeArgs* f, hipStream_t st) {
   // teams for wide p: one member per PPLS_TEAM_ROWS rows (QR: one block, Householder)
   auto team = [&](int rows) {
     if (f->qr || !f->team_bar) return 1;
-    const int k = (rows + PPLS_TEAM_ROWS - 1) / PPLS_TEAM_ROWS;
+    const int tr = f->team_rows > 0 ? f->team_rows : PPLS_TEAM_ROWS;
+    const int k = (rows + tr - 1) / tr;
     return k < 1 ? 1 : k > PPLS_TEAM_MAX ? PPLS_TEAM_MAX : k;
   };
   const int KX = team(f->p), KY = team(f->q);

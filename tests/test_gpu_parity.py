@@ -307,3 +307,24 @@ def test_polar1_fast_path_em_agrees(ctx, n, p, q, r):
     a, b = res[1][0], res[0][0]
     assert _relerr(res[1][1], res[0][1]) < 1e-13
     assert np.abs(a.W - b.W).max() < 1e-11 and np.abs(a.C - b.C).max() < 1e-11
+
+
+@pytest.mark.parametrize("team_rows", [256, 1000])
+def test_polar_team_sizes_agree(ctx, team_rows):
+    """The finalize's polar teams (option team_rows: rows of X'mu per member; default 2048) give
+    the single-block result: p = 3000 as 12 or 3 members vs one block, EM fits vs the oracle."""
+    n, p, q, r = 400, 3000, 2500, 4
+    X, Y, th0 = make_problem(n, p, q, r, seed=11 + team_rows)
+    ctx.set_data(X, Y)
+    res = {}
+    try:
+        for tr in (team_rows, 1 << 20):
+            ctx.set_option("team_rows", tr)
+            res[tr] = ctx.em_run(_theta(th0), 8, -np.inf, 0)
+    finally:
+        ctx.set_option("team_rows", 0)
+    ref = o.ppls_simult(X, Y, r, EMsteps=8, atol=-np.inf, theta0=th0)
+    a, b = res[team_rows], res[1 << 20]
+    assert _relerr(a[1], ref["loglik"]) < 1e-10 and np.abs(a[0].W - ref["estimates"]["W"]).max() < 1e-8
+    assert _relerr(a[1], b[1]) < 1e-13
+    assert np.abs(a[0].W - b[0].W).max() < 1e-11 and np.abs(a[0].C - b[0].C).max() < 1e-11
