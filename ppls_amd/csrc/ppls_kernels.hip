@@ -12,6 +12,7 @@
 #include <stdint.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <mutex>
 #include <set>
 #include <tuple>
@@ -262,22 +263,32 @@ __global__ void ppls_reduce_partials_kernel(const double* __restrict__ part, int
   out[j] = accumulate ? out[j] + t : t;
 }
 
-// Stage 1 of the two-stage reduction: tmp[chunk][j] = sum of groups [chunk*32, chunk*32+32).
-__global__ void ppls_reduce_chunks_kernel(const double* __restrict__ part, int ngroups, int64_t ld,
-                                          int64_t len, double* __restrict__ tmp,
-    const int* __restrict__ stop) {
+// One-launch fixed-order reduction: out[j] (+)= sum_g part[g*ld + j].  A 256-thread block owns 64
+// consecutive j (a wave reads 512 contiguous bytes per group) and splits the groups over 4 slices
+// (slice s: g = s, s+4, ...), each with 8 accumulators so 8 loads per thread are in flight; the
+// slices are added in slice order through LDS -> deterministic for a given ngroups.
+__global__ __launch_bounds__(256) void ppls_reduce_fused_kernel(const double* __restrict__ part, int ngroups,
+                                                                int64_t ld, int64_t len, double* __restrict__ out,
+                                                                int accumulate, const int* __restrict__ stop) {
   if (stop && *stop) return;   // em_run converged earlier (device stop flag)
-  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= len) return;
-  const int g0 = blockIdx.y * 32, g1 = min(ngroups, g0 + 32);
-  double s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  int g = g0;
-  for (; g + 8 <= g1; g += 8) {
+  __shared__ double sh[4][64];
+  const int c = threadIdx.x & 63, sl = threadIdx.x >> 6;
+  const int64_t j = (int64_t)blockIdx.x * 64 + c;
+  double a[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (j < len) {
+    int g = sl;
+    for (; g + 28 < ngroups; g += 32) {
 #pragma unroll
-    for (int u = 0; u < 8; ++u) s[u] += part[(int64_t)(g + u) * ld + j];
+      for (int u = 0; u < 8; ++u) a[u] += part[(int64_t)(g + 4 * u) * ld + j];
+    }
+    for (int u = 0; g < ngroups; g += 4, ++u) a[u] += part[(int64_t)g * ld + j];
   }
-  for (int u = 0; g < g1; ++g, ++u) s[u] += part[(int64_t)g * ld + j];
-  tmp[(int64_t)blockIdx.y * len + j] = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
+  sh[sl][c] = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+  __syncthreads();
+  if (sl == 0 && j < len) {
+    const double t = (sh[0][c] + sh[1][c]) + (sh[2][c] + sh[3][c]);
+    out[j] = accumulate ? out[j] + t : t;
+  }
 }
 
 #include "ppls_device.h"
@@ -2575,26 +2586,20 @@ int ppls_twopass_groups(int64_t n_local, int grid) {
   return (int)((n_local + rpc - 1) / rpc);
 }
 
-// Fixed-order two-stage reduction: stage 1 sums chunks of RCHUNK groups (many blocks busy), stage 2
-// sums the chunk results.  tmp: ceil(ngroups / RCHUNK) * len doubles (taken from the tail of part
-// when the caller passes tmp == nullptr is not allowed; see ppls_reduce_tmp_len).
-#define PPLS_RCHUNK 32
+// Scratch the statistics reduction needs behind the partials: none (one-launch fixed-order
+// reduction, ppls_reduce_fused_kernel; measured against the former two-stage form in
+// profiles/r2_reduce_fused_ab.txt).
 int64_t ppls_reduce_tmp_len(int ngroups, int64_t len) {
-  return ngroups > PPLS_RCHUNK ? (int64_t)((ngroups + PPLS_RCHUNK - 1) / PPLS_RCHUNK) * len : 0;
+  (void)ngroups;
+  (void)len;
+  return 0;
 }
 
 hipError_t ppls_launch_reduce2(const double* part, int ngroups, int64_t ld, int64_t len, double* out,
                                double* tmp, const int* stop, hipStream_t st) {
-  if (ngroups <= PPLS_RCHUNK || tmp == nullptr) {
-    hipLaunchKernelGGL(ppls_reduce_partials_kernel, dim3((unsigned)((len + 255) / 256)), dim3(256), 0,
-                       st, part, ngroups, ld, len, out, 0, stop);
-    return hipGetLastError();
-  }
-  const int nch = (ngroups + PPLS_RCHUNK - 1) / PPLS_RCHUNK;
-  hipLaunchKernelGGL(ppls_reduce_chunks_kernel, dim3((unsigned)((len + 255) / 256), nch), dim3(256), 0,
-                     st, part, ngroups, ld, len, tmp, stop);
-  hipLaunchKernelGGL(ppls_reduce_partials_kernel, dim3((unsigned)((len + 255) / 256)), dim3(256), 0,
-                     st, tmp, nch, len, len, out, 0, stop);
+  (void)tmp;   // one launch (ppls_reduce_fused_kernel); the two-stage form it replaced needed scratch
+  hipLaunchKernelGGL(ppls_reduce_fused_kernel, dim3((unsigned)((len + 63) / 64)), dim3(256), 0,
+                     st, part, ngroups, ld, len, out, 0, stop);
   return hipGetLastError();
 }
 
