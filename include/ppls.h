@@ -79,8 +79,9 @@ const char* ppls_last_error(const ppls_ctx* ctx);
  *                registers, else the panel sweep; 2 generic two-pass; 3 panel (wide p, two passes)),
  *       "rows_per_step" (split sweep: 0 auto, 1, 2), "pipe" (split sweep software pipelining, 0/1),
  *       "grid" (workgroups, 0 = auto),
- *       "polar1" (finalize polar factor: 1 (default) one Cholesky-QR pass when kappa(X'mu) <= 8,
- *                 else Cholesky-QR2; 0 always Cholesky-QR2),
+ *       "polar1" (finalize polar factor: 1 (default) one Cholesky-QR pass when
+ *                 ||R1||_F ||R1^-1||_F <= 2 r (R1 = chol(S'S)), else Cholesky-QR2; 0 always Cholesky-QR2),
+ *       "team_rows" (finalize polar factor: rows of S per workgroup of a team; 0 = default 2048),
  *       "dtype" (storage of X, Y: 0 fp64, 1 fp32; arithmetic stays fp64; set before loading data),
  *       "nt" (sweep loads with the non-temporal cache policy: -1 auto (default: when X, Y exceed
  *             the 256 MB MALL), 0 off, 1 on),
