@@ -386,7 +386,8 @@ __global__ __launch_bounds__(NT, 2 * NT / 512) void ppls_sweep_split_kernel(
     coff[j] = cinx[j] ? (uint32_t)min(ch * 1024 + lane * 16, ldx * 8 - 16)
                       : (uint32_t)min((ch - nchx) * 1024 + lane * 16, ldy * 8 - 16);
   }
-  auto issue_row = [&](int i) {
+  // nt: the non-temporal load policy (ablate bit 4), a compile-time choice per copy of the loop
+  auto issue_row = [&](int i, auto nt) {
     if ((ablate & 2) || !dma_wave) return;
     const int64_t row = rb + i;
     const char* xr = (const char*)(X + row * (int64_t)ldx);
@@ -396,13 +397,13 @@ __global__ __launch_bounds__(NT, 2 * NT / 512) void ppls_sweep_split_kernel(
     for (int j = 0; j < CPW; ++j) {
       const int ch = min(wave * CPW + j, nch - 1);
       const char* base = cinx[j] ? xr : yr;
-      if (ablate & 16) ppls_dma16s_nt(base, coff[j], sb + (uint32_t)(ch * 1024));
+      if constexpr (decltype(nt)::value) ppls_dma16s_nt(base, coff[j], sb + (uint32_t)(ch * 1024));
       else ppls_dma16s(base, coff[j], sb + (uint32_t)(ch * 1024));
     }
   };
-  auto issue_group = [&](int grp) {
+  auto issue_group = [&](int grp, auto nt) {
     for (int j = 0; j < RP; ++j)
-      if (grp * RP + j < nrows) issue_row(grp * RP + j);
+      if (grp * RP + j < nrows) issue_row(grp * RP + j, nt);
   };
   // FULL: this thread's NSH column pairs all lie inside the matrix's 1-KiB-aligned part of a slot,
   // which the DMA fills completely (lanes past the row's end copy its last 16 B), so the reads need
@@ -486,10 +487,10 @@ __global__ __launch_bounds__(NT, 2 * NT / 512) void ppls_sweep_split_kernel(
     }
   };
 
-  auto run = [&](auto full) {
+  auto run = [&](auto full, auto nt) {
     if (ngroups > 0) {
       const int npro = min(SLOTS, nrows);
-      for (int i = 0; i < npro; ++i) issue_row(i);
+      for (int i = 0; i < npro; ++i) issue_row(i, nt);
       if (write_mu) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       else ppls_wait_vmcnt((npro - min(RP, nrows)) * CPW);
       ppls_lds_barrier();
@@ -508,7 +509,7 @@ __global__ __launch_bounds__(NT, 2 * NT / 512) void ppls_sweep_split_kernel(
           ppls_wait_vmcnt(max(0, last_issued - ((gg + 2) * RP - 1)) * CPW);
         }
         ppls_lds_barrier();   // red[gg&1] complete, group gg+1 landed, slots of group gg free
-        if (gg * RP + SLOTS < nrows) issue_group(gg + SLOTS / RP);
+        if (gg * RP + SLOTS < nrows) issue_group(gg + SLOTS / RP, nt);
         if (ablate & 1) continue;
         double mta = 0.0, mua = 0.0;
         zsum(gg, mta, mua);
@@ -533,8 +534,14 @@ __global__ __launch_bounds__(NT, 2 * NT / 512) void ppls_sweep_split_kernel(
       }
     }
   };
-  if (NSH * HT * 16 <= nchx * 1024 && NSH * HT * 16 <= nchy * 1024) run(std::true_type{});
-  else run(std::false_type{});
+  const bool full = NSH * HT * 16 <= nchx * 1024 && NSH * HT * 16 <= nchy * 1024;
+  if (ablate & 16) {
+    if (full) run(std::true_type{}, std::true_type{});
+    else run(std::false_type{}, std::true_type{});
+  } else {
+    if (full) run(std::true_type{}, std::false_type{});
+    else run(std::false_type{}, std::false_type{});
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (tr) tr[2] = (long long)wall_clock64();
   double* pg = part + g * part_ld;
