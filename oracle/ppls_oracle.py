@@ -17,7 +17,9 @@ Every function cites the reference line it restates (paths relative to /root/ref
 * ``emstep_w``           Package/PPLS/R/EM_W_multi.R:51-73
 * ``pplsi``              Package/PPLS/R/EM_W_multi.R:116-180 (one direction; fconstraint :85-92)
 * ``ppls``               Package/PPLS/R/EM_W_multi.R:229-279 (sequential fit with deflation)
-* ``initial_guess``      Package/PPLS/R/EM_W_multi.R:126-140 ('equal'; 'random' with numpy draws)
+* ``initial_guess``      Package/PPLS/R/EM_W_multi.R:126-140 ('equal'; 'random' from an R stream,
+                         oracle/r_rng.py, or numpy draws)
+* ``print_ppls``         Package/PPLS/R/EM_W_multi.R:336-354 (print.PPLS's variance table)
 * ``scores_ppls``        Package/PPLS/R/EM_W_multi.R:411-420
 * ``ppls_simult_to_o2m`` Package/PPLS/R/PPLS_to_o2m.R:82-140
 * ``ppls_to_o2m``        Package/PPLS/R/PPLS_to_o2m.R:28-80 (literal, with the n x p products)
@@ -30,10 +32,15 @@ Every function cites the reference line it restates (paths relative to /root/ref
 * ``ssq``                OmicsPLS::ssq (not vendored); semantics Package/functions.R:380-385
 
 Parity pinning: R/Rcpp/Eigen are absent from this image, so the reference cannot run here.
-The restatement is pinned by the reference's own known-answer identity checks
-(Package/rank_one_inverse.R:45-59, Package/Benchmark.R:36-45) and by its own independent
-dense formulation (Expect_M(debug=TRUE)); see tests/test_oracle.py.  ``orth`` (OmicsPLS,
-unpinned version) is unpinned by any reference test.
+The restatement is pinned by the outputs the reference itself printed: the four example fits
+of its R CMD check run (Package/PPLS.Rcheck/PPLS-Ex.R:39-53 -> PPLS-Ex_x64.Rout:54-83), whose
+inputs and 'random' starting values are regenerated with R's default RNG (oracle/r_rng.py),
+reproduce every printed step count, variance ratio and log LR (tests/test_reference_examples.py).
+Also by the reference's known-answer identity checks (Package/rank_one_inverse.R:45-59,
+Package/Benchmark.R:36-45) and its independent dense formulation (Expect_M(debug=TRUE)); see
+tests/test_oracle.py.  ``orth`` comes from the un-vendored OmicsPLS/O2PLS; for the rank-1 fits
+above any sign convention gives the same (mirrored) fit, so the wide-r ``orth`` stays
+unpinned by a reference vector.
 
 Conventions: R matrices are column-major; here X, Y are numpy arrays (n x p, n x q) and the
 diagonal parameter matrices B, sigT are carried as r x r diagonal matrices exactly as in R.
@@ -423,19 +430,25 @@ def emstep_w(X, Y, W, C, B_T, sigX, sigY, sigH, sigT):
 
 
 def initial_guess(p, q, kind="equal", rng=None):
-    """PPLSi starting values -- EM_W_multi.R:126-140.  'equal' is deterministic; 'random' uses the
-    reference's distributions (orth(runif), rchisq(1,1), rchisq(2,100)/100, rchisq(2,10)/100) drawn
-    from numpy, since R's RNG stream is not reproducible here."""
+    """PPLSi starting values -- EM_W_multi.R:126-140.  'equal' is deterministic; 'random' draws
+    orth(runif(p)), orth(runif(q)), rchisq(1,1), rchisq(2,100)/100, rchisq(2,10)/100 in that order
+    (:133) from ``rng``: an R stream (oracle/r_rng.RRNG: R's own values) or a numpy Generator."""
     if kind == "equal":
         return dict(W=np.ones(p) / math.sqrt(p), C=np.ones(q) / math.sqrt(q), B=1.0,
                     sigE=1.0 / p, sigF=1.0 / q, sigH=1.0, sigT=1.0)
     if kind == "random":
         rng = rng if rng is not None else np.random.default_rng()
-        W = rng.uniform(size=p)
-        C = rng.uniform(size=q)
-        B = rng.chisquare(1)
-        siglat = rng.chisquare(100, size=2) / 100
-        sig = rng.chisquare(10, size=2) / 100
+        if hasattr(rng, "runif"):                       # R's stream (oracle/r_rng.RRNG), :133 order
+            W, C = rng.runif(p), rng.runif(q)
+            B = rng.rchisq(1, 1)[0]
+            siglat = rng.rchisq(2, 100) / 100
+            sig = rng.rchisq(2, 10) / 100
+        else:
+            W = rng.uniform(size=p)
+            C = rng.uniform(size=q)
+            B = rng.chisquare(1)
+            siglat = rng.chisquare(100, size=2) / 100
+            sig = rng.chisquare(10, size=2) / 100
         return dict(W=W / np.linalg.norm(W), C=C / np.linalg.norm(C), B=float(B), sigE=float(sig[0]),
                     sigF=float(sig[1]), sigH=float(siglat[0]), sigT=float(siglat[1]))
     raise ValueError(kind)
@@ -523,6 +536,27 @@ def ppls(X, Y, nr_comp=1, EMsteps=100, atol=1e-4, theta0s=None, constraints=None
                                               sig[i, 0], sig[i, 1], sig[i, 2], np.diag(sig[:i + 1, 3])))  # :274
         done = i + 1
     return dict(W=Wn[:, :done], C=Cn[:, :done], B=Bn[:done], sig=sig[:done], Other_output=other)
+
+
+def print_ppls(fit, perc=True, digits=3):
+    """print.PPLS -- Package/PPLS/R/EM_W_multi.R:336-354: rows (LV, ssq(T)/ssq(X), ssq(U)/ssq(Y),
+    sigH^2/ssq(U), log LR, #steps, last incr), rounded.  Note `sum(sig[1:i,4]^2*B[1:i]^2 +
+    sig[i,3]^2)` adds sigH^2 once per component; `signif(last, 3)` before rounding."""
+    p, q = fit["W"].shape[0], fit["C"].shape[0]
+    sig, B, oo = np.asarray(fit["sig"]), np.asarray(fit["B"]), fit["Other_output"]
+    dll = np.concatenate([[0.0], np.diff(np.asarray(oo["Loglikelihoods"], dtype=np.float64))])
+    pc = 1.0 if perc else 0.0
+    rows = []
+    for i in range(sig.shape[0]):
+        st = np.sum(sig[:i + 1, 3] ** 2)
+        su = np.sum(sig[:i + 1, 3] ** 2 * B[:i + 1] ** 2 + sig[i, 2] ** 2)
+        last = float(oo["Last_increment"][i])
+        if last != 0:
+            last = round(last, 2 - int(math.floor(math.log10(abs(last)))))
+        rows.append([i + 1, st / (pc * (st + p * sig[i, 0] ** 2) + (1 - pc)),
+                     su / (pc * (su + q * sig[i, 1] ** 2) + (1 - pc)), sig[i, 2] ** 2 / (pc * su + (1 - pc)),
+                     dll[i], oo["Number_steps"][i], last])
+    return np.round(np.array(rows, dtype=np.float64), digits)
 
 
 def simult_theta0_from_ppls(f0):

@@ -520,11 +520,10 @@ def loglC_fast(W, C, X, Y, sigX, sigY, sig2T, c1, c2, c3, Kc, ctx=None):
 
 
 def random_theta0(p, q, a, seed=0):
-    """Deterministic theta0: W0 = orth(N(0,1)), C0 = orth(N(0,1)), B0 = I, sigT0 = I, sigmas = 1.
-
-    The reference draws theta0 from a sequential PPLS(X, Y, a, 20, 1e-4, 'random') fit with R's
-    RNG (EM_W_multi.R:762-771); that initialiser is the next tier of this build.
-    """
+    """Deterministic synthetic theta0: W0 = orth(N(0,1)), C0 = orth(N(0,1)), B0 = I, sigT0 = I,
+    sigmas = 1 (the benchmark's starting point).  PPLS_simult's own default theta0 is
+    the sequential fit PPLS(X, Y, a, 20, 1e-4, 'random') (EM_W_multi.R:762-771), which
+    ``PPLS_simult`` below runs on the device."""
     rng = np.random.default_rng(seed)
 
     def polar(M):
@@ -536,20 +535,32 @@ def random_theta0(p, q, a, seed=0):
 
 
 def initial_guess(p, q, kind="equal", rng=None):
-    """PPLSi's starting values (EM_W_multi.R:126-140): 'equal' (deterministic) or 'random' with the
-    reference's distributions -- orth(runif(p)), orth(runif(q)), rchisq(1,1), rchisq(2,100)/100
-    (sigH, sigT), rchisq(2,10)/100 (sigE, sigF) -- drawn from numpy (R's RNG stream cannot be
-    reproduced; pass customGuess for exact starting values).  'o2m' needs OmicsPLS: not provided."""
+    """PPLSi's starting values (EM_W_multi.R:126-140): 'equal' (deterministic) or 'random' --
+    orth(runif(p)), orth(runif(q)), rchisq(1,1), rchisq(2,100)/100 (sigH, sigT), rchisq(2,10)/100
+    (sigE, sigF), drawn in that order (:133).
+
+    ``rng``: an R-compatible stream (any object with R's ``runif(n)`` and ``rchisq(n, df)``, e.g. a
+    restatement of R's Mersenne-Twister/Inversion defaults) reproduces R's draws after the same
+    ``set.seed``; a numpy ``Generator`` draws from the same distributions.  ``orth`` of a positive
+    vector is taken as v/||v|| (the QR form's -v/||v|| gives the mirrored, equivalent fit).
+    'o2m' needs OmicsPLS: not provided."""
     if kind == "equal":
         return dict(W=np.ones(p) / np.sqrt(p), C=np.ones(q) / np.sqrt(q), B=1.0, sigE=1.0 / p,
                     sigF=1.0 / q, sigH=1.0, sigT=1.0)
     if kind == "random":
         rng = rng if rng is not None else np.random.default_rng()
-        W = rng.uniform(size=p)
-        C = rng.uniform(size=q)
-        B = rng.chisquare(1)
-        siglat = rng.chisquare(100, size=2) / 100
-        sig = rng.chisquare(10, size=2) / 100
+        if hasattr(rng, "runif") and hasattr(rng, "rchisq"):      # R's own stream
+            W = np.asarray(rng.runif(p), dtype=np.float64)
+            C = np.asarray(rng.runif(q), dtype=np.float64)
+            B = float(np.ravel(rng.rchisq(1, 1))[0])
+            siglat = np.asarray(rng.rchisq(2, 100), dtype=np.float64) / 100
+            sig = np.asarray(rng.rchisq(2, 10), dtype=np.float64) / 100
+        else:
+            W = rng.uniform(size=p)
+            C = rng.uniform(size=q)
+            B = rng.chisquare(1)
+            siglat = rng.chisquare(100, size=2) / 100
+            sig = rng.chisquare(10, size=2) / 100
         return dict(W=W / np.linalg.norm(W), C=C / np.linalg.norm(C), B=float(B), sigE=float(sig[0]),
                     sigF=float(sig[1]), sigH=float(siglat[0]), sigT=float(siglat[1]))
     if kind == "o2m":
@@ -616,6 +627,38 @@ def PPLSi(X, Y, EMsteps=100, atol=1e-4, initialGuess=("equal", "o2m", "random", 
     return dict(W=fit["W"][:, 0], C=fit["C"][:, 0], B=fit["B"][0], sig=fit["sig"][0],
                 logvalue=oo["logvalue"][0], Last_increment=oo["Last_increment"][0],
                 Number_steps=int(oo["Number_steps"][0]))
+
+
+def _signif(x, digits):
+    if x == 0 or not np.isfinite(x):
+        return x
+    return round(x, digits - 1 - int(np.floor(np.log10(abs(x)))))
+
+
+def print_PPLS(x, perc=True, digits=3):
+    """print.PPLS (EM_W_multi.R:336-354): the per-component variance table of a PPLS fit.
+    Returns (rows, text): rows = n x 7 array (LV, ssq(T)/ssq(X), ssq(U)/ssq(Y), sigH^2/ssq(U),
+    log LR, #steps, last incr) rounded to ``digits``; ``perc=False`` gives the absolute variances.
+    As in R, sigH^2 is added once per component inside the ssq(U) sum."""
+    p, q = x["W"].shape[0], x["C"].shape[0]
+    sig, B, oo = np.asarray(x["sig"]), np.asarray(x["B"]), x["Other_output"]
+    ll = np.asarray(oo["Loglikelihoods"], dtype=np.float64)
+    dll = np.concatenate([[0.0], np.diff(ll)])
+    pc = 1.0 if perc else 0.0
+    rows = []
+    for i in range(sig.shape[0]):
+        st = float(np.sum(sig[: i + 1, 3] ** 2))
+        su = float(np.sum(sig[: i + 1, 3] ** 2 * B[: i + 1] ** 2 + sig[i, 2] ** 2))
+        rows.append([i + 1, st / (pc * (st + p * sig[i, 0] ** 2) + (1 - pc)),
+                     su / (pc * (su + q * sig[i, 1] ** 2) + (1 - pc)),
+                     sig[i, 2] ** 2 / (pc * su + (1 - pc)), dll[i], float(oo["Number_steps"][i]),
+                     _signif(float(oo["Last_increment"][i]), 3)])
+    rows = np.round(np.array(rows, dtype=np.float64), digits)
+    names = ["LV", "ssq(T)/ssq(X)" if perc else "ssq(T)", "ssq(U)/ssq(Y)" if perc else "ssq(U)",
+             "sigH^2/ssq(U)" if perc else "sigH^2", "log LR", "#steps", "last incr"]
+    text = "  ".join(names) + "\n" + "\n".join(
+        "  ".join(f"{v:g}" for v in row) for row in rows)
+    return rows, text
 
 
 def scores_PPLS(fit, X, Y, subset=None, ctx=None):
@@ -813,8 +856,9 @@ def PPLS_simult(X, Y, a, EMsteps=10, atol=1e-4, type=("SVD", "QR"), init=None, c
     """PPLS_simult (EM_W_multi.R:758-807) on the GPU.
 
     ``init``: dict(W, C, B, sigE, sigF, sigH, sigT) used as theta0.  Default: the reference's own
-    f0 = PPLS(X, Y, a, 20, 1e-4, 'random') (:762-770, retried up to three times), computed on the
-    device with numpy draws (``seed`` keyword).  Returns dict(Expectations, loglik, estimates) like
+    f0 = PPLS(X, Y, a, 20, 1e-4, 'random') (:762-770, retried when it raises, up to three times),
+    computed on the device; its draws come from ``rng`` (an R-compatible stream, see
+    ``initial_guess``) or numpy (``seed`` keyword).  Returns dict(Expectations, loglik, estimates) like
     the R list of class "PPLS_simult"; warns "Negative increments of likelihood" where the
     reference does (:801).
     """
@@ -823,19 +867,22 @@ def PPLS_simult(X, Y, a, EMsteps=10, atol=1e-4, type=("SVD", "QR"), init=None, c
     ctx = _ctx_with(X, Y, ctx)
     t = _orth_type(type)
     if init is None:
-        rng = np.random.default_rng(kw.get("seed"))
+        rng = kw.get("rng")
+        rng = rng if rng is not None else np.random.default_rng(kw.get("seed"))
         f0 = None
-        for _ in range(3):   # f0 = try(PPLS(...)) three times (:762-764)
+        for _ in range(3):   # f0 = try(PPLS(...)): retried only when PPLS raises (:762-764)
             try:
                 with warnings.catch_warnings():
                     warnings.simplefilter("ignore")
                     f0 = PPLS(None, None, a, 20, 1e-4, "random", rng=rng, ctx=ctx)
-                if len(f0["B"]) == a:
-                    break
+                break
             except PplsError:
                 f0 = None
-        if f0 is None or len(f0["B"]) < a:
+        if f0 is None:
             raise PplsError(-5, "PPLS initialisation failed three times")
+        if len(f0["B"]) < a:
+            # R carries the truncated f0 on and fails at W.[, rotLoad] (:773-776)
+            raise PplsError(-1, f"subscript out of bounds: PPLS returned {len(f0['B'])} of {a} components")
         init = dict(W=f0["W"], C=f0["C"], B=np.diag(f0["B"]), sigE=f0["sig"][a - 1, 0],
                     sigF=f0["sig"][a - 1, 1], sigH=f0["sig"][a - 1, 2], sigT=np.diag(f0["sig"][:, 3]))
     th = Theta(init["W"], init["C"], init["B"], init["sigE"], init["sigF"], init["sigH"], init["sigT"])

@@ -760,9 +760,9 @@ int ppls_comm_init(ppls_ctx* c, int nranks, int rank, const char id[128]) {
   if (!c || nranks < 1 || rank < 0 || rank >= nranks) return PPLS_E_ARG;
   HIPCHK(c, hipSetDevice(c->device));
   if (c->comm) { ncclCommDestroy(c->comm); c->comm = nullptr; }
+  if (nranks > 1 && !id) return fail(c, PPLS_E_ARG, "nranks=%d needs the root's unique id", nranks);
   c->nranks = nranks;
   c->rank = rank;
-  if (nranks > 1 && !id) return fail(c, PPLS_E_ARG, "nranks=%d needs the root's unique id", nranks);
   if (id) {
     ncclUniqueId u;
     memcpy(u.internal, id, 128);
@@ -1116,8 +1116,11 @@ int ppls_em_run(ppls_ctx* c, ppls_theta* th, int r, int max_steps, double atol, 
   // logl[i] - logl[i-1] < atol sets a flag, and every later kernel of the run exits at once, so the
   // host enqueues iterations without a per-iteration read-back.  It polls the flag's host-mapped
   // mirror and stays at most EM_LOOKAHEAD iterations ahead of the device (events), so a long
-  // EMsteps stops launching soon after convergence.  With collectives (RCCL or a host reducer)
-  // every rank enqueues every iteration, so the collective sequence is the same on all ranks.
+  // EMsteps stops launching soon after convergence.  With collectives (RCCL or a host reducer) the
+  // break must be the same on every rank: the mirror holds the iteration the rule fired at, which
+  // every rank computes from the same all-reduced statistics, and a rank breaks at iteration s
+  // iff that iteration is <= s - 1 - EM_LOOKAHEAD -- an iteration whose event it has just synced,
+  // so the answer does not depend on how far each device has run.
   if (do_check) {
     if ((rc = ensure_stop(c)) || (rc = reset_stop(c))) return rc;
     c->sweep_stop = c->stop_d;
@@ -1133,18 +1136,18 @@ int ppls_em_run(ppls_ctx* c, ppls_theta* th, int r, int max_steps, double atol, 
   } guard{c, {}};
   constexpr int EM_LOOKAHEAD = 8;
   std::vector<hipEvent_t>& evs = guard.evs;
-  const bool may_break = c->nranks == 1 && !c->reducer && !c->comm;
   int cur = 0;
   for (int s = 1; s <= max_steps + 1; ++s) {
-    if (do_check && may_break && s > EM_LOOKAHEAD) {
+    if (do_check && s > EM_LOOKAHEAD) {
       HIPCHK(c, hipEventSynchronize(evs[(size_t)(s - 1 - EM_LOOKAHEAD) % EM_LOOKAHEAD]));
-      if (__atomic_load_n(c->stop_mirror, __ATOMIC_ACQUIRE) != 0) break;   // converged: stop launching
+      const int fired = __atomic_load_n(c->stop_mirror, __ATOMIC_ACQUIRE);
+      if (fired != 0 && fired <= s - 1 - EM_LOOKAHEAD) break;   // converged: stop launching
     }
     const int nxt = cur ^ 1;
     const bool wm = want_mu && (do_check || s == max_steps + 1);
     if ((rc = sweep(c, r, cur, wm))) return rc;
     if ((rc = finalize(c, r, cur, nxt, s >= 2 ? s - 2 : -1, type, do_check && s >= 3 ? s : 0))) return rc;
-    if (do_check && may_break) {
+    if (do_check) {
       const size_t k = (size_t)(s - 1) % EM_LOOKAHEAD;
       if (evs.size() <= k) {
         hipEvent_t e;
@@ -1286,7 +1289,8 @@ struct Rank1Dev {
 // sweep and one ppls_rank1_step_kernel (loglik, stop rule, EMstepC_fast update, constraints, next
 // weights), no host round trip.  The host enqueues up to EMsteps steps, at most EM_LOOKAHEAD ahead
 // of the device, and stops launching once the step kernel reports the end of the fit (host-mapped
-// flag; with collectives every rank enqueues every step so the collective sequence matches).
+// flag = the step it ended at + 1; a rank breaks at step s iff that step is <= s - LOOKAHEAD, whose
+// event it has synced, so all ranks break at the same step and their collectives stay matched).
 // t: in = the constrained initial component, out = the fit.  lv: logvalue[0..i]; G: the last Gram.
 int rank1_fit_device(ppls_ctx* c, Rank1Dev& d, Rank1& t, const ppls_constraint* ck, int m, double ssqX,
                      double ssqY, int max_steps, double atol, int crit_abs, const std::vector<double>& Wp,
@@ -1331,16 +1335,16 @@ int rank1_fit_device(ppls_ctx* c, Rank1Dev& d, Rank1& t, const ppls_constraint* 
   } guard{c, {}};
   c->sweep_stop = c->stop_d;
   constexpr int LOOKAHEAD = 8;
-  const bool may_break = c->nranks == 1 && !c->reducer && !c->comm;
   for (int step = 0; step <= max_steps; ++step) {
-    if (may_break && step >= LOOKAHEAD) {
+    if (step >= LOOKAHEAD) {
       HIPCHK(c, hipEventSynchronize(guard.evs[(size_t)(step - LOOKAHEAD) % LOOKAHEAD]));
-      if (__atomic_load_n(c->stop_mirror, __ATOMIC_ACQUIRE) != 0) break;   // the fit ended
+      const int ended = __atomic_load_n(c->stop_mirror, __ATOMIC_ACQUIRE);
+      if (ended != 0 && ended - 1 <= step - LOOKAHEAD) break;   // the fit ended
     }
     if ((rc = sweep(c, 1, 0, false))) return rc;
     a.step = step;
     HIPCHK(c, ppls_launch_rank1_step(&a, c->stream));
-    if (may_break) {
+    {
       const size_t k = (size_t)step % LOOKAHEAD;
       if (guard.evs.size() <= k) {
         hipEvent_t e;
@@ -1354,7 +1358,7 @@ int rank1_fit_device(ppls_ctx* c, Rank1Dev& d, Rank1& t, const ppls_constraint* 
   int stop[2] = {0, 0};
   HIPCHK(c, hipMemcpy(stop, c->stop_d, sizeof stop, hipMemcpyDeviceToHost));
   *na = stop[1] != 0;
-  *steps = stop[0] > 0 ? stop[0] : max_steps;
+  *steps = stop[0] > 0 ? stop[0] : stop[0] < 0 ? -stop[0] : max_steps;   // < 0: sigma collapse at step -stop[0]-1
   std::vector<double> buf((size_t)max_steps + 5);
   HIPCHK(c, hipMemcpy(buf.data(), d.lv, sizeof(double) * buf.size(), hipMemcpyDeviceToHost));
   lv.assign(buf.begin(), buf.begin() + (*steps + 1));

@@ -1973,7 +1973,10 @@ __global__ __launch_bounds__(PPLS_FIN_THREADS) void ppls_finalize_kernel(
     int stage_lds, long long* __restrict__ trace,
     int* __restrict__ stop, int* __restrict__ stop_mirror, int stop_check, int stop_step, double atol,
     int KX, int KY, unsigned* __restrict__ team_bar, double* __restrict__ team_part) {
-  if (stop && *stop) return;   // em_run converged earlier (device stop flag)
+  // em_run converged at an EARLIER iteration: exit.  The flag this launch's own scalar block may
+  // set (== stop_step) must not stop a polar-team member that starts late, or its teammates would
+  // wait at the team barrier for a member that never comes.
+  if (stop && *stop && *stop != stop_step) return;
   constexpr int NT = PPLS_FIN_THREADS;
   constexpr int NG = R * (R + 1) / 2;
   extern __shared__ double dyn_lds[];
@@ -2091,7 +2094,7 @@ __global__ __launch_bounds__(256) void ppls_finalize_generic_kernel(
     PplsScalars* __restrict__ sc_nxt, PplsMoments* __restrict__ mom, double* __restrict__ loglik,
     int logl_index, double* __restrict__ work, int* __restrict__ status, int qr, int mode,
     int* __restrict__ stop, int* __restrict__ stop_mirror, int stop_check, int stop_step, double atol) {
-  if (stop && *stop) return;   // em_run converged earlier (device stop flag)
+  if (stop && *stop && *stop != stop_step) return;   // converged at an earlier iteration
   const double* SX = stats;
   const double* SY = stats + (int64_t)r * ldx;
   const double* G = SY + (int64_t)r * ldy;
@@ -2214,9 +2217,12 @@ __global__ __launch_bounds__(1024) void ppls_rank1_step_kernel(PplsRank1StepArgs
     const double tiny = 100.0 * 2.220446049250313e-16;   // 100 * .Machine$double.eps
     if (!ex && (t.sigE < tiny || t.sigF < tiny)) {
       a.stop[1] = 1;
+      a.stop[0] = -(a.step + 1);   // nonzero: the fit's remaining sweeps exit at entry too
       ex = 1;
     }
-    if (ex && a.stop_mirror) __hip_atomic_store(a.stop_mirror, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    // mirror = the step the fit ended at + 1, so every rank can break at the same host iteration
+    if (ex && a.stop_mirror)
+      __hip_atomic_store(a.stop_mirror, a.step + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     if (!ex) {
       PplsRank1 n;
       ppls_rank1_scalars(&t, G, a.ssqX, a.ssqY, a.N, a.p, a.q, &n);

@@ -56,7 +56,7 @@ def _relerr(a, b):
 
 
 def _golden():
-    return sorted(f for f in os.listdir(GOLD) if f.endswith(".npz") and not f.startswith(("seq_", "meta_")))
+    return sorted(f for f in os.listdir(GOLD) if f.endswith(".npz") and not f.startswith(("seq_", "meta_", "rcheck_")))
 
 
 @pytest.mark.parametrize("sweep", SWEEPS, ids=SWEEP_IDS)
@@ -328,3 +328,30 @@ def test_polar_team_sizes_agree(ctx, team_rows):
     assert _relerr(a[1], ref["loglik"]) < 1e-10 and np.abs(a[0].W - ref["estimates"]["W"]).max() < 1e-8
     assert _relerr(a[1], b[1]) < 1e-13
     assert np.abs(a[0].W - b[0].W).max() < 1e-11 and np.abs(a[0].C - b[0].C).max() < 1e-11
+
+
+def test_eout_is_expect_m_of_the_uncanonicalised_theta(ctx):
+    """PPLS_simult's `Expectations` (EM_W_multi.R:802) are Expect_M at the loop's LAST theta, before
+    the final sign/order canonicalisation (:794-799).  A fit whose components swap order and stops by
+    the rule (atol) after ~110 iterations: eout must equal the oracle's Expectations, which differ
+    from Expect_M at the canonicalised estimates."""
+    X, Y, th = make_problem(300, 20, 16, 2, seed=16)
+    th0 = dict(th, W=th["W"][:, ::-1].copy(), C=th["C"][:, ::-1].copy(), B=np.diag([0.6, 1.3]),
+               sigT=np.diag([0.5, 1.2]))
+    ref = o.ppls_simult(X, Y, 2, EMsteps=400, atol=1e-2, theta0=th0)
+    E, est_ref = ref["Expectations"], ref["estimates"]
+    E_canon = o.expect_m(X, Y, est_ref["W"], est_ref["C"], est_ref["B"], est_ref["sigE"], est_ref["sigF"],
+                         est_ref["sigH"], est_ref["sigT"])
+    assert 3 <= len(ref["loglik"]) < 400                                # the stop rule fired
+    assert np.abs(E["mu_T"] - E_canon["mu_T"]).max() > 1.0              # canonicalisation reordered
+    ctx.set_data(X, Y)
+    est, ll, eout, _ = ctx.em_run(_theta(th0), 400, 1e-2, 0)
+    assert len(ll) == len(ref["loglik"])
+    assert np.abs(est.W - est_ref["W"]).max() < 1e-8
+    assert _relerr(est.B, np.diag(est_ref["B"])) < 1e-8
+    for k in ("mu_T", "mu_U", "Chh"):
+        assert _relerr(getattr(eout, k), E[k]) < 1e-8, k
+    for k in ("Ctt", "Cuu", "Cut"):
+        assert _relerr(getattr(eout, k), np.diag(E[k])) < 1e-8, k
+    cee, cff = float(np.ravel(E["Cee"])[0]), float(np.ravel(E["Cff"])[0])
+    assert abs(eout.Cee - cee) / cee < 1e-8 and abs(eout.Cff - cff) / cff < 1e-8

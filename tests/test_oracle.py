@@ -71,7 +71,7 @@ def test_golden_fixtures_reproduce():
     import json, os
     here = os.path.join(os.path.dirname(__file__), "golden")
     for name in sorted(os.listdir(here)):
-        if not name.endswith(".npz") or name.startswith(("seq_", "meta_")):
+        if not name.endswith(".npz") or name.startswith(("seq_", "meta_", "rcheck_")):
             continue
         g = np.load(os.path.join(here, name))
         meta = json.loads(str(g["meta"]))
