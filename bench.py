@@ -11,6 +11,7 @@ normals) generated on the device before the timed region.  Rank 0 prints ONE JSO
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
 import sys
@@ -247,12 +248,30 @@ def main():
         dt = float(tt.item())
     est, ll = ctx.em_state()
     info = ctx.sweep_info(r)
+    rccl_nranks, rccl_rank, ar_ms, ar_calls = ctx.comm_info(reset=True)
+    # every rank's final theta and trace, hashed: a dp-N run proves its ranks stayed identical
+    h = hashlib.sha256()
+    for a in (est.W, est.C, est.B, est.sigT, np.array([est.sigE, est.sigF, est.sigH]), ll):
+        h.update(np.ascontiguousarray(a, dtype=np.float64).tobytes())
+    digest = h.hexdigest()[:16]
+    digests = [digest]
+    if dist is not None:
+        digests = [None] * world
+        dist.all_gather_object(digests, digest)
 
     if rank == 0:
         its = args.steps / dt
         avg_kernel_ms = kern_ms / max(launches, 1)
         achieved = info["bytes_per_sweep"] / (avg_kernel_ms * 1e-3) / 1e9 if launches else None
         wl = f"{args.config}_{'dp%d' % world}"
+        stat_doubles = (p + q) * r + 4 * r * r      # [X'mu_T | Y'mu_U | Gram], one all-reduce per iteration
+        if world == 1:
+            backend = "none"
+            parallelism = "dp1 (single rank, no all-reduce)"
+        else:
+            backend = "rccl" if args.comm == "rccl" else "host reducer over gloo"
+            parallelism = (f"dp{world} (rows sharded, 1 {'RCCL' if args.comm == 'rccl' else 'host (gloo)'} "
+                           f"all-reduce of {stat_doubles} doubles/iteration)")
         # compute side: 2r fp64 FMAs per element (r for the dots, r for the rank-1 update), on
         # VALU (no fp64 MFMA shape fits r <= 8 better, and its rate equals the VALU rate)
         flops = 4.0 * (n_local * (p + q)) * r
@@ -270,11 +289,19 @@ def main():
                    scaling="strong", vs_baseline=None, dtype="f64",
                    storage=cfg.get("storage", "f64"),
                    data="synthetic (simulC model: X=TW'+sigE E, Y=UC'+sigF F; Philox normals on device)",
-                   config=dict(workload=cfg["name"], n=n, p=p, q=q, r=r,
-                               parallelism=f"dp{world} (rows sharded, 1 {'RCCL' if args.comm == 'rccl' else 'host (gloo)'} "
-                                           f"all-reduce/iteration)"),
+                   config=dict(workload=cfg["name"], n=n, p=p, q=q, r=r, parallelism=parallelism),
                    roofline=roofline,
-                   loglik_last=float(ll[-1]) if len(ll) else None)
+                   # same theta0, warmup + steps iterations for every N: equal across dp1..dp8 to
+                   # rounding (the sharded sums are reordered)
+                   loglik_last=float(ll[-1]) if len(ll) else None,
+                   # nranks/rank as ncclCommCount/ncclCommUserRank report them (RCCL only)
+                   comm=dict(backend=backend,
+                             nranks_reported=rccl_nranks if backend == "rccl" else None,
+                             rank0_reported=rccl_rank if backend == "rccl" else None,
+                             allreduce_doubles=stat_doubles,
+                             allreduce_us=(1e3 * ar_ms / ar_calls) if ar_calls else None,
+                             allreduce_timed_calls=ar_calls),
+                   theta_sha16=digest, ranks_bitwise_identical=len(set(digests)) == 1)
         if world == 1 and not args.no_cpu:
             cb, rel, werr = cpu_baseline(ctx, th0, cfg, args.cpu_iters)
             out["cpu_baseline"] = cb

@@ -234,6 +234,11 @@ int ppls_gram(ppls_ctx* ctx, int xory, int nsplit, double* G, double* ms);
 /* ---- measurement ---------------------------------------------------------------------------- */
 /* Sum of HIP-event durations of the sweep kernel launches recorded since the last reset. */
 int ppls_sweep_timing(ppls_ctx* ctx, double* total_ms, int64_t* launches, int reset);
+/* The communicator as RCCL reports it (ncclCommCount / ncclCommUserRank; without RCCL the
+ * context's own nranks/rank, i.e. 1/0 or the host reducer's) and the summed HIP-event durations of
+ * the per-iteration statistics all-reduce on the timed sweeps (option "timing"; RCCL only). */
+int ppls_comm_info(ppls_ctx* ctx, int* nranks, int* rank, double* allreduce_ms, int64_t* allreduce_calls,
+                   int reset);
 /* Shape facts for the roofline: bytes of X and Y one sweep reads (algorithmic), kernel variant. */
 int ppls_sweep_info(ppls_ctx* ctx, int r, int64_t* bytes_per_sweep, int* variant, int* grid);
 /* The sweep kernel instantiation the next EM iteration with r components launches, as text

@@ -408,6 +408,13 @@ class Context:
         self._chk(self._L.ppls_sweep_timing(self.h, ct.byref(ms), ct.byref(n), int(reset)))
         return ms.value, n.value
 
+    def comm_info(self, reset=True):
+        """(nranks, rank) as RCCL's communicator reports them (ncclCommCount / ncclCommUserRank; the
+        context's own values without RCCL) and (total ms, calls) of the timed all-reduces."""
+        nr, rk, ms, n = ct.c_int(), ct.c_int(), ct.c_double(), ct.c_int64()
+        self._chk(self._L.ppls_comm_info(self.h, ct.byref(nr), ct.byref(rk), ct.byref(ms), ct.byref(n), int(reset)))
+        return nr.value, rk.value, ms.value, n.value
+
     def sweep_trace(self, grid):
         """Per-workgroup wall-clock stamps (us, relative to the earliest entry) of the last split
         sweep: (grid, 4) = entry, ring prologue done, row loop done, partials written."""

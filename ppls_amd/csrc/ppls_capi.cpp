@@ -99,6 +99,11 @@ struct ppls_ctx {
   size_t ev_used = 0;
   double timed_ms = 0.0;
   int64_t timed_launches = 0;
+  // the statistics all-reduce of the timed sweeps (RCCL only), same bookkeeping
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_ar;
+  size_t ev_ar_used = 0;
+  double ar_ms = 0.0;
+  int64_t ar_calls = 0;
 };
 
 namespace {
@@ -422,6 +427,19 @@ int sweep(ppls_ctx* c, int r, int slot, bool write_mu) {
     if (timed) HIPCHK(c, hipEventRecord(e1, c->stream));
     HIPCHK(c, ppls_launch_reduce2(c->part, groups, c->part_ld, c->part_ld, c->stats,
                                   c->part + (size_t)c->part_groups * c->part_ld, c->sweep_stop, c->stream));
+    if (timed && c->comm && !c->reducer) {   // time this iteration's RCCL all-reduce as well
+      if (c->ev_ar_used == c->ev_ar.size()) {
+        std::pair<hipEvent_t, hipEvent_t> pr;
+        HIPCHK(c, hipEventCreate(&pr.first));
+        HIPCHK(c, hipEventCreate(&pr.second));
+        c->ev_ar.push_back(pr);
+      }
+      const auto& pr = c->ev_ar[c->ev_ar_used++];
+      HIPCHK(c, hipEventRecord(pr.first, c->stream));
+      const int rc = allreduce(c, c->stats, (size_t)c->part_ld);
+      HIPCHK(c, hipEventRecord(pr.second, c->stream));
+      return rc;
+    }
   }
   return allreduce(c, c->stats, (size_t)c->part_ld);
 }
@@ -671,6 +689,7 @@ void ppls_ctx_destroy(ppls_ctx* c) {
   dfree(c->team_part);
   if (c->stop_mirror) (void)hipHostFree(c->stop_mirror);
   for (auto& e : c->ev) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
+  for (auto& e : c->ev_ar) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
   if (c->blas) (void)rocblas_destroy_handle(c->blas);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
@@ -2104,6 +2123,30 @@ int ppls_sweep_timing(ppls_ctx* c, double* total_ms, int64_t* launches, int rese
   if (total_ms) *total_ms = c->timed_ms;
   if (launches) *launches = c->timed_launches;
   if (reset) { c->timed_ms = 0.0; c->timed_launches = 0; }
+  return PPLS_OK;
+}
+
+int ppls_comm_info(ppls_ctx* c, int* nranks, int* rank, double* allreduce_ms, int64_t* allreduce_calls,
+                   int reset) {
+  if (!c) return PPLS_E_ARG;
+  int nr = c->nranks, rk = c->rank;
+  if (c->comm) {   // what RCCL itself reports for the communicator
+    RCCLCHK(c, ncclCommCount(c->comm, &nr));
+    RCCLCHK(c, ncclCommUserRank(c->comm, &rk));
+  }
+  if (nranks) *nranks = nr;
+  if (rank) *rank = rk;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  for (size_t i = 0; i < c->ev_ar_used; ++i) {
+    float ms = 0.f;
+    HIPCHK(c, hipEventElapsedTime(&ms, c->ev_ar[i].first, c->ev_ar[i].second));
+    c->ar_ms += ms;
+    ++c->ar_calls;
+  }
+  c->ev_ar_used = 0;
+  if (allreduce_ms) *allreduce_ms = c->ar_ms;
+  if (allreduce_calls) *allreduce_calls = c->ar_calls;
+  if (reset) { c->ar_ms = 0.0; c->ar_calls = 0; }
   return PPLS_OK;
 }
 

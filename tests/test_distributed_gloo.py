@@ -1,11 +1,13 @@
-"""World-size-2 coverage of the multi-GPU algorithm on CPU (gloo).
+"""ALGORITHM-LEVEL test of the data-parallel decomposition, world size 2 on CPU (gloo).
 
-Per EM iteration each rank reduces ITS rows to the sufficient statistics [X'mu_T | Y'mu_U | Gram]
-(here by the oracle, standing in for the device sweep), the ranks all-reduce them (the one RCCL
-call per iteration on the GPU), and every rank runs the SAME finalize (the library's
-ppls_finalize_host, i.e. the device finalize's ppls_math.h code compiled for the host) -- no
-broadcast.  Checks: the sharded run equals the unsharded oracle PPLS_simult, and both ranks hold
-bit-identical parameters after every iteration.
+This checks the sharding algorithm, not the device path: per EM iteration each rank reduces ITS
+rows to the sufficient statistics [X'mu_T | Y'mu_U | Gram] with the ORACLE's sweep_stats (no GPU
+here), the ranks all-reduce them (the one RCCL call per iteration on the GPU), and every rank runs
+the SAME finalize (the library's ppls_finalize_host, i.e. the device finalize's ppls_math.h code
+compiled for the host) -- no broadcast.  Checks: the sharded run equals the unsharded oracle
+PPLS_simult, and both ranks hold bit-identical parameters after every iteration.  The same
+decomposition through the device sweep is tests/test_gpu_multirank.py (k contexts, two gloo
+processes, and the full-size C4 eight-shard run).
 """
 import ctypes as ct
 import os

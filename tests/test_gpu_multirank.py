@@ -241,3 +241,44 @@ def test_k_contexts_device_stop_rule():
         assert np.array_equal(est.W, res[0][0].W)
     assert np.abs(res[0][1] - ref[1]).max() / np.abs(ref[1]).max() < 1e-12
     assert np.abs(res[0][0].W - ref[0].W).max() < 1e-12
+
+
+def test_c4_full_size_eight_shards():
+    """BASELINE config C4 at its full size through the sharded library path: n = 1e6, p = q = 2000,
+    r = 5 over 8 row shards (8 contexts on GPU 0, 4 GB each, the host reducer standing in for RCCL),
+    3 EM iterations from the bench's theta0.  Sharded must equal unsharded to 1e-12 and all 8 ranks
+    must hold bitwise-identical estimates (EM_W_multi.R:689-712, :732-733 are row sums)."""
+    from ppls_amd import Context, Theta
+    k, n, p, q, r, steps = 8, 1_000_000, 2000, 2000, 5, 3
+
+    def polar(M):
+        U, _, Vt = np.linalg.svd(M, full_matrices=False)
+        return U @ Vt
+
+    kk = np.arange(r)   # bench.py's truth and theta0 (SURVEY.md §8d)
+    truth = Theta(polar(np.random.default_rng(1).standard_normal((p, r))),
+                  polar(np.random.default_rng(2).standard_normal((q, r))),
+                  np.exp(np.log(1.5) - 0.3 * kk), 0.5, 0.5, 0.1, np.exp(-0.1 * kk))
+    th0 = dict(W=polar(np.random.default_rng(3).standard_normal((p, r))),
+               C=polar(np.random.default_rng(4).standard_normal((q, r))),
+               B=np.eye(r), sigE=1.0, sigF=1.0, sigH=1.0, sigT=np.eye(r))
+
+    def fit(c, row0, n_local):
+        c.generate_synthetic(n, p, q, truth, seed=20261015, row0=row0, n_local=n_local)
+        est, ll, _, _ = c.em_run(_theta(th0), steps, -np.inf, 0, want_eout=False)
+        return est, ll, c.sweep_kernel(r)
+
+    with Context(0) as c:
+        ref = fit(c, 0, n)
+    res = _run_ranks(k, lambda rank, c: fit(c, *Context.shard_range(n, k, rank)))
+    assert res[0][2] == ref[2] and res[0][2].startswith("split<5,")
+    for est, ll, _ in res:
+        for a, b in ((est.W, res[0][0].W), (est.C, res[0][0].C), (est.B, res[0][0].B),
+                     (est.sigT, res[0][0].sigT), (ll, res[0][1])):
+            assert np.array_equal(a, b)
+        assert (est.sigE, est.sigF, est.sigH) == (res[0][0].sigE, res[0][0].sigF, res[0][0].sigH)
+    est, ll, _ = res[0]
+    assert np.abs(ll - ref[1]).max() / np.abs(ref[1]).max() < 1e-12
+    assert np.abs(est.W - ref[0].W).max() < 1e-12 and np.abs(est.C - ref[0].C).max() < 1e-12
+    assert np.abs(est.B - ref[0].B).max() / np.abs(ref[0].B).max() < 1e-12
+    assert abs(est.sigE - ref[0].sigE) / ref[0].sigE < 1e-12
