@@ -72,6 +72,22 @@ def load_traffic(workload_key):
         return None
 
 
+def load_compute_counters(workload_key, kernel_sub):
+    """Counter-based MFMA / VALU utilisation of a kernel from a committed rocprofv3 PMC pass
+    (profiles/pmc_compute_<workload>.json, tools/pmc_compute.sh + pmc_compute_summary.py), or None."""
+    path = os.path.join(ROOT, "profiles", f"pmc_compute_{workload_key}.json")
+    try:
+        with open(path) as f:
+            k = json.load(f)["kernels"].get(kernel_sub)
+    except (OSError, ValueError, KeyError):
+        return None
+    if not k:
+        return None
+    return dict(mfma_busy=k["mfma_busy"], valu_busy=k["valu_busy"], effective_clock_ghz=k.get("effective_clock_ghz"),
+                fp64_valu_tflops=k.get("fp64_valu_tflops"), fp64_mfma_tflops=k.get("fp64_mfma_tflops"),
+                source=f"profiles/pmc_compute_{workload_key}.json ({kernel_sub})")
+
+
 def cpu_model():
     try:
         with open("/proc/cpuinfo") as f:
@@ -284,6 +300,12 @@ def main():
                         fp64_valu_frac=(tflops / FP64_PEAK_TF) if tflops else None,
                         measured_read_ceiling=READ_CEILING_GBS,
                         frac_of_measured_ceiling=(achieved / READ_CEILING_GBS) if achieved else None)
+        # rocprofv3 PMC counters (SQ_VALU_MFMA_BUSY_CYCLES, SQ_ACTIVE_INST_VALU, GRBM_GUI_ACTIVE) of the
+        # sweep kernel(s) at this workload, committed under profiles/
+        if info["variant"] == "panel":
+            roofline["counters"] = {k: load_compute_counters(wl, k) for k in ("panel_mfmadots", "panel_acc")}
+        else:
+            roofline["counters"] = {"sweep_split": load_compute_counters(wl, "sweep_split")}
         out = dict(metric=METRIC, value=its, unit="EM iterations/s", n_gpus=world, steps=args.steps,
                    warmup=args.warmup, ms_per_step=1e3 * dt / args.steps, higher_is_better=True,
                    scaling="strong", vs_baseline=None, dtype="f64",

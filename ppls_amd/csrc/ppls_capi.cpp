@@ -36,6 +36,7 @@ struct ppls_ctx {
   int ablate = 0;
   int team_rows = 0;   // finalize polar team: rows of S per member (0: PPLS_TEAM_ROWS)
   int polar1 = 1;   // finalize polar: Cholesky-QR1 fast path when kappa(X'mu) <= PPLS_POLAR1_KAPPA
+  int polar1_kappa = 0;   // its bound on ||R1||_F ||R1^-1||_F (0 = min(8 r, 40))
   int ldpad = 1;   // row padding of the panel sweep's rows (ld_of); 0 = 16-B rows (experiment)
   int dtype = 0;           // storage of X, Y: 0 fp64, 1 fp32 (arithmetic is fp64 either way)
   int nt_loads = -1;       // sweep LDS-DMA non-temporal: -1 auto (when X, Y exceed the MALL), 0 off, 1 on
@@ -301,6 +302,14 @@ int download_mu(ppls_ctx* c, int r, ppls_expect* e) {
   return PPLS_OK;
 }
 
+// The finalize's Cholesky-QR1 acceptance bound on ||R1||_F ||R1^-1||_F (>= kappa_2): CholQR1 loses
+// ~eps kappa^2 of orthogonality, so the default keeps kappa <= 40 (<= 1e-13); at C3/C4 it lets
+// Y'mu_U (kappa ~ 20) skip the second Cholesky-QR pass (profiles/r3_polar1_kappa_ab.txt).
+int polar1_bound(const ppls_ctx* c, int r) {
+  if (c->polar1_kappa > 0) return c->polar1_kappa;
+  return std::min(8 * r, 40);
+}
+
 int grid_of(ppls_ctx* c) { return c->grid_opt > 0 ? c->grid_opt : c->num_cus; }
 
 // Allreduce in place (sum) over ranks, on the context stream: RCCL, or the caller's host
@@ -466,7 +475,7 @@ int finalize(ppls_ctx* c, int r, int cur, int nxt, int logl_index, int type, int
   f.work = c->work;
   f.status = c->status;
   f.qr = type == PPLS_ORTH_QR ? 1 : 0;
-  f.mode = (3 & ~(c->ablate >> 2)) | (c->polar1 ? 4 : 0);   // ablate bit2: skip polar, bit3: skip scalars
+  f.mode = (3 & ~(c->ablate >> 2)) | (c->polar1 ? 4 : 0) | (polar1_bound(c, r) << 8);   // ablate bit2: skip polar, bit3: skip scalars
   f.trace = c->ftrace;
   f.gram_cur = c->gram[cur];
   f.gram_nxt = c->gram[nxt];
@@ -716,6 +725,9 @@ int ppls_set_option(ppls_ctx* c, const char* key, int64_t value) {
     c->team_rows = (int)value;
   } else if (!strcmp(key, "polar1")) {
     c->polar1 = value ? 1 : 0;
+  } else if (!strcmp(key, "polar1_kappa")) {
+    if (value < 0 || value > 255) return fail(c, PPLS_E_ARG, "polar1_kappa must be in [0, 255]");
+    c->polar1_kappa = (int)value;
   } else if (!strcmp(key, "pipe")) {
     c->pipe_opt = value ? 1 : 0;
   } else if (!strcmp(key, "ldpad")) {   // applies to data set or generated afterwards
@@ -1077,7 +1089,7 @@ int ppls_mstep(ppls_ctx* c, const ppls_expect* fit, int r, int type, ppls_theta*
   memset(&f, 0, sizeof f);
   f.stats = c->stats; f.ssq = c->ssq; f.N = (double)c->n_total; f.p = c->p; f.q = c->q; f.r = r;
   f.ldx = c->ldx; f.ldy = c->ldy; f.Wn = c->W[1]; f.Cn = c->C[1]; f.work = c->work; f.status = c->status;
-  f.logl_index = -1; f.qr = type == PPLS_ORTH_QR ? 1 : 0; f.mode = 1 | (c->polar1 ? 4 : 0);   // polar only
+  f.logl_index = -1; f.qr = type == PPLS_ORTH_QR ? 1 : 0; f.mode = 1 | (c->polar1 ? 4 : 0) | (polar1_bound(c, r) << 8);   // polar only
   HIPCHK(c, ppls_launch_finalize(&f, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   if ((rc = check_status(c))) return rc;

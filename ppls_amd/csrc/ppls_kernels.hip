@@ -1482,7 +1482,7 @@ __device__ bool ppls_block_polar_fast(const double* __restrict__ S, int64_t lds,
                                       double* __restrict__ out, int64_t ldo, int ldo_rows, double* Sl,
                                       double* sh, double* sm, double* __restrict__ gram_out,
                                       double* __restrict__ vstate, long long* tr, const PplsTeam& tm,
-                                      bool polar1) {
+                                      bool polar1, double kbound) {
   constexpr int NG = R * (R + 1) / 2;
   constexpr int NW = NT / 64;
   constexpr int G = PplsWaveBlk<R>::G, GG = G * G;
@@ -1594,7 +1594,8 @@ __device__ bool ppls_block_polar_fast(const double* __restrict__ S, int64_t lds,
   // Cholesky-QR1 fast path (polar1): when kappa(S) = kappa(R1) is small, Q1 = S R1^-1 is already
   // orthonormal to O(eps kappa^2) (~1e-14), so pass 2, its team barrier and chol(G2) are skipped:
   // T = R1 = U_T Sigma V' by the Jacobi, out = S F, F = R1^-1 U_T V'.  The test is the bound
-  // kappa_2(R1) <= ||R1||_F ||R1^-1||_F <= PPLS_POLAR1_KAPPA * R (no Jacobi is spent on a matrix
+  // kappa_2(R1) <= ||R1||_F ||R1^-1||_F <= kbound (option polar1_kappa; default min(8 R, 40): the
+  // loss of orthogonality ~ eps kappa^2 stays <= 1e-13; no Jacobi is spent on a matrix
   // that then takes the Cholesky-QR2 path).  Every member decides on the bitwise-identical G1, so
   // a team takes one path.
   __shared__ int fast;
@@ -1609,7 +1610,8 @@ __device__ bool ppls_block_polar_fast(const double* __restrict__ S, int64_t lds,
       }
       fr = ppls_wave_sum(fr);
       fi = ppls_wave_sum(fi);
-      fst = __shfl(fr * fi <= (PPLS_POLAR1_KAPPA * R) * (PPLS_POLAR1_KAPPA * R) ? 1 : 0, 0, 64) != 0;
+      const double kb = kbound > 0.0 ? kbound : PPLS_POLAR1_KAPPA * R;
+      fst = __shfl(fr * fi <= kb * kb ? 1 : 0, 0, 64) != 0;
     }
     if (fst) {
       load_vprev();
@@ -2013,7 +2015,8 @@ __global__ __launch_bounds__(PPLS_FIN_THREADS) void ppls_finalize_kernel(
     tm.status = status;
     tm.tr = tr;
     if (qr || !ppls_block_polar_fast<R, NT>(S, ld, rows, out, ld, ld, stage_lds ? dyn_lds : nullptr, sh,
-                                            sm, gout, vs, tr, tm, (mode & 4) != 0)) {
+                                            sm, gout, vs, tr, tm, (mode & 4) != 0,
+                                            (double)((mode >> 8) & 255))) {
       if (tm.rank != 0) return;   // the Householder fallback runs on one block
       ppls_block_polar(S, ld, rows, R, out, ld, ld, w2, w2 + (int64_t)rows * R, status, qr);
       if (gout) {

@@ -243,6 +243,51 @@ def test_k_contexts_device_stop_rule():
     assert np.abs(res[0][0].W - ref[0].W).max() < 1e-12
 
 
+def test_k_contexts_stop_launching_after_convergence():
+    """With collectives every rank breaks at the same iteration soon after the device stop rule
+    fires (not after all EMsteps): the number of all-reduces stays near the stopping iteration
+    plus the host's look-ahead of 8 iterations, and the fit equals the unsharded one."""
+    from ppls_amd import Context
+    k, n, p, q, r, steps = 3, 1500, 70, 40, 2, 5000
+    X, Y, th0 = make_problem(n, p, q, r, seed=91)
+
+    def fit(c, Xs, Ys, n_total):
+        c.set_data(Xs, Ys, n_total=n_total)
+        est, ll, _, _ = c.em_run(_theta(th0), steps, 1e-3, 0)
+        return est, ll
+
+    with Context(0) as c:
+        ref = fit(c, X, Y, None)
+    stop = len(ref[1])
+    assert 3 <= stop < 1000
+
+    red = ThreadAllReduce(k)
+    out, errs = [None] * k, []
+
+    def body(rank):
+        try:
+            with Context(0) as c:
+                c.set_reducer(red.fn(rank))
+                r0, nl = Context.shard_range(n, k, rank)
+                out[rank] = fit(c, X[r0:r0 + nl], Y[r0:r0 + nl], n)
+        except BaseException as e:   # noqa: BLE001
+            errs.append(e)
+            red.bar.abort()
+
+    ths = [threading.Thread(target=body, args=(i,)) for i in range(k)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join(timeout=300)
+    if errs:
+        raise errs[0]
+    # set_data's ||X||^2 all-reduce + one per iteration up to stop + 1 + look-ahead
+    assert red.calls <= stop + 1 + 8 + 3, (red.calls, stop)
+    for est, ll in out:
+        assert len(ll) == stop and np.array_equal(ll, out[0][1])
+    assert np.abs(out[0][1] - ref[1]).max() / np.abs(ref[1]).max() < 1e-12
+
+
 def test_c4_full_size_eight_shards():
     """BASELINE config C4 at its full size through the sharded library path: n = 1e6, p = q = 2000,
     r = 5 over 8 row shards (8 contexts on GPU 0, 4 GB each, the host reducer standing in for RCCL),
@@ -282,3 +327,41 @@ def test_c4_full_size_eight_shards():
     assert np.abs(est.W - ref[0].W).max() < 1e-12 and np.abs(est.C - ref[0].C).max() < 1e-12
     assert np.abs(est.B - ref[0].B).max() / np.abs(ref[0].B).max() < 1e-12
     assert abs(est.sigE - ref[0].sigE) / ref[0].sigE < 1e-12
+
+
+def test_c5_full_size_eight_shards():
+    """BASELINE config C5 at its full size through the sharded library path: n = 5e5, p = 1e4, q = 500,
+    r = 10, fp32 storage (the panel sweep) over 8 row shards (8 contexts on GPU 0, 2.6 GB each, the host
+    reducer standing in for RCCL), 2 EM iterations: sharded = unsharded to 1e-12, ranks bitwise equal."""
+    from ppls_amd import Context, Theta
+    k, n, p, q, r, steps = 8, 500_000, 10_000, 500, 10, 2
+
+    def polar(M):
+        U, _, Vt = np.linalg.svd(M, full_matrices=False)
+        return U @ Vt
+
+    kk = np.arange(r)
+    truth = Theta(polar(np.random.default_rng(1).standard_normal((p, r))),
+                  polar(np.random.default_rng(2).standard_normal((q, r))),
+                  np.exp(np.log(1.5) - 0.3 * kk), 0.5, 0.5, 0.1, np.exp(-0.1 * kk))
+    th0 = dict(W=polar(np.random.default_rng(3).standard_normal((p, r))),
+               C=polar(np.random.default_rng(4).standard_normal((q, r))),
+               B=np.eye(r), sigE=1.0, sigF=1.0, sigH=1.0, sigT=np.eye(r))
+
+    def fit(c, row0, n_local):
+        c.set_option("dtype", 1)
+        c.generate_synthetic(n, p, q, truth, seed=20261015, row0=row0, n_local=n_local)
+        est, ll, _, _ = c.em_run(_theta(th0), steps, -np.inf, 0, want_eout=False)
+        return est, ll, c.sweep_info(r)["variant"]
+
+    with Context(0) as c:
+        ref = fit(c, 0, n)
+    res = _run_ranks(k, lambda rank, c: fit(c, *Context.shard_range(n, k, rank)))
+    assert res[0][2] == ref[2] == "panel"
+    for est, ll, _ in res:
+        for a, b in ((est.W, res[0][0].W), (est.C, res[0][0].C), (est.B, res[0][0].B), (ll, res[0][1])):
+            assert np.array_equal(a, b)
+    est, ll, _ = res[0]
+    assert np.abs(ll - ref[1]).max() / np.abs(ref[1]).max() < 1e-12
+    assert np.abs(est.W - ref[0].W).max() < 1e-12 and np.abs(est.C - ref[0].C).max() < 1e-12
+    assert np.abs(est.B - ref[0].B).max() / np.abs(ref[0].B).max() < 1e-12

@@ -355,3 +355,21 @@ def test_eout_is_expect_m_of_the_uncanonicalised_theta(ctx):
         assert _relerr(getattr(eout, k), np.diag(E[k])) < 1e-8, k
     cee, cff = float(np.ravel(E["Cee"])[0]), float(np.ravel(E["Cff"])[0])
     assert abs(eout.Cee - cee) / cee < 1e-8 and abs(eout.Cff - cff) / cff < 1e-8
+
+
+def test_team_finalize_with_early_stop(ctx):
+    """A finite atol on a wide-p fit whose polar factor runs as a team of small members
+    (team_rows 256: p = 3000 -> 12 workgroups): the stop flag written by the finalize's scalar block
+    must not strand a late team member (the entry check ignores the flag of the current launch),
+    so the run ends without PPLS_E_HIP and matches the oracle."""
+    X, Y, th0 = make_problem(400, 3000, 300, 3, seed=5)
+    ctx.set_data(X, Y)
+    ctx.set_option("team_rows", 256)
+    try:
+        est, ll, eout, _ = ctx.em_run(_theta(th0), 500, 1.0, 0)
+    finally:
+        ctx.set_option("team_rows", 0)
+    ref = o.ppls_simult(X, Y, 3, EMsteps=500, atol=1.0, theta0=th0)
+    assert 3 <= len(ll) < 500 and len(ll) == len(ref["loglik"])
+    assert _relerr(ll, ref["loglik"]) < 1e-10
+    assert np.abs(est.W - ref["estimates"]["W"]).max() < 1e-8
