@@ -86,7 +86,9 @@ const char* ppls_last_error(const ppls_ctx* ctx);
  *       "dtype" (storage of X, Y: 0 fp64, 1 fp32; arithmetic stays fp64; set before loading data),
  *       "nt" (sweep loads with the non-temporal cache policy: -1 auto (default: when X, Y exceed
  *             the 256 MB MALL), 0 off, 1 on),
- *       "timing" (N > 0: record HIP events around every N-th sweep launch; 0 off) */
+ *       "timing" (N > 0: record HIP events around every N-th sweep launch; 0 off),
+ *       "balance" (split sweep row partition: 1 (default) calibrated per-XCD weights, measured once
+ *                  per data shape with 8 timed launches, from 2048 rows per workgroup; 0 the even split) */
 int ppls_set_option(ppls_ctx* ctx, const char* key, int64_t value);
 
 /* ---- multi-GPU: samples are sharded over ranks; one RCCL all-reduce per EM iteration ---- */
@@ -235,6 +237,10 @@ int ppls_gram(ppls_ctx* ctx, int xory, int nsplit, double* G, double* ms);
 /* ---- measurement ---------------------------------------------------------------------------- */
 /* Sum of HIP-event durations of the sweep kernel launches recorded since the last reset. */
 int ppls_sweep_timing(ppls_ctx* ctx, double* total_ms, int64_t* launches, int reset);
+/* The split sweep's calibrated row partition (option "balance"): the per-XCD-class weights w8[8]
+ * (1.0 before calibration) and up to cap of the grid + 1 row boundaries (*n_bounds = grid + 1, or 0
+ * while the even split is used). */
+int ppls_sweep_balance(ppls_ctx* ctx, double* w8, int64_t* bounds, int cap, int* n_bounds);
 /* The communicator as RCCL reports it (ncclCommCount / ncclCommUserRank; without RCCL the
  * context's own nranks/rank, i.e. 1/0 or the host reducer's) and the summed HIP-event durations of
  * the per-iteration statistics all-reduce on the timed sweeps (option "timing"; RCCL only). */

@@ -408,6 +408,17 @@ class Context:
         self._chk(self._L.ppls_sweep_timing(self.h, ct.byref(ms), ct.byref(n), int(reset)))
         return ms.value, n.value
 
+    def sweep_balance(self):
+        """(weights per XCD class g % 8, row boundaries per workgroup or None) of the split sweep's
+        calibrated row partition (option "balance")."""
+        w = np.ones(8)
+        cap = 4097
+        b = np.zeros(cap, dtype=np.int64)
+        nb = ct.c_int()
+        self._chk(self._L.ppls_sweep_balance(self.h, dptr(w), b.ctypes.data_as(ct.POINTER(ct.c_int64)), cap,
+                                             ct.byref(nb)))
+        return w, (b[: nb.value].copy() if nb.value else None)
+
     def comm_info(self, reset=True):
         """(nranks, rank) as RCCL's communicator reports them (ncclCommCount / ncclCommUserRank; the
         context's own values without RCCL) and (total ms, calls) of the timed all-reduces."""

@@ -81,6 +81,17 @@ struct ppls_ctx {
   unsigned* team_bar = nullptr;  // finalize polar teams (wide p): counters (self-resetting) + partials
   double* team_part = nullptr;
   long long* strace = nullptr;   // split sweep per-workgroup stamps (diagnostics, PPLS_STRACE_MAX_WG x 4)
+  // split-sweep load balance: the XCDs of one MI355X stream rows at rates that differ by up to ~3 %,
+  // the same way every iteration (profiles/r3_sweep_balance_*.txt), so the even row split leaves a
+  // tail.  The first full split sweep of the data is timed per workgroup (untimed calibration
+  // launches), workgroup g then owns a row block proportional to the measured rate of its class
+  // g % 8 (the XCD under round-robin dispatch); fixed afterwards, so results stay deterministic.
+  int balance = 1;                 // option "balance": 1 calibrate (default), 0 the even split
+  bool bal_done = false;           // calibrated for (bal_n, bal_grid)
+  int64_t bal_n = -1;
+  int bal_grid = -1;
+  double bal_w[8] = {1, 1, 1, 1, 1, 1, 1, 1};
+  int64_t* bal_bounds = nullptr;   // device: grid + 1 row boundaries
   double* coefs = nullptr;     // loglC_fast coefficient block (5r)
   double* scratch = nullptr;   // generic device scratch
   size_t scratch_bytes = 0;
@@ -376,6 +387,88 @@ int sweep_plan(ppls_ctx* c, int r, PplsSweepArgs* a) {
   return 4;
 }
 
+// Split-sweep row balance (see the context's bal_* fields).  For a full sweep of n_local rows on
+// `grid` workgroups, the first call runs PPLS_BAL_CAL calibration launches with per-workgroup
+// stamps (host syncs; their partials are overwritten by the real launch that follows): each times
+// when every workgroup's row loop ends under the current partition, and the rows of XCD class x
+// (g % 8) are rescaled by sqrt(mean end time / class end time) -- a damped fixed-point iteration
+// (the first launch only warms up), since a class that finishes early hands its HBM share to the
+// others, so the rates move with the partition.  Later calls reuse the boundaries, so results are
+// deterministic for the context.  Shapes with fewer than PPLS_BAL_MIN_ROWS rows per workgroup keep
+// the even split.
+#define PPLS_BAL_CAL 8
+#define PPLS_BAL_MIN_ROWS 2048   // C3: 3,906 rows per workgroup; at 488 (one GPU's C4 share) the calibration noise costs more than the tail
+namespace {
+void bal_bounds_of(const double* w, int grid, int64_t n, std::vector<int64_t>& bnd) {
+  bnd.assign((size_t)grid + 1, 0);
+  double tot = 0.0;
+  for (int g = 0; g < grid; ++g) tot += w[g % 8];
+  double cum = 0.0;
+  for (int g = 0; g < grid; ++g) {
+    cum += w[g % 8];
+    int64_t b = g + 1 == grid ? n : std::min<int64_t>(n, (int64_t)std::llround(cum / tot * (double)n));
+    bnd[(size_t)g + 1] = std::max(b, bnd[g]);
+  }
+}
+}  // namespace
+
+int balance_rows(ppls_ctx* c, PplsSweepArgs* a) {
+  const int grid = a->grid;
+  const int64_t n = a->n_local;
+  if (grid < 16 || grid > PPLS_STRACE_MAX_WG || n < (int64_t)PPLS_BAL_MIN_ROWS * grid) return PPLS_OK;
+  if (!(c->bal_done && c->bal_n == n && c->bal_grid == grid)) {
+    int rc;
+    const bool own = c->strace == nullptr;
+    if (own) HIPCHK(c, hipMalloc(&c->strace, (size_t)PPLS_STRACE_MAX_WG * 4 * sizeof(long long)));
+    if ((rc = dalloc(c, &c->bal_bounds, (size_t)grid + 1))) return rc;
+    PplsSweepArgs b = *a;
+    b.trace = c->strace;
+    b.row_bounds = c->bal_bounds;
+    b.stop = nullptr;
+    b.mu = nullptr;
+    b.write_mu = 0;
+    double w[8] = {1, 1, 1, 1, 1, 1, 1, 1};
+    std::vector<int64_t> bnd;
+    std::vector<long long> st((size_t)grid * 4);
+    for (int k = 0; k < PPLS_BAL_CAL; ++k) {
+      bal_bounds_of(w, grid, n, bnd);
+      HIPCHK(c, hipMemcpyAsync(c->bal_bounds, bnd.data(), sizeof(int64_t) * bnd.size(), hipMemcpyHostToDevice,
+                               c->stream));
+      HIPCHK(c, ppls_launch_sweep_split(&b, c->stream));
+      HIPCHK(c, hipMemcpyAsync(st.data(), c->strace, st.size() * sizeof(long long), hipMemcpyDeviceToHost, c->stream));
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+      long long t0 = st[0];
+      for (int g = 1; g < grid; ++g) t0 = std::min(t0, st[(size_t)g * 4]);
+      double cls[8] = {0}, cnt[8] = {0}, mean = 0.0;
+      for (int g = 0; g < grid; ++g) {
+        cls[g % 8] += (double)(st[(size_t)g * 4 + 2] - t0);   // this workgroup's row loop ends
+        cnt[g % 8] += 1.0;
+      }
+      bool ok = true;
+      for (int x = 0; x < 8; ++x) {
+        cls[x] = cnt[x] > 0 ? cls[x] / cnt[x] : 0.0;
+        ok = ok && cls[x] > 0.0;
+        mean += cls[x] / 8.0;
+      }
+      if (!ok) break;
+      if (k == 0) continue;   // the first launch warms caches and clocks; its times are not used
+      for (int x = 0; x < 8; ++x) w[x] *= std::sqrt(mean / cls[x]);   // damped: the rates move with the load
+      double wm = 0.0;
+      for (int x = 0; x < 8; ++x) wm += w[x] / 8.0;
+      for (int x = 0; x < 8; ++x) w[x] = std::min(1.1, std::max(0.9, w[x] / wm));   // a mis-measurement
+    }                                                                                 // cannot starve an XCD
+    if (own) { (void)hipFree(c->strace); c->strace = nullptr; }
+    for (int x = 0; x < 8; ++x) c->bal_w[x] = std::round(w[x] * 4096.0) / 4096.0;
+    bal_bounds_of(c->bal_w, grid, n, bnd);
+    HIPCHK(c, hipMemcpy(c->bal_bounds, bnd.data(), sizeof(int64_t) * bnd.size(), hipMemcpyHostToDevice));
+    c->bal_done = true;
+    c->bal_n = n;
+    c->bal_grid = grid;
+  }
+  a->row_bounds = c->bal_bounds;
+  return PPLS_OK;
+}
+
 // One sweep with theta[slot] -> c->stats (all-reduced).
 int sweep(ppls_ctx* c, int r, int slot, bool write_mu) {
   int rc;
@@ -430,8 +523,10 @@ int sweep(ppls_ctx* c, int r, int slot, bool write_mu) {
       ++c->ev_used;
       HIPCHK(c, hipEventRecord(e0, c->stream));
     }
-    if (plan == 3) HIPCHK(c, ppls_launch_sweep_split(&a, c->stream));
-    else if (plan == 4) HIPCHK(c, ppls_launch_sweep_panel(&a, c->dtype, c->Z, a.grid, c->stream));
+    if (plan == 3) {
+      if (c->balance && c->seg_rows < 0 && (rc = balance_rows(c, &a))) return rc;
+      HIPCHK(c, ppls_launch_sweep_split(&a, c->stream));
+    } else if (plan == 4) HIPCHK(c, ppls_launch_sweep_panel(&a, c->dtype, c->Z, a.grid, c->stream));
     else HIPCHK(c, ppls_launch_sweep_twopass(&a, c->Z, c->stream));
     if (timed) HIPCHK(c, hipEventRecord(e1, c->stream));
     HIPCHK(c, ppls_launch_reduce2(c->part, groups, c->part_ld, c->part_ld, c->stats,
@@ -694,6 +789,7 @@ void ppls_ctx_destroy(ppls_ctx* c) {
   if (c->ftrace) (void)hipFree(c->ftrace);
   if (c->strace) (void)hipFree(c->strace);
   dfree(c->stop_d);
+  dfree(c->bal_bounds);
   dfree(c->team_bar);
   dfree(c->team_part);
   if (c->stop_mirror) (void)hipHostFree(c->stop_mirror);
@@ -725,6 +821,8 @@ int ppls_set_option(ppls_ctx* c, const char* key, int64_t value) {
     c->team_rows = (int)value;
   } else if (!strcmp(key, "polar1")) {
     c->polar1 = value ? 1 : 0;
+  } else if (!strcmp(key, "balance")) {
+    c->balance = value ? 1 : 0;
   } else if (!strcmp(key, "polar1_kappa")) {
     if (value < 0 || value > 255) return fail(c, PPLS_E_ARG, "polar1_kappa must be in [0, 255]");
     c->polar1_kappa = (int)value;
@@ -2135,6 +2233,17 @@ int ppls_sweep_timing(ppls_ctx* c, double* total_ms, int64_t* launches, int rese
   if (total_ms) *total_ms = c->timed_ms;
   if (launches) *launches = c->timed_launches;
   if (reset) { c->timed_ms = 0.0; c->timed_launches = 0; }
+  return PPLS_OK;
+}
+
+int ppls_sweep_balance(ppls_ctx* c, double* w8, int64_t* bounds, int cap, int* n_bounds) {
+  if (!c) return PPLS_E_ARG;
+  if (w8)
+    for (int x = 0; x < 8; ++x) w8[x] = c->bal_done ? c->bal_w[x] : 1.0;
+  const int nb = c->bal_done ? c->bal_grid + 1 : 0;
+  if (n_bounds) *n_bounds = nb;
+  if (bounds && cap > 0 && nb > 0)
+    HIPCHK(c, hipMemcpy(bounds, c->bal_bounds, sizeof(int64_t) * (size_t)std::min(cap, nb), hipMemcpyDeviceToHost));
   return PPLS_OK;
 }
 

@@ -33,6 +33,8 @@ struct PplsSweepArgs {
   int dots_grid;         // panel dots workgroups (0 = one per 128-row group, capped)
   const int* stop;       // device stop flag (em_run's convergence test) or nullptr: kernels exit if set
   long long* trace;      // split sweep diagnostics: 4 wall-clock stamps per workgroup, or nullptr
+  const int64_t* row_bounds;   // split sweep: grid + 1 row boundaries (workgroup g owns rows
+                               // [b[g], b[g+1])), or nullptr for the even split
 };
 
 struct PplsFinalizeArgs {

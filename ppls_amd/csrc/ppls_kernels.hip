@@ -310,7 +310,7 @@ __global__ __launch_bounds__(NT, 2 * NT / 512) void ppls_sweep_split_kernel(
     const double* __restrict__ X, const double* __restrict__ Y, int64_t n_local, int ldx, int ldy,
     const double* __restrict__ Wp, const double* __restrict__ Cp, const PplsScalars* __restrict__ sc,
     double* __restrict__ part, int64_t part_ld, double* __restrict__ mu, int write_mu, int ablate,
-    const int* __restrict__ stop, long long* __restrict__ trace) {
+    const int* __restrict__ stop, long long* __restrict__ trace, const int64_t* __restrict__ row_bounds) {
   if (stop && *stop) return;   // em_run converged earlier (device stop flag)
   static_assert(SLOTS >= 2 * RP, "ring must hold the group being read and the group in flight");
   // diagnostics (set_option "strace"): per workgroup wall-clock stamps at entry, after the ring
@@ -335,7 +335,9 @@ __global__ __launch_bounds__(NT, 2 * NT / 512) void ppls_sweep_split_kernel(
   double* bc = red + 2 * NWAVES * V + wave * (2 * V);                 // per wave: [Xw Yc] rows
   double* cf = red + 2 * NWAVES * V + NWAVES * 2 * V;                 // alpha | beta | gamma | delta
   const int64_t g = blockIdx.x, G = gridDim.x;
-  const int64_t rb = n_local * g / G, re = n_local * (g + 1) / G;
+  // contiguous row block: the even split, or the calibrated per-XCD-weighted one (ppls_capi.cpp)
+  const int64_t rb = row_bounds ? row_bounds[g] : n_local * g / G;
+  const int64_t re = row_bounds ? row_bounds[g + 1] : n_local * (g + 1) / G;
   const int nrows = (int)(re - rb);
   const int ngroups = (nrows + RP - 1) / RP;
   const int np = isx ? (ldx >> 1) : (ldy >> 1);
@@ -2336,7 +2338,7 @@ hipError_t launch_split_t(const PplsSweepArgs& a, hipStream_t st) {
   }
   hipLaunchKernelGGL(kern, dim3(a.grid), dim3(512), split_lds(R, a.ldx, a.ldy, 512, RP), st, a.X, a.Y,
                      a.n_local, a.ldx, a.ldy, a.Wp, a.Cp, a.sc, a.part, a.part_ld, a.mu, a.write_mu,
-                     a.ablate, a.stop, a.trace);
+                     a.ablate, a.stop, a.trace, a.row_bounds);
   return hipGetLastError();
 }
 

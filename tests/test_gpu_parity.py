@@ -373,3 +373,35 @@ def test_team_finalize_with_early_stop(ctx):
     assert 3 <= len(ll) < 500 and len(ll) == len(ref["loglik"])
     assert _relerr(ll, ref["loglik"]) < 1e-10
     assert np.abs(est.W - ref["estimates"]["W"]).max() < 1e-8
+
+
+def test_split_sweep_balanced_partition():
+    """The split sweep's calibrated row partition (option balance, default on from 2048 rows per
+    workgroup): boundaries cover every row once, per-XCD-class weights stay within +-10 %, and the
+    fit equals the even split's to rounding (the row sums are only regrouped).  C3's column shape
+    (one 512-thread workgroup per CU) on 600,000 generated rows."""
+    from ppls_amd import Context, Theta
+    n, p, q, r = 600_000, 2000, 2000, 5
+    rng = np.random.default_rng(0)
+    W = np.linalg.qr(rng.standard_normal((p, r)))[0]
+    C = np.linalg.qr(rng.standard_normal((q, r)))[0]
+    truth = Theta(W, C, np.linspace(1.5, 0.8, r), 0.5, 0.5, 0.1, np.linspace(1.0, 0.7, r))
+    th0 = Theta(np.linalg.qr(rng.standard_normal((p, r)))[0], np.linalg.qr(rng.standard_normal((q, r)))[0],
+                np.ones(r), 1.0, 1.0, 1.0, np.ones(r))
+    out = {}
+    for bal in (1, 0):
+        with Context(0) as c:
+            c.set_option("balance", bal)
+            c.generate_synthetic(n, p, q, truth, seed=7)
+            est, ll, _, _ = c.em_run(th0, 4, -np.inf, 0, want_eout=False)
+            out[bal] = (est, ll, c.sweep_balance(), c.sweep_info(r)["grid"])
+    w, b = out[1][2]
+    grid = out[1][3]
+    assert b is not None and len(b) == grid + 1 and b[0] == 0 and b[-1] == n
+    assert np.all(np.diff(b) >= 0) and np.all((w >= 0.9) & (w <= 1.1))
+    rows = np.diff(b).astype(float)
+    for x in range(8):   # rows per workgroup follow the weight of its class
+        assert np.abs(rows[x::8].mean() / rows.mean() - w[x] / w[np.arange(grid) % 8].mean()) < 0.02
+    assert out[0][2][1] is None   # balance 0: the even split
+    assert _relerr(out[1][1], out[0][1]) < 1e-13
+    assert np.abs(out[1][0].W - out[0][0].W).max() < 1e-12

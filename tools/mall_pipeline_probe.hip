@@ -66,6 +66,12 @@ __global__ __launch_bounds__(256) void stream_kernel(const char* X, long n, long
   sink(r0 < r1 ? read_rows(X, ldb, r0, r1, nt != 0) : 0.0, out);
 }
 
+__global__ __launch_bounds__(256) void tile_kernel(const char* X, long n, long ldb, double* out) {
+  const long per = (n + gridDim.y - 1) / gridDim.y;
+  const long r0 = blockIdx.y * per, r1 = r0 + per < n ? r0 + per : n;
+  sink(r0 < r1 ? read_tile(X, ldb, blockIdx.x, r0, r1) : 0.0, out);
+}
+
 __device__ bool wait_ge(unsigned* ctr, unsigned target, int* err) {
   long spins = 0;
   while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
@@ -146,14 +152,55 @@ int main(int argc, char** argv) {
     printf("stream %s: one pass %.3f ms (%.0f GB/s); two passes %.3f ms\n", nt ? "nt" : "default", t1,
            bytes / (t1 * 1e-3) * 1e-9, t2);
   }
+  // chunk-level A/B with separate launches: per chunk of S rows, read it (first touch) and read it
+  // again right away (second touch), each launch timed by its own events
+  {
+    std::vector<hipEvent_t> ev(3);
+    for (auto& e : ev) (void)hipEventCreate(&e);
+    for (long S : {1536L, 3072L, 6144L}) {
+      for (int pat = 0; pat < 2; ++pat) {
+        const int K = (int)((n + S - 1) / S);
+        (void)hipMemset(flush, 1, 512L << 20);
+        (void)hipDeviceSynchronize();
+        double t_first = 0, t_second = 0;
+        hipEvent_t a0, a1;
+        (void)hipEventCreate(&a0); (void)hipEventCreate(&a1);
+        (void)hipEventRecord(a0);
+        for (int c = 0; c < K; ++c) {
+          const long r0 = (long)c * S, rows = r0 + S < n ? S : n - r0;
+          const char* Xc = X + r0 * ldb;
+          (void)hipEventRecord(ev[0]);
+          hipLaunchKernelGGL(stream_kernel, dim3(1024), dim3(256), 0, 0, Xc, rows, ldb, out, 0);
+          (void)hipEventRecord(ev[1]);
+          if (pat == 0)
+            hipLaunchKernelGGL(stream_kernel, dim3(1024), dim3(256), 0, 0, Xc, rows, ldb, out, 0);
+          else   // the accumulation pattern: 10 tiles x 96 row sub-ranges
+            hipLaunchKernelGGL(tile_kernel, dim3(10, 96), dim3(256), 0, 0, Xc, rows, ldb, out);
+          (void)hipEventRecord(ev[2]);
+          (void)hipEventSynchronize(ev[2]);
+          float m1, m2;
+          (void)hipEventElapsedTime(&m1, ev[0], ev[1]);
+          (void)hipEventElapsedTime(&m2, ev[1], ev[2]);
+          if (c > 0) { t_first += m1; t_second += m2; }
+        }
+        (void)hipEventRecord(a1);
+        (void)hipEventSynchronize(a1);
+        const double b = (double)(K - 1) * S * ldb;
+        printf("chunked launches S=%5ld rows (%.0f MB), second touch %s: first %.0f GB/s, second %.0f GB/s "
+               "(sum over chunks 2..K, per-launch events)\n", S, S * ldb * 1e-6,
+               pat ? "accumulation pattern" : "same stream pattern", b / (t_first * 1e-3) * 1e-9,
+               b / (t_second * 1e-3) * 1e-9);
+      }
+    }
+  }
   const int K_MAX = 4096;
   (void)hipMalloc(&ctr, 2 * K_MAX * sizeof(unsigned));
   (void)hipMalloc(&err, sizeof(int));
-  for (long S : {768L, 1536L, 3072L}) {
+  for (long S : {3072L}) {
     const int K = (int)((n + S - 1) / S);
     if (K > K_MAX) continue;
     for (int L : {1, 2, 3}) {
-      for (int NA : {256, 512}) {
+      for (int NA : {256}) {
         const int J = 48;   // second-touch workgroups: 10 tiles x 48 sub-ranges
         const int NB = (int)(ldb / 4096) * J;
         const float t = time_it([&] {
