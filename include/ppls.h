@@ -82,6 +82,8 @@ const char* ppls_last_error(const ppls_ctx* ctx);
  *       "polar1" (finalize polar factor: 1 (default) one Cholesky-QR pass when
  *                 ||R1||_F ||R1^-1||_F <= k (R1 = chol(S'S)), else Cholesky-QR2; 0 always Cholesky-QR2),
  *       "polar1_kappa" (that bound k: 0 = the default min(8 r, 40); up to 255),
+ *       "exact_gram" (finalize: 1 (default) the Gram W'W, C'C of the new loadings exactly, 0 the
+ *                     identity -- faster, less accurate at small sigma_E),
  *       "team_rows" (finalize polar factor: rows of S per workgroup of a team; 0 = default 2048),
  *       "dtype" (storage of X, Y: 0 fp64, 1 fp32; arithmetic stays fp64; set before loading data),
  *       "nt" (sweep loads with the non-temporal cache policy: -1 auto (default: when X, Y exceed

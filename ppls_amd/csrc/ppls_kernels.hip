@@ -1356,6 +1356,7 @@ __device__ int ppls_jacobi_wave(double* sA, double* sV) {
   for (int sweep = 0; sweep < 60; ++sweep) {
     ++sweeps;
     bool rot_any = false;
+    double cmax = 0.0;   // largest cos^2 between rotated column pairs this sweep (g^2 / (a b))
 #pragma unroll
     for (int m = 0; m < N - 1; ++m) {
       const int k = lane >> 3;
@@ -1378,6 +1379,7 @@ __device__ int ppls_jacobi_wave(double* sA, double* sV) {
       }
       const double a = ppls_group8_sum(aa), b = ppls_group8_sum(bb), g = ppls_group8_sum(gg);
       const bool rot = act && (g * g >= 1e-30 * (a * b)) && g != 0.0;
+      if (rot) cmax = fmax(cmax, g * g / (a * b));
       const double z = (b - a) * ppls_rcp(rot ? 2.0 * g : 1.0);
       const double z2 = fma(z, z, 1.0);
       const double uu = fabs(z) + z2 * ppls_rsq(z2);
@@ -1396,6 +1398,9 @@ __device__ int ppls_jacobi_wave(double* sA, double* sV) {
       ppls_wave_lds_fence();
     }
     if (!__any(rot_any)) break;
+    // Jacobi converges quadratically: after a sweep whose largest cosine was <= 1e-8 the remaining
+    // ones are ~1e-16, so the sweep that would only confirm it is skipped
+    if (!__any(cmax > 1e-16)) break;
   }
   return sweeps;
 }
@@ -2007,6 +2012,12 @@ __global__ __launch_bounds__(PPLS_FIN_THREADS) void ppls_finalize_kernel(
     const int ld = isx ? ldx : ldy, rows = isx ? p : q;
     double* out = isx ? Wn : Cn;
     double* gout = gram_nxt ? gram_nxt + (isx ? 0 : R * R) : nullptr;
+    // W'W of the new loadings (the next scalar update's Gram), computed exactly (mode bit 16, the
+    // default) or taken as I (they are orthonormal to O(eps kappa^2) <= 1e-13, and a team's pass 3
+    // then needs no last-member exchange; but Cee = (||X||^2 - 2 s tr + s^2 tr(Z'Z G)) / (N p)
+    // cancels at small sigma_E and amplifies the difference: option exact_gram).
+    const bool exact_gram = (mode & 16) != 0;
+    double* gacc = exact_gram ? gout : nullptr;
     double* w2 = work + (isx ? 0 : 2 * (int64_t)p * R);
     double* vs = vstate ? vstate + (isx ? 0 : R * R) : nullptr;
     PplsTeam tm;
@@ -2017,15 +2028,17 @@ __global__ __launch_bounds__(PPLS_FIN_THREADS) void ppls_finalize_kernel(
     tm.status = status;
     tm.tr = tr;
     if (qr || !ppls_block_polar_fast<R, NT>(S, ld, rows, out, ld, ld, stage_lds ? dyn_lds : nullptr, sh,
-                                            sm, gout, vs, tr, tm, (mode & 4) != 0,
+                                            sm, gacc, vs, tr, tm, (mode & 4) != 0,
                                             (double)((mode >> 8) & 255))) {
       if (tm.rank != 0) return;   // the Householder fallback runs on one block
       ppls_block_polar(S, ld, rows, R, out, ld, ld, w2, w2 + (int64_t)rows * R, status, qr);
-      if (gout) {
+      if (gacc) {
         __syncthreads();
-        ppls_block_gram_of<R, NT>(out, ld, rows, sh, gout);
+        ppls_block_gram_of<R, NT>(out, ld, rows, sh, gacc);
       }
     }
+    if (gout && !exact_gram && tm.rank == 0)
+      for (int e = tid; e < R * R; e += NT) gout[e] = (e % (R + 1) == 0) ? 1.0 : 0.0;
     ppls_stamp(tr, 5);
     if (tr && tid == 0) tr[12] = (long long)clock64();
     return;
