@@ -23,6 +23,8 @@ FILE_FLAGS = {"ppls_kernels.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"]}
 HEADERS = ["ppls_kernels.h", "ppls_math.h", "ppls_device.h"]
 CFLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function", "-Wno-inline-asm",
           "-I" + os.path.join(ROOT, "include"), "-I" + CSRC]
+# experiment builds only (e.g. tools/dots_ablate.sh: -DPPLS_DOTS_ABLATE=n into a copied tree)
+CFLAGS += [f for f in os.environ.get("PPLS_EXTRA_CFLAGS", "").split() if f]
 
 
 def _mtime(p):

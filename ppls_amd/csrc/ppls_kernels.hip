@@ -724,6 +724,19 @@ __global__ __launch_bounds__(256) void ppls_panel_mfmadots_kernel(
     double* __restrict__ Z, double* __restrict__ mu,
     const int* __restrict__ stop) {
   if (stop && *stop) return;   // em_run converged earlier (device stop flag)
+  // compile-time timing ablations for experiment builds (tools/dots_ablate.sh; results invalid):
+  // PPLS_DOTS_ABLATE bit 0 no MFMAs, bit 1 no X loads, bit 2 no B loads.  Runtime flags here
+  // changed the production code generation (549 -> 673 us at the C5 share).  Round 3 at the C5
+  // share: every variant ran 574-591 us (profiles/r3_dots_ablate_c5s.txt) -- the per-tile LDS
+  // transpose and its waits bound the kernel, not the MFMAs or either load stream; yet loading the
+  // MFMA operands straight from global memory (16 rows x 16 B per load instruction, no LDS) was
+  // slower still, 616 vs 560 us and 4.53 vs 3.92 ms at C5 (profiles/r3_dots_direct_ab.txt): the
+  // 16-row scatter costs more in the vector-memory pipeline than the transpose does in LDS.
+#ifndef PPLS_DOTS_ABLATE
+#define PPLS_DOTS_ABLATE 0
+#endif
+  constexpr bool ab_mfma = (PPLS_DOTS_ABLATE & 1) != 0, ab_x = (PPLS_DOTS_ABLATE & 2) != 0,
+                 ab_b = (PPLS_DOTS_ABLATE & 4) != 0;
   typedef double d4 __attribute__((ext_vector_type(4)));
   typedef float f4 __attribute__((ext_vector_type(4)));
   constexpr int ES = (int)sizeof(T);
@@ -768,6 +781,7 @@ __global__ __launch_bounds__(256) void ppls_panel_mfmadots_kernel(
       f4 xa[NL];
       auto ld4 = [&](const T* p) -> f4 { return *(const f4*)p; };   // (non-temporal: 16 % slower here)
       auto load_tile = [&](int tc, f4 (&b)[NL]) {
+        if constexpr (ab_x) return;
         const int c = tc < ntc ? tc : ntc - 1;
 #pragma unroll
         for (int u = 0; u < NL; ++u) b[u] = ld4(src[u] + c * KT);
@@ -782,11 +796,16 @@ __global__ __launch_bounds__(256) void ppls_panel_mfmadots_kernel(
         asm volatile("" ::: "memory");   // keep the loads below after the stores (buf is reused)
         double bw[KQ];
         const double* wb = wb0 + (int64_t)tc * KT * 16;
+        if constexpr (ab_b) {
 #pragma unroll
-        for (int s2 = 0; s2 < KQ; s2 += 2) {
-          const double2 w2 = *(const double2*)(wb + s2 * 16);
-          bw[s2] = w2.x;
-          bw[s2 + 1] = w2.y;
+          for (int s2 = 0; s2 < KQ; ++s2) bw[s2] = 1e-3 * s2;
+        } else {
+#pragma unroll
+          for (int s2 = 0; s2 < KQ; s2 += 2) {
+            const double2 w2 = *(const double2*)(wb + s2 * 16);
+            bw[s2] = w2.x;
+            bw[s2 + 1] = w2.y;
+          }
         }
         asm volatile("" ::: "memory");   // B before the next tiles' X in the vmcnt order
         load_tile(tc + 1, b);
@@ -802,9 +821,14 @@ __global__ __launch_bounds__(256) void ppls_panel_mfmadots_kernel(
 #pragma unroll
             for (int u = 0; u < 16 / ES; ++u) a[h * (16 / ES) + u] = pv[u];
           }
+          if constexpr (ab_mfma) {
 #pragma unroll
-          for (int s2 = 0; s2 < KQ; ++s2)
-            acc[bk] = __builtin_amdgcn_mfma_f64_16x16x4f64((double)a[s2], bw[s2], acc[bk], 0, 0, 0);
+            for (int s2 = 0; s2 < KQ; ++s2) acc[bk].x += (double)a[s2] * bw[s2];
+          } else {
+#pragma unroll
+            for (int s2 = 0; s2 < KQ; ++s2)
+              acc[bk] = __builtin_amdgcn_mfma_f64_16x16x4f64((double)a[s2], bw[s2], acc[bk], 0, 0, 0);
+          }
         }
       };
       load_tile(0, xa);

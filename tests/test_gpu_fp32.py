@@ -109,3 +109,4 @@ def test_row_padding_is_invisible(dtype, p, q):
     assert np.array_equal(o0.W, o1.W) and np.array_equal(o0.C, o1.C)
     assert _relerr(l1, l0) < 1e-14
     assert np.abs(e0.W - e1.W).max() < 1e-14 and np.abs(e0.C - e1.C).max() < 1e-14
+

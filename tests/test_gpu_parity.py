@@ -405,3 +405,25 @@ def test_split_sweep_balanced_partition():
     assert out[0][2][1] is None   # balance 0: the even split
     assert _relerr(out[1][1], out[0][1]) < 1e-13
     assert np.abs(out[1][0].W - out[0][0].W).max() < 1e-12
+
+
+@pytest.mark.parametrize("sweep", [dict(), dict(sweep=3)], ids=["auto", "panel"])
+@pytest.mark.parametrize("n,p,q,r", [(200, 3, 3, 3), (40, 2, 9, 2), (25, 300, 150, 3), (1, 5, 4, 1),
+                                     (2, 6, 5, 2), (500, 1, 1, 1), (64, 257, 3, 3)],
+                         ids=["r_eq_p_eq_q", "p_eq_r", "n_lt_p", "one_row", "two_rows", "p_q_1", "ragged"])
+def test_edge_shapes_vs_oracle(ctx, sweep, n, p, q, r):
+    """Edge shapes the reference accepts (ncol >= nr_comp, EM_W_multi.R:245): square loadings
+    (r = p = q), r = p < q, fewer rows than columns, one and two rows, p = q = 1, ragged widths;
+    5 EM iterations through em_run against the oracle.  (One- and two-row fits are ill-posed and
+    amplify rounding, hence their looser loading tolerance.)"""
+    X, Y, th0 = make_problem(n, p, q, r, seed=n + p)
+    _apply(ctx, sweep)
+    ctx.set_data(X, Y)
+    est, ll, eout, _ = ctx.em_run(_theta(th0), 5, -np.inf, 0)
+    ref = o.ppls_simult(X, Y, r, EMsteps=5, atol=-np.inf, theta0=th0)
+    tol = 1e-8 if n >= 25 else 1e-6
+    assert _relerr(ll, ref["loglik"]) < 1e-10
+    assert np.abs(est.W - ref["estimates"]["W"]).max() < tol
+    assert np.abs(est.C - ref["estimates"]["C"]).max() < tol
+    assert _relerr([est.sigE, est.sigF, est.sigH], [ref["estimates"][k] for k in ("sigE", "sigF", "sigH")]) < tol
+    assert _relerr(eout.mu_T, ref["Expectations"]["mu_T"]) < tol
