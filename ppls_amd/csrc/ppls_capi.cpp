@@ -512,6 +512,8 @@ int sweep(ppls_ctx* c, int r, int slot, bool write_mu) {
     a.ablate = c->ablate | (nt ? 16 : 0);
     a.stop = c->sweep_stop;
     a.trace = (plan == 3 && a.grid <= PPLS_STRACE_MAX_WG) ? c->strace : nullptr;
+    // the row partition (its one-time calibration launches stay outside the timed events)
+    if (plan == 3 && c->balance && c->seg_rows < 0 && (rc = balance_rows(c, &a))) return rc;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     const bool timed = c->timing > 0 && (c->sweep_count++ % c->timing) == 0;
     if (timed) {
@@ -526,10 +528,8 @@ int sweep(ppls_ctx* c, int r, int slot, bool write_mu) {
       ++c->ev_used;
       HIPCHK(c, hipEventRecord(e0, c->stream));
     }
-    if (plan == 3) {
-      if (c->balance && c->seg_rows < 0 && (rc = balance_rows(c, &a))) return rc;
-      HIPCHK(c, ppls_launch_sweep_split(&a, c->stream));
-    } else if (plan == 4) HIPCHK(c, ppls_launch_sweep_panel(&a, c->dtype, c->Z, a.grid, c->stream));
+    if (plan == 3) HIPCHK(c, ppls_launch_sweep_split(&a, c->stream));
+    else if (plan == 4) HIPCHK(c, ppls_launch_sweep_panel(&a, c->dtype, c->Z, a.grid, c->stream));
     else HIPCHK(c, ppls_launch_sweep_twopass(&a, c->Z, c->stream));
     if (timed) HIPCHK(c, hipEventRecord(e1, c->stream));
     HIPCHK(c, ppls_launch_reduce2(c->part, groups, c->part_ld, c->part_ld, c->stats,
@@ -2015,13 +2015,15 @@ int ppls_variances(ppls_ctx* c, const double* mu, const double* Cdiag, double si
     if (rocblas_create_handle(&c->blas) != rocblas_status_success) return done(fail(c, PPLS_E_HIP, "rocblas_create_handle failed"));
   }
   if (rocblas_set_stream(c->blas, c->stream) != rocblas_status_success) return done(fail(c, PPLS_E_HIP, "rocblas_set_stream failed"));
-  VRC(dalloc(c, &dM, pp));
+  // all a matrices at once: one strided-batched LU and inverse (rocSOLVER's panel factorisation is
+  // thousands of small launches per matrix; batching shares them -- profiles/r3_variances_*.txt)
+  VRC(dalloc(c, &dM, pp * (size_t)a));
   VRC(dalloc(c, &dv, (size_t)2 * p));
   VRC(dalloc(c, &dse, (size_t)p));
   if (SSt_exp) VRC(dalloc(c, &dexp, pp));
   if (SSt_star) VRC(dalloc(c, &dstar, pp));
-  VCHK(hipMalloc((void**)&ipiv, sizeof(rocblas_int) * p));
-  VCHK(hipMalloc((void**)&info, sizeof(rocblas_int)));
+  VCHK(hipMalloc((void**)&ipiv, sizeof(rocblas_int) * p * a));
+  VCHK(hipMalloc((void**)&info, sizeof(rocblas_int) * a));
   const double s2 = sigE * sigE, s4 = s2 * s2;
   std::vector<double> v2((size_t)2 * p);
   for (int i = 0; i < a; ++i) {
@@ -2036,21 +2038,28 @@ int ppls_variances(ppls_ctx* c, const double* mu, const double* Cdiag, double si
       v2[(size_t)p + e] = W[(size_t)i * p + e];
     }
     VCHK(hipMemcpyAsync(dv, v2.data(), sizeof(double) * 2 * p, hipMemcpyHostToDevice, c->stream));
-    VCHK(ppls_launch_varmat(dG, dv, dv + p, p, ctt, k1, k2, bstar, s4, N, dM, dexp, dstar, c->stream));
+    VCHK(ppls_launch_varmat(dG, dv, dv + p, p, ctt, k1, k2, bstar, s4, N, dM + pp * i, dexp, dstar, c->stream));
     if (SSt_exp) VCHK(hipMemcpyAsync(SSt_exp + (size_t)i * pp, dexp, sizeof(double) * pp, hipMemcpyDeviceToHost, c->stream));
     if (SSt_star) VCHK(hipMemcpyAsync(SSt_star + (size_t)i * pp, dstar, sizeof(double) * pp, hipMemcpyDeviceToHost, c->stream));
-    if (rocsolver_dgetrf(c->blas, p, p, dM, p, ipiv, info) != rocblas_status_success ||
-        rocsolver_dgetri(c->blas, p, dM, p, ipiv, info) != rocblas_status_success)
-      return done(fail(c, PPLS_E_HIP, "rocsolver getrf/getri failed"));
-    rocblas_int inf = 0;
-    VCHK(hipMemcpyAsync(&inf, info, sizeof inf, hipMemcpyDeviceToHost, c->stream));
-    VCHK(hipStreamSynchronize(c->stream));
-    if (inf != 0)   // solve(): "Lapack routine dgesv: system is exactly singular"
+    VCHK(hipStreamSynchronize(c->stream));   // dv is reused by the next component
+  }
+  if (rocsolver_dgetrf_strided_batched(c->blas, p, p, dM, p, (rocblas_stride)pp, ipiv, p, info, a) !=
+          rocblas_status_success ||
+      rocsolver_dgetri_strided_batched(c->blas, p, dM, p, (rocblas_stride)pp, ipiv, p, info, a) !=
+          rocblas_status_success)
+    return done(fail(c, PPLS_E_HIP, "rocsolver getrf/getri (strided batched) failed"));
+  std::vector<rocblas_int> inf(a, 0);
+  VCHK(hipMemcpyAsync(inf.data(), info, sizeof(rocblas_int) * a, hipMemcpyDeviceToHost, c->stream));
+  VCHK(hipStreamSynchronize(c->stream));
+  for (int i = 0; i < a; ++i)
+    if (inf[i] != 0)   // solve(): "Lapack routine dgesv: system is exactly singular"
       return done(fail(c, PPLS_E_NUMERIC, "component %d: B_exp - SSt_exp is exactly singular (U[%d,%d] = 0)", i + 1,
-                       (int)inf, (int)inf));
-    VCHK(ppls_launch_negdiag(dM, p, dse, c->stream));
-    if (varMatrix) VCHK(hipMemcpyAsync(varMatrix + (size_t)i * pp, dM, sizeof(double) * pp, hipMemcpyDeviceToHost, c->stream));
+                       (int)inf[i], (int)inf[i]));
+  for (int i = 0; i < a; ++i) {
+    VCHK(ppls_launch_negdiag(dM + pp * i, p, dse, c->stream));
+    if (varMatrix) VCHK(hipMemcpyAsync(varMatrix + (size_t)i * pp, dM + pp * i, sizeof(double) * pp, hipMemcpyDeviceToHost, c->stream));
     VCHK(hipMemcpyAsync(seLoad + (size_t)i * p, dse, sizeof(double) * p, hipMemcpyDeviceToHost, c->stream));
+    VCHK(hipStreamSynchronize(c->stream));   // dse is reused by the next component
   }
   VCHK(hipStreamSynchronize(c->stream));
 #undef VCHK
