@@ -421,8 +421,14 @@ int balance_rows(ppls_ctx* c, PplsSweepArgs* a) {
   if (grid < 16 || grid > PPLS_STRACE_MAX_WG || n < (int64_t)PPLS_BAL_MIN_ROWS * grid) return PPLS_OK;
   if (!(c->bal_done && c->bal_n == n && c->bal_grid == grid)) {
     int rc;
-    const bool own = c->strace == nullptr;
-    if (own) HIPCHK(c, hipMalloc(&c->strace, (size_t)PPLS_STRACE_MAX_WG * 4 * sizeof(long long)));
+    struct OwnTrace {   // a stamp buffer of our own unless tracing is on; freed on every exit path
+      ppls_ctx* c;
+      bool own;
+      ~OwnTrace() {
+        if (own && c->strace) { (void)hipFree(c->strace); c->strace = nullptr; }
+      }
+    } tg{c, c->strace == nullptr};
+    if (tg.own) HIPCHK(c, hipMalloc(&c->strace, (size_t)PPLS_STRACE_MAX_WG * 4 * sizeof(long long)));
     if ((rc = dalloc(c, &c->bal_bounds, (size_t)grid + 1))) return rc;
     PplsSweepArgs b = *a;
     b.trace = c->strace;
@@ -460,7 +466,6 @@ int balance_rows(ppls_ctx* c, PplsSweepArgs* a) {
       for (int x = 0; x < 8; ++x) wm += w[x] / 8.0;
       for (int x = 0; x < 8; ++x) w[x] = std::min(1.1, std::max(0.9, w[x] / wm));   // a mis-measurement
     }                                                                                 // cannot starve an XCD
-    if (own) { (void)hipFree(c->strace); c->strace = nullptr; }
     for (int x = 0; x < 8; ++x) c->bal_w[x] = std::round(w[x] * 4096.0) / 4096.0;
     bal_bounds_of(c->bal_w, grid, n, bnd);
     HIPCHK(c, hipMemcpy(c->bal_bounds, bnd.data(), sizeof(int64_t) * bnd.size(), hipMemcpyHostToDevice));
