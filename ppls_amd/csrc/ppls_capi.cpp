@@ -369,6 +369,7 @@ int sweep_plan(ppls_ctx* c, int r, PplsSweepArgs* a) {
   a->q = c->q;
   a->r = r;
   a->threads = 512;
+  a->num_cus = c->num_cus;
   if (c->sweep_mode == 2) {
     a->grid = grid_of(c);
     return 2;
@@ -2315,9 +2316,12 @@ int ppls_sweep_kernel(ppls_ctx* c, int r, char* buf, int len) {
   if (plan == 3) {
     if (ppls_split_describe(&a, k, sizeof k) != 0) return fail(c, PPLS_E_STATE, "no split instantiation for r=%d", r);
   } else if (plan == 4) {
-    const bool rows64 = (sweep_rows(c) >= 32768) != ((c->ablate & 4096) != 0);   // ppls_kernels.hip launch_panel_t
-    snprintf(k, sizeof k, "panel<%s,%d> (mfmadots %d rows/wave + acc, %d chunks)", c->dtype ? "float" : "double", r,
-             rows64 ? 64 : 32, a.grid);
+    // as ppls_kernels.hip launch_panel_t picks them
+    const bool rows64 = (sweep_rows(c) >= 32768) != ((c->ablate & 4096) != 0);
+    const int64_t wtiles = (sweep_rows(c) + (rows64 ? 63 : 31)) / (rows64 ? 64 : 32);
+    const bool pair = (wtiles < (int64_t)c->num_cus * 4 * (rows64 ? 2 : 3)) != ((c->ablate & 2048) != 0);
+    snprintf(k, sizeof k, "panel<%s,%d> (mfmadots %d rows/%s + acc, %d chunks)", c->dtype ? "float" : "double", r,
+             rows64 ? 64 : 32, pair ? "wave pair" : "wave", a.grid);
   } else {
     snprintf(k, sizeof k, "twopass (dots + acc, %d chunks)", a.grid);
   }

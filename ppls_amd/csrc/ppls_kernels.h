@@ -30,7 +30,8 @@ struct PplsSweepArgs {
   int* occ_out;          // split kernel: if set, report resident WGs per CU instead of launching
   int grid;              // workgroups (split) / row chunks (two-pass, panel accumulation)
   int ablate;            // timing experiments only (split): 1 no compute, 2 no HBM copies; 16 = nt loads
-  int dots_grid;         // panel dots workgroups (0 = one per 128-row group, capped)
+  int dots_grid;         // panel dots workgroups (0 = enough for every row tile, capped)
+  int num_cus;           // compute units of the device (panel dots: wave pairs on small shards)
   const int* stop;       // device stop flag (em_run's convergence test) or nullptr: kernels exit if set
   long long* trace;      // split sweep diagnostics: 4 wall-clock stamps per workgroup, or nullptr
   const int64_t* row_bounds;   // split sweep: grid + 1 row boundaries (workgroup g owns rows

@@ -716,10 +716,13 @@ __device__ __forceinline__ PplsVec16<T> ppls_load16(const T* p) {
 // operand (lane l: W[that column][l & 15]) is a plain per-lane load of the transposed, zero-padded
 // W.  The next tile's global loads are in flight during the MFMAs.  Result lane map (f64 MFMA):
 // row (l >> 4) + 4 reg, component l & 15 -- the same for the X and the Y product, so mu_T/mu_U are
-// formed in registers.
-template <typename T, int R, int NB>
+// formed in registers.  KS = 2 splits each row tile's columns over a wave pair of the workgroup
+// (the second half's dot sums are added to the first's through LDS, in that fixed order): for
+// shards with fewer row tiles than resident wave slots (C5's 8-GPU share: 977 tiles of 64 rows for
+// 2,048 slots), which would otherwise run one wave per SIMD.
+template <typename T, int R, int NB, int KS>
 __global__ __launch_bounds__(256) void ppls_panel_mfmadots_kernel(
-    const T* __restrict__ X, const T* __restrict__ Y, int64_t n, int ldx, int ldy,
+    const T* __restrict__ X, const T* __restrict__ Y, int64_t n, int ldx, int ldy, int px, int py,
     const double* __restrict__ Wt, const double* __restrict__ Ct, const PplsScalars* __restrict__ sc,
     double* __restrict__ Z, double* __restrict__ mu,
     const int* __restrict__ stop) {
@@ -748,19 +751,28 @@ __global__ __launch_bounds__(256) void ppls_panel_mfmadots_kernel(
   constexpr int V4 = 4 * R;
   static_assert(R <= 16, "one 16-wide MFMA tile of components");
   __shared__ __attribute__((aligned(16))) char lds[4 * 2 * RB * RS];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // uniform: scalar branches below
   const int i16 = lane & 15, kq = lane >> 4;
   const int lrow = lane >> 3, lchunk = lane & 7;   // loading: 8 lanes per row, 8 rows per load
   const int comp = i16 < R ? i16 : 0;
   const double al = sc->alpha[comp], be = sc->beta[comp], ga = sc->gamma[comp], de = sc->delta[comp];
+  static_assert(KS == 1 || KS == 2, "one wave or a wave pair per row tile");
+  static_assert(2 * NB * 4 * 64 * 8 <= 2 * RB * RS, "a wave's dot sums fit its transpose buffers");
+  constexpr int TPW = 4 / KS;                          // row tiles per workgroup pass
+  const int part = wave % KS;                          // this wave's share of the columns
   const int64_t ntiles = (n + RB - 1) / RB;
-  for (int64_t t = (int64_t)blockIdx.x * 4 + wave; t < ntiles; t += (int64_t)gridDim.x * 4) {
+  // the trip count is uniform over the workgroup (the pair combine has workgroup barriers)
+  for (int64_t tb = (int64_t)blockIdx.x * TPW; tb < ntiles; tb += (int64_t)gridDim.x * TPW) {
+    const int64_t t = tb + wave / KS;
+    const bool active = t < ntiles;
     const int64_t row0 = t * RB;
     d4 res[2][NB];   // [mat][block]
+    if (active) {
 #pragma unroll
     for (int mat = 0; mat < 2; ++mat) {
       const T* M = mat ? Y : X;
-      const int ld = mat ? ldy : ldx;
+      const int ld = mat ? ldy : ldx, pc = mat ? py : px;
       const double* Wm = mat ? Ct : Wt;
       d4 acc[NB];
 #pragma unroll
@@ -772,7 +784,10 @@ __global__ __launch_bounds__(256) void ppls_panel_mfmadots_kernel(
         if (rr >= n) rr = n - 1;
         src[u] = M + rr * ld + lchunk * (16 / ES);
       }
-      const int ntc = (ld + KT - 1) / KT;
+      // the tiles holding the pc data columns (row padding beyond them is zero and skipped, so a
+      // padded layout sums the same tiles in the same order as a 16-B-row one), split over the pair
+      const int ntc = (pc + KT - 1) / KT;
+      const int tc0 = ntc * part / KS, tc1 = ntc * (part + 1) / KS;   // this wave's column tiles
       // Loads are unconditional (no exec-mask branches, so the waitcnts stay precise): a partial
       // last tile reads past the row end into the next row (or the allocation's slack after the
       // last row), which meets the zero rows of Wt beyond ld and adds exactly 0; prefetches past
@@ -782,7 +797,7 @@ __global__ __launch_bounds__(256) void ppls_panel_mfmadots_kernel(
       auto ld4 = [&](const T* p) -> f4 { return *(const f4*)p; };   // (non-temporal: 16 % slower here)
       auto load_tile = [&](int tc, f4 (&b)[NL]) {
         if constexpr (ab_x) return;
-        const int c = tc < ntc ? tc : ntc - 1;
+        const int c = tc < tc1 ? tc : tc1 - 1;   // a prefetch past the range re-reads its last tile
 #pragma unroll
         for (int u = 0; u < NL; ++u) b[u] = ld4(src[u] + c * KT);
       };
@@ -831,12 +846,37 @@ __global__ __launch_bounds__(256) void ppls_panel_mfmadots_kernel(
           }
         }
       };
-      load_tile(0, xa);
-      for (int tc = 0; tc < ntc; ++tc) step(tc, xa);
+      if (tc0 < tc1) {
+        load_tile(tc0, xa);
+        for (int tc = tc0; tc < tc1; ++tc) step(tc, xa);
+      }
 #pragma unroll
       for (int bk = 0; bk < NB; ++bk) res[mat][bk] = acc[bk];
     }
-    if (i16 < R) {
+    }   // active
+    if constexpr (KS == 2) {
+      // the second wave of the pair hands its sums over through its own (now idle) transpose buffer
+      double* cb = (double*)(lds + (wave | 1) * 2 * RB * RS);
+      if (active && part == 1) {
+#pragma unroll
+        for (int mat = 0; mat < 2; ++mat)
+#pragma unroll
+          for (int bk = 0; bk < NB; ++bk)
+#pragma unroll
+            for (int reg = 0; reg < 4; ++reg) cb[((mat * NB + bk) * 4 + reg) * 64 + lane] = res[mat][bk][reg];
+      }
+      __syncthreads();
+      if (active && part == 0) {
+#pragma unroll
+        for (int mat = 0; mat < 2; ++mat)
+#pragma unroll
+          for (int bk = 0; bk < NB; ++bk)
+#pragma unroll
+            for (int reg = 0; reg < 4; ++reg) res[mat][bk][reg] += cb[((mat * NB + bk) * 4 + reg) * 64 + lane];
+      }
+      __syncthreads();   // the buffer is the partner's again
+    }
+    if (active && part == 0 && i16 < R) {
 #pragma unroll
       for (int blk = 0; blk < NB; ++blk)
 #pragma unroll
@@ -2485,6 +2525,7 @@ hipError_t ppls_launch_accumulate(const PplsSweepArgs* a, const double* Z, hipSt
 // ---- panel sweep launchers
 }  // extern "C"
 namespace {
+
 template <typename T, int R>
 hipError_t launch_panel_t(const PplsSweepArgs* a, const T* X, const T* Y, double* Z, int chunks, hipStream_t st) {
   // transposed W, C behind Z (see ppls_panel_z_len), rows padded to whole 32-column tiles
@@ -2503,15 +2544,24 @@ hipError_t launch_panel_t(const PplsSweepArgs* a, const T* X, const T* Y, double
     const bool big = a->n_local >= 32768;
     const int rb = (big != ((a->ablate & 4096) != 0)) ? 64 : 32;
     const int64_t wtiles = (a->n_local + rb - 1) / rb;
-    const int mblocks = (int)((wtiles + 3) / 4 < 16384 ? (wtiles + 3) / 4 : 16384);
+    // column split over wave pairs when one wave per row tile would leave resident wave slots
+    // (2 waves/SIMD at 64 rows, 3 at 32) empty; ablate bit 11 flips it
+    const int64_t slots = (int64_t)(a->num_cus > 0 ? a->num_cus : 256) * 4 * (rb == 64 ? 2 : 3);
+    const int ks = ((wtiles < slots) != ((a->ablate & 2048) != 0)) ? 2 : 1;
+    const int64_t wgs = (wtiles + 4 / ks - 1) / (4 / ks);
+    // the grid option (dots_grid) forces a smaller grid: tests of the grid-stride loop
+    const int mblocks = (int)(a->dots_grid > 0 && a->dots_grid < wgs ? a->dots_grid : wgs < 16384 ? wgs : 16384);
+    double* mu_out = a->write_mu ? a->mu : nullptr;
     // (also measured: the B operands prefetched a tile ahead, 256 VGPRs -- no faster, 7.70-7.88 vs
     // 7.69-7.78 ms; profiles/r2_c5_dots_rows.txt)
-    if (rb == 64)
-      hipLaunchKernelGGL((ppls_panel_mfmadots_kernel<T, R, 4>), dim3(mblocks), dim3(256), 0, st, X, Y,
-                         a->n_local, a->ldx, a->ldy, Wt, Ct, a->sc, Z, a->write_mu ? a->mu : nullptr, a->stop);
-    else
-      hipLaunchKernelGGL((ppls_panel_mfmadots_kernel<T, R, 2>), dim3(mblocks), dim3(256), 0, st, X, Y,
-                         a->n_local, a->ldx, a->ldy, Wt, Ct, a->sc, Z, a->write_mu ? a->mu : nullptr, a->stop);
+#define PPLS_LAUNCH_DOTS(NBV, KSV)                                                                   \
+  hipLaunchKernelGGL((ppls_panel_mfmadots_kernel<T, R, NBV, KSV>), dim3(mblocks), dim3(256), 0, st, X, Y, \
+                     a->n_local, a->ldx, a->ldy, a->p, a->q, Wt, Ct, a->sc, Z, mu_out, a->stop)
+    if (rb == 64 && ks == 2) PPLS_LAUNCH_DOTS(4, 2);
+    else if (rb == 64) PPLS_LAUNCH_DOTS(4, 1);
+    else if (ks == 2) PPLS_LAUNCH_DOTS(2, 2);
+    else PPLS_LAUNCH_DOTS(2, 1);
+#undef PPLS_LAUNCH_DOTS
   }
   constexpr int VEC = PplsVec16<T>::N;
   if (a->ablate & 256) return hipGetLastError();   // dots only (scores)

@@ -110,3 +110,37 @@ def test_row_padding_is_invisible(dtype, p, q):
     assert _relerr(l1, l0) < 1e-14
     assert np.abs(e0.W - e1.W).max() < 1e-14 and np.abs(e0.C - e1.C).max() < 1e-14
 
+
+
+@pytest.mark.parametrize("dtype,n,p,q,r,grid", [(1, 2000, 1500, 90, 10, 0), (1, 700, 65, 33, 3, 3),
+                                                 (0, 900, 2300, 17, 9, 0), (1, 5000, 31, 2, 2, 2)])
+def test_dots_wave_pair_equals_single_wave(dtype, n, p, q, r, grid):
+    """Panel dots on small shards split each row tile's columns over a wave pair (KS = 2 in
+    ppls_panel_mfmadots_kernel; ablate bit 11 forces one wave per tile).  Both forms sum the same
+    products in a different grouping: mu within 1e-13 of each other and of the oracle's E-step;
+    `grid` > 0 shrinks the dots grid so workgroups loop (the pair's LDS combine sits inside that
+    loop behind workgroup barriers); one column tile per matrix (p = 31, q = 2) leaves the pair's
+    first wave without columns."""
+    from ppls_amd import Context
+    X, Y, th0 = make_problem(n, p, q, r, seed=n + p)
+    if dtype:
+        X, Y = _round32(X), _round32(Y)
+    mus = []
+    for ab in (0, 2048):
+        with Context(0) as c:
+            c.set_option("dtype", dtype)
+            if grid:
+                c.set_option("grid", grid)
+            c.set_option("ablate", ab)
+            c.set_data(X, Y)
+            assert "panel" in c.sweep_kernel(r)
+            assert ("wave pair" in c.sweep_kernel(r)) == (ab == 0)
+            e = c.estep(_theta(th0))
+            mus.append((e.mu_T, e.mu_U))
+    ref = o.expect_m(X, Y, *(th0[k] for k in ("W", "C", "B", "sigE", "sigF", "sigH", "sigT")))
+    scale = max(np.abs(ref["mu_T"]).max(), np.abs(ref["mu_U"]).max())
+    for (mt, mu) in mus:
+        assert np.abs(mt - ref["mu_T"]).max() < 1e-12 * scale
+        assert np.abs(mu - ref["mu_U"]).max() < 1e-12 * scale
+    assert np.abs(mus[0][0] - mus[1][0]).max() < 1e-13 * scale
+    assert np.abs(mus[0][1] - mus[1][1]).max() < 1e-13 * scale

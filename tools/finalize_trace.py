@@ -22,13 +22,17 @@ def main():
         ctx.set_option("ftrace", 1)
         ctx.set_option("polar1", int(os.environ.get("POLAR1", "1")))
         ctx.em_begin(th0)
-        for it in range(4):
+        skip = int(os.environ.get("SKIP", "0"))   # steady state: trace after SKIP iterations
+        if skip:
+            ctx.em_iterate(skip)
+        for it in range(skip, skip + 4):
             ctx.em_iterate(1)
             tr = ctx.finalize_trace()
             raw = tr[0][10:]
             if raw[1] and raw[2]:
                 us = tr[0][5]
-                print(f"  block 0: jacobi sweeps {raw[0]}, core clock {(raw[2] - raw[1]) / (us * 1e3):.2f} GHz")
+                what = "Jacobi sweeps" if isinstance(raw[0], int) else "team barrier 1 all arrived at (us)"
+                print(f"  block 0: {what} {raw[0]}, core clock {(raw[2] - raw[1]) / (us * 1e3):.2f} GHz")
             print(f"{cfgname} polar1={os.environ.get('POLAR1', '1')} iter {it}: " + "; ".join(
                 f"block {b}: " + " ".join(f"{s}={v}" for s, v in enumerate(ts) if v is not None and s not in (10, 11, 12))
                 for b, ts in tr.items()), flush=True)
