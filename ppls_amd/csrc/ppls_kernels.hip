@@ -1222,47 +1222,6 @@ __device__ __forceinline__ void ppls_stamp(long long* tr, int slot) {
 // ---- r x r algebra in registers (compile-time R, fully unrolled; run by one thread) -----------
 // Matrices are T[row][col].
 
-// Upper Cholesky G = U'U; false if a pivot is not positive.
-template <int R>
-__device__ __forceinline__ bool ppls_chol_reg(const double (&G)[R][R], double (&U)[R][R], double (&dinv)[R]) {
-  bool ok = true;
-#pragma unroll
-  for (int j = 0; j < R; ++j) {
-#pragma unroll
-    for (int i = 0; i < R; ++i) {
-      if (i > j) { U[i][j] = 0.0; continue; }
-      double s = G[i][j];
-#pragma unroll
-      for (int k = 0; k < i; ++k) s = fma(-U[k][i], U[k][j], s);
-      if (i == j) {
-        ok = ok && (s > 0.0);
-        U[j][j] = sqrt(s > 0.0 ? s : 1.0);
-        dinv[j] = 1.0 / U[j][j];
-      } else {
-        U[i][j] = s * dinv[i];
-      }
-    }
-  }
-  return ok;
-}
-
-// Ui = inv(U) for upper-triangular U with reciprocal diagonal dinv.
-template <int R>
-__device__ __forceinline__ void ppls_inv_upper_reg(const double (&U)[R][R], const double (&dinv)[R],
-                                                   double (&Ui)[R][R]) {
-#pragma unroll
-  for (int j = 0; j < R; ++j)
-#pragma unroll
-    for (int ii = 0; ii < R; ++ii) {
-      const int i = R - 1 - ii;
-      if (i > j) { Ui[i][j] = 0.0; continue; }
-      double s = (i == j) ? 1.0 : 0.0;
-#pragma unroll
-      for (int k = i + 1; k <= j; ++k) s = fma(-U[i][k], Ui[k][j], s);
-      Ui[i][j] = s * dinv[i];
-    }
-}
-
 // 1/x and 1/sqrt(x) from the hardware estimates plus two Newton steps (~1 ulp; x normal, > 0
 // for rsq).  The serial r x r code is latency-bound on one wave, and these are 5-7 dependent
 // instructions against ~12-15 for the IEEE-exact expansions.
@@ -1298,6 +1257,52 @@ __device__ __forceinline__ void ppls_gram_unpack(const double (&vals)[R * (R + 1
   for (int b = 0; b < R; ++b)
 #pragma unroll
     for (int a = 0; a <= b; ++a) { G[a][b] = vals[e]; G[b][a] = vals[e]; ++e; }
+}
+
+// Packed upper triangles (element (a, b), a <= b, at b (b + 1) / 2 + a: the Gram sums' order) --
+// the register forms below then hold R(R+1)/2 values instead of R^2, so one thread keeps R = 10 in
+// registers.
+__host__ __device__ constexpr int ppls_pk(int a, int b) { return b * (b + 1) / 2 + a; }
+
+// In place: P = the packed Gram on entry, its upper Cholesky factor U (G = U'U) on exit.
+template <int R>
+__device__ __forceinline__ bool ppls_chol_pk(double (&P)[R * (R + 1) / 2], double (&dinv)[R]) {
+  bool ok = true;
+#pragma unroll
+  for (int j = 0; j < R; ++j)
+#pragma unroll
+    for (int i = 0; i <= j; ++i) {
+      double s = P[ppls_pk(i, j)];
+#pragma unroll
+      for (int k = 0; k < i; ++k) s = fma(-P[ppls_pk(k, i)], P[ppls_pk(k, j)], s);
+      if (i == j) {
+        ok = ok && (s > 0.0);
+        P[ppls_pk(j, j)] = sqrt(s > 0.0 ? s : 1.0);
+        dinv[j] = 1.0 / P[ppls_pk(j, j)];
+      } else {
+        P[ppls_pk(i, j)] = s * dinv[i];
+      }
+    }
+  return ok;
+}
+
+// In place: P = U on entry, inv(U) on exit.  Columns last to first: column j of the inverse needs
+// U's columns <= j only, and within the column the rows bottom-up.
+template <int R>
+__device__ __forceinline__ void ppls_inv_upper_pk(double (&P)[R * (R + 1) / 2], const double (&dinv)[R]) {
+#pragma unroll
+  for (int jj = 0; jj < R; ++jj) {
+    const int j = R - 1 - jj;
+#pragma unroll
+    for (int ii = 0; ii < R; ++ii) {
+      const int i = R - 1 - ii;
+      if (i > j) continue;
+      double s = (i == j) ? 1.0 : 0.0;
+#pragma unroll
+      for (int k = i + 1; k <= j; ++k) s = fma(-P[ppls_pk(i, k)], P[ppls_pk(k, j)], s);
+      P[ppls_pk(i, j)] = s * dinv[i];
+    }
+  }
 }
 
 // Sum over an aligned group of 8 lanes (DPP quad xor1, quad xor2, half-row mirror); every lane of
@@ -1548,6 +1553,9 @@ __device__ void ppls_team_sum(const PplsTeam& tm, int phase, double (&vals)[NG],
 // warm-started from vstate (the previous iteration's V; nullptr = identity).  sm: >= 2 R^2
 // doubles of LDS.  Returns false when S is numerically rank deficient (a Cholesky pivot fails or
 // sigma_min < 1e-14 sigma_max); the caller then falls back to Householder (which reports it).
+#ifndef PPLS_REG_RMAX
+#define PPLS_REG_RMAX 10   // the polar's Cholesky factors and inverses by one thread in registers up to this R
+#endif
 template <int R, int NT>
 __device__ bool ppls_block_polar_fast(const double* __restrict__ S, int64_t lds, int p,
                                       double* __restrict__ out, int64_t ldo, int ldo_rows, double* Sl,
@@ -1602,17 +1610,24 @@ __device__ bool ppls_block_polar_fast(const double* __restrict__ S, int64_t lds,
   ppls_stamp(tr, 14);
   ppls_team_sum<NG>(tm, 0, vals, sh);
   ppls_stamp(tr, 1);
-  if constexpr (R <= 6) {   // small R: one thread in registers is faster than the wave form
-    if (tid == 0) {
-      double Gm[R][R], U[R][R], Ui[R][R], dinv[R];
-      ppls_gram_unpack<R>(vals, Gm);
-      ok = ppls_chol_reg<R>(Gm, U, dinv);
-      ppls_inv_upper_reg<R>(U, dinv, Ui);
-      for (int e = 0; e < GG; ++e) sT[e] = 0.0;
+  if constexpr (R <= PPLS_REG_RMAX) {   // one thread in registers is faster than the wave form
+    if (tid < 64) {
+      for (int e = lane; e < GG; e += 64) sT[e] = 0.0;   // (in order before lane 0's stores)
+      if (lane == 0) {
+        double P[NG], dinv[R];
 #pragma unroll
-      for (int a = 0; a < R; ++a)
+        for (int e = 0; e < NG; ++e) P[e] = vals[e];
+        ok = ppls_chol_pk<R>(P, dinv);
 #pragma unroll
-        for (int b = 0; b < R; ++b) { sT[b * G + a] = U[a][b]; sF[b * R + a] = Ui[a][b]; }
+        for (int b = 0; b < R; ++b)
+#pragma unroll
+          for (int a = 0; a <= b; ++a) sT[b * G + a] = P[ppls_pk(a, b)];
+        ppls_inv_upper_pk<R>(P, dinv);
+#pragma unroll
+        for (int b = 0; b < R; ++b)
+#pragma unroll
+          for (int a = 0; a < R; ++a) sF[b * R + a] = a <= b ? P[ppls_pk(a, b)] : 0.0;
+      }
     }
   } else if (tid < 64) {   // R1 = chol(G1) -> sT, R1^-1 -> sF (ld R)
     for (int e = lane; e < GG; e += 64) {
@@ -1761,7 +1776,7 @@ __device__ bool ppls_block_polar_fast(const double* __restrict__ S, int64_t lds,
   ppls_team_leave(tm);   // the last barrier of this member
   ppls_stamp(tr, 3);
   if (tid < 64) {   // wave 0: R2 = chol(G2), T = R2 R1, warm start, Jacobi, F
-    if constexpr (R > 6) {
+    if constexpr (R > PPLS_REG_RMAX) {
       for (int e = lane; e < GG; e += 64) {
         const int a = e % G, b = e / G;
         double v = 0.0;
@@ -1774,21 +1789,26 @@ __device__ bool ppls_block_polar_fast(const double* __restrict__ S, int64_t lds,
     }
     ppls_wave_lds_fence();
     bool good = true;
-    if constexpr (R <= 6) {
+    if constexpr (R <= PPLS_REG_RMAX) {
+      for (int e = lane; e < GG; e += 64) { sA[e] = 0.0; sU[e] = 0.0; }   // (before lane 0's stores)
       if (lane == 0) {
-        double Gm[R][R], U2[R][R], dinv[R];
-        ppls_gram_unpack<R>(vals, Gm);
-        good = ppls_chol_reg<R>(Gm, U2, dinv);
-        for (int e = 0; e < GG; ++e) { sA[e] = 0.0; sU[e] = 0.0; }
+        double P[NG], R1[NG], dinv[R];
 #pragma unroll
-        for (int a = 0; a < R; ++a)                 // T = R2 R1 (upper); sU = R2
+        for (int e = 0; e < NG; ++e) P[e] = vals[e];
 #pragma unroll
-          for (int b = 0; b < R; ++b) {
+        for (int b = 0; b < R; ++b)
+#pragma unroll
+          for (int a = 0; a <= b; ++a) R1[ppls_pk(a, b)] = sT[b * G + a];
+        good = ppls_chol_pk<R>(P, dinv);            // P = R2
+#pragma unroll
+        for (int b = 0; b < R; ++b)                 // T = R2 R1 (upper); sU = R2
+#pragma unroll
+          for (int a = 0; a <= b; ++a) {
             double sacc = 0.0;
 #pragma unroll
-            for (int kk = 0; kk < R; ++kk) sacc = fma(U2[a][kk], sT[b * G + kk], sacc);
+            for (int kk = a; kk <= b; ++kk) sacc = fma(P[ppls_pk(a, kk)], R1[ppls_pk(kk, b)], sacc);
             sA[b * G + a] = sacc;
-            sU[b * G + a] = U2[a][b];
+            sU[b * G + a] = P[ppls_pk(a, b)];
           }
       }
       ppls_wave_lds_fence();
