@@ -142,6 +142,64 @@ def cpu_baseline(ctx, th0, cfg, iters=3, one_core_rows=100_000):
                                      f"value = rows*iterations/s / n")), rel, werr
 
 
+def bench_xprod(ctx, th0, args, barrier, dist, torch, r, ll_stream, t_stream):
+    """The cross-product form of the same iterations (option "xprod", ppls_xprod.hip): S = [X Y]'[X Y]
+    formed once (MFMA Gram of the local rows + ONE all-reduce of S), then every iteration reads S
+    (8 P^2 bytes) instead of X and Y and needs no collective.  Timed like the headline: barrier +
+    synchronize around the formation of S and around args.xprod_steps iterations, max over ranks."""
+    def tmax(v):
+        if dist is None:
+            return v
+        tt = torch.tensor([v], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        return float(tt.item())
+
+    barrier()
+    ctx.set_option("xprod", 1)
+    t0 = time.perf_counter()
+    gram_ms, _ = ctx.xprod_prepare()
+    barrier()
+    t_setup = tmax(time.perf_counter() - t0)
+    info = ctx.xprod_info(r)
+    ctx.em_begin(th0)
+    ctx.em_iterate(args.warmup)
+    barrier()
+    ctx.set_option("timing", 1)
+    ctx.sweep_timing(reset=True)
+    t0 = time.perf_counter()
+    ctx.em_iterate(args.xprod_steps)
+    barrier()
+    dt = tmax(time.perf_counter() - t0)
+    ctx.set_option("timing", 0)
+    kms, launches = ctx.sweep_timing(reset=True)
+    _, ll_x = ctx.em_state()
+    k = min(len(ll_x), len(ll_stream))
+    rel = float(np.abs(ll_x[:k] - ll_stream[:k]).max() / np.abs(ll_stream[:k]).max()) if k else None
+    t_x = dt / args.xprod_steps
+    avg_us = 1e3 * kms / max(launches, 1)
+    achieved = info["bytes_per_pass"] / (avg_us * 1e-6) / 1e9 if launches else None
+    gram_tf = info["gram_flops"] / (gram_ms * 1e-3) / 1e12 if gram_ms > 0 else None
+
+    def fit_s(steps):   # a whole PPLS_simult loop of `steps` iterations (+1 sweep for the last loglik)
+        return dict(stream=(steps + 1) * t_stream, xprod=t_setup + (steps + 1) * t_x)
+
+    return dict(
+        what="cross-product form: S = [X Y]'[X Y] formed once on MFMA (+1 all-reduce of S over ranks), then each "
+             "iteration reads S instead of X, Y (no per-iteration collective); same iterates, sums reordered",
+        setup_s=t_setup, gram_kernel_ms=gram_ms, gram_tflops=gram_tf,
+        gram_roofline=dict(bound="mfma", achieved=gram_tf, peak=FP64_PEAK_TF, unit="TFLOP/s",
+                           frac=(gram_tf / FP64_PEAK_TF) if gram_tf else None,
+                           flops_per_launch=info["gram_flops"]),
+        steps=args.xprod_steps, ms_per_step=1e3 * t_x, it_per_s=1.0 / t_x,
+        roofline=dict(bound="hbm", achieved=achieved, peak=HBM_PEAK_GBS, unit="GB/s",
+                      frac=(achieved / HBM_PEAK_GBS) if achieved else None, kernel="xprod_apply + xprod_gram",
+                      avg_kernel_us=avg_us, bytes_per_launch=info["bytes_per_pass"],
+                      rows_per_workgroup=info["rows_per_wave"]),
+        loglik_rel_diff_vs_streaming=rel, loglik_compared=k,
+        breakeven_steps=(t_setup / (t_stream - t_x)) if t_stream > t_x else None,
+        fit_seconds={str(s): fit_s(s) for s in (10, 100, 1000, 10000)})
+
+
 _DEVICE = {}
 
 
@@ -195,6 +253,8 @@ def main():
     ap.add_argument("--cpu-iters", type=int, default=3, help="timed CPU-baseline iterations (full n)")
     ap.add_argument("--timing-every", type=int, default=4,
                     help="bracket every N-th sweep of the timed region with HIP events")
+    ap.add_argument("--xprod-steps", type=int, default=2000,
+                    help="iterations of the cross-product form timed after the headline (0: skip it)")
     ap.add_argument("--comm", default="rccl", choices=["rccl", "host"],
                     help="N>1 statistics all-reduce: RCCL (default) or the host reducer hook over gloo "
                          "(ppls_set_reducer; rehearses the multi-rank bench with several ranks on one GPU)")
@@ -265,6 +325,10 @@ def main():
     est, ll = ctx.em_state()
     info = ctx.sweep_info(r)
     rccl_nranks, rccl_rank, ar_ms, ar_calls = ctx.comm_info(reset=True)
+    xp = None
+    if args.xprod_steps > 0:
+        xp = bench_xprod(ctx, th0, args, barrier, dist, torch, r, ll, dt / args.steps)
+        ctx.set_option("xprod", 0)
     # every rank's final theta and trace, hashed: a dp-N run proves its ranks stayed identical
     h = hashlib.sha256()
     for a in (est.W, est.C, est.B, est.sigT, np.array([est.sigE, est.sigF, est.sigH]), ll):
@@ -324,6 +388,7 @@ def main():
                              allreduce_us=(1e3 * ar_ms / ar_calls) if ar_calls else None,
                              allreduce_timed_calls=ar_calls),
                    theta_sha16=digest, ranks_bitwise_identical=len(set(digests)) == 1)
+        out["xprod"] = xp
         if world == 1 and not args.no_cpu:
             cb, rel, werr = cpu_baseline(ctx, th0, cfg, args.cpu_iters)
             out["cpu_baseline"] = cb

@@ -90,7 +90,12 @@ const char* ppls_last_error(const ppls_ctx* ctx);
  *             the 256 MB MALL), 0 off, 1 on),
  *       "timing" (N > 0: record HIP events around every N-th sweep launch; 0 off),
  *       "balance" (split sweep row partition: 1 (default) calibrated per-XCD weights, measured once
- *                  per data shape with 8 timed launches, from 2048 rows per workgroup; 0 the even split) */
+ *                  per data shape with 8 timed launches, from 2048 rows per workgroup; 0 the even split),
+ *       "xprod" (statistics of ppls_em_run / ppls_em_iterate: 0 (default) one streaming sweep over X, Y
+ *                per iteration; 1 from the cross-products S = [X Y]'[X Y], formed once per data set
+ *                on MFMA and all-reduced once, after which an iteration reads S (8 (p+q)^2 bytes) and
+ *                needs no collective; -1 auto: S when a cost model of max_steps iterations says so),
+ *       "xprod_rw" (rows of S per workgroup of the cross-product kernel: 0 auto, 1, 2, 4) */
 int ppls_set_option(ppls_ctx* ctx, const char* key, int64_t value);
 
 /* ---- multi-GPU: samples are sharded over ranks; one RCCL all-reduce per EM iteration ---- */
@@ -248,6 +253,13 @@ int ppls_sweep_balance(ppls_ctx* ctx, double* w8, int64_t* bounds, int cap, int*
  * the per-iteration statistics all-reduce on the timed sweeps (option "timing"; RCCL only). */
 int ppls_comm_info(ppls_ctx* ctx, int* nranks, int* rank, double* allreduce_ms, int64_t* allreduce_calls,
                    int reset);
+/* Cross-product form (option "xprod"): form S now (*ms = the MFMA Gram kernel time, *total_ms = with
+ * the all-reduce and allocation; both nullable) -- otherwise the first run that reads S forms it. */
+int ppls_xprod_prepare(ppls_ctx* ctx, double* ms, double* total_ms);
+/* Its state: *ready = S is formed for the current data, *bytes_per_pass = 8 P^2 (one iteration's
+ * algorithmic read, P = padded p + q), *flops = 2 n_local P^2 of the Gram as computed (lower tiles:
+ * ~ half the full product), *rows_per_wave = rows of S per workgroup of the apply kernel for r components. */
+int ppls_xprod_info(ppls_ctx* ctx, int r, int* ready, int64_t* bytes_per_pass, double* flops, int* rows_per_wave);
 /* Shape facts for the roofline: bytes of X and Y one sweep reads (algorithmic), kernel variant. */
 int ppls_sweep_info(ppls_ctx* ctx, int r, int64_t* bytes_per_sweep, int* variant, int* grid);
 /* The sweep kernel instantiation the next EM iteration with r components launches, as text

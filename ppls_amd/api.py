@@ -366,6 +366,19 @@ class Context:
         self._chk(self._L.ppls_gram(self.h, int(xory), int(nsplit), dptr(G), ct.byref(ms)))
         return G, ms.value
 
+    def xprod_prepare(self):
+        """Form the cross-products S = [X Y]'[X Y] now (option "xprod") -> (Gram kernel ms, total ms);
+        (0, 0) when S is already formed for the current data."""
+        ms, tot = ct.c_double(), ct.c_double()
+        self._chk(self._L.ppls_xprod_prepare(self.h, ct.byref(ms), ct.byref(tot)))
+        return ms.value, tot.value
+
+    def xprod_info(self, r=1):
+        """{ready, bytes_per_pass (8 P^2), gram_flops (as computed), rows_per_wave} of the cross-product form."""
+        rd, b, f, rw = ct.c_int(), ct.c_int64(), ct.c_double(), ct.c_int()
+        self._chk(self._L.ppls_xprod_info(self.h, int(r), ct.byref(rd), ct.byref(b), ct.byref(f), ct.byref(rw)))
+        return dict(ready=bool(rd.value), bytes_per_pass=b.value, gram_flops=f.value, rows_per_wave=rw.value)
+
     def scores(self, W, C):
         """scores.PPLS (EM_W_multi.R:411-420) on the resident rows: (X W, Y C), n_local x k each."""
         W = np.asfortranarray(np.array(W, dtype=np.float64, ndmin=2).reshape(self.p, -1))

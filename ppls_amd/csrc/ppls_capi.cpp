@@ -11,6 +11,7 @@
 #include <rocsolver/rocsolver.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -22,6 +23,7 @@
 #include "../../include/ppls.h"
 #include "ppls_kernels.h"
 #include "ppls_math.h"
+#include "ppls_xprod.h"
 
 struct ppls_ctx {
   int device = 0;
@@ -108,6 +110,17 @@ struct ppls_ctx {
   // device-resident iteration state (ppls_em_begin / ppls_em_iterate)
   int em_r = 0, em_cur = 0, em_iter = 0;
   bool em_active = false;
+  // cross-product form of the iteration (ppls_xprod.hip): S = [X Y]'[X Y] (P x P, P = ldx + ldy)
+  // formed once per data set, then every statistics step reads S instead of X and Y
+  int xprod = 0;            // option "xprod": 0 stream X, Y (default), 1 cross-products, -1 auto (cost model)
+  int xprod_rw = 0;         // option "xprod_rw": rows of S per wave of the apply kernel (0 auto)
+  bool xp_ready = false;    // S holds the (all-reduced) cross-products of the current data
+  bool xp_active = false;   // statistics steps of the current run read S
+  double* xp_S = nullptr;
+  double* xp_M = nullptr;   // M = S blockdiag(W, C), P x 2r scratch
+  double xp_setup_ms = 0.0; // last formation of S: Gram kernel (HIP events), and with the all-reduce
+  double xp_setup_total_ms = 0.0;
+  int xp_nsplit = 0;
   rocblas_handle blas = nullptr;   // rocSOLVER (variances.PPLS_simult's p x p inverse), created lazily
   // timing
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;
@@ -212,6 +225,7 @@ PplsScalars scalars_of(const ppls_theta* th, int r) {
 int ensure_r(ppls_ctx* c, int r, int max_steps) {
   int rc;
   c->em_active = false;   // every entry point that (re)stages theta ends an ppls_em_begin session
+  c->xp_active = false;
   if (r != c->r_alloc) {
     for (int i = 0; i < 2; ++i) {
       if ((rc = dalloc(c, &c->W[i], (size_t)c->ldx * r))) return rc;
@@ -478,6 +492,22 @@ int balance_rows(ppls_ctx* c, PplsSweepArgs* a) {
   return PPLS_OK;
 }
 
+// The next pair of timing events for a statistics launch, when option "timing" selects this one.
+int timing_pair(ppls_ctx* c, hipEvent_t* e0, hipEvent_t* e1) {
+  *e0 = *e1 = nullptr;
+  if (!(c->timing > 0 && (c->sweep_count++ % c->timing) == 0)) return PPLS_OK;
+  if (c->ev_used == c->ev.size()) {
+    std::pair<hipEvent_t, hipEvent_t> pr;
+    HIPCHK(c, hipEventCreate(&pr.first));
+    HIPCHK(c, hipEventCreate(&pr.second));
+    c->ev.push_back(pr);
+  }
+  *e0 = c->ev[c->ev_used].first;
+  *e1 = c->ev[c->ev_used].second;
+  ++c->ev_used;
+  return PPLS_OK;
+}
+
 // One sweep with theta[slot] -> c->stats (all-reduced).
 int sweep(ppls_ctx* c, int r, int slot, bool write_mu) {
   int rc;
@@ -520,20 +550,10 @@ int sweep(ppls_ctx* c, int r, int slot, bool write_mu) {
     a.trace = (plan == 3 && a.grid <= PPLS_STRACE_MAX_WG) ? c->strace : nullptr;
     // the row partition (its one-time calibration launches stay outside the timed events)
     if (plan == 3 && c->balance && c->seg_rows < 0 && (rc = balance_rows(c, &a))) return rc;
-    hipEvent_t e0 = nullptr, e1 = nullptr;
-    const bool timed = c->timing > 0 && (c->sweep_count++ % c->timing) == 0;
-    if (timed) {
-      if (c->ev_used == c->ev.size()) {
-        std::pair<hipEvent_t, hipEvent_t> pr;
-        HIPCHK(c, hipEventCreate(&pr.first));
-        HIPCHK(c, hipEventCreate(&pr.second));
-        c->ev.push_back(pr);
-      }
-      e0 = c->ev[c->ev_used].first;
-      e1 = c->ev[c->ev_used].second;
-      ++c->ev_used;
-      HIPCHK(c, hipEventRecord(e0, c->stream));
-    }
+    hipEvent_t e0, e1;
+    if ((rc = timing_pair(c, &e0, &e1))) return rc;
+    const bool timed = e0 != nullptr;
+    if (timed) HIPCHK(c, hipEventRecord(e0, c->stream));
     if (plan == 3) HIPCHK(c, ppls_launch_sweep_split(&a, c->stream));
     else if (plan == 4) HIPCHK(c, ppls_launch_sweep_panel(&a, c->dtype, c->Z, a.grid, c->stream));
     else HIPCHK(c, ppls_launch_sweep_twopass(&a, c->Z, c->stream));
@@ -557,7 +577,8 @@ int sweep(ppls_ctx* c, int r, int slot, bool write_mu) {
   return allreduce(c, c->stats, (size_t)c->part_ld);
 }
 
-int finalize(ppls_ctx* c, int r, int cur, int nxt, int logl_index, int type, int stop_step = 0) {
+int finalize(ppls_ctx* c, int r, int cur, int nxt, int logl_index, int type, int stop_step = 0,
+             bool scalars_only = false) {
   PplsFinalizeArgs f;
   f.stats = c->stats;
   f.ssq = c->ssq;
@@ -580,6 +601,7 @@ int finalize(ppls_ctx* c, int r, int cur, int nxt, int logl_index, int type, int
   f.status = c->status;
   f.qr = type == PPLS_ORTH_QR ? 1 : 0;
   f.mode = (3 & ~(c->ablate >> 2)) | (c->polar1 ? 4 : 0) | (c->exact_gram ? 16 : 0) | (polar1_bound(c, r) << 8);   // ablate bit2: skip polar, bit3: skip scalars
+  if (scalars_only) f.mode &= ~1;
   f.trace = c->ftrace;
   f.gram_cur = c->gram[cur];
   f.gram_nxt = c->gram[nxt];
@@ -604,6 +626,111 @@ int finalize(ppls_ctx* c, int r, int cur, int nxt, int logl_index, int type, int
   // start and the loglik slot are rewritten)
   if (c->ablate & 8192) HIPCHK(c, ppls_launch_finalize(&f, c->stream));
   return PPLS_OK;
+}
+
+// Row splits of the MFMA Gram of a p x p product over n rows: enough work items to fill the device
+// (whole rounds of resident workgroups), each split's p x p partial kept under 4 GB in all.
+int gram_splits(ppls_ctx* c, int p, int64_t n) {
+  const int ntiles = ppls_gram_tiles(p);
+  const int64_t slots = (int64_t)c->num_cus * ppls_gram_occupancy(c->dtype);
+  const double pp = (double)p * p;
+  int nsplit = 1;
+  double best = -1.0;
+  for (int sp = 1; sp <= 32; ++sp) {
+    if (sp > 1 && ((int64_t)sp * 512 > n || (double)sp * pp * 8.0 > 4.0e9)) break;
+    const int64_t w = (int64_t)ntiles * sp;
+    const double eff = (double)w / (double)(((w + slots - 1) / slots) * slots);
+    if (eff > best + 1e-9) { best = eff; nsplit = sp; }
+    if (eff >= 0.95) break;
+  }
+  return nsplit;
+}
+
+// Cross-product form (ppls_xprod.hip): S = [X Y]'[X Y] over the local rows on MFMA (fp64 products
+// of the stored values, exact for fp32 storage), summed over ranks by ONE all-reduce of P^2 doubles;
+// afterwards an iteration needs no collective at all (every rank holds the same S and theta).
+int xprod_setup(ppls_ctx* c) {
+  if (c->xp_ready) return PPLS_OK;
+  const int P = c->ldx + c->ldy;
+  const size_t PP = (size_t)P * P;
+  int rc;
+  const auto t0 = std::chrono::steady_clock::now();
+  if ((rc = dalloc(c, &c->xp_S, PP))) return rc;
+  c->xp_setup_ms = 0.0;
+  if (c->n_local > 0) {
+    const int nsplit = gram_splits(c, P, c->n_local);
+    c->xp_nsplit = nsplit;
+    double* part = nullptr;
+    if ((rc = dalloc(c, &part, (size_t)nsplit * PP))) return rc;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    hipError_t e = hipEventCreate(&e0);
+    if (e == hipSuccess) e = hipEventCreate(&e1);
+    if (e == hipSuccess) e = hipEventRecord(e0, c->stream);
+    if (e == hipSuccess)
+      e = ppls_launch_gram_joint(c->X, c->ldx, c->ldx, c->Y, c->ldy, c->ldy, c->dtype, c->n_local, P, nsplit, part,
+                                 (int64_t)PP, c->stream);
+    if (e == hipSuccess) e = ppls_launch_gram_finish(part, nsplit, (int64_t)PP, P, c->xp_S, c->stream);
+    if (e == hipSuccess) e = hipEventRecord(e1, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    float ms = 0.f;
+    if (e == hipSuccess) e = hipEventElapsedTime(&ms, e0, e1);
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    dfree(part);
+    if (e != hipSuccess) return fail(c, PPLS_E_HIP, "cross-products: %s", hipGetErrorString(e));
+    c->xp_setup_ms = ms;
+  } else {
+    HIPCHK(c, hipMemsetAsync(c->xp_S, 0, sizeof(double) * PP, c->stream));
+  }
+  if ((rc = allreduce(c, c->xp_S, PP))) return rc;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->xp_setup_total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  c->xp_ready = true;
+  return PPLS_OK;
+}
+
+// Whether a run of max_steps iterations reads S: option xprod = 1 always, 0 never, -1 when the
+// modelled cost of forming S plus max_steps + 1 passes over it undercuts max_steps + 1 streaming
+// sweeps.  The model uses only global sizes (n_total / nranks, never this rank's own row count or
+// free memory), so every rank of a sharded run takes the same path.
+bool xprod_choose(ppls_ctx* c, int max_steps) {
+  if (c->xprod == 0) return false;
+  const double P = (double)(c->ldx + c->ldy);
+  hipDeviceProp_t prop;
+  const double mem = hipGetDeviceProperties(&prop, c->device) == hipSuccess ? (double)prop.totalGlobalMem : 0.0;
+  if (8.0 * P * P * 2.0 > 0.25 * mem) return false;   // S and one split of partials within a quarter of HBM
+  if (c->xprod == 1) return true;
+  const double n = (double)((c->n_total + c->nranks - 1) / c->nranks);
+  const double esz = c->dtype ? 4.0 : 8.0;
+  const double t_sweep = esz * n * P / 6.5e12 + 5e-6;
+  const double t_pass = 8.0 * P * P / 6.5e12 + 5e-6;
+  const double t_setup = c->xp_ready ? 0.0 : n * P * P / 55e12 + (c->nranks > 1 ? 16.0 * P * P / 100e9 : 0.0);
+  return ((double)max_steps + 1.0) * (t_sweep - t_pass) > t_setup;
+}
+
+// One statistics step from S: c->stats for theta[slot] (no collective: S is global).
+int xprod_stats(ppls_ctx* c, int r, int slot) {
+  int rc;
+  const int P = c->ldx + c->ldy;
+  if (!c->xp_ready && (rc = xprod_setup(c))) return rc;
+  if (!c->xp_M) {
+    if ((rc = dalloc(c, &c->xp_M, (size_t)P * 2 * PPLS_RMAX))) return rc;
+  }
+  const int rw = ppls_xprod_rows_per_wave(P, r, c->xprod_rw);
+  hipEvent_t e0, e1;
+  if ((rc = timing_pair(c, &e0, &e1))) return rc;
+  if (e0) HIPCHK(c, hipEventRecord(e0, c->stream));
+  HIPCHK(c, ppls_launch_xprod_apply(c->xp_S, c->ldx, c->ldy, r, rw, c->W[slot], c->C[slot], c->sc[slot], c->stats,
+                                    c->xp_M, c->sweep_stop, c->stream));
+  if (e1) HIPCHK(c, hipEventRecord(e1, c->stream));
+  return PPLS_OK;
+}
+
+// The statistics of theta[slot] for an EM iteration: from S when the run reads the cross-products
+// (not for the mu write-out, which needs the rows), else one streaming sweep.
+int stats_step(ppls_ctx* c, int r, int slot, bool write_mu) {
+  if (c->xp_active && !write_mu && c->seg_rows < 0) return xprod_stats(c, r, slot);
+  return sweep(c, r, slot, write_mu);
 }
 
 // The device stop flag (2 ints) and its host-mapped mirror, allocated on first use.
@@ -636,6 +763,9 @@ int check_status(ppls_ctx* c) {
 
 int compute_ssq(ppls_ctx* c) {
   int rc;
+  c->xp_ready = false;   // data or communicator changed: the cross-products are stale
+  dfree(c->xp_S);
+  dfree(c->xp_M);
   const int nb = 1024;
   if ((rc = dalloc(c, &c->scratch, nb + 8))) return rc;
   HIPCHK(c, hipMemsetAsync(c->ssq, 0, 2 * sizeof(double), c->stream));
@@ -802,6 +932,8 @@ void ppls_ctx_destroy(ppls_ctx* c) {
   if (c->ftrace) (void)hipFree(c->ftrace);
   if (c->strace) (void)hipFree(c->strace);
   dfree(c->stop_d);
+  dfree(c->xp_S);
+  dfree(c->xp_M);
   dfree(c->bal_bounds);
   dfree(c->team_bar);
   dfree(c->team_part);
@@ -875,6 +1007,12 @@ int ppls_set_option(ppls_ctx* c, const char* key, int64_t value) {
   } else if (!strcmp(key, "nt")) {
     if (value < -1 || value > 1) return fail(c, PPLS_E_ARG, "nt must be -1 (auto), 0 or 1");
     c->nt_loads = (int)value;
+  } else if (!strcmp(key, "xprod")) {
+    if (value < -1 || value > 1) return fail(c, PPLS_E_ARG, "xprod must be -1 (auto), 0 (stream X, Y) or 1 (cross-products)");
+    c->xprod = (int)value;
+  } else if (!strcmp(key, "xprod_rw")) {
+    if (value != 0 && value != 1 && value != 2 && value != 4) return fail(c, PPLS_E_ARG, "xprod_rw must be 0, 1, 2 or 4");
+    c->xprod_rw = (int)value;
   } else if (!strcmp(key, "timing")) {
     if (value < 0) return fail(c, PPLS_E_ARG, "timing must be >= 0");
     c->timing = (int)value;
@@ -1256,6 +1394,9 @@ int ppls_em_run(ppls_ctx* c, ppls_theta* th, int r, int max_steps, double atol, 
   HIPCHK(c, hipMemsetAsync(c->status, 0, sizeof(int), c->stream));
   const bool want_mu = eout && (eout->mu_T || eout->mu_U);
   const bool do_check = !(atol == -INFINITY);   // atol = -Inf: the stop rule never fires
+  // statistics from the cross-products S (option xprod; formed here if needed, outside the loop)
+  c->xp_active = c->seg_rows < 0 && xprod_choose(c, max_steps);
+  if (c->xp_active && (rc = xprod_setup(c))) { c->xp_active = false; return rc; }
   // The stop rule (EM_W_multi.R:792) runs on the device: the finalize that sees
   // logl[i] - logl[i-1] < atol sets a flag, and every later kernel of the run exits at once, so the
   // host enqueues iterations without a per-iteration read-back.  It polls the flag's host-mapped
@@ -1275,6 +1416,7 @@ int ppls_em_run(ppls_ctx* c, ppls_theta* th, int r, int max_steps, double atol, 
     std::vector<hipEvent_t> evs;
     ~StopGuard() {
       c->sweep_stop = nullptr;
+      c->xp_active = false;
       for (auto e : evs) (void)hipEventDestroy(e);
     }
   } guard{c, {}};
@@ -1288,8 +1430,8 @@ int ppls_em_run(ppls_ctx* c, ppls_theta* th, int r, int max_steps, double atol, 
       if (fired != 0 && fired <= s - 1 - EM_LOOKAHEAD) break;   // converged: stop launching
     }
     const int nxt = cur ^ 1;
-    const bool wm = want_mu && (do_check || s == max_steps + 1);
-    if ((rc = sweep(c, r, cur, wm))) return rc;
+    const bool wm = want_mu && !c->xp_active && (do_check || s == max_steps + 1);
+    if ((rc = stats_step(c, r, cur, wm))) return rc;
     if ((rc = finalize(c, r, cur, nxt, s >= 2 ? s - 2 : -1, type, do_check && s >= 3 ? s : 0))) return rc;
     if (do_check) {
       const size_t k = (size_t)(s - 1) % EM_LOOKAHEAD;
@@ -1311,6 +1453,14 @@ int ppls_em_run(ppls_ctx* c, ppls_theta* th, int r, int max_steps, double atol, 
   cur = i_final & 1;
   HIPCHK(c, hipStreamSynchronize(c->stream));
   if ((rc = check_status(c))) return rc;
+  if (c->xp_active && want_mu) {
+    // Eout's mu_T, mu_U (:802) need the rows: one streaming sweep of theta_{i_final}, whose
+    // finalize (scalars only) also restates Eout's moments from that sweep
+    c->sweep_stop = nullptr;
+    if ((rc = sweep(c, r, cur, true))) return rc;
+    if ((rc = finalize(c, r, cur, cur ^ 1, -1, type, 0, true))) return rc;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+  }
   if (loglik) HIPCHK(c, hipMemcpy(loglik, c->loglik, sizeof(double) * i_final, hipMemcpyDeviceToHost));
   if (negative_increment) {
     std::vector<double> l(i_final);
@@ -2084,18 +2234,7 @@ int ppls_gram(ppls_ctx* c, int xory, int nsplit, double* G, double* ms) {
   const void* D = xory ? (const void*)c->Y : (const void*)c->X;
   const size_t pp = (size_t)p * p;
   if (c->n_local <= 0) return fail(c, PPLS_E_STATE, "no rows on this rank");
-  if (nsplit <= 0) {
-    const int ntiles = ppls_gram_tiles(p);
-    const int64_t slots = (int64_t)c->num_cus * ppls_gram_occupancy(c->dtype);
-    double best = -1.0;
-    for (int sp = 1; sp <= 32; ++sp) {
-      if (sp > 1 && ((int64_t)sp * 512 > c->n_local || (double)sp * pp * 8.0 > 4.0e9)) break;
-      const int64_t w = (int64_t)ntiles * sp;
-      const double eff = (double)w / (double)(((w + slots - 1) / slots) * slots);
-      if (eff > best + 1e-9) { best = eff; nsplit = sp; }
-      if (eff >= 0.95) break;
-    }
-  }
+  if (nsplit <= 0) nsplit = gram_splits(c, p, c->n_local);
   int rc;
   double *dpart = nullptr, *dG = nullptr;
   if ((rc = dalloc(c, &dpart, (size_t)nsplit * pp))) return rc;
@@ -2174,6 +2313,8 @@ int ppls_em_begin(ppls_ctx* c, const ppls_theta* th, int r) {
   c->em_r = r;
   c->em_cur = 0;
   c->em_iter = 0;
+  c->xp_active = c->seg_rows < 0 && xprod_choose(c, 1 << 16);
+  if (c->xp_active && (rc = xprod_setup(c))) { c->xp_active = false; return rc; }
   c->em_active = true;
   return PPLS_OK;
 }
@@ -2187,7 +2328,7 @@ int ppls_em_iterate(ppls_ctx* c, int nsteps, int type) {
   int rc;
   for (int s = 0; s < nsteps; ++s) {
     const int nxt = c->em_cur ^ 1;
-    if ((rc = sweep(c, c->em_r, c->em_cur, false))) return rc;
+    if ((rc = stats_step(c, c->em_r, c->em_cur, false))) return rc;
     if ((rc = finalize(c, c->em_r, c->em_cur, nxt, c->em_iter >= 1 ? c->em_iter - 1 : -1, type))) return rc;
     c->em_cur = nxt;
     ++c->em_iter;
@@ -2241,6 +2382,32 @@ int ppls_loglC_fast(ppls_ctx* c, const double* W, const double* C, const double*
   HIPCHK(c, ppls_launch_loglc(G, c->ssq, (double)c->n_total, p, q, a, sigX, sigY, c->coefs, c->loglik, c->stream));
   HIPCHK(c, hipMemcpyAsync(out, c->loglik, sizeof(double), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  return PPLS_OK;
+}
+
+int ppls_xprod_prepare(ppls_ctx* c, double* ms, double* total_ms) {
+  if (!c) return PPLS_E_ARG;
+  if (!c->have_data) return fail(c, PPLS_E_STATE, "no data");
+  HIPCHK(c, hipSetDevice(c->device));
+  const bool was = c->xp_ready;
+  int rc;
+  if ((rc = xprod_setup(c))) return rc;
+  if (ms) *ms = was ? 0.0 : c->xp_setup_ms;
+  if (total_ms) *total_ms = was ? 0.0 : c->xp_setup_total_ms;
+  return PPLS_OK;
+}
+
+int ppls_xprod_info(ppls_ctx* c, int r, int* ready, int64_t* bytes_per_pass, double* flops, int* rows_per_wave) {
+  if (!c) return PPLS_E_ARG;
+  if (!c->have_data) return fail(c, PPLS_E_STATE, "no data");
+  const int64_t P = (int64_t)c->ldx + c->ldy;
+  if (ready) *ready = c->xp_ready ? 1 : 0;
+  if (bytes_per_pass) *bytes_per_pass = 8 * P * P;
+  if (flops) {   // lower 128 x 128 tiles incl. the diagonal ones, 2 flops per multiply-add
+    const double nb = (double)((P + 127) / 128);
+    flops[0] = 2.0 * (double)c->n_local * nb * (nb + 1) / 2.0 * 128.0 * 128.0;
+  }
+  if (rows_per_wave) *rows_per_wave = ppls_xprod_rows_per_wave((int)P, r < 1 ? 1 : r, c->xprod_rw);
   return PPLS_OK;
 }
 

@@ -14,6 +14,7 @@
 #include <stdint.h>
 
 #include "ppls_kernels.h"
+#include "ppls_xprod.h"
 
 #define PPLS_GT 128   // output tile edge (4 waves x 64 x 64)
 #define PPLS_GK 16    // rows per LDS stage
@@ -52,10 +53,17 @@ struct GVec<float> {
 // transpose, since A[i][k] = X[k][i] and B[k][j] = X[k][j].  The next stage's global loads are in
 // flight during the MFMAs; one barrier per 16-row stage.  Output: part[s][i p + j] for the tile's
 // (i, j), i in block I >= block J (row-major of the lower blocks; coalesced over j).
+//
+// The column space is that of the joint matrix [X | Y] (ppls_xprod.hip's cross-product form of the
+// EM iteration): column c is X[:, c] for c < xcols and Y[:, c - xcols] for c - xcols < ycols (zero
+// beyond); xcols and ycols are multiples of the 16-B vector, so no load straddles the seam.  The
+// Gram of X alone is xcols = ld, ycols = 0, p the output edge.
 template <typename T>
-__global__ __launch_bounds__(256, 2) void ppls_gram_mfma_kernel(const T* __restrict__ X, int64_t n, int ld, int p,
-                                                                 int ntiles, int nsplit, int64_t work,
-                                                                 double* __restrict__ part, int64_t part_stride) {
+__global__ __launch_bounds__(256, 2) void ppls_gram_mfma_kernel(const T* __restrict__ X, int ldx, int xcols,
+                                                                 const T* __restrict__ Y, int ldy, int ycols,
+                                                                 int64_t n, int p, int ntiles, int nsplit,
+                                                                 int64_t work, double* __restrict__ part,
+                                                                 int64_t part_stride) {
   typedef double d4 __attribute__((ext_vector_type(4)));
   constexpr int EV = 16 / sizeof(T);              // elements per 16-B load
   constexpr int VPR = PPLS_GT / EV;               // 16-B vectors per panel row
@@ -81,8 +89,12 @@ __global__ __launch_bounds__(256, 2) void ppls_gram_mfma_kernel(const T* __restr
       const int c = tid + 256 * v, row = c / VPR, cv = c - row * VPR;
       const int64_t gr = k0 + row;
       const int ca = colA + cv * EV, cb = colB + cv * EV;
-      if (gr < r1 && ca < ld) ra[v].load(X + gr * ld + ca); else ra[v].zero();
-      if (gr < r1 && cb < ld) rb[v].load(X + gr * ld + cb); else rb[v].zero();
+      if (gr < r1 && ca < xcols) ra[v].load(X + gr * ldx + ca);
+      else if (gr < r1 && ca - xcols < ycols) ra[v].load(Y + gr * ldy + (ca - xcols));
+      else ra[v].zero();
+      if (gr < r1 && cb < xcols) rb[v].load(X + gr * ldx + cb);
+      else if (gr < r1 && cb - xcols < ycols) rb[v].load(Y + gr * ldy + (cb - xcols));
+      else rb[v].zero();
     }
   };
   auto store = [&](int buf) {
@@ -245,20 +257,27 @@ int ppls_gram_occupancy(int f32) {
   return e == hipSuccess && occ > 0 ? occ : 1;
 }
 
-hipError_t ppls_launch_gram(const void* X, int f32, int64_t n, int ld, int p, int nsplit, double* part,
-                            int64_t part_stride, hipStream_t st) {
-  if (n <= 0 || p <= 0 || nsplit < 1) return hipErrorInvalidValue;
+hipError_t ppls_launch_gram_joint(const void* X, int ldx, int xcols, const void* Y, int ldy, int ycols, int f32,
+                                  int64_t n, int p, int nsplit, double* part, int64_t part_stride, hipStream_t st) {
+  if (n <= 0 || p <= 0 || nsplit < 1 || xcols + ycols < 1) return hipErrorInvalidValue;
+  const int ev = f32 ? 4 : 2;
+  if (xcols % ev || ycols % ev) return hipErrorInvalidValue;
   const int ntiles = ppls_gram_tiles(p);
   const int64_t work = (int64_t)ntiles * nsplit;
   const int64_t grid = (work + 7) / 8 * 8;   // a multiple of 8: the XCD remap needs whole rounds
   if (grid > 0x7fffffff) return hipErrorInvalidValue;
   if (f32)
-    hipLaunchKernelGGL(ppls_gram_mfma_kernel<float>, dim3((unsigned)grid), dim3(256), 0, st, (const float*)X, n, ld,
-                       p, ntiles, nsplit, work, part, part_stride);
+    hipLaunchKernelGGL(ppls_gram_mfma_kernel<float>, dim3((unsigned)grid), dim3(256), 0, st, (const float*)X, ldx,
+                       xcols, (const float*)Y, ldy, ycols, n, p, ntiles, nsplit, work, part, part_stride);
   else
-    hipLaunchKernelGGL(ppls_gram_mfma_kernel<double>, dim3((unsigned)grid), dim3(256), 0, st, (const double*)X, n,
-                       ld, p, ntiles, nsplit, work, part, part_stride);
+    hipLaunchKernelGGL(ppls_gram_mfma_kernel<double>, dim3((unsigned)grid), dim3(256), 0, st, (const double*)X, ldx,
+                       xcols, (const double*)Y, ldy, ycols, n, p, ntiles, nsplit, work, part, part_stride);
   return hipGetLastError();
+}
+
+hipError_t ppls_launch_gram(const void* X, int f32, int64_t n, int ld, int p, int nsplit, double* part,
+                            int64_t part_stride, hipStream_t st) {
+  return ppls_launch_gram_joint(X, ld, ld, nullptr, 0, 0, f32, n, p, nsplit, part, part_stride, st);
 }
 
 hipError_t ppls_launch_gram_finish(const double* part, int nsplit, int64_t part_stride, int p, double* G,

@@ -1,0 +1,200 @@
+// ppls_xprod.hip -- the cross-product form of one PPLS_simult EM iteration (ppls_xprod.h).
+//
+// The reference reads X and Y about ten times per iteration; the streaming sweep
+// (ppls_kernels.hip) reads them once.  Every statistic of the iteration is a quadratic form in the
+// joint cross-product S = [X Y]'[X Y] (P x P, P = ldx + ldy; formed once per data set on MFMA by
+// ppls_gram_mfma_kernel), so an iteration here reads S instead: 8 P^2 bytes against
+// esz n (p + q) -- 128 MB against 32 GB at C3, and 128 MB fits the 256 MiB Infinity Cache.
+//
+//   ppls_xprod_apply_kernel  M = S B (B = blockdiag(W, C)) for RW rows of S per workgroup (its four
+//                            waves interleave over the columns), and from it
+//                            X'mu_T (:732), Y'mu_U (:733) rows: HBM/MALL-bound, one pass over S
+//   ppls_xprod_gram_kernel   Gram([Xw Yc]) = B'M (:696-712, loglC.cpp:335), one workgroup per
+//                            upper-triangle entry, mirrored (exactly symmetric, as the sweep's)
+// Row i of M needs row i of S only (S is symmetric, so rows and columns are interchangeable); W and
+// C are re-read from L1/L2 by every workgroup, RW rows of S share each load of them.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "ppls_device.h"
+#include "ppls_xprod.h"
+
+namespace {
+
+// Values a lane holds after ppls_rs's six butterfly levels on M values (M > 64: several).
+constexpr int ppls_rs_left(int m, int l) { return l == 6 ? m : (m == 1 ? 1 : ppls_rs_left((m + 1) / 2, l + 1)); }
+
+template <int R, int RW, bool NT>
+__global__ __launch_bounds__(256) void ppls_xprod_apply_kernel(const double* __restrict__ S, int ldx, int ldy,
+                                                               const double* __restrict__ Wp,
+                                                               const double* __restrict__ Cp,
+                                                               const PplsScalars* __restrict__ sc,
+                                                               double* __restrict__ stats, double* __restrict__ M,
+                                                               const int* __restrict__ stop) {
+  if (stop && *stop) return;   // em_run converged at an earlier iteration
+  constexpr int R2 = 2 * R, NV = RW * R2;
+  __shared__ double sm[4][NV];
+  const int P = ldx + ldy;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  // the workgroup's RW rows of S; its four waves take interleaved 128-column steps of each row
+  const int64_t i0 = (int64_t)blockIdx.x * RW;
+  const double* srow[RW];
+#pragma unroll
+  for (int rr = 0; rr < RW; ++rr) srow[rr] = S + (i0 + rr < P ? i0 + rr : (int64_t)P - 1) * P;   // rows past P: dropped
+  double acc[NV + 1];
+#pragma unroll
+  for (int v = 0; v <= NV; ++v) acc[v] = 0.0;
+  typedef double d2v __attribute__((ext_vector_type(2)));
+  auto lds2 = [](const double* a) -> d2v {
+    if constexpr (NT) return __builtin_nontemporal_load((const d2v*)a);
+    else return *(const d2v*)a;
+  };
+  const int j0 = 2 * lane + 128 * wave;
+  // X columns: M[i, k] += S[i, j] W[j, k], two columns j per lane and step (16-B loads)
+#pragma unroll 2
+  for (int j = j0; j < ldx; j += 512) {
+    d2v s[RW];
+#pragma unroll
+    for (int rr = 0; rr < RW; ++rr) s[rr] = lds2(srow[rr] + j);
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+      const d2v w = *(const d2v*)(Wp + (int64_t)k * ldx + j);
+#pragma unroll
+      for (int rr = 0; rr < RW; ++rr) acc[rr * R2 + k] = fma(s[rr].y, w.y, fma(s[rr].x, w.x, acc[rr * R2 + k]));
+    }
+  }
+  // Y columns: M[i, R + k] += S[i, ldx + j] C[j, k]
+#pragma unroll 2
+  for (int j = j0; j < ldy; j += 512) {
+    d2v s[RW];
+#pragma unroll
+    for (int rr = 0; rr < RW; ++rr) s[rr] = lds2(srow[rr] + ldx + j);
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+      const d2v cv = *(const d2v*)(Cp + (int64_t)k * ldy + j);
+#pragma unroll
+      for (int rr = 0; rr < RW; ++rr)
+        acc[rr * R2 + R + k] = fma(s[rr].y, cv.y, fma(s[rr].x, cv.x, acc[rr * R2 + R + k]));
+    }
+  }
+  // wave sums (reduce-scatter: lane ends with value(s) idx..), then the four waves in order
+  int idx = 0;
+  bool canon = true;
+  ppls_rs<NV, 0, NV + 1>(acc, lane, idx, canon);
+  constexpr int LEFT = ppls_rs_left(NV, 0);
+  if (canon) {
+#pragma unroll
+    for (int j = 0; j < LEFT; ++j)
+      if (idx + j < NV) sm[wave][idx + j] = acc[j];
+  }
+  __syncthreads();
+  if (threadIdx.x < NV) {
+    const int e = threadIdx.x;
+    const double v = (sm[0][e] + sm[1][e]) + (sm[2][e] + sm[3][e]);
+    const int rr = e / R2, b = e - rr * R2;
+    if (i0 + rr < P) M[(int64_t)b * P + i0 + rr] = v;
+    sm[0][e] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < RW * R) {
+    const int e = threadIdx.x;
+    const int rr = e / R, k = e - rr * R;
+    const int64_t i = i0 + rr;
+    if (i < P) {
+      const double mw = sm[0][rr * R2 + k], mc = sm[0][rr * R2 + R + k];
+      if (i < ldx) stats[(int64_t)k * ldx + i] = sc->alpha[k] * mw + sc->beta[k] * mc;   // X'mu_T
+      else stats[(int64_t)R * ldx + (int64_t)k * ldy + (i - ldx)] = sc->gamma[k] * mw + sc->delta[k] * mc;   // Y'mu_U
+    }
+  }
+}
+
+// Gram entry (a, b), a <= b, of B'M: sum over the rows where column a of B lives (X rows for
+// a < R, Y rows otherwise); written to (a, b) and (b, a).
+__global__ __launch_bounds__(256) void ppls_xprod_gram_kernel(int ldx, int ldy, int R, const double* __restrict__ Wp,
+                                                              const double* __restrict__ Cp,
+                                                              const double* __restrict__ M,
+                                                              double* __restrict__ stats,
+                                                              const int* __restrict__ stop) {
+  if (stop && *stop) return;
+  __shared__ double red[4];
+  const int R2 = 2 * R, P = ldx + ldy;
+  const int t = blockIdx.x;
+  int b = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
+  while ((b + 1) * (b + 2) / 2 <= t) ++b;
+  while (b * (b + 1) / 2 > t) --b;
+  const int a = t - b * (b + 1) / 2;
+  const double* Bcol = a < R ? Wp + (int64_t)a * ldx : Cp + (int64_t)(a - R) * ldy;
+  const double* Mcol = M + (int64_t)b * P + (a < R ? 0 : ldx);
+  const int rows = a < R ? ldx : ldy;
+  double v = 0.0;
+  for (int i = threadIdx.x; i < rows; i += 256) v = fma(Bcol[i], Mcol[i], v);
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const double g = (red[0] + red[1]) + (red[2] + red[3]);
+    double* G = stats + (int64_t)R * ldx + (int64_t)R * ldy;
+    G[(int64_t)b * R2 + a] = g;
+    G[(int64_t)a * R2 + b] = g;
+  }
+}
+
+template <int R, int RW>
+hipError_t launch_apply(const double* S, int ldx, int ldy, const double* Wp, const double* Cp, const PplsScalars* sc,
+                        double* stats, double* M, const int* stop, hipStream_t st) {
+  const int P = ldx + ldy;
+  const unsigned blocks = (unsigned)((P + RW - 1) / RW);
+  // S beyond the 256 MiB Infinity Cache is read once per iteration: non-temporal loads
+  if (8.0 * P * (double)P > 200.0 * (1 << 20))
+    hipLaunchKernelGGL((ppls_xprod_apply_kernel<R, RW, true>), dim3(blocks), dim3(256), 0, st, S, ldx, ldy, Wp, Cp, sc,
+                       stats, M, stop);
+  else
+    hipLaunchKernelGGL((ppls_xprod_apply_kernel<R, RW, false>), dim3(blocks), dim3(256), 0, st, S, ldx, ldy, Wp, Cp,
+                       sc, stats, M, stop);
+  return hipGetLastError();
+}
+
+template <int R>
+hipError_t launch_apply_rw(int rw, const double* S, int ldx, int ldy, const double* Wp, const double* Cp,
+                           const PplsScalars* sc, double* stats, double* M, const int* stop, hipStream_t st) {
+  if (rw == 1) return launch_apply<R, 1>(S, ldx, ldy, Wp, Cp, sc, stats, M, stop, st);
+  if (rw == 2) return launch_apply<R, 2>(S, ldx, ldy, Wp, Cp, sc, stats, M, stop, st);
+  if constexpr (R <= 8)
+    if (rw == 4) return launch_apply<R, 4>(S, ldx, ldy, Wp, Cp, sc, stats, M, stop, st);
+  return hipErrorInvalidValue;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ppls_xprod_rows_per_wave(int P, int r, int rw_opt) {
+  if (rw_opt == 1 || rw_opt == 2 || (rw_opt == 4 && r <= 8)) return rw_opt;
+  if (r <= 8 && P / 4 >= 1024) return 4;   // >= 4 workgroups per CU left at four rows per workgroup
+  return P / 2 >= 512 ? 2 : 1;
+}
+
+hipError_t ppls_launch_xprod_apply(const double* S, int ldx, int ldy, int r, int rw, const double* Wp,
+                                   const double* Cp, const PplsScalars* sc, double* stats, double* M,
+                                   const int* stop, hipStream_t st) {
+  if (ldx < 2 || ldy < 2 || (ldx & 1) || (ldy & 1) || r < 1 || r > PPLS_RMAX) return hipErrorInvalidValue;
+  if (((uintptr_t)S | (uintptr_t)Wp | (uintptr_t)Cp) & 15) return hipErrorInvalidValue;   // 16-B loads
+  hipError_t e;
+  switch (r) {
+#define PPLS_XP_CASE(k) \
+    case k: e = launch_apply_rw<k>(rw, S, ldx, ldy, Wp, Cp, sc, stats, M, stop, st); break;
+    PPLS_XP_CASE(1) PPLS_XP_CASE(2) PPLS_XP_CASE(3) PPLS_XP_CASE(4) PPLS_XP_CASE(5) PPLS_XP_CASE(6)
+    PPLS_XP_CASE(7) PPLS_XP_CASE(8) PPLS_XP_CASE(9) PPLS_XP_CASE(10) PPLS_XP_CASE(11) PPLS_XP_CASE(12)
+    PPLS_XP_CASE(13) PPLS_XP_CASE(14) PPLS_XP_CASE(15) PPLS_XP_CASE(16)
+#undef PPLS_XP_CASE
+    default: return hipErrorInvalidValue;
+  }
+  if (e != hipSuccess) return e;
+  const int R2 = 2 * r;
+  hipLaunchKernelGGL(ppls_xprod_gram_kernel, dim3((unsigned)(R2 * (R2 + 1) / 2)), dim3(256), 0, st, ldx, ldy, r, Wp,
+                     Cp, M, stats, stop);
+  return hipGetLastError();
+}
+
+}  // extern "C"
