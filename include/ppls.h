@@ -95,7 +95,9 @@ const char* ppls_last_error(const ppls_ctx* ctx);
  *                per iteration; 1 from the cross-products S = [X Y]'[X Y], formed once per data set
  *                on MFMA and all-reduced once, after which an iteration reads S (8 (p+q)^2 bytes) and
  *                needs no collective; -1 auto: S when a cost model of max_steps iterations says so),
- *       "xprod_rw" (rows of S per workgroup of the cross-product kernel: 0 auto, 1, 2, 4) */
+ *       "xprod_kernel" (cross-product kernel: 0 row tiles with W, C staged in LDS (default), 1 row
+ *                       groups reading W, C from L1/L2),
+ *       "xprod_rw" (rows of S per wave of that kernel: 0 auto, 1, 2, 4) */
 int ppls_set_option(ppls_ctx* ctx, const char* key, int64_t value);
 
 /* ---- multi-GPU: samples are sharded over ranks; one RCCL all-reduce per EM iteration ---- */
@@ -258,7 +260,7 @@ int ppls_comm_info(ppls_ctx* ctx, int* nranks, int* rank, double* allreduce_ms, 
 int ppls_xprod_prepare(ppls_ctx* ctx, double* ms, double* total_ms);
 /* Its state: *ready = S is formed for the current data, *bytes_per_pass = 8 P^2 (one iteration's
  * algorithmic read, P = padded p + q), *flops = 2 n_local P^2 of the Gram as computed (lower tiles:
- * ~ half the full product), *rows_per_wave = rows of S per workgroup of the apply kernel for r components. */
+ * ~ half the full product), *rows_per_wave = rows of S per wave of the apply kernel for r components. */
 int ppls_xprod_info(ppls_ctx* ctx, int r, int* ready, int64_t* bytes_per_pass, double* flops, int* rows_per_wave);
 /* Shape facts for the roofline: bytes of X and Y one sweep reads (algorithmic), kernel variant. */
 int ppls_sweep_info(ppls_ctx* ctx, int r, int64_t* bytes_per_sweep, int* variant, int* grid);

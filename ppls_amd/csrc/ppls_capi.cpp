@@ -113,6 +113,7 @@ struct ppls_ctx {
   // cross-product form of the iteration (ppls_xprod.hip): S = [X Y]'[X Y] (P x P, P = ldx + ldy)
   // formed once per data set, then every statistics step reads S instead of X and Y
   int xprod = 0;            // option "xprod": 0 stream X, Y (default), 1 cross-products, -1 auto (cost model)
+  int xprod_kernel = 0;     // option "xprod_kernel": 0 row tiles with B in LDS (default), 1 row groups (A/B)
   int xprod_rw = 0;         // option "xprod_rw": rows of S per wave of the apply kernel (0 auto)
   bool xp_ready = false;    // S holds the (all-reduced) cross-products of the current data
   bool xp_active = false;   // statistics steps of the current run read S
@@ -716,12 +717,13 @@ int xprod_stats(ppls_ctx* c, int r, int slot) {
   if (!c->xp_M) {
     if ((rc = dalloc(c, &c->xp_M, (size_t)P * 2 * PPLS_RMAX))) return rc;
   }
-  const int rw = ppls_xprod_rows_per_wave(P, r, c->xprod_rw);
+  const int rw = c->xprod_kernel == 1 ? ppls_xprod_rows_per_wave(P, r, c->xprod_rw)
+                                     : ppls_xprod_tile_rows(P, r, c->xprod_rw, c->num_cus);
   hipEvent_t e0, e1;
   if ((rc = timing_pair(c, &e0, &e1))) return rc;
   if (e0) HIPCHK(c, hipEventRecord(e0, c->stream));
-  HIPCHK(c, ppls_launch_xprod_apply(c->xp_S, c->ldx, c->ldy, r, rw, c->W[slot], c->C[slot], c->sc[slot], c->stats,
-                                    c->xp_M, c->sweep_stop, c->stream));
+  HIPCHK(c, ppls_launch_xprod_apply(c->xp_S, c->ldx, c->ldy, r, c->xprod_kernel, rw, c->W[slot], c->C[slot],
+                                    c->sc[slot], c->stats, c->xp_M, c->sweep_stop, c->stream));
   if (e1) HIPCHK(c, hipEventRecord(e1, c->stream));
   return PPLS_OK;
 }
@@ -766,6 +768,7 @@ int compute_ssq(ppls_ctx* c) {
   c->xp_ready = false;   // data or communicator changed: the cross-products are stale
   dfree(c->xp_S);
   dfree(c->xp_M);
+
   const int nb = 1024;
   if ((rc = dalloc(c, &c->scratch, nb + 8))) return rc;
   HIPCHK(c, hipMemsetAsync(c->ssq, 0, 2 * sizeof(double), c->stream));
@@ -1010,6 +1013,9 @@ int ppls_set_option(ppls_ctx* c, const char* key, int64_t value) {
   } else if (!strcmp(key, "xprod")) {
     if (value < -1 || value > 1) return fail(c, PPLS_E_ARG, "xprod must be -1 (auto), 0 (stream X, Y) or 1 (cross-products)");
     c->xprod = (int)value;
+  } else if (!strcmp(key, "xprod_kernel")) {
+    if (value != 0 && value != 1) return fail(c, PPLS_E_ARG, "xprod_kernel must be 0 (row tiles) or 1 (row groups)");
+    c->xprod_kernel = (int)value;
   } else if (!strcmp(key, "xprod_rw")) {
     if (value != 0 && value != 1 && value != 2 && value != 4) return fail(c, PPLS_E_ARG, "xprod_rw must be 0, 1, 2 or 4");
     c->xprod_rw = (int)value;
@@ -1535,7 +1541,7 @@ int rank1_sweep(ppls_ctx* c, const Rank1& t, const std::vector<double>& Wp, cons
                 int m, std::vector<double>& SX, std::vector<double>& SY, double G[4]) {
   int rc;
   if ((rc = rank1_stage(c, t, Wp, Cp, m))) return rc;
-  if ((rc = sweep(c, 1, 0, false))) return rc;
+  if ((rc = stats_step(c, 1, 0, false))) return rc;
   std::vector<double> st((size_t)c->part_ld);
   HIPCHK(c, hipMemcpyAsync(st.data(), c->stats, sizeof(double) * c->part_ld, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -1635,7 +1641,7 @@ int rank1_fit_device(ppls_ctx* c, Rank1Dev& d, Rank1& t, const ppls_constraint* 
       const int ended = __atomic_load_n(c->stop_mirror, __ATOMIC_ACQUIRE);
       if (ended != 0 && ended - 1 <= step - LOOKAHEAD) break;   // the fit ended
     }
-    if ((rc = sweep(c, 1, 0, false))) return rc;
+    if ((rc = stats_step(c, 1, 0, false))) return rc;
     a.step = step;
     HIPCHK(c, ppls_launch_rank1_step(&a, c->stream));
     {
@@ -1717,6 +1723,14 @@ int ppls_ppls_ex(ppls_ctx* c, int a, int max_steps, double atol, int crit_abs, c
   HIPCHK(c, hipSetDevice(c->device));
   int rc;
   if ((rc = ensure_r(c, 1, max_steps))) return rc;
+  // the rank-1 steps' statistics from the cross-products S (option xprod): the sweep's weights are
+  // the deflated P_0..P_{m-1} w, so S blockdiag(P w, P c) gives exactly the sweep's X'mu_T and Gram
+  c->xp_active = c->seg_rows < 0 && xprod_choose(c, a * max_steps);
+  if (c->xp_active && (rc = xprod_setup(c))) { c->xp_active = false; return rc; }
+  struct XpGuard {
+    ppls_ctx* c;
+    ~XpGuard() { c->xp_active = false; }
+  } xp_guard{c};
   const int p = c->p, q = c->q;
   const double N = (double)c->n_total;
   double ssqX = c->ssq_host[0], ssqY = c->ssq_host[1];   // ||Xc||^2, ||Yc||^2 of the current deflation
@@ -2407,7 +2421,9 @@ int ppls_xprod_info(ppls_ctx* c, int r, int* ready, int64_t* bytes_per_pass, dou
     const double nb = (double)((P + 127) / 128);
     flops[0] = 2.0 * (double)c->n_local * nb * (nb + 1) / 2.0 * 128.0 * 128.0;
   }
-  if (rows_per_wave) *rows_per_wave = ppls_xprod_rows_per_wave((int)P, r < 1 ? 1 : r, c->xprod_rw);
+  if (rows_per_wave)
+    *rows_per_wave = c->xprod_kernel == 1 ? ppls_xprod_rows_per_wave((int)P, r < 1 ? 1 : r, c->xprod_rw)
+                                          : ppls_xprod_tile_rows((int)P, r < 1 ? 1 : r, c->xprod_rw, c->num_cus);
   return PPLS_OK;
 }
 

@@ -21,16 +21,18 @@ extern "C" {
 hipError_t ppls_launch_gram_joint(const void* X, int ldx, int xcols, const void* Y, int ldy, int ycols, int f32,
                                   int64_t n, int p, int nsplit, double* part, int64_t part_stride, hipStream_t st);
 
-// Rows of S per workgroup of the apply kernel (rw_opt > 0 forces 1, 2 or 4 where instantiated).
+// Rows of S per wave of the apply kernels (rw_opt > 0 forces 1, 2 or 4 where instantiated):
+// kind 1 (row groups without LDS) and kind 0 (row tiles, B staged in LDS; the default).
 int ppls_xprod_rows_per_wave(int P, int r, int rw_opt);
+int ppls_xprod_tile_rows(int P, int r, int rw_opt, int num_cus);
 
 // One iteration's statistics from S (P x P row-major, P = ldx + ldy, symmetric) and theta = (Wp, Cp,
 // sc): stats = [X'mu_T (ldx x r) | Y'mu_U (ldy x r) | Gram (2r x 2r)], the layout the sweeps'
-// reduction writes.  Two launches: the apply kernel streams S once (rw rows per workgroup), writes the
-// X'mu_T, Y'mu_U rows and M = S B (P x 2r column-major, scratch); the Gram kernel forms B'M, one
-// workgroup per entry (fixed-order sums: deterministic).  stop: the em_run stop flag (both kernels
-// exit if it is set) or nullptr.
-hipError_t ppls_launch_xprod_apply(const double* S, int ldx, int ldy, int r, int rw, const double* Wp,
-                                   const double* Cp, const PplsScalars* sc, double* stats, double* M,
-                                   const int* stop, hipStream_t st);
+// reduction writes.  Two launches: the apply kernel (kind 0 row tiles, kind 1 row groups; rw rows
+// per wave) streams S once and writes the X'mu_T, Y'mu_U rows and M = S B (P x 2r column-major,
+// scratch); the Gram kernel forms B'M, one workgroup per entry (fixed-order sums: deterministic).
+// stop: the em_run stop flag (both kernels exit if it is set) or nullptr.
+hipError_t ppls_launch_xprod_apply(const double* S, int ldx, int ldy, int r, int kind, int rw, const double* Wp,
+                                   const double* Cp, const PplsScalars* sc, double* stats, double* M, const int* stop,
+                                   hipStream_t st);
 }

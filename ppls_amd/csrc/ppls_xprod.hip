@@ -6,9 +6,11 @@
 // ppls_gram_mfma_kernel), so an iteration here reads S instead: 8 P^2 bytes against
 // esz n (p + q) -- 128 MB against 32 GB at C3, and 128 MB fits the 256 MiB Infinity Cache.
 //
-//   ppls_xprod_apply_kernel  M = S B (B = blockdiag(W, C)) for RW rows of S per workgroup (its four
-//                            waves interleave over the columns), and from it
-//                            X'mu_T (:732), Y'mu_U (:733) rows: HBM/MALL-bound, one pass over S
+//   ppls_xprod_tile_kernel   M = S B (B = blockdiag(W, C)) by row groups of S walking 128-column
+//                            tiles, B staged in LDS per tile (default), and from it X'mu_T (:732),
+//                            Y'mu_U (:733) rows: HBM/MALL-bound, one pass over S
+//   ppls_xprod_apply_kernel  the same without LDS (option xprod_kernel = 1; W, C re-read per row
+//                            group from L1/L2: that traffic bounds it at wide p and large r)
 //   ppls_xprod_gram_kernel   Gram([Xw Yc]) = B'M (:696-712, loglC.cpp:335), one workgroup per
 //                            upper-triangle entry, mirrored (exactly symmetric, as the sweep's)
 // Row i of M needs row i of S only (S is symmetric, so rows and columns are interchangeable); W and
@@ -18,6 +20,10 @@
 
 #include "ppls_device.h"
 #include "ppls_xprod.h"
+
+#ifndef PPLS_XP_DEPTH
+#define PPLS_XP_DEPTH 2   // 128-column tiles of S in flight per wave in the row-tile kernel (2, 3, 4, 6: same within 1 %, 6 slower at r = 10)
+#endif
 
 namespace {
 
@@ -108,6 +114,131 @@ __global__ __launch_bounds__(256) void ppls_xprod_apply_kernel(const double* __r
   }
 }
 
+// Row-tile form (the default): a workgroup owns 4 RW rows of S (RW per wave) and walks the columns
+// in tiles of 128 -- first the X columns, then the Y columns.  Each tile's 128 x R values of B (W on
+// X columns, C on Y columns) are staged in LDS once per workgroup and read by all its rows, so W and
+// C cost ~R / (4 RW) of S's traffic from L2 (the row-group kernel above re-reads them per RW rows
+// from L1/L2: R / RW, which bounds it at wide p and large r).  S tiles stream through a register
+// ring PPLS_XP_DEPTH tiles ahead (enough bytes in flight per CU to cover HBM/MALL latency: one
+// 128-column tile is only 1 KB per wave and row), B one tile ahead through LDS; one barrier per tile.
+template <int R, int RW, bool NT>
+__device__ __forceinline__ void ppls_xprod_tile_phase(const double* const (&srow)[RW], const double* __restrict__ Bsrc,
+                                                      int ldb, int width, int soff, double (&acc)[RW * R + 1],
+                                                      double* __restrict__ sB, int lane) {
+  typedef double d2v __attribute__((ext_vector_type(2)));
+  constexpr int NB = (R * 64 + 255) / 256;   // 16-B B loads per thread and tile
+  constexpr int D = PPLS_XP_DEPTH;           // S tiles in flight per wave (register ring)
+  const int tid = threadIdx.x;
+  const int ntile = (width + 127) >> 7;
+  if (ntile == 0) return;
+  d2v bn[NB], ring[D][RW];
+  auto ld_s = [&](int n, d2v (&dst)[RW]) {   // tile n: S values of this lane's two columns
+    const int c = (n << 7) + 2 * lane;
+#pragma unroll
+    for (int rr = 0; rr < RW; ++rr) {
+      if (c < width) {
+        if constexpr (NT) dst[rr] = __builtin_nontemporal_load((const d2v*)(srow[rr] + soff + c));
+        else dst[rr] = *(const d2v*)(srow[rr] + soff + c);
+      } else {
+        dst[rr] = d2v{0.0, 0.0};
+      }
+    }
+  };
+  auto ld_b = [&](int n) {   // tile n: this thread's share of the 128 x R values of B
+#pragma unroll
+    for (int v = 0; v < NB; ++v) {
+      const int e = tid + 256 * v, t = e >> 6, cb = (n << 7) + 2 * (e & 63);
+      bn[v] = (e < R * 64 && cb < width) ? *(const d2v*)(Bsrc + (int64_t)t * ldb + cb) : d2v{0.0, 0.0};
+    }
+  };
+  auto st_b = [&](int buf) {
+#pragma unroll
+    for (int v = 0; v < NB; ++v) {
+      const int e = tid + 256 * v;
+      if (e < R * 64) ((d2v*)sB)[buf * R * 64 + e] = bn[v];
+    }
+  };
+#pragma unroll
+  for (int u = 0; u < D - 1; ++u)
+    if (u < ntile) ld_s(u, ring[u]);
+  ld_b(0);
+  st_b(0);
+  __syncthreads();
+  for (int n0 = 0; n0 < ntile; n0 += D) {
+#pragma unroll
+    for (int u = 0; u < D; ++u) {
+      const int n = n0 + u;
+      if (n >= ntile) break;
+      // B of the next tile first: the wait for it before st_b (vmcnt counts in issue order) then
+      // leaves the S loads issued after it in flight
+      if (n + 1 < ntile) ld_b(n + 1);
+      if (n + D - 1 < ntile) ld_s(n + D - 1, ring[(u + D - 1) % D]);
+      const d2v* b = (const d2v*)sB + (n & 1) * R * 64 + lane;
+#pragma unroll
+      for (int t = 0; t < R; ++t) {
+        const d2v bv = b[t * 64];
+#pragma unroll
+        for (int rr = 0; rr < RW; ++rr)
+          acc[rr * R + t] = fma(ring[u][rr].y, bv.y, fma(ring[u][rr].x, bv.x, acc[rr * R + t]));
+      }
+      if (n + 1 < ntile) st_b((n + 1) & 1);
+      __syncthreads();
+    }
+  }
+}
+
+template <int R, int RW, bool NT>
+__global__ __launch_bounds__(256) void ppls_xprod_tile_kernel(const double* __restrict__ S, int ldx, int ldy,
+                                                              const double* __restrict__ Wp,
+                                                              const double* __restrict__ Cp,
+                                                              const PplsScalars* __restrict__ sc,
+                                                              double* __restrict__ stats, double* __restrict__ M,
+                                                              const int* __restrict__ stop) {
+  if (stop && *stop) return;   // em_run converged at an earlier iteration
+  constexpr int R2 = 2 * R, NV = RW * R;
+  __shared__ double sB[2 * R * 128];
+  __shared__ double sm[4][RW * R2];
+  const int P = ldx + ldy;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t i0 = ((int64_t)blockIdx.x * 4 + wave) * RW;   // this wave's first row of S
+  const double* srow[RW];
+#pragma unroll
+  for (int rr = 0; rr < RW; ++rr) srow[rr] = S + (i0 + rr < P ? i0 + rr : (int64_t)P - 1) * P;   // rows past P: dropped
+  constexpr int LEFT = ppls_rs_left(NV, 0);
+#pragma unroll
+  for (int ph = 0; ph < 2; ++ph) {   // X columns with W, then Y columns with C
+    double acc[NV + 1];
+#pragma unroll
+    for (int v = 0; v <= NV; ++v) acc[v] = 0.0;
+    if (ph == 0) ppls_xprod_tile_phase<R, RW, NT>(srow, Wp, ldx, ldx, 0, acc, sB, lane);
+    else ppls_xprod_tile_phase<R, RW, NT>(srow, Cp, ldy, ldy, ldx, acc, sB, lane);
+    int idx = 0;
+    bool canon = true;
+    ppls_rs<NV, 0, NV + 1>(acc, lane, idx, canon);
+    if (canon) {
+#pragma unroll
+      for (int j = 0; j < LEFT; ++j)
+        if (idx + j < NV) {
+          const int rr = (idx + j) / R, t = idx + j - rr * R;
+          sm[wave][rr * R2 + ph * R + t] = acc[j];
+        }
+    }
+  }
+  __syncthreads();
+  for (int e = lane; e < RW * R2; e += 64) {
+    const int rr = e / R2, b = e - rr * R2;
+    if (i0 + rr < P) M[(int64_t)b * P + i0 + rr] = sm[wave][e];
+  }
+  for (int e = lane; e < RW * R; e += 64) {
+    const int rr = e / R, t = e - rr * R;
+    const int64_t i = i0 + rr;
+    if (i >= P) continue;
+    const double mw = sm[wave][rr * R2 + t], mc = sm[wave][rr * R2 + R + t];
+    if (i < ldx) stats[(int64_t)t * ldx + i] = sc->alpha[t] * mw + sc->beta[t] * mc;   // X'mu_T
+    else stats[(int64_t)R * ldx + (int64_t)t * ldy + (i - ldx)] = sc->gamma[t] * mw + sc->delta[t] * mc;   // Y'mu_U
+  }
+}
+
 // Gram entry (a, b), a <= b, of B'M: sum over the rows where column a of B lives (X rows for
 // a < R, Y rows otherwise); written to (a, b) and (b, a).
 __global__ __launch_bounds__(256) void ppls_xprod_gram_kernel(int ldx, int ldy, int R, const double* __restrict__ Wp,
@@ -165,6 +296,30 @@ hipError_t launch_apply_rw(int rw, const double* S, int ldx, int ldy, const doub
   return hipErrorInvalidValue;
 }
 
+template <int R, int RW>
+hipError_t launch_tile(const double* S, int ldx, int ldy, const double* Wp, const double* Cp, const PplsScalars* sc,
+                       double* stats, double* M, const int* stop, hipStream_t st) {
+  const int P = ldx + ldy;
+  const unsigned blocks = (unsigned)((P + 4 * RW - 1) / (4 * RW));
+  if (8.0 * P * (double)P > 200.0 * (1 << 20))   // S beyond the Infinity Cache: non-temporal loads
+    hipLaunchKernelGGL((ppls_xprod_tile_kernel<R, RW, true>), dim3(blocks), dim3(256), 0, st, S, ldx, ldy, Wp, Cp, sc,
+                       stats, M, stop);
+  else
+    hipLaunchKernelGGL((ppls_xprod_tile_kernel<R, RW, false>), dim3(blocks), dim3(256), 0, st, S, ldx, ldy, Wp, Cp,
+                       sc, stats, M, stop);
+  return hipGetLastError();
+}
+
+template <int R>
+hipError_t launch_tile_rw(int rw, const double* S, int ldx, int ldy, const double* Wp, const double* Cp,
+                          const PplsScalars* sc, double* stats, double* M, const int* stop, hipStream_t st) {
+  if (rw == 1) return launch_tile<R, 1>(S, ldx, ldy, Wp, Cp, sc, stats, M, stop, st);
+  if (rw == 2) return launch_tile<R, 2>(S, ldx, ldy, Wp, Cp, sc, stats, M, stop, st);
+  if constexpr (R <= 8)
+    if (rw == 4) return launch_tile<R, 4>(S, ldx, ldy, Wp, Cp, sc, stats, M, stop, st);
+  return hipErrorInvalidValue;
+}
+
 }  // namespace
 
 extern "C" {
@@ -175,15 +330,23 @@ int ppls_xprod_rows_per_wave(int P, int r, int rw_opt) {
   return P / 2 >= 512 ? 2 : 1;
 }
 
-hipError_t ppls_launch_xprod_apply(const double* S, int ldx, int ldy, int r, int rw, const double* Wp,
-                                   const double* Cp, const PplsScalars* sc, double* stats, double* M,
-                                   const int* stop, hipStream_t st) {
+int ppls_xprod_tile_rows(int P, int r, int rw_opt, int num_cus) {
+  if (rw_opt == 1 || rw_opt == 2 || (rw_opt == 4 && r <= 8)) return rw_opt;
+  return P / 8 >= 2 * num_cus ? 2 : 1;   // two rows per wave while >= 2 workgroups per CU remain
+}
+
+hipError_t ppls_launch_xprod_apply(const double* S, int ldx, int ldy, int r, int kind, int rw, const double* Wp,
+                                   const double* Cp, const PplsScalars* sc, double* stats, double* M, const int* stop,
+                                   hipStream_t st) {
   if (ldx < 2 || ldy < 2 || (ldx & 1) || (ldy & 1) || r < 1 || r > PPLS_RMAX) return hipErrorInvalidValue;
   if (((uintptr_t)S | (uintptr_t)Wp | (uintptr_t)Cp) & 15) return hipErrorInvalidValue;   // 16-B loads
   hipError_t e;
   switch (r) {
-#define PPLS_XP_CASE(k) \
-    case k: e = launch_apply_rw<k>(rw, S, ldx, ldy, Wp, Cp, sc, stats, M, stop, st); break;
+#define PPLS_XP_CASE(k)                                                                                  \
+    case k:                                                                                              \
+      e = kind == 0 ? launch_tile_rw<k>(rw, S, ldx, ldy, Wp, Cp, sc, stats, M, stop, st)                  \
+                    : launch_apply_rw<k>(rw, S, ldx, ldy, Wp, Cp, sc, stats, M, stop, st);               \
+      break;
     PPLS_XP_CASE(1) PPLS_XP_CASE(2) PPLS_XP_CASE(3) PPLS_XP_CASE(4) PPLS_XP_CASE(5) PPLS_XP_CASE(6)
     PPLS_XP_CASE(7) PPLS_XP_CASE(8) PPLS_XP_CASE(9) PPLS_XP_CASE(10) PPLS_XP_CASE(11) PPLS_XP_CASE(12)
     PPLS_XP_CASE(13) PPLS_XP_CASE(14) PPLS_XP_CASE(15) PPLS_XP_CASE(16)

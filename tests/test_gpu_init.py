@@ -23,10 +23,12 @@ GOLD = os.path.join(os.path.dirname(__file__), "golden")
 SEQ = sorted(f for f in os.listdir(GOLD) if f.startswith("seq_") and f.endswith(".npz"))
 
 
-@pytest.fixture(scope="module")
-def ctx():
+@pytest.fixture(scope="module", params=[0, 1], ids=["stream", "xprod"])
+def ctx(request):
+    """Every test on both statistics paths: streaming sweeps, and the cross-products S (option xprod)."""
     from ppls_amd import Context
     c = Context(0)
+    c.set_option("xprod", request.param)
     yield c
     c.close()
 

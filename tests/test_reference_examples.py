@@ -74,11 +74,15 @@ def test_oracle_reproduces_printed_example(name):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("xprod", [0, 1], ids=["stream", "xprod"])
 @pytest.mark.parametrize("name", list(EXAMPLES))
-def test_device_reproduces_printed_example(name):
+def test_device_reproduces_printed_example(name, xprod):
+    """Both statistics paths: one streaming sweep per EM step, or the cross-products S (the printed
+    step counts are exact integers, so the reordered sums must not move a single stop decision)."""
     from ppls_amd import PPLS, Context, print_PPLS
     a, inits, cons, table = EXAMPLES[name]
     with Context(0) as ctx:
+        ctx.set_option("xprod", xprod)
         if name == "random":
             # the R stream itself drives the API's 'random' initial guess
             exX, exY, rng = ppls_example_data()
@@ -95,13 +99,15 @@ def test_device_reproduces_printed_example(name):
 
 
 @pytest.mark.gpu
-def test_device_ppls_simult_default_init_from_r_stream():
+@pytest.mark.parametrize("xprod", [0, 1], ids=["stream", "xprod"])
+def test_device_ppls_simult_default_init_from_r_stream(xprod):
     """PPLS_simult(exX, exY, a) with its default init PPLS(X, Y, a, 20, 1e-4, 'random') drawn from
     R's stream after set.seed(1) + the data draws (EM_W_multi.R:762-806) vs the oracle."""
     from ppls_amd import PPLS_simult, Context
     exX, exY, rng = ppls_example_data()
     exX2, exY2, rng2 = ppls_example_data()
     with Context(0) as ctx:
+        ctx.set_option("xprod", xprod)
         out = PPLS_simult(exX, exY, 2, EMsteps=50, atol=1e-4, ctx=ctx, rng=rng)
     f0 = o.ppls(exX2, exY2, 2, 20, 1e-4, theta0s=[o.initial_guess(P, Q, "random", rng2) for _ in range(2)])
     ref = o.ppls_simult(exX2, exY2, 2, EMsteps=50, atol=1e-4, theta0=o.simult_theta0_from_ppls(f0))
