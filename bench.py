@@ -72,6 +72,20 @@ def load_traffic(workload_key):
         return None
 
 
+def load_xprod_traffic(config):
+    """Read bytes per launch of the cross-product tile kernel from a committed rocprofv3 PMC pass
+    (profiles/pmc_xprod_<config>_dp1.json), or None."""
+    try:
+        with open(os.path.join(ROOT, "profiles", f"pmc_xprod_{config}_dp1.json")) as f:
+            ks = json.load(f)["kernels"]
+    except (OSError, ValueError, KeyError):
+        return None
+    for name, k in ks.items():
+        if "tile" in name:
+            return k.get("read_bytes_per_launch")
+    return None
+
+
 def load_compute_counters(workload_key, kernel_sub):
     """Counter-based MFMA / VALU utilisation of a kernel from a committed rocprofv3 PMC pass
     (profiles/pmc_compute_<workload>.json, tools/pmc_compute.sh + pmc_compute_summary.py), or None."""
@@ -189,10 +203,12 @@ def bench_xprod(ctx, th0, args, barrier, dist, torch, r, ll_stream, t_stream):
         setup_s=t_setup, gram_kernel_ms=gram_ms, gram_tflops=gram_tf,
         gram_roofline=dict(bound="mfma", achieved=gram_tf, peak=FP64_PEAK_TF, unit="TFLOP/s",
                            frac=(gram_tf / FP64_PEAK_TF) if gram_tf else None,
-                           flops_per_launch=info["gram_flops"]),
+                           flops_per_launch=info["gram_flops"],
+                           counters=load_compute_counters(f"{args.config}_dp1", "gram_mfma")),
         steps=args.xprod_steps, ms_per_step=1e3 * t_x, it_per_s=1.0 / t_x,
         roofline=dict(bound="hbm", achieved=achieved, peak=HBM_PEAK_GBS, unit="GB/s",
-                      frac=(achieved / HBM_PEAK_GBS) if achieved else None, kernel="xprod_apply + xprod_gram",
+                      frac=(achieved / HBM_PEAK_GBS) if achieved else None, kernel="xprod_tile + xprod_gram",
+                      traffic=load_xprod_traffic(args.config),
                       avg_kernel_us=avg_us, bytes_per_launch=info["bytes_per_pass"],
                       rows_per_workgroup=info["rows_per_wave"]),
         loglik_rel_diff_vs_streaming=rel, loglik_compared=k,
