@@ -95,9 +95,10 @@ const char* ppls_last_error(const ppls_ctx* ctx);
  *                per iteration; 1 from the cross-products S = [X Y]'[X Y], formed once per data set
  *                on MFMA and all-reduced once, after which an iteration reads S (8 (p+q)^2 bytes) and
  *                needs no collective; -1 auto: S when a cost model of max_steps iterations says so),
- *       "xprod_kernel" (cross-product kernel: 0 row tiles with W, C staged in LDS (default), 1 row
- *                       groups reading W, C from L1/L2),
- *       "xprod_rw" (rows of S per wave of that kernel: 0 auto, 1, 2, 4) */
+ *       "xprod_kernel" (cross-product kernel: 0 auto (3 for r <= 10, else 2), 1 row groups reading
+ *                       W, C from L1/L2, 2 row tiles with W, C staged in LDS, 3 lower triangle: each
+ *                       off-diagonal tile of the symmetric S read once for its rows and its columns),
+ *       "xprod_rw" (rows of S per wave of kernels 1 and 2: 0 auto, 1, 2, 4) */
 int ppls_set_option(ppls_ctx* ctx, const char* key, int64_t value);
 
 /* ---- multi-GPU: samples are sharded over ranks; one RCCL all-reduce per EM iteration ---- */
@@ -258,10 +259,15 @@ int ppls_comm_info(ppls_ctx* ctx, int* nranks, int* rank, double* allreduce_ms, 
 /* Cross-product form (option "xprod"): form S now (*ms = the MFMA Gram kernel time, *total_ms = with
  * the all-reduce and allocation; both nullable) -- otherwise the first run that reads S forms it. */
 int ppls_xprod_prepare(ppls_ctx* ctx, double* ms, double* total_ms);
-/* Its state: *ready = S is formed for the current data, *bytes_per_pass = 8 P^2 (one iteration's
- * algorithmic read, P = padded p + q), *flops = 2 n_local P^2 of the Gram as computed (lower tiles:
- * ~ half the full product), *rows_per_wave = rows of S per wave of the apply kernel for r components. */
+/* Its state: *ready = S is formed for the current data, *bytes_per_pass = the bytes of S one
+ * iteration reads (8 P^2, P = padded p + q, or its lower 128 x 128 tiles for the triangle kernel),
+ * *flops = 2 n_local P^2 of the Gram as computed (lower tiles: ~ half the full product),
+ * *rows_per_wave = 100 x the kernel kind (1 row groups, 2 row tiles, 3 lower triangle) + rows per wave. */
 int ppls_xprod_info(ppls_ctx* ctx, int r, int* ready, int64_t* bytes_per_pass, double* flops, int* rows_per_wave);
+/* One statistics step from S for theta (the kernel option "xprod_kernel" selects): stats =
+ * [X'mu_T p x r | Y'mu_U q x r | Gram 2r x 2r], all column-major, as ppls_finalize_host takes them
+ * (unit parity of the cross-product kernels against the sweep and a host S B). */
+int ppls_xprod_stats(ppls_ctx* ctx, const ppls_theta* th, int r, double* stats);
 /* Shape facts for the roofline: bytes of X and Y one sweep reads (algorithmic), kernel variant. */
 int ppls_sweep_info(ppls_ctx* ctx, int r, int64_t* bytes_per_sweep, int* variant, int* grid);
 /* The sweep kernel instantiation the next EM iteration with r components launches, as text

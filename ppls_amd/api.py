@@ -373,6 +373,17 @@ class Context:
         self._chk(self._L.ppls_xprod_prepare(self.h, ct.byref(ms), ct.byref(tot)))
         return ms.value, tot.value
 
+    def xprod_stats(self, th: Theta):
+        """One statistics step from S for theta: (X'mu_T p x r, Y'mu_U q x r, Gram 2r x 2r)."""
+        r = th.r
+        out = np.zeros(r * (self.p + self.q) + 4 * r * r)
+        t = th.struct()
+        self._chk(self._L.ppls_xprod_stats(self.h, ct.byref(t), r, dptr(out)))
+        SX = out[: self.p * r].reshape(r, self.p).T
+        SY = out[self.p * r: (self.p + self.q) * r].reshape(r, self.q).T
+        G = out[(self.p + self.q) * r:].reshape(2 * r, 2 * r).T
+        return SX, SY, G
+
     def xprod_info(self, r=1):
         """{ready, bytes_per_pass (8 P^2), gram_flops (as computed), rows_per_wave} of the cross-product form."""
         rd, b, f, rw = ct.c_int(), ct.c_int64(), ct.c_double(), ct.c_int()

@@ -113,12 +113,18 @@ struct ppls_ctx {
   // cross-product form of the iteration (ppls_xprod.hip): S = [X Y]'[X Y] (P x P, P = ldx + ldy)
   // formed once per data set, then every statistics step reads S instead of X and Y
   int xprod = 0;            // option "xprod": 0 stream X, Y (default), 1 cross-products, -1 auto (cost model)
-  int xprod_kernel = 0;     // option "xprod_kernel": 0 row tiles with B in LDS (default), 1 row groups (A/B)
+  int xprod_kernel = 0;     // option "xprod_kernel": 0 auto (lower triangle for r <= PPLS_XP_TRI_RMAX, else
+                            // row tiles), 1 row groups, 2 row tiles with B in LDS, 3 lower triangle
   int xprod_rw = 0;         // option "xprod_rw": rows of S per wave of the apply kernel (0 auto)
   bool xp_ready = false;    // S holds the (all-reduced) cross-products of the current data
   bool xp_active = false;   // statistics steps of the current run read S
   double* xp_S = nullptr;
   double* xp_M = nullptr;   // M = S blockdiag(W, C), P x 2r scratch
+  int* xp_tri_items = nullptr;    // lower-triangle form: run list (4 ints per run) and run offsets per block row
+  int* xp_tri_rows = nullptr;
+  int xp_tri_nruns = 0, xp_tri_r = 0;
+  double* xp_rowpart = nullptr;   // its run and tile partials
+  double* xp_colpart = nullptr;
   double xp_setup_ms = 0.0; // last formation of S: Gram kernel (HIP events), and with the all-reduce
   double xp_setup_total_ms = 0.0;
   int xp_nsplit = 0;
@@ -709,6 +715,13 @@ bool xprod_choose(ppls_ctx* c, int max_steps) {
   return ((double)max_steps + 1.0) * (t_sweep - t_pass) > t_setup;
 }
 
+// The cross-product kernel for r components: 1 row groups, 2 row tiles, 3 lower triangle.
+int xprod_kind(const ppls_ctx* c, int r) {
+  if (c->xprod_kernel == 3 && r <= PPLS_XP_TRI_RMAX) return 3;
+  if (c->xprod_kernel == 1 || c->xprod_kernel == 2) return c->xprod_kernel;
+  return r <= PPLS_XP_TRI_RMAX ? 3 : 2;
+}
+
 // One statistics step from S: c->stats for theta[slot] (no collective: S is global).
 int xprod_stats(ppls_ctx* c, int r, int slot) {
   int rc;
@@ -717,13 +730,35 @@ int xprod_stats(ppls_ctx* c, int r, int slot) {
   if (!c->xp_M) {
     if ((rc = dalloc(c, &c->xp_M, (size_t)P * 2 * PPLS_RMAX))) return rc;
   }
-  const int rw = c->xprod_kernel == 1 ? ppls_xprod_rows_per_wave(P, r, c->xprod_rw)
-                                     : ppls_xprod_tile_rows(P, r, c->xprod_rw, c->num_cus);
+  const int kind = xprod_kind(c, r);
+  if (kind == 3 && c->xp_tri_r != r) {   // the triangle's run list and partials for this r
+    int64_t rl = 0, cl = 0;
+    const int nr = ppls_xprod_tri_plan(c->ldx, c->ldy, r, c->num_cus, nullptr, nullptr, &rl, &cl);
+    if (nr < 1) return fail(c, PPLS_E_ARG, "lower-triangle plan failed (r=%d)", r);
+    const int nb = (c->ldx + 127) / 128 + (c->ldy + 127) / 128;
+    std::vector<int> items((size_t)4 * nr), rows((size_t)nb + 1);
+    ppls_xprod_tri_plan(c->ldx, c->ldy, r, c->num_cus, items.data(), rows.data(), nullptr, nullptr);
+    if ((rc = dalloc(c, &c->xp_tri_items, items.size())) || (rc = dalloc(c, &c->xp_tri_rows, rows.size())) ||
+        (rc = dalloc(c, &c->xp_rowpart, (size_t)rl)) || (rc = dalloc(c, &c->xp_colpart, (size_t)cl)))
+      return rc;
+    HIPCHK(c, hipMemcpy(c->xp_tri_items, items.data(), sizeof(int) * items.size(), hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy(c->xp_tri_rows, rows.data(), sizeof(int) * rows.size(), hipMemcpyHostToDevice));
+    c->xp_tri_nruns = nr;
+    c->xp_tri_r = r;
+  }
   hipEvent_t e0, e1;
   if ((rc = timing_pair(c, &e0, &e1))) return rc;
   if (e0) HIPCHK(c, hipEventRecord(e0, c->stream));
-  HIPCHK(c, ppls_launch_xprod_apply(c->xp_S, c->ldx, c->ldy, r, c->xprod_kernel, rw, c->W[slot], c->C[slot],
-                                    c->sc[slot], c->stats, c->xp_M, c->sweep_stop, c->stream));
+  if (kind == 3) {
+    HIPCHK(c, ppls_launch_xprod_tri(c->xp_S, c->ldx, c->ldy, r, c->W[slot], c->C[slot], c->sc[slot], c->stats, c->xp_M,
+                                    c->xp_tri_items, c->xp_tri_nruns, c->xp_tri_rows, c->xp_rowpart, c->xp_colpart,
+                                    c->sweep_stop, c->stream));
+  } else {
+    const int rw = kind == 1 ? ppls_xprod_rows_per_wave(P, r, c->xprod_rw)
+                             : ppls_xprod_tile_rows(P, r, c->xprod_rw, c->num_cus);
+    HIPCHK(c, ppls_launch_xprod_apply(c->xp_S, c->ldx, c->ldy, r, kind == 1 ? 1 : 0, rw, c->W[slot], c->C[slot],
+                                      c->sc[slot], c->stats, c->xp_M, c->sweep_stop, c->stream));
+  }
   if (e1) HIPCHK(c, hipEventRecord(e1, c->stream));
   return PPLS_OK;
 }
@@ -768,6 +803,11 @@ int compute_ssq(ppls_ctx* c) {
   c->xp_ready = false;   // data or communicator changed: the cross-products are stale
   dfree(c->xp_S);
   dfree(c->xp_M);
+  dfree(c->xp_tri_items);
+  dfree(c->xp_tri_rows);
+  dfree(c->xp_rowpart);
+  dfree(c->xp_colpart);
+  c->xp_tri_nruns = c->xp_tri_r = 0;
 
   const int nb = 1024;
   if ((rc = dalloc(c, &c->scratch, nb + 8))) return rc;
@@ -937,6 +977,10 @@ void ppls_ctx_destroy(ppls_ctx* c) {
   dfree(c->stop_d);
   dfree(c->xp_S);
   dfree(c->xp_M);
+  dfree(c->xp_tri_items);
+  dfree(c->xp_tri_rows);
+  dfree(c->xp_rowpart);
+  dfree(c->xp_colpart);
   dfree(c->bal_bounds);
   dfree(c->team_bar);
   dfree(c->team_part);
@@ -1014,7 +1058,8 @@ int ppls_set_option(ppls_ctx* c, const char* key, int64_t value) {
     if (value < -1 || value > 1) return fail(c, PPLS_E_ARG, "xprod must be -1 (auto), 0 (stream X, Y) or 1 (cross-products)");
     c->xprod = (int)value;
   } else if (!strcmp(key, "xprod_kernel")) {
-    if (value != 0 && value != 1) return fail(c, PPLS_E_ARG, "xprod_kernel must be 0 (row tiles) or 1 (row groups)");
+    if (value < 0 || value > 3)
+      return fail(c, PPLS_E_ARG, "xprod_kernel must be 0 (auto), 1 (row groups), 2 (row tiles) or 3 (lower triangle)");
     c->xprod_kernel = (int)value;
   } else if (!strcmp(key, "xprod_rw")) {
     if (value != 0 && value != 1 && value != 2 && value != 4) return fail(c, PPLS_E_ARG, "xprod_rw must be 0, 1, 2 or 4");
@@ -2416,14 +2461,52 @@ int ppls_xprod_info(ppls_ctx* c, int r, int* ready, int64_t* bytes_per_pass, dou
   if (!c->have_data) return fail(c, PPLS_E_STATE, "no data");
   const int64_t P = (int64_t)c->ldx + c->ldy;
   if (ready) *ready = c->xp_ready ? 1 : 0;
-  if (bytes_per_pass) *bytes_per_pass = 8 * P * P;
+  if (bytes_per_pass) {   // S's bytes one iteration reads: the lower 128 x 128 tiles, or all of S
+    const int64_t nb = (c->ldx + 127) / 128 + (c->ldy + 127) / 128;
+    int64_t tri = 0;
+    for (int64_t I = 0; I < nb; ++I) {
+      const int64_t li = I < (c->ldx + 127) / 128 ? std::min<int64_t>(128, c->ldx - 128 * I)
+                                                   : std::min<int64_t>(128, c->ldy - 128 * (I - (c->ldx + 127) / 128));
+      for (int64_t J = 0; J <= I; ++J) {
+        const int64_t lj = J < (c->ldx + 127) / 128 ? std::min<int64_t>(128, c->ldx - 128 * J)
+                                                     : std::min<int64_t>(128, c->ldy - 128 * (J - (c->ldx + 127) / 128));
+        tri += li * lj;
+      }
+    }
+    *bytes_per_pass = xprod_kind(c, r < 1 ? 1 : r) == 3 ? 8 * tri : 8 * P * P;
+  }
   if (flops) {   // lower 128 x 128 tiles incl. the diagonal ones, 2 flops per multiply-add
     const double nb = (double)((P + 127) / 128);
     flops[0] = 2.0 * (double)c->n_local * nb * (nb + 1) / 2.0 * 128.0 * 128.0;
   }
-  if (rows_per_wave)
-    *rows_per_wave = c->xprod_kernel == 1 ? ppls_xprod_rows_per_wave((int)P, r < 1 ? 1 : r, c->xprod_rw)
-                                          : ppls_xprod_tile_rows((int)P, r < 1 ? 1 : r, c->xprod_rw, c->num_cus);
+  if (rows_per_wave) {   // the kernel kind in the hundreds, its rows per wave (1, 2 kinds) below
+    const int kind = xprod_kind(c, r < 1 ? 1 : r);
+    *rows_per_wave = 100 * kind + (kind == 1 ? ppls_xprod_rows_per_wave((int)P, r < 1 ? 1 : r, c->xprod_rw)
+                                  : kind == 2 ? ppls_xprod_tile_rows((int)P, r < 1 ? 1 : r, c->xprod_rw, c->num_cus)
+                                              : 32);
+  }
+  return PPLS_OK;
+}
+
+int ppls_xprod_stats(ppls_ctx* c, const ppls_theta* th, int r, double* stats) {
+  if (!c || !stats) return PPLS_E_ARG;
+  if (!c->have_data) return fail(c, PPLS_E_STATE, "no data");
+  int rc;
+  if ((rc = check_theta(c, th, r))) return rc;
+  HIPCHK(c, hipSetDevice(c->device));
+  if ((rc = ensure_r(c, r, 1))) return rc;
+  if ((rc = upload_theta(c, th, r, 0))) return rc;
+  if ((rc = xprod_stats(c, r, 0))) return rc;
+  std::vector<double> st((size_t)c->part_ld);
+  HIPCHK(c, hipMemcpyAsync(st.data(), c->stats, sizeof(double) * st.size(), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  for (int k = 0; k < r; ++k) {
+    for (int i = 0; i < c->p; ++i) stats[(size_t)k * c->p + i] = st[(size_t)k * c->ldx + i];
+    for (int i = 0; i < c->q; ++i)
+      stats[(size_t)r * c->p + (size_t)k * c->q + i] = st[(size_t)r * c->ldx + (size_t)k * c->ldy + i];
+  }
+  for (int e = 0; e < 4 * r * r; ++e)
+    stats[(size_t)r * (c->p + c->q) + e] = st[(size_t)r * (c->ldx + c->ldy) + e];
   return PPLS_OK;
 }
 

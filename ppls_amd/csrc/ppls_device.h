@@ -34,8 +34,11 @@ __device__ __forceinline__ void ppls_swap_pair(double& A, double& B) {
   }
 }
 
+// real: how many of the lane's current M values are real; an odd M is padded with one zero at its
+// end, and a lane whose kept half holds that pad below the top level would otherwise claim the
+// global index of a real value of the other half (both lanes "canonical": a write race).
 template <int M, int L, int N>
-__device__ __forceinline__ void ppls_rs(double (&a)[N], int lane, int& idx, bool& canon) {
+__device__ __forceinline__ void ppls_rs_r(double (&a)[N], int lane, int& idx, bool& canon, int& real) {
   if constexpr (L < 6) {
     const int beta = (lane >> (5 - L)) & 1;
     if constexpr (M == 1) {
@@ -47,10 +50,11 @@ __device__ __forceinline__ void ppls_rs(double (&a)[N], int lane, int& idx, bool
         a[0] += ppls_dpp_partner<L>(a[0]);
       }
       canon = canon && (beta == 0);
-      ppls_rs<1, L + 1, N>(a, lane, idx, canon);
+      ppls_rs_r<1, L + 1, N>(a, lane, idx, canon, real);
     } else {
       constexpr int H = (M + 1) / 2;
       static_assert(2 * H <= N, "reduce-scatter buffer too small");
+      real = beta ? (real > H ? real - H : 0) : (real < H ? real : H);
       if constexpr (M & 1) a[M] = 0.0;
 #pragma unroll
       for (int j = 0; j < H; ++j) {
@@ -65,9 +69,18 @@ __device__ __forceinline__ void ppls_rs(double (&a)[N], int lane, int& idx, bool
         }
       }
       idx += beta * H;
-      ppls_rs<H, L + 1, N>(a, lane, idx, canon);
+      ppls_rs_r<H, L + 1, N>(a, lane, idx, canon, real);
     }
   }
+}
+
+// V values per lane -> lane holds the wave sum of value idx (of the first LEFT <= 1 values for
+// M <= 64); canon = this lane is the one lane to publish it (pad slots and duplicates are not).
+template <int M, int L, int N>
+__device__ __forceinline__ void ppls_rs(double (&a)[N], int lane, int& idx, bool& canon) {
+  int real = M;
+  ppls_rs_r<M, L, N>(a, lane, idx, canon, real);
+  canon = canon && real > 0;
 }
 
 // ============================================================================ LDS-DMA helpers

@@ -239,6 +239,185 @@ __global__ __launch_bounds__(256) void ppls_xprod_tile_kernel(const double* __re
   }
 }
 
+// Lower-triangle form (the default for r <= PPLS_XP_TRI_RMAX): S is symmetric, so each
+// off-diagonal 128 x 128 tile S_IJ (J < I) is read once and used twice -- its rows give M[I] +=
+// S_IJ B_J, its columns give M[J] += S_IJ' B_I -- halving the bytes per iteration.  The blocks
+// I, J of the joint index space are aligned to the X/Y seam (X columns in 128-steps from 0, Y
+// columns from ldx), so a tile's B rows are all W or all C.  A workgroup takes a run of tiles
+// (I, J0..J1-1) of one block row: its four waves own 32 rows each, a lane two columns.
+//   column contribution: per lane, cc[k] (two columns) += S[i, j] B_I[i, k], B_I rows broadcast
+//     from LDS; summed over the four waves in LDS and written per tile (colpart);
+//   row contribution: per lane and row, the partial S[i, j..j+1] . B_J[j..j+1, k] of its two columns,
+//     G rows x r values at a time summed over the wave by a DPP reduce-scatter, accumulated over
+//     the run's tiles in registers and written per run (rowpart).
+// ppls_xprod_tri_reduce_kernel then sums, per row of M, its run partials and the column partials of
+// the tiles below it in a fixed order (deterministic), and writes M, X'mu_T and Y'mu_U.
+struct XpBlk {
+  int start, len, type;   // first row / column, width (<= 128), 0 = X block (B rows of W), 1 = Y (C)
+};
+__device__ __forceinline__ XpBlk ppls_xp_blk(int b, int bx, int ldx, int ldy) {
+  if (b < bx) {
+    const int st = b << 7;
+    return XpBlk{st, min(128, ldx - st), 0};
+  }
+  const int st = (b - bx) << 7;
+  return XpBlk{ldx + st, min(128, ldy - st), 1};
+}
+
+template <int R, bool NT>
+__global__ __launch_bounds__(256) void ppls_xprod_tri_kernel(const double* __restrict__ S, int ldx, int ldy,
+                                                             const double* __restrict__ Wp,
+                                                             const double* __restrict__ Cp,
+                                                             const int4* __restrict__ items,
+                                                             double* __restrict__ rowpart,
+                                                             double* __restrict__ colpart,
+                                                             const int* __restrict__ stop) {
+  if (stop && *stop) return;   // em_run converged at an earlier iteration
+  typedef double d2v __attribute__((ext_vector_type(2)));
+  constexpr int G = 32 / R > 0 ? 32 / R : 1;   // rows per reduce-scatter batch (G r <= 32 values)
+  constexpr int NVB = G * R;
+  constexpr int NBATCH = (32 + G - 1) / G;     // batches over a wave's 32 rows
+  __shared__ double sBI[128 * R];               // B rows of block I, [row][k]
+  __shared__ double red[R * 128];               // column contributions, [k][column]
+  const int P = ldx + ldy, bx = (ldx + 127) >> 7;
+  const int4 it = items[blockIdx.x];
+  const int I = it.x, J0 = it.y, J1 = it.z;
+  const XpBlk bI = ppls_xp_blk(I, bx, ldx, ldy);
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  for (int e = tid; e < 128 * R; e += 256) {
+    const int row = e / R, k = e - row * R;
+    sBI[e] = row < bI.len ? (bI.type ? Cp[(int64_t)k * ldy + (bI.start - ldx) + row] : Wp[(int64_t)k * ldx + bI.start + row])
+                          : 0.0;
+  }
+  __syncthreads();
+  const int r0 = 32 * wave, rlim = bI.len - r0;   // this wave's rows r0 + rr, rr < min(32, rlim)
+  const int c = 2 * lane;
+  double racc[2][NBATCH];
+#pragma unroll
+  for (int b = 0; b < NBATCH; ++b) racc[0][b] = racc[1][b] = 0.0;
+  int idx = 0;
+  bool canon = true;
+  for (int J = J0; J < J1; ++J) {
+    const XpBlk bJ = ppls_xp_blk(J, bx, ldx, ldy);
+    const bool off = J != I, cl = c < bJ.len;
+    const double* bsrc = bJ.type ? Cp + (bJ.start - ldx) + c : Wp + bJ.start + c;
+    const int ldb = bJ.type ? ldy : ldx;
+    d2v bj[R], cc[R];
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+      bj[k] = cl ? *(const d2v*)(bsrc + (int64_t)k * ldb) : d2v{0.0, 0.0};
+      cc[k] = d2v{0.0, 0.0};
+    }
+    const double* sb = S + (int64_t)(bI.start + r0) * P + bJ.start + c;
+    auto ld = [&](int rr) -> d2v {
+      if (!(cl && rr < rlim)) return d2v{0.0, 0.0};
+      if constexpr (NT) return __builtin_nontemporal_load((const d2v*)(sb + (int64_t)rr * P));
+      else return *(const d2v*)(sb + (int64_t)rr * P);
+    };
+    d2v sn[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) sn[g] = g < 32 ? ld(g) : d2v{0.0, 0.0};
+#pragma unroll
+    for (int b = 0; b < NBATCH; ++b) {
+      d2v sv[G];
+#pragma unroll
+      for (int g = 0; g < G; ++g) sv[g] = sn[g];
+      if (b + 1 < NBATCH) {   // next batch's rows in flight while this one is reduced
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+          const int rr = (b + 1) * G + g;
+          sn[g] = rr < 32 ? ld(rr) : d2v{0.0, 0.0};
+        }
+      }
+      double pr[NVB + 1];
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        const int rr = b * G + g;
+        if (off && rr < 32 && rr < rlim) {
+          const double* bi = sBI + (r0 + rr) * R;
+#pragma unroll
+          for (int k = 0; k < R; ++k) {
+            const double v = bi[k];
+            cc[k].x = fma(sv[g].x, v, cc[k].x);
+            cc[k].y = fma(sv[g].y, v, cc[k].y);
+          }
+        }
+#pragma unroll
+        for (int k = 0; k < R; ++k) pr[g * R + k] = fma(sv[g].y, bj[k].y, sv[g].x * bj[k].x);
+      }
+      pr[NVB] = 0.0;
+      idx = 0;
+      canon = true;
+      ppls_rs<NVB, 0, NVB + 1>(pr, lane, idx, canon);
+      if (bJ.type) racc[1][b] += pr[0];
+      else racc[0][b] += pr[0];
+    }
+    if (off) {   // M[J rows] += S_IJ' B_I: this tile's column partial, the four waves in order
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        if (wave == w) {
+#pragma unroll
+          for (int k = 0; k < R; ++k) {
+            red[k * 128 + c] = (w ? red[k * 128 + c] : 0.0) + cc[k].x;
+            red[k * 128 + c + 1] = (w ? red[k * 128 + c + 1] : 0.0) + cc[k].y;
+          }
+        }
+        __syncthreads();
+      }
+      double* cp = colpart + ((int64_t)I * (I + 1) / 2 + J) * (R * 128);
+      for (int e = tid; e < R * 128; e += 256) cp[e] = red[e];
+      __syncthreads();
+    }
+  }
+  // this run's row partial: rowpart[run][2r][128]; lane idx holds row g, component k of each batch
+  double* rp = rowpart + (int64_t)blockIdx.x * (2 * R * 128);
+  if (canon && idx < NVB) {
+    const int g = idx / R, k = idx - g * R;
+#pragma unroll
+    for (int b = 0; b < NBATCH; ++b) {
+      const int rr = b * G + g;
+      if (rr < 32) {
+        rp[k * 128 + r0 + rr] = racc[0][b];
+        rp[(R + k) * 128 + r0 + rr] = racc[1][b];
+      }
+    }
+  }
+}
+
+// Row i of M: its block's run partials (row_items[b] .. row_items[b + 1]) in run order, then the
+// column partials of the tiles (I, b) below it in I order; then X'mu_T / Y'mu_U of row i.
+template <int R>
+__global__ __launch_bounds__(256) void ppls_xprod_tri_reduce_kernel(int ldx, int ldy, const int* __restrict__ row_items,
+                                                                    const double* __restrict__ rowpart,
+                                                                    const double* __restrict__ colpart,
+                                                                    const PplsScalars* __restrict__ sc,
+                                                                    double* __restrict__ stats,
+                                                                    double* __restrict__ M,
+                                                                    const int* __restrict__ stop) {
+  if (stop && *stop) return;
+  const int P = ldx + ldy, bx = (ldx + 127) >> 7, nb = bx + ((ldy + 127) >> 7);
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= (int64_t)P * R) return;
+  const int k = (int)(e / P), i = (int)(e - (int64_t)k * P);
+  const int b = i < ldx ? i >> 7 : bx + ((i - ldx) >> 7);
+  const int r = i < ldx ? i & 127 : (i - ldx) & 127;
+  double m0 = 0.0, m1 = 0.0;
+  for (int t = row_items[b]; t < row_items[b + 1]; ++t) {
+    m0 += rowpart[(int64_t)t * (2 * R * 128) + k * 128 + r];
+    m1 += rowpart[(int64_t)t * (2 * R * 128) + (R + k) * 128 + r];
+  }
+#pragma unroll 4
+  for (int I = b + 1; I < nb; ++I) {
+    const double v = colpart[((int64_t)I * (I + 1) / 2 + b) * (R * 128) + k * 128 + r];
+    if (I < bx) m0 += v;
+    else m1 += v;
+  }
+  M[(int64_t)k * P + i] = m0;
+  M[(int64_t)(R + k) * P + i] = m1;
+  if (i < ldx) stats[(int64_t)k * ldx + i] = sc->alpha[k] * m0 + sc->beta[k] * m1;   // X'mu_T
+  else stats[(int64_t)R * ldx + (int64_t)k * ldy + (i - ldx)] = sc->gamma[k] * m0 + sc->delta[k] * m1;   // Y'mu_U
+}
+
 // Gram entry (a, b), a <= b, of B'M: sum over the rows where column a of B lives (X rows for
 // a < R, Y rows otherwise); written to (a, b) and (b, a).
 __global__ __launch_bounds__(256) void ppls_xprod_gram_kernel(int ldx, int ldy, int R, const double* __restrict__ Wp,
@@ -320,9 +499,78 @@ hipError_t launch_tile_rw(int rw, const double* S, int ldx, int ldy, const doubl
   return hipErrorInvalidValue;
 }
 
+template <int R>
+hipError_t launch_tri(const double* S, int ldx, int ldy, const double* Wp, const double* Cp, const PplsScalars* sc,
+                      double* stats, double* M, const int* items, int nruns, const int* row_items, double* rowpart,
+                      double* colpart, const int* stop, hipStream_t st) {
+  const int P = ldx + ldy;
+  if (4.0 * P * (double)P > 200.0 * (1 << 20))   // the lower triangle beyond the Infinity Cache: nt loads
+    hipLaunchKernelGGL((ppls_xprod_tri_kernel<R, true>), dim3((unsigned)nruns), dim3(256), 0, st, S, ldx, ldy, Wp, Cp,
+                       (const int4*)items, rowpart, colpart, stop);
+  else
+    hipLaunchKernelGGL((ppls_xprod_tri_kernel<R, false>), dim3((unsigned)nruns), dim3(256), 0, st, S, ldx, ldy, Wp, Cp,
+                       (const int4*)items, rowpart, colpart, stop);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const int64_t n = (int64_t)P * R;
+  hipLaunchKernelGGL((ppls_xprod_tri_reduce_kernel<R>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, ldx, ldy,
+                     row_items, rowpart, colpart, sc, stats, M, stop);
+  return hipGetLastError();
+}
+
 }  // namespace
 
 extern "C" {
+
+int ppls_xprod_tri_plan(int ldx, int ldy, int r, int num_cus, int* items, int* row_items, int64_t* rowpart_len,
+                        int64_t* colpart_len) {
+  if (r < 1 || r > PPLS_XP_TRI_RMAX || ldx < 2 || ldy < 2) return -1;
+  const int bx = (ldx + 127) / 128, nb = bx + (ldy + 127) / 128;
+  const int64_t ntiles = (int64_t)nb * (nb + 1) / 2;
+  int T = (int)(ntiles / (2 * (int64_t)(num_cus > 0 ? num_cus : 256)));   // ~2 runs per CU
+  if (T < 1) T = 1;
+  int nr = 0;
+  for (int I = 0; I < nb; ++I) {
+    if (row_items) row_items[I] = nr;
+    for (int J0 = 0; J0 <= I; J0 += T) {
+      if (items) {
+        items[4 * nr] = I;
+        items[4 * nr + 1] = J0;
+        items[4 * nr + 2] = J0 + T <= I + 1 ? J0 + T : I + 1;
+        items[4 * nr + 3] = 0;
+      }
+      ++nr;
+    }
+  }
+  if (row_items) row_items[nb] = nr;
+  if (rowpart_len) *rowpart_len = (int64_t)nr * 2 * r * 128;
+  if (colpart_len) *colpart_len = ntiles * r * 128;
+  return nr;
+}
+
+hipError_t ppls_launch_xprod_tri(const double* S, int ldx, int ldy, int r, const double* Wp, const double* Cp,
+                                 const PplsScalars* sc, double* stats, double* M, const int* items, int nruns,
+                                 const int* row_items, double* rowpart, double* colpart, const int* stop,
+                                 hipStream_t st) {
+  if (ldx < 2 || ldy < 2 || (ldx & 1) || (ldy & 1) || r < 1 || r > PPLS_XP_TRI_RMAX || nruns < 1)
+    return hipErrorInvalidValue;
+  if (((uintptr_t)S | (uintptr_t)Wp | (uintptr_t)Cp) & 15) return hipErrorInvalidValue;   // 16-B loads
+  hipError_t e;
+  switch (r) {
+#define PPLS_XT_CASE(k) \
+    case k: e = launch_tri<k>(S, ldx, ldy, Wp, Cp, sc, stats, M, items, nruns, row_items, rowpart, colpart, stop, st); break;
+    PPLS_XT_CASE(1) PPLS_XT_CASE(2) PPLS_XT_CASE(3) PPLS_XT_CASE(4) PPLS_XT_CASE(5) PPLS_XT_CASE(6)
+    PPLS_XT_CASE(7) PPLS_XT_CASE(8) PPLS_XT_CASE(9) PPLS_XT_CASE(10)
+#undef PPLS_XT_CASE
+    default: return hipErrorInvalidValue;
+  }
+  if (e != hipSuccess) return e;
+  const int R2 = 2 * r;
+  hipLaunchKernelGGL(ppls_xprod_gram_kernel, dim3((unsigned)(R2 * (R2 + 1) / 2)), dim3(256), 0, st, ldx, ldy, r, Wp,
+                     Cp, M, stats, stop);
+  return hipGetLastError();
+}
+
 
 int ppls_xprod_rows_per_wave(int P, int r, int rw_opt) {
   if (rw_opt == 1 || rw_opt == 2 || (rw_opt == 4 && r <= 8)) return rw_opt;

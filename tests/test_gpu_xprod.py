@@ -18,7 +18,7 @@ from oracle import ppls_oracle as o
 pytestmark = pytest.mark.gpu
 
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
-DEFAULTS = dict(xprod=0, xprod_rw=0, dtype=0)
+DEFAULTS = dict(xprod=0, xprod_kernel=0, xprod_rw=0, dtype=0)
 
 
 @pytest.fixture(scope="module")
@@ -52,12 +52,17 @@ def _golden():
     return sorted(f for f in os.listdir(GOLD) if f.endswith(".npz") and not f.startswith(("seq_", "meta_", "rcheck_")))
 
 
-@pytest.mark.parametrize("rw", [0, 1, 2, 4])
+# (xprod_kernel, xprod_rw): auto, row groups, row tiles (LDS-staged W, C), lower triangle
+KERNELS = [(0, 0), (1, 1), (1, 2), (2, 1), (2, 2), (2, 4), (3, 0)]
+
+
+@pytest.mark.parametrize("kernel,rw", KERNELS, ids=[f"k{k}rw{w}" for k, w in KERNELS])
 @pytest.mark.parametrize("name", _golden())
-def test_xprod_em_run_matches_golden(ctx, name, rw):
+def test_xprod_em_run_matches_golden(ctx, name, kernel, rw):
     g = np.load(os.path.join(GOLD, name))
     meta = json.loads(str(g["meta"]))
     ctx.set_option("xprod", 1)
+    ctx.set_option("xprod_kernel", kernel)
     ctx.set_option("xprod_rw", rw)
     ctx.set_data(g["X"], g["Y"])
     th0 = dict(W=g["W0"], C=g["C0"], B=np.diag(g["B0"]), sigE=g["sig0"][0], sigF=g["sig0"][1],
@@ -111,6 +116,26 @@ def test_xprod_equals_streaming(ctx, n, p, q, r):
     assert _relerr([est.sigE, est.sigF, est.sigH], [ref_est.sigE, ref_est.sigF, ref_est.sigH]) < 1e-8
     assert _relerr(eout.mu_T, ref_eout.mu_T) < 1e-9
     assert _relerr(eout.Chh, ref_eout.Chh) < 1e-9
+
+
+@pytest.mark.parametrize("n,p,q,r", [(900, 300, 260, 5), (500, 1025, 131, 10), (400, 129, 127, 3), (300, 2, 700, 1),
+                                     (600, 256, 256, 8)])
+def test_xprod_kernels_agree(ctx, n, p, q, r):
+    """The lower-triangle kernel (multi-block shapes, blocks cut by the X/Y seam, r up to its
+    limit) against the row-tile and row-group kernels that read all of S."""
+    X, Y, th0 = make_problem(n, p, q, r, seed=p + q + r)
+    ctx.set_option("xprod", 1)
+    ctx.set_data(X, Y)
+    out = {}
+    for kernel in (1, 2, 3):
+        ctx.set_option("xprod_kernel", kernel)
+        assert ctx.xprod_info(r)["rows_per_wave"] // 100 == kernel
+        est, ll, _, _ = ctx.em_run(_theta(th0), 12, -np.inf, 0, want_eout=False)
+        out[kernel] = (est, ll)
+    for kernel in (2, 3):
+        assert _relerr(out[kernel][1], out[1][1]) < 1e-12
+        assert np.abs(out[kernel][0].W - out[1][0].W).max() < 1e-10
+        assert np.abs(out[kernel][0].C - out[1][0].C).max() < 1e-10
 
 
 def test_xprod_matches_oracle_and_qr(ctx):
@@ -194,9 +219,12 @@ def test_xprod_prepare_and_info(ctx):
     ctx.set_data(X, Y)
     ms, tot = ctx.xprod_prepare()
     assert ms > 0 and tot >= ms
+    ctx.set_option("xprod_kernel", 2)
     info = ctx.xprod_info(2)
     P = 70 + 34   # ld of q = 33 fp64 columns: 34
     assert info["ready"] and info["bytes_per_pass"] == 8 * P * P
+    ctx.set_option("xprod_kernel", 3)   # blocks 70 | 34: lower tiles 70^2 + 34 x 70 + 34^2
+    assert ctx.xprod_info(2)["bytes_per_pass"] == 8 * (70 * 70 + 34 * 70 + 34 * 34)
     assert ctx.xprod_prepare() == (0.0, 0.0)   # already formed
 
 
@@ -236,3 +264,26 @@ def test_xprod_k_contexts_sharded(k, n, p, q, r, dtype):
     assert np.abs(est.W - ref[0].W).max() < tol and np.abs(est.C - ref[0].C).max() < tol
     mu = np.vstack([e.mu_T.reshape(-1, r) for _, _, e in res])
     assert _relerr(mu, ref[2].mu_T) < tol
+
+
+@pytest.mark.parametrize("kernel", [1, 2, 3])
+@pytest.mark.parametrize("n,p,q,r", [(200, 24, 18, 3), (300, 50, 50, 2), (400, 300, 131, 5), (350, 129, 258, 10),
+                                     (150, 7, 5, 1)])
+def test_xprod_stats_unit_parity(ctx, kernel, n, p, q, r):
+    """One statistics step from S against the host: X'mu_T, Y'mu_U (EM_W_multi.R:691-694,
+    :732-733) and the Gram of [XW YC] for a given theta, every cross-product kernel."""
+    from ppls_amd import Theta
+    X, Y, th0 = make_problem(n, p, q, r, seed=3 * p + q + r)
+    ctx.set_option("xprod_kernel", kernel)
+    ctx.set_data(X, Y)
+    th = _theta(th0)
+    SX, SY, G = ctx.xprod_stats(th)
+    cf = o.mu_coefficients(th0["B"], th0["sigE"], th0["sigF"], th0["sigH"], th0["sigT"])
+    a, b = X @ th0["W"], Y @ th0["C"]
+    muT = a * cf["alpha"] + b * cf["beta"]
+    muU = a * cf["gamma"] + b * cf["delta"]
+    Z = np.hstack([a, b])
+    assert _relerr(SX, X.T @ muT) < 1e-12
+    assert _relerr(SY, Y.T @ muU) < 1e-12
+    assert _relerr(G, Z.T @ Z) < 1e-12
+    assert np.array_equal(G, G.T)

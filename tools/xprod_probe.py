@@ -21,7 +21,7 @@ def main():
     ap.add_argument("configs", nargs="*", default=["c3"])
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--rw", type=int, default=0)
-    ap.add_argument("--kernel", type=int, default=0, help="0 row tiles (B in LDS), 1 row groups")
+    ap.add_argument("--kernel", type=int, default=0, help="0 auto, 1 row groups, 2 row tiles (B in LDS), 3 lower triangle")
     ap.add_argument("--stream-steps", type=int, default=20)
     args = ap.parse_args()
     from ppls_amd import Context
