@@ -95,10 +95,13 @@ const char* ppls_last_error(const ppls_ctx* ctx);
  *                per iteration; 1 from the cross-products S = [X Y]'[X Y], formed once per data set
  *                on MFMA and all-reduced once, after which an iteration reads S (8 (p+q)^2 bytes) and
  *                needs no collective; -1 auto: S when a cost model of max_steps iterations says so),
- *       "xprod_kernel" (cross-product kernel: 0 auto (3 for r <= 10, else 2), 1 row groups reading
- *                       W, C from L1/L2, 2 row tiles with W, C staged in LDS, 3 lower triangle: each
- *                       off-diagonal tile of the symmetric S read once for its rows and its columns),
- *       "xprod_rw" (rows of S per wave of kernels 1 and 2: 0 auto, 1, 2, 4) */
+ *       "xprod_kernel" (cross-product kernel: 0 auto (= 2), 1 row groups reading W, C from L1/L2,
+ *                       2 row tiles with W, C staged in LDS, 3 lower triangle (r <= 10): each
+ *                       off-diagonal tile of the symmetric S read once for its rows and its columns
+ *                       -- half the bytes, measured slower (latency-bound tiles + a partial reduction)),
+ *       "xprod_rw" (rows of S per wave of kernels 1 and 2: 0 auto, 1, 2, 4),
+ *       "xprod_fuse" (1, default: the finalize after a cross-product step forms the 2r x 2r Gram
+ *                     itself when r <= 8 and p + q <= 6144; 0: a separate Gram kernel) */
 int ppls_set_option(ppls_ctx* ctx, const char* key, int64_t value);
 
 /* ---- multi-GPU: samples are sharded over ranks; one RCCL all-reduce per EM iteration ---- */

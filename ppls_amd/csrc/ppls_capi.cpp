@@ -113,11 +113,13 @@ struct ppls_ctx {
   // cross-product form of the iteration (ppls_xprod.hip): S = [X Y]'[X Y] (P x P, P = ldx + ldy)
   // formed once per data set, then every statistics step reads S instead of X and Y
   int xprod = 0;            // option "xprod": 0 stream X, Y (default), 1 cross-products, -1 auto (cost model)
-  int xprod_kernel = 0;     // option "xprod_kernel": 0 auto (lower triangle for r <= PPLS_XP_TRI_RMAX, else
-                            // row tiles), 1 row groups, 2 row tiles with B in LDS, 3 lower triangle
+  int xprod_kernel = 0;     // option "xprod_kernel": 0 auto (= 2), 1 row groups, 2 row tiles with B in LDS,
+                            // 3 lower triangle (r <= PPLS_XP_TRI_RMAX; measured slower, §12)
   int xprod_rw = 0;         // option "xprod_rw": rows of S per wave of the apply kernel (0 auto)
   bool xp_ready = false;    // S holds the (all-reduced) cross-products of the current data
   bool xp_active = false;   // statistics steps of the current run read S
+  bool xp_pending_gram = false;   // the last statistics step left the Gram B'M to the next finalize
+  int xprod_fuse = 1;       // option "xprod_fuse": the finalize forms the Gram (r <= 8, P <= 6144)
   double* xp_S = nullptr;
   double* xp_M = nullptr;   // M = S blockdiag(W, C), P x 2r scratch
   int* xp_tri_items = nullptr;    // lower-triangle form: run list (4 ints per run) and run offsets per block row
@@ -627,6 +629,8 @@ int finalize(ppls_ctx* c, int r, int cur, int nxt, int logl_index, int type, int
   f.stop_check = stop_step > 0 ? 1 : 0;
   f.stop_step = stop_step;
   f.atol = c->stop_atol;
+  f.xpM = c->xp_pending_gram ? c->xp_M : nullptr;   // the Gram of a cross-product step, formed here
+  c->xp_pending_gram = false;
   HIPCHK(c, ppls_launch_finalize(&f, c->stream));
   // timing experiment (ablate bit 13): the same finalize again right away, with warm instruction
   // and data caches (results stay valid: it recomputes the same outputs, only the Jacobi warm
@@ -715,15 +719,19 @@ bool xprod_choose(ppls_ctx* c, int max_steps) {
   return ((double)max_steps + 1.0) * (t_sweep - t_pass) > t_setup;
 }
 
-// The cross-product kernel for r components: 1 row groups, 2 row tiles, 3 lower triangle.
+// The cross-product kernel for r components: 1 row groups, 2 row tiles (the default), 3 lower
+// triangle -- half the bytes of S, but at C3 its tiles are latency-bound (24.0 us against the row
+// tiles' 23.2 us for all of S) and its partial reduction adds 13-16 us.
 int xprod_kind(const ppls_ctx* c, int r) {
   if (c->xprod_kernel == 3 && r <= PPLS_XP_TRI_RMAX) return 3;
-  if (c->xprod_kernel == 1 || c->xprod_kernel == 2) return c->xprod_kernel;
-  return r <= PPLS_XP_TRI_RMAX ? 3 : 2;
+  if (c->xprod_kernel == 1) return 1;
+  return 2;
 }
 
-// One statistics step from S: c->stats for theta[slot] (no collective: S is global).
-int xprod_stats(ppls_ctx* c, int r, int slot) {
+// One statistics step from S: c->stats for theta[slot] (no collective: S is global).  fuse: a
+// finalize follows, which may form the Gram itself (its scalar block runs in the polar blocks'
+// slack: C3 ~2 us of it against the Gram kernel's 4 us + a launch boundary).
+int xprod_stats(ppls_ctx* c, int r, int slot, bool fuse = false) {
   int rc;
   const int P = c->ldx + c->ldy;
   if (!c->xp_ready && (rc = xprod_setup(c))) return rc;
@@ -756,8 +764,10 @@ int xprod_stats(ppls_ctx* c, int r, int slot) {
   } else {
     const int rw = kind == 1 ? ppls_xprod_rows_per_wave(P, r, c->xprod_rw)
                              : ppls_xprod_tile_rows(P, r, c->xprod_rw, c->num_cus);
+    const bool defer = fuse && c->xprod_fuse && r <= 8 && P <= 6144;
     HIPCHK(c, ppls_launch_xprod_apply(c->xp_S, c->ldx, c->ldy, r, kind == 1 ? 1 : 0, rw, c->W[slot], c->C[slot],
-                                      c->sc[slot], c->stats, c->xp_M, c->sweep_stop, c->stream));
+                                      c->sc[slot], c->stats, c->xp_M, c->sweep_stop, defer ? 0 : 1, c->stream));
+    c->xp_pending_gram = defer;
   }
   if (e1) HIPCHK(c, hipEventRecord(e1, c->stream));
   return PPLS_OK;
@@ -765,8 +775,9 @@ int xprod_stats(ppls_ctx* c, int r, int slot) {
 
 // The statistics of theta[slot] for an EM iteration: from S when the run reads the cross-products
 // (not for the mu write-out, which needs the rows), else one streaming sweep.
-int stats_step(ppls_ctx* c, int r, int slot, bool write_mu) {
-  if (c->xp_active && !write_mu && c->seg_rows < 0) return xprod_stats(c, r, slot);
+int stats_step(ppls_ctx* c, int r, int slot, bool write_mu, bool finalize_next = false) {
+  c->xp_pending_gram = false;
+  if (c->xp_active && !write_mu && c->seg_rows < 0) return xprod_stats(c, r, slot, finalize_next);
   return sweep(c, r, slot, write_mu);
 }
 
@@ -1061,6 +1072,8 @@ int ppls_set_option(ppls_ctx* c, const char* key, int64_t value) {
     if (value < 0 || value > 3)
       return fail(c, PPLS_E_ARG, "xprod_kernel must be 0 (auto), 1 (row groups), 2 (row tiles) or 3 (lower triangle)");
     c->xprod_kernel = (int)value;
+  } else if (!strcmp(key, "xprod_fuse")) {
+    c->xprod_fuse = value ? 1 : 0;
   } else if (!strcmp(key, "xprod_rw")) {
     if (value != 0 && value != 1 && value != 2 && value != 4) return fail(c, PPLS_E_ARG, "xprod_rw must be 0, 1, 2 or 4");
     c->xprod_rw = (int)value;
@@ -1482,7 +1495,7 @@ int ppls_em_run(ppls_ctx* c, ppls_theta* th, int r, int max_steps, double atol, 
     }
     const int nxt = cur ^ 1;
     const bool wm = want_mu && !c->xp_active && (do_check || s == max_steps + 1);
-    if ((rc = stats_step(c, r, cur, wm))) return rc;
+    if ((rc = stats_step(c, r, cur, wm, true))) return rc;
     if ((rc = finalize(c, r, cur, nxt, s >= 2 ? s - 2 : -1, type, do_check && s >= 3 ? s : 0))) return rc;
     if (do_check) {
       const size_t k = (size_t)(s - 1) % EM_LOOKAHEAD;
@@ -2387,7 +2400,7 @@ int ppls_em_iterate(ppls_ctx* c, int nsteps, int type) {
   int rc;
   for (int s = 0; s < nsteps; ++s) {
     const int nxt = c->em_cur ^ 1;
-    if ((rc = stats_step(c, c->em_r, c->em_cur, false))) return rc;
+    if ((rc = stats_step(c, c->em_r, c->em_cur, false, true))) return rc;
     if ((rc = finalize(c, c->em_r, c->em_cur, nxt, c->em_iter >= 1 ? c->em_iter - 1 : -1, type))) return rc;
     c->em_cur = nxt;
     ++c->em_iter;

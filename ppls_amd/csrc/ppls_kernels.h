@@ -69,6 +69,9 @@ struct PplsFinalizeArgs {
   unsigned* team_bar;    // wide-p polar teams: 8 zero-initialised counters, or nullptr (one block each)
   double* team_part;     // 2 x 3 x PPLS_TEAM_MAX x 64 doubles
   int team_rows;         // rows of S per team member (0: PPLS_TEAM_ROWS)
+  const double* xpM;     // cross-product form (ppls_xprod.hip): M = S blockdiag(Wc, Cc), (ldx + ldy) x 2r
+                         // column-major, or nullptr; when set, the scalar block forms the Gram B'M itself
+                         // (in the slack of the polar blocks) and writes it to stats' Gram slot
 };
 
 #define PPLS_TEAM_ROWS 2048   // rows of S per polar team member (tools/team_rows_ab.py: p = 2000 in one block is 4 us faster than a team of 2; C5 equal at 1024 and 2048)

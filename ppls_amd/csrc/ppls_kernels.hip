@@ -2048,6 +2048,74 @@ __device__ __forceinline__ void ppls_stop_test(const double* loglik, int idx, in
   }
 }
 
+// The cross-product form's Gram B'M (B = blockdiag(W, C), M = S B) on the finalize's scalar block,
+// in the slack of the polar blocks: entries (a, b) of the X rows with a < r, b in [a, 2r)
+// (W'X'XW upper triangle, then W'X'YC) and of the Y rows with a <= b < r (C'Y'YC upper triangle),
+// 2r^2 + r sums; per thread a stride of rows, then ppls_block_sum_t in passes of 64 entries.
+// Written mirrored to sG (LDS, what the moments read) and G (stats' Gram slot).  r <= 8.
+template <int R, int NT>
+__device__ void ppls_xp_gram_block(const double* __restrict__ M, const double* __restrict__ Wc,
+                                   const double* __restrict__ Cc, int ldx, int ldy, double* sG, double* G) {
+  constexpr int R2 = 2 * R, NX = R * (R + 1) / 2 + R * R, NE = NX + R * (R + 1) / 2;
+  constexpr int NPASS = (NE + 63) / 64;
+  __shared__ double sh[(NT / 64) * 64];
+  const int P = ldx + ldy, tid = threadIdx.x;
+  double acc[NPASS * 64];
+#pragma unroll
+  for (int e = 0; e < NPASS * 64; ++e) acc[e] = 0.0;
+  for (int i = tid; i < ldx; i += NT) {
+    double w[R], m[R2];
+#pragma unroll
+    for (int a = 0; a < R; ++a) w[a] = Wc[(int64_t)a * ldx + i];
+#pragma unroll
+    for (int b = 0; b < R2; ++b) m[b] = M[(int64_t)b * P + i];
+    int e = 0;
+#pragma unroll
+    for (int a = 0; a < R; ++a)
+#pragma unroll
+      for (int b = a; b < R2; ++b, ++e) acc[e] = fma(w[a], m[b], acc[e]);
+  }
+  for (int i = tid; i < ldy; i += NT) {
+    double cv[R], m[R];
+#pragma unroll
+    for (int a = 0; a < R; ++a) cv[a] = Cc[(int64_t)a * ldy + i];
+#pragma unroll
+    for (int b = 0; b < R; ++b) m[b] = M[(int64_t)(R + b) * P + ldx + i];
+    int e = NX;
+#pragma unroll
+    for (int a = 0; a < R; ++a)
+#pragma unroll
+      for (int b = a; b < R; ++b, ++e) acc[e] = fma(cv[a], m[b], acc[e]);
+  }
+#pragma unroll
+  for (int ps = 0; ps < NPASS; ++ps) {
+    double v[64];
+#pragma unroll
+    for (int e = 0; e < 64; ++e) v[e] = acc[ps * 64 + e];
+    ppls_block_sum_t<64, NT / 64>(v, sh);
+#pragma unroll
+    for (int e = 0; e < 64; ++e) acc[ps * 64 + e] = v[e];
+  }
+  if (tid == 0) {
+    int e = 0;
+#pragma unroll
+    for (int a = 0; a < R; ++a)
+#pragma unroll
+      for (int b = a; b < R2; ++b, ++e) {
+        sG[b * R2 + a] = sG[a * R2 + b] = acc[e];
+        G[b * R2 + a] = G[a * R2 + b] = acc[e];
+      }
+#pragma unroll
+    for (int a = 0; a < R; ++a)
+#pragma unroll
+      for (int b = a; b < R; ++b, ++e) {
+        sG[(R + b) * R2 + R + a] = sG[(R + a) * R2 + R + b] = acc[e];
+        G[(R + b) * R2 + R + a] = G[(R + a) * R2 + R + b] = acc[e];
+      }
+  }
+  __syncthreads();
+}
+
 #define PPLS_FIN_THREADS 256   // 1 wave per SIMD: the r x r code may use all 512 VGPR+AGPRs
 
 // Block 0: W_next = orth(S_X); block 1: C_next = orth(S_Y); block 2: scalars (moments, loglik,
@@ -2065,7 +2133,7 @@ __global__ __launch_bounds__(PPLS_FIN_THREADS) void ppls_finalize_kernel(
     const double* __restrict__ gram_cur, double* __restrict__ gram_nxt, double* __restrict__ vstate,
     int stage_lds, long long* __restrict__ trace,
     int* __restrict__ stop, int* __restrict__ stop_mirror, int stop_check, int stop_step, double atol,
-    int KX, int KY, unsigned* __restrict__ team_bar, double* __restrict__ team_part) {
+    int KX, int KY, unsigned* __restrict__ team_bar, double* __restrict__ team_part, const double* __restrict__ xpM) {
   // em_run converged at an EARLIER iteration: exit.  The flag this launch's own scalar block may
   // set (== stop_step) must not stop a polar-team member that starts late, or its teammates would
   // wait at the team barrier for a member that never comes.
@@ -2128,12 +2196,16 @@ __global__ __launch_bounds__(PPLS_FIN_THREADS) void ppls_finalize_kernel(
     return;
   }
   if (!(mode & 2)) return;
+  // cross-product form: the Gram of [XW YC] = B'M from M = S B (the polar blocks run meanwhile)
+  if constexpr (R <= 8)
+    if (xpM) ppls_xp_gram_block<R, NT>(xpM, Wc, Cc, ldx, ldy, s_G, const_cast<double*>(G));
   // stage theta's scalars, the Gram and W'W, C'C in LDS (all threads)
   {
     const double* src = (const double*)sc_cur;
     double* dst = (double*)&s_cur;
     for (int i = tid; i < (int)(sizeof(PplsScalars) / 8); i += NT) dst[i] = src[i];
-    for (int i = tid; i < 4 * R * R; i += NT) s_G[i] = G[i];
+    if (!xpM || R > 8)
+      for (int i = tid; i < 4 * R * R; i += NT) s_G[i] = G[i];
     if (gram_cur)
       for (int i = tid; i < R * R; i += NT) { s_WtW[i] = gram_cur[i]; s_CtC[i] = gram_cur[R * R + i]; }
   }
@@ -2408,7 +2480,7 @@ hipError_t launch_finalize_t(const PplsFinalizeArgs* f, hipStream_t st) {
                      f->N, f->p, f->q, f->ldx, f->ldy, f->Wc, f->Cc, f->sc_cur, f->Wn, f->Cn, f->sc_nxt, f->mom,
                      f->loglik, f->logl_index, f->work, f->status, f->qr, f->mode, f->gram_cur,
                      f->gram_nxt, f->vstate, use, f->trace, f->stop, f->stop_mirror, f->stop_check,
-                     f->stop_step, f->atol, KX, KY, f->team_bar, f->team_part);
+                     f->stop_step, f->atol, KX, KY, f->team_bar, f->team_part, f->xpM);
   return hipGetLastError();
 }
 

@@ -28,24 +28,25 @@ int ppls_xprod_tile_rows(int P, int r, int rw_opt, int num_cus);
 
 // One iteration's statistics from S (P x P row-major, P = ldx + ldy, symmetric) and theta = (Wp, Cp,
 // sc): stats = [X'mu_T (ldx x r) | Y'mu_U (ldy x r) | Gram (2r x 2r)], the layout the sweeps'
-// reduction writes.  Two launches: the apply kernel (kind 0 row tiles, kind 1 row groups; rw rows
-// per wave) streams S once and writes the X'mu_T, Y'mu_U rows and M = S B (P x 2r column-major,
-// scratch); the Gram kernel forms B'M, one workgroup per entry (fixed-order sums: deterministic).
+// reduction writes.  The apply kernel (kind 0 row tiles, kind 1 row groups; rw rows per wave)
+// streams S once and writes the X'mu_T, Y'mu_U rows and M = S B (P x 2r column-major, scratch); the
+// Gram kernel forms B'M, one workgroup per entry (fixed-order sums: deterministic) -- unless
+// with_gram = 0, when the finalize that follows forms it (PplsFinalizeArgs::xpM, r <= 8).
 // stop: the em_run stop flag (both kernels exit if it is set) or nullptr.
+hipError_t ppls_launch_xprod_apply(const double* S, int ldx, int ldy, int r, int kind, int rw, const double* Wp,
+                                   const double* Cp, const PplsScalars* sc, double* stats, double* M, const int* stop,
+                                   int with_gram, hipStream_t st);
+
 // Lower-triangle form (r <= PPLS_XP_TRI_RMAX; reads only S's lower 128 x 128 tiles): the run list
 // (runs of tiles of one block row; items: 4 ints per run {I, J0, J1, 0}, row_items: nb + 1 run
 // offsets per block row; both nullable) and the partials' lengths in doubles.  Returns the run count.
 #define PPLS_XP_TRI_RMAX 10
 int ppls_xprod_tri_plan(int ldx, int ldy, int r, int num_cus, int* items, int* row_items, int64_t* rowpart_len,
                         int64_t* colpart_len);
-// The same statistics as ppls_launch_xprod_apply from the lower triangle: the tile kernel, the
-// partial reduction (writes M, X'mu_T, Y'mu_U) and the Gram kernel (items, row_items on the device).
+// The same statistics from the lower triangle: the tile kernel, the partial reduction (writes M,
+// X'mu_T, Y'mu_U) and the Gram kernel (items, row_items on the device).
 hipError_t ppls_launch_xprod_tri(const double* S, int ldx, int ldy, int r, const double* Wp, const double* Cp,
                                  const PplsScalars* sc, double* stats, double* M, const int* items, int nruns,
                                  const int* row_items, double* rowpart, double* colpart, const int* stop,
                                  hipStream_t st);
-
-hipError_t ppls_launch_xprod_apply(const double* S, int ldx, int ldy, int r, int kind, int rw, const double* Wp,
-                                   const double* Cp, const PplsScalars* sc, double* stats, double* M, const int* stop,
-                                   hipStream_t st);
 }

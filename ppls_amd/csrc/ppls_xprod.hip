@@ -585,7 +585,7 @@ int ppls_xprod_tile_rows(int P, int r, int rw_opt, int num_cus) {
 
 hipError_t ppls_launch_xprod_apply(const double* S, int ldx, int ldy, int r, int kind, int rw, const double* Wp,
                                    const double* Cp, const PplsScalars* sc, double* stats, double* M, const int* stop,
-                                   hipStream_t st) {
+                                   int with_gram, hipStream_t st) {
   if (ldx < 2 || ldy < 2 || (ldx & 1) || (ldy & 1) || r < 1 || r > PPLS_RMAX) return hipErrorInvalidValue;
   if (((uintptr_t)S | (uintptr_t)Wp | (uintptr_t)Cp) & 15) return hipErrorInvalidValue;   // 16-B loads
   hipError_t e;
@@ -602,6 +602,7 @@ hipError_t ppls_launch_xprod_apply(const double* S, int ldx, int ldy, int r, int
     default: return hipErrorInvalidValue;
   }
   if (e != hipSuccess) return e;
+  if (!with_gram) return hipSuccess;   // the finalize's scalar block forms B'M (PplsFinalizeArgs::xpM)
   const int R2 = 2 * r;
   hipLaunchKernelGGL(ppls_xprod_gram_kernel, dim3((unsigned)(R2 * (R2 + 1) / 2)), dim3(256), 0, st, ldx, ldy, r, Wp,
                      Cp, M, stats, stop);

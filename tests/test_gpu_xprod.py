@@ -18,7 +18,7 @@ from oracle import ppls_oracle as o
 pytestmark = pytest.mark.gpu
 
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
-DEFAULTS = dict(xprod=0, xprod_kernel=0, xprod_rw=0, dtype=0)
+DEFAULTS = dict(xprod=0, xprod_kernel=0, xprod_rw=0, xprod_fuse=1, dtype=0)
 
 
 @pytest.fixture(scope="module")
@@ -52,18 +52,20 @@ def _golden():
     return sorted(f for f in os.listdir(GOLD) if f.endswith(".npz") and not f.startswith(("seq_", "meta_", "rcheck_")))
 
 
-# (xprod_kernel, xprod_rw): auto, row groups, row tiles (LDS-staged W, C), lower triangle
-KERNELS = [(0, 0), (1, 1), (1, 2), (2, 1), (2, 2), (2, 4), (3, 0)]
+# (xprod_kernel, xprod_rw, xprod_fuse): auto, row groups, row tiles (LDS-staged W, C), lower
+# triangle; the Gram formed by the finalize (fuse 1, default) or by its own kernel
+KERNELS = [(0, 0, 1), (0, 0, 0), (1, 1, 1), (1, 2, 1), (2, 1, 1), (2, 2, 1), (2, 4, 1), (3, 0, 1)]
 
 
-@pytest.mark.parametrize("kernel,rw", KERNELS, ids=[f"k{k}rw{w}" for k, w in KERNELS])
+@pytest.mark.parametrize("kernel,rw,fuse", KERNELS, ids=[f"k{k}rw{w}f{f}" for k, w, f in KERNELS])
 @pytest.mark.parametrize("name", _golden())
-def test_xprod_em_run_matches_golden(ctx, name, kernel, rw):
+def test_xprod_em_run_matches_golden(ctx, name, kernel, rw, fuse):
     g = np.load(os.path.join(GOLD, name))
     meta = json.loads(str(g["meta"]))
     ctx.set_option("xprod", 1)
     ctx.set_option("xprod_kernel", kernel)
     ctx.set_option("xprod_rw", rw)
+    ctx.set_option("xprod_fuse", fuse)
     ctx.set_data(g["X"], g["Y"])
     th0 = dict(W=g["W0"], C=g["C0"], B=np.diag(g["B0"]), sigE=g["sig0"][0], sigF=g["sig0"][1],
                sigH=g["sig0"][2], sigT=np.diag(g["T0"]))
