@@ -358,6 +358,27 @@ def sweep_stats(X, Y, W, C, coef):
     return dict(SX=X.T @ mu_T, SY=Y.T @ mu_U, G=Z.T @ Z, mu_T=mu_T, mu_U=mu_U)
 
 
+def crossproducts(X, Y):
+    """S = [X Y]'[X Y] ((p+q) x (p+q)): the cross-product form's one data pass."""
+    Z = np.hstack([X, Y])
+    return Z.T @ Z
+
+
+def xprod_stats(S, p, W, C, coef):
+    """sweep_stats from S instead of the rows: with B = blockdiag(W, C) and M = S B,
+    X'mu_T = M[:p] (alpha | beta), Y'mu_U = M[p:] (gamma | delta) (EM_W_multi.R:691-694, :732-733)
+    and Gram([Xw Yc]) = B' M (:696-712, loglC.cpp:334-335)."""
+    r = W.shape[1]
+    q = C.shape[0]
+    B = np.zeros((p + q, 2 * r))
+    B[:p, :r] = W
+    B[p:, r:] = C
+    M = S @ B
+    SX = M[:p, :r] * coef["alpha"] + M[:p, r:] * coef["beta"]
+    SY = M[p:, :r] * coef["gamma"] + M[p:, r:] * coef["delta"]
+    return dict(SX=SX, SY=SY, G=B.T @ M)
+
+
 def mu_coefficients(B, sigE, sigF, sigH, sigT):
     """alpha, beta, gamma, delta with mu_T[:,k] = alpha_k Xw_k + beta_k Yc_k and
     mu_U[:,k] = gamma_k Xw_k + delta_k Yc_k -- EM_W_multi.R:691-694 collected per column."""
