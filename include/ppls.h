@@ -260,7 +260,8 @@ int ppls_sweep_balance(ppls_ctx* ctx, double* w8, int64_t* bounds, int cap, int*
 int ppls_comm_info(ppls_ctx* ctx, int* nranks, int* rank, double* allreduce_ms, int64_t* allreduce_calls,
                    int reset);
 /* Cross-product form (option "xprod"): form S now (*ms = the MFMA Gram kernel time, *total_ms = with
- * the all-reduce and allocation; both nullable) -- otherwise the first run that reads S forms it. */
+ * the all-reduce and allocation; both nullable) -- otherwise the first run that reads S forms it.
+ * Collective when the rows are sharded: every rank calls it (one all-reduce of (p+q)^2 doubles). */
 int ppls_xprod_prepare(ppls_ctx* ctx, double* ms, double* total_ms);
 /* Its state: *ready = S is formed for the current data, *bytes_per_pass = the bytes of S one
  * iteration reads (8 P^2, P = padded p + q, or its lower 128 x 128 tiles for the triangle kernel),
