@@ -1075,7 +1075,8 @@ int ppls_set_option(ppls_ctx* c, const char* key, int64_t value) {
   } else if (!strcmp(key, "xprod_fuse")) {
     c->xprod_fuse = value ? 1 : 0;
   } else if (!strcmp(key, "xprod_rw")) {
-    if (value != 0 && value != 1 && value != 2 && value != 4) return fail(c, PPLS_E_ARG, "xprod_rw must be 0, 1, 2 or 4");
+    if (value != 0 && value != 1 && value != 2 && value != 4 && value != 8)
+      return fail(c, PPLS_E_ARG, "xprod_rw must be 0, 1, 2, 4 or 8");
     c->xprod_rw = (int)value;
   } else if (!strcmp(key, "timing")) {
     if (value < 0) return fail(c, PPLS_E_ARG, "timing must be >= 0");

@@ -494,8 +494,9 @@ hipError_t launch_tile_rw(int rw, const double* S, int ldx, int ldy, const doubl
                           const PplsScalars* sc, double* stats, double* M, const int* stop, hipStream_t st) {
   if (rw == 1) return launch_tile<R, 1>(S, ldx, ldy, Wp, Cp, sc, stats, M, stop, st);
   if (rw == 2) return launch_tile<R, 2>(S, ldx, ldy, Wp, Cp, sc, stats, M, stop, st);
+  if (rw == 4) return launch_tile<R, 4>(S, ldx, ldy, Wp, Cp, sc, stats, M, stop, st);   // one phase's RW r accumulators live
   if constexpr (R <= 8)
-    if (rw == 4) return launch_tile<R, 4>(S, ldx, ldy, Wp, Cp, sc, stats, M, stop, st);
+    if (rw == 8) return launch_tile<R, 8>(S, ldx, ldy, Wp, Cp, sc, stats, M, stop, st);
   return hipErrorInvalidValue;
 }
 
@@ -579,7 +580,7 @@ int ppls_xprod_rows_per_wave(int P, int r, int rw_opt) {
 }
 
 int ppls_xprod_tile_rows(int P, int r, int rw_opt, int num_cus) {
-  if (rw_opt == 1 || rw_opt == 2 || (rw_opt == 4 && r <= 8)) return rw_opt;
+  if (rw_opt == 1 || rw_opt == 2 || rw_opt == 4 || (rw_opt == 8 && r <= 8)) return rw_opt;
   return P / 8 >= 2 * num_cus ? 2 : 1;   // two rows per wave while >= 2 workgroups per CU remain
 }
 
