@@ -492,9 +492,13 @@ _DEFAULT_CTX = None
 
 
 def default_context() -> Context:
+    """The context the R-named functions use when no ``ctx`` is given: GPU 0, with the statistics
+    path chosen per run by the cost model (option "xprod" = -1, as the R shim in INTEGRATION.md
+    sets it: the cross-product form once a run is long enough to repay forming S)."""
     global _DEFAULT_CTX
     if _DEFAULT_CTX is None:
         _DEFAULT_CTX = Context(0)
+        _DEFAULT_CTX.set_option("xprod", -1)
     return _DEFAULT_CTX
 
 
