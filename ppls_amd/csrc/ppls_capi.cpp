@@ -2217,28 +2217,26 @@ int ppls_variances(ppls_ctx* c, const double* mu, const double* Cdiag, double si
   // W = orth(t(data) %*% mu, type = "SVD") (:831-832)
   if ((rc = host_orth(Sp.data(), p, a, PPLS_ORTH_SVD, W)))
     return done(fail(c, rc, "orth(t(data) %%*%% mu): rank-deficient"));
-  // ---- G = D'D on MFMA, split over row ranges, all-reduced ----------------------------------
+  // ---- G = D'D on MFMA, split over row ranges, all-reduced -- or, when the cross-product form
+  // has formed S = [X Y]'[X Y] for this data (ppls_xprod.hip), its X'X or Y'Y block as it stands
+  // (already summed over ranks; symmetric, so its row-major block is the column-major G) ------
   VRC(dalloc(c, &dG, pp));
-  if (n > 0) {
-    const int ntiles = ppls_gram_tiles(p);
-    const int64_t slots = (int64_t)c->num_cus * ppls_gram_occupancy(f32);
-    int nsplit = 1;
-    double best = -1.0;
-    for (int sp = 1; sp <= 32; ++sp) {
-      if (sp > 1 && ((int64_t)sp * 512 > n || (double)sp * pp * 8.0 > 4.0e9)) break;
-      const int64_t w = (int64_t)ntiles * sp;
-      const double eff = (double)w / (double)(((w + slots - 1) / slots) * slots);
-      if (eff > best + 1e-9) { best = eff; nsplit = sp; }
-      if (eff >= 0.95) break;
-    }
-    VRC(dalloc(c, &dpart, (size_t)nsplit * pp));
-    VCHK(ppls_launch_gram(D, f32, n, ld, p, nsplit, dpart, (int64_t)pp, c->stream));
-    VCHK(ppls_launch_gram_finish(dpart, nsplit, (int64_t)pp, p, dG, c->stream));
-    dfree(dpart);
+  if (c->xp_ready) {
+    const size_t P = (size_t)c->ldx + c->ldy, off = xory ? (size_t)c->ldx : 0;
+    VCHK(hipMemcpy2DAsync(dG, sizeof(double) * p, c->xp_S + off * P + off, sizeof(double) * P, sizeof(double) * p, p,
+                          hipMemcpyDeviceToDevice, c->stream));
   } else {
-    VCHK(hipMemsetAsync(dG, 0, sizeof(double) * pp, c->stream));
+    if (n > 0) {
+      const int nsplit = gram_splits(c, p, n);
+      VRC(dalloc(c, &dpart, (size_t)nsplit * pp));
+      VCHK(ppls_launch_gram(D, f32, n, ld, p, nsplit, dpart, (int64_t)pp, c->stream));
+      VCHK(ppls_launch_gram_finish(dpart, nsplit, (int64_t)pp, p, dG, c->stream));
+      dfree(dpart);
+    } else {
+      VCHK(hipMemsetAsync(dG, 0, sizeof(double) * pp, c->stream));
+    }
+    VRC(allreduce(c, dG, pp));
   }
-  VRC(allreduce(c, dG, pp));
   // ---- per component: M = B_exp - SSt_exp, varMatrix = -solve(M), seLoad --------------------
   if (!c->blas) {
     if (rocblas_create_handle(&c->blas) != rocblas_status_success) return done(fail(c, PPLS_E_HIP, "rocblas_create_handle failed"));

@@ -54,14 +54,20 @@ def test_gram_fp32_storage(ctx):
     assert _rel(G, X32.T @ X32) < 1e-13
 
 
+@pytest.mark.parametrize("from_s", [False, True], ids=["gram", "from_S"])
 @pytest.mark.parametrize("xy", ["X", "Y"])
-def test_variances_matches_oracle(ctx, xy):
+def test_variances_matches_oracle(ctx, xy, from_s):
+    """from_S: the cross-product form has formed S = [X Y]'[X Y] for this data, and the variances
+    take its X'X / Y'Y block instead of a Gram of their own (q = 29: the Y block starts mid-tile)."""
     import ppls_amd
     X, Y, th0 = make_problem(700, 37, 29, 3, seed=61)
     fit = o.ppls_simult(X, Y, 3, EMsteps=20, atol=-np.inf, theta0=th0)
     D = X if xy == "X" else Y
     ref = o.variances_ppls_simult(fit, D, xy)
     ctx.set_data(X, Y)
+    if from_s:
+        ctx.xprod_prepare()
+        assert ctx.xprod_info(3)["ready"]
     got = ppls_amd.variances_PPLS_simult(fit, None, xy, ctx=ctx)
     assert np.abs(got["W"] - ref["W"]).max() < 1e-10
     for i in range(3):
