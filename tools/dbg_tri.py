@@ -1,3 +1,6 @@
+"""Diagnostic: statistics from S by the lower-triangle kernel (option xprod_kernel 3) against the
+row-tile kernel (2), per block of the output -- the script that located the reduce-scatter pad race
+(DESIGN.md §12).  python tools/dbg_tri.py"""
 import sys, numpy as np
 sys.path.insert(0, '/root/repo'); sys.path.insert(0, '/root/repo/tests')
 from conftest import make_problem
