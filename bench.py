@@ -1,12 +1,20 @@
 """bench.py -- EM iterations/s of the PPLS_simult inner loop on MI355X (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2] [--no-cpu]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2|...] [--no-cpu]
+                    [--comm rccl|host] [--oversubscribe] [--xprod-steps K] [--no-call]
 
 One "step" = one EM iteration = sweep over X, Y (E-step sufficient statistics + log-likelihood of
 the current theta) + deterministic reduction + [RCCL all-reduce] + finalize (M-step incl. polar
 factor).  Workload: BASELINE config C3 (n = 1e6, p = q = 2000, r = 5, fp64) by default; samples
 are sharded over ranks (strong scaling: n is fixed).  Data are synthetic (simulC model, Philox
-normals) generated on the device before the timed region.  Rank 0 prints ONE JSON line.
+normals) generated on the device before the timed region.  Rank 0 prints ONE JSON line -- or, when
+the ranks disagree (theta digests, RCCL's own rank count, a non-finite log-likelihood), nothing on
+stdout, the reason on stderr and exit status 3.
+
+Beside the headline: the cross-product form of the same iterations ("xprod"), and the whole
+user-facing call PPLS_simult(X, Y, r) with its defaults ("call": the 'random' PPLS(X, Y, r, 20,
+1e-4) initialiser, EMsteps = 10, atol = 1e-4, Expectations) under each statistics path, with the
+C restatement of the same call timed on a row sample of the host.
 """
 from __future__ import annotations
 
@@ -37,7 +45,11 @@ CONFIGS = {
 METRIC = "EM iterations/sec + log-lik rel-err vs CPU ref, n=1e6 p=q=2000 r=5"
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 READ_CEILING_GBS = 6848.0   # measured read-only ceiling, profiles/r1_read_bw_probe.txt (tools/read_bw_probe.hip)
+MALL_REREAD_GBS = 6800.0    # measured re-read of a 128 MB (MALL-resident) buffer, low end of 6.8-7.8 TB/s
+                            # (profiles/r3_mall_read_probe.txt, tools/mall_read_probe.hip)
 FP64_PEAK_TF = 78.6     # MI355X fp64 vector (= fp64 MFMA) dense peak, TFLOP/s
+CALL_SEED = 20261017    # numpy stream of the 'random' initial guesses of the timed PPLS_simult calls
+READBACK = "readback of a committed rocprofv3 PMC summary under profiles/ (not measured in this run)"
 
 
 def polar(M):
@@ -60,46 +72,52 @@ def make_truth_and_theta0(p, q, r):
     return truth, th0
 
 
-def load_traffic(workload_key):
-    """HBM bytes per sweep launch from a committed rocprofv3 PMC pass (profiles/), or None."""
-    path = os.path.join(ROOT, "profiles", f"pmc_sweep_{workload_key}.json")
-    if not os.path.exists(path):
-        return None
+def _profile_json(name):
     try:
-        with open(path) as f:
-            return json.load(f).get("hbm_bytes_per_launch")
+        with open(os.path.join(ROOT, "profiles", name)) as f:
+            return json.load(f)
     except (OSError, ValueError):
         return None
 
 
+def _source(name, js):
+    """Where a committed number came from: the file, the source tree the profiled run used (when
+    the summary records it) and its own description."""
+    return dict(file=f"profiles/{name}", profiled_tree=js.get("profiled_tree"), recorded=js.get("source"),
+                kind=READBACK)
+
+
+def load_traffic(workload_key):
+    """(HBM bytes per sweep launch, provenance) from a committed rocprofv3 PMC pass, or (None, None)."""
+    name = f"pmc_sweep_{workload_key}.json"
+    js = _profile_json(name)
+    if not js or js.get("hbm_bytes_per_launch") is None:
+        return None, None
+    return js["hbm_bytes_per_launch"], _source(name, js)
+
+
 def load_xprod_traffic(config):
-    """Read bytes per launch of the cross-product tile kernel from a committed rocprofv3 PMC pass
-    (profiles/pmc_xprod_<config>_dp1.json), or None."""
-    try:
-        with open(os.path.join(ROOT, "profiles", f"pmc_xprod_{config}_dp1.json")) as f:
-            ks = json.load(f)["kernels"]
-    except (OSError, ValueError, KeyError):
-        return None
-    for name, k in ks.items():
-        if "tile" in name:
-            return k.get("read_bytes_per_launch")
-    return None
+    """(Read bytes per launch of the cross-product tile kernel, provenance) from a committed
+    rocprofv3 PMC pass (profiles/pmc_xprod_<config>_dp1.json), or (None, None)."""
+    name = f"pmc_xprod_{config}_dp1.json"
+    js = _profile_json(name)
+    for kname, k in ((js or {}).get("kernels") or {}).items():
+        if "tile" in kname:
+            return k.get("read_bytes_per_launch"), _source(name, js)
+    return None, None
 
 
 def load_compute_counters(workload_key, kernel_sub):
     """Counter-based MFMA / VALU utilisation of a kernel from a committed rocprofv3 PMC pass
     (profiles/pmc_compute_<workload>.json, tools/pmc_compute.sh + pmc_compute_summary.py), or None."""
-    path = os.path.join(ROOT, "profiles", f"pmc_compute_{workload_key}.json")
-    try:
-        with open(path) as f:
-            k = json.load(f)["kernels"].get(kernel_sub)
-    except (OSError, ValueError, KeyError):
-        return None
+    name = f"pmc_compute_{workload_key}.json"
+    js = _profile_json(name)
+    k = ((js or {}).get("kernels") or {}).get(kernel_sub)
     if not k:
         return None
     return dict(mfma_busy=k["mfma_busy"], valu_busy=k["valu_busy"], effective_clock_ghz=k.get("effective_clock_ghz"),
                 fp64_valu_tflops=k.get("fp64_valu_tflops"), fp64_mfma_tflops=k.get("fp64_mfma_tflops"),
-                source=f"profiles/pmc_compute_{workload_key}.json ({kernel_sub})")
+                source=dict(_source(name, js), kernel=kernel_sub))
 
 
 def cpu_model():
@@ -138,9 +156,9 @@ def cpu_baseline(ctx, th0, cfg, iters=3, one_core_rows=100_000):
     t0 = time.perf_counter()
     cpu_ref.em_steps(Xs, Ys, th, iters, nthreads=1)
     dt1 = time.perf_counter() - t0
-    cpu_ref.load().cpu_ref_em_step   # noqa: B018 (keep the library loaded)
     del X, Y, Xs, Ys
     # GPU on the same resident rows, same theta0, iters + 1 iterations
+    ctx.set_option("xprod", 0)
     est, ll_gpu, _, _ = ctx.em_run(th0, iters + 1, -np.inf, 0, want_eout=False)
     rel = float(np.abs(ll_gpu - ll_all).max() / np.abs(ll_all).max())
     Wc, Cc, _, _ = canonicalize(th_cpu["W"], th_cpu["C"], th_cpu["B"], th_cpu["sigT"])
@@ -156,24 +174,27 @@ def cpu_baseline(ctx, th0, cfg, iters=3, one_core_rows=100_000):
                                      f"value = rows*iterations/s / n")), rel, werr
 
 
-def bench_xprod(ctx, th0, args, barrier, dist, torch, r, ll_stream, t_stream):
+def _reduce_max(dist, torch, v):
+    if dist is None:
+        return v
+    tt = torch.tensor([v], dtype=torch.float64)
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    return float(tt.item())
+
+
+def bench_xprod(ctx, th0, args, barrier, tmax, r, ll_stream, t_stream):
     """The cross-product form of the same iterations (option "xprod", ppls_xprod.hip): S = [X Y]'[X Y]
     formed once (MFMA Gram of the local rows + ONE all-reduce of S), then every iteration reads S
     (8 P^2 bytes) instead of X and Y and needs no collective.  Timed like the headline: barrier +
     synchronize around the formation of S and around args.xprod_steps iterations, max over ranks."""
-    def tmax(v):
-        if dist is None:
-            return v
-        tt = torch.tensor([v], dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        return float(tt.item())
-
     barrier()
     ctx.set_option("xprod", 1)
+    ctx.xprod_release()
     t0 = time.perf_counter()
     gram_ms, _ = ctx.xprod_prepare()
     barrier()
     t_setup = tmax(time.perf_counter() - t0)
+    _, ar_ms, total_ms = ctx.xprod_setup_times()
     info = ctx.xprod_info(r)
     ctx.em_begin(th0)
     ctx.em_iterate(args.warmup)
@@ -186,41 +207,107 @@ def bench_xprod(ctx, th0, args, barrier, dist, torch, r, ll_stream, t_stream):
     dt = tmax(time.perf_counter() - t0)
     ctx.set_option("timing", 0)
     kms, launches = ctx.sweep_timing(reset=True)
-    _, ll_x = ctx.em_state()
+    est, ll_x = ctx.em_state()
     k = min(len(ll_x), len(ll_stream))
     rel = float(np.abs(ll_x[:k] - ll_stream[:k]).max() / np.abs(ll_stream[:k]).max()) if k else None
     t_x = dt / args.xprod_steps
     avg_us = 1e3 * kms / max(launches, 1)
     achieved = info["bytes_per_pass"] / (avg_us * 1e-6) / 1e9 if launches else None
     gram_tf = info["gram_flops"] / (gram_ms * 1e-3) / 1e12 if gram_ms > 0 else None
+    traffic, traffic_src = load_xprod_traffic(args.config)
 
-    def fit_s(steps):   # a whole PPLS_simult loop of `steps` iterations (+1 sweep for the last loglik)
+    def fit_s(steps):   # a PPLS_simult loop of `steps` iterations (+1 sweep for the last loglik)
         return dict(stream=(steps + 1) * t_stream, xprod=t_setup + (steps + 1) * t_x)
 
-    return dict(
+    return est, ll_x, dict(
         what="cross-product form: S = [X Y]'[X Y] formed once on MFMA (+1 all-reduce of S over ranks), then each "
              "iteration reads S instead of X, Y (no per-iteration collective); same iterates, sums reordered",
         setup_s=t_setup, gram_kernel_ms=gram_ms, gram_tflops=gram_tf,
+        setup_allreduce_ms=ar_ms, setup_allreduce_bytes=info["bytes_per_pass"] if ar_ms > 0 else 0,
+        setup_total_ms_rank0=total_ms,
         gram_roofline=dict(bound="mfma", achieved=gram_tf, peak=FP64_PEAK_TF, unit="TFLOP/s",
                            frac=(gram_tf / FP64_PEAK_TF) if gram_tf else None,
                            flops_per_launch=info["gram_flops"],
                            counters=load_compute_counters(f"{args.config}_dp1", "gram_mfma")),
         steps=args.xprod_steps, ms_per_step=1e3 * t_x, it_per_s=1.0 / t_x,
         roofline=dict(bound="hbm", achieved=achieved, peak=HBM_PEAK_GBS, unit="GB/s",
-                      frac=(achieved / HBM_PEAK_GBS) if achieved else None, kernel="xprod_tile + xprod_gram",
-                      traffic=load_xprod_traffic(args.config),
+                      frac=(achieved / HBM_PEAK_GBS) if achieved else None,
+                      # S (128 MB at C3) lives in the 256 MiB Infinity Cache between iterations: the
+                      # measured re-read rate of such a buffer is the ceiling that applies there
+                      measured_mall_reread=MALL_REREAD_GBS,
+                      frac_of_mall_reread=(achieved / MALL_REREAD_GBS) if achieved else None,
+                      kernel="xprod_tile (+ the Gram B'M in the finalize)",
+                      traffic=traffic, traffic_source=traffic_src,
                       avg_kernel_us=avg_us, bytes_per_launch=info["bytes_per_pass"],
-                      rows_per_workgroup=info["rows_per_wave"]),
+                      rows_per_wave=info["rows_per_wave"]),
         loglik_rel_diff_vs_streaming=rel, loglik_compared=k,
         breakeven_steps=(t_setup / (t_stream - t_x)) if t_stream > t_x else None,
         fit_seconds={str(s): fit_s(s) for s in (10, 100, 1000, 10000)})
 
 
+def bench_call(ctx, r, barrier, tmax):
+    """The whole user-facing PPLS_simult(X, Y, r) (EM_W_multi.R:758-807) with its defaults: the
+    initialiser PPLS(X, Y, r, 20, 1e-4, 'random') (:762, :229-279; draws from a fixed numpy stream),
+    EMsteps = 10, atol = 1e-4, and the Expectations (mu_T, mu_U of this rank's rows copied to the
+    host), through ppls_amd.PPLS_simult on the resident data.  Once per statistics path: stream
+    (option xprod 0), xprod (1: S formed inside the call) and auto (-1: the cost model, S formed
+    inside the call when it chooses it).  Barrier + synchronize around each call, max over ranks."""
+    from ppls_amd import PPLS_simult
+    out = {}
+    for mode, opt in (("stream", 0), ("xprod", 1), ("auto", -1)):
+        ctx.set_option("xprod", opt)
+        ctx.xprod_release()   # every call pays for its own S
+        tm = {}
+        barrier()
+        t0 = time.perf_counter()
+        fit = PPLS_simult(None, None, r, ctx=ctx, seed=CALL_SEED, timings=tm)
+        barrier()
+        dt = tmax(time.perf_counter() - t0)
+        ll = fit["loglik"]
+        out[mode] = dict(seconds=dt, init_seconds=tmax(tm["init"]), loop_seconds=tmax(tm["loop"]),
+                         init_steps=[int(v) for v in tm["init_steps"]], em_steps=int(len(ll)),
+                         read_S=bool(ctx.xprod_info(r)["ready"]), loglik_last=float(ll[-1]))
+        out[f"_{mode}_fit"] = fit
+    ctx.set_option("xprod", 0)
+    ref = out["stream"]["loglik_last"]
+    for mode in ("xprod", "auto"):
+        out[mode]["loglik_rel_diff_vs_stream"] = abs(out[mode]["loglik_last"] - ref) / abs(ref)
+    return out
+
+
+def cpu_call_baseline(ctx, r, cfg, device, rows):
+    """oracle/cpu_ref.c's restatement of the same PPLS_simult(X, Y, r) call (cpu_ref_ppls_simult:
+    the initialiser on explicitly deflated copies, the EM loop, Eout; the same 'random' draws) timed
+    on the host cores over the first `rows` rows, its seconds scaled by n / rows (every pass is
+    linear in n); and the GPU running the same call on the same rows, for parity."""
+    from oracle import cpu_ref
+    from ppls_amd import Context, PPLS_simult, initial_guess
+    X, Y = ctx.get_data_rows(0, rows)
+    rng = np.random.default_rng(CALL_SEED)
+    inits = [initial_guess(cfg["p"], cfg["q"], "random", rng) for _ in range(r)]
+    cores = cpu_ref.load().cpu_ref_max_threads()
+    t0 = time.perf_counter()
+    est, ll, cs, secs = cpu_ref.ppls_simult_call(X, Y, r, inits)
+    dt = time.perf_counter() - t0
+    with Context(device) as c2:   # the GPU on the same rows, same draws (streaming statistics)
+        c2.set_data(X, Y)
+        fit = PPLS_simult(None, None, r, ctx=c2, seed=CALL_SEED)
+    gl = fit["loglik"]
+    k = min(len(gl), len(ll))
+    scale = cfg["n"] / rows
+    return dict(value=dt * scale, unit="seconds per PPLS_simult call (scaled to n)", cores=int(cores), kind="port",
+                sample=f"PPLS_simult(X, Y, {r}) with the defaults (PPLS(X, Y, {r}, 20, 1e-4) from the same 'random' "
+                       f"draws, EMsteps 10, atol 1e-4, Eout) on the first {rows} of n = {cfg['n']} rows in {dt:.1f} s "
+                       f"(init {secs['init']:.1f} s, loop {secs['loop']:.1f} s, Eout {secs['eout']:.2f} s; "
+                       f"init steps {list(map(int, cs))}, EM steps {len(ll)}), x {scale:.0f}: oracle/cpu_ref.c, "
+                       f"OpenMP {cores} threads, {cpu_model()}",
+                sample_seconds=dt,
+                em_steps_cpu=int(len(ll)), em_steps_gpu=int(len(gl)),
+                loglik_rel_err_gpu_vs_cpu=float(np.abs(gl[:k] - ll[:k]).max() / np.abs(ll[:k]).max()) if k else None,
+                W_abs_err_gpu_vs_cpu=float(np.abs(fit["estimates"]["W"] - est["W"]).max()))
+
+
 _DEVICE = {}
-
-
-def ctx_device(ctx):
-    return _DEVICE.get(id(ctx), 0)
 
 
 def _rank_entry(rank, world, port, argv):
@@ -228,18 +315,20 @@ def _rank_entry(rank, world, port, argv):
     os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world), LOCAL_WORLD_SIZE=str(world),
                       MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     sys.argv = argv
-    main()
+    sys.exit(main())
 
 
-def spawn_ranks(n):
+def spawn_ranks(n, oversubscribe=False):
     """`bench.py --gpus N` without torchrun: N fresh rank processes (multiprocessing spawn), one per
     GPU, started before this process touches a GPU; returns the exit status (non-zero if any rank
-    failed or fewer than N GPUs are visible)."""
+    failed or fewer than N GPUs are visible).  oversubscribe: several ranks per GPU (rank % GPUs),
+    for rehearsing the multi-rank flow on fewer GPUs (only with --comm host: RCCL refuses two ranks
+    on one device)."""
     import multiprocessing as mp
     import socket
     import torch
     ndev = torch.cuda.device_count()   # does not initialise the GPU on this image
-    if ndev < n:
+    if ndev < 1 or (ndev < n and not oversubscribe):
         print(f"error: --gpus {n} but only {ndev} GPU(s) visible", file=sys.stderr)
         return 2
     with socket.socket() as sk:
@@ -251,11 +340,22 @@ def spawn_ranks(n):
         p.start()
     for p in procs:
         p.join()
-    bad = [r for r, p in enumerate(procs) if p.exitcode != 0]
+    bad = [(r, p.exitcode) for r, p in enumerate(procs) if p.exitcode != 0]
     if bad:
-        print(f"error: rank(s) {bad} failed", file=sys.stderr)
-        return 1
+        print(f"error: rank(s) failed (rank, exit status): {bad}", file=sys.stderr)
+        return max(3 if c == 3 else 1 for _, c in bad)
     return 0
+
+
+def _digest(arrays):
+    h = hashlib.sha256()
+    for a in arrays:
+        h.update(np.ascontiguousarray(a, dtype=np.float64).tobytes())
+    return h.hexdigest()[:16]
+
+
+def _theta_arrays(est, ll):
+    return [est.W, est.C, est.B, est.sigT, np.array([est.sigE, est.sigF, est.sigH]), ll]
 
 
 def main():
@@ -264,26 +364,34 @@ def main():
     ap.add_argument("--steps", type=int, default=200)   # C3: ~1 s timed, long enough for a GPU-busy sampler
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
-    ap.add_argument("--sweep", type=int, default=0, help="0 auto, 2 two-pass, 3 panel")
+    ap.add_argument("--sweep", type=int, default=0, help="0 auto, 3 panel")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-iters", type=int, default=3, help="timed CPU-baseline iterations (full n)")
+    ap.add_argument("--cpu-call-rows", type=int, default=0,
+                    help="rows of the host PPLS_simult-call sample (0: n / 20, at least 5000)")
     ap.add_argument("--timing-every", type=int, default=4,
                     help="bracket every N-th sweep of the timed region with HIP events")
     ap.add_argument("--xprod-steps", type=int, default=2000,
                     help="iterations of the cross-product form timed after the headline (0: skip it)")
+    ap.add_argument("--no-call", action="store_true", help="skip the whole-call PPLS_simult timings")
     ap.add_argument("--comm", default="rccl", choices=["rccl", "host"],
                     help="N>1 statistics all-reduce: RCCL (default) or the host reducer hook over gloo "
                          "(ppls_set_reducer; rehearses the multi-rank bench with several ranks on one GPU)")
+    ap.add_argument("--oversubscribe", action="store_true",
+                    help="with --comm host: allow more ranks than visible GPUs (rank r on GPU r % count)")
     args = ap.parse_args()
+    if args.oversubscribe and args.comm != "host":
+        print("error: --oversubscribe needs --comm host (RCCL refuses two ranks on one GPU)", file=sys.stderr)
+        return 2
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world == 1 and args.gpus > 1 and "WORLD_SIZE" not in os.environ:
-        sys.exit(spawn_ranks(args.gpus))   # no launcher: one child process per GPU (spawn, no exec)
+        return spawn_ranks(args.gpus, args.oversubscribe)   # no launcher: one child process per GPU (spawn, no exec)
     if world != args.gpus:
         print(f"error: {world} rank(s) (WORLD_SIZE) but --gpus {args.gpus}", file=sys.stderr)
-        sys.exit(2)
+        return 2
     dist = None
     if world > 1:
         import torch.distributed as dist  # gloo: barriers, max-over-ranks, RCCL id exchange
@@ -295,6 +403,9 @@ def main():
     cfg = CONFIGS[args.config]
     n, p, q, r = cfg["n"], cfg["p"], cfg["q"], cfg["r"]
     ndev = max(1, torch.cuda.device_count())   # does not initialise the GPU
+    if world > ndev and not args.oversubscribe:
+        print(f"error: {world} ranks on {ndev} GPU(s) (use --oversubscribe with --comm host)", file=sys.stderr)
+        return 2
     device = local % ndev
     ctx = Context(device)
     _DEVICE[id(ctx)] = device
@@ -323,6 +434,9 @@ def main():
         if dist is not None:
             dist.barrier()
 
+    def tmax(v):
+        return _reduce_max(dist, torch, v)
+
     ctx.em_begin(th0)
     ctx.em_iterate(args.warmup)
     barrier()
@@ -331,29 +445,51 @@ def main():
     t0 = time.perf_counter()
     ctx.em_iterate(args.steps)
     barrier()
-    dt = time.perf_counter() - t0
+    dt = tmax(time.perf_counter() - t0)
     ctx.set_option("timing", 0)
     kern_ms, launches = ctx.sweep_timing(reset=True)
-    if dist is not None:
-        tt = torch.tensor([dt], dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        dt = float(tt.item())
     est, ll = ctx.em_state()
     info = ctx.sweep_info(r)
     rccl_nranks, rccl_rank, ar_ms, ar_calls = ctx.comm_info(reset=True)
+    digest_parts = _theta_arrays(est, ll)
     xp = None
     if args.xprod_steps > 0:
-        xp = bench_xprod(ctx, th0, args, barrier, dist, torch, r, ll, dt / args.steps)
+        est_x, ll_x, xp = bench_xprod(ctx, th0, args, barrier, tmax, r, ll, dt / args.steps)
+        digest_parts += _theta_arrays(est_x, ll_x)
         ctx.set_option("xprod", 0)
-    # every rank's final theta and trace, hashed: a dp-N run proves its ranks stayed identical
-    h = hashlib.sha256()
-    for a in (est.W, est.C, est.B, est.sigT, np.array([est.sigE, est.sigF, est.sigH]), ll):
-        h.update(np.ascontiguousarray(a, dtype=np.float64).tobytes())
-    digest = h.hexdigest()[:16]
+    call = None
+    if not args.no_call:
+        call = bench_call(ctx, r, barrier, tmax)
+        for mode in ("stream", "xprod", "auto"):
+            f = call.pop(f"_{mode}_fit")
+            e = f["estimates"]
+            digest_parts += [e["W"], e["C"], e["B"], e["sigT"], np.array([e["sigE"], e["sigF"], e["sigH"]]), f["loglik"]]
+    # every rank's theta and traces (headline, cross-product, calls) hashed: a dp-N run proves its
+    # ranks stayed identical, and fails loudly when they did not (PPLS_BENCH_TEST_DIVERGE = a rank:
+    # that rank's digest is perturbed -- tests/test_gpu_bench.py checks the failure path)
+    if os.environ.get("PPLS_BENCH_TEST_DIVERGE") == str(rank):
+        digest_parts.append(np.ones(1))
+    digest = _digest(digest_parts)
     digests = [digest]
     if dist is not None:
         digests = [None] * world
         dist.all_gather_object(digests, digest)
+    backend = "none" if world == 1 else ("rccl" if args.comm == "rccl" else "host reducer over gloo")
+    problems = []
+    if len(set(digests)) != 1:
+        problems.append(f"ranks hold different estimates (theta digests {digests})")
+    if backend == "rccl" and rccl_nranks != world:
+        problems.append(f"RCCL reports {rccl_nranks} ranks for a world of {world}")
+    if not (len(ll) and np.isfinite(ll).all()):
+        problems.append("non-finite log-likelihood")
+    if problems:
+        if rank == 0:
+            print("error: " + "; ".join(problems), file=sys.stderr)
+        ctx.close()
+        if dist is not None:
+            dist.barrier()
+            dist.destroy_process_group()
+        return 3
 
     if rank == 0:
         its = args.steps / dt
@@ -362,26 +498,26 @@ def main():
         wl = f"{args.config}_{'dp%d' % world}"
         stat_doubles = (p + q) * r + 4 * r * r      # [X'mu_T | Y'mu_U | Gram], one all-reduce per iteration
         if world == 1:
-            backend = "none"
             parallelism = "dp1 (single rank, no all-reduce)"
         else:
-            backend = "rccl" if args.comm == "rccl" else "host reducer over gloo"
             parallelism = (f"dp{world} (rows sharded, 1 {'RCCL' if args.comm == 'rccl' else 'host (gloo)'} "
-                           f"all-reduce of {stat_doubles} doubles/iteration)")
+                           f"all-reduce of {stat_doubles} doubles/iteration"
+                           f"{'; ranks oversubscribed on ' + str(ndev) + ' GPU(s)' if world > ndev else ''})")
         # compute side: 2r fp64 FMAs per element (r for the dots, r for the rank-1 update), on
         # VALU (no fp64 MFMA shape fits r <= 8 better, and its rate equals the VALU rate)
         flops = 4.0 * (n_local * (p + q)) * r
         tflops = flops / (avg_kernel_ms * 1e-3) / 1e12 if launches else None
+        traffic, traffic_src = load_traffic(wl)
         roofline = dict(bound="hbm", achieved=achieved, peak=HBM_PEAK_GBS, unit="GB/s",
                         frac=(achieved / HBM_PEAK_GBS) if achieved else None,
-                        traffic=load_traffic(wl), kernel=ctx.sweep_kernel(r),
+                        traffic=traffic, traffic_source=traffic_src, kernel=ctx.sweep_kernel(r),
                         avg_kernel_ms=avg_kernel_ms, bytes_per_launch=info["bytes_per_sweep"],
                         grid=info["grid"], fp64_valu_tflops=tflops, fp64_valu_peak_tflops=FP64_PEAK_TF,
                         fp64_valu_frac=(tflops / FP64_PEAK_TF) if tflops else None,
                         measured_read_ceiling=READ_CEILING_GBS,
                         frac_of_measured_ceiling=(achieved / READ_CEILING_GBS) if achieved else None)
         # rocprofv3 PMC counters (SQ_VALU_MFMA_BUSY_CYCLES, SQ_ACTIVE_INST_VALU, GRBM_GUI_ACTIVE) of the
-        # sweep kernel(s) at this workload, committed under profiles/
+        # sweep kernel(s) at this workload, committed under profiles/ (readbacks, see their source)
         if info["variant"] == "panel":
             roofline["counters"] = {k: load_compute_counters(wl, k) for k in ("panel_mfmadots", "panel_acc")}
         else:
@@ -403,13 +539,21 @@ def main():
                              allreduce_doubles=stat_doubles,
                              allreduce_us=(1e3 * ar_ms / ar_calls) if ar_calls else None,
                              allreduce_timed_calls=ar_calls),
-                   theta_sha16=digest, ranks_bitwise_identical=len(set(digests)) == 1)
+                   theta_sha16=digest, ranks_bitwise_identical=True)
         out["xprod"] = xp
+        if call is not None:
+            out["call_seconds"] = {m: call[m]["seconds"] for m in ("stream", "xprod", "auto")}
+            out["call"] = dict(what=f"PPLS_simult(X, Y, {r}) with its defaults: PPLS(X, Y, {r}, 20, 1e-4, 'random') "
+                                    "initialiser, EMsteps 10, atol 1e-4, Expectations to the host; S formed inside "
+                                    "the xprod / auto calls", **call)
         if world == 1 and not args.no_cpu:
             cb, rel, werr = cpu_baseline(ctx, th0, cfg, args.cpu_iters)
             out["cpu_baseline"] = cb
             out["loglik_rel_err_vs_cpu"] = rel
             out["W_abs_err_vs_cpu"] = werr
+            if call is not None:
+                rows = args.cpu_call_rows or max(5000, n // 20)
+                out["call"]["cpu_ref"] = cpu_call_baseline(ctx, r, cfg, device, min(rows, n))
         else:
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)
@@ -417,7 +561,8 @@ def main():
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

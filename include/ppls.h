@@ -76,7 +76,7 @@ int ppls_ctx_create(int device, ppls_ctx** out);
 void ppls_ctx_destroy(ppls_ctx* ctx);
 const char* ppls_last_error(const ppls_ctx* ctx);
 /* keys: "sweep" (0 auto: the single-pass split sweep where W, C and the X'mu accumulators fit in
- *                registers, else the panel sweep; 2 generic two-pass; 3 panel (wide p, two passes)),
+ *                registers, else the panel sweep; 3 panel (wide p, two passes)),
  *       "rows_per_step" (split sweep: 0 auto, 1, 2), "pipe" (split sweep software pipelining, 0/1),
  *       "grid" (workgroups, 0 = auto),
  *       "polar1" (finalize polar factor: 1 (default) one Cholesky-QR pass when
@@ -89,19 +89,22 @@ const char* ppls_last_error(const ppls_ctx* ctx);
  *       "nt" (sweep loads with the non-temporal cache policy: -1 auto (default: when X, Y exceed
  *             the 256 MB MALL), 0 off, 1 on),
  *       "timing" (N > 0: record HIP events around every N-th sweep launch; 0 off),
- *       "balance" (split sweep row partition: 1 (default) calibrated per-XCD weights, measured once
- *                  per data shape with 8 timed launches, from 2048 rows per workgroup; 0 the even split),
+ *       "balance" (split sweep row partition: 0 (default) the even split -- bitwise reproducible
+ *                  across processes; 1 per-XCD weights calibrated once per context and data shape
+ *                  with 8 timed launches, from 2048 rows per workgroup: ~0.5 % faster at C3, but
+ *                  the row grouping of the sums, hence the last bits, then vary between contexts),
  *       "xprod" (statistics of ppls_em_run / ppls_em_iterate: 0 (default) one streaming sweep over X, Y
  *                per iteration; 1 from the cross-products S = [X Y]'[X Y], formed once per data set
  *                on MFMA and all-reduced once, after which an iteration reads S (8 (p+q)^2 bytes) and
- *                needs no collective; -1 auto: S when a cost model of max_steps iterations says so),
- *       "xprod_kernel" (cross-product kernel: 0 auto (= 2), 1 row groups reading W, C from L1/L2,
- *                       2 row tiles with W, C staged in LDS, 3 lower triangle (r <= 10): each
- *                       off-diagonal tile of the symmetric S read once for its rows and its columns
- *                       -- half the bytes, measured slower (latency-bound tiles + a partial reduction)),
- *       "xprod_rw" (rows of S per wave of kernels 1 and 2: 0 auto, 1, 2, 4),
+ *                needs no collective; -1 auto: S when a cost model of max_steps iterations says so;
+ *                S stays resident (8 (p+q)^2 bytes) until the data change, 0 is set again, or
+ *                ppls_xprod_release),
+ *       "xprod_rw" (rows of S per wave of the cross-product tile kernel: 0 auto, 1, 2, 4, 8),
  *       "xprod_fuse" (1, default: the finalize after a cross-product step forms the 2r x 2r Gram
- *                     itself when r <= 8 and p + q <= 6144; 0: a separate Gram kernel) */
+ *                     itself when r <= 8 and p + q <= 6144; 0: a separate Gram kernel),
+ *       "dots_rows" (panel sweep dots: rows per wave, 0 auto (64 from 32768 rows, else 32), 32, 64),
+ *       "dots_pair" (panel sweep dots: a wave pair per row tile, -1 auto (when row tiles are fewer
+ *                    than resident wave slots), 0, 1) */
 int ppls_set_option(ppls_ctx* ctx, const char* key, int64_t value);
 
 /* ---- multi-GPU: samples are sharded over ranks; one RCCL all-reduce per EM iteration ---- */
@@ -125,10 +128,6 @@ int ppls_set_data(ppls_ctx* ctx, const double* X, const double* Y, int64_t n_loc
  * counter-based Philox4x32-10 normals keyed by (seed, element index): independent of sharding. */
 int ppls_generate_synthetic(ppls_ctx* ctx, int64_t n_total, int64_t row0, int64_t n_local, int p,
                             int q, int r, const ppls_theta* truth, uint64_t seed);
-/* The generator's Philox4x32-10 block function on the device, for known-answer checks: out[4i..4i+3]
- * = philox4x32_10(ctr[4i..4i+3], key = {key & 0xffffffff, key >> 32}), i < count (host arrays).
- * The generator uses ctr = {pair lo, pair hi, stream, 0}, key = seed. */
-int ppls_philox4x32_10(ppls_ctx* ctx, const uint32_t* ctr, int64_t count, uint64_t key, uint32_t* out);
 int ppls_get_data(ppls_ctx* ctx, double* X, double* Y, int64_t row_begin, int64_t nrows);
 /* The same rows in row-major layout (X: nrows x p, Y: nrows x q, C order), streamed without a
  * device-side transpose: what a row-oriented host consumer (the CPU baseline) reads. */
@@ -243,50 +242,14 @@ int ppls_loglC_fast(ppls_ctx* ctx, const double* W, const double* C, const doubl
 int ppls_variances(ppls_ctx* ctx, const double* mu, const double* Cdiag, double sigE, int a, int xory,
                    double* W, double* B_exp, double* varMatrix, double* SSt_exp, double* SSt_star,
                    double* seLoad);
-/* The Gram D'D alone (D = X for xory 0, Y for 1; nsplit 0 = auto), for tests and benchmarks:
- * G (p x p, column-major, nullable), *ms = the MFMA kernel's duration. */
-int ppls_gram(ppls_ctx* ctx, int xory, int nsplit, double* G, double* ms);
 
-/* ---- measurement ---------------------------------------------------------------------------- */
-/* Sum of HIP-event durations of the sweep kernel launches recorded since the last reset. */
-int ppls_sweep_timing(ppls_ctx* ctx, double* total_ms, int64_t* launches, int reset);
-/* The split sweep's calibrated row partition (option "balance"): the per-XCD-class weights w8[8]
- * (1.0 before calibration) and up to cap of the grid + 1 row boundaries (*n_bounds = grid + 1, or 0
- * while the even split is used). */
-int ppls_sweep_balance(ppls_ctx* ctx, double* w8, int64_t* bounds, int cap, int* n_bounds);
-/* The communicator as RCCL reports it (ncclCommCount / ncclCommUserRank; without RCCL the
- * context's own nranks/rank, i.e. 1/0 or the host reducer's) and the summed HIP-event durations of
- * the per-iteration statistics all-reduce on the timed sweeps (option "timing"; RCCL only). */
-int ppls_comm_info(ppls_ctx* ctx, int* nranks, int* rank, double* allreduce_ms, int64_t* allreduce_calls,
-                   int reset);
-/* Cross-product form (option "xprod"): form S now (*ms = the MFMA Gram kernel time, *total_ms = with
- * the all-reduce and allocation; both nullable) -- otherwise the first run that reads S forms it.
- * Collective when the rows are sharded: every rank calls it (one all-reduce of (p+q)^2 doubles). */
+/* ---- cross-product form (option "xprod") ----------------------------------------------------
+ * Form S = [X Y]'[X Y] now (*ms = the MFMA Gram kernel time, *total_ms = with the all-reduce and
+ * allocation; both nullable) -- otherwise the first run that reads S forms it.  Collective when the
+ * rows are sharded: every rank calls it (one all-reduce of (p+q)^2 doubles). */
 int ppls_xprod_prepare(ppls_ctx* ctx, double* ms, double* total_ms);
-/* Its state: *ready = S is formed for the current data, *bytes_per_pass = the bytes of S one
- * iteration reads (8 P^2, P = padded p + q, or its lower 128 x 128 tiles for the triangle kernel),
- * *flops = 2 n_local P^2 of the Gram as computed (lower tiles: ~ half the full product),
- * *rows_per_wave = 100 x the kernel kind (1 row groups, 2 row tiles, 3 lower triangle) + rows per wave. */
-int ppls_xprod_info(ppls_ctx* ctx, int r, int* ready, int64_t* bytes_per_pass, double* flops, int* rows_per_wave);
-/* One statistics step from S for theta (the kernel option "xprod_kernel" selects): stats =
- * [X'mu_T p x r | Y'mu_U q x r | Gram 2r x 2r], all column-major, as ppls_finalize_host takes them
- * (unit parity of the cross-product kernels against the sweep and a host S B). */
-int ppls_xprod_stats(ppls_ctx* ctx, const ppls_theta* th, int r, double* stats);
-/* Shape facts for the roofline: bytes of X and Y one sweep reads (algorithmic), kernel variant. */
-int ppls_sweep_info(ppls_ctx* ctx, int r, int64_t* bytes_per_sweep, int* variant, int* grid);
-/* The sweep kernel instantiation the next EM iteration with r components launches, as text
- * (e.g. "split<5,4,512,2,false,4,4> nt"): tests assert the production kernel is the one checked. */
-int ppls_sweep_kernel(ppls_ctx* ctx, int r, char* buf, int len);
-
-/* Diagnostics: wall-clock stamps of the last finalize's phases (PPLS_FTRACE_LEN = 3 blocks x 16
- * slots; 0 = slot not reached) and the tick length in ns.  Requires set_option("ftrace", 1). */
-#define PPLS_FTRACE_LEN 48
-int ppls_finalize_trace(ppls_ctx* ctx, int64_t* stamps, double* tick_ns);
-/* Diagnostics: wall-clock stamps of the last split sweep per workgroup (entry, ring prologue done,
- * row loop done, partials written; 4 per workgroup, row-major), up to PPLS_STRACE_MAX_WG workgroups;
- * *n = workgroups copied.  Requires set_option("strace", 1). */
-#define PPLS_STRACE_MAX_WG 4096
-int ppls_sweep_trace(ppls_ctx* ctx, int64_t* stamps, int cap, int* n, double* tick_ns);
+/* Free S (and its scratch) now; the next run that reads S forms it again. */
+int ppls_xprod_release(ppls_ctx* ctx);
 
 /* ---- host-side algebra (no GPU; the same code the device finalize runs) ------------------------ */
 /* From the all-reduced sufficient statistics of one sweep with theta (stats = [X'mu_T p x r |

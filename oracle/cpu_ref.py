@@ -38,6 +38,11 @@ def load():
     lib.cpu_ref_em_step.argtypes = [_dp, _dp, ct.c_int64, ct.c_int, ct.c_int, ct.c_int, _dp, _dp, _dp, _dp,
                                     _dp, _dp, ct.c_int]
     lib.cpu_ref_max_threads.restype = ct.c_int
+    _ip = ct.POINTER(ct.c_int)
+    lib.cpu_ref_ppls_simult.restype = ct.c_int
+    lib.cpu_ref_ppls_simult.argtypes = [_dp, _dp, ct.c_int64, ct.c_int, ct.c_int, ct.c_int, _dp, _dp, _dp, ct.c_int,
+                                        ct.c_double, ct.c_int, ct.c_double, _dp, _dp, _dp, _dp, _dp, _dp, _ip, _ip,
+                                        _dp, ct.c_int]
     return lib
 
 
@@ -63,3 +68,34 @@ def em_steps(X, Y, theta, steps, nthreads=0):
             raise RuntimeError("cpu_ref_em_step failed")
         ll[s] = out.value
     return dict(W=W, C=C, B=np.diag(b), sigT=np.diag(t), sigE=sig[0], sigF=sig[1], sigH=sig[2]), ll
+
+
+def ppls_simult_call(X, Y, a, inits, EMsteps=10, atol=1e-4, init_steps=20, init_atol=1e-4, nthreads=0):
+    """The whole PPLS_simult(X, Y, a, EMsteps, atol) call (EM_W_multi.R:758-807) on row-major X, Y:
+    the initialiser PPLS(X, Y, a, init_steps, init_atol) from the starting values ``inits`` (one
+    dict per component: W, C, B, sigE, sigF, sigH, sigT -- PPLSi's 'random' draws), the EM loop and
+    Eout.  Returns (estimates dict, loglik, component steps, {init, loop, eout} seconds)."""
+    lib = load()
+    X = np.ascontiguousarray(X, dtype=np.float64)
+    Y = np.ascontiguousarray(Y, dtype=np.float64)
+    n, p = X.shape
+    q = Y.shape[1]
+    iw = np.asfortranarray(np.column_stack([np.ravel(t["W"]) for t in inits]), dtype=np.float64)
+    ic = np.asfortranarray(np.column_stack([np.ravel(t["C"]) for t in inits]), dtype=np.float64)
+    th = np.ascontiguousarray([[float(np.ravel(t[k])[0]) for k in ("B", "sigE", "sigF", "sigH", "sigT")]
+                               for t in inits], dtype=np.float64)
+    W = np.zeros((p, a), order="F")
+    C = np.zeros((q, a), order="F")
+    b, t, sig = np.zeros(a), np.zeros(a), np.zeros(3)
+    ll = np.zeros(EMsteps)
+    steps = ct.c_int()
+    cs = np.zeros(a, dtype=np.int32)
+    secs = np.zeros(3)
+    P = lambda v: v.ctypes.data_as(_dp)  # noqa: E731
+    rc = lib.cpu_ref_ppls_simult(P(X), P(Y), n, p, q, a, P(th), P(iw), P(ic), int(init_steps), float(init_atol),
+                                 int(EMsteps), float(atol), P(W), P(C), P(b), P(t), P(sig), P(ll), ct.byref(steps),
+                                 cs.ctypes.data_as(ct.POINTER(ct.c_int)), P(secs), int(nthreads))
+    if rc != 0:
+        raise RuntimeError(f"cpu_ref_ppls_simult failed ({rc})")
+    est = dict(W=W, C=C, B=np.diag(b), sigT=np.diag(t), sigE=sig[0], sigF=sig[1], sigH=sig[2])
+    return est, ll[: steps.value].copy(), cs.copy(), dict(init=secs[0], loop=secs[1], eout=secs[2])

@@ -21,6 +21,7 @@ from __future__ import annotations
 
 import ctypes as ct
 import math
+import time
 import warnings
 
 import numpy as np
@@ -373,6 +374,17 @@ class Context:
         self._chk(self._L.ppls_xprod_prepare(self.h, ct.byref(ms), ct.byref(tot)))
         return ms.value, tot.value
 
+    def xprod_release(self):
+        """Free the cross-products S now (ppls_xprod_release; 8 (p+q)^2 bytes of HBM); the next run
+        that reads S forms it again."""
+        self._chk(self._L.ppls_xprod_release(self.h))
+
+    def xprod_setup_times(self):
+        """(Gram kernel ms, all-reduce of S ms, whole setup ms) of the last formation of S."""
+        g, a, t = ct.c_double(), ct.c_double(), ct.c_double()
+        self._chk(self._L.ppls_xprod_setup_times(self.h, ct.byref(g), ct.byref(a), ct.byref(t)))
+        return g.value, a.value, t.value
+
     def xprod_stats(self, th: Theta):
         """One statistics step from S for theta: (X'mu_T p x r, Y'mu_U q x r, Gram 2r x 2r)."""
         r = th.r
@@ -478,7 +490,7 @@ class Context:
     def sweep_info(self, r):
         b, v, g = ct.c_int64(), ct.c_int(), ct.c_int()
         self._chk(self._L.ppls_sweep_info(self.h, int(r), ct.byref(b), ct.byref(v), ct.byref(g)))
-        return dict(bytes_per_sweep=b.value, variant={2: "twopass", 4: "split512", 5: "panel"}[v.value], grid=g.value)
+        return dict(bytes_per_sweep=b.value, variant={4: "split512", 5: "panel"}[v.value], grid=g.value)
 
     def sweep_kernel(self, r):
         """The sweep kernel instantiation an EM iteration with r components launches (text)."""
@@ -494,7 +506,10 @@ _DEFAULT_CTX = None
 def default_context() -> Context:
     """The context the R-named functions use when no ``ctx`` is given: GPU 0, with the statistics
     path chosen per run by the cost model (option "xprod" = -1, as the R shim in INTEGRATION.md
-    sets it: the cross-product form once a run is long enough to repay forming S)."""
+    sets it: the cross-product form once a run is long enough to repay forming S).  A formed S
+    stays resident for the data (8 (p+q)^2 bytes of HBM: 128 MB at p = q = 2000, 0.9 GB at
+    p + q = 10,500) until new data are loaded, ``xprod`` is set to 0, or
+    ``default_context().xprod_release()`` frees it."""
     global _DEFAULT_CTX
     if _DEFAULT_CTX is None:
         _DEFAULT_CTX = Context(0)
@@ -906,12 +921,16 @@ def PPLS_simult(X, Y, a, EMsteps=10, atol=1e-4, type=("SVD", "QR"), init=None, c
     computed on the device; its draws come from ``rng`` (an R-compatible stream, see
     ``initial_guess``) or numpy (``seed`` keyword).  Returns dict(Expectations, loglik, estimates) like
     the R list of class "PPLS_simult"; warns "Negative increments of likelihood" where the
-    reference does (:801).
+    reference does (:801).  ``timings`` (keyword, a dict): filled with the wall seconds of the
+    initialiser (``init``) and of the loop + Expectations (``loop``) and the initialiser's steps.
     """
     if kw.get("debug"):
         raise NotImplementedError("debug=TRUE is an oracle-only cross-check")
+    timings = kw.get("timings")   # optional dict: init / loop seconds and the initialiser's steps
+    t0 = time.perf_counter()
     ctx = _ctx_with(X, Y, ctx)
     t = _orth_type(type)
+    init_steps = []
     if init is None:
         rng = kw.get("rng")
         rng = rng if rng is not None else np.random.default_rng(kw.get("seed"))
@@ -931,6 +950,8 @@ def PPLS_simult(X, Y, a, EMsteps=10, atol=1e-4, type=("SVD", "QR"), init=None, c
             raise PplsError(-1, f"subscript out of bounds: PPLS returned {len(f0['B'])} of {a} components")
         init = dict(W=f0["W"], C=f0["C"], B=np.diag(f0["B"]), sigE=f0["sig"][a - 1, 0],
                     sigF=f0["sig"][a - 1, 1], sigH=f0["sig"][a - 1, 2], sigT=np.diag(f0["sig"][:, 3]))
+        init_steps = list(f0["Other_output"]["Number_steps"])
+    t1 = time.perf_counter()
     th = Theta(init["W"], init["C"], init["B"], init["sigE"], init["sigF"], init["sigH"], init["sigT"])
     if th.r != a:
         raise ValueError(f"init has {th.r} components, a = {a}")
@@ -942,4 +963,6 @@ def PPLS_simult(X, Y, a, EMsteps=10, atol=1e-4, type=("SVD", "QR"), init=None, c
                      sigT=d["sigT"])
     out = dict(Expectations=eout.as_dict(), loglik=ll, estimates=estimates)
     out["class"] = "PPLS_simult"
+    if timings is not None:
+        timings.update(init=t1 - t0, loop=time.perf_counter() - t1, init_steps=init_steps)
     return out

@@ -23,7 +23,7 @@ SOURCES = ["ppls_kernels.hip", "ppls_variances.hip", "ppls_xprod.hip", "ppls_cap
 FILE_FLAGS = {"ppls_kernels.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"]}
 CFLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function", "-Wno-inline-asm",
           "-I" + os.path.join(ROOT, "include"), "-I" + CSRC]
-# experiment builds only (e.g. tools/dots_ablate.sh: -DPPLS_DOTS_ABLATE=n into a copied tree)
+# experiment builds only (e.g. tools/variant_ab.sh: -DPPLS_REG_RMAX=6 into a copied tree)
 CFLAGS += [f for f in os.environ.get("PPLS_EXTRA_CFLAGS", "").split() if f]
 
 

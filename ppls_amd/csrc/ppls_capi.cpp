@@ -21,6 +21,7 @@
 #include <vector>
 
 #include "../../include/ppls.h"
+#include "../../include/ppls_debug.h"
 #include "ppls_kernels.h"
 #include "ppls_math.h"
 #include "ppls_xprod.h"
@@ -31,11 +32,12 @@ struct ppls_ctx {
   std::string err;
   int num_cus = 256;
   // options
-  int sweep_mode = 0;      // 0 auto, 2 generic two-pass, 3 panel
+  int sweep_mode = 0;      // 0 auto, 3 panel
   int grid_opt = 0;
   int rp_opt = 0;   // rows per pipeline step: 0 auto (2 where the kernel fits in registers)
   int pipe_opt = 1;     // split kernel: software-pipelined order
-  int ablate = 0;
+  int dots_rows = 0;   // panel dots rows per wave: 0 auto, 32, 64 (tests of both forms)
+  int dots_pair = -1;  // panel dots wave pair per row tile: -1 auto, 0, 1
   int team_rows = 0;   // finalize polar team: rows of S per member (0: PPLS_TEAM_ROWS)
   int polar1 = 1;   // finalize polar: Cholesky-QR1 fast path when kappa(X'mu) <= PPLS_POLAR1_KAPPA
   int polar1_kappa = 0;   // its bound on ||R1||_F ||R1^-1||_F (0 = min(8 r, 40))
@@ -91,7 +93,8 @@ struct ppls_ctx {
   // tail.  The first full split sweep of the data is timed per workgroup (untimed calibration
   // launches), workgroup g then owns a row block proportional to the measured rate of its class
   // g % 8 (the XCD under round-robin dispatch); fixed afterwards, so results stay deterministic.
-  int balance = 1;                 // option "balance": 1 calibrate (default), 0 the even split
+  int balance = 0;                 // option "balance": 1 calibrate, 0 the even split (default: bitwise
+                                   // reproducible across processes; the calibrated split regroups the sums)
   bool bal_done = false;           // calibrated for (bal_n, bal_grid)
   int64_t bal_n = -1;
   int bal_grid = -1;
@@ -113,22 +116,16 @@ struct ppls_ctx {
   // cross-product form of the iteration (ppls_xprod.hip): S = [X Y]'[X Y] (P x P, P = ldx + ldy)
   // formed once per data set, then every statistics step reads S instead of X and Y
   int xprod = 0;            // option "xprod": 0 stream X, Y (default), 1 cross-products, -1 auto (cost model)
-  int xprod_kernel = 0;     // option "xprod_kernel": 0 auto (= 2), 1 row groups, 2 row tiles with B in LDS,
-                            // 3 lower triangle (r <= PPLS_XP_TRI_RMAX; measured slower, §12)
-  int xprod_rw = 0;         // option "xprod_rw": rows of S per wave of the apply kernel (0 auto)
+  int xprod_rw = 0;         // option "xprod_rw": rows of S per wave of the tile kernel (0 auto)
   bool xp_ready = false;    // S holds the (all-reduced) cross-products of the current data
   bool xp_active = false;   // statistics steps of the current run read S
   bool xp_pending_gram = false;   // the last statistics step left the Gram B'M to the next finalize
   int xprod_fuse = 1;       // option "xprod_fuse": the finalize forms the Gram (r <= 8, P <= 6144)
   double* xp_S = nullptr;
   double* xp_M = nullptr;   // M = S blockdiag(W, C), P x 2r scratch
-  int* xp_tri_items = nullptr;    // lower-triangle form: run list (4 ints per run) and run offsets per block row
-  int* xp_tri_rows = nullptr;
-  int xp_tri_nruns = 0, xp_tri_r = 0;
-  double* xp_rowpart = nullptr;   // its run and tile partials
-  double* xp_colpart = nullptr;
   double xp_setup_ms = 0.0; // last formation of S: Gram kernel (HIP events), and with the all-reduce
   double xp_setup_total_ms = 0.0;
+  double xp_setup_ar_ms = 0.0;   // the all-reduce of S (wall clock around it and its stream sync)
   int xp_nsplit = 0;
   rocblas_handle blas = nullptr;   // rocSOLVER (variances.PPLS_simult's p x p inverse), created lazily
   // timing
@@ -379,7 +376,7 @@ int ensure_part(ppls_ctx* c, int groups) {
 }
 
 // Which sweep kernel runs for this shape: 3 = split ownership (default), 4 = panel (wide p, large r
-// or fp32 storage), 2 = generic two-pass (option sweep = 2); a->grid is the workgroup count.
+// or fp32 storage, or option sweep = 3); a->grid is the workgroup count.
 int64_t sweep_rows(const ppls_ctx* c) { return c->seg_rows >= 0 ? c->seg_rows : c->n_local; }
 
 int sweep_plan(ppls_ctx* c, int r, PplsSweepArgs* a) {
@@ -393,10 +390,8 @@ int sweep_plan(ppls_ctx* c, int r, PplsSweepArgs* a) {
   a->r = r;
   a->threads = 512;
   a->num_cus = c->num_cus;
-  if (c->sweep_mode == 2) {
-    a->grid = grid_of(c);
-    return 2;
-  }
+  a->dots_rows = c->dots_rows;
+  a->dots_pair = c->dots_pair;
   if (c->sweep_mode != 3 && !c->dtype && nsplit > 0) {
     a->ns = nsplit;
     a->pipe = c->pipe_opt;
@@ -517,26 +512,26 @@ int timing_pair(ppls_ctx* c, hipEvent_t* e0, hipEvent_t* e1) {
   return PPLS_OK;
 }
 
-// One sweep with theta[slot] -> c->stats (all-reduced).
-int sweep(ppls_ctx* c, int r, int slot, bool write_mu) {
+// One sweep with theta[slot] -> c->stats (all-reduced).  mu_only: just this rank's mu rows (the
+// statistics are not reduced: no collective).
+int sweep(ppls_ctx* c, int r, int slot, bool write_mu, bool mu_only = false) {
   int rc;
   PplsSweepArgs a;
   const int plan = sweep_plan(c, r, &a);
   const int64_t nrows = sweep_rows(c);
   if (c->seg_rows >= 0 && write_mu) return fail(c, PPLS_E_STATE, "mu write-out is not available for row segments");
-  const int groups = plan == 2 ? ppls_twopass_groups(std::max<int64_t>(nrows, 1), a.grid) : a.grid;
+  const int groups = a.grid;
   if ((rc = ensure_part(c, groups))) return rc;
   if (write_mu && !c->mu)
     if ((rc = dalloc(c, &c->mu, (size_t)std::max<int64_t>(c->n_local, 1) * 2 * r))) return rc;
-  if ((plan == 2 || plan == 4) && c->z_cols < (plan == 4 ? 4 : 2) * r) {
+  if (plan == 4 && c->z_cols < 4 * r) {
     dfree(c->Z);
     c->z_cols = 0;
-    const size_t len = plan == 4 ? (size_t)ppls_panel_z_len(c->n_local, c->ldx, c->ldy, r)
-                                 : (size_t)std::max<int64_t>(c->n_local, 1) * 2 * r;
-    if ((rc = dalloc(c, &c->Z, len))) return rc;
-    c->z_cols = (plan == 4 ? 4 : 2) * r;
+    if ((rc = dalloc(c, &c->Z, (size_t)ppls_panel_z_len(c->n_local, c->ldx, c->ldy, r)))) return rc;
+    c->z_cols = 4 * r;
   }
   if (nrows == 0) {
+    if (mu_only) return PPLS_OK;
     HIPCHK(c, hipMemsetAsync(c->stats, 0, sizeof(double) * c->part_ld, c->stream));
   } else {
     const size_t esz = c->dtype ? sizeof(float) : sizeof(double);
@@ -554,18 +549,22 @@ int sweep(ppls_ctx* c, int r, int slot, bool write_mu) {
     // (6.53 vs 6.34 TB/s at C3); smaller X, Y stay MALL-resident across iterations by default
     const bool nt = c->nt_loads > 0 ||
                     (c->nt_loads < 0 && 8.0 * nrows * (double)(c->ldx + c->ldy) > 256.0 * (1 << 20));
-    a.ablate = c->ablate | (nt ? 16 : 0);
+    a.nt = nt ? 1 : 0;
     a.stop = c->sweep_stop;
     a.trace = (plan == 3 && a.grid <= PPLS_STRACE_MAX_WG) ? c->strace : nullptr;
     // the row partition (its one-time calibration launches stay outside the timed events)
     if (plan == 3 && c->balance && c->seg_rows < 0 && (rc = balance_rows(c, &a))) return rc;
+    if (mu_only) {   // the rows' mu only (untimed): the panel sweep's dots pass, or the split sweep
+      if (plan == 4) HIPCHK(c, ppls_launch_panel_dots(&a, c->dtype, c->Z, c->stream));
+      else HIPCHK(c, ppls_launch_sweep_split(&a, c->stream));
+      return PPLS_OK;
+    }
     hipEvent_t e0, e1;
     if ((rc = timing_pair(c, &e0, &e1))) return rc;
     const bool timed = e0 != nullptr;
     if (timed) HIPCHK(c, hipEventRecord(e0, c->stream));
     if (plan == 3) HIPCHK(c, ppls_launch_sweep_split(&a, c->stream));
-    else if (plan == 4) HIPCHK(c, ppls_launch_sweep_panel(&a, c->dtype, c->Z, a.grid, c->stream));
-    else HIPCHK(c, ppls_launch_sweep_twopass(&a, c->Z, c->stream));
+    else HIPCHK(c, ppls_launch_sweep_panel(&a, c->dtype, c->Z, a.grid, c->stream));
     if (timed) HIPCHK(c, hipEventRecord(e1, c->stream));
     HIPCHK(c, ppls_launch_reduce2(c->part, groups, c->part_ld, c->part_ld, c->stats,
                                   c->part + (size_t)c->part_groups * c->part_ld, c->sweep_stop, c->stream));
@@ -586,8 +585,7 @@ int sweep(ppls_ctx* c, int r, int slot, bool write_mu) {
   return allreduce(c, c->stats, (size_t)c->part_ld);
 }
 
-int finalize(ppls_ctx* c, int r, int cur, int nxt, int logl_index, int type, int stop_step = 0,
-             bool scalars_only = false) {
+int finalize(ppls_ctx* c, int r, int cur, int nxt, int logl_index, int type, int stop_step = 0) {
   PplsFinalizeArgs f;
   f.stats = c->stats;
   f.ssq = c->ssq;
@@ -609,8 +607,7 @@ int finalize(ppls_ctx* c, int r, int cur, int nxt, int logl_index, int type, int
   f.work = c->work;
   f.status = c->status;
   f.qr = type == PPLS_ORTH_QR ? 1 : 0;
-  f.mode = (3 & ~(c->ablate >> 2)) | (c->polar1 ? 4 : 0) | (c->exact_gram ? 16 : 0) | (polar1_bound(c, r) << 8);   // ablate bit2: skip polar, bit3: skip scalars
-  if (scalars_only) f.mode &= ~1;
+  f.mode = 3 | (c->polar1 ? 4 : 0) | (c->exact_gram ? 16 : 0) | (polar1_bound(c, r) << 8);
   f.trace = c->ftrace;
   f.gram_cur = c->gram[cur];
   f.gram_nxt = c->gram[nxt];
@@ -632,10 +629,6 @@ int finalize(ppls_ctx* c, int r, int cur, int nxt, int logl_index, int type, int
   f.xpM = c->xp_pending_gram ? c->xp_M : nullptr;   // the Gram of a cross-product step, formed here
   c->xp_pending_gram = false;
   HIPCHK(c, ppls_launch_finalize(&f, c->stream));
-  // timing experiment (ablate bit 13): the same finalize again right away, with warm instruction
-  // and data caches (results stay valid: it recomputes the same outputs, only the Jacobi warm
-  // start and the loglik slot are rewritten)
-  if (c->ablate & 8192) HIPCHK(c, ppls_launch_finalize(&f, c->stream));
   return PPLS_OK;
 }
 
@@ -693,8 +686,10 @@ int xprod_setup(ppls_ctx* c) {
   } else {
     HIPCHK(c, hipMemsetAsync(c->xp_S, 0, sizeof(double) * PP, c->stream));
   }
+  const auto ta = std::chrono::steady_clock::now();
   if ((rc = allreduce(c, c->xp_S, PP))) return rc;
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->xp_setup_ar_ms = c->nranks > 1 || c->reducer ? std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ta).count() : 0.0;
   c->xp_setup_total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   c->xp_ready = true;
   return PPLS_OK;
@@ -702,14 +697,15 @@ int xprod_setup(ppls_ctx* c) {
 
 // Whether a run of max_steps iterations reads S: option xprod = 1 always, 0 never, -1 when the
 // modelled cost of forming S plus max_steps + 1 passes over it undercuts max_steps + 1 streaming
-// sweeps.  The model uses only global sizes (n_total / nranks, never this rank's own row count or
-// free memory), so every rank of a sharded run takes the same path.
+// sweeps.  The model and the size gate use only global sizes (n_total / nranks, P; never this
+// rank's own row count or device memory), so every rank of a sharded run takes the same path and
+// issues the same collectives.  Size gate: S and at most one S-sized set of Gram partials, 16 P^2
+// bytes, within PPLS_XPROD_MAX_BYTES (64 GiB, below a quarter of an MI355X's 288 GB: P <= 65,536).
+#define PPLS_XPROD_MAX_BYTES (64.0 * 1024 * 1024 * 1024)
 bool xprod_choose(ppls_ctx* c, int max_steps) {
   if (c->xprod == 0) return false;
   const double P = (double)(c->ldx + c->ldy);
-  hipDeviceProp_t prop;
-  const double mem = hipGetDeviceProperties(&prop, c->device) == hipSuccess ? (double)prop.totalGlobalMem : 0.0;
-  if (8.0 * P * P * 2.0 > 0.25 * mem) return false;   // S and one split of partials within a quarter of HBM
+  if (16.0 * P * P > PPLS_XPROD_MAX_BYTES) return false;
   if (c->xprod == 1) return true;
   const double n = (double)((c->n_total + c->nranks - 1) / c->nranks);
   const double esz = c->dtype ? 4.0 : 8.0;
@@ -717,15 +713,6 @@ bool xprod_choose(ppls_ctx* c, int max_steps) {
   const double t_pass = 8.0 * P * P / 6.5e12 + 5e-6;
   const double t_setup = c->xp_ready ? 0.0 : n * P * P / 55e12 + (c->nranks > 1 ? 16.0 * P * P / 100e9 : 0.0);
   return ((double)max_steps + 1.0) * (t_sweep - t_pass) > t_setup;
-}
-
-// The cross-product kernel for r components: 1 row groups, 2 row tiles (the default), 3 lower
-// triangle -- half the bytes of S, but at C3 its tiles are latency-bound (24.0 us against the row
-// tiles' 23.2 us for all of S) and its partial reduction adds 13-16 us.
-int xprod_kind(const ppls_ctx* c, int r) {
-  if (c->xprod_kernel == 3 && r <= PPLS_XP_TRI_RMAX) return 3;
-  if (c->xprod_kernel == 1) return 1;
-  return 2;
 }
 
 // One statistics step from S: c->stats for theta[slot] (no collective: S is global).  fuse: a
@@ -738,37 +725,14 @@ int xprod_stats(ppls_ctx* c, int r, int slot, bool fuse = false) {
   if (!c->xp_M) {
     if ((rc = dalloc(c, &c->xp_M, (size_t)P * 2 * PPLS_RMAX))) return rc;
   }
-  const int kind = xprod_kind(c, r);
-  if (kind == 3 && c->xp_tri_r != r) {   // the triangle's run list and partials for this r
-    int64_t rl = 0, cl = 0;
-    const int nr = ppls_xprod_tri_plan(c->ldx, c->ldy, r, c->num_cus, nullptr, nullptr, &rl, &cl);
-    if (nr < 1) return fail(c, PPLS_E_ARG, "lower-triangle plan failed (r=%d)", r);
-    const int nb = (c->ldx + 127) / 128 + (c->ldy + 127) / 128;
-    std::vector<int> items((size_t)4 * nr), rows((size_t)nb + 1);
-    ppls_xprod_tri_plan(c->ldx, c->ldy, r, c->num_cus, items.data(), rows.data(), nullptr, nullptr);
-    if ((rc = dalloc(c, &c->xp_tri_items, items.size())) || (rc = dalloc(c, &c->xp_tri_rows, rows.size())) ||
-        (rc = dalloc(c, &c->xp_rowpart, (size_t)rl)) || (rc = dalloc(c, &c->xp_colpart, (size_t)cl)))
-      return rc;
-    HIPCHK(c, hipMemcpy(c->xp_tri_items, items.data(), sizeof(int) * items.size(), hipMemcpyHostToDevice));
-    HIPCHK(c, hipMemcpy(c->xp_tri_rows, rows.data(), sizeof(int) * rows.size(), hipMemcpyHostToDevice));
-    c->xp_tri_nruns = nr;
-    c->xp_tri_r = r;
-  }
   hipEvent_t e0, e1;
   if ((rc = timing_pair(c, &e0, &e1))) return rc;
   if (e0) HIPCHK(c, hipEventRecord(e0, c->stream));
-  if (kind == 3) {
-    HIPCHK(c, ppls_launch_xprod_tri(c->xp_S, c->ldx, c->ldy, r, c->W[slot], c->C[slot], c->sc[slot], c->stats, c->xp_M,
-                                    c->xp_tri_items, c->xp_tri_nruns, c->xp_tri_rows, c->xp_rowpart, c->xp_colpart,
-                                    c->sweep_stop, c->stream));
-  } else {
-    const int rw = kind == 1 ? ppls_xprod_rows_per_wave(P, r, c->xprod_rw)
-                             : ppls_xprod_tile_rows(P, r, c->xprod_rw, c->num_cus);
-    const bool defer = fuse && c->xprod_fuse && r <= 8 && P <= 6144;
-    HIPCHK(c, ppls_launch_xprod_apply(c->xp_S, c->ldx, c->ldy, r, kind == 1 ? 1 : 0, rw, c->W[slot], c->C[slot],
-                                      c->sc[slot], c->stats, c->xp_M, c->sweep_stop, defer ? 0 : 1, c->stream));
-    c->xp_pending_gram = defer;
-  }
+  const int rw = ppls_xprod_tile_rows(P, r, c->xprod_rw, c->num_cus);
+  const bool defer = fuse && c->xprod_fuse && r <= 8 && P <= 6144;
+  HIPCHK(c, ppls_launch_xprod_tile(c->xp_S, c->ldx, c->ldy, r, rw, c->W[slot], c->C[slot], c->sc[slot], c->stats,
+                                   c->xp_M, c->sweep_stop, defer ? 0 : 1, c->stream));
+  c->xp_pending_gram = defer;
   if (e1) HIPCHK(c, hipEventRecord(e1, c->stream));
   return PPLS_OK;
 }
@@ -809,16 +773,16 @@ int check_status(ppls_ctx* c) {
   return PPLS_OK;
 }
 
-int compute_ssq(ppls_ctx* c) {
-  int rc;
-  c->xp_ready = false;   // data or communicator changed: the cross-products are stale
+void xprod_free(ppls_ctx* c) {
+  c->xp_ready = false;
+  c->xp_active = false;
   dfree(c->xp_S);
   dfree(c->xp_M);
-  dfree(c->xp_tri_items);
-  dfree(c->xp_tri_rows);
-  dfree(c->xp_rowpart);
-  dfree(c->xp_colpart);
-  c->xp_tri_nruns = c->xp_tri_r = 0;
+}
+
+int compute_ssq(ppls_ctx* c) {
+  int rc;
+  xprod_free(c);   // data or communicator changed: the cross-products are stale
 
   const int nb = 1024;
   if ((rc = dalloc(c, &c->scratch, nb + 8))) return rc;
@@ -988,10 +952,6 @@ void ppls_ctx_destroy(ppls_ctx* c) {
   dfree(c->stop_d);
   dfree(c->xp_S);
   dfree(c->xp_M);
-  dfree(c->xp_tri_items);
-  dfree(c->xp_tri_rows);
-  dfree(c->xp_rowpart);
-  dfree(c->xp_colpart);
   dfree(c->bal_bounds);
   dfree(c->team_bar);
   dfree(c->team_part);
@@ -1008,8 +968,7 @@ const char* ppls_last_error(const ppls_ctx* c) { return c ? c->err.c_str() : "nu
 int ppls_set_option(ppls_ctx* c, const char* key, int64_t value) {
   if (!c || !key) return PPLS_E_ARG;
   if (!strcmp(key, "sweep")) {
-    if (value != 0 && value != 2 && value != 3)
-      return fail(c, PPLS_E_ARG, "sweep must be 0 (auto), 2 (two-pass) or 3 (panel)");
+    if (value != 0 && value != 3) return fail(c, PPLS_E_ARG, "sweep must be 0 (auto) or 3 (panel)");
     c->sweep_mode = (int)value;
   } else if (!strcmp(key, "grid")) {
     if (value < 0 || value > 65535) return fail(c, PPLS_E_ARG, "grid out of range");
@@ -1035,9 +994,12 @@ int ppls_set_option(ppls_ctx* c, const char* key, int64_t value) {
     c->pipe_opt = value ? 1 : 0;
   } else if (!strcmp(key, "ldpad")) {   // applies to data set or generated afterwards
     c->ldpad = value ? 1 : 0;
-  } else if (!strcmp(key, "ablate")) {
-    if (value < 0 || value > 65535) return fail(c, PPLS_E_ARG, "ablate must be in [0,65535]");
-    c->ablate = (int)value;   // timing experiments (bits 0-9 break results; 10+ select equivalent variants)
+  } else if (!strcmp(key, "dots_rows")) {
+    if (value != 0 && value != 32 && value != 64) return fail(c, PPLS_E_ARG, "dots_rows must be 0 (auto), 32 or 64");
+    c->dots_rows = (int)value;
+  } else if (!strcmp(key, "dots_pair")) {
+    if (value < -1 || value > 1) return fail(c, PPLS_E_ARG, "dots_pair must be -1 (auto), 0 or 1");
+    c->dots_pair = (int)value;
   } else if (!strcmp(key, "strace")) {
     if (value && !c->strace) {
       HIPCHK(c, hipMalloc(&c->strace, (size_t)PPLS_STRACE_MAX_WG * 4 * sizeof(long long)));
@@ -1068,10 +1030,7 @@ int ppls_set_option(ppls_ctx* c, const char* key, int64_t value) {
   } else if (!strcmp(key, "xprod")) {
     if (value < -1 || value > 1) return fail(c, PPLS_E_ARG, "xprod must be -1 (auto), 0 (stream X, Y) or 1 (cross-products)");
     c->xprod = (int)value;
-  } else if (!strcmp(key, "xprod_kernel")) {
-    if (value < 0 || value > 3)
-      return fail(c, PPLS_E_ARG, "xprod_kernel must be 0 (auto), 1 (row groups), 2 (row tiles) or 3 (lower triangle)");
-    c->xprod_kernel = (int)value;
+    if (value == 0) xprod_free(c);   // streaming from now on: S's 8 (p+q)^2 bytes go back
   } else if (!strcmp(key, "xprod_fuse")) {
     c->xprod_fuse = value ? 1 : 0;
   } else if (!strcmp(key, "xprod_rw")) {
@@ -1369,7 +1328,7 @@ int ppls_mstep(ppls_ctx* c, const ppls_expect* fit, int r, int type, ppls_theta*
   int rc;
   if ((rc = ensure_r(c, r, 1))) return rc;
   const int grid = grid_of(c);
-  const int groups = ppls_twopass_groups(std::max<int64_t>(c->n_local, 1), grid);
+  const int groups = ppls_acc_groups(std::max<int64_t>(c->n_local, 1), grid);
   if ((rc = ensure_part(c, groups))) return rc;
   if (c->z_cols < 2 * r) {
     dfree(c->Z);
@@ -1469,8 +1428,8 @@ int ppls_em_run(ppls_ctx* c, ppls_theta* th, int r, int max_steps, double atol, 
   // EMsteps stops launching soon after convergence.  With collectives (RCCL or a host reducer) the
   // break must be the same on every rank: the mirror holds the iteration the rule fired at, which
   // every rank computes from the same all-reduced statistics, and a rank breaks at iteration s
-  // iff that iteration is <= s - 1 - EM_LOOKAHEAD -- an iteration whose event it has just synced,
-  // so the answer does not depend on how far each device has run.
+  // iff that iteration is <= s - EM_LOOKAHEAD -- the iteration whose event it has just synced, so
+  // the answer does not depend on how far each device has run.
   if (do_check) {
     if ((rc = ensure_stop(c)) || (rc = reset_stop(c))) return rc;
     c->sweep_stop = c->stop_d;
@@ -1492,7 +1451,7 @@ int ppls_em_run(ppls_ctx* c, ppls_theta* th, int r, int max_steps, double atol, 
     if (do_check && s > EM_LOOKAHEAD) {
       HIPCHK(c, hipEventSynchronize(evs[(size_t)(s - 1 - EM_LOOKAHEAD) % EM_LOOKAHEAD]));
       const int fired = __atomic_load_n(c->stop_mirror, __ATOMIC_ACQUIRE);
-      if (fired != 0 && fired <= s - 1 - EM_LOOKAHEAD) break;   // converged: stop launching
+      if (fired != 0 && fired <= s - EM_LOOKAHEAD) break;   // converged: stop launching
     }
     const int nxt = cur ^ 1;
     const bool wm = want_mu && !c->xp_active && (do_check || s == max_steps + 1);
@@ -1519,11 +1478,12 @@ int ppls_em_run(ppls_ctx* c, ppls_theta* th, int r, int max_steps, double atol, 
   HIPCHK(c, hipStreamSynchronize(c->stream));
   if ((rc = check_status(c))) return rc;
   if (c->xp_active && want_mu) {
-    // Eout's mu_T, mu_U (:802) need the rows: one streaming sweep of theta_{i_final}, whose
-    // finalize (scalars only) also restates Eout's moments from that sweep
+    // Eout's mu_T, mu_U (:802) need the rows: one sweep of theta_{i_final} that only writes this
+    // rank's mu rows (mu = a_i diag(alpha) + b_i diag(beta), ... from the rank's own rows and
+    // theta's scalars: no collective, so ranks may ask for mu or not independently).  Eout's
+    // moments are those the loop's finalize computed from S for theta_{i_final}.
     c->sweep_stop = nullptr;
-    if ((rc = sweep(c, r, cur, true))) return rc;
-    if ((rc = finalize(c, r, cur, cur ^ 1, -1, type, 0, true))) return rc;
+    if ((rc = sweep(c, r, cur, true, true))) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));
   }
   if (loglik) HIPCHK(c, hipMemcpy(loglik, c->loglik, sizeof(double) * i_final, hipMemcpyDeviceToHost));
@@ -2359,6 +2319,7 @@ int ppls_scores(ppls_ctx* c, const double* W, const double* C, int k, double* T,
   memset(&a, 0, sizeof a);
   a.X = c->X; a.Y = c->Y; a.n_local = c->n_local; a.p = c->p; a.q = c->q; a.ldx = c->ldx; a.ldy = c->ldy;
   a.Wp = c->W[0]; a.Cp = c->C[0]; a.sc = c->sc[0]; a.mu = c->mu; a.write_mu = 1; a.r = k;
+  a.num_cus = c->num_cus; a.dots_rows = c->dots_rows; a.dots_pair = c->dots_pair;
   HIPCHK(c, ppls_launch_panel_dots(&a, c->dtype, c->Z, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   const size_t blk = sizeof(double) * (size_t)c->n_local * k;
@@ -2468,35 +2429,33 @@ int ppls_xprod_prepare(ppls_ctx* c, double* ms, double* total_ms) {
   return PPLS_OK;
 }
 
+int ppls_xprod_release(ppls_ctx* c) {
+  if (!c) return PPLS_E_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  xprod_free(c);
+  return PPLS_OK;
+}
+
+int ppls_xprod_setup_times(ppls_ctx* c, double* gram_ms, double* allreduce_ms, double* total_ms) {
+  if (!c) return PPLS_E_ARG;
+  if (gram_ms) *gram_ms = c->xp_setup_ms;
+  if (allreduce_ms) *allreduce_ms = c->xp_setup_ar_ms;
+  if (total_ms) *total_ms = c->xp_setup_total_ms;
+  return PPLS_OK;
+}
+
 int ppls_xprod_info(ppls_ctx* c, int r, int* ready, int64_t* bytes_per_pass, double* flops, int* rows_per_wave) {
   if (!c) return PPLS_E_ARG;
   if (!c->have_data) return fail(c, PPLS_E_STATE, "no data");
   const int64_t P = (int64_t)c->ldx + c->ldy;
   if (ready) *ready = c->xp_ready ? 1 : 0;
-  if (bytes_per_pass) {   // S's bytes one iteration reads: the lower 128 x 128 tiles, or all of S
-    const int64_t nb = (c->ldx + 127) / 128 + (c->ldy + 127) / 128;
-    int64_t tri = 0;
-    for (int64_t I = 0; I < nb; ++I) {
-      const int64_t li = I < (c->ldx + 127) / 128 ? std::min<int64_t>(128, c->ldx - 128 * I)
-                                                   : std::min<int64_t>(128, c->ldy - 128 * (I - (c->ldx + 127) / 128));
-      for (int64_t J = 0; J <= I; ++J) {
-        const int64_t lj = J < (c->ldx + 127) / 128 ? std::min<int64_t>(128, c->ldx - 128 * J)
-                                                     : std::min<int64_t>(128, c->ldy - 128 * (J - (c->ldx + 127) / 128));
-        tri += li * lj;
-      }
-    }
-    *bytes_per_pass = xprod_kind(c, r < 1 ? 1 : r) == 3 ? 8 * tri : 8 * P * P;
-  }
+  if (bytes_per_pass) *bytes_per_pass = 8 * P * P;   // S's bytes one iteration reads
   if (flops) {   // lower 128 x 128 tiles incl. the diagonal ones, 2 flops per multiply-add
     const double nb = (double)((P + 127) / 128);
     flops[0] = 2.0 * (double)c->n_local * nb * (nb + 1) / 2.0 * 128.0 * 128.0;
   }
-  if (rows_per_wave) {   // the kernel kind in the hundreds, its rows per wave (1, 2 kinds) below
-    const int kind = xprod_kind(c, r < 1 ? 1 : r);
-    *rows_per_wave = 100 * kind + (kind == 1 ? ppls_xprod_rows_per_wave((int)P, r < 1 ? 1 : r, c->xprod_rw)
-                                  : kind == 2 ? ppls_xprod_tile_rows((int)P, r < 1 ? 1 : r, c->xprod_rw, c->num_cus)
-                                              : 32);
-  }
+  if (rows_per_wave) *rows_per_wave = ppls_xprod_tile_rows((int)P, r < 1 ? 1 : r, c->xprod_rw, c->num_cus);
   return PPLS_OK;
 }
 
@@ -2593,15 +2552,13 @@ int ppls_sweep_kernel(ppls_ctx* c, int r, char* buf, int len) {
   char k[128];
   if (plan == 3) {
     if (ppls_split_describe(&a, k, sizeof k) != 0) return fail(c, PPLS_E_STATE, "no split instantiation for r=%d", r);
-  } else if (plan == 4) {
+  } else {
     // as ppls_kernels.hip launch_panel_t picks them
-    const bool rows64 = (sweep_rows(c) >= 32768) != ((c->ablate & 4096) != 0);
+    const bool rows64 = c->dots_rows ? c->dots_rows == 64 : sweep_rows(c) >= 32768;
     const int64_t wtiles = (sweep_rows(c) + (rows64 ? 63 : 31)) / (rows64 ? 64 : 32);
-    const bool pair = (wtiles < (int64_t)c->num_cus * 4 * (rows64 ? 2 : 3)) != ((c->ablate & 2048) != 0);
+    const bool pair = c->dots_pair >= 0 ? c->dots_pair == 1 : wtiles < (int64_t)c->num_cus * 4 * (rows64 ? 2 : 3);
     snprintf(k, sizeof k, "panel<%s,%d> (mfmadots %d rows/%s + acc, %d chunks)", c->dtype ? "float" : "double", r,
              rows64 ? 64 : 32, pair ? "wave pair" : "wave", a.grid);
-  } else {
-    snprintf(k, sizeof k, "twopass (dots + acc, %d chunks)", a.grid);
   }
   snprintf(buf, (size_t)len, "%s%s", k, plan == 3 && nt ? " nt" : "");
   return PPLS_OK;

@@ -28,9 +28,12 @@ struct PplsSweepArgs {
   int rp;                // split sweep rows per pipeline step (0 auto, 1 or 2)
   int pipe;              // split kernel: 1 = dots(g+1) before update(g), 0 = after
   int* occ_out;          // split kernel: if set, report resident WGs per CU instead of launching
-  int grid;              // workgroups (split) / row chunks (two-pass, panel accumulation)
-  int ablate;            // timing experiments only (split): 1 no compute, 2 no HBM copies; 16 = nt loads
+  int grid;              // workgroups (split) / row chunks (accumulation, panel accumulation)
+  int nt;                // non-temporal loads of X, Y (data larger than the MALL)
   int dots_grid;         // panel dots workgroups (0 = enough for every row tile, capped)
+  int dots_rows;         // panel dots rows per wave: 0 auto (64 from 32768 rows, else 32), 32, 64
+  int dots_pair;         // panel dots wave pair per row tile: -1 auto (when tiles < wave slots), 0, 1
+  int dots_only;         // panel: the dots pass only (Z and mu; scores)
   int num_cus;           // compute units of the device (panel dots: wave pairs on small shards)
   const int* stop;       // device stop flag (em_run's convergence test) or nullptr: kernels exit if set
   long long* trace;      // split sweep diagnostics: 4 wall-clock stamps per workgroup, or nullptr
@@ -110,9 +113,9 @@ extern "C" {
 int ppls_split_supported(int r, int ldx, int ldy);
 hipError_t ppls_launch_sweep_split(const PplsSweepArgs* a, hipStream_t st);
 int ppls_split_describe(const PplsSweepArgs* a, char* buf, int len);
-hipError_t ppls_launch_sweep_twopass(const PplsSweepArgs* a, double* Z, hipStream_t st);
+// Maximiz_M on caller-supplied moments: X'mu_T, Y'mu_U partials from Z = [mu_T | mu_U] (row-major)
 hipError_t ppls_launch_accumulate(const PplsSweepArgs* a, const double* Z, hipStream_t st);
-int ppls_twopass_groups(int64_t n_local, int grid);
+int ppls_acc_groups(int64_t n_local, int grid);
 // Wide-p panel sweep (two GEMM-shaped passes); Z: n_local x 4r doubles; chunks = partial groups.
 int ppls_panel_chunks(int64_t n_local, int ldx, int ldy, int num_cus, int dtype_f32, int r);
 int64_t ppls_panel_z_len(int64_t n_local, int ldx, int ldy, int r);   // doubles of Z (+ transposed W, C)

@@ -309,7 +309,7 @@ template <int R, int NSH, int NT, int RP, bool PIPE, int SLOTS, int CPW>
 __global__ __launch_bounds__(NT, 2 * NT / 512) void ppls_sweep_split_kernel(
     const double* __restrict__ X, const double* __restrict__ Y, int64_t n_local, int ldx, int ldy,
     const double* __restrict__ Wp, const double* __restrict__ Cp, const PplsScalars* __restrict__ sc,
-    double* __restrict__ part, int64_t part_ld, double* __restrict__ mu, int write_mu, int ablate,
+    double* __restrict__ part, int64_t part_ld, double* __restrict__ mu, int write_mu, int nt_loads,
     const int* __restrict__ stop, long long* __restrict__ trace, const int64_t* __restrict__ row_bounds) {
   if (stop && *stop) return;   // em_run converged earlier (device stop flag)
   static_assert(SLOTS >= 2 * RP, "ring must hold the group being read and the group in flight");
@@ -388,9 +388,9 @@ __global__ __launch_bounds__(NT, 2 * NT / 512) void ppls_sweep_split_kernel(
     coff[j] = cinx[j] ? (uint32_t)min(ch * 1024 + lane * 16, ldx * 8 - 16)
                       : (uint32_t)min((ch - nchx) * 1024 + lane * 16, ldy * 8 - 16);
   }
-  // nt: the non-temporal load policy (ablate bit 4), a compile-time choice per copy of the loop
+  // nt: the non-temporal load policy (nt_loads), a compile-time choice per copy of the loop
   auto issue_row = [&](int i, auto nt) {
-    if ((ablate & 2) || !dma_wave) return;
+    if (!dma_wave) return;
     const int64_t row = rb + i;
     const char* xr = (const char*)(X + row * (int64_t)ldx);
     const char* yr = (const char*)(Y + row * (int64_t)ldy);
@@ -499,7 +499,7 @@ __global__ __launch_bounds__(NT, 2 * NT / 512) void ppls_sweep_split_kernel(
       if (tr) tr[1] = (long long)wall_clock64();
       double2 xc[RP][NSH] = {};
       load_x(0, xc, full);
-      if (!(ablate & 1)) dots(0, xc);
+      dots(0, xc);
       for (int gg = 0; gg < ngroups; ++gg) {
         if (write_mu) {
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -512,7 +512,6 @@ __global__ __launch_bounds__(NT, 2 * NT / 512) void ppls_sweep_split_kernel(
         }
         ppls_lds_barrier();   // red[gg&1] complete, group gg+1 landed, slots of group gg free
         if (gg * RP + SLOTS < nrows) issue_group(gg + SLOTS / RP, nt);
-        if (ablate & 1) continue;
         double mta = 0.0, mua = 0.0;
         zsum(gg, mta, mua);
         if constexpr (PIPE) {
@@ -537,7 +536,7 @@ __global__ __launch_bounds__(NT, 2 * NT / 512) void ppls_sweep_split_kernel(
     }
   };
   const bool full = NSH * HT * 16 <= nchx * 1024 && NSH * HT * 16 <= nchy * 1024;
-  if (ablate & 16) {
+  if (nt_loads) {
     if (full) run(std::true_type{}, std::true_type{});
     else run(std::false_type{}, std::true_type{});
   } else {
@@ -567,45 +566,10 @@ __global__ __launch_bounds__(NT, 2 * NT / 512) void ppls_sweep_split_kernel(
   }
 }
 
-// ============================================================================ generic two-pass
-// Pass 1: Z = [X W | Y C] (n_local x 2R row-major), one wave per row.
-__global__ __launch_bounds__(256) void ppls_dots_kernel(
-    const double* __restrict__ X, const double* __restrict__ Y, int64_t n_local, int ldx, int ldy,
-    const double* __restrict__ Wp, const double* __restrict__ Cp, int r, double* __restrict__ Z,
-    const int* __restrict__ stop) {
-  if (stop && *stop) return;   // em_run converged earlier (device stop flag)
-  const int lane = threadIdx.x & 63;
-  const int64_t wid = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  const int npx = ldx >> 1, npy = ldy >> 1;
-  for (int64_t row = wid; row < n_local; row += nw) {
-    double acc[2 * PPLS_RMAX];
-    for (int k = 0; k < 2 * r; ++k) acc[k] = 0.0;
-    const double2* xr = (const double2*)(X + row * ldx);
-    const double2* yr = (const double2*)(Y + row * ldy);
-    for (int pp = lane; pp < npx; pp += 64) {
-      const double2 x = xr[pp];
-      for (int k = 0; k < r; ++k) {
-        const double2 wv = *(const double2*)(Wp + (int64_t)k * ldx + 2 * pp);
-        acc[k] = fma(x.x, wv.x, fma(x.y, wv.y, acc[k]));
-      }
-    }
-    for (int pp = lane; pp < npy; pp += 64) {
-      const double2 y = yr[pp];
-      for (int k = 0; k < r; ++k) {
-        const double2 cv = *(const double2*)(Cp + (int64_t)k * ldy + 2 * pp);
-        acc[r + k] = fma(y.x, cv.x, fma(y.y, cv.y, acc[r + k]));
-      }
-    }
-    for (int k = 0; k < 2 * r; ++k) {
-      const double s = ppls_wave_sum(acc[k]);
-      if (lane == 0) Z[row * 2 * r + k] = s;
-    }
-  }
-}
-
-// Pass 2: S_X / S_Y partials over a chunk of rows, one thread per column pair; the Gram partial
-// of the chunk is computed by the block with blockIdx.x == 0.
+// ============================================================================ Maximiz_M on given moments
+// X'mu_T / Y'mu_U partials over a chunk of rows from caller-supplied moments Z = [mu_T | mu_U]
+// (ppls_mstep: Maximiz_M, EM_W_multi.R:732-733), one thread per column pair; the Gram partial of
+// the chunk is computed by the block with blockIdx.x == 0.
 __global__ __launch_bounds__(256) void ppls_acc_kernel(
     const double* __restrict__ X, const double* __restrict__ Y, int64_t n_local, int ldx, int ldy,
     const double* __restrict__ Z, int r, const PplsScalars* __restrict__ sc, int64_t rows_per_chunk,
@@ -727,19 +691,12 @@ __global__ __launch_bounds__(256) void ppls_panel_mfmadots_kernel(
     double* __restrict__ Z, double* __restrict__ mu,
     const int* __restrict__ stop) {
   if (stop && *stop) return;   // em_run converged earlier (device stop flag)
-  // compile-time timing ablations for experiment builds (tools/dots_ablate.sh; results invalid):
-  // PPLS_DOTS_ABLATE bit 0 no MFMAs, bit 1 no X loads, bit 2 no B loads.  Runtime flags here
-  // changed the production code generation (549 -> 673 us at the C5 share).  Round 3 at the C5
-  // share: every variant ran 574-591 us (profiles/r3_dots_ablate_c5s.txt) -- the per-tile LDS
+  // Round 3 at the C5 share (compile-time ablations of an experiment build: no MFMAs, no X loads,
+  // no B loads -- every variant ran 574-591 us, profiles/r3_dots_ablate_c5s.txt): the per-tile LDS
   // transpose and its waits bound the kernel, not the MFMAs or either load stream; yet loading the
   // MFMA operands straight from global memory (16 rows x 16 B per load instruction, no LDS) was
   // slower still, 616 vs 560 us and 4.53 vs 3.92 ms at C5 (profiles/r3_dots_direct_ab.txt): the
   // 16-row scatter costs more in the vector-memory pipeline than the transpose does in LDS.
-#ifndef PPLS_DOTS_ABLATE
-#define PPLS_DOTS_ABLATE 0
-#endif
-  constexpr bool ab_mfma = (PPLS_DOTS_ABLATE & 1) != 0, ab_x = (PPLS_DOTS_ABLATE & 2) != 0,
-                 ab_b = (PPLS_DOTS_ABLATE & 4) != 0;
   typedef double d4 __attribute__((ext_vector_type(4)));
   typedef float f4 __attribute__((ext_vector_type(4)));
   constexpr int ES = (int)sizeof(T);
@@ -796,7 +753,6 @@ __global__ __launch_bounds__(256) void ppls_panel_mfmadots_kernel(
       f4 xa[NL];
       auto ld4 = [&](const T* p) -> f4 { return *(const f4*)p; };   // (non-temporal: 16 % slower here)
       auto load_tile = [&](int tc, f4 (&b)[NL]) {
-        if constexpr (ab_x) return;
         const int c = tc < tc1 ? tc : tc1 - 1;   // a prefetch past the range re-reads its last tile
 #pragma unroll
         for (int u = 0; u < NL; ++u) b[u] = ld4(src[u] + c * KT);
@@ -811,16 +767,11 @@ __global__ __launch_bounds__(256) void ppls_panel_mfmadots_kernel(
         asm volatile("" ::: "memory");   // keep the loads below after the stores (buf is reused)
         double bw[KQ];
         const double* wb = wb0 + (int64_t)tc * KT * 16;
-        if constexpr (ab_b) {
 #pragma unroll
-          for (int s2 = 0; s2 < KQ; ++s2) bw[s2] = 1e-3 * s2;
-        } else {
-#pragma unroll
-          for (int s2 = 0; s2 < KQ; s2 += 2) {
-            const double2 w2 = *(const double2*)(wb + s2 * 16);
-            bw[s2] = w2.x;
-            bw[s2 + 1] = w2.y;
-          }
+        for (int s2 = 0; s2 < KQ; s2 += 2) {
+          const double2 w2 = *(const double2*)(wb + s2 * 16);
+          bw[s2] = w2.x;
+          bw[s2 + 1] = w2.y;
         }
         asm volatile("" ::: "memory");   // B before the next tiles' X in the vmcnt order
         load_tile(tc + 1, b);
@@ -836,14 +787,9 @@ __global__ __launch_bounds__(256) void ppls_panel_mfmadots_kernel(
 #pragma unroll
             for (int u = 0; u < 16 / ES; ++u) a[h * (16 / ES) + u] = pv[u];
           }
-          if constexpr (ab_mfma) {
 #pragma unroll
-            for (int s2 = 0; s2 < KQ; ++s2) acc[bk].x += (double)a[s2] * bw[s2];
-          } else {
-#pragma unroll
-            for (int s2 = 0; s2 < KQ; ++s2)
-              acc[bk] = __builtin_amdgcn_mfma_f64_16x16x4f64((double)a[s2], bw[s2], acc[bk], 0, 0, 0);
-          }
+          for (int s2 = 0; s2 < KQ; ++s2)
+            acc[bk] = __builtin_amdgcn_mfma_f64_16x16x4f64((double)a[s2], bw[s2], acc[bk], 0, 0, 0);
         }
       };
       if (tc0 < tc1) {
@@ -2507,7 +2453,7 @@ hipError_t launch_split_t(const PplsSweepArgs& a, hipStream_t st) {
   }
   hipLaunchKernelGGL(kern, dim3(a.grid), dim3(512), split_lds(R, a.ldx, a.ldy, 512, RP), st, a.X, a.Y,
                      a.n_local, a.ldx, a.ldy, a.Wp, a.Cp, a.sc, a.part, a.part_ld, a.mu, a.write_mu,
-                     a.ablate, a.stop, a.trace, a.row_bounds);
+                     a.nt, a.stop, a.trace, a.row_bounds);
   return hipGetLastError();
 }
 
@@ -2588,22 +2534,6 @@ hipError_t ppls_launch_sweep_split(const PplsSweepArgs* a, hipStream_t st) {
   }
 }
 
-hipError_t ppls_launch_sweep_twopass(const PplsSweepArgs* a, double* Z, hipStream_t st) {
-  if (a->n_local <= 0) return hipSuccess;
-  const int64_t nw = a->n_local;
-  int blocks = (int)((nw * 64 + 255) / 256);
-  if (blocks > 4096) blocks = 4096;
-  hipLaunchKernelGGL(ppls_dots_kernel, dim3(blocks), dim3(256), 0, st, a->X, a->Y, a->n_local,
-                     a->ldx, a->ldy, a->Wp, a->Cp, a->r, Z, a->stop);
-  const int np = (a->ldx >> 1) + (a->ldy >> 1);
-  const int64_t rpc = (a->n_local + a->grid - 1) / a->grid;
-  const int chunks = (int)((a->n_local + rpc - 1) / rpc);
-  hipLaunchKernelGGL(ppls_acc_kernel, dim3((np + 255) / 256, chunks), dim3(256), 0, st, a->X, a->Y,
-                     a->n_local, a->ldx, a->ldy, Z, a->r, a->sc, rpc, a->part, a->part_ld, a->mu,
-                     a->write_mu, a->stop);
-  return hipGetLastError();
-}
-
 hipError_t ppls_launch_accumulate(const PplsSweepArgs* a, const double* Z, hipStream_t st) {
   if (a->n_local <= 0) return hipSuccess;
   const int np = (a->ldx >> 1) + (a->ldy >> 1);
@@ -2632,14 +2562,13 @@ hipError_t launch_panel_t(const PplsSweepArgs* a, const T* X, const T* Y, double
     // rows per wave: 64 (four 16-row blocks per B load: half the B traffic of 32 rows; 246 VGPRs,
     // 2 waves/SIMD) from 32768 rows per shard, else 32 (146 VGPRs, 3 waves/SIMD).  C5 fp32: 8.28 ->
     // 7.80 ms per sweep; C5's 8-GPU share (62,500 rows): 1.125 -> 1.09 ms (profiles/r2_c5_dots_rows.txt).
-    // ablate bit 12 flips it.
-    const bool big = a->n_local >= 32768;
-    const int rb = (big != ((a->ablate & 4096) != 0)) ? 64 : 32;
+    // Option dots_rows (32 or 64) forces one.
+    const int rb = a->dots_rows == 32 || a->dots_rows == 64 ? a->dots_rows : a->n_local >= 32768 ? 64 : 32;
     const int64_t wtiles = (a->n_local + rb - 1) / rb;
     // column split over wave pairs when one wave per row tile would leave resident wave slots
-    // (2 waves/SIMD at 64 rows, 3 at 32) empty; ablate bit 11 flips it
+    // (2 waves/SIMD at 64 rows, 3 at 32) empty; option dots_pair (0 or 1) forces one form
     const int64_t slots = (int64_t)(a->num_cus > 0 ? a->num_cus : 256) * 4 * (rb == 64 ? 2 : 3);
-    const int ks = ((wtiles < slots) != ((a->ablate & 2048) != 0)) ? 2 : 1;
+    const int ks = a->dots_pair >= 0 ? (a->dots_pair ? 2 : 1) : wtiles < slots ? 2 : 1;
     const int64_t wgs = (wtiles + 4 / ks - 1) / (4 / ks);
     // the grid option (dots_grid) forces a smaller grid: tests of the grid-stride loop
     const int mblocks = (int)(a->dots_grid > 0 && a->dots_grid < wgs ? a->dots_grid : wgs < 16384 ? wgs : 16384);
@@ -2656,24 +2585,19 @@ hipError_t launch_panel_t(const PplsSweepArgs* a, const T* X, const T* Y, double
 #undef PPLS_LAUNCH_DOTS
   }
   constexpr int VEC = PplsVec16<T>::N;
-  if (a->ablate & 256) return hipGetLastError();   // dots only (scores)
-  PplsChunks ck;
-  if (a->ablate & 1024) {   // experiment: equal chunks
-    ck.big = ck.small = (a->n_local + chunks - 1) / chunks;
-    ck.nbig = chunks;
-  } else {   // half the chunks at 4x the rows of the other half
-    ck.nbig = chunks / 2;
-    const int nsmall = chunks - ck.nbig;
-    ck.big = (4 * a->n_local + 4 * ck.nbig + nsmall - 1) / (4 * ck.nbig + nsmall);
-    ck.small = (ck.big + 3) / 4;
-    if (ck.small < 1) ck.small = 1;
-  }
+  if (a->dots_only) return hipGetLastError();   // scores: Z and mu only
+  PplsChunks ck;   // half the chunks at 4x the rows of the other half (equal chunks: profiles/r2_c5_dots_rows.txt)
+  ck.nbig = chunks / 2;
+  const int nsmall = chunks - ck.nbig;
+  ck.big = (4 * a->n_local + 4 * ck.nbig + nsmall - 1) / (4 * ck.nbig + nsmall);
+  ck.small = (ck.big + 3) / 4;
+  if (ck.small < 1) ck.small = 1;
   // VALU accumulation: at C5 an MFMA form measured no faster in fp64 storage (7.7 vs 7.5 ms) and
   // slower in fp32 (6.0 vs 4.5 ms; profiles/r1_c5_*_acc_variants.txt) -- the pass is load-bound
   const int ntx = (a->ldx + 256 * VEC - 1) / (256 * VEC), nty = (a->ldy + 256 * VEC - 1) / (256 * VEC);
   // the accumulation pass's once-read stream: non-temporal loads where X, Y exceed the MALL (the
-  // sweep's nt policy, ablate bit 16): C5 fp32 4.05 -> 3.89 ms (profiles/r2_c5_nt_policy.txt)
-  if (a->ablate & 16)
+  // sweep's nt policy): C5 fp32 4.05 -> 3.89 ms (profiles/r2_c5_nt_policy.txt)
+  if (a->nt)
     hipLaunchKernelGGL((ppls_panel_acc_kernel<T, R, true>), dim3(ntx + nty, chunks), dim3(256), 0, st, X, Y,
                        a->n_local, a->ldx, a->ldy, Z, ck, a->part, a->part_ld, a->stop);
   else
@@ -2766,7 +2690,7 @@ int ppls_panel_chunks(int64_t n_local, int ldx, int ldy, int num_cus, int dtype_
 hipError_t ppls_launch_panel_dots(const PplsSweepArgs* a, int dtype_f32, double* Z, hipStream_t st) {
   if (a->n_local <= 0) return hipSuccess;
   PplsSweepArgs b = *a;
-  b.ablate = a->ablate | 256;   // dots only
+  b.dots_only = 1;
   if (dtype_f32) return launch_panel_dt<float>(&b, (const float*)a->X, (const float*)a->Y, Z, 0, st);
   return launch_panel_dt<double>(&b, a->X, a->Y, Z, 0, st);
 }
@@ -2778,7 +2702,7 @@ hipError_t ppls_launch_sweep_panel(const PplsSweepArgs* a, int dtype_f32, double
   return launch_panel_dt<double>(a, a->X, a->Y, Z, chunks, st);
 }
 
-int ppls_twopass_groups(int64_t n_local, int grid) {
+int ppls_acc_groups(int64_t n_local, int grid) {
   const int64_t rpc = (n_local + grid - 1) / grid;
   return (int)((n_local + rpc - 1) / rpc);
 }

@@ -21,32 +21,17 @@ extern "C" {
 hipError_t ppls_launch_gram_joint(const void* X, int ldx, int xcols, const void* Y, int ldy, int ycols, int f32,
                                   int64_t n, int p, int nsplit, double* part, int64_t part_stride, hipStream_t st);
 
-// Rows of S per wave of the apply kernels (rw_opt > 0 forces 1, 2 or 4 where instantiated):
-// kind 1 (row groups without LDS) and kind 0 (row tiles, B staged in LDS; the default).
-int ppls_xprod_rows_per_wave(int P, int r, int rw_opt);
+// Rows of S per wave of the tile kernel (rw_opt 1, 2, 4 or 8 (r <= 8) forces it; 0 = auto).
 int ppls_xprod_tile_rows(int P, int r, int rw_opt, int num_cus);
 
 // One iteration's statistics from S (P x P row-major, P = ldx + ldy, symmetric) and theta = (Wp, Cp,
 // sc): stats = [X'mu_T (ldx x r) | Y'mu_U (ldy x r) | Gram (2r x 2r)], the layout the sweeps'
-// reduction writes.  The apply kernel (kind 0 row tiles, kind 1 row groups; rw rows per wave)
-// streams S once and writes the X'mu_T, Y'mu_U rows and M = S B (P x 2r column-major, scratch); the
-// Gram kernel forms B'M, one workgroup per entry (fixed-order sums: deterministic) -- unless
-// with_gram = 0, when the finalize that follows forms it (PplsFinalizeArgs::xpM, r <= 8).
+// reduction writes.  The tile kernel (rw rows of S per wave) streams S once and writes the X'mu_T,
+// Y'mu_U rows and M = S B (P x 2r column-major, scratch); the Gram kernel forms B'M, one workgroup
+// per entry (fixed-order sums: deterministic) -- unless with_gram = 0, when the finalize that
+// follows forms it (PplsFinalizeArgs::xpM, r <= 8).
 // stop: the em_run stop flag (both kernels exit if it is set) or nullptr.
-hipError_t ppls_launch_xprod_apply(const double* S, int ldx, int ldy, int r, int kind, int rw, const double* Wp,
-                                   const double* Cp, const PplsScalars* sc, double* stats, double* M, const int* stop,
-                                   int with_gram, hipStream_t st);
-
-// Lower-triangle form (r <= PPLS_XP_TRI_RMAX; reads only S's lower 128 x 128 tiles): the run list
-// (runs of tiles of one block row; items: 4 ints per run {I, J0, J1, 0}, row_items: nb + 1 run
-// offsets per block row; both nullable) and the partials' lengths in doubles.  Returns the run count.
-#define PPLS_XP_TRI_RMAX 10
-int ppls_xprod_tri_plan(int ldx, int ldy, int r, int num_cus, int* items, int* row_items, int64_t* rowpart_len,
-                        int64_t* colpart_len);
-// The same statistics from the lower triangle: the tile kernel, the partial reduction (writes M,
-// X'mu_T, Y'mu_U) and the Gram kernel (items, row_items on the device).
-hipError_t ppls_launch_xprod_tri(const double* S, int ldx, int ldy, int r, const double* Wp, const double* Cp,
-                                 const PplsScalars* sc, double* stats, double* M, const int* items, int nruns,
-                                 const int* row_items, double* rowpart, double* colpart, const int* stop,
-                                 hipStream_t st);
+hipError_t ppls_launch_xprod_tile(const double* S, int ldx, int ldy, int r, int rw, const double* Wp,
+                                  const double* Cp, const PplsScalars* sc, double* stats, double* M, const int* stop,
+                                  int with_gram, hipStream_t st);
 }

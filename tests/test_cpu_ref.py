@@ -32,3 +32,23 @@ def test_cpu_ref_deterministic_per_thread_count():
     assert np.array_equal(a[1], b[1]) and np.array_equal(a[0]["W"], b[0]["W"])
     c = cpu_ref.em_steps(X, Y, th0, 3, nthreads=1)
     assert np.abs(c[1] - a[1]).max() / np.abs(a[1]).max() < 1e-13
+
+
+@pytest.mark.parametrize("n,p,q,a", [(300, 24, 18, 3), (200, 40, 9, 2)])
+def test_cpu_ref_whole_call_matches_oracle(n, p, q, a):
+    """cpu_ref_ppls_simult -- the whole PPLS_simult(X, Y, a) call bench.py times on the host (the
+    initialiser PPLS(X, Y, a, 20, 1e-4, 'random') from given draws, the EM loop with its stop rule,
+    Eout) -- against the numpy oracle's PPLS (EM_W_multi.R:229-279) + PPLS_simult (:758-807)."""
+    X, Y, _ = make_problem(n, p, q, a, seed=3 * n + a)
+    rng = np.random.default_rng(a)
+    inits = [o.initial_guess(p, q, "random", rng) for _ in range(a)]
+    est, ll, cs, secs = cpu_ref.ppls_simult_call(X, Y, a, inits, nthreads=2)
+    f0 = o.ppls(X, Y, a, 20, 1e-4, theta0s=inits)
+    assert list(cs) == list(f0["Other_output"]["Number_steps"])
+    ref = o.ppls_simult(X, Y, a, EMsteps=10, atol=1e-4, theta0=o.simult_theta0_from_ppls(f0))
+    assert len(ll) == len(ref["loglik"])
+    assert np.abs(ll - ref["loglik"]).max() / np.abs(ref["loglik"]).max() < 1e-11
+    assert np.abs(est["W"] - ref["estimates"]["W"]).max() < 1e-8
+    assert np.abs(est["C"] - ref["estimates"]["C"]).max() < 1e-8
+    assert abs(est["sigE"] - ref["estimates"]["sigE"]) < 1e-9
+    assert all(v >= 0 for v in secs.values())

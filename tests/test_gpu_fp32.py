@@ -116,7 +116,7 @@ def test_row_padding_is_invisible(dtype, p, q):
                                                  (0, 900, 2300, 17, 9, 0), (1, 5000, 31, 2, 2, 2)])
 def test_dots_wave_pair_equals_single_wave(dtype, n, p, q, r, grid):
     """Panel dots on small shards split each row tile's columns over a wave pair (KS = 2 in
-    ppls_panel_mfmadots_kernel; ablate bit 11 forces one wave per tile).  Both forms sum the same
+    ppls_panel_mfmadots_kernel; option dots_pair = 0 forces one wave per tile).  Both forms sum the same
     products in a different grouping: mu within 1e-13 of each other and of the oracle's E-step;
     `grid` > 0 shrinks the dots grid so workgroups loop (the pair's LDS combine sits inside that
     loop behind workgroup barriers); one column tile per matrix (p = 31, q = 2) leaves the pair's
@@ -126,15 +126,15 @@ def test_dots_wave_pair_equals_single_wave(dtype, n, p, q, r, grid):
     if dtype:
         X, Y = _round32(X), _round32(Y)
     mus = []
-    for ab in (0, 2048):
+    for pair in (-1, 0):
         with Context(0) as c:
             c.set_option("dtype", dtype)
             if grid:
                 c.set_option("grid", grid)
-            c.set_option("ablate", ab)
+            c.set_option("dots_pair", pair)
             c.set_data(X, Y)
             assert "panel" in c.sweep_kernel(r)
-            assert ("wave pair" in c.sweep_kernel(r)) == (ab == 0)
+            assert ("wave pair" in c.sweep_kernel(r)) == (pair == -1)
             e = c.estep(_theta(th0))
             mus.append((e.mu_T, e.mu_U))
     ref = o.expect_m(X, Y, *(th0[k] for k in ("W", "C", "B", "sigE", "sigF", "sigH", "sigT")))

@@ -121,11 +121,11 @@ def test_c3_full_size_properties(ctx):
 def test_c5_kernel_parity_vs_oracle(ctx, rows64):
     """The C5 panel sweep (fp32 storage) on n = 5,000 rows of the C5 model vs the fp64 oracle on the
     fp32-rounded data (the data as stored); dots64 = the 64-rows-per-wave dots kernel the full-size
-    C5 run uses (ablate bit 12 selects it below 32768 rows)."""
+    C5 run uses (option dots_rows selects it below 32768 rows)."""
     n, p, q, r, steps = 5_000, 10_000, 500, 10, 3
     truth, th0 = _truth_theta0(p, q, r)
     ctx.set_option("dtype", 1)
-    ctx.set_option("ablate", 4096 * rows64)
+    ctx.set_option("dots_rows", 64 if rows64 else 0)
     try:
         ctx.generate_synthetic(n, p, q, truth, seed=SEED)
         assert ctx.sweep_info(r)["variant"] == "panel"
@@ -134,7 +134,7 @@ def test_c5_kernel_parity_vs_oracle(ctx, rows64):
         X, Y = ctx.get_data()
     finally:
         ctx.set_option("dtype", 0)
-        ctx.set_option("ablate", 0)
+        ctx.set_option("dots_rows", 0)
     assert np.array_equal(X.astype(np.float32).astype(np.float64), X)   # widened fp32 values
     assert not neg and np.all(np.diff(ll) > 0)
     _check_vs_oracle(est, ll, X, Y, r, steps, th0)

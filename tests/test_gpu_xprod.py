@@ -18,7 +18,7 @@ from oracle import ppls_oracle as o
 pytestmark = pytest.mark.gpu
 
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
-DEFAULTS = dict(xprod=0, xprod_kernel=0, xprod_rw=0, xprod_fuse=1, dtype=0)
+DEFAULTS = dict(xprod=0, xprod_rw=0, xprod_fuse=1, dtype=0)
 
 
 @pytest.fixture(scope="module")
@@ -52,18 +52,17 @@ def _golden():
     return sorted(f for f in os.listdir(GOLD) if f.endswith(".npz") and not f.startswith(("seq_", "meta_", "rcheck_")))
 
 
-# (xprod_kernel, xprod_rw, xprod_fuse): auto, row groups, row tiles (LDS-staged W, C), lower
-# triangle; the Gram formed by the finalize (fuse 1, default) or by its own kernel
-KERNELS = [(0, 0, 1), (0, 0, 0), (1, 1, 1), (1, 2, 1), (2, 1, 1), (2, 2, 1), (2, 4, 1), (3, 0, 1)]
+# (xprod_rw, xprod_fuse): rows of S per wave of the tile kernel (0 auto); the Gram formed by the
+# finalize (fuse 1, default) or by its own kernel
+KERNELS = [(0, 1), (0, 0), (1, 1), (2, 1), (4, 1), (8, 1)]
 
 
-@pytest.mark.parametrize("kernel,rw,fuse", KERNELS, ids=[f"k{k}rw{w}f{f}" for k, w, f in KERNELS])
+@pytest.mark.parametrize("rw,fuse", KERNELS, ids=[f"rw{w}f{f}" for w, f in KERNELS])
 @pytest.mark.parametrize("name", _golden())
-def test_xprod_em_run_matches_golden(ctx, name, kernel, rw, fuse):
+def test_xprod_em_run_matches_golden(ctx, name, rw, fuse):
     g = np.load(os.path.join(GOLD, name))
     meta = json.loads(str(g["meta"]))
     ctx.set_option("xprod", 1)
-    ctx.set_option("xprod_kernel", kernel)
     ctx.set_option("xprod_rw", rw)
     ctx.set_option("xprod_fuse", fuse)
     ctx.set_data(g["X"], g["Y"])
@@ -122,22 +121,22 @@ def test_xprod_equals_streaming(ctx, n, p, q, r):
 
 @pytest.mark.parametrize("n,p,q,r", [(900, 300, 260, 5), (500, 1025, 131, 10), (400, 129, 127, 3), (300, 2, 700, 1),
                                      (600, 256, 256, 8)])
-def test_xprod_kernels_agree(ctx, n, p, q, r):
-    """The lower-triangle kernel (multi-block shapes, blocks cut by the X/Y seam, r up to its
-    limit) against the row-tile and row-group kernels that read all of S."""
+def test_xprod_rows_per_wave_agree(ctx, n, p, q, r):
+    """The tile kernel's rows-per-wave forms (multi-tile shapes, tiles cut by the X/Y seam, r up
+    to 10) give the same iterates: every form sums each row of M = S B in the same column order."""
     X, Y, th0 = make_problem(n, p, q, r, seed=p + q + r)
     ctx.set_option("xprod", 1)
     ctx.set_data(X, Y)
     out = {}
-    for kernel in (1, 2, 3):
-        ctx.set_option("xprod_kernel", kernel)
-        assert ctx.xprod_info(r)["rows_per_wave"] // 100 == kernel
+    for rw in (1, 2, 4) + ((8,) if r <= 8 else ()):
+        ctx.set_option("xprod_rw", rw)
+        assert ctx.xprod_info(r)["rows_per_wave"] == rw
         est, ll, _, _ = ctx.em_run(_theta(th0), 12, -np.inf, 0, want_eout=False)
-        out[kernel] = (est, ll)
-    for kernel in (2, 3):
-        assert _relerr(out[kernel][1], out[1][1]) < 1e-12
-        assert np.abs(out[kernel][0].W - out[1][0].W).max() < 1e-10
-        assert np.abs(out[kernel][0].C - out[1][0].C).max() < 1e-10
+        out[rw] = (est, ll)
+    for rw in out:
+        assert _relerr(out[rw][1], out[1][1]) < 1e-12
+        assert np.abs(out[rw][0].W - out[1][0].W).max() < 1e-10
+        assert np.abs(out[rw][0].C - out[1][0].C).max() < 1e-10
 
 
 def test_xprod_matches_oracle_and_qr(ctx):
@@ -221,13 +220,18 @@ def test_xprod_prepare_and_info(ctx):
     ctx.set_data(X, Y)
     ms, tot = ctx.xprod_prepare()
     assert ms > 0 and tot >= ms
-    ctx.set_option("xprod_kernel", 2)
+    g, ar, tot2 = ctx.xprod_setup_times()
+    assert g == ms and ar == 0.0 and tot2 == tot   # one rank: no all-reduce of S
     info = ctx.xprod_info(2)
     P = 70 + 34   # ld of q = 33 fp64 columns: 34
     assert info["ready"] and info["bytes_per_pass"] == 8 * P * P
-    ctx.set_option("xprod_kernel", 3)   # blocks 70 | 34: lower tiles 70^2 + 34 x 70 + 34^2
-    assert ctx.xprod_info(2)["bytes_per_pass"] == 8 * (70 * 70 + 34 * 70 + 34 * 34)
     assert ctx.xprod_prepare() == (0.0, 0.0)   # already formed
+    ctx.xprod_release()
+    assert not ctx.xprod_info(2)["ready"]
+    ms2, _ = ctx.xprod_prepare()
+    assert ms2 > 0 and ctx.xprod_info(2)["ready"]
+    ctx.set_option("xprod", 0)   # streaming from now on frees S
+    assert not ctx.xprod_info(2)["ready"]
 
 
 @pytest.mark.parametrize("k,n,p,q,r,dtype", [(3, 3001, 300, 200, 4, 0), (4, 2000, 700, 90, 10, 1),
@@ -268,15 +272,14 @@ def test_xprod_k_contexts_sharded(k, n, p, q, r, dtype):
     assert _relerr(mu, ref[2].mu_T) < tol
 
 
-@pytest.mark.parametrize("kernel", [1, 2, 3])
+@pytest.mark.parametrize("rw", [1, 2, 4])
 @pytest.mark.parametrize("n,p,q,r", [(200, 24, 18, 3), (300, 50, 50, 2), (400, 300, 131, 5), (350, 129, 258, 10),
                                      (150, 7, 5, 1)])
-def test_xprod_stats_unit_parity(ctx, kernel, n, p, q, r):
+def test_xprod_stats_unit_parity(ctx, rw, n, p, q, r):
     """One statistics step from S against the host: X'mu_T, Y'mu_U (EM_W_multi.R:691-694,
-    :732-733) and the Gram of [XW YC] for a given theta, every cross-product kernel."""
-    from ppls_amd import Theta
+    :732-733) and the Gram of [XW YC] for a given theta, every rows-per-wave form."""
     X, Y, th0 = make_problem(n, p, q, r, seed=3 * p + q + r)
-    ctx.set_option("xprod_kernel", kernel)
+    ctx.set_option("xprod_rw", rw)
     ctx.set_data(X, Y)
     th = _theta(th0)
     SX, SY, G = ctx.xprod_stats(th)

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Panel dots: a wave pair per row tile (column split, default on shards with fewer row tiles than
-# wave slots) vs one wave per row tile (ablate bit 11 flips the choice).  Interleaved arms in one
+# wave slots) vs one wave per row tile (option dots_pair = 0 forces it).  Interleaved arms in one
 # process; kernel trace gives the dots/acc averages per arm.  usage: tools/dots_pair_ab.sh <config>...
 set -o pipefail
 R="${GRAFT_REPO_ROOT:-$(pwd)}"
@@ -9,7 +9,7 @@ for cfg in "$@"; do
   out="$R/gpurun_out/dpair_$cfg"
   rm -rf "$out"
   timeout -s KILL 150 rocprofv3 --kernel-trace --output-format csv -d "$out" -o run \
-    -- python3 "$R/tools/option_ab.py" "$cfg" "" "ablate=2048" --reps 3 --iters 60 > "$out.log" 2>&1 || exit $?
+    -- python3 "$R/tools/option_ab.py" "$cfg" "" "dots_pair=0" --reps 3 --iters 60 > "$out.log" 2>&1 || exit $?
   grep "ms/iter" "$out.log"
   python3 - "$out/run_kernel_trace.csv" <<'PY'
 import csv, sys, collections

@@ -21,7 +21,6 @@ def main():
     ap.add_argument("configs", nargs="*", default=["c3"])
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--rw", type=int, default=0)
-    ap.add_argument("--kernel", type=int, default=0, help="0 auto, 1 row groups, 2 row tiles (B in LDS), 3 lower triangle")
     ap.add_argument("--stream-steps", type=int, default=20)
     args = ap.parse_args()
     from ppls_amd import Context
@@ -45,7 +44,6 @@ def main():
             # cross-products
             ctx.set_option("xprod", 1)
             ctx.set_option("xprod_rw", args.rw)
-            ctx.set_option("xprod_kernel", args.kernel)
             gram_ms, tot_ms = ctx.xprod_prepare()
             info = ctx.xprod_info(r)
             ctx.em_begin(th0)
@@ -66,7 +64,7 @@ def main():
             print(f"{key}: stream {1e3 * t_stream:.3f} ms/it ({1 / t_stream:.1f} it/s) | S: Gram {gram_ms:.1f} ms "
                   f"({info['gram_flops'] / (gram_ms * 1e-3) / 1e12:.1f} TF/s), total {tot_ms:.1f} ms | "
                   f"xprod {1e3 * t_xp:.4f} ms/it ({1 / t_xp:.0f} it/s), apply+gram kernels {1e3 * apply_ms:.1f} us "
-                  f"({info['bytes_per_pass'] / (apply_ms * 1e-3) / 1e12:.2f} TB/s of S, kernel={args.kernel} rows={info['rows_per_wave']}) | "
+                  f"({info['bytes_per_pass'] / (apply_ms * 1e-3) / 1e12:.2f} TB/s of S, rows={info['rows_per_wave']}) | "
                   f"break-even {tot_ms / (1e3 * (t_stream - t_xp)):.0f} iterations | loglik rel diff {rel:.1e}",
                   flush=True)
 
