@@ -194,7 +194,7 @@ def test_xprod_eout_requested_by_one_rank():
 def test_default_split_is_reproducible_across_contexts():
     """The split sweep's default row partition is the even split (option balance = 0), so two fresh
     contexts give bit-identical fits on a shape past the calibrated partition's threshold (>= 2048
-    rows per workgroup); balance = 1 changes only the last bits."""
+    rows per workgroup: 600,000 rows on a 256-workgroup grid); balance = 1 changes only the last bits."""
     from ppls_amd import Context
     n, p, q, r = 600_000, 64, 48, 3
     truth, th0 = _bench_model(p, q, r)
@@ -202,6 +202,7 @@ def test_default_split_is_reproducible_across_contexts():
     for bal in (0, 0, 1):
         with Context(0) as c:
             c.set_option("balance", bal)
+            c.set_option("grid", 256)
             c.generate_synthetic(n, p, q, truth, seed=SEED)
             assert c.sweep_info(r)["variant"] == "split512"
             est, ll, _, _ = c.em_run(th0, 5, -np.inf, 0, want_eout=False)
