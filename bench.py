@@ -102,7 +102,7 @@ def load_xprod_traffic(config):
     name = f"pmc_xprod_{config}_dp1.json"
     js = _profile_json(name)
     for kname, k in ((js or {}).get("kernels") or {}).items():
-        if "tile" in kname:
+        if "pass" in kname or "tile" in kname:
             return k.get("read_bytes_per_launch"), _source(name, js)
     return None, None
 

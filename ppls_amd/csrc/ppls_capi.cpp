@@ -138,6 +138,7 @@ struct ppls_ctx {
   double xp_setup_ar_ms = 0.0;   // the all-reduce of S (wall clock around it and its stream sync)
   int xp_nsplit = 0;
   rocblas_handle blas = nullptr;   // rocSOLVER (variances.PPLS_simult's p x p inverse), created lazily
+  int var_chol = 1;                // option "var_chol": that inverse by Cholesky when positive definite (1) or LU (0)
   // timing
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;
   size_t ev_used = 0;
@@ -1154,6 +1155,8 @@ int ppls_set_option(ppls_ctx* c, const char* key, int64_t value) {
     if (value == 0) xprod_free(c);   // streaming from now on: S's 8 (p+q)^2 bytes go back
   } else if (!strcmp(key, "xprod_fuse")) {
     c->xprod_fuse = value ? 1 : 0;
+  } else if (!strcmp(key, "var_chol")) {
+    c->var_chol = value ? 1 : 0;
   } else if (!strcmp(key, "xprod_pipe")) {
     int rc;
     if ((rc = xp_pipe_sync(c))) return rc;
@@ -2265,11 +2268,11 @@ int ppls_variances(ppls_ctx* c, const double* mu, const double* Cdiag, double si
   const double N = (double)c->n_total;
   if (a > p) return fail(c, PPLS_E_ARG, "more components (%d) than columns (%d)", a, p);
   int rc = PPLS_OK;
-  double *dmu = nullptr, *dpart = nullptr, *dS = nullptr, *dG = nullptr, *dM = nullptr, *dv = nullptr;
+  double *dmu = nullptr, *dpart = nullptr, *dS = nullptr, *dG = nullptr, *dM = nullptr, *dv = nullptr, *dMc = nullptr;
   double *dexp = nullptr, *dstar = nullptr, *dse = nullptr;
   rocblas_int *ipiv = nullptr, *info = nullptr;
   auto done = [&](int code) {
-    dfree(dmu); dfree(dpart); dfree(dS); dfree(dG); dfree(dM); dfree(dv); dfree(dexp); dfree(dstar); dfree(dse);
+    dfree(dmu); dfree(dpart); dfree(dS); dfree(dG); dfree(dM); dfree(dMc); dfree(dv); dfree(dexp); dfree(dstar); dfree(dse);
     if (ipiv) (void)hipFree(ipiv);
     if (info) (void)hipFree(info);
     return code;
@@ -2366,20 +2369,43 @@ int ppls_variances(ppls_ctx* c, const double* mu, const double* Cdiag, double si
     if (SSt_star) VCHK(hipMemcpyAsync(SSt_star + (size_t)i * pp, dstar, sizeof(double) * pp, hipMemcpyDeviceToHost, c->stream));
     VCHK(hipStreamSynchronize(c->stream));   // dv is reused by the next component
   }
-  if (rocsolver_dgetrf_strided_batched(c->blas, p, p, dM, p, (rocblas_stride)pp, ipiv, p, info, a) !=
-          rocblas_status_success ||
-      rocsolver_dgetri_strided_batched(c->blas, p, dM, p, (rocblas_stride)pp, ipiv, p, info, a) !=
-          rocblas_status_success)
-    return done(fail(c, PPLS_E_HIP, "rocsolver getrf/getri (strided batched) failed"));
+  // varMatrix = -solve(M) = (-M)^-1, and -M = SSt_exp - B_exp is the observed information: symmetric
+  // and, at a proper fit, positive definite.  Cholesky potrf + potri (half the flops of LU + inverse)
+  // on a copy of -M; if any matrix is not positive definite, the batch takes R's solve() route, LU
+  // getrf + getri, from the untouched M.  Either inverse is backward stable: they agree to ~kappa eps.
   std::vector<rocblas_int> inf(a, 0);
+  bool chol = c->var_chol != 0;
+  if (chol) {
+    VRC(dalloc(c, &dMc, pp * (size_t)a));
+    VCHK(hipMemcpyAsync(dMc, dM, sizeof(double) * pp * a, hipMemcpyDeviceToDevice, c->stream));
+    VCHK(ppls_launch_negate(dMc, (int64_t)pp * a, c->stream));
+    if (rocsolver_dpotrf_strided_batched(c->blas, rocblas_fill_lower, p, dMc, p, (rocblas_stride)pp, info, a) !=
+        rocblas_status_success)
+      return done(fail(c, PPLS_E_HIP, "rocsolver potrf (strided batched) failed"));
+    VCHK(hipMemcpyAsync(inf.data(), info, sizeof(rocblas_int) * a, hipMemcpyDeviceToHost, c->stream));
+    VCHK(hipStreamSynchronize(c->stream));
+    for (int i = 0; i < a; ++i) chol = chol && inf[i] == 0;
+    if (chol && rocsolver_dpotri_strided_batched(c->blas, rocblas_fill_lower, p, dMc, p, (rocblas_stride)pp, info, a) !=
+                    rocblas_status_success)
+      return done(fail(c, PPLS_E_HIP, "rocsolver potri (strided batched) failed"));
+  }
+  if (!chol) {
+    if (rocsolver_dgetrf_strided_batched(c->blas, p, p, dM, p, (rocblas_stride)pp, ipiv, p, info, a) !=
+            rocblas_status_success ||
+        rocsolver_dgetri_strided_batched(c->blas, p, dM, p, (rocblas_stride)pp, ipiv, p, info, a) !=
+            rocblas_status_success)
+      return done(fail(c, PPLS_E_HIP, "rocsolver getrf/getri (strided batched) failed"));
+  }
   VCHK(hipMemcpyAsync(inf.data(), info, sizeof(rocblas_int) * a, hipMemcpyDeviceToHost, c->stream));
   VCHK(hipStreamSynchronize(c->stream));
   for (int i = 0; i < a; ++i)
     if (inf[i] != 0)   // solve(): "Lapack routine dgesv: system is exactly singular"
       return done(fail(c, PPLS_E_NUMERIC, "component %d: B_exp - SSt_exp is exactly singular (U[%d,%d] = 0)", i + 1,
                        (int)inf[i], (int)inf[i]));
+  if (chol) std::swap(dM, dMc);   // the inverse to copy out
   for (int i = 0; i < a; ++i) {
-    VCHK(ppls_launch_negdiag(dM + pp * i, p, dse, c->stream));
+    if (chol) VCHK(ppls_launch_symdiag(dM + pp * i, p, dse, c->stream));
+    else VCHK(ppls_launch_negdiag(dM + pp * i, p, dse, c->stream));
     if (varMatrix) VCHK(hipMemcpyAsync(varMatrix + (size_t)i * pp, dM + pp * i, sizeof(double) * pp, hipMemcpyDeviceToHost, c->stream));
     VCHK(hipMemcpyAsync(seLoad + (size_t)i * p, dse, sizeof(double) * p, hipMemcpyDeviceToHost, c->stream));
     VCHK(hipStreamSynchronize(c->stream));   // dse is reused by the next component

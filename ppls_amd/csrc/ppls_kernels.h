@@ -162,6 +162,8 @@ hipError_t ppls_launch_varmat(const double* G, const double* cxt, const double* 
                               double k2, double bstar, double s4, double N, double* M, double* sst_exp,
                               double* sst_star, hipStream_t st);
 hipError_t ppls_launch_negdiag(double* M, int p, double* se, hipStream_t st);
+hipError_t ppls_launch_negate(double* M, int64_t len, hipStream_t st);
+hipError_t ppls_launch_symdiag(double* M, int p, double* se, hipStream_t st);
 hipError_t ppls_launch_to_colmajor(const double* src, int64_t n, int p, int ld, double* dst,
                                    hipStream_t st);
 }

@@ -8,8 +8,11 @@
 //   ppls_gram_finish_kernel sum of the splits, mirrored into a full column-major p x p
 //   ppls_xtmu_kernel        Cxt = X' mu (p x a) partials per row chunk (HBM-bound, one pass)
 //   ppls_varmat_kernel      B_exp - SSt_exp (and SSt_exp, SSt_star on request) of one component
-//   ppls_negdiag_kernel     varMatrix = -solve(.) and seLoad = sqrt(diag(varMatrix))
-// The p x p LU inverse between the last two is rocSOLVER getrf/getri (library factorisation).
+//   ppls_negdiag_kernel     varMatrix = -solve(.) and seLoad = sqrt(diag(varMatrix))  (LU path)
+//   ppls_negate_kernel, ppls_symdiag_kernel   the Cholesky path: -(B_exp - SSt_exp), then the
+//                           inverse's lower triangle mirrored and seLoad
+// The p x p inverse between them is rocSOLVER (library factorisation): Cholesky potrf/potri of the
+// observed information -(B_exp - SSt_exp) when it is positive definite, else LU getrf/getri.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -243,7 +246,34 @@ __global__ void ppls_negdiag_kernel(double* __restrict__ M, int p, double* __res
   if (a == b) se[a] = sqrt(v);
 }
 
+// batch x (p x p): M <- -M (before the Cholesky factorisation of -(B_exp - SSt_exp)).
+__global__ void ppls_negate_kernel(double* __restrict__ M, int64_t len) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < len) M[e] = -M[e];
+}
+
+// The lower triangle potri wrote (varMatrix = (-(B_exp - SSt_exp))^-1) mirrored into the upper one,
+// and seLoad = sqrt(diag(varMatrix)).
+__global__ void ppls_symdiag_kernel(double* __restrict__ M, int p, double* __restrict__ se) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (int64_t)p * p) return;
+  const int b = (int)(e / p), a = (int)(e - (int64_t)b * p);   // element (a, b), column-major
+  if (a < b) M[e] = M[(int64_t)a * p + b];
+  else if (a == b) se[a] = sqrt(M[e]);
+}
+
 extern "C" {
+
+hipError_t ppls_launch_negate(double* M, int64_t len, hipStream_t st) {
+  hipLaunchKernelGGL(ppls_negate_kernel, dim3((unsigned)((len + 255) / 256)), dim3(256), 0, st, M, len);
+  return hipGetLastError();
+}
+
+hipError_t ppls_launch_symdiag(double* M, int p, double* se, hipStream_t st) {
+  const int64_t pp = (int64_t)p * p;
+  hipLaunchKernelGGL(ppls_symdiag_kernel, dim3((unsigned)((pp + 255) / 256)), dim3(256), 0, st, M, p, se);
+  return hipGetLastError();
+}
 
 int ppls_gram_tiles(int p) {
   const int nb = (p + PPLS_GT - 1) / PPLS_GT;

@@ -2,8 +2,9 @@
 oracle (oracle.ppls_oracle.variances_ppls_simult, a literal restatement).
 
 Tolerances (fp64): the Gram 1e-13 relative (and exactly symmetric); W 1e-10 absolute; SSt_exp,
-SSt_star 1e-11 relative; varMatrix and seLoad 1e-8 relative (an LU inverse: rocSOLVER getrf/getri
-vs LAPACK gesv, both backward stable, differ by ~cond * eps).
+SSt_star 1e-11 relative; varMatrix and seLoad 1e-8 relative (the inverse of the observed information:
+rocSOLVER Cholesky potrf/potri by default, LU getrf/getri with option var_chol = 0 or when the matrix
+is not positive definite, vs LAPACK gesv -- all backward stable, they differ by ~cond * eps).
 """
 import numpy as np
 import pytest
@@ -54,9 +55,10 @@ def test_gram_fp32_storage(ctx):
     assert _rel(G, X32.T @ X32) < 1e-13
 
 
+@pytest.mark.parametrize("chol", [1, 0], ids=["chol", "lu"])
 @pytest.mark.parametrize("from_s", [False, True], ids=["gram", "from_S"])
 @pytest.mark.parametrize("xy", ["X", "Y"])
-def test_variances_matches_oracle(ctx, xy, from_s):
+def test_variances_matches_oracle(ctx, xy, from_s, chol):
     """from_S: the cross-product form has formed S = [X Y]'[X Y] for this data, and the variances
     take its X'X / Y'Y block instead of a Gram of their own (q = 29: the Y block starts mid-tile)."""
     import ppls_amd
@@ -64,11 +66,15 @@ def test_variances_matches_oracle(ctx, xy, from_s):
     fit = o.ppls_simult(X, Y, 3, EMsteps=20, atol=-np.inf, theta0=th0)
     D = X if xy == "X" else Y
     ref = o.variances_ppls_simult(fit, D, xy)
+    ctx.set_option("var_chol", chol)
     ctx.set_data(X, Y)
     if from_s:
         ctx.xprod_prepare()
         assert ctx.xprod_info(3)["ready"]
-    got = ppls_amd.variances_PPLS_simult(fit, None, xy, ctx=ctx)
+    try:
+        got = ppls_amd.variances_PPLS_simult(fit, None, xy, ctx=ctx)
+    finally:
+        ctx.set_option("var_chol", 1)
     assert np.abs(got["W"] - ref["W"]).max() < 1e-10
     for i in range(3):
         g, r = got["components"][i], ref["components"][i]

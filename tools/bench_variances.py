@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--nsplit", type=int, default=0)
     ap.add_argument("--em-steps", type=int, default=3)
     ap.add_argument("--no-full", action="store_true", help="skip the whole variances call")
+    ap.add_argument("--chol", type=int, default=1, help="1 Cholesky inverse (default), 0 LU")
     args = ap.parse_args()
     from ppls_amd import Context
     cfg = CONFIGS[args.config]
@@ -50,6 +51,7 @@ def main():
                fp64_mfma_peak_tflops=FP64_PEAK_TF, mfma_frac=exec_flops / ms / 1e9 / FP64_PEAK_TF,
                tiles=tiles)
     if not args.no_full:
+        ctx.set_option("var_chol", args.chol)
         est, ll, eout, _ = ctx.em_run(th0, args.em_steps, -np.inf, 0, want_eout=True, want_mu=True)
         t0 = time.perf_counter()
         W, Bx, V, se, _, _ = ctx.variances(eout.mu_T, eout.Ctt, est.sigE, 0, full=False)

@@ -19,6 +19,24 @@ from collections import defaultdict
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+
+def profiled_tree():
+    """The source tree the profiled run used: PPLS_PROFILED_TREE if set, else this checkout's HEAD
+    (+ "-dirty" when it has uncommitted changes) -- the summaries are written right after the
+    gpurun call that profiled this same tree."""
+    import subprocess
+    t = os.environ.get("PPLS_PROFILED_TREE")
+    if t:
+        return t
+    try:
+        h = subprocess.run(["git", "rev-parse", "--short=12", "HEAD"], cwd=ROOT, capture_output=True, text=True,
+                           check=True).stdout.strip()
+        dirty = subprocess.run(["git", "status", "--porcelain", "--untracked-files=no"], cwd=ROOT,
+                               capture_output=True, text=True).stdout.strip()
+        return h + ("-dirty" if dirty else "")
+    except (OSError, subprocess.CalledProcessError):
+        return None
+
 def load(path, sub):
     """{counter: average per dispatch} over the dispatches of kernels whose name contains sub."""
     acc = defaultdict(lambda: defaultdict(float))
@@ -40,7 +58,8 @@ def main():
     tag, workload, subs = args[0], args[1], args[2].split(",")
     base = os.path.join(ROOT, "gpurun_out", f"pmcc_{tag}")
     out = dict(workload=workload, kernels={}, definitions=__doc__.split("Definitions")[1].split("Writes")[0].strip(),
-               source=f"tools/pmc_compute.sh {tag} (rocprofv3 --pmc, 2 passes, separate runs)")
+               source=f"tools/pmc_compute.sh {tag} (rocprofv3 --pmc, 2 passes, separate runs)",
+               profiled_tree=profiled_tree())
     durations = {}
     if trace:
         for r in csv.DictReader(open(trace)):

@@ -20,6 +20,24 @@ from collections import defaultdict
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+
+def profiled_tree():
+    """The source tree the profiled run used: PPLS_PROFILED_TREE if set, else this checkout's HEAD
+    (+ "-dirty" when it has uncommitted changes) -- the summaries are written right after the
+    gpurun call that profiled this same tree."""
+    import subprocess
+    t = os.environ.get("PPLS_PROFILED_TREE")
+    if t:
+        return t
+    try:
+        h = subprocess.run(["git", "rev-parse", "--short=12", "HEAD"], cwd=ROOT, capture_output=True, text=True,
+                           check=True).stdout.strip()
+        dirty = subprocess.run(["git", "status", "--porcelain", "--untracked-files=no"], cwd=ROOT,
+                               capture_output=True, text=True).stdout.strip()
+        return h + ("-dirty" if dirty else "")
+    except (OSError, subprocess.CalledProcessError):
+        return None
+
 def per_launch(path, counter, subs=("sweep",)):
     """Sum over the kernels matching subs of the kernel's average counter value per dispatch."""
     total, names, launches = 0.0, set(), 0
@@ -55,7 +73,8 @@ def main():
                           "(MI355X_MICROARCH.md, HBM): read bytes = 2 x FETCH_SIZE x 1024; WRITE_SIZE exact",
                hbm_bytes_per_launch=hbm, algorithmic_bytes_per_launch=alg,
                traffic_over_algorithmic=hbm / alg,
-               source=f"rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) -- python3 bench.py; {note}")
+               source=f"rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) -- python3 bench.py; {note}",
+               profiled_tree=profiled_tree())
     path = os.path.join(ROOT, "profiles", f"pmc_sweep_{workload}.json")
     with open(path, "w") as f:
         json.dump(out, f, indent=1)
