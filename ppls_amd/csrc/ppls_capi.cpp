@@ -886,6 +886,7 @@ int check_status(ppls_ctx* c) {
 }
 
 void xprod_free(ppls_ctx* c) {
+  (void)xp_pipe_sync(c);   // a pipelined ppls_em_iterate session may still read S, M, T, K
   c->xp_ready = false;
   c->xp_active = false;
   c->xp_m_valid = false;
@@ -918,6 +919,8 @@ int compute_ssq(ppls_ctx* c) {
 
 int alloc_data(ppls_ctx* c, int64_t n_local, int p, int q, int64_t n_total) {
   int rc;
+  if ((rc = xp_pipe_sync(c))) return rc;
+  c->em_active = false;
   if (n_local < 0 || p < 1 || q < 1) return fail(c, PPLS_E_ARG, "bad shape n=%lld p=%d q=%d", (long long)n_local, p, q);
   c->n_local = n_local;
   c->n_total = n_total > 0 ? n_total : n_local;
