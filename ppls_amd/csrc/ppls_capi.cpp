@@ -830,11 +830,15 @@ int xp_pipe_step(ppls_ctx* c, int r, int cur, int nxt, int logl_index, int type,
   const int rw = std::min(4, ppls_xprod_tile_rows(P, r, c->xprod_rw, c->num_cus));
   if (!c->xp_m_valid) {
     HIPCHK(c, ppls_launch_xprod_tile(c->xp_S, c->ldx, c->ldy, r, rw, c->W[cur], c->C[cur], c->sc[cur], c->stats,
-                                     c->xp_M, c->sweep_stop, fuse ? 0 : 1, c->xp_sa));
+                                     c->xp_M, c->sweep_stop, 0, c->xp_sa));
     c->xp_m_valid = true;
   }
   HIPCHK(c, hipEventRecord(c->xp_ev_ready, c->xp_sa));
   HIPCHK(c, hipStreamWaitEvent(c->xp_sb, c->xp_ev_ready, 0));
+  // the Gram B'M of theta[cur]: formed by the finalize's scalar block (r <= 8, P <= 6144), else by its
+  // own kernel -- on the finalize's stream, so the next pass over S need not wait for it
+  if (!fuse)
+    HIPCHK(c, ppls_launch_xprod_gram(c->ldx, c->ldy, r, c->W[cur], c->C[cur], c->xp_M, c->stats, c->sweep_stop, c->xp_sb));
   c->xp_pending_gram = fuse;
   if ((rc = finalize(c, r, cur, nxt, logl_index, type, stop_step, c->xp_sb, c->xp_K))) return rc;
   HIPCHK(c, hipEventRecord(c->xp_ev_fin, c->xp_sb));
@@ -852,8 +856,6 @@ int xp_pipe_step(ppls_ctx* c, int r, int cur, int nxt, int logl_index, int type,
   HIPCHK(c, hipStreamWaitEvent(c->xp_sa, c->xp_ev_fin, 0));
   HIPCHK(c, ppls_launch_xprod_pipe(1, c->xp_S, c->ldx, c->ldy, r, rw, c->W[nxt], c->C[nxt], c->sc[cur], c->sc[nxt],
                                    c->xp_T, c->xp_K, c->stats, c->xp_M, c->sweep_stop, c->xp_sa));
-  if (!fuse)
-    HIPCHK(c, ppls_launch_xprod_gram(c->ldx, c->ldy, r, c->W[nxt], c->C[nxt], c->xp_M, c->stats, c->sweep_stop, c->xp_sa));
   return PPLS_OK;
 }
 

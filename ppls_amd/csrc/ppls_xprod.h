@@ -40,7 +40,7 @@ hipError_t ppls_launch_xprod_tile(const double* S, int ldx, int ldy, int r, int 
 // the apply M = [T^X K^X | T^Y K^Y] + theta_{i+1}'s X'mu_T, Y'mu_U into stats, with K = {F (r x r),
 // G (r x r), flag_X, flag_C} from the finalize (PplsFinalizeArgs::fexp) -- or, if a flag is 0, the
 // tile kernel's S blockdiag(Wn, Cn) from S.  Same grid as the tile kernel (rows per wave rw <= 4).
-#define PPLS_XP_PIPE_RMAX 8
+#define PPLS_XP_PIPE_RMAX 10
 // The Gram B'M alone (B = blockdiag(Wp, Cp)), one workgroup per upper-triangle entry, into stats.
 hipError_t ppls_launch_xprod_gram(int ldx, int ldy, int r, const double* Wp, const double* Cp, const double* M,
                                   double* stats, const int* stop, hipStream_t st);

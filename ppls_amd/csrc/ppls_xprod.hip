@@ -380,7 +380,7 @@ hipError_t ppls_launch_xprod_pipe(int which, const double* S, int ldx, int ldy, 
 #define PPLS_XPP_CASE(k) \
     case k: return launch_pipe_rw<k>(rw, which, S, ldx, ldy, Wn, Cn, sc_cur, sc_nxt, T, K, stats, M, stop, st);
     PPLS_XPP_CASE(1) PPLS_XPP_CASE(2) PPLS_XPP_CASE(3) PPLS_XPP_CASE(4) PPLS_XPP_CASE(5) PPLS_XPP_CASE(6)
-    PPLS_XPP_CASE(7) PPLS_XPP_CASE(8)
+    PPLS_XPP_CASE(7) PPLS_XPP_CASE(8) PPLS_XPP_CASE(9) PPLS_XPP_CASE(10)
 #undef PPLS_XPP_CASE
     default: return hipErrorInvalidValue;
   }

@@ -298,7 +298,7 @@ def test_xprod_stats_unit_parity(ctx, rw, n, p, q, r):
 # iteration i runs, M_{i+1} = [T^X K^X | T^Y K^Y]; against the serial cross-product iteration
 @pytest.mark.parametrize("n,p,q,r,dtype", [(900, 300, 260, 5, 0), (500, 1025, 131, 8, 0), (400, 129, 127, 3, 0),
                                            (300, 2, 700, 1, 0), (600, 256, 256, 8, 1), (2000, 33, 7, 2, 0),
-                                           (700, 64, 31, 4, 1)])
+                                           (700, 64, 31, 4, 1), (500, 700, 90, 10, 0), (300, 6200, 90, 9, 1)])
 def test_xprod_pipelined_equals_serial(ctx, n, p, q, r, dtype):
     X, Y, th0 = make_problem(n, p, q, r, seed=5 * n + p + r)
     ctx.set_option("dtype", dtype)
