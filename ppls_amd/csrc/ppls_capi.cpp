@@ -124,9 +124,9 @@ struct ppls_ctx {
   // the pipelined cross-product iteration (option "xprod_pipe", r <= 8, SVD): the
   // pass over S of iteration i runs on xp_sa while the finalize of iteration i runs on xp_sb, on
   // disjoint CUs (the finalize's blocks need a whole CU each: one wave per SIMD)
-  int xprod_pipe = 1;
+  int xprod_pipe = 1;       // 0 off, 1 CU-partitioned streams, 2 plain streams (the finalize's at top priority)
   hipStream_t xp_sa = nullptr, xp_sb = nullptr;
-  int xp_sb_cus = 0;
+  int xp_sb_cus = 0, xp_stream_mode = 0;
   hipEvent_t xp_ev_ready = nullptr, xp_ev_fin = nullptr, xp_ev_join = nullptr;
   double* xp_T = nullptr;   // T = S blockdiag(M[X, :], M[Y, :]), P x 4r
   double* xp_K = nullptr;   // F, G (r x r each) + 2 flags, exported by the finalize
@@ -788,18 +788,27 @@ int xp_pipe_setup(ppls_ctx* c, int r) {
   const int need = team(c->p) + team(c->q) + 1;
   const int cus = std::max(8, (need + 7) / 8 * 8);
   if (2 * cus > c->num_cus) return fail(c, PPLS_E_ARG, "pipelined cross-products: %d finalize CUs of %d", cus, c->num_cus);
-  if (!c->xp_sa || c->xp_sb_cus != cus) {
+  const int mode = c->xprod_pipe;
+  if (!c->xp_sa || c->xp_stream_mode != mode || (mode == 1 && c->xp_sb_cus != cus)) {
     int rc;
     if ((rc = xp_pipe_sync(c))) return rc;
     if (c->xp_sa) (void)hipStreamDestroy(c->xp_sa);
     if (c->xp_sb) (void)hipStreamDestroy(c->xp_sb);
     c->xp_sa = c->xp_sb = nullptr;
-    const int nw = (c->num_cus + 31) / 32;
-    std::vector<uint32_t> ma((size_t)nw, 0u), mb((size_t)nw, 0u);
-    for (int cu = 0; cu < c->num_cus; ++cu) (cu < cus ? mb : ma)[(size_t)(cu >> 5)] |= 1u << (cu & 31);
-    HIPCHK(c, hipExtStreamCreateWithCUMask(&c->xp_sa, (uint32_t)nw, ma.data()));
-    HIPCHK(c, hipExtStreamCreateWithCUMask(&c->xp_sb, (uint32_t)nw, mb.data()));
-    c->xp_sb_cus = cus;
+    if (mode == 1) {
+      const int nw = (c->num_cus + 31) / 32;
+      std::vector<uint32_t> ma((size_t)nw, 0u), mb((size_t)nw, 0u);
+      for (int cu = 0; cu < c->num_cus; ++cu) (cu < cus ? mb : ma)[(size_t)(cu >> 5)] |= 1u << (cu & 31);
+      HIPCHK(c, hipExtStreamCreateWithCUMask(&c->xp_sa, (uint32_t)nw, ma.data()));
+      HIPCHK(c, hipExtStreamCreateWithCUMask(&c->xp_sb, (uint32_t)nw, mb.data()));
+    } else {
+      int lo = 0, hi = 0;
+      HIPCHK(c, hipDeviceGetStreamPriorityRange(&lo, &hi));
+      HIPCHK(c, hipStreamCreateWithFlags(&c->xp_sa, hipStreamNonBlocking));
+      HIPCHK(c, hipStreamCreateWithPriority(&c->xp_sb, hipStreamNonBlocking, hi));
+    }
+    c->xp_sb_cus = mode == 1 ? cus : 0;
+    c->xp_stream_mode = mode;
   }
   if (!c->xp_ev_ready) {
     HIPCHK(c, hipEventCreateWithFlags(&c->xp_ev_ready, hipEventDisableTiming));
@@ -1163,9 +1172,10 @@ int ppls_set_option(ppls_ctx* c, const char* key, int64_t value) {
   } else if (!strcmp(key, "var_chol")) {
     c->var_chol = value ? 1 : 0;
   } else if (!strcmp(key, "xprod_pipe")) {
+    if (value < 0 || value > 2) return fail(c, PPLS_E_ARG, "xprod_pipe must be 0 (off), 1 (CU-partitioned) or 2 (priority)");
     int rc;
     if ((rc = xp_pipe_sync(c))) return rc;
-    c->xprod_pipe = value ? 1 : 0;
+    c->xprod_pipe = (int)value;
     c->em_active = false;
   } else if (!strcmp(key, "xprod_rw")) {
     if (value != 0 && value != 1 && value != 2 && value != 4 && value != 8)
@@ -2613,6 +2623,18 @@ int ppls_xprod_release(ppls_ctx* c) {
   HIPCHK(c, hipSetDevice(c->device));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   xprod_free(c);
+  return PPLS_OK;
+}
+
+int ppls_xprod_pipe_masks(ppls_ctx* c, uint32_t* mask_a, uint32_t* mask_b, int words, int* cus_b) {
+  if (!c || words < 0) return PPLS_E_ARG;
+  if (cus_b) *cus_b = c->xp_sb_cus;
+  for (int w = 0; w < words; ++w) {
+    if (mask_a) mask_a[w] = 0;
+    if (mask_b) mask_b[w] = 0;
+  }
+  if (c->xp_sa && mask_a && words > 0) HIPCHK(c, hipExtStreamGetCUMask(c->xp_sa, (uint32_t)words, mask_a));
+  if (c->xp_sb && mask_b && words > 0) HIPCHK(c, hipExtStreamGetCUMask(c->xp_sb, (uint32_t)words, mask_b));
   return PPLS_OK;
 }
 

@@ -82,6 +82,16 @@ __device__ __forceinline__ void ppls_rs(double (&a)[N], int lane, int& idx, bool
   ppls_rs_r<M, L, N>(a, lane, idx, canon, real);
   canon = canon && real > 0;
 }
+// The same; for M > 64 (several values per lane) nreal = how many of the lane's values
+// idx, idx + 1, ... are real -- only those may be published (the rest are pad slots whose indices
+// belong to real values of other lanes).
+template <int M, int L, int N>
+__device__ __forceinline__ void ppls_rs(double (&a)[N], int lane, int& idx, bool& canon, int& nreal) {
+  int real = M;
+  ppls_rs_r<M, L, N>(a, lane, idx, canon, real);
+  canon = canon && real > 0;
+  nreal = real;
+}
 
 // ============================================================================ LDS-DMA helpers
 __device__ __forceinline__ void ppls_wait_vmcnt(int n) {

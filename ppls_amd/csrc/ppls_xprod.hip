@@ -125,13 +125,13 @@ __device__ __forceinline__ void ppls_xprod_rows(const double* __restrict__ S, in
     for (int v = 0; v <= NV; ++v) acc[v] = 0.0;
     if (ph == 0) ppls_xprod_tile_phase<RB, RW, NT>(srow, Bx, ldbx, ldx, 0, acc, sB, lane);
     else ppls_xprod_tile_phase<RB, RW, NT>(srow, By, ldby, ldy, ldx, acc, sB, lane);
-    int idx = 0;
+    int idx = 0, nreal = 0;
     bool canon = true;
-    ppls_rs<NV, 0, NV + 1>(acc, lane, idx, canon);
+    ppls_rs<NV, 0, NV + 1>(acc, lane, idx, canon, nreal);
     if (canon) {
 #pragma unroll
       for (int j = 0; j < LEFT; ++j)
-        if (idx + j < NV) {
+        if (j < nreal && idx + j < NV) {
           const int rr = (idx + j) / RB, t = idx + j - rr * RB;
           smw[rr * R2 + ph * RB + t] = acc[j];
         }
