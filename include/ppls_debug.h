@@ -33,9 +33,6 @@ int ppls_xprod_info(ppls_ctx* ctx, int r, int* ready, int64_t* bytes_per_pass, d
 /* The last formation of S: the MFMA Gram (HIP events), the all-reduce of S over ranks (wall clock
  * around the collective and its stream synchronisation; 0 on one rank) and the whole setup. */
 int ppls_xprod_setup_times(ppls_ctx* ctx, double* gram_ms, double* allreduce_ms, double* total_ms);
-/* The pipelined cross-product iteration's streams (option "xprod_pipe"): their CU masks as HIP reports
- * them (words 32-bit words each; zeros for a stream not created) and the CUs given to the finalize. */
-int ppls_xprod_pipe_masks(ppls_ctx* ctx, uint32_t* mask_a, uint32_t* mask_b, int words, int* cus_b);
 /* One statistics step from S for theta: stats = [X'mu_T p x r | Y'mu_U q x r | Gram 2r x 2r], all
  * column-major, as ppls_finalize_host takes them (unit parity against the sweep and a host S B). */
 int ppls_xprod_stats(ppls_ctx* ctx, const ppls_theta* th, int r, double* stats);

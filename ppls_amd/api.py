@@ -379,15 +379,6 @@ class Context:
         that reads S forms it again."""
         self._chk(self._L.ppls_xprod_release(self.h))
 
-    def xprod_pipe_masks(self, words=16):
-        """(CU mask of the pass/apply stream, CU mask of the finalize stream, finalize CUs) of the
-        pipelined cross-product iteration, as HIP reports them (lists of 32-bit words)."""
-        a = (ct.c_uint32 * words)()
-        b = (ct.c_uint32 * words)()
-        n = ct.c_int()
-        self._chk(self._L.ppls_xprod_pipe_masks(self.h, a, b, int(words), ct.byref(n)))
-        return list(a), list(b), n.value
-
     def xprod_setup_times(self):
         """(Gram kernel ms, all-reduce of S ms, whole setup ms) of the last formation of S."""
         g, a, t = ct.c_double(), ct.c_double(), ct.c_double()

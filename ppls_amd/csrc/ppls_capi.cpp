@@ -121,16 +121,6 @@ struct ppls_ctx {
   bool xp_active = false;   // statistics steps of the current run read S
   bool xp_pending_gram = false;   // the last statistics step left the Gram B'M to the next finalize
   int xprod_fuse = 1;       // option "xprod_fuse": the finalize forms the Gram (r <= 8, P <= 6144)
-  // the pipelined cross-product iteration (option "xprod_pipe", r <= 8, SVD): the
-  // pass over S of iteration i runs on xp_sa while the finalize of iteration i runs on xp_sb, on
-  // disjoint CUs (the finalize's blocks need a whole CU each: one wave per SIMD)
-  int xprod_pipe = 1;       // 0 off, 1 CU-partitioned streams, 2 plain streams (the finalize's at top priority)
-  hipStream_t xp_sa = nullptr, xp_sb = nullptr;
-  int xp_sb_cus = 0, xp_stream_mode = 0;
-  hipEvent_t xp_ev_ready = nullptr, xp_ev_fin = nullptr, xp_ev_join = nullptr;
-  double* xp_T = nullptr;   // T = S blockdiag(M[X, :], M[Y, :]), P x 4r
-  double* xp_K = nullptr;   // F, G (r x r each) + 2 flags, exported by the finalize
-  bool xp_m_valid = false;  // M and stats hold the current theta's statistics (pipelined run)
   double* xp_S = nullptr;
   double* xp_M = nullptr;   // M = S blockdiag(W, C), P x 2r scratch
   double xp_setup_ms = 0.0; // last formation of S: Gram kernel (HIP events), and with the all-reduce
@@ -239,14 +229,10 @@ PplsScalars scalars_of(const ppls_theta* th, int r) {
   return s;
 }
 
-int xp_pipe_sync(ppls_ctx* c);
-
 int ensure_r(ppls_ctx* c, int r, int max_steps) {
   int rc;
-  if ((rc = xp_pipe_sync(c))) return rc;   // a ppls_em_iterate session may still run on the pipeline streams
   c->em_active = false;   // every entry point that (re)stages theta ends an ppls_em_begin session
   c->xp_active = false;
-  c->xp_m_valid = false;
   if (r != c->r_alloc) {
     for (int i = 0; i < 2; ++i) {
       if ((rc = dalloc(c, &c->W[i], (size_t)c->ldx * r))) return rc;
@@ -600,9 +586,7 @@ int sweep(ppls_ctx* c, int r, int slot, bool write_mu, bool mu_only = false) {
   return allreduce(c, c->stats, (size_t)c->part_ld);
 }
 
-int finalize(ppls_ctx* c, int r, int cur, int nxt, int logl_index, int type, int stop_step = 0,
-             hipStream_t st = nullptr, double* fexp = nullptr) {
-  if (!st) st = c->stream;
+int finalize(ppls_ctx* c, int r, int cur, int nxt, int logl_index, int type, int stop_step = 0) {
   PplsFinalizeArgs f;
   f.stats = c->stats;
   f.ssq = c->ssq;
@@ -646,8 +630,7 @@ int finalize(ppls_ctx* c, int r, int cur, int nxt, int logl_index, int type, int
   f.atol = c->stop_atol;
   f.xpM = c->xp_pending_gram ? c->xp_M : nullptr;   // the Gram of a cross-product step, formed here
   c->xp_pending_gram = false;
-  f.fexp = fexp;
-  HIPCHK(c, ppls_launch_finalize(&f, st));
+  HIPCHK(c, ppls_launch_finalize(&f, c->stream));
   return PPLS_OK;
 }
 
@@ -764,110 +747,6 @@ int stats_step(ppls_ctx* c, int r, int slot, bool write_mu, bool finalize_next =
   return sweep(c, r, slot, write_mu);
 }
 
-// ---- the pipelined cross-product iteration
-bool xp_pipe_on(const ppls_ctx* c, int r, int type) {
-  return c->xp_active && c->xprod_pipe && r <= PPLS_XP_PIPE_RMAX && type == PPLS_ORTH_SVD && c->seg_rows < 0;
-}
-
-// Wait for the pipeline streams (before the context's own stream touches their buffers).
-int xp_pipe_sync(ppls_ctx* c) {
-  if (c->xp_sa) HIPCHK(c, hipStreamSynchronize(c->xp_sa));
-  if (c->xp_sb) HIPCHK(c, hipStreamSynchronize(c->xp_sb));
-  return PPLS_OK;
-}
-
-// The two CU-partitioned streams (the finalize's KX + KY + 1 blocks get CUs [0, cus), the pass and
-// apply kernels the rest), their events and the T, K buffers; xp_sa then waits for the context
-// stream's work so far.
-int xp_pipe_setup(ppls_ctx* c, int r) {
-  auto team = [&](int rows) {
-    const int tr = c->team_rows > 0 ? c->team_rows : PPLS_TEAM_ROWS;
-    const int k = (rows + tr - 1) / tr;
-    return k < 1 ? 1 : k > PPLS_TEAM_MAX ? PPLS_TEAM_MAX : k;
-  };
-  const int need = team(c->p) + team(c->q) + 1;
-  const int cus = std::max(8, (need + 7) / 8 * 8);
-  if (2 * cus > c->num_cus) return fail(c, PPLS_E_ARG, "pipelined cross-products: %d finalize CUs of %d", cus, c->num_cus);
-  const int mode = c->xprod_pipe;
-  if (!c->xp_sa || c->xp_stream_mode != mode || (mode == 1 && c->xp_sb_cus != cus)) {
-    int rc;
-    if ((rc = xp_pipe_sync(c))) return rc;
-    if (c->xp_sa) (void)hipStreamDestroy(c->xp_sa);
-    if (c->xp_sb) (void)hipStreamDestroy(c->xp_sb);
-    c->xp_sa = c->xp_sb = nullptr;
-    if (mode == 1) {
-      const int nw = (c->num_cus + 31) / 32;
-      std::vector<uint32_t> ma((size_t)nw, 0u), mb((size_t)nw, 0u);
-      for (int cu = 0; cu < c->num_cus; ++cu) (cu < cus ? mb : ma)[(size_t)(cu >> 5)] |= 1u << (cu & 31);
-      HIPCHK(c, hipExtStreamCreateWithCUMask(&c->xp_sa, (uint32_t)nw, ma.data()));
-      HIPCHK(c, hipExtStreamCreateWithCUMask(&c->xp_sb, (uint32_t)nw, mb.data()));
-    } else {
-      int lo = 0, hi = 0;
-      HIPCHK(c, hipDeviceGetStreamPriorityRange(&lo, &hi));
-      HIPCHK(c, hipStreamCreateWithFlags(&c->xp_sa, hipStreamNonBlocking));
-      HIPCHK(c, hipStreamCreateWithPriority(&c->xp_sb, hipStreamNonBlocking, hi));
-    }
-    c->xp_sb_cus = mode == 1 ? cus : 0;
-    c->xp_stream_mode = mode;
-  }
-  if (!c->xp_ev_ready) {
-    HIPCHK(c, hipEventCreateWithFlags(&c->xp_ev_ready, hipEventDisableTiming));
-    HIPCHK(c, hipEventCreateWithFlags(&c->xp_ev_fin, hipEventDisableTiming));
-    HIPCHK(c, hipEventCreateWithFlags(&c->xp_ev_join, hipEventDisableTiming));
-  }
-  const int P = c->ldx + c->ldy;
-  int rc;
-  if (!c->xp_T && (rc = dalloc(c, &c->xp_T, (size_t)P * 4 * PPLS_XP_PIPE_RMAX))) return rc;
-  if (!c->xp_K && (rc = dalloc(c, &c->xp_K, (size_t)2 * PPLS_XP_PIPE_RMAX * PPLS_XP_PIPE_RMAX + 2))) return rc;
-  if (!c->xp_M && (rc = dalloc(c, &c->xp_M, (size_t)P * 2 * PPLS_RMAX))) return rc;
-  HIPCHK(c, hipEventRecord(c->xp_ev_join, c->stream));
-  HIPCHK(c, hipStreamWaitEvent(c->xp_sa, c->xp_ev_join, 0));
-  c->xp_m_valid = false;
-  return PPLS_OK;
-}
-
-// One EM iteration theta[cur] -> theta[nxt] of the pipelined form.  M and stats of theta[cur] are
-// on xp_sa (or are formed first, by the tile kernel from S); then
-//   xp_sb: finalize (moments, loglik, stop rule, theta[nxt], F and G exported)
-//   xp_sa: pass T = S blockdiag(M[X, :], M[Y, :])    -- concurrently, on the other CUs
-//   xp_sa: (after the finalize) apply: M, stats of theta[nxt] from T, F, G (or from S, see the kernel)
-// `last`: the run's final statistics step -- only the finalize (its loglik and moments) is needed.
-int xp_pipe_step(ppls_ctx* c, int r, int cur, int nxt, int logl_index, int type, int stop_step, bool last) {
-  int rc;
-  const int P = c->ldx + c->ldy;
-  const bool fuse = c->xprod_fuse && r <= 8 && P <= 6144;
-  const int rw = std::min(4, ppls_xprod_tile_rows(P, r, c->xprod_rw, c->num_cus));
-  if (!c->xp_m_valid) {
-    HIPCHK(c, ppls_launch_xprod_tile(c->xp_S, c->ldx, c->ldy, r, rw, c->W[cur], c->C[cur], c->sc[cur], c->stats,
-                                     c->xp_M, c->sweep_stop, 0, c->xp_sa));
-    c->xp_m_valid = true;
-  }
-  HIPCHK(c, hipEventRecord(c->xp_ev_ready, c->xp_sa));
-  HIPCHK(c, hipStreamWaitEvent(c->xp_sb, c->xp_ev_ready, 0));
-  // the Gram B'M of theta[cur]: formed by the finalize's scalar block (r <= 8, P <= 6144), else by its
-  // own kernel -- on the finalize's stream, so the next pass over S need not wait for it
-  if (!fuse)
-    HIPCHK(c, ppls_launch_xprod_gram(c->ldx, c->ldy, r, c->W[cur], c->C[cur], c->xp_M, c->stats, c->sweep_stop, c->xp_sb));
-  c->xp_pending_gram = fuse;
-  if ((rc = finalize(c, r, cur, nxt, logl_index, type, stop_step, c->xp_sb, c->xp_K))) return rc;
-  HIPCHK(c, hipEventRecord(c->xp_ev_fin, c->xp_sb));
-  if (last) {
-    HIPCHK(c, hipStreamWaitEvent(c->xp_sa, c->xp_ev_fin, 0));
-    c->xp_m_valid = false;
-    return PPLS_OK;
-  }
-  hipEvent_t e0, e1;
-  if ((rc = timing_pair(c, &e0, &e1))) return rc;
-  if (e0) HIPCHK(c, hipEventRecord(e0, c->xp_sa));
-  HIPCHK(c, ppls_launch_xprod_pipe(0, c->xp_S, c->ldx, c->ldy, r, rw, nullptr, nullptr, nullptr, nullptr, c->xp_T,
-                                   nullptr, nullptr, c->xp_M, c->sweep_stop, c->xp_sa));
-  if (e1) HIPCHK(c, hipEventRecord(e1, c->xp_sa));
-  HIPCHK(c, hipStreamWaitEvent(c->xp_sa, c->xp_ev_fin, 0));
-  HIPCHK(c, ppls_launch_xprod_pipe(1, c->xp_S, c->ldx, c->ldy, r, rw, c->W[nxt], c->C[nxt], c->sc[cur], c->sc[nxt],
-                                   c->xp_T, c->xp_K, c->stats, c->xp_M, c->sweep_stop, c->xp_sa));
-  return PPLS_OK;
-}
-
 // The device stop flag (2 ints) and its host-mapped mirror, allocated on first use.
 int ensure_stop(ppls_ctx* c) {
   if (c->stop_d) return PPLS_OK;
@@ -897,14 +776,10 @@ int check_status(ppls_ctx* c) {
 }
 
 void xprod_free(ppls_ctx* c) {
-  (void)xp_pipe_sync(c);   // a pipelined ppls_em_iterate session may still read S, M, T, K
   c->xp_ready = false;
   c->xp_active = false;
-  c->xp_m_valid = false;
   dfree(c->xp_S);
   dfree(c->xp_M);
-  dfree(c->xp_T);
-  dfree(c->xp_K);
 }
 
 int compute_ssq(ppls_ctx* c) {
@@ -930,7 +805,6 @@ int compute_ssq(ppls_ctx* c) {
 
 int alloc_data(ppls_ctx* c, int64_t n_local, int p, int q, int64_t n_total) {
   int rc;
-  if ((rc = xp_pipe_sync(c))) return rc;
   c->em_active = false;
   if (n_local < 0 || p < 1 || q < 1) return fail(c, PPLS_E_ARG, "bad shape n=%lld p=%d q=%d", (long long)n_local, p, q);
   c->n_local = n_local;
@@ -1069,7 +943,6 @@ void ppls_ctx_destroy(ppls_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  (void)xp_pipe_sync(c);
   if (c->comm) ncclCommDestroy(c->comm);
   dfree(c->X); dfree(c->Y); dfree(c->ssq);
   for (int i = 0; i < 2; ++i) { dfree(c->W[i]); dfree(c->C[i]); dfree(c->sc[i]); dfree(c->gram[i]); }
@@ -1089,12 +962,6 @@ void ppls_ctx_destroy(ppls_ctx* c) {
   for (auto& e : c->ev) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
   for (auto& e : c->ev_ar) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
   if (c->blas) (void)rocblas_destroy_handle(c->blas);
-  dfree(c->xp_T);
-  dfree(c->xp_K);
-  for (hipEvent_t e : {c->xp_ev_ready, c->xp_ev_fin, c->xp_ev_join})
-    if (e) (void)hipEventDestroy(e);
-  if (c->xp_sa) (void)hipStreamDestroy(c->xp_sa);
-  if (c->xp_sb) (void)hipStreamDestroy(c->xp_sb);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -1171,12 +1038,6 @@ int ppls_set_option(ppls_ctx* c, const char* key, int64_t value) {
     c->xprod_fuse = value ? 1 : 0;
   } else if (!strcmp(key, "var_chol")) {
     c->var_chol = value ? 1 : 0;
-  } else if (!strcmp(key, "xprod_pipe")) {
-    if (value < 0 || value > 2) return fail(c, PPLS_E_ARG, "xprod_pipe must be 0 (off), 1 (CU-partitioned) or 2 (priority)");
-    int rc;
-    if ((rc = xp_pipe_sync(c))) return rc;
-    c->xprod_pipe = (int)value;
-    c->em_active = false;
   } else if (!strcmp(key, "xprod_rw")) {
     if (value != 0 && value != 1 && value != 2 && value != 4 && value != 8)
       return fail(c, PPLS_E_ARG, "xprod_rw must be 0, 1, 2, 4 or 8");
@@ -1565,9 +1426,6 @@ int ppls_em_run(ppls_ctx* c, ppls_theta* th, int r, int max_steps, double atol, 
   // statistics from the cross-products S (option xprod; formed here if needed, outside the loop)
   c->xp_active = c->seg_rows < 0 && xprod_choose(c, max_steps);
   if (c->xp_active && (rc = xprod_setup(c))) { c->xp_active = false; return rc; }
-  const bool pipe = xp_pipe_on(c, r, type);
-  if (pipe && (rc = xp_pipe_setup(c, r))) return rc;
-  hipStream_t tail = pipe ? c->xp_sa : c->stream;   // where an iteration ends
   // The stop rule (EM_W_multi.R:792) runs on the device: the finalize that sees
   // logl[i] - logl[i-1] < atol sets a flag, and every later kernel of the run exits at once, so the
   // host enqueues iterations without a per-iteration read-back.  It polls the flag's host-mapped
@@ -1602,13 +1460,8 @@ int ppls_em_run(ppls_ctx* c, ppls_theta* th, int r, int max_steps, double atol, 
     }
     const int nxt = cur ^ 1;
     const bool wm = want_mu && !c->xp_active && (do_check || s == max_steps + 1);
-    if (pipe) {
-      if ((rc = xp_pipe_step(c, r, cur, nxt, s >= 2 ? s - 2 : -1, type, do_check && s >= 3 ? s : 0, s == max_steps + 1)))
-        return rc;
-    } else {
-      if ((rc = stats_step(c, r, cur, wm, true))) return rc;
-      if ((rc = finalize(c, r, cur, nxt, s >= 2 ? s - 2 : -1, type, do_check && s >= 3 ? s : 0))) return rc;
-    }
+    if ((rc = stats_step(c, r, cur, wm, true))) return rc;
+    if ((rc = finalize(c, r, cur, nxt, s >= 2 ? s - 2 : -1, type, do_check && s >= 3 ? s : 0))) return rc;
     if (do_check) {
       const size_t k = (size_t)(s - 1) % EM_LOOKAHEAD;
       if (evs.size() <= k) {
@@ -1616,12 +1469,10 @@ int ppls_em_run(ppls_ctx* c, ppls_theta* th, int r, int max_steps, double atol, 
         HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
         evs.push_back(e);
       }
-      HIPCHK(c, hipEventRecord(evs[k], tail));
+      HIPCHK(c, hipEventRecord(evs[k], c->stream));
     }
     cur = nxt;
   }
-  if (pipe && (rc = xp_pipe_sync(c))) return rc;
-  c->xp_m_valid = false;
   HIPCHK(c, hipStreamSynchronize(c->stream));
   // the iteration the run ended at: the finalize of sweep s_stop saw the stop rule fire, so
   // theta_{s_stop - 1} (slot (s_stop - 1) & 1) is the estimate and logl[1 .. s_stop - 1] the trace
@@ -2524,7 +2375,6 @@ int ppls_em_begin(ppls_ctx* c, const ppls_theta* th, int r) {
   c->em_iter = 0;
   c->xp_active = c->seg_rows < 0 && xprod_choose(c, 1 << 16);
   if (c->xp_active && (rc = xprod_setup(c))) { c->xp_active = false; return rc; }
-  if (xp_pipe_on(c, r, PPLS_ORTH_SVD) && (rc = xp_pipe_setup(c, r))) return rc;
   c->em_active = true;
   return PPLS_OK;
 }
@@ -2536,18 +2386,10 @@ int ppls_em_iterate(ppls_ctx* c, int nsteps, int type) {
   if (c->em_iter + nsteps + 2 > c->loglik_cap) return fail(c, PPLS_E_ARG, "too many iterations for one run");
   HIPCHK(c, hipSetDevice(c->device));
   int rc;
-  const bool pipe = xp_pipe_on(c, c->em_r, type) && c->xp_sa;
-  if (!pipe && (rc = xp_pipe_sync(c))) return rc;   // a QR-type call after pipelined SVD steps
-  if (!pipe) c->xp_m_valid = false;
   for (int s = 0; s < nsteps; ++s) {
     const int nxt = c->em_cur ^ 1;
-    if (pipe) {
-      if ((rc = xp_pipe_step(c, c->em_r, c->em_cur, nxt, c->em_iter >= 1 ? c->em_iter - 1 : -1, type, 0, false)))
-        return rc;
-    } else {
-      if ((rc = stats_step(c, c->em_r, c->em_cur, false, true))) return rc;
-      if ((rc = finalize(c, c->em_r, c->em_cur, nxt, c->em_iter >= 1 ? c->em_iter - 1 : -1, type))) return rc;
-    }
+    if ((rc = stats_step(c, c->em_r, c->em_cur, false, true))) return rc;
+    if ((rc = finalize(c, c->em_r, c->em_cur, nxt, c->em_iter >= 1 ? c->em_iter - 1 : -1, type))) return rc;
     c->em_cur = nxt;
     ++c->em_iter;
   }
@@ -2558,7 +2400,6 @@ int ppls_em_state(ppls_ctx* c, ppls_theta* out, double* loglik, int cap, int* n_
   if (!c) return PPLS_E_ARG;
   if (!c->em_active) return fail(c, PPLS_E_STATE, "call ppls_em_begin first");
   int rc;
-  if ((rc = xp_pipe_sync(c))) return rc;
   HIPCHK(c, hipStreamSynchronize(c->stream));
   if ((rc = check_status(c))) return rc;
   if (out && (rc = download_theta(c, c->em_r, c->em_cur, out))) return rc;
@@ -2570,8 +2411,6 @@ int ppls_em_state(ppls_ctx* c, ppls_theta* out, double* loglik, int cap, int* n_
 
 int ppls_synchronize(ppls_ctx* c) {
   if (!c) return PPLS_E_ARG;
-  int rc;
-  if ((rc = xp_pipe_sync(c))) return rc;
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return PPLS_OK;
 }
@@ -2626,18 +2465,6 @@ int ppls_xprod_release(ppls_ctx* c) {
   return PPLS_OK;
 }
 
-int ppls_xprod_pipe_masks(ppls_ctx* c, uint32_t* mask_a, uint32_t* mask_b, int words, int* cus_b) {
-  if (!c || words < 0) return PPLS_E_ARG;
-  if (cus_b) *cus_b = c->xp_sb_cus;
-  for (int w = 0; w < words; ++w) {
-    if (mask_a) mask_a[w] = 0;
-    if (mask_b) mask_b[w] = 0;
-  }
-  if (c->xp_sa && mask_a && words > 0) HIPCHK(c, hipExtStreamGetCUMask(c->xp_sa, (uint32_t)words, mask_a));
-  if (c->xp_sb && mask_b && words > 0) HIPCHK(c, hipExtStreamGetCUMask(c->xp_sb, (uint32_t)words, mask_b));
-  return PPLS_OK;
-}
-
 int ppls_xprod_setup_times(ppls_ctx* c, double* gram_ms, double* allreduce_ms, double* total_ms) {
   if (!c) return PPLS_E_ARG;
   if (gram_ms) *gram_ms = c->xp_setup_ms;
@@ -2684,8 +2511,6 @@ int ppls_xprod_stats(ppls_ctx* c, const ppls_theta* th, int r, double* stats) {
 
 int ppls_sweep_timing(ppls_ctx* c, double* total_ms, int64_t* launches, int reset) {
   if (!c) return PPLS_E_ARG;
-  int rc;
-  if ((rc = xp_pipe_sync(c))) return rc;
   HIPCHK(c, hipStreamSynchronize(c->stream));
   for (size_t i = 0; i < c->ev_used; ++i) {
     float ms = 0.f;

@@ -75,9 +75,6 @@ struct PplsFinalizeArgs {
   const double* xpM;     // cross-product form (ppls_xprod.hip): M = S blockdiag(Wc, Cc), (ldx + ldy) x 2r
                          // column-major, or nullptr; when set, the scalar block forms the Gram B'M itself
                          // (in the slack of the polar blocks) and writes it to stats' Gram slot
-  double* fexp;          // nullptr, or 2 r^2 + 2 doubles: the polar factors' right factors F (W_next = SX F)
-                         // and G, and a flag per matrix: 1 when the Cholesky-QR1 path produced them
-                         // (the pipelined cross-product iteration, ppls_xprod_apply_kernel), else 0
 };
 
 #define PPLS_TEAM_ROWS 2048   // rows of S per polar team member (tools/team_rows_ab.py: p = 2000 in one block is 4 us faster than a team of 2; C5 equal at 1024 and 2048)

@@ -1507,8 +1507,7 @@ __device__ bool ppls_block_polar_fast(const double* __restrict__ S, int64_t lds,
                                       double* __restrict__ out, int64_t ldo, int ldo_rows, double* Sl,
                                       double* sh, double* sm, double* __restrict__ gram_out,
                                       double* __restrict__ vstate, long long* tr, const PplsTeam& tm,
-                                      bool polar1, double kbound, double* __restrict__ fexp,
-                                      double* __restrict__ fflag) {
+                                      bool polar1, double kbound) {
   constexpr int NG = R * (R + 1) / 2;
   constexpr int NW = NT / 64;
   constexpr int G = PplsWaveBlk<R>::G, GG = G * G;
@@ -1674,7 +1673,6 @@ __device__ bool ppls_block_polar_fast(const double* __restrict__ S, int64_t lds,
           for (int kk = 0; kk < R; ++kk) s = fma(sF[kk * R + a], sU[b * G + kk], s);
           sF[R * R + b * R + a] = s;
           if (vstate && tm.rank == 0) vstate[b * R + a] = sV[b * G + a];   // every member's V is identical
-          if (fexp && tm.rank == 0) fexp[b * R + a] = s;   // F for the pipelined cross-product iteration
         }
       }
     }
@@ -1682,7 +1680,6 @@ __device__ bool ppls_block_polar_fast(const double* __restrict__ S, int64_t lds,
   }
   __syncthreads();
   const bool use1 = fast != 0;
-  if (fflag && use1 && tm.rank == 0 && tid == 0) *fflag = 1.0;   // F exported (the kernel zeroed the flag)
   // the rows pass 3 multiplies: S itself (fast path), else Q1, kept where pass 3 reads it back
   // (each thread its own rows): over S in LDS, else in out
   const double* Qs = use1 ? Sr : (Sl ? Sl : out);
@@ -2082,8 +2079,7 @@ __global__ __launch_bounds__(PPLS_FIN_THREADS) void ppls_finalize_kernel(
     const double* __restrict__ gram_cur, double* __restrict__ gram_nxt, double* __restrict__ vstate,
     int stage_lds, long long* __restrict__ trace,
     int* __restrict__ stop, int* __restrict__ stop_mirror, int stop_check, int stop_step, double atol,
-    int KX, int KY, unsigned* __restrict__ team_bar, double* __restrict__ team_part, const double* __restrict__ xpM,
-    double* __restrict__ fexp) {
+    int KX, int KY, unsigned* __restrict__ team_bar, double* __restrict__ team_part, const double* __restrict__ xpM) {
   // em_run converged at an EARLIER iteration: exit.  The flag this launch's own scalar block may
   // set (== stop_step) must not stop a polar-team member that starts late, or its teammates would
   // wait at the team barrier for a member that never comes.
@@ -2122,13 +2118,6 @@ __global__ __launch_bounds__(PPLS_FIN_THREADS) void ppls_finalize_kernel(
     double* gacc = exact_gram ? gout : nullptr;
     double* w2 = work + (isx ? 0 : 2 * (int64_t)p * R);
     double* vs = vstate ? vstate + (isx ? 0 : R * R) : nullptr;
-    // fexp = {F (R x R), G (R x R), flag_X, flag_C}: the polar factor's right factor out = S F when the
-    // Cholesky-QR1 path produced it (flag 1), for the pipelined cross-product iteration
-    // (ppls_xprod_apply_kernel); flag 0 otherwise.  The block's own F slot is passed with its flag at
-    // offset 2 R^2 from it (X: [0, R^2) and flag 2R^2; C: [R^2, 2R^2) and flag 2R^2 + 1).
-    double* fx = fexp ? fexp + (isx ? 0 : R * R) : nullptr;
-    double* ff = fexp ? fexp + 2 * R * R + (isx ? 0 : 1) : nullptr;
-    if (ff && (isx ? b == 0 : b == KX) && tid == 0) *ff = 0.0;
     PplsTeam tm;
     tm.K = isx ? KX : KY;
     tm.rank = isx ? b : b - KX;
@@ -2138,7 +2127,7 @@ __global__ __launch_bounds__(PPLS_FIN_THREADS) void ppls_finalize_kernel(
     tm.tr = tr;
     if (qr || !ppls_block_polar_fast<R, NT>(S, ld, rows, out, ld, ld, stage_lds ? dyn_lds : nullptr, sh,
                                             sm, gacc, vs, tr, tm, (mode & 4) != 0,
-                                            (double)((mode >> 8) & 255), fx, ff)) {
+                                            (double)((mode >> 8) & 255))) {
       if (tm.rank != 0) return;   // the Householder fallback runs on one block
       ppls_block_polar(S, ld, rows, R, out, ld, ld, w2, w2 + (int64_t)rows * R, status, qr);
       if (gacc) {
@@ -2437,7 +2426,7 @@ hipError_t launch_finalize_t(const PplsFinalizeArgs* f, hipStream_t st) {
                      f->N, f->p, f->q, f->ldx, f->ldy, f->Wc, f->Cc, f->sc_cur, f->Wn, f->Cn, f->sc_nxt, f->mom,
                      f->loglik, f->logl_index, f->work, f->status, f->qr, f->mode, f->gram_cur,
                      f->gram_nxt, f->vstate, use, f->trace, f->stop, f->stop_mirror, f->stop_check,
-                     f->stop_step, f->atol, KX, KY, f->team_bar, f->team_part, f->xpM, f->fexp);
+                     f->stop_step, f->atol, KX, KY, f->team_bar, f->team_part, f->xpM);
   return hipGetLastError();
 }
 

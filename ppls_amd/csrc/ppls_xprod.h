@@ -35,16 +35,4 @@ hipError_t ppls_launch_xprod_tile(const double* S, int ldx, int ldy, int r, int 
                                   const double* Cp, const PplsScalars* sc, double* stats, double* M, const int* stop,
                                   int with_gram, hipStream_t st);
 
-// The pipelined iteration (r <= PPLS_XP_PIPE_RMAX; ppls_xprod.hip): which = 0 the pass
-// T = S blockdiag(M[X, :], M[Y, :]) (P x 4r; runs while the finalize computes theta_{i+1}); which = 1
-// the apply M = [T^X K^X | T^Y K^Y] + theta_{i+1}'s X'mu_T, Y'mu_U into stats, with K = {F (r x r),
-// G (r x r), flag_X, flag_C} from the finalize (PplsFinalizeArgs::fexp) -- or, if a flag is 0, the
-// tile kernel's S blockdiag(Wn, Cn) from S.  Same grid as the tile kernel (rows per wave rw <= 4).
-#define PPLS_XP_PIPE_RMAX 10
-// The Gram B'M alone (B = blockdiag(Wp, Cp)), one workgroup per upper-triangle entry, into stats.
-hipError_t ppls_launch_xprod_gram(int ldx, int ldy, int r, const double* Wp, const double* Cp, const double* M,
-                                  double* stats, const int* stop, hipStream_t st);
-hipError_t ppls_launch_xprod_pipe(int which, const double* S, int ldx, int ldy, int r, int rw, const double* Wn,
-                                  const double* Cn, const PplsScalars* sc_cur, const PplsScalars* sc_nxt, double* T,
-                                  const double* K, double* stats, double* M, const int* stop, hipStream_t st);
 }

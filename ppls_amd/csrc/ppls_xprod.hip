@@ -14,8 +14,9 @@
 //                            the finalize does not form it itself (r > 8 or p + q > 6144)
 // Row i of M needs row i of S only (S is symmetric, so rows and columns are interchangeable).
 // Measured and removed: a row-group form without LDS (W, C re-read from L1/L2 per
-// row group: 350 vs 210 us at C5) and a lower-triangle form (half the bytes, but latency-bound tiles
-// plus a partial reduction: not faster at C3 or C5).
+// row group: 350 vs 210 us at C5), a lower-triangle form (half the bytes, but latency-bound tiles
+// plus a partial reduction: not faster at C3 or C5), and a two-stream pipeline running the pass over
+// S of iteration i beside its finalize (cross-queue waits and a 2r-wide pass: slower at C3 and C5).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -180,98 +181,6 @@ __global__ __launch_bounds__(256) void ppls_xprod_tile_kernel(const double* __re
   ppls_xprod_tile_body<R, RW, NT>(S, ldx, ldy, Wp, Cp, sc, stats, M, sB, sm[wave], i0, lane);
 }
 
-// ---- the pipelined iteration.  With W_{i+1} = SX_i F_i (the polar factor:
-// F_i = R1^-1 U V' of the finalize's Cholesky-QR1 path) and SX_i = M_i[X, :] [diag alpha_i;
-// diag beta_i], the next iteration's M_{i+1} = S blockdiag(W_{i+1}, C_{i+1}) equals
-//   [T_i^X K_i^X | T_i^Y K_i^Y],  T_i^X = S[:, X] M_i[X, :],  T_i^Y = S[:, Y] M_i[Y, :]  (P x 2r each),
-//   K_i^X = [diag alpha_i; diag beta_i] F_i,  K_i^Y = [diag gamma_i; diag delta_i] G_i   (2r x r).
-// T_i needs only M_i, so the pass over S (ppls_xprod_pass_kernel) runs WHILE the finalize of
-// iteration i computes F_i, G_i and theta_{i+1}'s scalars; ppls_xprod_apply_kernel then forms
-// M_{i+1} and X'mu_T, Y'mu_U of theta_{i+1} from T_i (P x 4r) in a few microseconds.
-
-// T = S blockdiag(M[X, :], M[Y, :]) (P x 4R column-major: [T^X | T^Y]).
-template <int R, int RW, bool NT>
-__global__ __launch_bounds__(256) void ppls_xprod_pass_kernel(const double* __restrict__ S, int ldx, int ldy,
-                                                              const double* __restrict__ M, double* __restrict__ T,
-                                                              const int* __restrict__ stop) {
-  if (stop && *stop) return;
-  constexpr int RB = 2 * R, R4 = 4 * R;
-  __shared__ double sB[2 * RB * 128];
-  __shared__ double sm[4][RW * R4];
-  const int P = ldx + ldy;
-  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t i0 = ((int64_t)blockIdx.x * 4 + wave) * RW;
-  ppls_xprod_rows<RB, RW, NT>(S, ldx, ldy, M, P, M + ldx, P, i0, sB, sm[wave], lane);
-  __syncthreads();
-  for (int e = lane; e < RW * R4; e += 64) {
-    const int rr = e / R4, b = e - rr * R4;
-    if (i0 + rr < P) T[(int64_t)b * P + i0 + rr] = sm[wave][e];
-  }
-}
-
-// M_{i+1} = [T^X K^X | T^Y K^Y] and theta_{i+1}'s X'mu_T, Y'mu_U for the workgroup's 4 RW rows.
-// K = {F_i (R x R, column-major), G_i, flag_X, flag_C}: the finalize of iteration i sets a flag to
-// 1 when its polar block took the Cholesky-QR1 path (kappa(X'mu_T) <= the polar1 bound, so the
-// products above lose at most ~kappa eps) and exported F; otherwise (Cholesky-QR2, Householder,
-// QR type) the workgroup forms M_{i+1} = S blockdiag(W_{i+1}, C_{i+1}) from S itself, exactly as
-// the tile kernel -- same grid, so either branch covers every row.
-template <int R, int RW, bool NT>
-__global__ __launch_bounds__(256) void ppls_xprod_apply_kernel(const double* __restrict__ S, int ldx, int ldy,
-                                                               const double* __restrict__ Wn,
-                                                               const double* __restrict__ Cn,
-                                                               const PplsScalars* __restrict__ sc_cur,
-                                                               const PplsScalars* __restrict__ sc_nxt,
-                                                               const double* __restrict__ T,
-                                                               const double* __restrict__ K,
-                                                               double* __restrict__ stats, double* __restrict__ M,
-                                                               const int* __restrict__ stop) {
-  if (stop && *stop) return;
-  constexpr int R2 = 2 * R, RR = R * R;
-  __shared__ double sB[2 * R * 128];
-  __shared__ double sm[4][RW * 2 * R];
-  __shared__ double sK[2 * R2 * R];   // K^X (2R x R), then K^Y, column-major
-  const int P = ldx + ldy;
-  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const bool pipe = K[2 * RR] != 0.0 && K[2 * RR + 1] != 0.0;   // uniform over the grid
-  if (!pipe) {
-    const int64_t i0 = ((int64_t)blockIdx.x * 4 + wave) * RW;
-    ppls_xprod_tile_body<R, RW, NT>(S, ldx, ldy, Wn, Cn, sc_nxt, stats, M, sB, sm[wave], i0, lane);
-    return;
-  }
-  for (int e = tid; e < 2 * R2 * R; e += 256) {
-    const int mat = e / (R2 * R), f = e - mat * R2 * R, col = f / R2, b = f - col * R2;
-    const int a = b < R ? b : b - R;   // row a of F (G)
-    const double cf = mat == 0 ? (b < R ? sc_cur->alpha[a] : sc_cur->beta[a])
-                               : (b < R ? sc_cur->gamma[a] : sc_cur->delta[a]);
-    sK[e] = cf * K[mat * RR + col * R + a];
-  }
-  __syncthreads();
-  const int64_t r0 = (int64_t)blockIdx.x * 4 * RW;
-  double* smb = &sm[0][0];   // [4 RW rows][2R] of M_{i+1}
-  for (int e = tid; e < 4 * RW * R2; e += 256) {
-    const int rr = e / R2, col = e - rr * R2;
-    const int64_t i = r0 + rr;
-    if (i >= P) continue;
-    const int mat = col < R ? 0 : 1, k = col - mat * R;
-    const double* t = T + (int64_t)(mat * R2) * P + i;
-    const double* kk = sK + mat * R2 * R + k * R2;
-    double v = 0.0;
-#pragma unroll
-    for (int b = 0; b < R2; ++b) v = fma(t[(int64_t)b * P], kk[b], v);
-    M[(int64_t)col * P + i] = v;
-    smb[e] = v;
-  }
-  __syncthreads();
-  for (int e = tid; e < 4 * RW * R; e += 256) {
-    const int rr = e / R, k = e - rr * R;
-    const int64_t i = r0 + rr;
-    if (i >= P) continue;
-    const double mw = smb[rr * R2 + k], mc = smb[rr * R2 + R + k];
-    if (i < ldx) stats[(int64_t)k * ldx + i] = sc_nxt->alpha[k] * mw + sc_nxt->beta[k] * mc;
-    else stats[(int64_t)R * ldx + (int64_t)k * ldy + (i - ldx)] = sc_nxt->gamma[k] * mw + sc_nxt->delta[k] * mc;
-  }
-}
-
 // Gram entry (a, b), a <= b, of B'M: sum over the rows where column a of B lives (X rows for
 // a < R, Y rows otherwise); written to (a, b) and (b, a).
 __global__ __launch_bounds__(256) void ppls_xprod_gram_kernel(int ldx, int ldy, int R, const double* __restrict__ Wp,
@@ -329,37 +238,6 @@ hipError_t launch_tile_rw(int rw, const double* S, int ldx, int ldy, const doubl
   return hipErrorInvalidValue;
 }
 
-template <int R, int RW>
-hipError_t launch_pipe(int which, const double* S, int ldx, int ldy, const double* Wn, const double* Cn,
-                       const PplsScalars* sc_cur, const PplsScalars* sc_nxt, double* T, const double* K, double* stats,
-                       double* M, const int* stop, hipStream_t st) {
-  const int P = ldx + ldy;
-  const unsigned blocks = (unsigned)((P + 4 * RW - 1) / (4 * RW));
-  const bool nt = 8.0 * P * (double)P > 200.0 * (1 << 20);
-  if (which == 0) {
-    if (nt) hipLaunchKernelGGL((ppls_xprod_pass_kernel<R, RW, true>), dim3(blocks), dim3(256), 0, st, S, ldx, ldy, M, T, stop);
-    else hipLaunchKernelGGL((ppls_xprod_pass_kernel<R, RW, false>), dim3(blocks), dim3(256), 0, st, S, ldx, ldy, M, T, stop);
-  } else {
-    if (nt)
-      hipLaunchKernelGGL((ppls_xprod_apply_kernel<R, RW, true>), dim3(blocks), dim3(256), 0, st, S, ldx, ldy, Wn, Cn,
-                         sc_cur, sc_nxt, T, K, stats, M, stop);
-    else
-      hipLaunchKernelGGL((ppls_xprod_apply_kernel<R, RW, false>), dim3(blocks), dim3(256), 0, st, S, ldx, ldy, Wn, Cn,
-                         sc_cur, sc_nxt, T, K, stats, M, stop);
-  }
-  return hipGetLastError();
-}
-
-template <int R>
-hipError_t launch_pipe_rw(int rw, int which, const double* S, int ldx, int ldy, const double* Wn, const double* Cn,
-                          const PplsScalars* sc_cur, const PplsScalars* sc_nxt, double* T, const double* K,
-                          double* stats, double* M, const int* stop, hipStream_t st) {
-  if (rw == 1) return launch_pipe<R, 1>(which, S, ldx, ldy, Wn, Cn, sc_cur, sc_nxt, T, K, stats, M, stop, st);
-  if (rw == 2) return launch_pipe<R, 2>(which, S, ldx, ldy, Wn, Cn, sc_cur, sc_nxt, T, K, stats, M, stop, st);
-  if (rw == 4) return launch_pipe<R, 4>(which, S, ldx, ldy, Wn, Cn, sc_cur, sc_nxt, T, K, stats, M, stop, st);
-  return hipErrorInvalidValue;
-}
-
 }  // namespace
 
 extern "C" {
@@ -367,31 +245,6 @@ extern "C" {
 int ppls_xprod_tile_rows(int P, int r, int rw_opt, int num_cus) {
   if (rw_opt == 1 || rw_opt == 2 || rw_opt == 4 || (rw_opt == 8 && r <= 8)) return rw_opt;
   return P / 8 >= 2 * num_cus ? 2 : 1;   // two rows per wave while >= 2 workgroups per CU remain
-}
-
-hipError_t ppls_launch_xprod_pipe(int which, const double* S, int ldx, int ldy, int r, int rw, const double* Wn,
-                                  const double* Cn, const PplsScalars* sc_cur, const PplsScalars* sc_nxt, double* T,
-                                  const double* K, double* stats, double* M, const int* stop, hipStream_t st) {
-  if (ldx < 2 || ldy < 2 || (ldx & 1) || (ldy & 1) || r < 1 || r > PPLS_XP_PIPE_RMAX || (which != 0 && which != 1))
-    return hipErrorInvalidValue;
-  if (((uintptr_t)S | (uintptr_t)M | (uintptr_t)T) & 15) return hipErrorInvalidValue;   // 16-B loads
-  if (rw == 8) rw = 4;
-  switch (r) {
-#define PPLS_XPP_CASE(k) \
-    case k: return launch_pipe_rw<k>(rw, which, S, ldx, ldy, Wn, Cn, sc_cur, sc_nxt, T, K, stats, M, stop, st);
-    PPLS_XPP_CASE(1) PPLS_XPP_CASE(2) PPLS_XPP_CASE(3) PPLS_XPP_CASE(4) PPLS_XPP_CASE(5) PPLS_XPP_CASE(6)
-    PPLS_XPP_CASE(7) PPLS_XPP_CASE(8) PPLS_XPP_CASE(9) PPLS_XPP_CASE(10)
-#undef PPLS_XPP_CASE
-    default: return hipErrorInvalidValue;
-  }
-}
-
-hipError_t ppls_launch_xprod_gram(int ldx, int ldy, int r, const double* Wp, const double* Cp, const double* M,
-                                  double* stats, const int* stop, hipStream_t st) {
-  const int R2 = 2 * r;
-  hipLaunchKernelGGL(ppls_xprod_gram_kernel, dim3((unsigned)(R2 * (R2 + 1) / 2)), dim3(256), 0, st, ldx, ldy, r, Wp,
-                     Cp, M, stats, stop);
-  return hipGetLastError();
 }
 
 hipError_t ppls_launch_xprod_tile(const double* S, int ldx, int ldy, int r, int rw, const double* Wp,

@@ -18,7 +18,7 @@ from oracle import ppls_oracle as o
 pytestmark = pytest.mark.gpu
 
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
-DEFAULTS = dict(xprod=0, xprod_rw=0, xprod_fuse=1, xprod_pipe=1, polar1=1, dtype=0)
+DEFAULTS = dict(xprod=0, xprod_rw=0, xprod_fuse=1, polar1=1, dtype=0)
 
 
 @pytest.fixture(scope="module")
@@ -294,24 +294,23 @@ def test_xprod_stats_unit_parity(ctx, rw, n, p, q, r):
     assert np.array_equal(G, G.T)
 
 
-# the pipelined iteration: the pass over S of iteration i runs while the finalize of
-# iteration i runs, M_{i+1} = [T^X K^X | T^Y K^Y]; against the serial cross-product iteration
+# the cross-product iteration through both entry points: em_run and an em_begin / em_iterate session
+# in two calls, against each other and the streaming sweep (shapes with ragged ldx, r = 1 .. 10, fp32)
 @pytest.mark.parametrize("n,p,q,r,dtype", [(900, 300, 260, 5, 0), (500, 1025, 131, 8, 0), (400, 129, 127, 3, 0),
                                            (300, 2, 700, 1, 0), (600, 256, 256, 8, 1), (2000, 33, 7, 2, 0),
                                            (700, 64, 31, 4, 1), (500, 700, 90, 10, 0), (300, 6200, 90, 9, 1)])
-def test_xprod_pipelined_equals_serial(ctx, n, p, q, r, dtype):
+def test_xprod_session_equals_run_and_stream(ctx, n, p, q, r, dtype):
     X, Y, th0 = make_problem(n, p, q, r, seed=5 * n + p + r)
     ctx.set_option("dtype", dtype)
-    ctx.set_option("xprod", 1)
     ctx.set_data(X, Y)
     out = {}
-    for pipe in (0, 1):
-        ctx.set_option("xprod_pipe", pipe)
-        out[pipe] = ctx.em_run(_theta(th0), 30, -np.inf, 0)
-        ctx.em_begin(_theta(th0))   # the em_begin / em_iterate session too
+    for xp in (0, 1):
+        ctx.set_option("xprod", xp)
+        out[xp] = ctx.em_run(_theta(th0), 30, -np.inf, 0)
+        ctx.em_begin(_theta(th0))
         ctx.em_iterate(7)
         ctx.em_iterate(5)
-        out[pipe] = out[pipe] + ctx.em_state()
+        out[xp] = out[xp] + ctx.em_state()
     (e0, l0, x0, _, t0, s0), (e1, l1, x1, _, t1, s1) = out[0], out[1]
     assert len(l0) == len(l1) == 30
     assert _relerr(l1, l0) < 1e-12
@@ -320,26 +319,22 @@ def test_xprod_pipelined_equals_serial(ctx, n, p, q, r, dtype):
     assert _relerr([e1.sigE, e1.sigF, e1.sigH], [e0.sigE, e0.sigF, e0.sigH]) < 1e-10
     assert _relerr(x1.mu_T, x0.mu_T) < 1e-10 and _relerr(x1.Chh, x0.Chh) < 1e-10
     assert len(s0) == len(s1) == 11 and _relerr(s1, s0) < 1e-12
+    assert np.array_equal(s1, l1[:11])   # the session's trace is the run's first 11 entries
     assert np.abs(t1.W - t0.W).max() < 1e-10
 
 
-def test_xprod_pipelined_fallback_and_stop_rule(ctx):
-    """With Cholesky-QR1 refused (polar1 = 0) every finalize takes Cholesky-QR2, exports no F and the
-    apply kernel forms M from S itself (the fallback branch): same iterates.  The device stop rule
-    fires at the same iteration as on the serial path and as the oracle."""
+def test_xprod_stop_rule_both_polar_paths(ctx):
+    """The device stop rule on the cross-product path, with Cholesky-QR1 allowed (polar1 = 1) and
+    refused (every finalize takes Cholesky-QR2): it fires at the same iteration as the oracle's."""
     X, Y, th0 = make_problem(800, 40, 30, 3, seed=5)
     ctx.set_option("xprod", 1)
     ctx.set_data(X, Y)
     res = {}
     for polar1 in (1, 0):
         ctx.set_option("polar1", polar1)
-        for pipe in (0, 1):
-            ctx.set_option("xprod_pipe", pipe)
-            res[polar1, pipe] = ctx.em_run(_theta(th0), 3000, 1e-2, 0)
+        res[polar1] = ctx.em_run(_theta(th0), 3000, 1e-2, 0)
     ref = o.ppls_simult(X, Y, 3, EMsteps=3000, atol=1e-2, theta0=th0)
     for key, (est, ll, _, _) in res.items():
         assert len(ll) == len(ref["loglik"]) < 3000, key
         assert _relerr(ll, ref["loglik"]) < 1e-10, key
         assert np.abs(est.W - ref["estimates"]["W"]).max() < 1e-8, key
-    for polar1 in (1, 0):
-        assert _relerr(res[polar1, 1][1], res[polar1, 0][1]) < 1e-12
