@@ -6,7 +6,8 @@ Data: the bench's synthetic simulC model generated on the device; the fit is a s
 PPLS_simult run (its Expectations feed variances).  Prints one JSON line: Gram kernel time and
 fp64 MFMA TFLOP/s (executed tile flops and the useful n p (p + 1) SYRK flops) against the 78.6 TF
 fp64 matrix peak, and the wall time of the whole variances call (Cxt pass, Gram, per-component
-p x p build + rocSOLVER inverse + copies).
+p x p build + rocSOLVER inverse + copies), after one untimed call, for the Cholesky and the LU
+inverse alternately.
 """
 import argparse
 import json
@@ -29,7 +30,8 @@ def main():
     ap.add_argument("--nsplit", type=int, default=0)
     ap.add_argument("--em-steps", type=int, default=3)
     ap.add_argument("--no-full", action="store_true", help="skip the whole variances call")
-    ap.add_argument("--chol", type=int, default=1, help="1 Cholesky inverse (default), 0 LU")
+    ap.add_argument("--chol", type=int, default=1, help="the arm variances_s reports: 1 Cholesky (default), 0 LU")
+    ap.add_argument("--full-reps", type=int, default=3, help="timed whole calls per arm after one warm-up")
     args = ap.parse_args()
     from ppls_amd import Context
     cfg = CONFIGS[args.config]
@@ -51,13 +53,22 @@ def main():
                fp64_mfma_peak_tflops=FP64_PEAK_TF, mfma_frac=exec_flops / ms / 1e9 / FP64_PEAK_TF,
                tiles=tiles)
     if not args.no_full:
-        ctx.set_option("var_chol", args.chol)
         est, ll, eout, _ = ctx.em_run(th0, args.em_steps, -np.inf, 0, want_eout=True, want_mu=True)
-        t0 = time.perf_counter()
-        W, Bx, V, se, _, _ = ctx.variances(eout.mu_T, eout.Ctt, est.sigE, 0, full=False)
-        out["variances_s"] = time.perf_counter() - t0
-        out["seLoad_median"] = float(np.median(se))
-        out["seLoad_finite"] = bool(np.all(np.isfinite(se)))
+        arms = {"chol": 1, "lu": 0}
+        secs = {k: [] for k in arms}
+        for rep in range(args.full_reps + 1):   # rep 0: warm-up (rocSOLVER/rocBLAS code objects, handle)
+            for k, v in arms.items():
+                ctx.set_option("var_chol", v)
+                t0 = time.perf_counter()
+                W, Bx, V, se, _, _ = ctx.variances(eout.mu_T, eout.Ctt, est.sigE, 0, full=False)
+                if rep:
+                    secs[k].append(time.perf_counter() - t0)
+                out[f"seLoad_median_{k}"] = float(np.median(se))
+                out[f"seLoad_finite_{k}"] = bool(np.all(np.isfinite(se)))
+        ctx.set_option("var_chol", args.chol)
+        for k in arms:
+            out[f"variances_s_{k}"] = secs[k]
+        out["variances_s"] = float(np.median(secs["chol" if args.chol else "lu"]))
     ctx.close()
     print(json.dumps(out), flush=True)
 
