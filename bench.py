@@ -199,15 +199,21 @@ def bench_xprod(ctx, th0, args, barrier, tmax, r, ll_stream, t_stream):
     ctx.em_begin(th0)
     ctx.em_iterate(args.warmup)
     barrier()
-    ctx.set_option("timing", 1)
-    ctx.sweep_timing(reset=True)
     t0 = time.perf_counter()
-    ctx.em_iterate(args.xprod_steps)
+    ctx.em_iterate(args.xprod_steps)   # wall clock: no events between the launches
     barrier()
     dt = tmax(time.perf_counter() - t0)
+    est, ll_x = ctx.em_state()
+    # the tile kernel's average duration: HIP events around every launch of a second, separate run
+    # of the same iterations (events between ~40-us iterations would lengthen the timed one)
+    ctx.em_begin(th0)
+    ctx.em_iterate(args.warmup)
+    ctx.set_option("timing", 1)
+    ctx.sweep_timing(reset=True)
+    ctx.em_iterate(args.xprod_steps)
+    ctx.synchronize()
     ctx.set_option("timing", 0)
     kms, launches = ctx.sweep_timing(reset=True)
-    est, ll_x = ctx.em_state()
     k = min(len(ll_x), len(ll_stream))
     rel = float(np.abs(ll_x[:k] - ll_stream[:k]).max() / np.abs(ll_stream[:k]).max()) if k else None
     t_x = dt / args.xprod_steps

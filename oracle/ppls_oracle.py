@@ -407,27 +407,29 @@ def emstepc_fast(W, C, B, X, Y, sigX, sigY, sigH, sigT, c1, c2, c3):
     sig2X, sig2Y, sig2H, sig2T = sigX * sigX, sigY * sigY, sigH * sigH, sigT * sigT
     N = X.shape[0]
     p, q = W.shape[0], C.shape[0]
-    Xw = X @ W                                                                    # :351
+    Xw = X @ W                                                                    # :353
     Yc = Y @ C
-    mu_T = Xw * sig2T * (-c1 + -c2 * B + 1 / sig2X) + Yc * sig2T * (-c2 + -c3 * B + 1 / sig2Y * B)   # :354
-    Cxt = X.T @ mu_T / N                                                          # :355
-    Ctt = sig2T - sig2T * sig2T * (-c1 - 2 * B * c2 - B * B * (c3 - 1 / sig2Y) + 1 / sig2X) + mu_T @ mu_T / N
+    mu_T = Xw * sig2T * (-c1 + -c2 * B + 1 / sig2X) + Yc * sig2T * (-c2 + -c3 * B + 1 / sig2Y * B)   # :356
+    Cxt = X.T @ mu_T / N                                                          # :357
+    Ctt = (sig2T - sig2T * sig2T * (-c1 - 2 * B * c2 - B * B * (c3 - 1 / sig2Y) + 1 / sig2X)
+           + mu_T @ mu_T / N)                                                     # :358
     v = sig2T * B * B + sig2H
-    mu_U = Xw * (-sig2T * B * c1 + -c2 * v + 1 / sig2X * B * sig2T) + Yc * (-c2 * B * sig2T + -c3 * v + 1 / sig2Y * v)
-    Cyu = Y.T @ mu_U / N                                                          # :360
+    mu_U = (Xw * (-sig2T * B * c1 + -c2 * v + 1 / sig2X * B * sig2T)
+            + Yc * (-c2 * B * sig2T + -c3 * v + 1 / sig2Y * v))                    # :361
+    Cyu = Y.T @ mu_U / N                                                          # :362
     Cuu = v - (-(c1 - 1 / sig2X) * sig2T * sig2T * B * B - 2 * sig2T * B * v * c2 - v ** 2 * (c3 - 1 / sig2Y)) \
-        + mu_U @ mu_U / N                                                         # :361
+        + mu_U @ mu_U / N                                                         # :363
     Cut = sig2T * B - (-sig2T * sig2T * B * (c1 - 1 / sig2X) - sig2T * sig2T * B * B * c2 - sig2T * v * c2
-                       - v * sig2T * B * (c3 - 1 / sig2Y)) + mu_U @ mu_T / N       # :363
+                       - v * sig2T * B * (c3 - 1 / sig2Y)) + mu_U @ mu_T / N       # :365
     xw2, yc2, xy = Xw @ Xw, Yc @ Yc, Xw @ Yc
     Ceetmp = (c1 * c1 * sig2X * sig2X * xw2 + ssq(X) + c2 * c2 * sig2X * sig2X * yc2 - 2 * c1 * sig2X * xw2
-              + 2 * c1 * c2 * sig2X * sig2X * xy - 2 * c2 * sig2X * xy)           # :365-366
-    Cee = sig2X - (-sig2X * sig2X * c1 + p * sig2X) / p + Ceetmp / N / p          # :367
+              + 2 * c1 * c2 * sig2X * sig2X * xy - 2 * c2 * sig2X * xy)           # :367-368
+    Cee = sig2X - (-sig2X * sig2X * c1 + p * sig2X) / p + Ceetmp / N / p          # :369
     Cfftmp = (c3 * c3 * sig2Y * sig2Y * yc2 + ssq(Y) + c2 * c2 * sig2Y * sig2Y * xw2 - 2 * c3 * sig2Y * yc2
-              + 2 * c3 * c2 * sig2Y * sig2Y * xy - 2 * c2 * sig2Y * xy)           # :369-370
-    Cff = sig2Y - (-sig2Y * sig2Y * c3 + q * sig2Y) / q + Cfftmp / N / q          # :371
+              + 2 * c3 * c2 * sig2Y * sig2Y * xy - 2 * c2 * sig2Y * xy)           # :371-372
+    Cff = sig2Y - (-sig2Y * sig2Y * c3 + q * sig2Y) / q + Cfftmp / N / q          # :373
     mh = -c2 * sig2H * Xw - (c3 - 1 / sig2Y) * sig2H * Yc
-    Chh = sig2H - (-sig2H * sig2H * (c3 - 1 / sig2Y)) + mh @ mh / N               # :373
+    Chh = sig2H - (-sig2H * sig2H * (c3 - 1 / sig2Y)) + mh @ mh / N               # :375
     return dict(mu_T=mu_T, mu_U=mu_U, W=Cxt / np.linalg.norm(Cxt), C=Cyu / np.linalg.norm(Cyu),
                 B=Cut / Ctt, sighat=_rsqrt(np.array([Cee, Cff])),
                 siglathat=_rsqrt(np.array([Chh, Ctt])),

@@ -1582,7 +1582,7 @@ double rank1_loglik(const Rank1& t, const double G[4], double ssqX, double ssqY,
 }
 
 // The rank-1 E-step moments and M-step scalars from one sweep's Gram (ppls_rank1_scalars, shared
-// with the device step kernel): the arithmetic of EMstepC_fast (loglC.cpp:354-385) and meta_Estep /
+// with the device step kernel): the arithmetic of EMstepC_fast (loglC.cpp:353-387) and meta_Estep /
 // meta_Mstep (loglC.cpp:399-474).
 void rank1_scalars(const Rank1& t, const double G[4], double ssqX, double ssqY, double N, int p, int q,
                    Rank1* n) {

@@ -1997,67 +1997,94 @@ __device__ __forceinline__ void ppls_stop_test(const double* loglik, int idx, in
 // The cross-product form's Gram B'M (B = blockdiag(W, C), M = S B) on the finalize's scalar block,
 // in the slack of the polar blocks: entries (a, b) of the X rows with a < r, b in [a, 2r)
 // (W'X'XW upper triangle, then W'X'YC) and of the Y rows with a <= b < r (C'Y'YC upper triangle),
-// 2r^2 + r sums; per thread a stride of rows, then ppls_block_sum_t in passes of 64 entries.
-// Written mirrored to sG (LDS, what the moments read) and G (stats' Gram slot).  r <= 8.
+// 2r^2 + r sums, in passes of 64 entries (one pass up to r = 5; 3 at r = 8, which re-read the rows
+// from L2 but keep 64 accumulators per thread instead of 192 -- all of them spilled to scratch):
+// per thread a stride of rows, then ppls_block_sum_t.  Written mirrored to sG (LDS, what the
+// moments read) and G (stats' Gram slot).  r <= 8.
 template <int R, int NT>
 __device__ void ppls_xp_gram_block(const double* __restrict__ M, const double* __restrict__ Wc,
                                    const double* __restrict__ Cc, int ldx, int ldy, double* sG, double* G) {
   constexpr int R2 = 2 * R, NX = R * (R + 1) / 2 + R * R, NE = NX + R * (R + 1) / 2;
   constexpr int NPASS = (NE + 63) / 64;
+  // U rows per thread per batch, all their loads issued before the FMAs: M was just written by the
+  // tile kernel on other XCDs, so every load is a far (MALL) round trip, and one batch of U rows
+  // costs one round trip instead of U.  Rows past the end load the last row with weight 0 (adds
+  // +-0: the sums equal the row-by-row loop's bitwise).
+  constexpr int U = R <= 5 ? 4 : (R == 6 ? 2 : 1);   // larger batches spill beyond r = 5
   __shared__ double sh[(NT / 64) * 64];
   const int P = ldx + ldy, tid = threadIdx.x;
-  double acc[NPASS * 64];
-#pragma unroll
-  for (int e = 0; e < NPASS * 64; ++e) acc[e] = 0.0;
-  for (int i = tid; i < ldx; i += NT) {
-    double w[R], m[R2];
-#pragma unroll
-    for (int a = 0; a < R; ++a) w[a] = Wc[(int64_t)a * ldx + i];
-#pragma unroll
-    for (int b = 0; b < R2; ++b) m[b] = M[(int64_t)b * P + i];
-    int e = 0;
-#pragma unroll
-    for (int a = 0; a < R; ++a)
-#pragma unroll
-      for (int b = a; b < R2; ++b, ++e) acc[e] = fma(w[a], m[b], acc[e]);
-  }
-  for (int i = tid; i < ldy; i += NT) {
-    double cv[R], m[R];
-#pragma unroll
-    for (int a = 0; a < R; ++a) cv[a] = Cc[(int64_t)a * ldy + i];
-#pragma unroll
-    for (int b = 0; b < R; ++b) m[b] = M[(int64_t)(R + b) * P + ldx + i];
-    int e = NX;
-#pragma unroll
-    for (int a = 0; a < R; ++a)
-#pragma unroll
-      for (int b = a; b < R; ++b, ++e) acc[e] = fma(cv[a], m[b], acc[e]);
-  }
 #pragma unroll
   for (int ps = 0; ps < NPASS; ++ps) {
-    double v[64];
+    const int lo = ps * 64;
+    double acc[64];
 #pragma unroll
-    for (int e = 0; e < 64; ++e) v[e] = acc[ps * 64 + e];
-    ppls_block_sum_t<64, NT / 64>(v, sh);
+    for (int e = 0; e < 64; ++e) acc[e] = 0.0;
+    if (lo < NX) {
+      for (int i0 = tid; i0 < ldx; i0 += U * NT) {
+        double w[U][R], m[U][R2];
 #pragma unroll
-    for (int e = 0; e < 64; ++e) acc[ps * 64 + e] = v[e];
-  }
-  if (tid == 0) {
-    int e = 0;
+        for (int u = 0; u < U; ++u) {
+          const int i = min(i0 + u * NT, ldx - 1);
 #pragma unroll
-    for (int a = 0; a < R; ++a)
+          for (int a = 0; a < R; ++a) w[u][a] = Wc[(int64_t)a * ldx + i];
 #pragma unroll
-      for (int b = a; b < R2; ++b, ++e) {
-        sG[b * R2 + a] = sG[a * R2 + b] = acc[e];
-        G[b * R2 + a] = G[a * R2 + b] = acc[e];
+          for (int b = 0; b < R2; ++b) m[u][b] = M[(int64_t)b * P + i];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const bool ok = i0 + u * NT < ldx;
+          int e = 0;
+#pragma unroll
+          for (int a = 0; a < R; ++a)
+#pragma unroll
+            for (int b = a; b < R2; ++b, ++e)
+              if (e >= lo && e < lo + 64) acc[e - lo] = fma(ok ? w[u][a] : 0.0, m[u][b], acc[e - lo]);
+        }
       }
+    }
+    if (lo + 64 > NX) {
+      for (int i0 = tid; i0 < ldy; i0 += U * NT) {
+        double cv[U][R], m[U][R];
 #pragma unroll
-    for (int a = 0; a < R; ++a)
+        for (int u = 0; u < U; ++u) {
+          const int i = min(i0 + u * NT, ldy - 1);
 #pragma unroll
-      for (int b = a; b < R; ++b, ++e) {
-        sG[(R + b) * R2 + R + a] = sG[(R + a) * R2 + R + b] = acc[e];
-        G[(R + b) * R2 + R + a] = G[(R + a) * R2 + R + b] = acc[e];
+          for (int a = 0; a < R; ++a) cv[u][a] = Cc[(int64_t)a * ldy + i];
+#pragma unroll
+          for (int b = 0; b < R; ++b) m[u][b] = M[(int64_t)(R + b) * P + ldx + i];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const bool ok = i0 + u * NT < ldy;
+          int e = NX;
+#pragma unroll
+          for (int a = 0; a < R; ++a)
+#pragma unroll
+            for (int b = a; b < R; ++b, ++e)
+              if (e >= lo && e < lo + 64) acc[e - lo] = fma(ok ? cv[u][a] : 0.0, m[u][b], acc[e - lo]);
+        }
       }
+    }
+    ppls_block_sum_t<64, NT / 64>(acc, sh);
+    if (tid == 0) {
+      int e = 0;
+#pragma unroll
+      for (int a = 0; a < R; ++a)
+#pragma unroll
+        for (int b = a; b < R2; ++b, ++e)
+          if (e >= lo && e < lo + 64) {
+            sG[b * R2 + a] = sG[a * R2 + b] = acc[e - lo];
+            G[b * R2 + a] = G[a * R2 + b] = acc[e - lo];
+          }
+#pragma unroll
+      for (int a = 0; a < R; ++a)
+#pragma unroll
+        for (int b = a; b < R; ++b, ++e)
+          if (e >= lo && e < lo + 64) {
+            sG[(R + b) * R2 + R + a] = sG[(R + a) * R2 + R + b] = acc[e - lo];
+            G[(R + b) * R2 + R + a] = G[(R + a) * R2 + R + b] = acc[e - lo];
+          }
+    }
   }
   __syncthreads();
 }
@@ -2264,7 +2291,7 @@ __global__ __launch_bounds__(256) void ppls_finalize_generic_kernel(
 }
 
 // ============================================================================ initialiser step
-// Loading update of one rank-1 EM step (EMstepC_fast, src/loglC.cpp:355, :383): t = S (the sweep's
+// Loading update of one rank-1 EM step (EMstepC_fast, src/loglC.cpp:357, :385): t = S (the sweep's
 // X'mu_T over the undeflated data), deflated t = P_{m-1}..P_0 t (= Xc'mu_T), t /= N, normalised --
 // or the fixed loading of an fconstraint -- then the next sweep's weight dst = P_0..P_{m-1} t
 // (so the sweep over X computes Xc t).  Every thread keeps its own indices i = tid + k * nt, so

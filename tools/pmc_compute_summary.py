@@ -44,7 +44,7 @@ def load(path, sub):
     for r in csv.DictReader(open(path)):
         if sub in r["Kernel_Name"]:
             acc[r["Counter_Name"]][r["Dispatch_Id"]] += float(r["Counter_Value"])
-            names.add(r["Kernel_Name"].split("(")[0])
+            names.add(r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0])
     return {k: sum(v.values()) / len(v) for k, v in acc.items()}, {k: len(v) for k, v in acc.items()}, names
 
 
@@ -63,7 +63,7 @@ def main():
     durations = {}
     if trace:
         for r in csv.DictReader(open(trace)):
-            durations[r["Name"].split("(")[0]] = float(r["AverageNs"])
+            durations[r["Name"].replace("(anonymous namespace)::", "").split("(")[0]] = float(r["AverageNs"])
     for sub in subs:
         c = {}
         n = {}
@@ -93,13 +93,20 @@ def main():
             d.update(duration_ms=t * 1e3, effective_clock_ghz=cyc / t / 1e9,
                      fp64_valu_tflops=flops_valu / t / 1e12, fp64_mfma_tflops=flops_mfma / t / 1e12,
                      fp64_total_frac_of_78_6=(flops_valu + flops_mfma) / t / 78.6e12)
+            if cyc / t > 2.4e9:   # a short dispatch: the counter window is longer than the kernel
+                c24 = t * 2.4e9
+                d.update(effective_clock_ghz=None,
+                         note="GRBM_GUI_ACTIVE spans more than the kernel (short dispatch): busy fractions "
+                              "against duration x 2.4 GHz given as *_at_2p4ghz (lower bounds on the clock)",
+                         mfma_busy_at_2p4ghz=c.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0) / (1024.0 * c24),
+                         valu_busy_at_2p4ghz=c.get("SQ_ACTIVE_INST_VALU", 0.0) / (256.0 * c24))
         out["kernels"][sub] = d
     path = os.path.join(ROOT, "profiles", f"pmc_compute_{workload}.json")
     with open(path, "w") as f:
         json.dump(out, f, indent=1)
     for sub, d in out["kernels"].items():
         print(sub, f"mfma_busy {d['mfma_busy']:.3f} valu_busy {d['valu_busy']:.3f}",
-              {k: round(v, 3) for k, v in d.items() if k.startswith(("fp64_", "effective", "duration"))})
+              {k: (round(v, 3) if v is not None else None) for k, v in d.items() if k.startswith(("fp64_", "effective", "duration", "valu_busy_at"))})
     print(path)
 
 
