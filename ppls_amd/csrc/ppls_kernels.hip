@@ -2003,7 +2003,8 @@ __device__ __forceinline__ void ppls_stop_test(const double* loglik, int idx, in
 // moments read) and G (stats' Gram slot).  r <= 8.
 template <int R, int NT>
 __device__ void ppls_xp_gram_block(const double* __restrict__ M, const double* __restrict__ Wc,
-                                   const double* __restrict__ Cc, int ldx, int ldy, double* sG, double* G) {
+                                   const double* __restrict__ Cc, int ldx, int ldy, double* sG, double* G,
+                                   long long* tr) {
   constexpr int R2 = 2 * R, NX = R * (R + 1) / 2 + R * R, NE = NX + R * (R + 1) / 2;
   constexpr int NPASS = (NE + 63) / 64;
   // U rows per thread per batch, all their loads issued before the FMAs: M was just written by the
@@ -2042,6 +2043,7 @@ __device__ void ppls_xp_gram_block(const double* __restrict__ M, const double* _
         }
       }
     }
+    if (ps == 0) ppls_stamp(tr, 5);   // X rows of the first pass
     if (lo + 64 > NX) {
       for (int i0 = tid; i0 < ldy; i0 += U * NT) {
         double cv[U][R], m[U][R];
@@ -2065,7 +2067,9 @@ __device__ void ppls_xp_gram_block(const double* __restrict__ M, const double* _
         }
       }
     }
+    if (ps == 0) ppls_stamp(tr, 6);   // rows of the first pass summed per thread
     ppls_block_sum_t<64, NT / 64>(acc, sh);
+    if (ps == 0) ppls_stamp(tr, 7);
     if (tid == 0) {
       int e = 0;
 #pragma unroll
@@ -2171,7 +2175,8 @@ __global__ __launch_bounds__(PPLS_FIN_THREADS) void ppls_finalize_kernel(
   if (!(mode & 2)) return;
   // cross-product form: the Gram of [XW YC] = B'M from M = S B (the polar blocks run meanwhile)
   if constexpr (R <= 8)
-    if (xpM) ppls_xp_gram_block<R, NT>(xpM, Wc, Cc, ldx, ldy, s_G, const_cast<double*>(G));
+    if (xpM) ppls_xp_gram_block<R, NT>(xpM, Wc, Cc, ldx, ldy, s_G, const_cast<double*>(G), tr);
+  ppls_stamp(tr, 8);
   // stage theta's scalars, the Gram and W'W, C'C in LDS (all threads)
   {
     const double* src = (const double*)sc_cur;

@@ -1,7 +1,11 @@
 """HBM/MALL traffic of the cross-product tile kernel per launch from the rocprofv3 PMC passes
 written by tools/profile.sh (bench.py's xprod section runs in the same profiled command).
 
-    python tools/pmc_xprod_summary.py <tag> <config> [note]
+    python tools/pmc_xprod_summary.py <tag> <config> [note] [--bytes B]
+
+--bytes: S's bytes (8 P^2 with P the padded ldx + ldy, as ppls_xprod_info reports it; default from
+p and q rounded to even, which is exact for the split sweep's 16-B rows but not for the panel
+sweep's padded ones: C5 has P = 10,240 + 512).
 
 Reads gpurun_out/prof_<tag>/pmc_{FETCH_SIZE,WRITE_SIZE}/run_counter_collection.csv and the kernel
 trace's stats (average duration), writes profiles/pmc_xprod_<config>_dp1.json.  gfx950 correction
@@ -25,13 +29,19 @@ def avg_us(stats, sub):
 
 
 def main():
-    tag, config = sys.argv[1], sys.argv[2]
-    note = sys.argv[3] if len(sys.argv) > 3 else ""
+    args = list(sys.argv[1:])
+    nbytes = None
+    if "--bytes" in args:
+        i = args.index("--bytes")
+        nbytes = float(args[i + 1])
+        del args[i:i + 2]
+    tag, config = args[0], args[1]
+    note = args[2] if len(args) > 2 else ""
     import bench
     cfg = bench.CONFIGS[config]
     ldx, ldy = (cfg["p"] + 1) // 2 * 2, (cfg["q"] + 1) // 2 * 2
     P = ldx + ldy
-    alg = 8.0 * P * P
+    alg = nbytes if nbytes else 8.0 * P * P
     base = os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
     names, n, fetch = per_launch(os.path.join(base, "pmc_FETCH_SIZE", "run_counter_collection.csv"), "FETCH_SIZE",
                                  ("xprod_tile",))
