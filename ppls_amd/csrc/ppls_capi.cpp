@@ -117,7 +117,6 @@ struct ppls_ctx {
   // formed once per data set, then every statistics step reads S instead of X and Y
   int xprod = 0;            // option "xprod": 0 stream X, Y (default), 1 cross-products, -1 auto (cost model)
   int xprod_rw = 0;         // option "xprod_rw": rows of S per wave of the tile kernel (0 auto)
-  int xprod_waves = 4;      // option "xprod_waves": waves per tile-kernel workgroup (4; 8, 16 with rw <= 2)
   bool xp_ready = false;    // S holds the (all-reduced) cross-products of the current data
   bool xp_active = false;   // statistics steps of the current run read S
   bool xp_pending_gram = false;   // the last statistics step left the Gram B'M to the next finalize
@@ -733,7 +732,7 @@ int xprod_stats(ppls_ctx* c, int r, int slot, bool fuse = false) {
   if (e0) HIPCHK(c, hipEventRecord(e0, c->stream));
   const int rw = ppls_xprod_tile_rows(P, r, c->xprod_rw, c->num_cus);
   const bool defer = fuse && c->xprod_fuse && r <= 8 && P <= 6144;
-  HIPCHK(c, ppls_launch_xprod_tile(c->xp_S, c->ldx, c->ldy, r, rw, rw <= 2 ? c->xprod_waves : 4, c->W[slot], c->C[slot], c->sc[slot], c->stats,
+  HIPCHK(c, ppls_launch_xprod_tile(c->xp_S, c->ldx, c->ldy, r, rw, c->W[slot], c->C[slot], c->sc[slot], c->stats,
                                    c->xp_M, c->sweep_stop, defer ? 0 : 1, c->stream));
   c->xp_pending_gram = defer;
   if (e1) HIPCHK(c, hipEventRecord(e1, c->stream));
@@ -1039,9 +1038,6 @@ int ppls_set_option(ppls_ctx* c, const char* key, int64_t value) {
     c->xprod_fuse = value ? 1 : 0;
   } else if (!strcmp(key, "var_chol")) {
     c->var_chol = value ? 1 : 0;
-  } else if (!strcmp(key, "xprod_waves")) {
-    if (value != 4 && value != 8 && value != 16) return fail(c, PPLS_E_ARG, "xprod_waves must be 4, 8 or 16");
-    c->xprod_waves = (int)value;
   } else if (!strcmp(key, "xprod_rw")) {
     if (value != 0 && value != 1 && value != 2 && value != 4 && value != 8)
       return fail(c, PPLS_E_ARG, "xprod_rw must be 0, 1, 2, 4 or 8");

@@ -27,12 +27,11 @@ int ppls_xprod_tile_rows(int P, int r, int rw_opt, int num_cus);
 // One iteration's statistics from S (P x P row-major, P = ldx + ldy, symmetric) and theta = (Wp, Cp,
 // sc): stats = [X'mu_T (ldx x r) | Y'mu_U (ldy x r) | Gram (2r x 2r)], the layout the sweeps'
 // reduction writes.  The tile kernel (rw rows of S per wave) streams S once and writes the X'mu_T,
-// Y'mu_U rows and M = S B (P x 2r column-major, scratch) with `waves` (4; 8 or 16 for rw <= 2) rows-
-// of-waves per workgroup sharing each staged B tile; the Gram kernel forms B'M, one workgroup
+// Y'mu_U rows and M = S B (P x 2r column-major, scratch); the Gram kernel forms B'M, one workgroup
 // per entry (fixed-order sums: deterministic) -- unless with_gram = 0, when the finalize that
 // follows forms it (PplsFinalizeArgs::xpM, r <= 8).
 // stop: the em_run stop flag (both kernels exit if it is set) or nullptr.
-hipError_t ppls_launch_xprod_tile(const double* S, int ldx, int ldy, int r, int rw, int waves, const double* Wp,
+hipError_t ppls_launch_xprod_tile(const double* S, int ldx, int ldy, int r, int rw, const double* Wp,
                                   const double* Cp, const PplsScalars* sc, double* stats, double* M, const int* stop,
                                   int with_gram, hipStream_t st);
 

@@ -38,12 +38,12 @@ constexpr int ppls_rs_left(int m, int l) { return l == 6 ? m : (m == 1 ? 1 : ppl
 // C cost ~R / (4 RW) of S's traffic from L2.  S tiles stream through a register
 // ring PPLS_XP_DEPTH tiles ahead (enough bytes in flight per CU to cover HBM/MALL latency: one
 // 128-column tile is only 1 KB per wave and row), B one tile ahead through LDS; one barrier per tile.
-template <int R, int RW, bool NT, int NTH>
+template <int R, int RW, bool NT>
 __device__ __forceinline__ void ppls_xprod_tile_phase(const double* const (&srow)[RW], const double* __restrict__ Bsrc,
                                                       int ldb, int width, int soff, double (&acc)[RW * R + 1],
                                                       double* __restrict__ sB, int lane) {
   typedef double d2v __attribute__((ext_vector_type(2)));
-  constexpr int NB = (R * 64 + NTH - 1) / NTH;   // 16-B B loads per thread and tile
+  constexpr int NB = (R * 64 + 255) / 256;   // 16-B B loads per thread and tile
   constexpr int D = PPLS_XP_DEPTH;           // S tiles in flight per wave (register ring)
   const int tid = threadIdx.x;
   const int ntile = (width + 127) >> 7;
@@ -64,14 +64,14 @@ __device__ __forceinline__ void ppls_xprod_tile_phase(const double* const (&srow
   auto ld_b = [&](int n) {   // tile n: this thread's share of the 128 x R values of B
 #pragma unroll
     for (int v = 0; v < NB; ++v) {
-      const int e = tid + NTH * v, t = e >> 6, cb = (n << 7) + 2 * (e & 63);
+      const int e = tid + 256 * v, t = e >> 6, cb = (n << 7) + 2 * (e & 63);
       bn[v] = (e < R * 64 && cb < width) ? *(const d2v*)(Bsrc + (int64_t)t * ldb + cb) : d2v{0.0, 0.0};
     }
   };
   auto st_b = [&](int buf) {
 #pragma unroll
     for (int v = 0; v < NB; ++v) {
-      const int e = tid + NTH * v;
+      const int e = tid + 256 * v;
       if (e < R * 64) ((d2v*)sB)[buf * R * 64 + e] = bn[v];
     }
   };
@@ -108,7 +108,7 @@ __device__ __forceinline__ void ppls_xprod_tile_phase(const double* const (&srow
 // lives on the X columns of S with leading dimension ldbx, By on the Y columns): on return
 // smw[rr * 2 RB + b] = S[i0 + rr, X] Bx[:, b] and smw[rr * 2 RB + RB + b] = S[i0 + rr, Y] By[:, b]
 // (this wave's slice of LDS; the caller synchronises before reading it).
-template <int RB, int RW, bool NT, int NTH>
+template <int RB, int RW, bool NT>
 __device__ __forceinline__ void ppls_xprod_rows(const double* __restrict__ S, int ldx, int ldy,
                                                 const double* __restrict__ Bx, int ldbx,
                                                 const double* __restrict__ By, int ldby, int64_t i0,
@@ -124,8 +124,8 @@ __device__ __forceinline__ void ppls_xprod_rows(const double* __restrict__ S, in
     double acc[NV + 1];
 #pragma unroll
     for (int v = 0; v <= NV; ++v) acc[v] = 0.0;
-    if (ph == 0) ppls_xprod_tile_phase<RB, RW, NT, NTH>(srow, Bx, ldbx, ldx, 0, acc, sB, lane);
-    else ppls_xprod_tile_phase<RB, RW, NT, NTH>(srow, By, ldby, ldy, ldx, acc, sB, lane);
+    if (ph == 0) ppls_xprod_tile_phase<RB, RW, NT>(srow, Bx, ldbx, ldx, 0, acc, sB, lane);
+    else ppls_xprod_tile_phase<RB, RW, NT>(srow, By, ldby, ldy, ldx, acc, sB, lane);
     int idx = 0, nreal = 0;
     bool canon = true;
     ppls_rs<NV, 0, NV + 1>(acc, lane, idx, canon, nreal);
@@ -142,7 +142,7 @@ __device__ __forceinline__ void ppls_xprod_rows(const double* __restrict__ S, in
 
 // M = S blockdiag(W, C) for a wave's RW rows, then X'mu_T / Y'mu_U of those rows (the statistics
 // step of an iteration from S: EM_W_multi.R:691-694, :732-733).
-template <int R, int RW, bool NT, int NTH>
+template <int R, int RW, bool NT>
 __device__ __forceinline__ void ppls_xprod_tile_body(const double* __restrict__ S, int ldx, int ldy,
                                                      const double* __restrict__ Wp, const double* __restrict__ Cp,
                                                      const PplsScalars* __restrict__ sc, double* __restrict__ stats,
@@ -150,7 +150,7 @@ __device__ __forceinline__ void ppls_xprod_tile_body(const double* __restrict__ 
                                                      double* __restrict__ smw, int64_t i0, int lane) {
   constexpr int R2 = 2 * R;
   const int P = ldx + ldy;
-  ppls_xprod_rows<R, RW, NT, NTH>(S, ldx, ldy, Wp, ldx, Cp, ldy, i0, sB, smw, lane);
+  ppls_xprod_rows<R, RW, NT>(S, ldx, ldy, Wp, ldx, Cp, ldy, i0, sB, smw, lane);
   __syncthreads();
   for (int e = lane; e < RW * R2; e += 64) {
     const int rr = e / R2, b = e - rr * R2;
@@ -166,8 +166,8 @@ __device__ __forceinline__ void ppls_xprod_tile_body(const double* __restrict__ 
   }
 }
 
-template <int R, int RW, bool NT, int NWV>
-__global__ __launch_bounds__(64 * NWV) void ppls_xprod_tile_kernel(const double* __restrict__ S, int ldx, int ldy,
+template <int R, int RW, bool NT>
+__global__ __launch_bounds__(256) void ppls_xprod_tile_kernel(const double* __restrict__ S, int ldx, int ldy,
                                                               const double* __restrict__ Wp,
                                                               const double* __restrict__ Cp,
                                                               const PplsScalars* __restrict__ sc,
@@ -175,10 +175,10 @@ __global__ __launch_bounds__(64 * NWV) void ppls_xprod_tile_kernel(const double*
                                                               const int* __restrict__ stop) {
   if (stop && *stop) return;   // em_run converged at an earlier iteration
   __shared__ double sB[2 * R * 128];
-  __shared__ double sm[NWV][RW * 2 * R];
+  __shared__ double sm[4][RW * 2 * R];
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t i0 = ((int64_t)blockIdx.x * NWV + wave) * RW;   // this wave's first row of S
-  ppls_xprod_tile_body<R, RW, NT, 64 * NWV>(S, ldx, ldy, Wp, Cp, sc, stats, M, sB, sm[wave], i0, lane);
+  const int64_t i0 = ((int64_t)blockIdx.x * 4 + wave) * RW;   // this wave's first row of S
+  ppls_xprod_tile_body<R, RW, NT>(S, ldx, ldy, Wp, Cp, sc, stats, M, sB, sm[wave], i0, lane);
 }
 
 // Gram entry (a, b), a <= b, of B'M: sum over the rows where column a of B lives (X rows for
@@ -213,39 +213,28 @@ __global__ __launch_bounds__(256) void ppls_xprod_gram_kernel(int ldx, int ldy, 
   }
 }
 
-template <int R, int RW, int NWV>
+template <int R, int RW>
 hipError_t launch_tile(const double* S, int ldx, int ldy, const double* Wp, const double* Cp, const PplsScalars* sc,
                        double* stats, double* M, const int* stop, hipStream_t st) {
   const int P = ldx + ldy;
-  const unsigned blocks = (unsigned)((P + NWV * RW - 1) / (NWV * RW));
+  const unsigned blocks = (unsigned)((P + 4 * RW - 1) / (4 * RW));
   if (8.0 * P * (double)P > 200.0 * (1 << 20))   // S beyond the Infinity Cache: non-temporal loads
-    hipLaunchKernelGGL((ppls_xprod_tile_kernel<R, RW, true, NWV>), dim3(blocks), dim3(64 * NWV), 0, st, S, ldx, ldy,
-                       Wp, Cp, sc, stats, M, stop);
+    hipLaunchKernelGGL((ppls_xprod_tile_kernel<R, RW, true>), dim3(blocks), dim3(256), 0, st, S, ldx, ldy, Wp, Cp, sc,
+                       stats, M, stop);
   else
-    hipLaunchKernelGGL((ppls_xprod_tile_kernel<R, RW, false, NWV>), dim3(blocks), dim3(64 * NWV), 0, st, S, ldx, ldy,
-                       Wp, Cp, sc, stats, M, stop);
+    hipLaunchKernelGGL((ppls_xprod_tile_kernel<R, RW, false>), dim3(blocks), dim3(256), 0, st, S, ldx, ldy, Wp, Cp,
+                       sc, stats, M, stop);
   return hipGetLastError();
 }
 
 template <int R>
-hipError_t launch_tile_rw(int rw, int waves, const double* S, int ldx, int ldy, const double* Wp, const double* Cp,
+hipError_t launch_tile_rw(int rw, const double* S, int ldx, int ldy, const double* Wp, const double* Cp,
                           const PplsScalars* sc, double* stats, double* M, const int* stop, hipStream_t st) {
-  if (waves == 8) {
-    if (rw == 1) return launch_tile<R, 1, 8>(S, ldx, ldy, Wp, Cp, sc, stats, M, stop, st);
-    if (rw == 2) return launch_tile<R, 2, 8>(S, ldx, ldy, Wp, Cp, sc, stats, M, stop, st);
-    return hipErrorInvalidValue;
-  }
-  if (waves == 16) {
-    if (rw == 1) return launch_tile<R, 1, 16>(S, ldx, ldy, Wp, Cp, sc, stats, M, stop, st);
-    if (rw == 2) return launch_tile<R, 2, 16>(S, ldx, ldy, Wp, Cp, sc, stats, M, stop, st);
-    return hipErrorInvalidValue;
-  }
-  if (waves != 4) return hipErrorInvalidValue;
-  if (rw == 1) return launch_tile<R, 1, 4>(S, ldx, ldy, Wp, Cp, sc, stats, M, stop, st);
-  if (rw == 2) return launch_tile<R, 2, 4>(S, ldx, ldy, Wp, Cp, sc, stats, M, stop, st);
-  if (rw == 4) return launch_tile<R, 4, 4>(S, ldx, ldy, Wp, Cp, sc, stats, M, stop, st);   // one phase's RW r accumulators live
+  if (rw == 1) return launch_tile<R, 1>(S, ldx, ldy, Wp, Cp, sc, stats, M, stop, st);
+  if (rw == 2) return launch_tile<R, 2>(S, ldx, ldy, Wp, Cp, sc, stats, M, stop, st);
+  if (rw == 4) return launch_tile<R, 4>(S, ldx, ldy, Wp, Cp, sc, stats, M, stop, st);   // one phase's RW r accumulators live
   if constexpr (R <= 8)
-    if (rw == 8) return launch_tile<R, 8, 4>(S, ldx, ldy, Wp, Cp, sc, stats, M, stop, st);
+    if (rw == 8) return launch_tile<R, 8>(S, ldx, ldy, Wp, Cp, sc, stats, M, stop, st);
   return hipErrorInvalidValue;
 }
 
@@ -258,7 +247,7 @@ int ppls_xprod_tile_rows(int P, int r, int rw_opt, int num_cus) {
   return P / 8 >= 2 * num_cus ? 2 : 1;   // two rows per wave while >= 2 workgroups per CU remain
 }
 
-hipError_t ppls_launch_xprod_tile(const double* S, int ldx, int ldy, int r, int rw, int waves, const double* Wp,
+hipError_t ppls_launch_xprod_tile(const double* S, int ldx, int ldy, int r, int rw, const double* Wp,
                                   const double* Cp, const PplsScalars* sc, double* stats, double* M, const int* stop,
                                   int with_gram, hipStream_t st) {
   if (ldx < 2 || ldy < 2 || (ldx & 1) || (ldy & 1) || r < 1 || r > PPLS_RMAX) return hipErrorInvalidValue;
@@ -266,7 +255,7 @@ hipError_t ppls_launch_xprod_tile(const double* S, int ldx, int ldy, int r, int 
   hipError_t e;
   switch (r) {
 #define PPLS_XP_CASE(k) \
-    case k: e = launch_tile_rw<k>(rw, waves, S, ldx, ldy, Wp, Cp, sc, stats, M, stop, st); break;
+    case k: e = launch_tile_rw<k>(rw, S, ldx, ldy, Wp, Cp, sc, stats, M, stop, st); break;
     PPLS_XP_CASE(1) PPLS_XP_CASE(2) PPLS_XP_CASE(3) PPLS_XP_CASE(4) PPLS_XP_CASE(5) PPLS_XP_CASE(6)
     PPLS_XP_CASE(7) PPLS_XP_CASE(8) PPLS_XP_CASE(9) PPLS_XP_CASE(10) PPLS_XP_CASE(11) PPLS_XP_CASE(12)
     PPLS_XP_CASE(13) PPLS_XP_CASE(14) PPLS_XP_CASE(15) PPLS_XP_CASE(16)
