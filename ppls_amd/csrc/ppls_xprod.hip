@@ -26,6 +26,9 @@
 #ifndef PPLS_XP_DEPTH
 #define PPLS_XP_DEPTH 2   // 128-column tiles of S in flight per wave in the row-tile kernel (2, 3, 4, 6: same within 1 %, 6 slower at r = 10)
 #endif
+#ifndef PPLS_XP_TPB
+#define PPLS_XP_TPB 1     // 128-column sub-tiles per staged B tile and workgroup barrier
+#endif
 
 namespace {
 
@@ -43,36 +46,42 @@ __device__ __forceinline__ void ppls_xprod_tile_phase(const double* const (&srow
                                                       int ldb, int width, int soff, double (&acc)[RW * R + 1],
                                                       double* __restrict__ sB, int lane) {
   typedef double d2v __attribute__((ext_vector_type(2)));
-  constexpr int NB = (R * 64 + 255) / 256;   // 16-B B loads per thread and tile
+  constexpr int TP = PPLS_XP_TPB;            // 128-column sub-tiles per staged tile (one barrier each)
+  constexpr int TV = TP * R * 64;            // 16-B values of B per staged tile
+  constexpr int NB = (TV + 255) / 256;       // 16-B B loads per thread and tile
   constexpr int D = PPLS_XP_DEPTH;           // S tiles in flight per wave (register ring)
   const int tid = threadIdx.x;
-  const int ntile = (width + 127) >> 7;
+  const int ntile = (width + 128 * TP - 1) / (128 * TP);
   if (ntile == 0) return;
-  d2v bn[NB], ring[D][RW];
-  auto ld_s = [&](int n, d2v (&dst)[RW]) {   // tile n: S values of this lane's two columns
-    const int c = (n << 7) + 2 * lane;
+  d2v bn[NB], ring[D][RW][TP];
+  auto ld_s = [&](int n, d2v (&dst)[RW][TP]) {   // tile n: S values of this lane's two columns per sub-tile
 #pragma unroll
-    for (int rr = 0; rr < RW; ++rr) {
-      if (c < width) {
-        if constexpr (NT) dst[rr] = __builtin_nontemporal_load((const d2v*)(srow[rr] + soff + c));
-        else dst[rr] = *(const d2v*)(srow[rr] + soff + c);
-      } else {
-        dst[rr] = d2v{0.0, 0.0};
+    for (int sp = 0; sp < TP; ++sp) {
+      const int c = (n * TP + sp) * 128 + 2 * lane;
+#pragma unroll
+      for (int rr = 0; rr < RW; ++rr) {
+        if (c < width) {
+          if constexpr (NT) dst[rr][sp] = __builtin_nontemporal_load((const d2v*)(srow[rr] + soff + c));
+          else dst[rr][sp] = *(const d2v*)(srow[rr] + soff + c);
+        } else {
+          dst[rr][sp] = d2v{0.0, 0.0};
+        }
       }
     }
   };
-  auto ld_b = [&](int n) {   // tile n: this thread's share of the 128 x R values of B
+  auto ld_b = [&](int n) {   // tile n: this thread's share of the TP x 128 x R values of B
 #pragma unroll
     for (int v = 0; v < NB; ++v) {
-      const int e = tid + 256 * v, t = e >> 6, cb = (n << 7) + 2 * (e & 63);
-      bn[v] = (e < R * 64 && cb < width) ? *(const d2v*)(Bsrc + (int64_t)t * ldb + cb) : d2v{0.0, 0.0};
+      const int e = tid + 256 * v, sp = e / (R * 64), f = e - sp * R * 64, t = f >> 6;
+      const int cb = (n * TP + sp) * 128 + 2 * (f & 63);
+      bn[v] = (e < TV && cb < width) ? *(const d2v*)(Bsrc + (int64_t)t * ldb + cb) : d2v{0.0, 0.0};
     }
   };
   auto st_b = [&](int buf) {
 #pragma unroll
     for (int v = 0; v < NB; ++v) {
       const int e = tid + 256 * v;
-      if (e < R * 64) ((d2v*)sB)[buf * R * 64 + e] = bn[v];
+      if (e < TV) ((d2v*)sB)[buf * TV + e] = bn[v];
     }
   };
 #pragma unroll
@@ -90,13 +99,16 @@ __device__ __forceinline__ void ppls_xprod_tile_phase(const double* const (&srow
       // leaves the S loads issued after it in flight
       if (n + 1 < ntile) ld_b(n + 1);
       if (n + D - 1 < ntile) ld_s(n + D - 1, ring[(u + D - 1) % D]);
-      const d2v* b = (const d2v*)sB + (n & 1) * R * 64 + lane;
 #pragma unroll
-      for (int t = 0; t < R; ++t) {
-        const d2v bv = b[t * 64];
+      for (int sp = 0; sp < TP; ++sp) {   // sub-tiles in column order: the sums equal TP = 1's
+        const d2v* b = (const d2v*)sB + (n & 1) * TV + sp * R * 64 + lane;
 #pragma unroll
-        for (int rr = 0; rr < RW; ++rr)
-          acc[rr * R + t] = fma(ring[u][rr].y, bv.y, fma(ring[u][rr].x, bv.x, acc[rr * R + t]));
+        for (int t = 0; t < R; ++t) {
+          const d2v bv = b[t * 64];
+#pragma unroll
+          for (int rr = 0; rr < RW; ++rr)
+            acc[rr * R + t] = fma(ring[u][rr][sp].y, bv.y, fma(ring[u][rr][sp].x, bv.x, acc[rr * R + t]));
+        }
       }
       if (n + 1 < ntile) st_b((n + 1) & 1);
       __syncthreads();
@@ -174,7 +186,7 @@ __global__ __launch_bounds__(256) void ppls_xprod_tile_kernel(const double* __re
                                                               double* __restrict__ stats, double* __restrict__ M,
                                                               const int* __restrict__ stop) {
   if (stop && *stop) return;   // em_run converged at an earlier iteration
-  __shared__ double sB[2 * R * 128];
+  __shared__ double sB[2 * R * 128 * PPLS_XP_TPB];
   __shared__ double sm[4][RW * 2 * R];
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t i0 = ((int64_t)blockIdx.x * 4 + wave) * RW;   // this wave's first row of S
