@@ -27,10 +27,14 @@
 #define PPLS_XP_DEPTH 2   // 128-column tiles of S in flight per wave in the row-tile kernel (2, 3, 4, 6: same within 1 %, 6 slower at r = 10)
 #endif
 #ifndef PPLS_XP_TPB
-#define PPLS_XP_TPB 1     // 128-column sub-tiles per staged B tile and workgroup barrier
+#define PPLS_XP_TPB 0     // 128-column sub-tiles per staged B tile and workgroup barrier (0: ppls_xp_tpb)
 #endif
 
 namespace {
+
+// Sub-tiles per staged B tile (one workgroup barrier each): 2 for r <= 5 (C3: tile 23.5 -> 22.9 us),
+// else 1 (C5, r = 10: 2 is 6 % slower, 4 is slower at C3; profiles/r4_xprod_tpb_ab.txt).
+constexpr int ppls_xp_tpb(int r) { return PPLS_XP_TPB > 0 ? PPLS_XP_TPB : (r <= 5 ? 2 : 1); }
 
 // Values a lane holds after ppls_rs's six butterfly levels on M values (M > 64: several).
 constexpr int ppls_rs_left(int m, int l) { return l == 6 ? m : (m == 1 ? 1 : ppls_rs_left((m + 1) / 2, l + 1)); }
@@ -40,13 +44,14 @@ constexpr int ppls_rs_left(int m, int l) { return l == 6 ? m : (m == 1 ? 1 : ppl
 // X columns, C on Y columns) are staged in LDS once per workgroup and read by all its rows, so W and
 // C cost ~R / (4 RW) of S's traffic from L2.  S tiles stream through a register
 // ring PPLS_XP_DEPTH tiles ahead (enough bytes in flight per CU to cover HBM/MALL latency: one
-// 128-column tile is only 1 KB per wave and row), B one tile ahead through LDS; one barrier per tile.
+// 128-column tile is only 1 KB per wave and row), B one tile ahead through LDS; one barrier per
+// staged tile of ppls_xp_tpb(R) 128-column sub-tiles.
 template <int R, int RW, bool NT>
 __device__ __forceinline__ void ppls_xprod_tile_phase(const double* const (&srow)[RW], const double* __restrict__ Bsrc,
                                                       int ldb, int width, int soff, double (&acc)[RW * R + 1],
                                                       double* __restrict__ sB, int lane) {
   typedef double d2v __attribute__((ext_vector_type(2)));
-  constexpr int TP = PPLS_XP_TPB;            // 128-column sub-tiles per staged tile (one barrier each)
+  constexpr int TP = ppls_xp_tpb(R);         // 128-column sub-tiles per staged tile (one barrier each)
   constexpr int TV = TP * R * 64;            // 16-B values of B per staged tile
   constexpr int NB = (TV + 255) / 256;       // 16-B B loads per thread and tile
   constexpr int D = PPLS_XP_DEPTH;           // S tiles in flight per wave (register ring)
@@ -186,7 +191,7 @@ __global__ __launch_bounds__(256) void ppls_xprod_tile_kernel(const double* __re
                                                               double* __restrict__ stats, double* __restrict__ M,
                                                               const int* __restrict__ stop) {
   if (stop && *stop) return;   // em_run converged at an earlier iteration
-  __shared__ double sB[2 * R * 128 * PPLS_XP_TPB];
+  __shared__ double sB[2 * R * 128 * ppls_xp_tpb(R)];
   __shared__ double sm[4][RW * 2 * R];
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t i0 = ((int64_t)blockIdx.x * 4 + wave) * RW;   // this wave's first row of S
