@@ -704,14 +704,17 @@ int xprod_setup(ppls_ctx* c) {
 // issues the same collectives.  Size gate: S and at most one S-sized set of Gram partials, 16 P^2
 // bytes, within PPLS_XPROD_MAX_BYTES (64 GiB, below a quarter of an MI355X's 288 GB: P <= 65,536).
 #define PPLS_XPROD_MAX_BYTES (64.0 * 1024 * 1024 * 1024)
-bool xprod_choose(ppls_ctx* c, int max_steps) {
+bool xprod_choose(ppls_ctx* c, int max_steps, int r) {
   if (c->xprod == 0) return false;
   const double P = (double)(c->ldx + c->ldy);
   if (16.0 * P * P > PPLS_XPROD_MAX_BYTES) return false;
   if (c->xprod == 1) return true;
   const double n = (double)((c->n_total + c->nranks - 1) / c->nranks);
   const double esz = c->dtype ? 4.0 : 8.0;
-  const double t_sweep = esz * n * P / 6.5e12 + 5e-6;
+  // the split sweep reads X, Y once; the panel sweep (wide p, r > 8, fp32 storage) twice -- also
+  // at r = 1 (C5's initialiser steps: 7.3 ms each, like its r = 10 iterations)
+  const bool split = c->sweep_mode != 3 && !c->dtype && ppls_split_supported(r, c->ldx, c->ldy) > 0;
+  const double t_sweep = (split ? 1.0 : 2.0) * esz * n * P / 6.5e12 + 5e-6;
   const double t_pass = 8.0 * P * P / 6.5e12 + 5e-6;
   const double t_setup = c->xp_ready ? 0.0 : n * P * P / 55e12 + (c->nranks > 1 ? 16.0 * P * P / 100e9 : 0.0);
   return ((double)max_steps + 1.0) * (t_sweep - t_pass) > t_setup;
@@ -1424,7 +1427,7 @@ int ppls_em_run(ppls_ctx* c, ppls_theta* th, int r, int max_steps, double atol, 
   const bool want_mu = eout && (eout->mu_T || eout->mu_U);
   const bool do_check = !(atol == -INFINITY);   // atol = -Inf: the stop rule never fires
   // statistics from the cross-products S (option xprod; formed here if needed, outside the loop)
-  c->xp_active = c->seg_rows < 0 && xprod_choose(c, max_steps);
+  c->xp_active = c->seg_rows < 0 && xprod_choose(c, max_steps, r);
   if (c->xp_active && (rc = xprod_setup(c))) { c->xp_active = false; return rc; }
   // The stop rule (EM_W_multi.R:792) runs on the device: the finalize that sees
   // logl[i] - logl[i-1] < atol sets a flag, and every later kernel of the run exits at once, so the
@@ -1749,7 +1752,7 @@ int ppls_ppls_ex(ppls_ctx* c, int a, int max_steps, double atol, int crit_abs, c
   if ((rc = ensure_r(c, 1, max_steps))) return rc;
   // the rank-1 steps' statistics from the cross-products S (option xprod): the sweep's weights are
   // the deflated P_0..P_{m-1} w, so S blockdiag(P w, P c) gives exactly the sweep's X'mu_T and Gram
-  c->xp_active = c->seg_rows < 0 && xprod_choose(c, a * max_steps);
+  c->xp_active = c->seg_rows < 0 && xprod_choose(c, a * max_steps, 1);
   if (c->xp_active && (rc = xprod_setup(c))) { c->xp_active = false; return rc; }
   struct XpGuard {
     ppls_ctx* c;
@@ -2373,7 +2376,7 @@ int ppls_em_begin(ppls_ctx* c, const ppls_theta* th, int r) {
   c->em_r = r;
   c->em_cur = 0;
   c->em_iter = 0;
-  c->xp_active = c->seg_rows < 0 && xprod_choose(c, 1 << 16);
+  c->xp_active = c->seg_rows < 0 && xprod_choose(c, 1 << 16, r);
   if (c->xp_active && (rc = xprod_setup(c))) { c->xp_active = false; return rc; }
   c->em_active = true;
   return PPLS_OK;
