@@ -175,14 +175,10 @@ int dalloc(ppls_ctx* c, T** p, size_t count) {
     *p = nullptr;
   }
   if (count == 0) count = 1;
-  size_t bytes = count * sizeof(T);
-#ifdef PPLS_ALLOC_ROUND   // experiment builds: every buffer a whole number of PPLS_ALLOC_ROUND bytes
-  bytes = (bytes + PPLS_ALLOC_ROUND - 1) / PPLS_ALLOC_ROUND * PPLS_ALLOC_ROUND;
-#endif
-  hipError_t e = hipMalloc((void**)p, bytes);
+  hipError_t e = hipMalloc((void**)p, count * sizeof(T));
   if (e != hipSuccess) {
     *p = nullptr;
-    return fail(c, PPLS_E_NOMEM, "hipMalloc(%zu bytes): %s", bytes, hipGetErrorString(e));
+    return fail(c, PPLS_E_NOMEM, "hipMalloc(%zu bytes): %s", count * sizeof(T), hipGetErrorString(e));
   }
   return PPLS_OK;
 }
