@@ -1647,8 +1647,11 @@ __device__ bool ppls_block_polar_fast(const double* __restrict__ S, int64_t lds,
     }
     if (fst) {
       load_vprev();
+      ppls_stamp(tr, 6);
       ppls_matmul_wave<R, false>(sT, sV, sA);                // sA = R1 V (sT keeps R1)
+      ppls_stamp(tr, 7);
       ppls_jacobi_wave<R>(sA, sV);
+      ppls_stamp(tr, 8);
       if (lane < R) {
         double nrm = 0.0;
 #pragma unroll
