@@ -615,10 +615,9 @@ int finalize(ppls_ctx* c, int r, int cur, int nxt, int logl_index, int type, int
   f.vstate = c->vstate;
   if (!c->team_bar) {
     int rc;
-    if ((rc = dalloc(c, &c->team_bar, 16)) ||
-        (rc = dalloc(c, &c->team_part, (size_t)2 * 3 * PPLS_TEAM_MAX * 64 + (size_t)PPLS_GRAM_HELPERS_MAX * 192)))
+    if ((rc = dalloc(c, &c->team_bar, 8)) || (rc = dalloc(c, &c->team_part, (size_t)2 * 3 * PPLS_TEAM_MAX * 64)))
       return rc;
-    HIPCHK(c, hipMemsetAsync(c->team_bar, 0, 16 * sizeof(unsigned), c->stream));
+    HIPCHK(c, hipMemsetAsync(c->team_bar, 0, 8 * sizeof(unsigned), c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
   }
   f.team_bar = c->team_bar;
@@ -772,7 +771,7 @@ int check_status(ppls_ctx* c) {
   int st = 0;
   HIPCHK(c, hipMemcpy(&st, c->status, sizeof st, hipMemcpyDeviceToHost));
   if (st == -7) {   // a polar team member waited too long: clear the team counters, report
-    if (c->team_bar) HIPCHK(c, hipMemset(c->team_bar, 0, 16 * sizeof(unsigned)));
+    if (c->team_bar) HIPCHK(c, hipMemset(c->team_bar, 0, 8 * sizeof(unsigned)));
     return fail(c, PPLS_E_HIP, "finalize polar team barrier timed out (status -7)");
   }
   if (st != 0) return fail(c, PPLS_E_NUMERIC, "rank-deficient X'mu_T or Y'mu_U in the M-step (status %d)", st);

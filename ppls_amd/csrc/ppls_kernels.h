@@ -70,7 +70,7 @@ struct PplsFinalizeArgs {
   int stop_check, stop_step;
   double atol;
   unsigned* team_bar;    // wide-p polar teams: 8 zero-initialised counters, or nullptr (one block each)
-  double* team_part;     // 2 x 3 x PPLS_TEAM_MAX x 64 doubles (+ PPLS_GRAM_HELPERS_MAX x 192: Gram slots)
+  double* team_part;     // 2 x 3 x PPLS_TEAM_MAX x 64 doubles
   int team_rows;         // rows of S per team member (0: PPLS_TEAM_ROWS)
   const double* xpM;     // cross-product form (ppls_xprod.hip): M = S blockdiag(Wc, Cc), (ldx + ldy) x 2r
                          // column-major, or nullptr; when set, the scalar block forms the Gram B'M itself
@@ -79,7 +79,6 @@ struct PplsFinalizeArgs {
 
 #define PPLS_TEAM_ROWS 2048   // rows of S per polar team member (tools/team_rows_ab.py: p = 2000 in one block is 4 us faster than a team of 2; C5 equal at 1024 and 2048)
 #define PPLS_TEAM_MAX 32
-#define PPLS_GRAM_HELPERS_MAX 8   // finalize blocks forming the cross-product Gram's row slices
 // finalize polar: Cholesky-QR1 (one pass, no second team barrier) when ||R1||_F ||R1^-1||_F <= this x r
 // (a bound on kappa_2(X'mu); ||R||_F ||R^-1||_F >= r for any R)
 #define PPLS_POLAR1_KAPPA 2.0

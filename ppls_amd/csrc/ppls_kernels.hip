@@ -1490,6 +1490,15 @@ __device__ void ppls_team_sum(const PplsTeam& tm, int phase, double (&vals)[NG],
   __syncthreads();
 }
 
+// Polar factor U V' of the p x R matrix S (column-major, ld lds) by Cholesky-QR2 (S = Q1 R1,
+// Q1 = Q R2) and one-sided Jacobi on T = R2 R1 = U_T Sigma V': U V' = Q1 R2^-1 U_T V'.  Three
+// block passes: the first stages S into LDS (Sl, p*R doubles; nullptr = re-read from global); the
+// second forms Q1 = S R1^-1 (kept in Sl, else in out) and its Gram; the last
+// writes out = Q1 P, P = R2^-1 U_T V', and, if gram_out != nullptr, the Gram out'out the next
+// iteration's scalar update needs.  All R x R algebra runs on wave 0 in LDS; the Jacobi is
+// warm-started from vstate (the previous iteration's V; nullptr = identity).  sm: >= 2 R^2
+// doubles of LDS.  Returns false when S is numerically rank deficient (a Cholesky pivot fails or
+// sigma_min < 1e-14 sigma_max); the caller then falls back to Householder (which reports it).
 // Polar factor U V' of a nonsingular R x R matrix by the scaled Newton iteration
 // X <- (zeta X + X^-T / zeta) / 2, zeta = (||X^-1||_F / ||X||_F)^(1/2) while the step is large, then
 // unscaled (quadratic) steps; X^-T = X (X'X)^-1 through the packed Cholesky helpers.  One thread, in
@@ -1555,15 +1564,6 @@ __device__ __forceinline__ int ppls_polar_newton(double (&X)[R][R]) {
   return 30;
 }
 
-// Polar factor U V' of the p x R matrix S (column-major, ld lds) by Cholesky-QR2 (S = Q1 R1,
-// Q1 = Q R2) and one-sided Jacobi on T = R2 R1 = U_T Sigma V': U V' = Q1 R2^-1 U_T V'.  Three
-// block passes: the first stages S into LDS (Sl, p*R doubles; nullptr = re-read from global); the
-// second forms Q1 = S R1^-1 (kept in Sl, else in out) and its Gram; the last
-// writes out = Q1 P, P = R2^-1 U_T V', and, if gram_out != nullptr, the Gram out'out the next
-// iteration's scalar update needs.  All R x R algebra runs on wave 0 in LDS; the Jacobi is
-// warm-started from vstate (the previous iteration's V; nullptr = identity).  sm: >= 2 R^2
-// doubles of LDS.  Returns false when S is numerically rank deficient (a Cholesky pivot fails or
-// sigma_min < 1e-14 sigma_max); the caller then falls back to Householder (which reports it).
 #ifndef PPLS_REG_RMAX
 #define PPLS_REG_RMAX 10   // the polar's Cholesky factors and inverses by one thread in registers up to this R
 #endif
@@ -1690,8 +1690,7 @@ __device__ bool ppls_block_polar_fast(const double* __restrict__ S, int64_t lds,
   };
   // Cholesky-QR1 fast path (polar1): when kappa(S) = kappa(R1) is small, Q1 = S R1^-1 is already
   // orthonormal to O(eps kappa^2) (~1e-14), so pass 2, its team barrier and chol(G2) are skipped:
-  // polar(R1) = U_T V' (by scaled Newton in registers for R <= PPLS_NEWTON_RMAX, else the warm-
-  // started Jacobi on T = R1 = U_T Sigma V'), out = S F, F = R1^-1 U_T V'.  The test is the bound
+  // T = R1 = U_T Sigma V' by the Jacobi, out = S F, F = R1^-1 U_T V'.  The test is the bound
   // kappa_2(R1) <= ||R1||_F ||R1^-1||_F <= kbound (option polar1_kappa; default min(8 R, 40): the
   // loss of orthogonality ~ eps kappa^2 stays <= 1e-13; no Jacobi is spent on a matrix
   // that then takes the Cholesky-QR2 path).  Every member decides on the bitwise-identical G1, so
@@ -2086,186 +2085,101 @@ __device__ __forceinline__ void ppls_stop_test(const double* loglik, int idx, in
   }
 }
 
-// The cross-product form's Gram B'M (B = blockdiag(W, C), M = S B): entries (a, b) of the X rows
-// with a < r, b in [a, 2r) (W'X'XW upper triangle, then W'X'YC) and of the Y rows with a <= b < r
-// (C'Y'YC upper triangle), 2r^2 + r sums, in passes of 64 entries (one pass up to r = 5; 3 at r = 8,
-// which re-read the rows from L2 but keep 64 accumulators per thread).  Formed in the finalize
-// while the polar blocks run: by PplsFinalizeArgs' Gram helper blocks over row slices (each a
-// partial per entry into team_part, then one arrival on team_bar[8]), summed by the scalar block in
-// slice order; or, for small p + q, by the scalar block alone.  r <= 8.
-//
-// One pass's per-thread sums over X rows [x0, x1) and Y rows [y0, y1): batches of UX X rows and UY
-// Y rows per thread with every load of a batch issued before the first FMA (M was just written by
-// the tile kernel on other XCDs: each batch is one far round trip).  Rows past a range's end load
-// its last row with weight 0 (adds +-0).
-template <int R, int NT, int UX, int UY>
-__device__ __forceinline__ void ppls_xp_gram_acc(const double* __restrict__ M, const double* __restrict__ Wc,
-                                                 const double* __restrict__ Cc, int ldx, int ldy, int x0, int x1,
-                                                 int y0, int y1, int lo, double (&acc)[64]) {
-  constexpr int R2 = 2 * R, NX = R * (R + 1) / 2 + R * R;
-  const int P = ldx + ldy, tid = threadIdx.x;
-  const bool doX = lo < NX, doY = lo + 64 > NX;
-#pragma unroll
-  for (int e = 0; e < 64; ++e) acc[e] = 0.0;
-  for (int k = 0;; ++k) {
-    const int bx = x0 + k * UX * NT, by = y0 + k * UY * NT;   // uniform over the block
-    const bool mx = doX && bx < x1, my = doY && by < y1;
-    if (!mx && !my) break;
-    double w[UX][R], m[UX][R2], cv[UY][R], n[UY][R];
-    if (mx) {
-#pragma unroll
-      for (int u = 0; u < UX; ++u) {
-        const int i = min(bx + u * NT + tid, x1 - 1);
-#pragma unroll
-        for (int a = 0; a < R; ++a) w[u][a] = Wc[(int64_t)a * ldx + i];
-#pragma unroll
-        for (int c = 0; c < R2; ++c) m[u][c] = M[(int64_t)c * P + i];
-      }
-    }
-    if (my) {
-#pragma unroll
-      for (int u = 0; u < UY; ++u) {
-        const int i = min(by + u * NT + tid, y1 - 1);
-#pragma unroll
-        for (int a = 0; a < R; ++a) cv[u][a] = Cc[(int64_t)a * ldy + i];
-#pragma unroll
-        for (int c = 0; c < R; ++c) n[u][c] = M[(int64_t)(R + c) * P + ldx + i];
-      }
-    }
-    if (mx) {
-#pragma unroll
-      for (int u = 0; u < UX; ++u) {
-        const bool ok = bx + u * NT + tid < x1;
-        int e = 0;
-#pragma unroll
-        for (int a = 0; a < R; ++a)
-#pragma unroll
-          for (int c = a; c < R2; ++c, ++e)
-            if (e >= lo && e < lo + 64) acc[e - lo] = fma(ok ? w[u][a] : 0.0, m[u][c], acc[e - lo]);
-      }
-    }
-    if (my) {
-#pragma unroll
-      for (int u = 0; u < UY; ++u) {
-        const bool ok = by + u * NT + tid < y1;
-        int e = NX;
-#pragma unroll
-        for (int a = 0; a < R; ++a)
-#pragma unroll
-          for (int c = a; c < R; ++c, ++e)
-            if (e >= lo && e < lo + 64) acc[e - lo] = fma(ok ? cv[u][a] : 0.0, n[u][c], acc[e - lo]);
-      }
-    }
-  }
-}
-
-// Thread 0: entries [lo, lo + n) of the Gram's enumeration, v[e - lo], to their two (mirrored)
-// positions in the 2r x 2r column-major Gram (compile-time enumeration).
-template <int R, typename V>
-__device__ __forceinline__ void ppls_xp_gram_put(int lo, int n, const V& v, double* sG, double* G) {
-  constexpr int R2 = 2 * R;
-  int e = 0;
-#pragma unroll
-  for (int a = 0; a < R; ++a)
-#pragma unroll
-    for (int c = a; c < R2; ++c, ++e)
-      if (e >= lo && e < lo + n) {
-        sG[c * R2 + a] = sG[a * R2 + c] = v[e - lo];
-        G[c * R2 + a] = G[a * R2 + c] = v[e - lo];
-      }
-#pragma unroll
-  for (int a = 0; a < R; ++a)
-#pragma unroll
-    for (int c = a; c < R; ++c, ++e)
-      if (e >= lo && e < lo + n) {
-        sG[(R + c) * R2 + R + a] = sG[(R + a) * R2 + R + c] = v[e - lo];
-        G[(R + c) * R2 + R + a] = G[(R + a) * R2 + R + c] = v[e - lo];
-      }
-}
-
-// Rows per thread and batch of the Gram's row passes (larger batches spill beyond r = 5).
-template <int R>
-struct PplsXpGramU {
-  static constexpr int HX = R <= 5 ? 2 : 1;   // helper blocks: X rows, Y rows per batch
-  static constexpr int SX = R <= 5 ? 2 : 1;   // the scalar block alone
-};
-
-// A Gram helper block: the block sums of its row slice into slot (NPASS x 64 doubles), then one
-// arrival on bar (release).  x0..y1: the slice.
-template <int R, int NT>
-__device__ void ppls_xp_gram_helper(const double* __restrict__ M, const double* __restrict__ Wc,
-                                    const double* __restrict__ Cc, int ldx, int ldy, int x0, int x1, int y0, int y1,
-                                    double* __restrict__ slot, unsigned* bar) {
-  constexpr int NE = R * (R + 1) / 2 + R * R + R * (R + 1) / 2, NPASS = (NE + 63) / 64;
-  constexpr int U = PplsXpGramU<R>::HX;
-  __shared__ double sh[(NT / 64) * 64];
-  const int tid = threadIdx.x;
-#pragma unroll
-  for (int ps = 0; ps < NPASS; ++ps) {
-    double acc[64];
-    ppls_xp_gram_acc<R, NT, U, U>(M, Wc, Cc, ldx, ldy, x0, x1, y0, y1, ps * 64, acc);
-    ppls_block_sum_t<64, NT / 64>(acc, sh);
-    if (tid < 64) {
-#pragma unroll
-      for (int e = 0; e < 64; ++e)
-        if (tid == e) slot[ps * 64 + e] = acc[e];
-    }
-  }
-  __syncthreads();
-  if (tid == 0) {
-    __threadfence();   // release the slot
-    atomicAdd(bar, 1u);
-  }
-}
-
-// The scalar block's Gram: from nh helper slots (stride NPASS x 64, summed in slice order), or by
-// itself over all rows (nh = 0).  Written mirrored to sG (LDS, what the moments read) and G (stats'
-// Gram slot).
+// The cross-product form's Gram B'M (B = blockdiag(W, C), M = S B) on the finalize's scalar block,
+// in the slack of the polar blocks: entries (a, b) of the X rows with a < r, b in [a, 2r)
+// (W'X'XW upper triangle, then W'X'YC) and of the Y rows with a <= b < r (C'Y'YC upper triangle),
+// 2r^2 + r sums, in passes of 64 entries (one pass up to r = 5; 3 at r = 8, which re-read the rows
+// from L2 but keep 64 accumulators per thread instead of 192 -- all of them spilled to scratch):
+// per thread a stride of rows, then ppls_block_sum_t.  Written mirrored to sG (LDS, what the
+// moments read) and G (stats' Gram slot).  r <= 8.
 template <int R, int NT>
 __device__ void ppls_xp_gram_block(const double* __restrict__ M, const double* __restrict__ Wc,
                                    const double* __restrict__ Cc, int ldx, int ldy, double* sG, double* G,
-                                   int nh, const double* __restrict__ slots, unsigned* bar, int* status,
                                    long long* tr) {
-  constexpr int NE = R * (R + 1) / 2 + R * R + R * (R + 1) / 2, NPASS = (NE + 63) / 64;
-  constexpr int U = PplsXpGramU<R>::SX;
+  constexpr int R2 = 2 * R, NX = R * (R + 1) / 2 + R * R, NE = NX + R * (R + 1) / 2;
+  constexpr int NPASS = (NE + 63) / 64;
+  // U rows per thread per batch, all their loads issued before the FMAs: M was just written by the
+  // tile kernel on other XCDs, so every load is a far (MALL) round trip, and one batch of U rows
+  // costs one round trip instead of U.  Rows past the end load the last row with weight 0 (adds
+  // +-0: the sums equal the row-by-row loop's bitwise).
+  constexpr int U = R <= 5 ? 4 : (R == 6 ? 2 : 1);   // larger batches spill beyond r = 5
   __shared__ double sh[(NT / 64) * 64];
-  const int tid = threadIdx.x;
-  if (nh > 0) {
-    __syncthreads();
-    if (tid == 0) {
-      long spins = 0;
-      while (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)nh) {
-        if (++spins > (1L << 21)) {
-          atomicExch(status, -7);
-          break;
-        }
-        __builtin_amdgcn_s_sleep(2);
-      }
-      ppls_stamp(tr, 6);
-      __threadfence();            // acquire the helpers' slots
-      atomicExch(bar, 0u);        // every helper has arrived: reset for the next launch
-    }
-    __syncthreads();
-    __shared__ double sE[NPASS * 64];
-    for (int e = tid; e < NE; e += NT) {
-      double t = 0.0;
-      for (int h = 0; h < nh; ++h) t += __builtin_nontemporal_load(slots + (int64_t)h * NPASS * 64 + e);
-      sE[e] = t;
-    }
-    __syncthreads();
-    if (tid == 0) ppls_xp_gram_put<R>(0, NE, sE, sG, G);
-    ppls_stamp(tr, 7);
-    __syncthreads();
-    return;
-  }
+  const int P = ldx + ldy, tid = threadIdx.x;
 #pragma unroll
   for (int ps = 0; ps < NPASS; ++ps) {
+    const int lo = ps * 64;
     double acc[64];
-    ppls_xp_gram_acc<R, NT, U, U>(M, Wc, Cc, ldx, ldy, 0, ldx, 0, ldy, ps * 64, acc);
+#pragma unroll
+    for (int e = 0; e < 64; ++e) acc[e] = 0.0;
+    if (lo < NX) {
+      for (int i0 = tid; i0 < ldx; i0 += U * NT) {
+        double w[U][R], m[U][R2];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int i = min(i0 + u * NT, ldx - 1);
+#pragma unroll
+          for (int a = 0; a < R; ++a) w[u][a] = Wc[(int64_t)a * ldx + i];
+#pragma unroll
+          for (int b = 0; b < R2; ++b) m[u][b] = M[(int64_t)b * P + i];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const bool ok = i0 + u * NT < ldx;
+          int e = 0;
+#pragma unroll
+          for (int a = 0; a < R; ++a)
+#pragma unroll
+            for (int b = a; b < R2; ++b, ++e)
+              if (e >= lo && e < lo + 64) acc[e - lo] = fma(ok ? w[u][a] : 0.0, m[u][b], acc[e - lo]);
+        }
+      }
+    }
+    if (ps == 0) ppls_stamp(tr, 5);   // X rows of the first pass
+    if (lo + 64 > NX) {
+      for (int i0 = tid; i0 < ldy; i0 += U * NT) {
+        double cv[U][R], m[U][R];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int i = min(i0 + u * NT, ldy - 1);
+#pragma unroll
+          for (int a = 0; a < R; ++a) cv[u][a] = Cc[(int64_t)a * ldy + i];
+#pragma unroll
+          for (int b = 0; b < R; ++b) m[u][b] = M[(int64_t)(R + b) * P + ldx + i];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const bool ok = i0 + u * NT < ldy;
+          int e = NX;
+#pragma unroll
+          for (int a = 0; a < R; ++a)
+#pragma unroll
+            for (int b = a; b < R; ++b, ++e)
+              if (e >= lo && e < lo + 64) acc[e - lo] = fma(ok ? cv[u][a] : 0.0, m[u][b], acc[e - lo]);
+        }
+      }
+    }
     if (ps == 0) ppls_stamp(tr, 6);   // rows of the first pass summed per thread
     ppls_block_sum_t<64, NT / 64>(acc, sh);
     if (ps == 0) ppls_stamp(tr, 7);
-    if (tid == 0) ppls_xp_gram_put<R>(ps * 64, 64, acc, sG, G);
+    if (tid == 0) {
+      int e = 0;
+#pragma unroll
+      for (int a = 0; a < R; ++a)
+#pragma unroll
+        for (int b = a; b < R2; ++b, ++e)
+          if (e >= lo && e < lo + 64) {
+            sG[b * R2 + a] = sG[a * R2 + b] = acc[e - lo];
+            G[b * R2 + a] = G[a * R2 + b] = acc[e - lo];
+          }
+#pragma unroll
+      for (int a = 0; a < R; ++a)
+#pragma unroll
+        for (int b = a; b < R; ++b, ++e)
+          if (e >= lo && e < lo + 64) {
+            sG[(R + b) * R2 + R + a] = sG[(R + a) * R2 + R + b] = acc[e - lo];
+            G[(R + b) * R2 + R + a] = G[(R + a) * R2 + R + b] = acc[e - lo];
+          }
+    }
   }
   __syncthreads();
 }
@@ -2287,8 +2201,7 @@ __global__ __launch_bounds__(PPLS_FIN_THREADS) void ppls_finalize_kernel(
     const double* __restrict__ gram_cur, double* __restrict__ gram_nxt, double* __restrict__ vstate,
     int stage_lds, long long* __restrict__ trace,
     int* __restrict__ stop, int* __restrict__ stop_mirror, int stop_check, int stop_step, double atol,
-    int KX, int KY, unsigned* __restrict__ team_bar, double* __restrict__ team_part, const double* __restrict__ xpM,
-    int NGH) {
+    int KX, int KY, unsigned* __restrict__ team_bar, double* __restrict__ team_part, const double* __restrict__ xpM) {
   // em_run converged at an EARLIER iteration: exit.  The flag this launch's own scalar block may
   // set (== stop_step) must not stop a polar-team member that starts late, or its teammates would
   // wait at the team barrier for a member that never comes.
@@ -2306,21 +2219,7 @@ __global__ __launch_bounds__(PPLS_FIN_THREADS) void ppls_finalize_kernel(
   const double* G = SY + (int64_t)R * ldy;
   const int tid = threadIdx.x;
   const int b = blockIdx.x;
-  // blocks [0, KX): the team computing W_next; [KX, KX + KY): C_next; block KX + KY: scalars;
-  // then NGH helpers forming row slices of the cross-product Gram for the scalar block
-  double* gslots = team_part + (int64_t)2 * 3 * PPLS_TEAM_MAX * 64;
-  if (b > KX + KY) {
-    if constexpr (R <= 8) {
-      if (!(mode & 2) || !xpM) return;
-      const int h = b - KX - KY - 1;
-      const int x0 = (int)((int64_t)ldx * h / NGH), x1 = (int)((int64_t)ldx * (h + 1) / NGH);
-      const int y0 = (int)((int64_t)ldy * h / NGH), y1 = (int)((int64_t)ldy * (h + 1) / NGH);
-      constexpr int NE = R * (R + 1) / 2 + R * R + R * (R + 1) / 2, NPASS = (NE + 63) / 64;
-      ppls_xp_gram_helper<R, PPLS_FIN_THREADS>(xpM, Wc, Cc, ldx, ldy, x0, x1, y0, y1,
-                                               gslots + (int64_t)h * NPASS * 64, team_bar + 8);
-    }
-    return;
-  }
+  // blocks [0, KX): the team computing W_next; [KX, KX + KY): C_next; the last block: scalars
   const int slot = b < KX ? 0 : b < KX + KY ? 1 : 2;
   const bool lead = b == 0 || b == KX || b == KX + KY;   // member 0 of its team / the scalar block
   long long* tr = (trace && lead) ? trace + 16 * slot : nullptr;
@@ -2367,8 +2266,7 @@ __global__ __launch_bounds__(PPLS_FIN_THREADS) void ppls_finalize_kernel(
   if (!(mode & 2)) return;
   // cross-product form: the Gram of [XW YC] = B'M from M = S B (the polar blocks run meanwhile)
   if constexpr (R <= 8)
-    if (xpM) ppls_xp_gram_block<R, NT>(xpM, Wc, Cc, ldx, ldy, s_G, const_cast<double*>(G), NGH, gslots,
-                                       team_bar + 8, status, tr);
+    if (xpM) ppls_xp_gram_block<R, NT>(xpM, Wc, Cc, ldx, ldy, s_G, const_cast<double*>(G), tr);
   ppls_stamp(tr, 8);
   // stage theta's scalars, the Gram and W'W, C'C in LDS (all threads)
   {
@@ -2647,19 +2545,11 @@ hipError_t launch_finalize_t(const PplsFinalizeArgs* f, hipStream_t st) {
   const int mrows = (f->p + KX - 1) / KX > (f->q + KY - 1) / KY ? (f->p + KX - 1) / KX : (f->q + KY - 1) / KY;
   const size_t stage = (size_t)R * mrows * sizeof(double);   // a member stages its own rows
   const int use = stage <= dyn_max && !f->qr;
-  // the cross-product Gram over row slices of <= 2 rows per thread each, by helper blocks, when
-  // that takes >= 2 of them (team_bar / team_part hold their arrivals and slots)
-  int ngh = 0;
-  if (f->xpM && R <= 8 && f->team_bar) {
-    const int rows = f->ldx > f->ldy ? f->ldx : f->ldy;
-    ngh = (rows + 2 * PPLS_FIN_THREADS - 1) / (2 * PPLS_FIN_THREADS);
-    ngh = ngh < 2 ? 0 : ngh > PPLS_GRAM_HELPERS_MAX ? PPLS_GRAM_HELPERS_MAX : ngh;
-  }
-  hipLaunchKernelGGL(kern, dim3(KX + KY + 1 + ngh), dim3(PPLS_FIN_THREADS), use ? stage : 0, st, f->stats, f->ssq,
+  hipLaunchKernelGGL(kern, dim3(KX + KY + 1), dim3(PPLS_FIN_THREADS), use ? stage : 0, st, f->stats, f->ssq,
                      f->N, f->p, f->q, f->ldx, f->ldy, f->Wc, f->Cc, f->sc_cur, f->Wn, f->Cn, f->sc_nxt, f->mom,
                      f->loglik, f->logl_index, f->work, f->status, f->qr, f->mode, f->gram_cur,
                      f->gram_nxt, f->vstate, use, f->trace, f->stop, f->stop_mirror, f->stop_check,
-                     f->stop_step, f->atol, KX, KY, f->team_bar, f->team_part, f->xpM, ngh);
+                     f->stop_step, f->atol, KX, KY, f->team_bar, f->team_part, f->xpM);
   return hipGetLastError();
 }
 
