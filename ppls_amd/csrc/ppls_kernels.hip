@@ -1499,71 +1499,6 @@ __device__ void ppls_team_sum(const PplsTeam& tm, int phase, double (&vals)[NG],
 // warm-started from vstate (the previous iteration's V; nullptr = identity).  sm: >= 2 R^2
 // doubles of LDS.  Returns false when S is numerically rank deficient (a Cholesky pivot fails or
 // sigma_min < 1e-14 sigma_max); the caller then falls back to Householder (which reports it).
-// Polar factor U V' of a nonsingular R x R matrix by the scaled Newton iteration
-// X <- (zeta X + X^-T / zeta) / 2, zeta = (||X^-1||_F / ||X||_F)^(1/2) while the step is large, then
-// unscaled (quadratic) steps; X^-T = X (X'X)^-1 through the packed Cholesky helpers.  One thread, in
-// registers.  Stops after the unscaled step that moved X by <= 1e-8 sqrt(R) (the error left is the
-// square of that); returns the iterations, or -1 if a Cholesky pivot failed (X singular).
-#ifndef PPLS_NEWTON_RMAX
-#define PPLS_NEWTON_RMAX 6   // the Cholesky-QR1 polar path's R x R factor by Newton up to this R, else Jacobi
-#endif
-template <int R>
-__device__ __forceinline__ int ppls_polar_newton(double (&X)[R][R]) {
-  constexpr int NG = R * (R + 1) / 2;
-  bool scale = true;
-  for (int it = 1; it <= 30; ++it) {
-    double P[NG], dinv[R];
-#pragma unroll
-    for (int b = 0; b < R; ++b)
-#pragma unroll
-      for (int a = 0; a <= b; ++a) {
-        double g = 0.0;
-#pragma unroll
-        for (int k = 0; k < R; ++k) g = fma(X[k][a], X[k][b], g);
-        P[ppls_pk(a, b)] = g;
-      }
-    if (!ppls_chol_pk<R>(P, dinv)) return -1;
-    ppls_inv_upper_pk<R>(P, dinv);   // Rc^-1 (upper), X'X = Rc' Rc
-    double Gi[R][R];                 // (X'X)^-1 = Rc^-1 Rc^-T
-#pragma unroll
-    for (int a = 0; a < R; ++a)
-#pragma unroll
-      for (int b = a; b < R; ++b) {
-        double g = 0.0;
-#pragma unroll
-        for (int k = b; k < R; ++k) g = fma(P[ppls_pk(a, k)], P[ppls_pk(b, k)], g);
-        Gi[a][b] = g;
-        Gi[b][a] = g;
-      }
-    double Y[R][R], nx = 0.0, ny = 0.0;
-#pragma unroll
-    for (int a = 0; a < R; ++a)
-#pragma unroll
-      for (int b = 0; b < R; ++b) {
-        double y = 0.0;
-#pragma unroll
-        for (int k = 0; k < R; ++k) y = fma(X[a][k], Gi[k][b], y);
-        Y[a][b] = y;
-        nx = fma(X[a][b], X[a][b], nx);
-        ny = fma(y, y, ny);
-      }
-    const double z = scale ? sqrt(sqrt(ny / nx)) : 1.0, zi = scale ? 1.0 / z : 1.0;
-    double d = 0.0;
-#pragma unroll
-    for (int a = 0; a < R; ++a)
-#pragma unroll
-      for (int b = 0; b < R; ++b) {
-        const double xn = 0.5 * fma(z, X[a][b], zi * Y[a][b]);
-        const double e = xn - X[a][b];
-        d = fma(e, e, d);
-        X[a][b] = xn;
-      }
-    if (!scale && d <= 1e-16 * R) return it;
-    if (d <= 1e-4 * R) scale = false;
-  }
-  return 30;
-}
-
 #ifndef PPLS_REG_RMAX
 #define PPLS_REG_RMAX 10   // the polar's Cholesky factors and inverses by one thread in registers up to this R
 #endif
@@ -1710,30 +1645,7 @@ __device__ bool ppls_block_polar_fast(const double* __restrict__ S, int64_t lds,
       const double kb = kbound > 0.0 ? kbound : PPLS_POLAR1_KAPPA * R;
       fst = __shfl(fr * fi <= kb * kb ? 1 : 0, 0, 64) != 0;
     }
-    if constexpr (R <= PPLS_NEWTON_RMAX) {
-      // the polar factor of R1 by Newton on lane 0, F = R1^-1 polar(R1) (no Jacobi, no LDS round
-      // trips; the carried V is left for the Cholesky-QR2 path's Jacobi)
-      if (fst && lane == 0) {
-        double X[R][R];
-#pragma unroll
-        for (int a = 0; a < R; ++a)
-#pragma unroll
-          for (int b = 0; b < R; ++b) X[a][b] = a <= b ? sT[b * G + a] : 0.0;
-        const int its = ppls_polar_newton<R>(X);
-        if (tr) tr[10] = its;
-#pragma unroll
-        for (int a = 0; a < R; ++a)
-#pragma unroll
-          for (int b = 0; b < R; ++b) {
-            double f = 0.0;
-#pragma unroll
-            for (int k = a; k < R; ++k) f = fma(sF[k * R + a], X[k][b], f);   // R1^-1 upper
-            sF[R * R + b * R + a] = f;
-          }
-        if (its < 0) fst = false;   // not reached for a matrix that passed the kappa test
-      }
-      ppls_stamp(tr, 8);
-    } else if (fst) {
+    if (fst) {
       load_vprev();
       ppls_stamp(tr, 6);
       ppls_matmul_wave<R, false>(sT, sV, sA);                // sA = R1 V (sT keeps R1)
