@@ -16,7 +16,7 @@ def main():
     out = os.path.join(ROOT, "abtest", name)
     if os.path.exists(out):
         shutil.rmtree(out)
-    for d in ("ppls_amd", "tools", "oracle", "include"):
+    for d in ("ppls_amd", "tools", "oracle", "include", "tests"):
         shutil.copytree(os.path.join(ROOT, d), os.path.join(out, d),
                         ignore=shutil.ignore_patterns("_build", "__pycache__", "*.so", "*.o"))
     for f in ("bench.py", "__graft_entry__.py"):
