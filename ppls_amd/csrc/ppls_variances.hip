@@ -159,8 +159,12 @@ __global__ __launch_bounds__(256, 2) void ppls_gram_mfma_kernel(const T* __restr
 #ifndef PPLS_GRAM_DMA
 #define PPLS_GRAM_DMA 0   // fp64 Gram: 1 = rows stream HBM -> LDS by LDS-DMA through a 4-slot ring (experiment)
 #endif
+#ifndef PPLS_GDK
 #define PPLS_GDK 8     // rows per ring slot (DMA form)
-#define PPLS_GDS 4     // ring slots: 3 stages in flight
+#endif
+#ifndef PPLS_GDS
+#define PPLS_GDS 4     // ring slots: PPLS_GDS - 1 stages in flight
+#endif
 
 // The fp64 Gram with rows copied HBM -> LDS by global_load_lds_dwordx4 (no register staging, no
 // per-load address VALU: the saddr form with a per-row SGPR base and a per-lane offset fixed per
@@ -260,7 +264,8 @@ __global__ __launch_bounds__(256, 2) void ppls_gram_dma_kernel(const double* __r
       __syncthreads();
     }
   } else {
-    // LDS-DMA ring.  Wave w copies rows 2w, 2w + 1 of both panels of each stage (4 copies).
+    // LDS-DMA ring.  Wave w copies rows [RPW w, RPW w + RPW) of both panels of each stage.
+    constexpr int RPW = PPLS_GDK / 4;
     const int cA = colA + 2 * lane, cB = colB + 2 * lane;
     const bool actA = sA == 0 ? cA < xcols : cA - xcols < ycols;   // lanes past the last column: no copy
     const bool actB = sB == 0 ? cB < xcols : cB - xcols < ycols;
@@ -276,8 +281,8 @@ __global__ __launch_bounds__(256, 2) void ppls_gram_dma_kernel(const double* __r
     auto issued = [&](int64_t k) {
       int c = 0;
 #pragma unroll
-      for (int rr = 0; rr < 2; ++rr) {
-        const int64_t gr = r0 + k * PPLS_GDK + 2 * wave + rr;
+      for (int rr = 0; rr < RPW; ++rr) {
+        const int64_t gr = r0 + k * PPLS_GDK + RPW * wave + rr;
         if (gr < r1) c += (anyA ? 1 : 0) + (anyB ? 1 : 0);
       }
       return c;
@@ -285,8 +290,8 @@ __global__ __launch_bounds__(256, 2) void ppls_gram_dma_kernel(const double* __r
     auto issue = [&](int64_t k) {
       const int slot = (int)(k % PPLS_GDS);
 #pragma unroll
-      for (int rr = 0; rr < 2; ++rr) {
-        const int row = 2 * wave + rr;
+      for (int rr = 0; rr < RPW; ++rr) {
+        const int row = RPW * wave + rr;
         const int64_t gr = r0 + k * PPLS_GDK + row;
         const uint32_t la = lds0 + (uint32_t)((((slot * 2 + 0) * PPLS_GDK + row) * PPLS_GLD) * 8);
         const uint32_t lb = lds0 + (uint32_t)((((slot * 2 + 1) * PPLS_GDK + row) * PPLS_GLD) * 8);
