@@ -16,7 +16,6 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include "ppls_device.h"
 #include "ppls_kernels.h"
 #include "ppls_xprod.h"
 
@@ -141,184 +140,6 @@ __global__ __launch_bounds__(256, 2) void ppls_gram_mfma_kernel(const T* __restr
     }
     if (st + 1 < nsteps) store(buf ^ 1);
     __syncthreads();
-  }
-  double* out = part + (int64_t)s * part_stride;
-#pragma unroll
-  for (int m = 0; m < 4; ++m)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int j = colB + wj * 64 + q * 16 + cl;
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {   // f64 MFMA D map: col = lane & 15, row = (lane >> 4) + 4 g
-        const int i = colA + wi * 64 + m * 16 + ko + 4 * g;
-        if (i < p && j < p) out[(int64_t)i * p + j] = acc[m][q][g];
-      }
-    }
-}
-
-#ifndef PPLS_GRAM_DMA
-#define PPLS_GRAM_DMA 0   // fp64 Gram: 1 = rows stream HBM -> LDS by LDS-DMA through a 4-slot ring (experiment)
-#endif
-#ifndef PPLS_GDK
-#define PPLS_GDK 8     // rows per ring slot (DMA form)
-#endif
-#ifndef PPLS_GDS
-#define PPLS_GDS 4     // ring slots: PPLS_GDS - 1 stages in flight
-#endif
-
-// The fp64 Gram with rows copied HBM -> LDS by global_load_lds_dwordx4 (no register staging, no
-// per-load address VALU: the saddr form with a per-row SGPR base and a per-lane offset fixed per
-// work item) through a PPLS_GDS-slot ring of PPLS_GDK-row stages -- PPLS_GDS - 1 stages in flight,
-// one barrier per stage.  Same work items, MFMA loop and output as ppls_gram_mfma_kernel; a work
-// item whose column panel straddles the X/Y seam (lanes of one DMA would need two base arrays)
-// takes that kernel's register-staged loop instead (same LDS, reinterpreted).  Rows past the
-// split's end are zero-filled with LDS stores.  Columns past xcols + ycols are not copied: they
-// only reach output rows/columns >= p, which are never written.
-__global__ __launch_bounds__(256, 2) void ppls_gram_dma_kernel(const double* __restrict__ X, int ldx, int xcols,
-                                                              const double* __restrict__ Y, int ldy, int ycols,
-                                                              int64_t n, int p, int ntiles, int nsplit, int64_t work,
-                                                              double* __restrict__ part, int64_t part_stride) {
-  typedef double d4 __attribute__((ext_vector_type(4)));
-  constexpr int SLOT = 2 * PPLS_GDK * PPLS_GLD;   // doubles per ring slot (two panels)
-  __shared__ __attribute__((aligned(16))) double sm[PPLS_GDS * SLOT];
-  static_assert(PPLS_GDS * 2 * PPLS_GDK == 2 * 2 * PPLS_GK, "the register path reuses the same LDS");
-  const int64_t per = gridDim.x >> 3;
-  const int64_t L = (int64_t)(blockIdx.x & 7) * per + (blockIdx.x >> 3);
-  if (L >= work) return;
-  const int s = (int)(L / ntiles), t = (int)(L - (int64_t)s * ntiles);
-  int I = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
-  while ((I + 1) * (I + 2) / 2 <= t) ++I;
-  while (I * (I + 1) / 2 > t) --I;
-  const int J = t - I * (I + 1) / 2;
-  const int64_t r0 = n * s / nsplit, r1 = n * (s + 1) / nsplit;
-  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wi = wave >> 1, wj = wave & 1;
-  const int colA = I * PPLS_GT, colB = J * PPLS_GT;
-  // panel sources (uniform): 0 = X only, 1 = Y only, 2 = straddles the seam
-  auto src_of = [&](int c0) {
-    const int c1 = c0 + PPLS_GT;   // exclusive
-    if (c1 <= xcols || ycols == 0) return 0;
-    if (c0 >= xcols) return 1;
-    return 2;
-  };
-  const int sA = src_of(colA), sB = src_of(colB);
-  d4 acc[4][4];
-#pragma unroll
-  for (int m = 0; m < 4; ++m)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) acc[m][q] = d4{0.0, 0.0, 0.0, 0.0};
-  const int ko = lane >> 4, cl = lane & 15;
-  auto mfma_rows = [&](const double* pa, const double* pb, int ksteps) {   // rows of a stage
-#pragma unroll 2
-    for (int kk = 0; kk < ksteps; ++kk) {
-      const double* ar = pa + (kk * 4 + ko) * PPLS_GLD + wi * 64 + cl;
-      const double* br = pb + (kk * 4 + ko) * PPLS_GLD + wj * 64 + cl;
-      double a[4], b[4];
-#pragma unroll
-      for (int m = 0; m < 4; ++m) a[m] = ar[m * 16];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) b[q] = br[q * 16];
-#pragma unroll
-      for (int m = 0; m < 4; ++m)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) acc[m][q] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[m], b[q], acc[m][q], 0, 0, 0);
-    }
-  };
-  if (sA == 2 || sB == 2) {
-    // register-staged loop of ppls_gram_mfma_kernel (16-row stages, two LDS buffers)
-    constexpr int NV = PPLS_GK * (PPLS_GT / 2) / 256;
-    double2 ra[NV], rb[NV];
-    auto load = [&](int64_t k0) {
-#pragma unroll
-      for (int v = 0; v < NV; ++v) {
-        const int c = tid + 256 * v, row = c / (PPLS_GT / 2), cv = c - row * (PPLS_GT / 2);
-        const int64_t gr = k0 + row;
-        const int ca = colA + cv * 2, cb = colB + cv * 2;
-        if (gr < r1 && ca < xcols) ra[v] = *(const double2*)(X + gr * ldx + ca);
-        else if (gr < r1 && ca - xcols < ycols) ra[v] = *(const double2*)(Y + gr * ldy + (ca - xcols));
-        else ra[v] = make_double2(0.0, 0.0);
-        if (gr < r1 && cb < xcols) rb[v] = *(const double2*)(X + gr * ldx + cb);
-        else if (gr < r1 && cb - xcols < ycols) rb[v] = *(const double2*)(Y + gr * ldy + (cb - xcols));
-        else rb[v] = make_double2(0.0, 0.0);
-      }
-    };
-    auto store = [&](int buf) {
-#pragma unroll
-      for (int v = 0; v < NV; ++v) {
-        const int c = tid + 256 * v, row = c / (PPLS_GT / 2), cv = c - row * (PPLS_GT / 2);
-        *(double2*)&sm[((buf * 2 + 0) * PPLS_GK + row) * PPLS_GLD + cv * 2] = ra[v];
-        *(double2*)&sm[((buf * 2 + 1) * PPLS_GK + row) * PPLS_GLD + cv * 2] = rb[v];
-      }
-    };
-    const int64_t nsteps = (r1 - r0 + PPLS_GK - 1) / PPLS_GK;
-    if (nsteps > 0) {
-      load(r0);
-      store(0);
-    }
-    __syncthreads();
-    for (int64_t st = 0; st < nsteps; ++st) {
-      const int buf = (int)(st & 1);
-      if (st + 1 < nsteps) load(r0 + (st + 1) * PPLS_GK);
-      mfma_rows(&sm[(buf * 2 + 0) * PPLS_GK * PPLS_GLD], &sm[(buf * 2 + 1) * PPLS_GK * PPLS_GLD], PPLS_GK / 4);
-      if (st + 1 < nsteps) store(buf ^ 1);
-      __syncthreads();
-    }
-  } else {
-    // LDS-DMA ring.  Wave w copies rows [RPW w, RPW w + RPW) of both panels of each stage.
-    constexpr int RPW = PPLS_GDK / 4;
-    const int cA = colA + 2 * lane, cB = colB + 2 * lane;
-    const bool actA = sA == 0 ? cA < xcols : cA - xcols < ycols;   // lanes past the last column: no copy
-    const bool actB = sB == 0 ? cB < xcols : cB - xcols < ycols;
-    const uint32_t offA = (uint32_t)((sA == 0 ? cA : cA - xcols) * 8), offB = (uint32_t)((sB == 0 ? cB : cB - xcols) * 8);
-    const double* baseA = sA == 0 ? X : Y;
-    const double* baseB = sB == 0 ? X : Y;
-    const int ldA = sA == 0 ? ldx : ldy, ldB = sB == 0 ? ldx : ldy;
-    const bool anyA = __builtin_amdgcn_readfirstlane((int)(colA < (sA == 0 ? xcols : xcols + ycols))) != 0;
-    const bool anyB = __builtin_amdgcn_readfirstlane((int)(colB < (sB == 0 ? xcols : xcols + ycols))) != 0;
-    const uint32_t lds0 = (uint32_t)(uintptr_t)sm;
-    const int64_t nsteps = (r1 - r0 + PPLS_GDK - 1) / PPLS_GDK;
-    // copies this wave issues for stage k (the same count in every lane: wave-uniform)
-    auto issued = [&](int64_t k) {
-      int c = 0;
-#pragma unroll
-      for (int rr = 0; rr < RPW; ++rr) {
-        const int64_t gr = r0 + k * PPLS_GDK + RPW * wave + rr;
-        if (gr < r1) c += (anyA ? 1 : 0) + (anyB ? 1 : 0);
-      }
-      return c;
-    };
-    auto issue = [&](int64_t k) {
-      const int slot = (int)(k % PPLS_GDS);
-#pragma unroll
-      for (int rr = 0; rr < RPW; ++rr) {
-        const int row = RPW * wave + rr;
-        const int64_t gr = r0 + k * PPLS_GDK + row;
-        const uint32_t la = lds0 + (uint32_t)((((slot * 2 + 0) * PPLS_GDK + row) * PPLS_GLD) * 8);
-        const uint32_t lb = lds0 + (uint32_t)((((slot * 2 + 1) * PPLS_GDK + row) * PPLS_GLD) * 8);
-        if (gr < r1) {
-          if (anyA && actA) ppls_dma16s(baseA + gr * ldA, offA, la);
-          if (anyB && actB) ppls_dma16s(baseB + gr * ldB, offB, lb);
-        } else {   // past the split's end: zeros
-          *(double2*)&sm[(((slot * 2 + 0) * PPLS_GDK + row) * PPLS_GLD) + 2 * lane] = make_double2(0.0, 0.0);
-          *(double2*)&sm[(((slot * 2 + 1) * PPLS_GDK + row) * PPLS_GLD) + 2 * lane] = make_double2(0.0, 0.0);
-        }
-      }
-    };
-#pragma unroll
-    for (int k = 0; k < PPLS_GDS - 1; ++k)
-      if (k < nsteps) issue(k);
-    for (int64_t st = 0; st < nsteps; ++st) {
-      // stage st's copies are done when at most the later stages' copies are in flight
-      int later = 0;
-#pragma unroll
-      for (int k = 1; k < PPLS_GDS - 1; ++k)
-        if (st + k < nsteps) later += issued(st + k);
-      ppls_wait_vmcnt(later);
-      ppls_lds_barrier();
-      if (st + PPLS_GDS - 1 < nsteps) issue(st + PPLS_GDS - 1);   // into the slot read at stage st - 1
-      const int slot = (int)(st % PPLS_GDS);
-      mfma_rows(&sm[(slot * 2 + 0) * PPLS_GDK * PPLS_GLD], &sm[(slot * 2 + 1) * PPLS_GDK * PPLS_GLD], PPLS_GDK / 4);
-    }
   }
   double* out = part + (int64_t)s * part_stride;
 #pragma unroll
@@ -478,9 +299,6 @@ hipError_t ppls_launch_gram_joint(const void* X, int ldx, int xcols, const void*
   if (f32)
     hipLaunchKernelGGL(ppls_gram_mfma_kernel<float>, dim3((unsigned)grid), dim3(256), 0, st, (const float*)X, ldx,
                        xcols, (const float*)Y, ldy, ycols, n, p, ntiles, nsplit, work, part, part_stride);
-  else if (PPLS_GRAM_DMA)
-    hipLaunchKernelGGL(ppls_gram_dma_kernel, dim3((unsigned)grid), dim3(256), 0, st, (const double*)X, ldx,
-                       xcols, (const double*)Y, ldy, ycols, n, p, ntiles, nsplit, work, part, part_stride);
   else
     hipLaunchKernelGGL(ppls_gram_mfma_kernel<double>, dim3((unsigned)grid), dim3(256), 0, st, (const double*)X, ldx,
                        xcols, (const double*)Y, ldy, ycols, n, p, ntiles, nsplit, work, part, part_stride);
