@@ -24,7 +24,9 @@
 #include "ppls_xprod.h"
 
 #ifndef PPLS_XP_DEPTH
-#define PPLS_XP_DEPTH 2   // 128-column tiles of S in flight per wave in the row-tile kernel (2, 3, 4, 6: same within 1 %, 6 slower at r = 10)
+#define PPLS_XP_DEPTH 1   // staged tiles of S in flight per wave (1: loaded right before use; round 3: 2, 3, 4, 6
+                          // equal within 1 %; round 4, with two sub-tiles per barrier at r <= 5: 1 is fastest --
+                          // C3 tile 22.9 -> 21.7 us, C5 202 -> 200 us; profiles/r4_xprod_depth_ab_*.txt)
 #endif
 #ifndef PPLS_XP_TPB
 #define PPLS_XP_TPB 0     // 128-column sub-tiles per staged B tile and workgroup barrier (0: ppls_xp_tpb)
@@ -42,10 +44,10 @@ constexpr int ppls_rs_left(int m, int l) { return l == 6 ? m : (m == 1 ? 1 : ppl
 // Row-tile form: a workgroup owns 4 RW rows of S (RW per wave) and walks the columns
 // in tiles of 128 -- first the X columns, then the Y columns.  Each tile's 128 x R values of B (W on
 // X columns, C on Y columns) are staged in LDS once per workgroup and read by all its rows, so W and
-// C cost ~R / (4 RW) of S's traffic from L2.  S tiles stream through a register
-// ring PPLS_XP_DEPTH tiles ahead (enough bytes in flight per CU to cover HBM/MALL latency: one
-// 128-column tile is only 1 KB per wave and row), B one tile ahead through LDS; one barrier per
-// staged tile of ppls_xp_tpb(R) 128-column sub-tiles.
+// C cost ~R / (4 RW) of S's traffic from L2.  S tiles are loaded into a register ring
+// PPLS_XP_DEPTH - 1 staged tiles ahead of their use (default: none -- the 16 resident waves per CU
+// keep enough bytes in flight, and fewer live registers measured faster), B one tile ahead through
+// LDS; one barrier per staged tile of ppls_xp_tpb(R) 128-column sub-tiles.
 template <int R, int RW, bool NT>
 __device__ __forceinline__ void ppls_xprod_tile_phase(const double* const (&srow)[RW], const double* __restrict__ Bsrc,
                                                       int ldb, int width, int soff, double (&acc)[RW * R + 1],
