@@ -28,6 +28,9 @@
                           // equal within 1 %; round 4, with two sub-tiles per barrier at r <= 5: 1 is fastest --
                           // C3 tile 22.9 -> 21.7 us, C5 202 -> 200 us; profiles/r4_xprod_depth_ab_*.txt)
 #endif
+#ifndef PPLS_XP_WAVES
+#define PPLS_XP_WAVES 4   // waves (rows of S per RW) per tile-kernel workgroup, sharing each staged B tile
+#endif
 #ifndef PPLS_XP_TPB
 #define PPLS_XP_TPB 0     // 128-column sub-tiles per staged B tile and workgroup barrier (0: ppls_xp_tpb)
 #endif
@@ -55,7 +58,8 @@ __device__ __forceinline__ void ppls_xprod_tile_phase(const double* const (&srow
   typedef double d2v __attribute__((ext_vector_type(2)));
   constexpr int TP = ppls_xp_tpb(R);         // 128-column sub-tiles per staged tile (one barrier each)
   constexpr int TV = TP * R * 64;            // 16-B values of B per staged tile
-  constexpr int NB = (TV + 255) / 256;       // 16-B B loads per thread and tile
+  constexpr int NTH = 64 * PPLS_XP_WAVES;
+  constexpr int NB = (TV + NTH - 1) / NTH;   // 16-B B loads per thread and tile
   constexpr int D = PPLS_XP_DEPTH;           // S tiles in flight per wave (register ring)
   const int tid = threadIdx.x;
   const int ntile = (width + 128 * TP - 1) / (128 * TP);
@@ -79,7 +83,7 @@ __device__ __forceinline__ void ppls_xprod_tile_phase(const double* const (&srow
   auto ld_b = [&](int n) {   // tile n: this thread's share of the TP x 128 x R values of B
 #pragma unroll
     for (int v = 0; v < NB; ++v) {
-      const int e = tid + 256 * v, sp = e / (R * 64), f = e - sp * R * 64, t = f >> 6;
+      const int e = tid + NTH * v, sp = e / (R * 64), f = e - sp * R * 64, t = f >> 6;
       const int cb = (n * TP + sp) * 128 + 2 * (f & 63);
       bn[v] = (e < TV && cb < width) ? *(const d2v*)(Bsrc + (int64_t)t * ldb + cb) : d2v{0.0, 0.0};
     }
@@ -87,7 +91,7 @@ __device__ __forceinline__ void ppls_xprod_tile_phase(const double* const (&srow
   auto st_b = [&](int buf) {
 #pragma unroll
     for (int v = 0; v < NB; ++v) {
-      const int e = tid + 256 * v;
+      const int e = tid + NTH * v;
       if (e < TV) ((d2v*)sB)[buf * TV + e] = bn[v];
     }
   };
@@ -186,7 +190,7 @@ __device__ __forceinline__ void ppls_xprod_tile_body(const double* __restrict__ 
 }
 
 template <int R, int RW, bool NT>
-__global__ __launch_bounds__(256) void ppls_xprod_tile_kernel(const double* __restrict__ S, int ldx, int ldy,
+__global__ __launch_bounds__(64 * PPLS_XP_WAVES) void ppls_xprod_tile_kernel(const double* __restrict__ S, int ldx, int ldy,
                                                               const double* __restrict__ Wp,
                                                               const double* __restrict__ Cp,
                                                               const PplsScalars* __restrict__ sc,
@@ -194,9 +198,9 @@ __global__ __launch_bounds__(256) void ppls_xprod_tile_kernel(const double* __re
                                                               const int* __restrict__ stop) {
   if (stop && *stop) return;   // em_run converged at an earlier iteration
   __shared__ double sB[2 * R * 128 * ppls_xp_tpb(R)];
-  __shared__ double sm[4][RW * 2 * R];
+  __shared__ double sm[PPLS_XP_WAVES][RW * 2 * R];
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t i0 = ((int64_t)blockIdx.x * 4 + wave) * RW;   // this wave's first row of S
+  const int64_t i0 = ((int64_t)blockIdx.x * PPLS_XP_WAVES + wave) * RW;   // this wave's first row of S
   ppls_xprod_tile_body<R, RW, NT>(S, ldx, ldy, Wp, Cp, sc, stats, M, sB, sm[wave], i0, lane);
 }
 
@@ -236,12 +240,12 @@ template <int R, int RW>
 hipError_t launch_tile(const double* S, int ldx, int ldy, const double* Wp, const double* Cp, const PplsScalars* sc,
                        double* stats, double* M, const int* stop, hipStream_t st) {
   const int P = ldx + ldy;
-  const unsigned blocks = (unsigned)((P + 4 * RW - 1) / (4 * RW));
+  const unsigned blocks = (unsigned)((P + PPLS_XP_WAVES * RW - 1) / (PPLS_XP_WAVES * RW));
   if (8.0 * P * (double)P > 200.0 * (1 << 20))   // S beyond the Infinity Cache: non-temporal loads
-    hipLaunchKernelGGL((ppls_xprod_tile_kernel<R, RW, true>), dim3(blocks), dim3(256), 0, st, S, ldx, ldy, Wp, Cp, sc,
+    hipLaunchKernelGGL((ppls_xprod_tile_kernel<R, RW, true>), dim3(blocks), dim3(64 * PPLS_XP_WAVES), 0, st, S, ldx, ldy, Wp, Cp, sc,
                        stats, M, stop);
   else
-    hipLaunchKernelGGL((ppls_xprod_tile_kernel<R, RW, false>), dim3(blocks), dim3(256), 0, st, S, ldx, ldy, Wp, Cp,
+    hipLaunchKernelGGL((ppls_xprod_tile_kernel<R, RW, false>), dim3(blocks), dim3(64 * PPLS_XP_WAVES), 0, st, S, ldx, ldy, Wp, Cp,
                        sc, stats, M, stop);
   return hipGetLastError();
 }
