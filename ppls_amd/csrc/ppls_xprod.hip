@@ -222,8 +222,15 @@ __global__ __launch_bounds__(256) void ppls_xprod_gram_kernel(int ldx, int ldy, 
   const double* Bcol = a < R ? Wp + (int64_t)a * ldx : Cp + (int64_t)(a - R) * ldy;
   const double* Mcol = M + (int64_t)b * P + (a < R ? 0 : ldx);
   const int rows = a < R ? ldx : ldy;
-  double v = 0.0;
-  for (int i = threadIdx.x; i < rows; i += 256) v = fma(Bcol[i], Mcol[i], v);
+  // four independent partial sums per thread (loads of four rows in flight), added in fixed order
+  double v4[4] = {0.0, 0.0, 0.0, 0.0};
+  int i = threadIdx.x;
+  for (; i + 3 * 256 < rows; i += 4 * 256) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v4[u] = fma(Bcol[i + u * 256], Mcol[i + u * 256], v4[u]);
+  }
+  for (; i < rows; i += 256) v4[0] = fma(Bcol[i], Mcol[i], v4[0]);
+  double v = (v4[0] + v4[1]) + (v4[2] + v4[3]);
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
