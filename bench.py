@@ -204,16 +204,11 @@ def bench_xprod(ctx, th0, args, barrier, tmax, r, ll_stream, t_stream):
     barrier()
     dt = tmax(time.perf_counter() - t0)
     est, ll_x = ctx.em_state()
-    # the tile kernel's average duration: HIP events around every launch of a second, separate run
-    # of the same iterations (events between ~40-us iterations would lengthen the timed one)
-    ctx.em_begin(th0)
-    ctx.em_iterate(args.warmup)
-    ctx.set_option("timing", 1)
-    ctx.sweep_timing(reset=True)
-    ctx.em_iterate(args.xprod_steps)
-    ctx.synchronize()
-    ctx.set_option("timing", 0)
-    kms, launches = ctx.sweep_timing(reset=True)
+    # the tile kernel's average duration: HIP events around a batch of back-to-back launches for the
+    # final theta (an event pair around every ~20-us launch reads ~3 us long; rocprofv3 agrees with
+    # the batch figure)
+    launches = max(args.xprod_steps, 1)
+    kms = ctx.xprod_tile_timing(launches) * launches
     k = min(len(ll_x), len(ll_stream))
     rel = float(np.abs(ll_x[:k] - ll_stream[:k]).max() / np.abs(ll_stream[:k]).max()) if k else None
     t_x = dt / args.xprod_steps
@@ -244,7 +239,8 @@ def bench_xprod(ctx, th0, args, barrier, tmax, r, ll_stream, t_stream):
                       frac_of_mall_reread=(achieved / MALL_REREAD_GBS) if achieved else None,
                       kernel="xprod_tile (+ the Gram B'M in the finalize)",
                       traffic=traffic, traffic_source=traffic_src,
-                      avg_kernel_us=avg_us, bytes_per_launch=info["bytes_per_pass"],
+                      avg_kernel_us=avg_us, timing=f"HIP events around {launches} back-to-back launches",
+                      bytes_per_launch=info["bytes_per_pass"],
                       rows_per_wave=info["rows_per_wave"]),
         loglik_rel_diff_vs_streaming=rel, loglik_compared=k,
         breakeven_steps=(t_setup / (t_stream - t_x)) if t_stream > t_x else None,

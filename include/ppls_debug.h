@@ -33,6 +33,10 @@ int ppls_xprod_info(ppls_ctx* ctx, int r, int* ready, int64_t* bytes_per_pass, d
 /* The last formation of S: the MFMA Gram (HIP events), the all-reduce of S over ranks (wall clock
  * around the collective and its stream synchronisation; 0 on one rank) and the whole setup. */
 int ppls_xprod_setup_times(ppls_ctx* ctx, double* gram_ms, double* allreduce_ms, double* total_ms);
+/* The cross-product tile kernel alone, reps launches back to back between two HIP events, for the
+ * current theta of an ppls_em_begin session (S formed): *ms = the average per launch.  Rewrites the
+ * session's statistics buffer with that theta's (the next ppls_em_iterate recomputes it anyway). */
+int ppls_xprod_tile_timing(ppls_ctx* ctx, int reps, double* ms);
 /* One statistics step from S for theta: stats = [X'mu_T p x r | Y'mu_U q x r | Gram 2r x 2r], all
  * column-major, as ppls_finalize_host takes them (unit parity against the sweep and a host S B). */
 int ppls_xprod_stats(ppls_ctx* ctx, const ppls_theta* th, int r, double* stats);

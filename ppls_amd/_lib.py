@@ -104,6 +104,7 @@ SIGNATURES = {
     "ppls_xprod_prepare": (ct.c_int, [ct.c_void_p, _dp, _dp]),
     "ppls_xprod_release": (ct.c_int, [ct.c_void_p]),
     "ppls_xprod_setup_times": (ct.c_int, [ct.c_void_p, _dp, _dp, _dp]),
+    "ppls_xprod_tile_timing": (ct.c_int, [ct.c_void_p, ct.c_int, _dp]),
     "ppls_xprod_stats": (ct.c_int, [ct.c_void_p, ct.POINTER(PplsTheta), ct.c_int, _dp]),
     "ppls_xprod_info": (ct.c_int, [ct.c_void_p, ct.c_int, ct.POINTER(ct.c_int), ct.POINTER(ct.c_int64), _dp,
                                    ct.POINTER(ct.c_int)]),

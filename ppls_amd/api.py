@@ -379,6 +379,13 @@ class Context:
         that reads S forms it again."""
         self._chk(self._L.ppls_xprod_release(self.h))
 
+    def xprod_tile_timing(self, reps=200):
+        """Average ms of the cross-product tile kernel over reps back-to-back launches (HIP events
+        around the batch) for the current em_begin session's theta."""
+        ms = ct.c_double()
+        self._chk(self._L.ppls_xprod_tile_timing(self.h, int(reps), ct.byref(ms)))
+        return ms.value
+
     def xprod_setup_times(self):
         """(Gram kernel ms, all-reduce of S ms, whole setup ms) of the last formation of S."""
         g, a, t = ct.c_double(), ct.c_double(), ct.c_double()

@@ -2476,6 +2476,31 @@ int ppls_xprod_setup_times(ppls_ctx* c, double* gram_ms, double* allreduce_ms, d
   return PPLS_OK;
 }
 
+int ppls_xprod_tile_timing(ppls_ctx* c, int reps, double* ms) {
+  if (!c || reps < 1 || !ms) return PPLS_E_ARG;
+  if (!c->em_active || c->r_alloc != c->em_r) return fail(c, PPLS_E_STATE, "call ppls_em_begin first");
+  if (!c->xp_ready || !c->xp_M) return fail(c, PPLS_E_STATE, "the cross-products S are not formed");
+  HIPCHK(c, hipSetDevice(c->device));
+  const int r = c->em_r, slot = c->em_cur, P = c->ldx + c->ldy;
+  const int rw = ppls_xprod_tile_rows(P, r, c->xprod_rw, c->num_cus);
+  hipEvent_t e0, e1;
+  HIPCHK(c, hipEventCreate(&e0));
+  HIPCHK(c, hipEventCreate(&e1));
+  hipError_t e = hipEventRecord(e0, c->stream);
+  for (int i = 0; e == hipSuccess && i < reps; ++i)   // the statistics of the current theta, rewritten
+    e = ppls_launch_xprod_tile(c->xp_S, c->ldx, c->ldy, r, rw, c->W[slot], c->C[slot], c->sc[slot], c->stats,
+                               c->xp_M, nullptr, 0, c->stream);
+  if (e == hipSuccess) e = hipEventRecord(e1, c->stream);
+  if (e == hipSuccess) e = hipEventSynchronize(e1);
+  float t = 0.f;
+  if (e == hipSuccess) e = hipEventElapsedTime(&t, e0, e1);
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  HIPCHK(c, e);
+  *ms = (double)t / reps;
+  return PPLS_OK;
+}
+
 int ppls_xprod_info(ppls_ctx* c, int r, int* ready, int64_t* bytes_per_pass, double* flops, int* rows_per_wave) {
   if (!c) return PPLS_E_ARG;
   if (!c->have_data) return fail(c, PPLS_E_STATE, "no data");

@@ -230,6 +230,19 @@ def test_xprod_prepare_and_info(ctx):
     assert not ctx.xprod_info(2)["ready"]
     ms2, _ = ctx.xprod_prepare()
     assert ms2 > 0 and ctx.xprod_info(2)["ready"]
+    # the tile kernel timed alone (bench.py's xprod roofline) in the middle of a session leaves its
+    # iterates as they were
+    ctx.set_option("xprod", 1)
+    th = _theta(make_problem(1000, 70, 33, 2, seed=4)[2])
+    ctx.em_begin(th)
+    ctx.em_iterate(3)
+    assert ctx.xprod_tile_timing(20) > 0.0
+    ctx.em_iterate(3)
+    est_a, ll_a = ctx.em_state()
+    ctx.em_begin(th)
+    ctx.em_iterate(6)
+    est_b, ll_b = ctx.em_state()
+    assert len(ll_a) == 5 and np.array_equal(ll_a, ll_b) and np.array_equal(est_a.W, est_b.W)
     ctx.set_option("xprod", 0)   # streaming from now on frees S
     assert not ctx.xprod_info(2)["ready"]
 
