@@ -1601,7 +1601,8 @@ __device__ bool ppls_block_polar_fast(const double* __restrict__ S, int64_t lds,
   const double* Sr = Sl ? Sl : S;
   const int64_t ldr = Sl ? nr : lds;
   const int sro = Sl ? i0 : 0;
-  // re-orthonormalise the carried V in sV (modified Gram-Schmidt, rows on lanes; wave 0)
+  // re-orthonormalise the carried V in sV (wave 0: Cholesky QR on lane 0 for R <= 6, else modified
+  // Gram-Schmidt with rows on lanes)
   auto load_vprev = [&]() {
     for (int e = lane; e < GG; e += 64) {
 #pragma unroll
@@ -1609,7 +1610,42 @@ __device__ bool ppls_block_polar_fast(const double* __restrict__ S, int64_t lds,
         if (e == lane + 64 * u) sV[e] = vprev[u];
     }
     ppls_wave_lds_fence();
-    if (vstate) {
+    if constexpr (R <= 6) {   // (at r = 10 the 165 register values spill)
+      // V <- V Rc^-1, V'V = Rc' Rc (Cholesky QR of a nearly orthonormal V: exact to rounding), on
+      // lane 0 in registers -- one step instead of the R (R - 1) / 2 dependent column sums of
+      // Gram-Schmidt; a singular V (not a carried state) restarts from the identity
+      if (vstate && lane == 0) {
+        double V[R][R], P[R * (R + 1) / 2], dinv[R];
+#pragma unroll
+        for (int a = 0; a < R; ++a)
+#pragma unroll
+          for (int k = 0; k < R; ++k) V[k][a] = sV[a * G + k];
+#pragma unroll
+        for (int b = 0; b < R; ++b)
+#pragma unroll
+          for (int a = 0; a <= b; ++a) {
+            double g = 0.0;
+#pragma unroll
+            for (int k = 0; k < R; ++k) g = fma(V[k][a], V[k][b], g);
+            P[ppls_pk(a, b)] = g;
+          }
+        const bool okc = ppls_chol_pk<R>(P, dinv);
+#pragma unroll
+        for (int k = 0; k < R; ++k)
+#pragma unroll
+          for (int j = 0; j < R; ++j) {
+            double x = V[k][j];
+#pragma unroll
+            for (int i = 0; i < j; ++i) x = fma(-V[k][i], P[ppls_pk(i, j)], x);   // V[k][i] already solved
+            V[k][j] = okc ? x * dinv[j] : (k == j ? 1.0 : 0.0);
+          }
+#pragma unroll
+        for (int a = 0; a < R; ++a)
+#pragma unroll
+          for (int k = 0; k < R; ++k) sV[a * G + k] = V[k][a];
+      }
+      ppls_wave_lds_fence();
+    } else if (vstate) {
       const int rt = lane % G;
       for (int j = 0; j < R; ++j) {
         double vj = sV[j * G + rt];
@@ -2071,29 +2107,40 @@ __device__ void ppls_xp_gram_block(const double* __restrict__ M, const double* _
       }
     }
     if (ps == 0) ppls_stamp(tr, 6);   // rows of the first pass summed per thread
-    ppls_block_sum_t<64, NT / 64>(acc, sh);
-    if (ps == 0) ppls_stamp(tr, 7);
-    if (tid == 0) {
-      int e = 0;
+    // block sums as ppls_block_sum_t forms them (wave reduce-scatter, then the waves' partials in
+    // wave order), but each entry summed and placed by its own thread
+    {
+      constexpr int NW = NT / 64;
+      const int lane = tid & 63, wave = tid >> 6;
+      int idx = 0;
+      bool canon = true;
+      ppls_rs<64, 0, 64>(acc, lane, idx, canon);
+      if (canon && idx < 64) sh[wave * 64 + idx] = acc[0];
+      __syncthreads();
+      const int e = lo + tid;
+      if (tid < 64 && e < NE) {
+        double t = 0.0;
 #pragma unroll
-      for (int a = 0; a < R; ++a)
-#pragma unroll
-        for (int b = a; b < R2; ++b, ++e)
-          if (e >= lo && e < lo + 64) {
-            sG[b * R2 + a] = sG[a * R2 + b] = acc[e - lo];
-            G[b * R2 + a] = G[a * R2 + b] = acc[e - lo];
-          }
-#pragma unroll
-      for (int a = 0; a < R; ++a)
-#pragma unroll
-        for (int b = a; b < R; ++b, ++e)
-          if (e >= lo && e < lo + 64) {
-            sG[(R + b) * R2 + R + a] = sG[(R + a) * R2 + R + b] = acc[e - lo];
-            G[(R + b) * R2 + R + a] = G[(R + a) * R2 + R + b] = acc[e - lo];
-          }
+        for (int w = 0; w < NW; ++w) t += sh[w * 64 + tid];
+        int a = 0, b, f = e;   // entry e -> (a, b): X rows' (a <= b < 2R), then Y rows' (a <= b < R)
+        const bool yp = f >= NX;
+        if (yp) f -= NX;
+        const int span = yp ? R : R2;
+        while (f >= span - a) {
+          f -= span - a;
+          ++a;
+        }
+        b = a + f;
+        const int o = yp ? R : 0;
+        sG[(o + b) * R2 + o + a] = t;
+        sG[(o + a) * R2 + o + b] = t;
+        G[(o + b) * R2 + o + a] = t;
+        G[(o + a) * R2 + o + b] = t;
+      }
+      __syncthreads();
     }
+    if (ps == 0) ppls_stamp(tr, 7);
   }
-  __syncthreads();
 }
 
 #define PPLS_FIN_THREADS 256   // 1 wave per SIMD: the r x r code may use all 512 VGPR+AGPRs
