@@ -1507,7 +1507,7 @@ __device__ bool ppls_block_polar_fast(const double* __restrict__ S, int64_t lds,
                                       double* __restrict__ out, int64_t ldo, int ldo_rows, double* Sl,
                                       double* sh, double* sm, double* __restrict__ gram_out,
                                       double* __restrict__ vstate, long long* tr, const PplsTeam& tm,
-                                      bool polar1, double kbound) {
+                                      bool polar1, double kbound, bool reorth) {
   constexpr int NG = R * (R + 1) / 2;
   constexpr int NW = NT / 64;
   constexpr int G = PplsWaveBlk<R>::G, GG = G * G;
@@ -1601,8 +1601,9 @@ __device__ bool ppls_block_polar_fast(const double* __restrict__ S, int64_t lds,
   const double* Sr = Sl ? Sl : S;
   const int64_t ldr = Sl ? nr : lds;
   const int sro = Sl ? i0 : 0;
-  // re-orthonormalise the carried V in sV (wave 0: Cholesky QR on lane 0 for R <= 6, else modified
-  // Gram-Schmidt with rows on lanes)
+  // the carried V in sV, re-orthonormalised (modified Gram-Schmidt, rows on lanes; wave 0) when
+  // reorth: every 8th iteration -- between, the Jacobi's rotations keep it orthonormal to a few eps
+  // per iteration (1.6 us of the C3 cross-product finalize's critical path saved 7 times in 8)
   auto load_vprev = [&]() {
     for (int e = lane; e < GG; e += 64) {
 #pragma unroll
@@ -1610,42 +1611,7 @@ __device__ bool ppls_block_polar_fast(const double* __restrict__ S, int64_t lds,
         if (e == lane + 64 * u) sV[e] = vprev[u];
     }
     ppls_wave_lds_fence();
-    if constexpr (R <= 6) {   // (at r = 10 the 165 register values spill)
-      // V <- V Rc^-1, V'V = Rc' Rc (Cholesky QR of a nearly orthonormal V: exact to rounding), on
-      // lane 0 in registers -- one step instead of the R (R - 1) / 2 dependent column sums of
-      // Gram-Schmidt; a singular V (not a carried state) restarts from the identity
-      if (vstate && lane == 0) {
-        double V[R][R], P[R * (R + 1) / 2], dinv[R];
-#pragma unroll
-        for (int a = 0; a < R; ++a)
-#pragma unroll
-          for (int k = 0; k < R; ++k) V[k][a] = sV[a * G + k];
-#pragma unroll
-        for (int b = 0; b < R; ++b)
-#pragma unroll
-          for (int a = 0; a <= b; ++a) {
-            double g = 0.0;
-#pragma unroll
-            for (int k = 0; k < R; ++k) g = fma(V[k][a], V[k][b], g);
-            P[ppls_pk(a, b)] = g;
-          }
-        const bool okc = ppls_chol_pk<R>(P, dinv);
-#pragma unroll
-        for (int k = 0; k < R; ++k)
-#pragma unroll
-          for (int j = 0; j < R; ++j) {
-            double x = V[k][j];
-#pragma unroll
-            for (int i = 0; i < j; ++i) x = fma(-V[k][i], P[ppls_pk(i, j)], x);   // V[k][i] already solved
-            V[k][j] = okc ? x * dinv[j] : (k == j ? 1.0 : 0.0);
-          }
-#pragma unroll
-        for (int a = 0; a < R; ++a)
-#pragma unroll
-          for (int k = 0; k < R; ++k) sV[a * G + k] = V[k][a];
-      }
-      ppls_wave_lds_fence();
-    } else if (vstate) {
+    if (vstate && reorth) {
       const int rt = lane % G;
       for (int j = 0; j < R; ++j) {
         double vj = sV[j * G + rt];
@@ -2208,7 +2174,7 @@ __global__ __launch_bounds__(PPLS_FIN_THREADS) void ppls_finalize_kernel(
     tm.tr = tr;
     if (qr || !ppls_block_polar_fast<R, NT>(S, ld, rows, out, ld, ld, stage_lds ? dyn_lds : nullptr, sh,
                                             sm, gacc, vs, tr, tm, (mode & 4) != 0,
-                                            (double)((mode >> 8) & 255))) {
+                                            (double)((mode >> 8) & 255), logl_index < 0 || (logl_index & 7) == 0)) {
       if (tm.rank != 0) return;   // the Householder fallback runs on one block
       ppls_block_polar(S, ld, rows, R, out, ld, ld, w2, w2 + (int64_t)rows * R, status, qr);
       if (gacc) {
