@@ -2189,11 +2189,8 @@ __global__ __launch_bounds__(PPLS_FIN_THREADS) void ppls_finalize_kernel(
     return;
   }
   if (!(mode & 2)) return;
-  // cross-product form: the Gram of [XW YC] = B'M from M = S B (the polar blocks run meanwhile)
-  if constexpr (R <= 8)
-    if (xpM) ppls_xp_gram_block<R, NT>(xpM, Wc, Cc, ldx, ldy, s_G, const_cast<double*>(G), tr);
-  ppls_stamp(tr, 8);
-  // stage theta's scalars, the Gram and W'W, C'C in LDS (all threads)
+  // stage theta's scalars, the Gram and W'W, C'C in LDS (all threads) -- first, so that these loads
+  // are not one more far round trip after the cross-product Gram's
   {
     const double* src = (const double*)sc_cur;
     double* dst = (double*)&s_cur;
@@ -2203,6 +2200,10 @@ __global__ __launch_bounds__(PPLS_FIN_THREADS) void ppls_finalize_kernel(
     if (gram_cur)
       for (int i = tid; i < R * R; i += NT) { s_WtW[i] = gram_cur[i]; s_CtC[i] = gram_cur[R * R + i]; }
   }
+  // cross-product form: the Gram of [XW YC] = B'M from M = S B (the polar blocks run meanwhile)
+  if constexpr (R <= 8)
+    if (xpM) ppls_xp_gram_block<R, NT>(xpM, Wc, Cc, ldx, ldy, s_G, const_cast<double*>(G), tr);
+  ppls_stamp(tr, 8);
   if (!gram_cur) {   // W'W and C'C by a pass over W, then one over C
     for (int mat = 0; mat < 2; ++mat) {
       const double* M = mat ? Cc : Wc;
