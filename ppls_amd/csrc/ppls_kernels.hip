@@ -1849,8 +1849,10 @@ __device__ bool ppls_block_polar_fast(const double* __restrict__ S, int64_t lds,
     }
     ppls_gram_acc<R>(o, vals);
   }
+  if (use1) ppls_stamp(tr, 3);   // (fast path) pass-3 rows done
   if (gram_out) {
     ppls_block_sum_t<NG, NW>(vals, sh);
+    if (use1) ppls_stamp(tr, 15);
     if (tm.K > 1) {   // the last member to finish sums the members' Grams in rank order
       __shared__ int last;
       double* slot = tm.part + ((int64_t)2 * tm.K) * 64;
