@@ -1834,30 +1834,8 @@ __device__ bool ppls_block_polar_fast(const double* __restrict__ S, int64_t lds,
     for (int b = 0; b < R; ++b) F[a][b] = sF[R * R + b * R + a];
 #pragma unroll
   for (int e = 0; e < NG; ++e) vals[e] = 0.0;
-  // small R: the first OB rows per thread are kept in registers and stored after the Gram's block
-  // sum (its barriers then do not sit behind the stores; measured: the stores inside the loop made
-  // it 2.6 us at C3); later rows (a team member's padding rows) and larger R store in the loop
-  constexpr int OB = R <= 6 ? (PPLS_TEAM_ROWS + NT - 1) / NT : 0;
-  double ob[OB > 0 ? OB : 1][R];
-#pragma unroll
-  for (int u = 0; u < OB; ++u) {
-    const int i = i0 + tid + u * NT;
-    if (i < o1) {
-      double xq[R];
-#pragma unroll
-      for (int k = 0; k < R; ++k) xq[k] = (i < p) ? Qs[(int64_t)k * ldq + i - qo] : 0.0;
-#pragma unroll
-      for (int j = 0; j < R; ++j) {
-        double s = 0.0;
-#pragma unroll
-        for (int k = 0; k < R; ++k) s = fma(xq[k], F[k][j], s);
-        ob[u][j] = s;
-      }
-      ppls_gram_acc<R>(ob[u], vals);
-    }
-  }
 #pragma unroll 2
-  for (int i = i0 + tid + OB * NT; i < o1; i += NT) {
+  for (int i = i0 + tid; i < o1; i += NT) {
     double xq[R], o[R];
 #pragma unroll
     for (int k = 0; k < R; ++k) xq[k] = (i < p) ? Qs[(int64_t)k * ldq + i - qo] : 0.0;
@@ -1872,20 +1850,8 @@ __device__ bool ppls_block_polar_fast(const double* __restrict__ S, int64_t lds,
     ppls_gram_acc<R>(o, vals);
   }
   if (use1) ppls_stamp(tr, 3);   // (fast path) pass-3 rows done
-  auto store_ob = [&]() {
-#pragma unroll
-    for (int u = 0; u < OB; ++u) {
-      const int i = i0 + tid + u * NT;
-      if (i < o1) {
-#pragma unroll
-        for (int j = 0; j < R; ++j) out[(int64_t)j * ldo + i] = ob[u][j];
-      }
-    }
-  };
-  if (!gram_out) store_ob();
   if (gram_out) {
     ppls_block_sum_t<NG, NW>(vals, sh);
-    store_ob();
     if (use1) ppls_stamp(tr, 15);
     if (tm.K > 1) {   // the last member to finish sums the members' Grams in rank order
       __shared__ int last;
