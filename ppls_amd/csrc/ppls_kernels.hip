@@ -1499,6 +1499,10 @@ __device__ void ppls_team_sum(const PplsTeam& tm, int phase, double (&vals)[NG],
 // warm-started from vstate (the previous iteration's V; nullptr = identity).  sm: >= 2 R^2
 // doubles of LDS.  Returns false when S is numerically rank deficient (a Cholesky pivot fails or
 // sigma_min < 1e-14 sigma_max); the caller then falls back to Householder (which reports it).
+// The staged rows live in LDS: accessed through this type the compiler emits ds_read/ds_write
+// (a plain double* to LDS compiles to flat loads and stores, which take the vector-memory path).
+typedef __attribute__((address_space(3))) double ppls_lds_double;
+
 #ifndef PPLS_REG_RMAX
 #define PPLS_REG_RMAX 10   // the polar's Cholesky factors and inverses by one thread in registers up to this R
 #endif
@@ -1545,8 +1549,9 @@ __device__ bool ppls_block_polar_fast(const double* __restrict__ S, int64_t lds,
     for (int u = 0; u < PU; ++u) {
       const int i = c0 + u * NT + tid;
       if (Sl && i < i1) {
+        ppls_lds_double* L = (ppls_lds_double*)Sl;
 #pragma unroll
-        for (int k = 0; k < R; ++k) Sl[k * nr + (i - i0)] = x[u][k];
+        for (int k = 0; k < R; ++k) L[k * nr + (i - i0)] = x[u][k];
       }
       ppls_gram_acc<R>(x[u], vals);
     }
@@ -1704,22 +1709,26 @@ __device__ bool ppls_block_polar_fast(const double* __restrict__ S, int64_t lds,
       for (int b = 0; b < R; ++b) M[a][b] = sF[b * R + a];
 #pragma unroll
     for (int e = 0; e < NG; ++e) vals[e] = 0.0;
+    auto pass2 = [&](auto SrP, auto QwP) {
 #pragma unroll 2
-    for (int i = i0 + tid; i < i1; i += NT) {
-      double xq[R], qv[R];
+      for (int i = i0 + tid; i < i1; i += NT) {
+        double xq[R], qv[R];
 #pragma unroll
-      for (int k = 0; k < R; ++k) xq[k] = Sr[(int64_t)k * ldr + i - sro];
+        for (int k = 0; k < R; ++k) xq[k] = SrP[(int64_t)k * ldr + i - sro];
 #pragma unroll
-      for (int j = 0; j < R; ++j) {
-        double s = 0.0;
+        for (int j = 0; j < R; ++j) {
+          double s = 0.0;
 #pragma unroll
-        for (int k = 0; k <= j; ++k) s = fma(xq[k], M[k][j], s);
-        qv[j] = s;
+          for (int k = 0; k <= j; ++k) s = fma(xq[k], M[k][j], s);
+          qv[j] = s;
+        }
+        ppls_gram_acc<R>(qv, vals);
+#pragma unroll
+        for (int j = 0; j < R; ++j) QwP[(int64_t)j * ldq + i - qo] = qv[j];
       }
-      ppls_gram_acc<R>(qv, vals);
-#pragma unroll
-      for (int j = 0; j < R; ++j) Qw[(int64_t)j * ldq + i - qo] = qv[j];
-    }
+    };
+    if (Sl) pass2((const ppls_lds_double*)Sl, (ppls_lds_double*)Sl);
+    else pass2(Sr, Qw);
   }
   ppls_stamp(tr, 15);
   ppls_block_sum_t<NG, NW>(vals, sh);
@@ -1834,21 +1843,25 @@ __device__ bool ppls_block_polar_fast(const double* __restrict__ S, int64_t lds,
     for (int b = 0; b < R; ++b) F[a][b] = sF[R * R + b * R + a];
 #pragma unroll
   for (int e = 0; e < NG; ++e) vals[e] = 0.0;
+  auto pass3 = [&](auto QsP) {
 #pragma unroll 2
-  for (int i = i0 + tid; i < o1; i += NT) {
-    double xq[R], o[R];
+    for (int i = i0 + tid; i < o1; i += NT) {
+      double xq[R], o[R];
 #pragma unroll
-    for (int k = 0; k < R; ++k) xq[k] = (i < p) ? Qs[(int64_t)k * ldq + i - qo] : 0.0;
+      for (int k = 0; k < R; ++k) xq[k] = (i < p) ? QsP[(int64_t)k * ldq + i - qo] : 0.0;
 #pragma unroll
-    for (int j = 0; j < R; ++j) {
-      double s = 0.0;
+      for (int j = 0; j < R; ++j) {
+        double s = 0.0;
 #pragma unroll
-      for (int k = 0; k < R; ++k) s = fma(xq[k], F[k][j], s);
-      o[j] = s;
-      out[(int64_t)j * ldo + i] = s;
+        for (int k = 0; k < R; ++k) s = fma(xq[k], F[k][j], s);
+        o[j] = s;
+        out[(int64_t)j * ldo + i] = s;
+      }
+      ppls_gram_acc<R>(o, vals);
     }
-    ppls_gram_acc<R>(o, vals);
-  }
+  };
+  if (Sl) pass3((const ppls_lds_double*)Sl);   // Qs is the staged S (fast path) or Q1 in LDS
+  else pass3(Qs);
   if (use1) ppls_stamp(tr, 3);   // (fast path) pass-3 rows done
   if (gram_out) {
     ppls_block_sum_t<NG, NW>(vals, sh);
