@@ -29,7 +29,7 @@
                           // C3 tile 22.9 -> 21.7 us, C5 202 -> 200 us; profiles/r4_xprod_depth_ab_*.txt)
 #endif
 #ifndef PPLS_XP_WAVES
-#define PPLS_XP_WAVES 4   // waves (rows of S per RW) per tile-kernel workgroup, sharing each staged B tile
+#define PPLS_XP_WAVES 0   // waves per tile-kernel workgroup sharing each staged B tile (0: ppls_xp_waves)
 #endif
 #ifndef PPLS_XP_TPB
 #define PPLS_XP_TPB 0     // 128-column sub-tiles per staged B tile and workgroup barrier (0: ppls_xp_tpb)
@@ -40,6 +40,9 @@ namespace {
 // Sub-tiles per staged B tile (one workgroup barrier each): 2 for r <= 5 (C3: tile 23.5 -> 22.9 us),
 // else 1 (C5, r = 10: 2 is 6 % slower, 4 is slower at C3; profiles/r4_xprod_tpb_ab.txt).
 constexpr int ppls_xp_tpb(int r) { return PPLS_XP_TPB > 0 ? PPLS_XP_TPB : (r <= 5 ? 2 : 1); }
+// Waves per workgroup: 8 for r <= 5 (C3 tile 21.7 -> 21.5 us), else 4 (C5: 8 is 1-3 % slower, 2 is
+// 25 % slower everywhere; profiles/r4_xprod_waves8_depth1_ab.txt, r4_xprod_waves2_ab.txt).
+constexpr int ppls_xp_waves(int r) { return PPLS_XP_WAVES > 0 ? PPLS_XP_WAVES : (r <= 5 ? 8 : 4); }
 
 // Values a lane holds after ppls_rs's six butterfly levels on M values (M > 64: several).
 constexpr int ppls_rs_left(int m, int l) { return l == 6 ? m : (m == 1 ? 1 : ppls_rs_left((m + 1) / 2, l + 1)); }
@@ -58,7 +61,7 @@ __device__ __forceinline__ void ppls_xprod_tile_phase(const double* const (&srow
   typedef double d2v __attribute__((ext_vector_type(2)));
   constexpr int TP = ppls_xp_tpb(R);         // 128-column sub-tiles per staged tile (one barrier each)
   constexpr int TV = TP * R * 64;            // 16-B values of B per staged tile
-  constexpr int NTH = 64 * PPLS_XP_WAVES;
+  constexpr int NTH = 64 * ppls_xp_waves(R);
   constexpr int NB = (TV + NTH - 1) / NTH;   // 16-B B loads per thread and tile
   constexpr int D = PPLS_XP_DEPTH;           // S tiles in flight per wave (register ring)
   const int tid = threadIdx.x;
@@ -190,7 +193,7 @@ __device__ __forceinline__ void ppls_xprod_tile_body(const double* __restrict__ 
 }
 
 template <int R, int RW, bool NT>
-__global__ __launch_bounds__(64 * PPLS_XP_WAVES) void ppls_xprod_tile_kernel(const double* __restrict__ S, int ldx, int ldy,
+__global__ __launch_bounds__(64 * ppls_xp_waves(R)) void ppls_xprod_tile_kernel(const double* __restrict__ S, int ldx, int ldy,
                                                               const double* __restrict__ Wp,
                                                               const double* __restrict__ Cp,
                                                               const PplsScalars* __restrict__ sc,
@@ -198,9 +201,9 @@ __global__ __launch_bounds__(64 * PPLS_XP_WAVES) void ppls_xprod_tile_kernel(con
                                                               const int* __restrict__ stop) {
   if (stop && *stop) return;   // em_run converged at an earlier iteration
   __shared__ double sB[2 * R * 128 * ppls_xp_tpb(R)];
-  __shared__ double sm[PPLS_XP_WAVES][RW * 2 * R];
+  __shared__ double sm[ppls_xp_waves(R)][RW * 2 * R];
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t i0 = ((int64_t)blockIdx.x * PPLS_XP_WAVES + wave) * RW;   // this wave's first row of S
+  const int64_t i0 = ((int64_t)blockIdx.x * ppls_xp_waves(R) + wave) * RW;   // this wave's first row of S
   ppls_xprod_tile_body<R, RW, NT>(S, ldx, ldy, Wp, Cp, sc, stats, M, sB, sm[wave], i0, lane);
 }
 
@@ -247,12 +250,13 @@ template <int R, int RW>
 hipError_t launch_tile(const double* S, int ldx, int ldy, const double* Wp, const double* Cp, const PplsScalars* sc,
                        double* stats, double* M, const int* stop, hipStream_t st) {
   const int P = ldx + ldy;
-  const unsigned blocks = (unsigned)((P + PPLS_XP_WAVES * RW - 1) / (PPLS_XP_WAVES * RW));
+  constexpr int NWV = ppls_xp_waves(R);
+  const unsigned blocks = (unsigned)((P + NWV * RW - 1) / (NWV * RW));
   if (8.0 * P * (double)P > 200.0 * (1 << 20))   // S beyond the Infinity Cache: non-temporal loads
-    hipLaunchKernelGGL((ppls_xprod_tile_kernel<R, RW, true>), dim3(blocks), dim3(64 * PPLS_XP_WAVES), 0, st, S, ldx, ldy, Wp, Cp, sc,
+    hipLaunchKernelGGL((ppls_xprod_tile_kernel<R, RW, true>), dim3(blocks), dim3(64 * NWV), 0, st, S, ldx, ldy, Wp, Cp, sc,
                        stats, M, stop);
   else
-    hipLaunchKernelGGL((ppls_xprod_tile_kernel<R, RW, false>), dim3(blocks), dim3(64 * PPLS_XP_WAVES), 0, st, S, ldx, ldy, Wp, Cp,
+    hipLaunchKernelGGL((ppls_xprod_tile_kernel<R, RW, false>), dim3(blocks), dim3(64 * NWV), 0, st, S, ldx, ldy, Wp, Cp,
                        sc, stats, M, stop);
   return hipGetLastError();
 }
