@@ -2121,7 +2121,8 @@ int ppls_meta_ppls(ppls_ctx* c, int npop, const int64_t* pop_local, const int64_
 
 // variances.PPLS_simult (EM_W_multi.R:830-860).  X'X (or Y'Y) once on MFMA for all components,
 // Cxt = X' mu in one HBM pass, then per component the p x p B_exp - SSt_exp on the device and its
-// inverse by rocSOLVER getrf/getri (R's solve()).  Data-dependent sums are all-reduced over ranks.
+// inverse by rocSOLVER: Cholesky potrf/potri of -(B_exp - SSt_exp), or getrf/getri (R's solve())
+// when one is not positive definite.  Data-dependent sums are all-reduced over ranks.
 int ppls_variances(ppls_ctx* c, const double* mu, const double* Cdiag, double sigE, int a, int xory, double* W,
                    double* B_exp, double* varMatrix, double* SSt_exp, double* SSt_star, double* seLoad) {
   if (!c) return PPLS_E_ARG;
