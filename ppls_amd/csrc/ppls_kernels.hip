@@ -1361,7 +1361,7 @@ __device__ void ppls_matmul_wave(const double* sA, const double* sB, double* sC)
 // the column dots are 8-lane DPP sums.  Same rotation and stopping rule as ppls_small_polar_n
 // (ppls_math.h).  Wave-uniform.
 template <int R>
-__device__ int ppls_jacobi_wave(double* sA, double* sV) {
+__device__ __forceinline__ int ppls_jacobi_wave(double* sA, double* sV) {
   constexpr int N = R + (R & 1);
   constexpr int G = PplsWaveBlk<R>::G;
   constexpr int RPL = (R + 7) / 8;                  // rows per lane (G = 16 layout for R > 8)
