@@ -96,9 +96,14 @@ const char* ppls_last_error(const ppls_ctx* ctx);
  *       "xprod" (statistics of ppls_em_run / ppls_em_iterate: 0 (default) one streaming sweep over X, Y
  *                per iteration; 1 from the cross-products S = [X Y]'[X Y], formed once per data set
  *                on MFMA and all-reduced once, after which an iteration reads S (8 (p+q)^2 bytes) and
- *                needs no collective; -1 auto: S when a cost model of max_steps iterations says so;
- *                S stays resident (8 (p+q)^2 bytes) until the data change, 0 is set again, or
- *                ppls_xprod_release),
+ *                needs no collective; -1 auto: S when a cost model of max_steps iterations says so
+ *                and S with its Gram partials fits the smallest free HBM over all ranks (measured when
+ *                the data were loaded; falls back to streaming, on every rank alike, if S cannot be
+ *                allocated); S stays resident (8 (p+q)^2 bytes) until the data change, xprod goes from
+ *                non-zero to 0 (not for an S of ppls_xprod_prepare), or ppls_xprod_release; 0 is
+ *                refused (PPLS_E_STATE) during an ppls_em_begin session that reads S),
+ *       "vorth" (the finalize re-orthonormalises the Jacobi warm start it carries between
+ *                iterations every vorth-th iteration: 1 .. 255, default 8),
  *       "xprod_rw" (rows of S per wave of the cross-product tile kernel: 0 auto, 1, 2, 4, 8),
  *       "xprod_fuse" (1, default: the finalize after a cross-product step forms the 2r x 2r Gram
  *                     itself when r <= 8 and p + q <= 6144; 0: a separate Gram kernel),
@@ -120,7 +125,12 @@ int ppls_comm_init(ppls_ctx* ctx, int nranks, int rank, const char id[128]);
 typedef int (*ppls_reduce_fn)(void* user, double* buf, int64_t count);
 int ppls_set_reducer(ppls_ctx* ctx, ppls_reduce_fn fn, void* user);
 
-/* ---- data (X: n_local x p, Y: n_local x q; this rank's rows of an n_total-sample problem) ---- */
+/* ---- data (X: n_local x p, Y: n_local x q; this rank's rows of an n_total-sample problem) ----
+ * A NaN or Inf anywhere in X or Y (on any rank) -> PPLS_E_ARG on every rank, with the data dropped:
+ * the reference's svd() in orth() stops on non-finite data (EM_W_multi.R:732-733).  It is detected
+ * from the all-reduced sums of squares, so all ranks return together (no rank waits alone in a
+ * collective).  Fits (ppls_em_run, ppls_em_begin, ppls_ppls*, ppls_meta_ppls) refuse an all-zero X
+ * or Y with PPLS_E_ARG: the reference's fit stops on the NA increment that data produce. */
 int ppls_set_data(ppls_ctx* ctx, const double* X, const double* Y, int64_t n_local, int p, int q,
                   int layout, int64_t n_total);
 /* simulC-model synthetic data generated on the device (src/loglC.cpp:268-315, r >= 1):
@@ -143,7 +153,9 @@ int ppls_loglik(ppls_ctx* ctx, const ppls_theta* th, int r, double* out);
 /* PPLS_simult's loop and tail (EM_W_multi.R:773-806) from an explicit theta0 (in `th`).
  * On return `th` holds the canonicalised estimates (:794-799), loglik[0..*steps_done-1] the
  * log-likelihood trace, and eout (nullable) Expect_M at the un-canonicalised final theta (:802).
- * Returns PPLS_OK; *negative_increment = 1 where the reference warns (:801). */
+ * Returns PPLS_OK; *negative_increment = 1 where the reference warns (:801).  A NaN log-likelihood
+ * increment under a finite atol is R's `if (NA < atol)` error (:792): the run stops there and
+ * returns PPLS_E_NUMERIC, as it does for any non-finite trace entry or estimate -- never PPLS_OK. */
 int ppls_em_run(ppls_ctx* ctx, ppls_theta* th, int r, int max_steps, double atol, int type,
                 double* loglik, int* steps_done, int* negative_increment, ppls_expect* eout);
 

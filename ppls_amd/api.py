@@ -942,17 +942,18 @@ def PPLS_simult(X, Y, a, EMsteps=10, atol=1e-4, type=("SVD", "QR"), init=None, c
     if init is None:
         rng = kw.get("rng")
         rng = rng if rng is not None else np.random.default_rng(kw.get("seed"))
-        f0 = None
+        f0, last = None, None
         for _ in range(3):   # f0 = try(PPLS(...)): retried only when PPLS raises (:762-764)
             try:
                 with warnings.catch_warnings():
                     warnings.simplefilter("ignore")
                     f0 = PPLS(None, None, a, 20, 1e-4, "random", rng=rng, ctx=ctx)
                 break
-            except PplsError:
-                f0 = None
-        if f0 is None:
-            raise PplsError(-5, "PPLS initialisation failed three times")
+            except PplsError as e:
+                f0, last = None, e
+        if f0 is None:   # R: f0 is a try-error and `f0$W` stops the call (:765)
+            raise PplsError(last.code, f"f0 = try(PPLS(X, Y, a, 20, 1e-4, 'random')) failed three times "
+                                       f"(EM_W_multi.R:762-765): {last}")
         if len(f0["B"]) < a:
             # R carries the truncated f0 on and fails at W.[, rotLoad] (:773-776)
             raise PplsError(-1, f"subscript out of bounds: PPLS returned {len(f0['B'])} of {a} components")

@@ -65,6 +65,10 @@ struct ppls_ctx {
   double* Y = nullptr;
   double* ssq = nullptr;       // {||X||^2, ||Y||^2} (global)
   double ssq_host[2] = {0, 0};
+  // the smallest free HBM over all ranks when the data were loaded (all-reduced beside ||X||^2,
+  // ||Y||^2, so every rank sees the same value): the cross-product form's memory gate
+  double mem_free_min = 0.0;
+  double* flag = nullptr;      // 8 doubles for small agreement all-reduces (allocated with the data)
   // per-r state
   int r_alloc = 0;
   double* W[2] = {nullptr, nullptr};
@@ -121,6 +125,9 @@ struct ppls_ctx {
   bool xp_active = false;   // statistics steps of the current run read S
   bool xp_pending_gram = false;   // the last statistics step left the Gram B'M to the next finalize
   int xprod_fuse = 1;       // option "xprod_fuse": the finalize forms the Gram (r <= 8, P <= 6144)
+  bool xp_explicit = false; // S was formed by ppls_xprod_prepare: kept until ppls_xprod_release / new data
+  int vorth = 8;            // option "vorth": the finalize re-orthonormalises its carried Jacobi V every
+                            // vorth-th iteration (1 = every iteration)
   double* xp_S = nullptr;
   double* xp_M = nullptr;   // M = S blockdiag(W, C), P x 2r scratch
   double xp_setup_ms = 0.0; // last formation of S: Gram kernel (HIP events), and with the all-reduce
@@ -209,6 +216,9 @@ int check_theta(ppls_ctx* c, const ppls_theta* th, int r) {
   if (r < 1 || r > PPLS_RMAX) return fail(c, PPLS_E_ARG, "r=%d outside [1,%d]", r, PPLS_RMAX);
   if (!(th->sigE > 0) || !(th->sigF > 0) || !(th->sigH >= 0))
     return fail(c, PPLS_E_ARG, "variances must be positive");
+  bool fin = std::isfinite(th->sigE) && std::isfinite(th->sigF) && std::isfinite(th->sigH);
+  for (int k = 0; k < r; ++k) fin = fin && std::isfinite(th->B[k]) && std::isfinite(th->sigT[k]);
+  if (!fin) return fail(c, PPLS_E_ARG, "theta has non-finite B, sigT or variances");
   // PPLS: stopifnot(ncol(X) >= nr_comp, ncol(Y) >= nr_comp)  (EM_W_multi.R:245)
   if (c && c->p > 0 && (c->p < r || c->q < r))
     return fail(c, PPLS_E_ARG, "ncol(X)=%d, ncol(Y)=%d must be >= number of components %d", c->p, c->q, r);
@@ -608,7 +618,7 @@ int finalize(ppls_ctx* c, int r, int cur, int nxt, int logl_index, int type, int
   f.work = c->work;
   f.status = c->status;
   f.qr = type == PPLS_ORTH_QR ? 1 : 0;
-  f.mode = 3 | (c->polar1 ? 4 : 0) | (c->exact_gram ? 16 : 0) | (polar1_bound(c, r) << 8);
+  f.mode = 3 | (c->polar1 ? 4 : 0) | (c->exact_gram ? 16 : 0) | (polar1_bound(c, r) << 8) | (c->vorth << 16);
   f.trace = c->ftrace;
   f.gram_cur = c->gram[cur];
   f.gram_nxt = c->gram[nxt];
@@ -652,6 +662,35 @@ int gram_splits(ppls_ctx* c, int p, int64_t n) {
   return nsplit;
 }
 
+int xprod_setup(ppls_ctx* c);
+bool xprod_choose(ppls_ctx* c, int max_steps, int r);
+
+// Rows per rank the cross-product setup is sized for: the same on every rank (ceil(n_total / nranks)).
+int64_t xprod_rows(const ppls_ctx* c) { return (c->n_total + c->nranks - 1) / c->nranks; }
+
+// HBM the cross-product form allocates: S (8 P^2 B), the Gram partials while S is formed
+// (gram_splits x 8 P^2 B) and M (P x 2 RMAX doubles).
+double xprod_bytes(ppls_ctx* c) {
+  const int P = c->ldx + c->ldy;
+  const double PP = (double)P * P;
+  return 8.0 * PP * (1.0 + gram_splits(c, P, xprod_rows(c))) + 16.0 * P * PPLS_RMAX;
+}
+
+// Start a run (or session) on the cross-products when the policy picks them.  In auto mode (-1) a
+// failed allocation of S -- which xprod_setup reports on every rank alike -- falls back to streaming.
+int xprod_begin(ppls_ctx* c, int steps, int r) {
+  c->xp_active = c->seg_rows < 0 && xprod_choose(c, steps, r);
+  if (!c->xp_active) return PPLS_OK;
+  const int rc = xprod_setup(c);
+  if (rc == PPLS_OK) return PPLS_OK;
+  c->xp_active = false;
+  if (rc == PPLS_E_NOMEM && c->xprod < 0) {
+    c->err.clear();
+    return PPLS_OK;
+  }
+  return rc;
+}
+
 // Cross-product form (ppls_xprod.hip): S = [X Y]'[X Y] over the local rows on MFMA (fp64 products
 // of the stored values, exact for fp32 storage), summed over ranks by ONE all-reduce of P^2 doubles;
 // afterwards an iteration needs no collective at all (every rank holds the same S and theta).
@@ -661,13 +700,34 @@ int xprod_setup(ppls_ctx* c) {
   const size_t PP = (size_t)P * P;
   int rc;
   const auto t0 = std::chrono::steady_clock::now();
-  if ((rc = dalloc(c, &c->xp_S, PP))) return rc;
+  // S and the Gram partials; with collectives every rank must know that all ranks allocated them
+  // before anyone enters the all-reduce of S (a rank that returned here alone would leave the
+  // others waiting in it), so the allocation outcome is all-reduced first
+  const int nsplit = gram_splits(c, P, xprod_rows(c));
+  double* part = nullptr;
+  int rc_alloc = dalloc(c, &c->xp_S, PP);
+  if (!rc_alloc && c->n_local > 0) rc_alloc = dalloc(c, &part, (size_t)nsplit * PP);
+  if (c->nranks > 1 || c->reducer) {
+    const double f = rc_alloc ? 1.0 : 0.0;
+    double tot = 0.0;
+    HIPCHK(c, hipMemcpyAsync(c->flag, &f, sizeof f, hipMemcpyHostToDevice, c->stream));
+    if ((rc = allreduce(c, c->flag, 1))) { dfree(part); dfree(c->xp_S); return rc; }
+    HIPCHK(c, hipMemcpyAsync(&tot, c->flag, sizeof tot, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (tot > 0.0) {
+      dfree(part);
+      dfree(c->xp_S);
+      return fail(c, PPLS_E_NOMEM, "cross-products S: %d rank(s) could not allocate %.3g GB of S and Gram partials",
+                  (int)tot, (double)PP * 8.0 * (1.0 + nsplit) / 1e9);
+    }
+  } else if (rc_alloc) {
+    dfree(part);
+    dfree(c->xp_S);
+    return rc_alloc;
+  }
   c->xp_setup_ms = 0.0;
   if (c->n_local > 0) {
-    const int nsplit = gram_splits(c, P, c->n_local);
     c->xp_nsplit = nsplit;
-    double* part = nullptr;
-    if ((rc = dalloc(c, &part, (size_t)nsplit * PP))) return rc;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     hipError_t e = hipEventCreate(&e0);
     if (e == hipSuccess) e = hipEventCreate(&e1);
@@ -699,16 +759,16 @@ int xprod_setup(ppls_ctx* c) {
 
 // Whether a run of max_steps iterations reads S: option xprod = 1 always, 0 never, -1 when the
 // modelled cost of forming S plus max_steps + 1 passes over it undercuts max_steps + 1 streaming
-// sweeps.  The model and the size gate use only global sizes (n_total / nranks, P; never this
-// rank's own row count or device memory), so every rank of a sharded run takes the same path and
-// issues the same collectives.  Size gate: S and at most one S-sized set of Gram partials, 16 P^2
-// bytes, within PPLS_XPROD_MAX_BYTES (64 GiB, below a quarter of an MI355X's 288 GB: P <= 65,536).
-#define PPLS_XPROD_MAX_BYTES (64.0 * 1024 * 1024 * 1024)
+// sweeps and S fits.  The model and the memory gate use only values every rank shares (n_total /
+// nranks, P, and the smallest free HBM over all ranks, all-reduced when the data were loaded), so
+// every rank of a sharded run takes the same path and issues the same collectives.  Memory gate:
+// S, its Gram partials and M (xprod_bytes) within the smallest free HBM less max(1 GiB, 5 %).
 bool xprod_choose(ppls_ctx* c, int max_steps, int r) {
   if (c->xprod == 0) return false;
+  if (c->xprod == 1) return true;   // forced: xprod_setup reports a failed allocation (all ranks alike)
+  if (!c->xp_ready && xprod_bytes(c) > c->mem_free_min - std::max(1073741824.0, 0.05 * c->mem_free_min))
+    return false;
   const double P = (double)(c->ldx + c->ldy);
-  if (16.0 * P * P > PPLS_XPROD_MAX_BYTES) return false;
-  if (c->xprod == 1) return true;
   const double n = (double)((c->n_total + c->nranks - 1) / c->nranks);
   const double esz = c->dtype ? 4.0 : 8.0;
   // the split sweep reads X, Y once; the panel sweep (wide p, r > 8, fp32 storage) twice -- also
@@ -780,6 +840,7 @@ int check_status(ppls_ctx* c) {
 
 void xprod_free(ppls_ctx* c) {
   c->xp_ready = false;
+  c->xp_explicit = false;
   c->xp_active = false;
   dfree(c->xp_S);
   dfree(c->xp_M);
@@ -790,7 +851,8 @@ int compute_ssq(ppls_ctx* c) {
   xprod_free(c);   // data or communicator changed: the cross-products are stale
 
   const int nb = 1024;
-  if ((rc = dalloc(c, &c->scratch, nb + 8))) return rc;
+  const int nred = 2 + c->nranks;   // {||X||^2, ||Y||^2, free HBM of rank 0, 1, ...}
+  if ((rc = dalloc(c, &c->scratch, (size_t)nb + nred))) return rc;
   HIPCHK(c, hipMemsetAsync(c->ssq, 0, 2 * sizeof(double), c->stream));
   if (c->n_local > 0 && c->dtype) {
     HIPCHK(c, ppls_launch_sumsq_f32((const float*)c->X, c->n_local * c->ldx, c->scratch, nb, c->ssq, c->stream));
@@ -799,10 +861,56 @@ int compute_ssq(ppls_ctx* c) {
     HIPCHK(c, ppls_launch_sumsq(c->X, c->n_local * c->ldx, c->scratch, nb, c->ssq, 0, c->stream));
     HIPCHK(c, ppls_launch_sumsq(c->Y, c->n_local * c->ldy, c->scratch, nb, c->ssq + 1, 0, c->stream));
   }
-  if ((rc = allreduce(c, c->ssq, 2))) return rc;
-  HIPCHK(c, hipMemcpyAsync(c->ssq_host, c->ssq, 2 * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  // one all-reduce carries the sums of squares and every rank's free HBM (in its own slot), so the
+  // cross-product form's memory gate (xprod_choose) is the same on every rank
+  size_t mfree = 0, mtot = 0;
+  HIPCHK(c, hipMemGetInfo(&mfree, &mtot));
+  std::vector<double> slots((size_t)c->nranks, 0.0);
+  slots[(size_t)c->rank] = (double)mfree;
+  double* red = c->scratch + nb;
+  HIPCHK(c, hipMemcpyAsync(red, c->ssq, 2 * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(red + 2, slots.data(), sizeof(double) * slots.size(), hipMemcpyHostToDevice, c->stream));
+  if ((rc = allreduce(c, red, (size_t)nred))) return rc;
+  HIPCHK(c, hipMemcpyAsync(c->ssq, red, 2 * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
+  std::vector<double> h((size_t)nred);
+  HIPCHK(c, hipMemcpyAsync(h.data(), red, sizeof(double) * nred, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->ssq_host[0] = h[0];
+  c->ssq_host[1] = h[1];
+  c->mem_free_min = h[2];
+  for (int k = 1; k < c->nranks; ++k) c->mem_free_min = std::min(c->mem_free_min, h[(size_t)2 + k]);
   dfree(c->scratch);
+  return PPLS_OK;
+}
+
+// Non-finite data: R's svd() in orth() refuses X'mu_T with NaN/Inf entries (EM_W_multi.R:732-733),
+// so the reference stops on such data.  Detected from the all-reduced sums of squares (a NaN or Inf
+// element -- or values past ~1.3e154, whose squares overflow -- makes the global sum non-finite), so
+// every rank of a sharded run reaches the same verdict and none is left waiting in a collective.
+int check_finite_data(ppls_ctx* c) {
+  for (int m = 0; m < 2; ++m)
+    if (!std::isfinite(c->ssq_host[m])) {
+      c->have_data = false;
+      xprod_free(c);
+      return fail(c, PPLS_E_ARG,
+                  "%c contains NaN or Inf (its sum of squares over all ranks is %g; values beyond 1.3e154 "
+                  "also overflow it): the reference's svd() in orth() stops on non-finite data "
+                  "(EM_W_multi.R:732-733)",
+                  m ? 'Y' : 'X', c->ssq_host[m]);
+    }
+  return PPLS_OK;
+}
+
+// A fit needs ssq(X) > 0 and ssq(Y) > 0: on an all-zero block the reference's first EM step
+// divides 0 by 0 (EMstepC_fast's loading normalisation, loglC.cpp:357,385), its log-likelihood
+// increment is NA and `if (NA < atol)` stops the fit (EM_W_multi.R:173, :792).
+int check_fit_data(ppls_ctx* c) {
+  for (int m = 0; m < 2; ++m)
+    if (!(c->ssq_host[m] > 0.0))
+      return fail(c, PPLS_E_ARG,
+                  "%c is all zero (sum of squares over all ranks = 0): the PPLS model is degenerate and the "
+                  "reference's fit stops on the NA log-likelihood increment it produces (EM_W_multi.R:173,792)",
+                  m ? 'Y' : 'X');
   return PPLS_OK;
 }
 
@@ -827,6 +935,7 @@ int alloc_data(ppls_ctx* c, int64_t n_local, int p, int q, int64_t n_total) {
   HIPCHK(c, hipMemsetAsync((char*)c->X + xb, 0, ((xb + 7) / 8 + 64) * 8 - xb, c->stream));
   HIPCHK(c, hipMemsetAsync((char*)c->Y + yb, 0, ((yb + 7) / 8 + 64) * 8 - yb, c->stream));
   if (!c->ssq && (rc = dalloc(c, &c->ssq, 2))) return rc;
+  if (!c->flag && (rc = dalloc(c, &c->flag, 8))) return rc;
   c->r_alloc = 0;   // force per-r buffers to be re-sized for the new shape
   dfree(c->part);
   dfree(c->Z);
@@ -857,6 +966,14 @@ void canonicalize(ppls_theta* th, int p, int q, int r) {
     th->B[j] = B[j];
     th->sigT[j] = T[j];
   }
+}
+
+bool theta_finite(const ppls_theta* th, int p, int q, int r) {
+  bool ok = std::isfinite(th->sigE) && std::isfinite(th->sigF) && std::isfinite(th->sigH);
+  for (int k = 0; k < r && ok; ++k) ok = std::isfinite(th->B[k]) && std::isfinite(th->sigT[k]);
+  for (size_t e = 0; e < (size_t)p * r && ok; ++e) ok = std::isfinite(th->W[e]);
+  for (size_t e = 0; e < (size_t)q * r && ok; ++e) ok = std::isfinite(th->C[e]);
+  return ok;
 }
 
 // Host polar factor / QR factor of the p x r matrix S (ld p): sequential Householder QR, then the
@@ -947,7 +1064,7 @@ void ppls_ctx_destroy(ppls_ctx* c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->comm) ncclCommDestroy(c->comm);
-  dfree(c->X); dfree(c->Y); dfree(c->ssq);
+  dfree(c->X); dfree(c->Y); dfree(c->ssq); dfree(c->flag);
   for (int i = 0; i < 2; ++i) { dfree(c->W[i]); dfree(c->C[i]); dfree(c->sc[i]); dfree(c->gram[i]); }
   dfree(c->vstate);
   dfree(c->mom); dfree(c->stats); dfree(c->part); dfree(c->Z); dfree(c->mu); dfree(c->loglik);
@@ -1035,8 +1152,21 @@ int ppls_set_option(ppls_ctx* c, const char* key, int64_t value) {
     c->nt_loads = (int)value;
   } else if (!strcmp(key, "xprod")) {
     if (value < -1 || value > 1) return fail(c, PPLS_E_ARG, "xprod must be -1 (auto), 0 (stream X, Y) or 1 (cross-products)");
+    // the path of an ppls_em_begin session is fixed at em_begin: no switch to streaming under it
+    if (value == 0 && c->em_active && c->xp_active)
+      return fail(c, PPLS_E_STATE, "xprod = 0 during an ppls_em_begin session on the cross-products: end it first "
+                                   "(ppls_em_begin again, or any fit entry point)");
+    const int was = c->xprod;
     c->xprod = (int)value;
-    if (value == 0) xprod_free(c);   // streaming from now on: S's 8 (p+q)^2 bytes go back
+    // streaming from now on: S's 8 (p+q)^2 bytes go back -- unless S came from ppls_xprod_prepare
+    // (kept for variances() and later runs until ppls_xprod_release)
+    if (value == 0 && was != 0 && !c->xp_explicit) {
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+      xprod_free(c);
+    }
+  } else if (!strcmp(key, "vorth")) {
+    if (value < 1 || value > 255) return fail(c, PPLS_E_ARG, "vorth must be in [1, 255]");
+    c->vorth = (int)value;
   } else if (!strcmp(key, "xprod_fuse")) {
     c->xprod_fuse = value ? 1 : 0;
   } else if (!strcmp(key, "var_chol")) {
@@ -1155,7 +1285,8 @@ int ppls_set_data(ppls_ctx* c, const double* X, const double* Y, int64_t n_local
   }
   HIPCHK(c, hipStreamSynchronize(c->stream));
   c->have_data = true;
-  return compute_ssq(c);
+  if ((rc = compute_ssq(c))) return rc;
+  return check_finite_data(c);
 }
 
 int ppls_generate_synthetic(ppls_ctx* c, int64_t n_total, int64_t row0, int64_t n_local, int p, int q,
@@ -1194,7 +1325,8 @@ int ppls_generate_synthetic(ppls_ctx* c, int64_t n_total, int64_t row0, int64_t 
   dfree(Wt); dfree(Ct); dfree(TU);
   if (e != hipSuccess) return fail(c, PPLS_E_HIP, "synthetic generation: %s", hipGetErrorString(e));
   c->have_data = true;
-  return compute_ssq(c);
+  if ((rc = compute_ssq(c))) return rc;
+  return check_finite_data(c);
 }
 
 int ppls_philox4x32_10(ppls_ctx* c, const uint32_t* ctr, int64_t count, uint64_t key, uint32_t* out) {
@@ -1413,6 +1545,8 @@ int ppls_em_run(ppls_ctx* c, ppls_theta* th, int r, int max_steps, double atol, 
   if ((rc = check_theta(c, th, r))) return rc;
   if (max_steps < 1) return fail(c, PPLS_E_ARG, "EMsteps must be >= 1");
   if (type != PPLS_ORTH_SVD && type != PPLS_ORTH_QR) return fail(c, PPLS_E_ARG, "type must be SVD (0) or QR (1)");
+  if ((rc = check_fit_data(c))) return rc;
+  if (!theta_finite(th, c->p, c->q, r)) return fail(c, PPLS_E_ARG, "theta0 has non-finite entries");
   HIPCHK(c, hipSetDevice(c->device));
   if ((rc = ensure_r(c, r, max_steps))) return rc;
   // :773-778 canonicalise theta0 (on a copy; th is overwritten with the estimates at the end)
@@ -1427,8 +1561,7 @@ int ppls_em_run(ppls_ctx* c, ppls_theta* th, int r, int max_steps, double atol, 
   const bool want_mu = eout && (eout->mu_T || eout->mu_U);
   const bool do_check = !(atol == -INFINITY);   // atol = -Inf: the stop rule never fires
   // statistics from the cross-products S (option xprod; formed here if needed, outside the loop)
-  c->xp_active = c->seg_rows < 0 && xprod_choose(c, max_steps, r);
-  if (c->xp_active && (rc = xprod_setup(c))) { c->xp_active = false; return rc; }
+  if ((rc = xprod_begin(c, max_steps, r))) return rc;
   // The stop rule (EM_W_multi.R:792) runs on the device: the finalize that sees
   // logl[i] - logl[i-1] < atol sets a flag, and every later kernel of the run exits at once, so the
   // host enqueues iterations without a per-iteration read-back.  It polls the flag's host-mapped
@@ -1479,12 +1612,17 @@ int ppls_em_run(ppls_ctx* c, ppls_theta* th, int r, int max_steps, double atol, 
   HIPCHK(c, hipStreamSynchronize(c->stream));
   // the iteration the run ended at: the finalize of sweep s_stop saw the stop rule fire, so
   // theta_{s_stop - 1} (slot (s_stop - 1) & 1) is the estimate and logl[1 .. s_stop - 1] the trace
-  int s_stop = 0;
-  if (do_check) HIPCHK(c, hipMemcpy(&s_stop, c->stop_d, sizeof(int), hipMemcpyDeviceToHost));
+  int stopv[2] = {0, 0};   // {sweep the stop rule fired at, 1 if its increment was NaN}
+  if (do_check) HIPCHK(c, hipMemcpy(stopv, c->stop_d, sizeof stopv, hipMemcpyDeviceToHost));
+  const int s_stop = stopv[0];
   const int i_final = s_stop > 0 ? s_stop - 1 : max_steps;
   cur = i_final & 1;
   HIPCHK(c, hipStreamSynchronize(c->stream));
   if ((rc = check_status(c))) return rc;
+  if (stopv[1])   // every rank saw the same all-reduced increment, so every rank returns this
+    return fail(c, PPLS_E_NUMERIC,
+                "the log-likelihood increment of EM iteration %d is NaN: the reference stops PPLS_simult with "
+                "an error there (`if (NA < atol)`, EM_W_multi.R:792)", i_final);
   if (c->xp_active && want_mu) {
     // Eout's mu_T, mu_U (:802) need the rows: one sweep of theta_{i_final} that only writes this
     // rank's mu rows (mu = a_i diag(alpha) + b_i diag(beta), ... from the rank's own rows and
@@ -1494,16 +1632,21 @@ int ppls_em_run(ppls_ctx* c, ppls_theta* th, int r, int max_steps, double atol, 
     if ((rc = sweep(c, r, cur, true, true))) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));
   }
-  if (loglik) HIPCHK(c, hipMemcpy(loglik, c->loglik, sizeof(double) * i_final, hipMemcpyDeviceToHost));
+  std::vector<double> l(i_final);
+  HIPCHK(c, hipMemcpy(l.data(), c->loglik, sizeof(double) * i_final, hipMemcpyDeviceToHost));
+  if (loglik) std::copy(l.begin(), l.end(), loglik);
   if (negative_increment) {
-    std::vector<double> l(i_final);
-    HIPCHK(c, hipMemcpy(l.data(), c->loglik, sizeof(double) * i_final, hipMemcpyDeviceToHost));
     int neg = 0;
     for (int i = 1; i < i_final; ++i) neg |= (l[i] - l[i - 1] < 0);
     *negative_increment = neg;   // warning("Negative increments of likelihood"), :801
   }
   if (steps_done) *steps_done = i_final;
   if ((rc = download_theta(c, r, cur, th))) return rc;
+  // never PPLS_OK with a non-finite trace or estimate (with atol = -Inf no stop rule looks at them)
+  for (int i = 0; i < i_final; ++i)
+    if (!std::isfinite(l[i]))
+      return fail(c, PPLS_E_NUMERIC, "non-finite log-likelihood %g at EM iteration %d", l[i], i + 1);
+  if (!theta_finite(th, c->p, c->q, r)) return fail(c, PPLS_E_NUMERIC, "non-finite estimates after %d EM iterations", i_final);
   canonicalize(th, c->p, c->q, r);   // :794-799
   if ((rc = download_moments(c, r, eout))) return rc;
   return download_mu(c, r, eout);
@@ -1684,6 +1827,10 @@ int rank1_fit_device(ppls_ctx* c, Rank1Dev& d, Rank1& t, const ppls_constraint* 
   HIPCHK(c, hipStreamSynchronize(c->stream));
   int stop[2] = {0, 0};
   HIPCHK(c, hipMemcpy(stop, c->stop_d, sizeof stop, hipMemcpyDeviceToHost));
+  if (stop[1] == 2)   // every rank computed the same all-reduced increment
+    return fail(c, PPLS_E_NUMERIC,
+                "PPLSi component %d: the log-likelihood increment of EM step %d is NaN; the reference stops with "
+                "an error there (`if (critfunc(NA) < atol)`, EM_W_multi.R:173)", m + 1, stop[0]);
   *na = stop[1] != 0;
   *steps = stop[0] > 0 ? stop[0] : stop[0] < 0 ? -stop[0] : max_steps;   // < 0: sigma collapse at step -stop[0]-1
   std::vector<double> buf((size_t)max_steps + 5);
@@ -1744,16 +1891,16 @@ int ppls_ppls_ex(ppls_ctx* c, int a, int max_steps, double atol, int crit_abs, c
   if (c->p < a || c->q < a)   // stopifnot(ncol(X) >= nr_comp, ncol(Y) >= nr_comp) (:245)
     return fail(c, PPLS_E_ARG, "ncol(X)=%d, ncol(Y)=%d must be >= number of components %d", c->p, c->q, a);
   if (max_steps < 1) return fail(c, PPLS_E_ARG, "EMsteps must be >= 1");
+  int rc;
+  if ((rc = check_fit_data(c))) return rc;
   for (int k = 0; k < a; ++k)
     if (!init[k].W || !init[k].C || !init[k].B || !init[k].sigT)
       return fail(c, PPLS_E_ARG, "init[%d] has NULL fields", k);
   HIPCHK(c, hipSetDevice(c->device));
-  int rc;
   if ((rc = ensure_r(c, 1, max_steps))) return rc;
   // the rank-1 steps' statistics from the cross-products S (option xprod): the sweep's weights are
   // the deflated P_0..P_{m-1} w, so S blockdiag(P w, P c) gives exactly the sweep's X'mu_T and Gram
-  c->xp_active = c->seg_rows < 0 && xprod_choose(c, a * max_steps, 1);
-  if (c->xp_active && (rc = xprod_setup(c))) { c->xp_active = false; return rc; }
+  if ((rc = xprod_begin(c, a * max_steps, 1))) return rc;
   struct XpGuard {
     ppls_ctx* c;
     ~XpGuard() { c->xp_active = false; }
@@ -2066,8 +2213,9 @@ int ppls_meta_ppls(ppls_ctx* c, int npop, const int64_t* pop_local, const int64_
   if (!init || !init->W || !init->C || !init->B || !init->sigT || !out || !out->W || !out->C || !out->params)
     return fail(c, PPLS_E_ARG, "NULL argument");
   if (max_steps < 1) return fail(c, PPLS_E_ARG, "EMsteps must be >= 1");
-  HIPCHK(c, hipSetDevice(c->device));
   int rc;
+  if ((rc = check_fit_data(c))) return rc;
+  HIPCHK(c, hipSetDevice(c->device));
   if ((rc = ensure_r(c, 1, max_steps))) return rc;
   std::vector<MetaPop> pops;
   if ((rc = meta_setup(c, npop, pop_local, pop_total, pops))) return rc;
@@ -2110,6 +2258,8 @@ int ppls_meta_ppls(ppls_ctx* c, int npop, const int64_t* pop_local, const int64_
         prev[j] = lj;
       }
       out->steps = i;
+      if (std::isnan(s_new - s_old))                            // `if (NA < atol)` stops meta_PPLSi (:575)
+        return fail(c, PPLS_E_NUMERIC, "meta_PPLSi: the log-likelihood increment of EM step %d is NaN", i);
       if (crit(s_new - s_old) < atol) break;                    // :575-578
     }
   }
@@ -2366,6 +2516,8 @@ int ppls_em_begin(ppls_ctx* c, const ppls_theta* th, int r) {
   if (!c->have_data) return fail(c, PPLS_E_STATE, "no data");
   int rc;
   if ((rc = check_theta(c, th, r))) return rc;
+  if ((rc = check_fit_data(c))) return rc;
+  if (!theta_finite(th, c->p, c->q, r)) return fail(c, PPLS_E_ARG, "theta0 has non-finite entries");
   HIPCHK(c, hipSetDevice(c->device));
   if ((rc = ensure_r(c, r, 1 << 16))) return rc;
   std::vector<double> W(th->W, th->W + (size_t)c->p * r), C(th->C, th->C + (size_t)c->q * r);
@@ -2377,8 +2529,7 @@ int ppls_em_begin(ppls_ctx* c, const ppls_theta* th, int r) {
   c->em_r = r;
   c->em_cur = 0;
   c->em_iter = 0;
-  c->xp_active = c->seg_rows < 0 && xprod_choose(c, 1 << 16, r);
-  if (c->xp_active && (rc = xprod_setup(c))) { c->xp_active = false; return rc; }
+  if ((rc = xprod_begin(c, 1 << 16, r))) return rc;
   c->em_active = true;
   return PPLS_OK;
 }
@@ -2409,7 +2560,14 @@ int ppls_em_state(ppls_ctx* c, ppls_theta* out, double* loglik, int cap, int* n_
   if (out && (rc = download_theta(c, c->em_r, c->em_cur, out))) return rc;
   const int n = c->em_iter >= 1 ? c->em_iter - 1 : 0;
   if (n_loglik) *n_loglik = n;
-  if (loglik && n > 0) HIPCHK(c, hipMemcpy(loglik, c->loglik, sizeof(double) * std::min(n, cap), hipMemcpyDeviceToHost));
+  std::vector<double> l((size_t)n);
+  if (n > 0) HIPCHK(c, hipMemcpy(l.data(), c->loglik, sizeof(double) * n, hipMemcpyDeviceToHost));
+  if (loglik && n > 0) std::copy(l.begin(), l.begin() + std::min(n, cap), loglik);
+  for (int i = 0; i < n; ++i)
+    if (!std::isfinite(l[i]))
+      return fail(c, PPLS_E_NUMERIC, "non-finite log-likelihood %g at EM iteration %d", l[i], i + 1);
+  if (out && !theta_finite(out, c->p, c->q, c->em_r))
+    return fail(c, PPLS_E_NUMERIC, "non-finite estimates after %d EM iterations", c->em_iter);
   return PPLS_OK;
 }
 
@@ -2456,6 +2614,7 @@ int ppls_xprod_prepare(ppls_ctx* c, double* ms, double* total_ms) {
   const bool was = c->xp_ready;
   int rc;
   if ((rc = xprod_setup(c))) return rc;
+  c->xp_explicit = true;
   if (ms) *ms = was ? 0.0 : c->xp_setup_ms;
   if (total_ms) *total_ms = was ? 0.0 : c->xp_setup_total_ms;
   return PPLS_OK;

@@ -1607,8 +1607,10 @@ __device__ bool ppls_block_polar_fast(const double* __restrict__ S, int64_t lds,
   const int64_t ldr = Sl ? nr : lds;
   const int sro = Sl ? i0 : 0;
   // the carried V in sV, re-orthonormalised (modified Gram-Schmidt, rows on lanes; wave 0) when
-  // reorth: every 8th iteration -- between, the Jacobi's rotations keep it orthonormal to a few eps
-  // per iteration (1.6 us of the C3 cross-product finalize's critical path saved 7 times in 8)
+  // reorth: every 8th iteration by default (context option "vorth", mode bits 16-23) -- between, the
+  // Jacobi's rotations keep it orthonormal to a few eps per iteration (1.6 us of the C3
+  // cross-product finalize's critical path saved 7 times in 8; tests/test_gpu_nonfinite.py runs
+  // 400 iterations at cadence 8 against cadence 1)
   auto load_vprev = [&]() {
     for (int e = lane; e < GG; e += 64) {
 #pragma unroll
@@ -2004,11 +2006,16 @@ __device__ void ppls_scalars_wave(const double* sG, const double* sWtW, const do
 
 // The PPLS_simult stop rule on the device (EM_W_multi.R:792: logl[i] - logl[i-1] < atol, i > 1),
 // evaluated by one thread right after it wrote loglik[idx]: sets the stop flag (every later kernel
-// of the run then exits at once) and its host-mapped mirror the host polls.
+// of the run then exits at once) and its host-mapped mirror the host polls.  A NaN increment is
+// R's `if (NA < atol)`, which stops PPLS_simult with an error: the run stops there too and
+// stop[1] = 1 tells the host to report it (every rank computes the same all-reduced increment).
 __device__ __forceinline__ void ppls_stop_test(const double* loglik, int idx, int* stop, int* stop_mirror,
                                                int stop_check, int stop_step, double atol) {
   if (!stop_check || !stop || idx < 1) return;
-  if (loglik[idx] - loglik[idx - 1] < atol) {
+  const double d = loglik[idx] - loglik[idx - 1];
+  const bool nan = d != d;
+  if (nan || d < atol) {
+    if (nan) stop[1] = 1;
     *stop = stop_step;
     if (stop_mirror) __hip_atomic_store(stop_mirror, stop_step, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
@@ -2189,7 +2196,9 @@ __global__ __launch_bounds__(PPLS_FIN_THREADS) void ppls_finalize_kernel(
     tm.tr = tr;
     if (qr || !ppls_block_polar_fast<R, NT>(S, ld, rows, out, ld, ld, stage_lds ? dyn_lds : nullptr, sh,
                                             sm, gacc, vs, tr, tm, (mode & 4) != 0,
-                                            (double)((mode >> 8) & 255), logl_index < 0 || (logl_index & 7) == 0)) {
+                                            (double)((mode >> 8) & 255),
+                                            logl_index < 0 || ((mode >> 16) & 255) <= 1 ||
+                                                logl_index % ((mode >> 16) & 255) == 0)) {
       if (tm.rank != 0) return;   // the Householder fallback runs on one block
       ppls_block_polar(S, ld, rows, R, out, ld, ld, w2, w2 + (int64_t)rows * R, status, qr);
       if (gacc) {
@@ -2394,6 +2403,10 @@ __global__ __launch_bounds__(1024) void ppls_rank1_step_kernel(PplsRank1StepArgs
       const double incr = l - a.lv[a.step - 1];
       if ((a.crit_abs ? fabs(incr) : incr) < a.atol) {
         a.stop[0] = a.step;
+        ex = 1;
+      } else if (incr != incr) {   // `if (critfunc(NA) < atol)` stops PPLSi with an error (:173)
+        a.stop[0] = a.step;
+        a.stop[1] = 2;
         ex = 1;
       }
     }
