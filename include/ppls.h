@@ -100,8 +100,9 @@ const char* ppls_last_error(const ppls_ctx* ctx);
  *                and S with its Gram partials fits the smallest free HBM over all ranks (measured when
  *                the data were loaded; falls back to streaming, on every rank alike, if S cannot be
  *                allocated); S stays resident (8 (p+q)^2 bytes) until the data change, xprod goes from
- *                non-zero to 0 (not for an S of ppls_xprod_prepare), or ppls_xprod_release; 0 is
- *                refused (PPLS_E_STATE) during an ppls_em_begin session that reads S),
+ *                non-zero to 0 (not for an S of ppls_xprod_prepare), or ppls_xprod_release; setting 0
+ *                ends an ppls_em_begin session that reads S: ppls_em_iterate then returns
+ *                PPLS_E_STATE until the next ppls_em_begin -- never a silent switch to streaming),
  *       "vorth" (the finalize re-orthonormalises the Jacobi warm start it carries between
  *                iterations every vorth-th iteration: 1 .. 255, default 8),
  *       "xprod_rw" (rows of S per wave of the cross-product tile kernel: 0 auto, 1, 2, 4, 8),

@@ -1152,10 +1152,12 @@ int ppls_set_option(ppls_ctx* c, const char* key, int64_t value) {
     c->nt_loads = (int)value;
   } else if (!strcmp(key, "xprod")) {
     if (value < -1 || value > 1) return fail(c, PPLS_E_ARG, "xprod must be -1 (auto), 0 (stream X, Y) or 1 (cross-products)");
-    // the path of an ppls_em_begin session is fixed at em_begin: no switch to streaming under it
-    if (value == 0 && c->em_active && c->xp_active)
-      return fail(c, PPLS_E_STATE, "xprod = 0 during an ppls_em_begin session on the cross-products: end it first "
-                                   "(ppls_em_begin again, or any fit entry point)");
+    // the path of an ppls_em_begin session is fixed at em_begin: a session on S does not switch to
+    // streaming under it -- xprod = 0 ends it (ppls_em_iterate then asks for ppls_em_begin)
+    if (value == 0 && c->em_active && c->xp_active) {
+      c->em_active = false;
+      c->xp_active = false;
+    }
     const int was = c->xprod;
     c->xprod = (int)value;
     // streaming from now on: S's 8 (p+q)^2 bytes go back -- unless S came from ppls_xprod_prepare

@@ -82,7 +82,7 @@ def case_nan_x(mode):
     with Context(0) as ctx:
         ctx.set_option("xprod", 1 if mode == "xprod" else 0)
         res["set_data"] = _err(lambda: ctx.set_data(Xb, Y))
-        res["after"] = _err(lambda: ctx.em_run(_theta(th0), 5, -np.inf, 0))
+        res["after"] = _err(lambda: ctx.em_run(_theta(th0), 5, -np.inf, 0, want_eout=False))
         ctx.set_data(X, Y)
         est, ll, _, _ = ctx.em_run(_theta(th0), 5, -np.inf, 0)
         res["recovered"] = bool(np.all(np.isfinite(ll)) and len(ll) == 5)

@@ -216,6 +216,7 @@ def test_xprod_auto_policy(ctx):
 
 
 def test_xprod_prepare_and_info(ctx):
+    from ppls_amd import PplsError
     X, Y, _ = make_problem(1000, 70, 33, 2, seed=4)
     ctx.set_data(X, Y)
     ms, tot = ctx.xprod_prepare()
@@ -243,8 +244,23 @@ def test_xprod_prepare_and_info(ctx):
     ctx.em_iterate(6)
     est_b, ll_b = ctx.em_state()
     assert len(ll_a) == 5 and np.array_equal(ll_a, ll_b) and np.array_equal(est_a.W, est_b.W)
-    ctx.set_option("xprod", 0)   # streaming from now on frees S
+    # xprod = 0 ends a session that reads S (no silent switch to streaming under it), and keeps an S
+    # formed by xprod_prepare until xprod_release
+    ctx.set_option("xprod", 0)
+    with pytest.raises(PplsError, match="ppls_em_begin first"):
+        ctx.em_iterate(1)
+    assert ctx.xprod_info(2)["ready"]
+    ctx.xprod_release()
+    # an S the run formed itself goes back when xprod goes from non-zero to 0 -- not when 0 is restated
+    ctx.set_option("xprod", 1)
+    ctx.em_run(th, 3, -np.inf, 0)
+    assert ctx.xprod_info(2)["ready"]
+    ctx.set_option("xprod", 0)
     assert not ctx.xprod_info(2)["ready"]
+    ctx.xprod_prepare()
+    ctx.set_option("xprod", 0)
+    assert ctx.xprod_info(2)["ready"]
+    ctx.xprod_release()
 
 
 @pytest.mark.parametrize("k,n,p,q,r,dtype", [(3, 3001, 300, 200, 4, 0), (4, 2000, 700, 90, 10, 1),
