@@ -134,6 +134,11 @@ struct ppls_ctx {
   double xp_setup_total_ms = 0.0;
   double xp_setup_ar_ms = 0.0;   // the all-reduce of S (wall clock around it and its stream sync)
   int xp_nsplit = 0;
+  // the MFMA Gram (S, variances' X'X): option "gram" = PPLS_GRAM_* bits (default PPLS_GRAM_DEFAULT)
+  // and the persistent form's work queue, prepared for (gq_p, gq_nsplit, gq_variant)
+  int gram_variant = PPLS_GRAM_DEFAULT;
+  int* gram_q = nullptr;
+  int gq_p = -1, gq_nsplit = -1, gq_variant = -1;
   rocblas_handle blas = nullptr;   // rocSOLVER (variances.PPLS_simult's p x p inverse), created lazily
   int var_chol = 1;                // option "var_chol": that inverse by Cholesky when positive definite (1) or LU (0)
   // timing
@@ -647,19 +652,26 @@ int finalize(ppls_ctx* c, int r, int cur, int nxt, int logl_index, int type, int
 // Row splits of the MFMA Gram of a p x p product over n rows: enough work items to fill the device
 // (whole rounds of resident workgroups), each split's p x p partial kept under 4 GB in all.
 int gram_splits(ppls_ctx* c, int p, int64_t n) {
-  const int ntiles = ppls_gram_tiles(p);
-  const int64_t slots = (int64_t)c->num_cus * ppls_gram_occupancy(c->dtype);
-  const double pp = (double)p * p;
-  int nsplit = 1;
-  double best = -1.0;
-  for (int sp = 1; sp <= 32; ++sp) {
-    if (sp > 1 && ((int64_t)sp * 512 > n || (double)sp * pp * 8.0 > 4.0e9)) break;
-    const int64_t w = (int64_t)ntiles * sp;
-    const double eff = (double)w / (double)(((w + slots - 1) / slots) * slots);
-    if (eff > best + 1e-9) { best = eff; nsplit = sp; }
-    if (eff >= 0.95) break;
+  return ppls_gram_splits(p, n, c->num_cus * ppls_gram_occupancy(c->dtype), c->gram_variant);
+}
+
+// The persistent Gram's work queue for a p x p Gram in nsplit row splits (prepared once per shape).
+int gram_queue(ppls_ctx* c, int p, int nsplit, int** q) {
+  *q = nullptr;
+  if (!(c->gram_variant & PPLS_GRAM_DYN)) return PPLS_OK;
+  if (c->gram_q && c->gq_p == p && c->gq_nsplit == nsplit && c->gq_variant == c->gram_variant) {
+    *q = c->gram_q;
+    return PPLS_OK;
   }
-  return nsplit;
+  int rc;
+  c->gq_p = -1;
+  if ((rc = dalloc(c, &c->gram_q, (size_t)ppls_gram_queue_ints(p, nsplit)))) return rc;
+  HIPCHK(c, ppls_gram_queue_prepare(c->gram_q, p, nsplit, c->gram_variant, c->stream));
+  c->gq_p = p;
+  c->gq_nsplit = nsplit;
+  c->gq_variant = c->gram_variant;
+  *q = c->gram_q;
+  return PPLS_OK;
 }
 
 int xprod_setup(ppls_ctx* c);
@@ -705,8 +717,10 @@ int xprod_setup(ppls_ctx* c) {
   // others waiting in it), so the allocation outcome is all-reduced first
   const int nsplit = gram_splits(c, P, xprod_rows(c));
   double* part = nullptr;
+  int* gq = nullptr;
   int rc_alloc = dalloc(c, &c->xp_S, PP);
   if (!rc_alloc && c->n_local > 0) rc_alloc = dalloc(c, &part, (size_t)nsplit * PP);
+  if (!rc_alloc && c->n_local > 0) rc_alloc = gram_queue(c, P, nsplit, &gq);
   if (c->nranks > 1 || c->reducer) {
     const double f = rc_alloc ? 1.0 : 0.0;
     double tot = 0.0;
@@ -734,7 +748,7 @@ int xprod_setup(ppls_ctx* c) {
     if (e == hipSuccess) e = hipEventRecord(e0, c->stream);
     if (e == hipSuccess)
       e = ppls_launch_gram_joint(c->X, c->ldx, c->ldx, c->Y, c->ldy, c->ldy, c->dtype, c->n_local, P, nsplit, part,
-                                 (int64_t)PP, c->stream);
+                                 (int64_t)PP, gq, c->gram_variant, c->stream);
     if (e == hipSuccess) e = ppls_launch_gram_finish(part, nsplit, (int64_t)PP, P, c->xp_S, c->stream);
     if (e == hipSuccess) e = hipEventRecord(e1, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
@@ -1078,6 +1092,7 @@ void ppls_ctx_destroy(ppls_ctx* c) {
   dfree(c->bal_bounds);
   dfree(c->team_bar);
   dfree(c->team_part);
+  dfree(c->gram_q);
   if (c->stop_mirror) (void)hipHostFree(c->stop_mirror);
   for (auto& e : c->ev) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
   for (auto& e : c->ev_ar) { (void)hipEventDestroy(e.first); (void)hipEventDestroy(e.second); }
@@ -1166,6 +1181,9 @@ int ppls_set_option(ppls_ctx* c, const char* key, int64_t value) {
       HIPCHK(c, hipStreamSynchronize(c->stream));
       xprod_free(c);
     }
+  } else if (!strcmp(key, "gram")) {
+    if (value < 0 || value > 3) return fail(c, PPLS_E_ARG, "gram must be in [0, 3] (PPLS_GRAM_SKIP | PPLS_GRAM_DYN)");
+    c->gram_variant = (int)value;
   } else if (!strcmp(key, "vorth")) {
     if (value < 1 || value > 255) return fail(c, PPLS_E_ARG, "vorth must be in [1, 255]");
     c->vorth = (int)value;
@@ -2350,7 +2368,9 @@ int ppls_variances(ppls_ctx* c, const double* mu, const double* Cdiag, double si
     if (n > 0) {
       const int nsplit = gram_splits(c, p, n);
       VRC(dalloc(c, &dpart, (size_t)nsplit * pp));
-      VCHK(ppls_launch_gram(D, f32, n, ld, p, nsplit, dpart, (int64_t)pp, c->stream));
+      int* gq = nullptr;
+      VRC(gram_queue(c, p, nsplit, &gq));
+      VCHK(ppls_launch_gram(D, f32, n, ld, p, nsplit, dpart, (int64_t)pp, gq, c->gram_variant, c->stream));
       VCHK(ppls_launch_gram_finish(dpart, nsplit, (int64_t)pp, p, dG, c->stream));
       dfree(dpart);
     } else {
@@ -2454,11 +2474,13 @@ int ppls_gram(ppls_ctx* c, int xory, int nsplit, double* G, double* ms) {
   double *dpart = nullptr, *dG = nullptr;
   if ((rc = dalloc(c, &dpart, (size_t)nsplit * pp))) return rc;
   if ((rc = dalloc(c, &dG, pp))) { dfree(dpart); return rc; }
+  int* gq = nullptr;
+  if ((rc = gram_queue(c, p, nsplit, &gq))) { dfree(dpart); dfree(dG); return rc; }
   hipEvent_t e0, e1;
   HIPCHK(c, hipEventCreate(&e0));
   HIPCHK(c, hipEventCreate(&e1));
   hipError_t e = hipEventRecord(e0, c->stream);
-  if (e == hipSuccess) e = ppls_launch_gram(D, c->dtype, c->n_local, ld, p, nsplit, dpart, (int64_t)pp, c->stream);
+  if (e == hipSuccess) e = ppls_launch_gram(D, c->dtype, c->n_local, ld, p, nsplit, dpart, (int64_t)pp, gq, c->gram_variant, c->stream);
   if (e == hipSuccess) e = hipEventRecord(e1, c->stream);
   if (e == hipSuccess) e = ppls_launch_gram_finish(dpart, nsplit, (int64_t)pp, p, dG, c->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(c->stream);

@@ -146,10 +146,16 @@ hipError_t ppls_launch_philox(const uint32_t* ctr, int64_t count, uint64_t key, 
 hipError_t ppls_launch_to_rowmajor(const double* src, int64_t n, int p, int ld, double* dst,
                                    hipStream_t st);
 // variances.PPLS_simult (ppls_variances.hip)
+#define PPLS_GRAM_SKIP 1       // MFMA Gram: skip blocks in the padding and above the diagonal
+#define PPLS_GRAM_DYN 2        // MFMA Gram: persistent workgroups + per-XCD-group work queues
+#define PPLS_GRAM_DEFAULT 3
 int ppls_gram_tiles(int p);
 int ppls_gram_occupancy(int f32);
+int ppls_gram_splits(int p, int64_t n, int slots, int variant);
+int64_t ppls_gram_queue_ints(int p, int nsplit);
+hipError_t ppls_gram_queue_prepare(int* queue, int p, int nsplit, int variant, hipStream_t st);
 hipError_t ppls_launch_gram(const void* X, int f32, int64_t n, int ld, int p, int nsplit, double* part,
-                            int64_t part_stride, hipStream_t st);
+                            int64_t part_stride, int* queue, int variant, hipStream_t st);
 hipError_t ppls_launch_gram_finish(const double* part, int nsplit, int64_t part_stride, int p, double* G,
                                    hipStream_t st);
 int ppls_xtmu_chunks(int64_t n, int ld, int f32);

@@ -16,6 +16,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+#include <vector>
+
 #include "ppls_kernels.h"
 #include "ppls_xprod.h"
 
@@ -48,42 +51,83 @@ struct GVec<float> {
 
 }  // namespace
 
-// X'X on MFMA.  Work item L (blockIdx remapped so that each XCD -- blockIdx mod 8 -- gets a
-// contiguous range of items, i.e. tiles that share column panels share an L2) = split s x
-// lower tile t = (I, J), J <= I.  A wave owns a 64 x 64 sub-tile = 4 x 4 MFMA blocks (64 fp64
-// accumulators per lane); per 4-row k-step it reads 4 A and 4 B operands from LDS (lane l: row
-// l >> 4 of the step, column l & 15 of its block) -- both straight from the row-major panels, no
-// transpose, since A[i][k] = X[k][i] and B[k][j] = X[k][j].  The next stage's global loads are in
-// flight during the MFMAs; one barrier per 16-row stage.  Output: part[s][i p + j] for the tile's
-// (i, j), i in block I >= block J (row-major of the lower blocks; coalesced over j).
+// Active 16 x 16 MFMA blocks of wave (wi, wj) in the lower tile (I, J) of a p x p Gram: bit m * 4 + q
+// for the wave's block row m and block column q.  A block is skipped when its rows or columns lie
+// wholly in the padding past p, or -- in a diagonal tile -- when it lies wholly above the diagonal
+// (the finish kernel reads only the lower triangle).  C3 (p = 4000 -> 32 blocks of 128): the last
+// block row is 3/4 padding and the diagonal tiles 7/16 upper half, 7 % of the executed flops.
+__host__ __device__ inline unsigned ppls_gram_active(int I, int J, int wi, int wj, int p) {
+  unsigned act = 0;
+  for (int m = 0; m < 4; ++m)
+    for (int q = 0; q < 4; ++q) {
+      const int i0 = I * PPLS_GT + wi * 64 + m * 16, j0 = J * PPLS_GT + wj * 64 + q * 16;
+      if (i0 < p && j0 < p && (I != J || wj * 4 + q <= wi * 4 + m)) act |= 1u << (m * 4 + q);
+    }
+  return act;
+}
+
+__host__ __device__ inline void ppls_gram_tile_of(int t, int* I, int* J) {
+  int i = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
+  while ((i + 1) * (i + 2) / 2 <= t) ++i;
+  while (i * (i + 1) / 2 > t) --i;
+  *I = i;
+  *J = t - i * (i + 1) / 2;
+}
+
+// The persistent form's next work item: group g's queue first (its workgroups share an XCD, so
+// their items -- consecutive tiles of one row split -- share column panels in that L2), then the
+// other groups' (stealing: an XCD that runs ahead takes the cheap tail of a slower one).  One
+// global atomic per grab (items take milliseconds); -1 when every queue is empty.
+__device__ inline int ppls_gram_next(unsigned* cnt, const int* qoff, const int* items, int g) {
+  for (int k = 0; k < 8; ++k) {
+    const int gg = (g + k) & 7;
+    const int len = qoff[gg + 1] - qoff[gg];
+    const unsigned idx = atomicAdd(&cnt[gg], 1u);
+    if ((int)idx < len) return items[qoff[gg] + idx];
+  }
+  return -1;
+}
+
+// X'X on MFMA.  Work item L = split s x lower tile t = (I, J), J <= I.  A wave owns a 64 x 64
+// sub-tile = 4 x 4 MFMA blocks (64 fp64 accumulators per lane); per 4-row k-step it reads 4 A and 4
+// B operands from LDS (lane l: row l >> 4 of the step, column l & 15 of its block) -- both straight
+// from the row-major panels, no transpose, since A[i][k] = X[k][i] and B[k][j] = X[k][j].  The next
+// stage's global loads are in flight during the MFMAs; one barrier per 16-row stage.  Output:
+// part[s][i p + j] for the tile's (i, j), i in block I >= block J (row-major of the lower blocks;
+// coalesced over j).
+//
+// Scheduling (template DYN): the static form runs one work item per workgroup, blockIdx remapped so
+// that each XCD -- blockIdx mod 8 -- gets a contiguous range of items (tiles that share column panels
+// share an L2).  Its items all take the same time, so the last round of them leaves the slots that
+// have none idle (C3: 6,336 items on 512 slots, the 13th round 3/8 full: ~5 % of the kernel).  The
+// persistent form (DYN) launches one workgroup per slot; each takes items from the queue of its group
+// (blockIdx mod 8: the same contiguous ranges), costliest first -- tiles with skipped blocks (SKIP)
+// are cheaper and come last, so the final items of every queue are short -- and steals from the
+// other groups' queues once its own is empty.  Each item's sums depend only on the item, so the
+// result is the same bit for bit whichever workgroup runs it.
 //
 // The column space is that of the joint matrix [X | Y] (ppls_xprod.hip's cross-product form of the
 // EM iteration): column c is X[:, c] for c < xcols and Y[:, c - xcols] for c - xcols < ycols (zero
 // beyond); xcols and ycols are multiples of the 16-B vector, so no load straddles the seam.  The
 // Gram of X alone is xcols = ld, ycols = 0, p the output edge.
-template <typename T>
-__global__ __launch_bounds__(256, 2) void ppls_gram_mfma_kernel(const T* __restrict__ X, int ldx, int xcols,
-                                                                 const T* __restrict__ Y, int ldy, int ycols,
-                                                                 int64_t n, int p, int ntiles, int nsplit,
-                                                                 int64_t work, double* __restrict__ part,
-                                                                 int64_t part_stride) {
+template <typename T, bool SKIP, bool MASKED>
+__device__ __forceinline__ void ppls_gram_item(const T* __restrict__ X, int ldx, int xcols, const T* __restrict__ Y,
+                                               int ldy, int ycols, int64_t n, int p, int ntiles, int nsplit,
+                                               int64_t L, double* __restrict__ part, int64_t part_stride,
+                                               double (*sm)[2][PPLS_GK][PPLS_GLD]) {
   typedef double d4 __attribute__((ext_vector_type(4)));
   constexpr int EV = 16 / sizeof(T);              // elements per 16-B load
   constexpr int VPR = PPLS_GT / EV;               // 16-B vectors per panel row
   constexpr int NV = PPLS_GK * VPR / 256;         // per thread per panel (fp64: 4, fp32: 2)
-  __shared__ __attribute__((aligned(16))) double sm[2][2][PPLS_GK][PPLS_GLD];
-  const int64_t per = gridDim.x >> 3;
-  const int64_t L = (int64_t)(blockIdx.x & 7) * per + (blockIdx.x >> 3);
-  if (L >= work) return;
   const int s = (int)(L / ntiles), t = (int)(L - (int64_t)s * ntiles);
-  int I = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
-  while ((I + 1) * (I + 2) / 2 <= t) ++I;
-  while (I * (I + 1) / 2 > t) --I;
-  const int J = t - I * (I + 1) / 2;
+  int I, J;
+  ppls_gram_tile_of(t, &I, &J);
   const int64_t r0 = n * s / nsplit, r1 = n * (s + 1) / nsplit;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wi = wave >> 1, wj = wave & 1;
   const int colA = I * PPLS_GT, colB = J * PPLS_GT;
+  // wave-uniform (SGPR) block mask; MASKED code paths test it per MFMA, the full path does not
+  const unsigned act = SKIP ? ppls_gram_active(I, J, wi, wj, p) : 0xffffu;
 
   GVec<T> ra[NV], rb[NV];
   auto load = [&](int64_t k0) {
@@ -124,19 +168,23 @@ __global__ __launch_bounds__(256, 2) void ppls_gram_mfma_kernel(const T* __restr
   for (int64_t st = 0; st < nsteps; ++st) {
     const int buf = (int)(st & 1);
     if (st + 1 < nsteps) load(r0 + (st + 1) * PPLS_GK);
+    if (!MASKED || act) {
 #pragma unroll
-    for (int kk = 0; kk < PPLS_GK / 4; ++kk) {
-      const double* ar = &sm[buf][0][kk * 4 + ko][wi * 64 + cl];
-      const double* br = &sm[buf][1][kk * 4 + ko][wj * 64 + cl];
-      double a[4], b[4];
+      for (int kk = 0; kk < PPLS_GK / 4; ++kk) {
+        const double* ar = &sm[buf][0][kk * 4 + ko][wi * 64 + cl];
+        const double* br = &sm[buf][1][kk * 4 + ko][wj * 64 + cl];
+        double a[4], b[4];
 #pragma unroll
-      for (int m = 0; m < 4; ++m) a[m] = ar[m * 16];
+        for (int m = 0; m < 4; ++m) a[m] = ar[m * 16];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) b[q] = br[q * 16];
+        for (int q = 0; q < 4; ++q) b[q] = br[q * 16];
 #pragma unroll
-      for (int m = 0; m < 4; ++m)
+        for (int m = 0; m < 4; ++m)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) acc[m][q] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[m], b[q], acc[m][q], 0, 0, 0);
+          for (int q = 0; q < 4; ++q)
+            if (!MASKED || ((act >> (m * 4 + q)) & 1u))
+              acc[m][q] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[m], b[q], acc[m][q], 0, 0, 0);
+      }
     }
     if (st + 1 < nsteps) store(buf ^ 1);
     __syncthreads();
@@ -146,6 +194,7 @@ __global__ __launch_bounds__(256, 2) void ppls_gram_mfma_kernel(const T* __restr
   for (int m = 0; m < 4; ++m)
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
+      if (MASKED && !((act >> (m * 4 + q)) & 1u)) continue;
       const int j = colB + wj * 64 + q * 16 + cl;
 #pragma unroll
       for (int g = 0; g < 4; ++g) {   // f64 MFMA D map: col = lane & 15, row = (lane >> 4) + 4 g
@@ -153,6 +202,49 @@ __global__ __launch_bounds__(256, 2) void ppls_gram_mfma_kernel(const T* __restr
         if (i < p && j < p) out[(int64_t)i * p + j] = acc[m][q][g];
       }
     }
+}
+
+template <typename T, bool DYN, bool SKIP>
+__global__ __launch_bounds__(256, 2) void ppls_gram_mfma_kernel(const T* __restrict__ X, int ldx, int xcols,
+                                                                 const T* __restrict__ Y, int ldy, int ycols,
+                                                                 int64_t n, int p, int ntiles, int nsplit,
+                                                                 int64_t work, double* __restrict__ part,
+                                                                 int64_t part_stride, int* __restrict__ queue) {
+  __shared__ __attribute__((aligned(16))) double sm[2][2][PPLS_GK][PPLS_GLD];
+  if constexpr (!DYN) {
+    const int64_t per = gridDim.x >> 3;
+    const int64_t L = (int64_t)(blockIdx.x & 7) * per + (blockIdx.x >> 3);
+    if (L >= work) return;
+    if (SKIP) {
+      int I, J;
+      ppls_gram_tile_of((int)(L % ntiles), &I, &J);
+      if (I == J || (I + 1) * PPLS_GT > p) {   // a tile with skipped blocks: the masked code path
+        ppls_gram_item<T, true, true>(X, ldx, xcols, Y, ldy, ycols, n, p, ntiles, nsplit, L, part, part_stride, sm);
+        return;
+      }
+    }
+    ppls_gram_item<T, false, false>(X, ldx, xcols, Y, ldy, ycols, n, p, ntiles, nsplit, L, part, part_stride, sm);
+  } else {
+    // queue = [qoff (9) | counters (8, zeroed before the launch) | items (work)]
+    const int* qoff = queue;
+    unsigned* cnt = (unsigned*)(queue + 9);
+    const int* items = queue + 17;
+    __shared__ int s_next;
+    const int g = blockIdx.x & 7;
+    for (;;) {
+      if (threadIdx.x == 0) s_next = ppls_gram_next(cnt, qoff, items, g);
+      __syncthreads();
+      const int L = s_next;
+      __syncthreads();   // every thread has read s_next before thread 0 writes the next one
+      if (L < 0) return;
+      int I, J;
+      ppls_gram_tile_of(L % ntiles, &I, &J);
+      if (SKIP && (I == J || (I + 1) * PPLS_GT > p))
+        ppls_gram_item<T, true, true>(X, ldx, xcols, Y, ldy, ycols, n, p, ntiles, nsplit, L, part, part_stride, sm);
+      else
+        ppls_gram_item<T, false, false>(X, ldx, xcols, Y, ldy, ycols, n, p, ntiles, nsplit, L, part, part_stride, sm);
+    }
+  }
 }
 
 // G (p x p column-major, full) = sum over splits of the lower-block entries: element (a, b) is read
@@ -282,32 +374,115 @@ int ppls_gram_tiles(int p) {
 
 int ppls_gram_occupancy(int f32) {
   int occ = 0;
-  hipError_t e = f32 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, ppls_gram_mfma_kernel<float>, 256, 0)
-                     : hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, ppls_gram_mfma_kernel<double>, 256, 0);
+  hipError_t e = f32 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, ppls_gram_mfma_kernel<float, true, true>, 256, 0)
+                     : hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, ppls_gram_mfma_kernel<double, true, true>, 256, 0);
   return e == hipSuccess && occ > 0 ? occ : 1;
 }
 
+// MFMA blocks an item of tile t executes (of 64): the persistent queue's cost order.
+static int ppls_gram_cost(int t, int p, int variant) {
+  if (!(variant & PPLS_GRAM_SKIP)) return 64;
+  int I, J;
+  ppls_gram_tile_of(t, &I, &J);
+  int c = 0;
+  for (int w = 0; w < 4; ++w) c += __builtin_popcount(ppls_gram_active(I, J, w >> 1, w & 1, p));
+  return c;
+}
+
+// Row splits of a p x p Gram over n rows (partials: nsplit x 8 p^2 bytes, kept under 4 GB).
+// Static form: enough items to fill whole rounds of the slots (>= 95 % of the last round).  Persistent
+// form: about 12 items per slot, so the queues end on short items.
+int ppls_gram_splits(int p, int64_t n, int slots, int variant) {
+  const int ntiles = ppls_gram_tiles(p);
+  const double pp = (double)p * p;
+  auto allowed = [&](int sp) { return sp == 1 || ((int64_t)sp * 512 <= n && (double)sp * pp * 8.0 <= 4.0e9); };
+  if (variant & PPLS_GRAM_DYN) {
+    int sp = (int)((12LL * slots + ntiles - 1) / ntiles);
+    sp = sp < 1 ? 1 : (sp > 32 ? 32 : sp);
+    while (sp > 1 && !allowed(sp)) --sp;
+    return sp;
+  }
+  int nsplit = 1;
+  double best = -1.0;
+  for (int sp = 1; sp <= 32; ++sp) {
+    if (!allowed(sp)) break;
+    const int64_t w = (int64_t)ntiles * sp;
+    const double eff = (double)w / (double)(((w + slots - 1) / slots) * slots);
+    if (eff > best + 1e-9) { best = eff; nsplit = sp; }
+    if (eff >= 0.95) break;
+  }
+  return nsplit;
+}
+
+int64_t ppls_gram_queue_ints(int p, int nsplit) { return 17 + (int64_t)ppls_gram_tiles(p) * nsplit; }
+
+// The persistent form's queues (device ints, ppls_gram_queue_ints): group g gets the contiguous item
+// range [g W / 8, (g + 1) W / 8) of the split-major order (its XCD's tiles share column panels),
+// sorted costliest first (stable: ties keep the split-major order).  Synchronous (host staging);
+// the launch resets the counters, so one prepared queue serves any number of launches.
+hipError_t ppls_gram_queue_prepare(int* queue, int p, int nsplit, int variant, hipStream_t st) {
+  const int ntiles = ppls_gram_tiles(p);
+  const int64_t work = (int64_t)ntiles * nsplit;
+  std::vector<int> h((size_t)ppls_gram_queue_ints(p, nsplit), 0);
+  std::vector<int> tc((size_t)ntiles);
+  for (int t = 0; t < ntiles; ++t) tc[(size_t)t] = ppls_gram_cost(t, p, variant);
+  int* items = h.data() + 17;
+  for (int g = 0; g < 8; ++g) {
+    const int64_t a = work * g / 8, b = work * (g + 1) / 8;
+    h[(size_t)g] = (int)a;
+    for (int64_t L = a; L < b; ++L) items[L] = (int)L;
+    std::stable_sort(items + a, items + b,
+                     [&](int x, int y) { return tc[(size_t)(x % ntiles)] > tc[(size_t)(y % ntiles)]; });
+  }
+  h[8] = (int)work;
+  hipError_t e = hipMemcpyAsync(queue, h.data(), sizeof(int) * h.size(), hipMemcpyHostToDevice, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  return e;
+}
+
 hipError_t ppls_launch_gram_joint(const void* X, int ldx, int xcols, const void* Y, int ldy, int ycols, int f32,
-                                  int64_t n, int p, int nsplit, double* part, int64_t part_stride, hipStream_t st) {
+                                  int64_t n, int p, int nsplit, double* part, int64_t part_stride, int* queue,
+                                  int variant, hipStream_t st) {
   if (n <= 0 || p <= 0 || nsplit < 1 || xcols + ycols < 1) return hipErrorInvalidValue;
   const int ev = f32 ? 4 : 2;
   if (xcols % ev || ycols % ev) return hipErrorInvalidValue;
   const int ntiles = ppls_gram_tiles(p);
   const int64_t work = (int64_t)ntiles * nsplit;
-  const int64_t grid = (work + 7) / 8 * 8;   // a multiple of 8: the XCD remap needs whole rounds
-  if (grid > 0x7fffffff) return hipErrorInvalidValue;
-  if (f32)
-    hipLaunchKernelGGL(ppls_gram_mfma_kernel<float>, dim3((unsigned)grid), dim3(256), 0, st, (const float*)X, ldx,
-                       xcols, (const float*)Y, ldy, ycols, n, p, ntiles, nsplit, work, part, part_stride);
-  else
-    hipLaunchKernelGGL(ppls_gram_mfma_kernel<double>, dim3((unsigned)grid), dim3(256), 0, st, (const double*)X, ldx,
-                       xcols, (const double*)Y, ldy, ycols, n, p, ntiles, nsplit, work, part, part_stride);
+  const bool dyn = (variant & PPLS_GRAM_DYN) != 0, skip = (variant & PPLS_GRAM_SKIP) != 0;
+  if (work > 0x7fffffff - 32) return hipErrorInvalidValue;
+  int64_t grid;
+  if (dyn) {
+    if (!queue) return hipErrorInvalidValue;
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    grid = (int64_t)cus * ppls_gram_occupancy(f32);
+    grid = (grid + 7) / 8 * 8;
+    hipError_t e = hipMemsetAsync(queue + 9, 0, 8 * sizeof(int), st);   // the queue counters
+    if (e != hipSuccess) return e;
+  } else {
+    grid = (work + 7) / 8 * 8;   // a multiple of 8: the XCD remap needs whole rounds
+  }
+#define PPLS_GRAM_LAUNCH(TT, D, S)                                                                           \
+  hipLaunchKernelGGL((ppls_gram_mfma_kernel<TT, D, S>), dim3((unsigned)grid), dim3(256), 0, st, (const TT*)X, ldx, \
+                     xcols, (const TT*)Y, ldy, ycols, n, p, ntiles, nsplit, work, part, part_stride, queue)
+  if (f32) {
+    if (dyn && skip) PPLS_GRAM_LAUNCH(float, true, true);
+    else if (dyn) PPLS_GRAM_LAUNCH(float, true, false);
+    else if (skip) PPLS_GRAM_LAUNCH(float, false, true);
+    else PPLS_GRAM_LAUNCH(float, false, false);
+  } else {
+    if (dyn && skip) PPLS_GRAM_LAUNCH(double, true, true);
+    else if (dyn) PPLS_GRAM_LAUNCH(double, true, false);
+    else if (skip) PPLS_GRAM_LAUNCH(double, false, true);
+    else PPLS_GRAM_LAUNCH(double, false, false);
+  }
+#undef PPLS_GRAM_LAUNCH
   return hipGetLastError();
 }
 
 hipError_t ppls_launch_gram(const void* X, int f32, int64_t n, int ld, int p, int nsplit, double* part,
-                            int64_t part_stride, hipStream_t st) {
-  return ppls_launch_gram_joint(X, ld, ld, nullptr, 0, 0, f32, n, p, nsplit, part, part_stride, st);
+                            int64_t part_stride, int* queue, int variant, hipStream_t st) {
+  return ppls_launch_gram_joint(X, ld, ld, nullptr, 0, 0, f32, n, p, nsplit, part, part_stride, queue, variant, st);
 }
 
 hipError_t ppls_launch_gram_finish(const double* part, int nsplit, int64_t part_stride, int p, double* G,

@@ -17,9 +17,13 @@
 extern "C" {
 // Gram of the joint column space [X | Y] (xcols columns of X at stride ldx, then ycols of Y at
 // stride ldy; both multiples of the 16-B vector): lower 128 x 128 tiles per row split into part
-// (p x p row-major per split, p = output edge); ppls_launch_gram_finish mirrors them.
+// (p x p row-major per split, p = output edge); ppls_launch_gram_finish mirrors them.  variant:
+// PPLS_GRAM_SKIP (no MFMAs on padding or above the diagonal) | PPLS_GRAM_DYN (persistent workgroups
+// taking items from per-XCD-group queues; `queue` = ppls_gram_queue_ints(p, nsplit) device ints
+// filled once by ppls_gram_queue_prepare).
 hipError_t ppls_launch_gram_joint(const void* X, int ldx, int xcols, const void* Y, int ldy, int ycols, int f32,
-                                  int64_t n, int p, int nsplit, double* part, int64_t part_stride, hipStream_t st);
+                                  int64_t n, int p, int nsplit, double* part, int64_t part_stride, int* queue,
+                                  int variant, hipStream_t st);
 
 // Rows of S per wave of the tile kernel (rw_opt 1, 2, 4 or 8 (r <= 8) forces it; 0 = auto).
 int ppls_xprod_tile_rows(int P, int r, int rw_opt, int num_cus);
