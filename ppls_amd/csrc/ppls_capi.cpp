@@ -656,18 +656,24 @@ int gram_splits(ppls_ctx* c, int p, int64_t n) {
 }
 
 // The persistent Gram's work queue for a p x p Gram in nsplit row splits (prepared once per shape).
-int gram_queue(ppls_ctx* c, int p, int nsplit, int** q) {
+// joint: the S = [X Y]'[X Y] column space (X's and Y's real columns within their padded rows), else
+// the p columns of one block.
+int gram_queue(ppls_ctx* c, int p, int nsplit, bool joint, int** q) {
   *q = nullptr;
   if (!(c->gram_variant & PPLS_GRAM_DYN)) return PPLS_OK;
-  if (c->gram_q && c->gq_p == p && c->gq_nsplit == nsplit && c->gq_variant == c->gram_variant) {
+  const int key = joint ? -p : p;
+  if (c->gram_q && c->gq_p == key && c->gq_nsplit == nsplit && c->gq_variant == c->gram_variant) {
     *q = c->gram_q;
     return PPLS_OK;
   }
   int rc;
   c->gq_p = -1;
   if ((rc = dalloc(c, &c->gram_q, (size_t)ppls_gram_queue_ints(p, nsplit)))) return rc;
-  HIPCHK(c, ppls_gram_queue_prepare(c->gram_q, p, nsplit, c->gram_variant, c->stream));
-  c->gq_p = p;
+  if (joint)
+    HIPCHK(c, ppls_gram_queue_prepare(c->gram_q, p, c->p, c->ldx, c->q, nsplit, c->gram_variant, c->stream));
+  else
+    HIPCHK(c, ppls_gram_queue_prepare(c->gram_q, p, p, p, 0, nsplit, c->gram_variant, c->stream));
+  c->gq_p = key;
   c->gq_nsplit = nsplit;
   c->gq_variant = c->gram_variant;
   *q = c->gram_q;
@@ -720,7 +726,7 @@ int xprod_setup(ppls_ctx* c) {
   int* gq = nullptr;
   int rc_alloc = dalloc(c, &c->xp_S, PP);
   if (!rc_alloc && c->n_local > 0) rc_alloc = dalloc(c, &part, (size_t)nsplit * PP);
-  if (!rc_alloc && c->n_local > 0) rc_alloc = gram_queue(c, P, nsplit, &gq);
+  if (!rc_alloc && c->n_local > 0) rc_alloc = gram_queue(c, P, nsplit, true, &gq);
   if (c->nranks > 1 || c->reducer) {
     const double f = rc_alloc ? 1.0 : 0.0;
     double tot = 0.0;
@@ -747,8 +753,8 @@ int xprod_setup(ppls_ctx* c) {
     if (e == hipSuccess) e = hipEventCreate(&e1);
     if (e == hipSuccess) e = hipEventRecord(e0, c->stream);
     if (e == hipSuccess)
-      e = ppls_launch_gram_joint(c->X, c->ldx, c->ldx, c->Y, c->ldy, c->ldy, c->dtype, c->n_local, P, nsplit, part,
-                                 (int64_t)PP, gq, c->gram_variant, c->stream);
+      e = ppls_launch_gram_joint(c->X, c->ldx, c->ldx, c->p, c->Y, c->ldy, c->ldy, c->q, c->dtype, c->n_local, P,
+                                 nsplit, part, (int64_t)PP, gq, c->gram_variant, c->stream);
     if (e == hipSuccess) e = ppls_launch_gram_finish(part, nsplit, (int64_t)PP, P, c->xp_S, c->stream);
     if (e == hipSuccess) e = hipEventRecord(e1, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
@@ -2369,7 +2375,7 @@ int ppls_variances(ppls_ctx* c, const double* mu, const double* Cdiag, double si
       const int nsplit = gram_splits(c, p, n);
       VRC(dalloc(c, &dpart, (size_t)nsplit * pp));
       int* gq = nullptr;
-      VRC(gram_queue(c, p, nsplit, &gq));
+      VRC(gram_queue(c, p, nsplit, false, &gq));
       VCHK(ppls_launch_gram(D, f32, n, ld, p, nsplit, dpart, (int64_t)pp, gq, c->gram_variant, c->stream));
       VCHK(ppls_launch_gram_finish(dpart, nsplit, (int64_t)pp, p, dG, c->stream));
       dfree(dpart);
@@ -2475,7 +2481,7 @@ int ppls_gram(ppls_ctx* c, int xory, int nsplit, double* G, double* ms) {
   if ((rc = dalloc(c, &dpart, (size_t)nsplit * pp))) return rc;
   if ((rc = dalloc(c, &dG, pp))) { dfree(dpart); return rc; }
   int* gq = nullptr;
-  if ((rc = gram_queue(c, p, nsplit, &gq))) { dfree(dpart); dfree(dG); return rc; }
+  if ((rc = gram_queue(c, p, nsplit, false, &gq))) { dfree(dpart); dfree(dG); return rc; }
   hipEvent_t e0, e1;
   HIPCHK(c, hipEventCreate(&e0));
   HIPCHK(c, hipEventCreate(&e1));

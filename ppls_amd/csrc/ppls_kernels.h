@@ -153,7 +153,9 @@ int ppls_gram_tiles(int p);
 int ppls_gram_occupancy(int f32);
 int ppls_gram_splits(int p, int64_t n, int slots, int variant);
 int64_t ppls_gram_queue_ints(int p, int nsplit);
-hipError_t ppls_gram_queue_prepare(int* queue, int p, int nsplit, int variant, hipStream_t st);
+// xreal, xcols, yreal: the joint columns that can be non-zero ([0, xreal) and [xcols, xcols + yreal))
+hipError_t ppls_gram_queue_prepare(int* queue, int p, int xreal, int xcols, int yreal, int nsplit, int variant,
+                                   hipStream_t st);
 hipError_t ppls_launch_gram(const void* X, int f32, int64_t n, int ld, int p, int nsplit, double* part,
                             int64_t part_stride, int* queue, int variant, hipStream_t st);
 hipError_t ppls_launch_gram_finish(const double* part, int nsplit, int64_t part_stride, int p, double* G,

@@ -51,19 +51,41 @@ struct GVec<float> {
 
 }  // namespace
 
+// The columns of the joint space that can be non-zero: [0, xreal) of X and [xcols, xcols + yreal) of
+// Y -- between and after them lie the rows' zero padding (C5: X columns 10,000 .. 10,239).
+struct PplsGramCols {
+  int p, xreal, xcols, yend;
+};
+
+// Whether the 16 columns [a, a + 16) of the joint space hold any that can be non-zero.
+__host__ __device__ inline bool ppls_gram_live(const PplsGramCols& g, int a) {
+  return a < g.p && (a < g.xreal || (a + 16 > g.xcols && a < g.yend));
+}
+
 // Active 16 x 16 MFMA blocks of wave (wi, wj) in the lower tile (I, J) of a p x p Gram: bit m * 4 + q
-// for the wave's block row m and block column q.  A block is skipped when its rows or columns lie
-// wholly in the padding past p, or -- in a diagonal tile -- when it lies wholly above the diagonal
-// (the finish kernel reads only the lower triangle).  C3 (p = 4000 -> 32 blocks of 128): the last
-// block row is 3/4 padding and the diagonal tiles 7/16 upper half, 7 % of the executed flops.
-__host__ __device__ inline unsigned ppls_gram_active(int I, int J, int wi, int wj, int p) {
+// for the wave's block row m and block column q.  A block is skipped when its rows or columns are
+// all zero padding (past p, or between X's real columns and Y's), or -- in a diagonal tile -- when it
+// lies wholly above the diagonal (the finish kernel reads only the lower triangle).  C3 (p = 4000 ->
+// 32 blocks of 128): the last block row is 3/4 padding and the diagonal tiles 7/16 upper half, 7 %
+// of the executed flops; C5 also skips the 240 padding columns of X's 40,960-B rows (4 %).  Skipped
+// blocks inside p are written as the zeros they are (their accumulators are never touched).
+__host__ __device__ inline unsigned ppls_gram_active(int I, int J, int wi, int wj, const PplsGramCols& g) {
   unsigned act = 0;
   for (int m = 0; m < 4; ++m)
     for (int q = 0; q < 4; ++q) {
       const int i0 = I * PPLS_GT + wi * 64 + m * 16, j0 = J * PPLS_GT + wj * 64 + q * 16;
-      if (i0 < p && j0 < p && (I != J || wj * 4 + q <= wi * 4 + m)) act |= 1u << (m * 4 + q);
+      if (ppls_gram_live(g, i0) && ppls_gram_live(g, j0) && (I != J || wj * 4 + q <= wi * 4 + m))
+        act |= 1u << (m * 4 + q);
     }
   return act;
+}
+
+// Whether tile (I, J) has any skipped block (its items take the masked code path).
+__host__ __device__ inline bool ppls_gram_partial(int I, int J, const PplsGramCols& g) {
+  if (I == J) return true;
+  for (int a = 0; a < PPLS_GT; a += 16)
+    if (!ppls_gram_live(g, I * PPLS_GT + a) || !ppls_gram_live(g, J * PPLS_GT + a)) return true;
+  return false;
 }
 
 __host__ __device__ inline void ppls_gram_tile_of(int t, int* I, int* J) {
@@ -114,7 +136,7 @@ template <typename T, bool SKIP, bool MASKED>
 __device__ __forceinline__ void ppls_gram_item(const T* __restrict__ X, int ldx, int xcols, const T* __restrict__ Y,
                                                int ldy, int ycols, int64_t n, int p, int ntiles, int nsplit,
                                                int64_t L, double* __restrict__ part, int64_t part_stride,
-                                               double (*sm)[2][PPLS_GK][PPLS_GLD]) {
+                                               const PplsGramCols gc, double (*sm)[2][PPLS_GK][PPLS_GLD]) {
   typedef double d4 __attribute__((ext_vector_type(4)));
   constexpr int EV = 16 / sizeof(T);              // elements per 16-B load
   constexpr int VPR = PPLS_GT / EV;               // 16-B vectors per panel row
@@ -127,7 +149,7 @@ __device__ __forceinline__ void ppls_gram_item(const T* __restrict__ X, int ldx,
   const int wi = wave >> 1, wj = wave & 1;
   const int colA = I * PPLS_GT, colB = J * PPLS_GT;
   // wave-uniform (SGPR) block mask; MASKED code paths test it per MFMA, the full path does not
-  const unsigned act = SKIP ? ppls_gram_active(I, J, wi, wj, p) : 0xffffu;
+  const unsigned act = SKIP ? ppls_gram_active(I, J, wi, wj, gc) : 0xffffu;
 
   GVec<T> ra[NV], rb[NV];
   auto load = [&](int64_t k0) {
@@ -194,7 +216,6 @@ __device__ __forceinline__ void ppls_gram_item(const T* __restrict__ X, int ldx,
   for (int m = 0; m < 4; ++m)
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      if (MASKED && !((act >> (m * 4 + q)) & 1u)) continue;
       const int j = colB + wj * 64 + q * 16 + cl;
 #pragma unroll
       for (int g = 0; g < 4; ++g) {   // f64 MFMA D map: col = lane & 15, row = (lane >> 4) + 4 g
@@ -209,7 +230,8 @@ __global__ __launch_bounds__(256, 2) void ppls_gram_mfma_kernel(const T* __restr
                                                                  const T* __restrict__ Y, int ldy, int ycols,
                                                                  int64_t n, int p, int ntiles, int nsplit,
                                                                  int64_t work, double* __restrict__ part,
-                                                                 int64_t part_stride, int* __restrict__ queue) {
+                                                                 int64_t part_stride, int* __restrict__ queue,
+                                                                 PplsGramCols gc) {
   __shared__ __attribute__((aligned(16))) double sm[2][2][PPLS_GK][PPLS_GLD];
   if constexpr (!DYN) {
     const int64_t per = gridDim.x >> 3;
@@ -218,12 +240,12 @@ __global__ __launch_bounds__(256, 2) void ppls_gram_mfma_kernel(const T* __restr
     if (SKIP) {
       int I, J;
       ppls_gram_tile_of((int)(L % ntiles), &I, &J);
-      if (I == J || (I + 1) * PPLS_GT > p) {   // a tile with skipped blocks: the masked code path
-        ppls_gram_item<T, true, true>(X, ldx, xcols, Y, ldy, ycols, n, p, ntiles, nsplit, L, part, part_stride, sm);
+      if (ppls_gram_partial(I, J, gc)) {   // a tile with skipped blocks: the masked code path
+        ppls_gram_item<T, true, true>(X, ldx, xcols, Y, ldy, ycols, n, p, ntiles, nsplit, L, part, part_stride, gc, sm);
         return;
       }
     }
-    ppls_gram_item<T, false, false>(X, ldx, xcols, Y, ldy, ycols, n, p, ntiles, nsplit, L, part, part_stride, sm);
+    ppls_gram_item<T, false, false>(X, ldx, xcols, Y, ldy, ycols, n, p, ntiles, nsplit, L, part, part_stride, gc, sm);
   } else {
     // queue = [qoff (9) | counters (8, zeroed before the launch) | items (work)]
     const int* qoff = queue;
@@ -239,10 +261,10 @@ __global__ __launch_bounds__(256, 2) void ppls_gram_mfma_kernel(const T* __restr
       if (L < 0) return;
       int I, J;
       ppls_gram_tile_of(L % ntiles, &I, &J);
-      if (SKIP && (I == J || (I + 1) * PPLS_GT > p))
-        ppls_gram_item<T, true, true>(X, ldx, xcols, Y, ldy, ycols, n, p, ntiles, nsplit, L, part, part_stride, sm);
+      if (SKIP && ppls_gram_partial(I, J, gc))
+        ppls_gram_item<T, true, true>(X, ldx, xcols, Y, ldy, ycols, n, p, ntiles, nsplit, L, part, part_stride, gc, sm);
       else
-        ppls_gram_item<T, false, false>(X, ldx, xcols, Y, ldy, ycols, n, p, ntiles, nsplit, L, part, part_stride, sm);
+        ppls_gram_item<T, false, false>(X, ldx, xcols, Y, ldy, ycols, n, p, ntiles, nsplit, L, part, part_stride, gc, sm);
     }
   }
 }
@@ -380,12 +402,12 @@ int ppls_gram_occupancy(int f32) {
 }
 
 // MFMA blocks an item of tile t executes (of 64): the persistent queue's cost order.
-static int ppls_gram_cost(int t, int p, int variant) {
+static int ppls_gram_cost(int t, const PplsGramCols& gc, int variant) {
   if (!(variant & PPLS_GRAM_SKIP)) return 64;
   int I, J;
   ppls_gram_tile_of(t, &I, &J);
   int c = 0;
-  for (int w = 0; w < 4; ++w) c += __builtin_popcount(ppls_gram_active(I, J, w >> 1, w & 1, p));
+  for (int w = 0; w < 4; ++w) c += __builtin_popcount(ppls_gram_active(I, J, w >> 1, w & 1, gc));
   return c;
 }
 
@@ -420,12 +442,14 @@ int64_t ppls_gram_queue_ints(int p, int nsplit) { return 17 + (int64_t)ppls_gram
 // range [g W / 8, (g + 1) W / 8) of the split-major order (its XCD's tiles share column panels),
 // sorted costliest first (stable: ties keep the split-major order).  Synchronous (host staging);
 // the launch resets the counters, so one prepared queue serves any number of launches.
-hipError_t ppls_gram_queue_prepare(int* queue, int p, int nsplit, int variant, hipStream_t st) {
+hipError_t ppls_gram_queue_prepare(int* queue, int p, int xreal, int xcols, int yreal, int nsplit, int variant,
+                                   hipStream_t st) {
+  const PplsGramCols gc{p, xreal, xcols, xcols + yreal};
   const int ntiles = ppls_gram_tiles(p);
   const int64_t work = (int64_t)ntiles * nsplit;
   std::vector<int> h((size_t)ppls_gram_queue_ints(p, nsplit), 0);
   std::vector<int> tc((size_t)ntiles);
-  for (int t = 0; t < ntiles; ++t) tc[(size_t)t] = ppls_gram_cost(t, p, variant);
+  for (int t = 0; t < ntiles; ++t) tc[(size_t)t] = ppls_gram_cost(t, gc, variant);
   int* items = h.data() + 17;
   for (int g = 0; g < 8; ++g) {
     const int64_t a = work * g / 8, b = work * (g + 1) / 8;
@@ -440,10 +464,11 @@ hipError_t ppls_gram_queue_prepare(int* queue, int p, int nsplit, int variant, h
   return e;
 }
 
-hipError_t ppls_launch_gram_joint(const void* X, int ldx, int xcols, const void* Y, int ldy, int ycols, int f32,
-                                  int64_t n, int p, int nsplit, double* part, int64_t part_stride, int* queue,
-                                  int variant, hipStream_t st) {
-  if (n <= 0 || p <= 0 || nsplit < 1 || xcols + ycols < 1) return hipErrorInvalidValue;
+hipError_t ppls_launch_gram_joint(const void* X, int ldx, int xcols, int xreal, const void* Y, int ldy, int ycols,
+                                  int yreal, int f32, int64_t n, int p, int nsplit, double* part, int64_t part_stride,
+                                  int* queue, int variant, hipStream_t st) {
+  if (n <= 0 || p <= 0 || nsplit < 1 || xcols + ycols < 1 || xreal > xcols || yreal > ycols) return hipErrorInvalidValue;
+  const PplsGramCols gc{p, xreal, xcols, xcols + yreal};
   const int ev = f32 ? 4 : 2;
   if (xcols % ev || ycols % ev) return hipErrorInvalidValue;
   const int ntiles = ppls_gram_tiles(p);
@@ -464,7 +489,7 @@ hipError_t ppls_launch_gram_joint(const void* X, int ldx, int xcols, const void*
   }
 #define PPLS_GRAM_LAUNCH(TT, D, S)                                                                           \
   hipLaunchKernelGGL((ppls_gram_mfma_kernel<TT, D, S>), dim3((unsigned)grid), dim3(256), 0, st, (const TT*)X, ldx, \
-                     xcols, (const TT*)Y, ldy, ycols, n, p, ntiles, nsplit, work, part, part_stride, queue)
+                     xcols, (const TT*)Y, ldy, ycols, n, p, ntiles, nsplit, work, part, part_stride, queue, gc)
   if (f32) {
     if (dyn && skip) PPLS_GRAM_LAUNCH(float, true, true);
     else if (dyn) PPLS_GRAM_LAUNCH(float, true, false);
@@ -482,7 +507,7 @@ hipError_t ppls_launch_gram_joint(const void* X, int ldx, int xcols, const void*
 
 hipError_t ppls_launch_gram(const void* X, int f32, int64_t n, int ld, int p, int nsplit, double* part,
                             int64_t part_stride, int* queue, int variant, hipStream_t st) {
-  return ppls_launch_gram_joint(X, ld, ld, nullptr, 0, 0, f32, n, p, nsplit, part, part_stride, queue, variant, st);
+  return ppls_launch_gram_joint(X, ld, ld, p, nullptr, 0, 0, 0, f32, n, p, nsplit, part, part_stride, queue, variant, st);
 }
 
 hipError_t ppls_launch_gram_finish(const double* part, int nsplit, int64_t part_stride, int p, double* G,

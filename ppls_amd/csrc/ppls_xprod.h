@@ -21,9 +21,10 @@ extern "C" {
 // PPLS_GRAM_SKIP (no MFMAs on padding or above the diagonal) | PPLS_GRAM_DYN (persistent workgroups
 // taking items from per-XCD-group queues; `queue` = ppls_gram_queue_ints(p, nsplit) device ints
 // filled once by ppls_gram_queue_prepare).
-hipError_t ppls_launch_gram_joint(const void* X, int ldx, int xcols, const void* Y, int ldy, int ycols, int f32,
-                                  int64_t n, int p, int nsplit, double* part, int64_t part_stride, int* queue,
-                                  int variant, hipStream_t st);
+// xreal / yreal: X's and Y's real columns (the rest of xcols / ycols is zero padding, skipped).
+hipError_t ppls_launch_gram_joint(const void* X, int ldx, int xcols, int xreal, const void* Y, int ldy, int ycols,
+                                  int yreal, int f32, int64_t n, int p, int nsplit, double* part, int64_t part_stride,
+                                  int* queue, int variant, hipStream_t st);
 
 // Rows of S per wave of the tile kernel (rw_opt 1, 2, 4 or 8 (r <= 8) forces it; 0 = auto).
 int ppls_xprod_tile_rows(int P, int r, int rw_opt, int num_cus);
