@@ -120,6 +120,17 @@ def load_compute_counters(workload_key, kernel_sub):
                 source=dict(_source(name, js), kernel=kernel_sub))
 
 
+def host_cores():
+    """What "all cores" means on this host: the machine's CPUs (os.cpu_count = nproc without an
+    affinity mask), the CPUs this process may run on (its affinity mask), and the OpenMP thread
+    count the C baseline runs with (OMP_NUM_THREADS or the runtime default)."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = None
+    return dict(nproc=os.cpu_count(), affinity=aff, omp_num_threads_env=os.environ.get("OMP_NUM_THREADS"))
+
+
 def cpu_model():
     try:
         with open("/proc/cpuinfo") as f:
@@ -165,7 +176,7 @@ def cpu_baseline(ctx, th0, cfg, iters=3, one_core_rows=100_000):
     werr = float(max(np.abs(est.W - Wc).max(), np.abs(est.C - Cc).max()))
     n = cfg["n"]
     one_core = iters * ns / dt1 / n
-    return dict(value=iters / dt, unit="EM iterations/s", cores=int(cores), kind="port",
+    return dict(value=iters / dt, unit="EM iterations/s", cores=int(cores), kind="port", host=host_cores(),
                 sample=f"{iters} steady-state EM iterations (after 1 untimed, {t_first:.1f} s) on all n={n} rows "
                        f"in {dt:.1f} s: oracle/cpu_ref.c (reference pass structure), OpenMP {cores} threads, "
                        f"-O3 -march=native, {cpu_model()}",
@@ -214,7 +225,11 @@ def bench_xprod(ctx, th0, args, barrier, tmax, r, ll_stream, t_stream):
     t_x = dt / args.xprod_steps
     avg_us = 1e3 * kms / max(launches, 1)
     achieved = info["bytes_per_pass"] / (avg_us * 1e-6) / 1e9 if launches else None
-    gram_tf = info["gram_flops"] / (gram_ms * 1e-3) / 1e12 if gram_ms > 0 else None
+    # useful flops of S: the lower triangle incl. the diagonal over the real columns, n P (P + 1)
+    # (P = p + q; the kernel also runs the zero padding of 128-column tiles it cannot skip)
+    Pr = float(ctx.p + ctx.q)
+    useful = float(ctx.n_local) * Pr * (Pr + 1.0)   # this rank's rows: its kernel's time
+    gram_tf = useful / (gram_ms * 1e-3) / 1e12 if gram_ms > 0 else None
     traffic, traffic_src = load_xprod_traffic(args.config)
 
     def fit_s(steps):   # a PPLS_simult loop of `steps` iterations (+1 sweep for the last loglik)
@@ -228,7 +243,8 @@ def bench_xprod(ctx, th0, args, barrier, tmax, r, ll_stream, t_stream):
         setup_total_ms_rank0=total_ms,
         gram_roofline=dict(bound="mfma", achieved=gram_tf, peak=FP64_PEAK_TF, unit="TFLOP/s",
                            frac=(gram_tf / FP64_PEAK_TF) if gram_tf else None,
-                           flops_per_launch=info["gram_flops"],
+                           flops_per_launch=useful, flops="useful: n P (P + 1), P = p + q, this rank's rows",
+                           tile_flops_per_launch=info["gram_flops"],
                            counters=load_compute_counters(f"{args.config}_dp1", "gram_mfma")),
         steps=args.xprod_steps, ms_per_step=1e3 * t_x, it_per_s=1.0 / t_x,
         roofline=dict(bound="hbm", achieved=achieved, peak=HBM_PEAK_GBS, unit="GB/s",
@@ -298,6 +314,7 @@ def cpu_call_baseline(ctx, r, cfg, device, rows):
     k = min(len(gl), len(ll))
     scale = cfg["n"] / rows
     return dict(value=dt * scale, unit="seconds per PPLS_simult call (scaled to n)", cores=int(cores), kind="port",
+                host=host_cores(),
                 sample=f"PPLS_simult(X, Y, {r}) with the defaults (PPLS(X, Y, {r}, 20, 1e-4) from the same 'random' "
                        f"draws, EMsteps 10, atol 1e-4, Eout) on the first {rows} of n = {cfg['n']} rows in {dt:.1f} s "
                        f"(init {secs['init']:.1f} s, loop {secs['loop']:.1f} s, Eout {secs['eout']:.2f} s; "
@@ -473,9 +490,19 @@ def main():
         digest_parts.append(np.ones(1))
     digest = _digest(digest_parts)
     digests = [digest]
+    # per rank: its sweep kernel's average (HIP events), its statistics all-reduce (RCCL: events
+    # around the collective) and the all-reduce of S -- a scaling run shows load balance and
+    # collective cost without re-profiling
+    mine = dict(sweep_kernel_ms=kern_ms / max(launches, 1) if launches else None,
+                allreduce_us=(1e3 * ar_ms / ar_calls) if ar_calls else None,
+                xprod_setup_allreduce_ms=xp["setup_allreduce_ms"] if xp else None,
+                xprod_gram_kernel_ms=xp["gram_kernel_ms"] if xp else None, rows=n_local)
+    ranks = [mine]
     if dist is not None:
         digests = [None] * world
         dist.all_gather_object(digests, digest)
+        ranks = [None] * world
+        dist.all_gather_object(ranks, mine)
     backend = "none" if world == 1 else ("rccl" if args.comm == "rccl" else "host reducer over gloo")
     problems = []
     if len(set(digests)) != 1:
@@ -524,6 +551,19 @@ def main():
             roofline["counters"] = {k: load_compute_counters(wl, k) for k in ("panel_mfmadots", "panel_acc")}
         else:
             roofline["counters"] = {"sweep_split": load_compute_counters(wl, "sweep_split")}
+        if xp is not None:
+            # the north star's "MFMA utilisation on the M-step GEMMs": the GEMM on MFMA is the Gram that
+            # forms S (every statistic of the M-step is then read off S); the streaming sweep's
+            # X'mu_T runs on fp64 VALU (r = 5 fills 5 of an MFMA's 16 columns, gfx950's fp64 MFMA and
+            # VALU rates are equal, and the sweep already sits at its HBM read ceiling)
+            g = xp["gram_roofline"]
+            roofline["mfma_gemm"] = dict(
+                gemm="S = [X Y]'[X Y], the cross-product form of the M-step sums X'mu_T, Y'mu_U and the E-step Gram "
+                     "(EM_W_multi.R:689-690, 732-733); variances.PPLS_simult's X'X (:846) runs the same kernel",
+                kernel="ppls_gram_mfma_kernel (v_mfma_f64_16x16x4_f64)", fp64_mfma_tflops=g["achieved"],
+                peak_tflops=FP64_PEAK_TF, frac=g["frac"], kernel_ms=xp["gram_kernel_ms"],
+                flops=g["flops"], counters=g["counters"],
+                sweep_note="the streaming sweep's X'mu_T / Y'mu_U run on fp64 VALU (counters.sweep_split)")
         out = dict(metric=METRIC, value=its, unit="EM iterations/s", n_gpus=world, steps=args.steps,
                    warmup=args.warmup, ms_per_step=1e3 * dt / args.steps, higher_is_better=True,
                    scaling="strong", vs_baseline=None, dtype="f64",
@@ -543,6 +583,13 @@ def main():
                              allreduce_timed_calls=ar_calls),
                    theta_sha16=digest, ranks_bitwise_identical=True)
         out["xprod"] = xp
+        if world > 1:
+            def spread(key):
+                v = [rk[key] for rk in ranks]
+                ok = [x for x in v if x is not None]
+                return dict(min=min(ok) if ok else None, max=max(ok) if ok else None, per_rank=v)
+            out["per_rank"] = {k: spread(k) for k in ("sweep_kernel_ms", "allreduce_us", "xprod_setup_allreduce_ms",
+                                                      "xprod_gram_kernel_ms", "rows")}
         if call is not None:
             out["call_seconds"] = {m: call[m]["seconds"] for m in ("stream", "xprod", "auto")}
             out["call"] = dict(what=f"PPLS_simult(X, Y, {r}) with its defaults: PPLS(X, Y, {r}, 20, 1e-4, 'random') "

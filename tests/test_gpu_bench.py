@@ -49,6 +49,19 @@ def test_bench_two_ranks_spawn_path_equals_one_rank():
         assert a["em_steps"] == b["em_steps"] and a["init_steps"] == b["init_steps"]
         assert abs(a["loglik_last"] - b["loglik_last"]) <= 1e-10 * abs(b["loglik_last"])
     assert two["call"]["xprod"]["read_S"] and not two["call"]["stream"]["read_S"]
+    # per-rank spreads (a scaling run explains itself): every rank's sweep kernel time and rows, the
+    # all-reduce of S; the statistics all-reduce is timed on the RCCL path only (None here)
+    pr_ = two["per_rank"]
+    assert len(pr_["sweep_kernel_ms"]["per_rank"]) == 2
+    assert 0 < pr_["sweep_kernel_ms"]["min"] <= pr_["sweep_kernel_ms"]["max"]
+    assert sum(pr_["rows"]["per_rank"]) == 125_000
+    assert pr_["xprod_setup_allreduce_ms"]["min"] > 0
+    assert pr_["allreduce_us"]["per_rank"] == [None, None]
+    assert "per_rank" not in one
+    # the Gram that forms S is reported on its useful flops, and beside the MFMA peak
+    g = one["xprod"]["gram_roofline"]
+    assert g["bound"] == "mfma" and 0 < g["frac"] < 1 and g["flops_per_launch"] < g["tile_flops_per_launch"]
+    assert one["roofline"]["mfma_gemm"]["kernel"].startswith("ppls_gram_mfma")
 
 
 def test_bench_diverging_ranks_fail_loudly():
