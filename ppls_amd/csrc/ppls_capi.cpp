@@ -134,11 +134,9 @@ struct ppls_ctx {
   double xp_setup_total_ms = 0.0;
   double xp_setup_ar_ms = 0.0;   // the all-reduce of S (wall clock around it and its stream sync)
   int xp_nsplit = 0;
-  // the MFMA Gram (S, variances' X'X): option "gram" = PPLS_GRAM_* bits (default PPLS_GRAM_DEFAULT)
-  // and the persistent form's work queue, prepared for (gq_p, gq_nsplit, gq_variant)
-  int gram_variant = PPLS_GRAM_DEFAULT;
+  // the MFMA Gram's work queue (S, variances' X'X), prepared for one shape
   int* gram_q = nullptr;
-  int gq_p = -1, gq_nsplit = -1, gq_variant = -1;
+  int64_t gq_key[6] = {-1, -1, -1, -1, -1, -1};   // (p, xreal, xcols, yreal, n, nsplit_req) of gram_q
   rocblas_handle blas = nullptr;   // rocSOLVER (variances.PPLS_simult's p x p inverse), created lazily
   int var_chol = 1;                // option "var_chol": that inverse by Cholesky when positive definite (1) or LU (0)
   // timing
@@ -649,34 +647,75 @@ int finalize(ppls_ctx* c, int r, int cur, int nxt, int logl_index, int type, int
   return PPLS_OK;
 }
 
-// Row splits of the MFMA Gram of a p x p product over n rows: enough work items to fill the device
-// (whole rounds of resident workgroups), each split's p x p partial kept under 4 GB in all.
-int gram_splits(ppls_ctx* c, int p, int64_t n) {
-  return ppls_gram_splits(p, n, c->num_cus * ppls_gram_occupancy(c->dtype), c->gram_variant);
+// The column space of one MFMA Gram (ppls_variances.hip): joint = S = [X Y]'[X Y] over the padded
+// rows (X's p real columns of ldx, then Y's q of ldy), else D'D for D = X (xory 0) or Y.
+struct GramShape {
+  int p, xreal, xcols, yreal;
+  const void* X;
+  int ldx;
+  const void* Y;
+  int ldy, ycols;
+};
+
+GramShape gram_shape(const ppls_ctx* c, bool joint, int xory) {
+  if (joint) return GramShape{c->ldx + c->ldy, c->p, c->ldx, c->q, c->X, c->ldx, c->Y, c->ldy, c->ldy};
+  const int p = xory ? c->q : c->p, ld = xory ? c->ldy : c->ldx;
+  return GramShape{p, p, ld, 0, xory ? (const void*)c->Y : (const void*)c->X, ld, nullptr, 0, 0};
 }
 
-// The persistent Gram's work queue for a p x p Gram in nsplit row splits (prepared once per shape).
-// joint: the S = [X Y]'[X Y] column space (X's and Y's real columns within their padded rows), else
-// the p columns of one block.
-int gram_queue(ppls_ctx* c, int p, int nsplit, bool joint, int** q) {
-  *q = nullptr;
-  if (!(c->gram_variant & PPLS_GRAM_DYN)) return PPLS_OK;
-  const int key = joint ? -p : p;
-  if (c->gram_q && c->gq_p == key && c->gq_nsplit == nsplit && c->gq_variant == c->gram_variant) {
+int gram_wave_slots(const ppls_ctx* c) { return c->num_cus * ppls_gram_occupancy(c->dtype) * 4; }
+
+// Row splits of a Gram over n rows (0 = auto: halving splits, ppls_gram_plan).
+int gram_nsplit(const ppls_ctx* c, const GramShape& g, int64_t n, int req) {
+  return ppls_gram_plan(g.p, g.xreal, g.xcols, g.yreal, n, gram_wave_slots(c), req, nullptr);
+}
+
+// The Gram's work queue for (shape, n, req), prepared once and kept while the shape repeats.
+int gram_queue(ppls_ctx* c, const GramShape& g, int64_t n, int req, int** q) {
+  const int64_t key[6] = {g.p, g.xreal, g.xcols, g.yreal, n, req};
+  if (c->gram_q && !memcmp(key, c->gq_key, sizeof key)) {
     *q = c->gram_q;
     return PPLS_OK;
   }
+  *q = nullptr;
   int rc;
-  c->gq_p = -1;
-  if ((rc = dalloc(c, &c->gram_q, (size_t)ppls_gram_queue_ints(p, nsplit)))) return rc;
-  if (joint)
-    HIPCHK(c, ppls_gram_queue_prepare(c->gram_q, p, c->p, c->ldx, c->q, nsplit, c->gram_variant, c->stream));
-  else
-    HIPCHK(c, ppls_gram_queue_prepare(c->gram_q, p, p, p, 0, nsplit, c->gram_variant, c->stream));
-  c->gq_p = key;
-  c->gq_nsplit = nsplit;
-  c->gq_variant = c->gram_variant;
+  c->gq_key[0] = -1;
+  const int nsplit = gram_nsplit(c, g, n, req);
+  if ((rc = dalloc(c, &c->gram_q, (size_t)ppls_gram_queue_ints(g.p, nsplit)))) return rc;
+  HIPCHK(c, ppls_gram_queue_prepare(c->gram_q, g.p, g.xreal, g.xcols, g.yreal, n, gram_wave_slots(c), req, c->stream));
+  memcpy(c->gq_key, key, sizeof key);
   *q = c->gram_q;
+  return PPLS_OK;
+}
+
+// G (device, p x p column-major) = the Gram of this rank's n rows: the MFMA kernel into per-item
+// partials, then the finish (sum over splits, mirrored).  ms: the MFMA kernel's duration (HIP
+// events), if not null.  The partials are allocated here and freed.
+int gram_run(ppls_ctx* c, const GramShape& g, int64_t n, int req, double* G, float* ms) {
+  int rc;
+  const int nsplit = gram_nsplit(c, g, n, req);
+  double* part = nullptr;
+  int* q = nullptr;
+  if ((rc = dalloc(c, &part, (size_t)ppls_gram_part_doubles(g.p, nsplit)))) return rc;
+  if ((rc = gram_queue(c, g, n, req, &q))) { dfree(part); return rc; }
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  hipError_t e = hipSuccess;
+  if (ms) {
+    e = hipEventCreate(&e0);
+    if (e == hipSuccess) e = hipEventCreate(&e1);
+    if (e == hipSuccess) e = hipEventRecord(e0, c->stream);
+  }
+  if (e == hipSuccess)
+    e = ppls_launch_gram_joint(g.X, g.ldx, g.xcols, g.xreal, g.Y, g.ldy, g.ycols, g.yreal, c->dtype, n, g.p, nsplit, part,
+                               q, c->stream);
+  if (e == hipSuccess && ms) e = hipEventRecord(e1, c->stream);
+  if (e == hipSuccess) e = ppls_launch_gram_finish(part, nsplit, g.p, g.xreal, g.xcols, g.yreal, G, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  if (e == hipSuccess && ms) e = hipEventElapsedTime(ms, e0, e1);
+  if (e0) (void)hipEventDestroy(e0);
+  if (e1) (void)hipEventDestroy(e1);
+  dfree(part);
+  if (e != hipSuccess) return fail(c, PPLS_E_HIP, "MFMA Gram: %s", hipGetErrorString(e));
   return PPLS_OK;
 }
 
@@ -686,12 +725,13 @@ bool xprod_choose(ppls_ctx* c, int max_steps, int r);
 // Rows per rank the cross-product setup is sized for: the same on every rank (ceil(n_total / nranks)).
 int64_t xprod_rows(const ppls_ctx* c) { return (c->n_total + c->nranks - 1) / c->nranks; }
 
-// HBM the cross-product form allocates: S (8 P^2 B), the Gram partials while S is formed
-// (gram_splits x 8 P^2 B) and M (P x 2 RMAX doubles).
+// HBM the cross-product form allocates: S (8 P^2 B), the Gram partials while S is formed (32 KB
+// per quadrant item and split; a rank with fewer rows plans no more splits) and M (P x 2 RMAX doubles).
 double xprod_bytes(ppls_ctx* c) {
-  const int P = c->ldx + c->ldy;
-  const double PP = (double)P * P;
-  return 8.0 * PP * (1.0 + gram_splits(c, P, xprod_rows(c))) + 16.0 * P * PPLS_RMAX;
+  const GramShape g = gram_shape(c, true, 0);
+  const double PP = (double)g.p * g.p;
+  return 8.0 * PP + 8.0 * (double)ppls_gram_part_doubles(g.p, gram_nsplit(c, g, xprod_rows(c), 0)) +
+         16.0 * g.p * PPLS_RMAX;
 }
 
 // Start a run (or session) on the cross-products when the policy picks them.  In auto mode (-1) a
@@ -718,52 +758,38 @@ int xprod_setup(ppls_ctx* c) {
   const size_t PP = (size_t)P * P;
   int rc;
   const auto t0 = std::chrono::steady_clock::now();
-  // S and the Gram partials; with collectives every rank must know that all ranks allocated them
-  // before anyone enters the all-reduce of S (a rank that returned here alone would leave the
-  // others waiting in it), so the allocation outcome is all-reduced first
-  const int nsplit = gram_splits(c, P, xprod_rows(c));
-  double* part = nullptr;
-  int* gq = nullptr;
+  // S (and, inside gram_run, the Gram partials); with collectives every rank must know that all ranks
+  // allocated S before anyone enters the all-reduce of S (a rank that returned here alone would leave
+  // the others waiting in it), so the allocation outcome is all-reduced first -- the partials are
+  // allocated beside S and released at once, so their outcome is part of it
+  const GramShape g = gram_shape(c, true, 0);
   int rc_alloc = dalloc(c, &c->xp_S, PP);
-  if (!rc_alloc && c->n_local > 0) rc_alloc = dalloc(c, &part, (size_t)nsplit * PP);
-  if (!rc_alloc && c->n_local > 0) rc_alloc = gram_queue(c, P, nsplit, true, &gq);
+  if (!rc_alloc && c->n_local > 0) {
+    double* probe = nullptr;
+    rc_alloc = dalloc(c, &probe, (size_t)ppls_gram_part_doubles(P, gram_nsplit(c, g, c->n_local, 0)));
+    dfree(probe);
+  }
   if (c->nranks > 1 || c->reducer) {
     const double f = rc_alloc ? 1.0 : 0.0;
     double tot = 0.0;
     HIPCHK(c, hipMemcpyAsync(c->flag, &f, sizeof f, hipMemcpyHostToDevice, c->stream));
-    if ((rc = allreduce(c, c->flag, 1))) { dfree(part); dfree(c->xp_S); return rc; }
+    if ((rc = allreduce(c, c->flag, 1))) { dfree(c->xp_S); return rc; }
     HIPCHK(c, hipMemcpyAsync(&tot, c->flag, sizeof tot, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     if (tot > 0.0) {
-      dfree(part);
       dfree(c->xp_S);
       return fail(c, PPLS_E_NOMEM, "cross-products S: %d rank(s) could not allocate %.3g GB of S and Gram partials",
-                  (int)tot, (double)PP * 8.0 * (1.0 + nsplit) / 1e9);
+                  (int)tot, xprod_bytes(c) / 1e9);
     }
   } else if (rc_alloc) {
-    dfree(part);
     dfree(c->xp_S);
     return rc_alloc;
   }
   c->xp_setup_ms = 0.0;
   if (c->n_local > 0) {
-    c->xp_nsplit = nsplit;
-    hipEvent_t e0 = nullptr, e1 = nullptr;
-    hipError_t e = hipEventCreate(&e0);
-    if (e == hipSuccess) e = hipEventCreate(&e1);
-    if (e == hipSuccess) e = hipEventRecord(e0, c->stream);
-    if (e == hipSuccess)
-      e = ppls_launch_gram_joint(c->X, c->ldx, c->ldx, c->p, c->Y, c->ldy, c->ldy, c->q, c->dtype, c->n_local, P,
-                                 nsplit, part, (int64_t)PP, gq, c->gram_variant, c->stream);
-    if (e == hipSuccess) e = ppls_launch_gram_finish(part, nsplit, (int64_t)PP, P, c->xp_S, c->stream);
-    if (e == hipSuccess) e = hipEventRecord(e1, c->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    c->xp_nsplit = gram_nsplit(c, g, c->n_local, 0);
     float ms = 0.f;
-    if (e == hipSuccess) e = hipEventElapsedTime(&ms, e0, e1);
-    if (e0) (void)hipEventDestroy(e0);
-    if (e1) (void)hipEventDestroy(e1);
-    dfree(part);
-    if (e != hipSuccess) return fail(c, PPLS_E_HIP, "cross-products: %s", hipGetErrorString(e));
+    if ((rc = gram_run(c, g, c->n_local, 0, c->xp_S, &ms))) { dfree(c->xp_S); return rc; }
     c->xp_setup_ms = ms;
   } else {
     HIPCHK(c, hipMemsetAsync(c->xp_S, 0, sizeof(double) * PP, c->stream));
@@ -1187,9 +1213,6 @@ int ppls_set_option(ppls_ctx* c, const char* key, int64_t value) {
       HIPCHK(c, hipStreamSynchronize(c->stream));
       xprod_free(c);
     }
-  } else if (!strcmp(key, "gram")) {
-    if (value < 0 || value > 3) return fail(c, PPLS_E_ARG, "gram must be in [0, 3] (PPLS_GRAM_SKIP | PPLS_GRAM_DYN)");
-    c->gram_variant = (int)value;
   } else if (!strcmp(key, "vorth")) {
     if (value < 1 || value > 255) return fail(c, PPLS_E_ARG, "vorth must be in [1, 255]");
     c->vorth = (int)value;
@@ -2372,13 +2395,7 @@ int ppls_variances(ppls_ctx* c, const double* mu, const double* Cdiag, double si
                           hipMemcpyDeviceToDevice, c->stream));
   } else {
     if (n > 0) {
-      const int nsplit = gram_splits(c, p, n);
-      VRC(dalloc(c, &dpart, (size_t)nsplit * pp));
-      int* gq = nullptr;
-      VRC(gram_queue(c, p, nsplit, false, &gq));
-      VCHK(ppls_launch_gram(D, f32, n, ld, p, nsplit, dpart, (int64_t)pp, gq, c->gram_variant, c->stream));
-      VCHK(ppls_launch_gram_finish(dpart, nsplit, (int64_t)pp, p, dG, c->stream));
-      dfree(dpart);
+      VRC(gram_run(c, gram_shape(c, false, xory), n, 0, dG, nullptr));
     } else {
       VCHK(hipMemsetAsync(dG, 0, sizeof(double) * pp, c->stream));
     }
@@ -2464,42 +2481,27 @@ int ppls_variances(ppls_ctx* c, const double* mu, const double* Cdiag, double si
   return done(PPLS_OK);
 }
 
-// Diagnostics / benchmark: G = D'D (D = X for xory 0, Y for 1) on the MFMA Gram kernel only, with an
-// explicit split count (0 = auto as in ppls_variances); G (p x p, column-major) may be NULL.
+// Diagnostics / benchmark: G = D'D (D = X for xory 0, Y for 1) on the MFMA Gram kernel only, with
+// nsplit equal row splits (0 = the automatic halving splits, as in ppls_variances); G (p x p,
+// column-major) may be NULL.
 // *ms receives the Gram kernel's duration (HIP events on the context stream).
 int ppls_gram(ppls_ctx* c, int xory, int nsplit, double* G, double* ms) {
   if (!c) return PPLS_E_ARG;
   if (!c->have_data) return fail(c, PPLS_E_STATE, "no data");
   HIPCHK(c, hipSetDevice(c->device));
-  const int p = xory ? c->q : c->p, ld = xory ? c->ldy : c->ldx;
-  const void* D = xory ? (const void*)c->Y : (const void*)c->X;
+  const int p = xory ? c->q : c->p;
   const size_t pp = (size_t)p * p;
   if (c->n_local <= 0) return fail(c, PPLS_E_STATE, "no rows on this rank");
-  if (nsplit <= 0) nsplit = gram_splits(c, p, c->n_local);
   int rc;
-  double *dpart = nullptr, *dG = nullptr;
-  if ((rc = dalloc(c, &dpart, (size_t)nsplit * pp))) return rc;
-  if ((rc = dalloc(c, &dG, pp))) { dfree(dpart); return rc; }
-  int* gq = nullptr;
-  if ((rc = gram_queue(c, p, nsplit, false, &gq))) { dfree(dpart); dfree(dG); return rc; }
-  hipEvent_t e0, e1;
-  HIPCHK(c, hipEventCreate(&e0));
-  HIPCHK(c, hipEventCreate(&e1));
-  hipError_t e = hipEventRecord(e0, c->stream);
-  if (e == hipSuccess) e = ppls_launch_gram(D, c->dtype, c->n_local, ld, p, nsplit, dpart, (int64_t)pp, gq, c->gram_variant, c->stream);
-  if (e == hipSuccess) e = hipEventRecord(e1, c->stream);
-  if (e == hipSuccess) e = ppls_launch_gram_finish(dpart, nsplit, (int64_t)pp, p, dG, c->stream);
-  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  double* dG = nullptr;
+  if ((rc = dalloc(c, &dG, pp))) return rc;
   float t = 0.f;
-  if (e == hipSuccess) e = hipEventElapsedTime(&t, e0, e1);
-  if (e == hipSuccess && G) e = hipMemcpy(G, dG, sizeof(double) * pp, hipMemcpyDeviceToHost);
-  (void)hipEventDestroy(e0);
-  (void)hipEventDestroy(e1);
-  dfree(dpart);
+  rc = gram_run(c, gram_shape(c, false, xory), c->n_local, nsplit > 0 ? nsplit : 0, dG, &t);
+  if (!rc && G && hipMemcpy(G, dG, sizeof(double) * pp, hipMemcpyDeviceToHost) != hipSuccess)
+    rc = fail(c, PPLS_E_HIP, "gram: copy-out failed");
   dfree(dG);
-  if (e != hipSuccess) return fail(c, PPLS_E_HIP, "gram: %s", hipGetErrorString(e));
-  if (ms) *ms = t;
-  return PPLS_OK;
+  if (!rc && ms) *ms = t;
+  return rc;
 }
 
 // scores.PPLS (EM_W_multi.R:411-420): T = X W, U = Y C (local rows, column-major n_local x k) in

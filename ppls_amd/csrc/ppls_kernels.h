@@ -146,19 +146,19 @@ hipError_t ppls_launch_philox(const uint32_t* ctr, int64_t count, uint64_t key, 
 hipError_t ppls_launch_to_rowmajor(const double* src, int64_t n, int p, int ld, double* dst,
                                    hipStream_t st);
 // variances.PPLS_simult (ppls_variances.hip)
-#define PPLS_GRAM_SKIP 1       // MFMA Gram: skip blocks in the padding and above the diagonal
-#define PPLS_GRAM_DYN 2        // MFMA Gram: persistent workgroups + per-XCD-group work queues
-#define PPLS_GRAM_DEFAULT 3
+// The MFMA Gram.  xreal, xcols, yreal: the joint columns that can be non-zero ([0, xreal) of X and
+// [xcols, xcols + yreal) of Y; for one block xcols = its ld, xreal = p, yreal = 0).
 int ppls_gram_tiles(int p);
 int ppls_gram_occupancy(int f32);
-int ppls_gram_splits(int p, int64_t n, int slots, int variant);
+// row splits for n rows (nsplit_req > 0: equal splits; 0: halving) and their bounds (nsplit + 1, nullable)
+int ppls_gram_plan(int p, int xreal, int xcols, int yreal, int64_t n, int wave_slots, int nsplit_req, int64_t* bounds);
+int64_t ppls_gram_part_doubles(int p, int nsplit);   // the per-item partials a launch writes
 int64_t ppls_gram_queue_ints(int p, int nsplit);
-// xreal, xcols, yreal: the joint columns that can be non-zero ([0, xreal) and [xcols, xcols + yreal))
-hipError_t ppls_gram_queue_prepare(int* queue, int p, int xreal, int xcols, int yreal, int nsplit, int variant,
-                                   hipStream_t st);
-hipError_t ppls_launch_gram(const void* X, int f32, int64_t n, int ld, int p, int nsplit, double* part,
-                            int64_t part_stride, int* queue, int variant, hipStream_t st);
-hipError_t ppls_launch_gram_finish(const double* part, int nsplit, int64_t part_stride, int p, double* G,
+hipError_t ppls_gram_queue_prepare(int* queue, int p, int xreal, int xcols, int yreal, int64_t n, int wave_slots,
+                                   int nsplit_req, hipStream_t st);
+hipError_t ppls_launch_gram(const void* X, int f32, int64_t n, int ld, int p, int nsplit, double* part, int* queue,
+                            hipStream_t st);
+hipError_t ppls_launch_gram_finish(const double* part, int nsplit, int p, int xreal, int xcols, int yreal, double* G,
                                    hipStream_t st);
 int ppls_xtmu_chunks(int64_t n, int ld, int f32);
 hipError_t ppls_launch_xtmu(const void* X, int f32, int64_t n, int ld, const double* mu, int a, int chunks,

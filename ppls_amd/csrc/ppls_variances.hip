@@ -22,10 +22,9 @@
 #include "ppls_kernels.h"
 #include "ppls_xprod.h"
 
-#define PPLS_GT 128   // output tile edge (4 waves x 64 x 64)
-#define PPLS_GK 16    // rows per LDS stage
-#define PPLS_GLD 144  // LDS row stride in doubles: 1152 B = 128 mod 256, so the 4 row groups of a
-                      // ds_read_b64 wave fall in disjoint bank halves per half-wave
+#define PPLS_GT 128   // output tile edge (4 quadrants of 64 x 64, one wave each)
+#define PPLS_GQ 64    // quadrant edge
+#define PPLS_GRING 3  // k-steps of MFMA operands in flight per wave (2-4 measured equal, 6 spills)
 
 namespace {
 
@@ -57,35 +56,13 @@ struct PplsGramCols {
   int p, xreal, xcols, yend;
 };
 
+__host__ __device__ inline bool ppls_gram_col_live(const PplsGramCols& g, int c) {
+  return c < g.p && (c < g.xreal || (c >= g.xcols && c < g.yend));
+}
+
 // Whether the 16 columns [a, a + 16) of the joint space hold any that can be non-zero.
 __host__ __device__ inline bool ppls_gram_live(const PplsGramCols& g, int a) {
   return a < g.p && (a < g.xreal || (a + 16 > g.xcols && a < g.yend));
-}
-
-// Active 16 x 16 MFMA blocks of wave (wi, wj) in the lower tile (I, J) of a p x p Gram: bit m * 4 + q
-// for the wave's block row m and block column q.  A block is skipped when its rows or columns are
-// all zero padding (past p, or between X's real columns and Y's), or -- in a diagonal tile -- when it
-// lies wholly above the diagonal (the finish kernel reads only the lower triangle).  C3 (p = 4000 ->
-// 32 blocks of 128): the last block row is 3/4 padding and the diagonal tiles 7/16 upper half, 7 %
-// of the executed flops; C5 also skips the 240 padding columns of X's 40,960-B rows (4 %).  Skipped
-// blocks inside p are written as the zeros they are (their accumulators are never touched).
-__host__ __device__ inline unsigned ppls_gram_active(int I, int J, int wi, int wj, const PplsGramCols& g) {
-  unsigned act = 0;
-  for (int m = 0; m < 4; ++m)
-    for (int q = 0; q < 4; ++q) {
-      const int i0 = I * PPLS_GT + wi * 64 + m * 16, j0 = J * PPLS_GT + wj * 64 + q * 16;
-      if (ppls_gram_live(g, i0) && ppls_gram_live(g, j0) && (I != J || wj * 4 + q <= wi * 4 + m))
-        act |= 1u << (m * 4 + q);
-    }
-  return act;
-}
-
-// Whether tile (I, J) has any skipped block (its items take the masked code path).
-__host__ __device__ inline bool ppls_gram_partial(int I, int J, const PplsGramCols& g) {
-  if (I == J) return true;
-  for (int a = 0; a < PPLS_GT; a += 16)
-    if (!ppls_gram_live(g, I * PPLS_GT + a) || !ppls_gram_live(g, J * PPLS_GT + a)) return true;
-  return false;
 }
 
 __host__ __device__ inline void ppls_gram_tile_of(int t, int* I, int* J) {
@@ -96,10 +73,27 @@ __host__ __device__ inline void ppls_gram_tile_of(int t, int* I, int* J) {
   *J = t - i * (i + 1) / 2;
 }
 
-// The persistent form's next work item: group g's queue first (its workgroups share an XCD, so
-// their items -- consecutive tiles of one row split -- share column panels in that L2), then the
-// other groups' (stealing: an XCD that runs ahead takes the cheap tail of a slower one).  One
-// global atomic per grab (items take milliseconds); -1 when every queue is empty.
+// Whether quadrant quad = 2 wi + wj (one wave's 64 x 64 output) of the lower tile (I, J) is computed:
+// not when it lies wholly above the diagonal (the finish reads only the lower triangle), nor when
+// its rows or its columns are all zero padding (past p, or between X's real columns and Y's).
+// C3 (p = 4000): the last tile row's lower 64 rows and the diagonal tiles' upper quadrants, 4.5 % of
+// the quadrants; C5 also the quadrants of X's 240 padding columns.
+__host__ __device__ inline bool ppls_gram_quad_live(const PplsGramCols& g, int I, int J, int quad) {
+  const int wi = quad >> 1, wj = quad & 1;
+  if (I == J && wi == 0 && wj == 1) return false;
+  bool ra = false, cb = false;
+  for (int a = 0; a < PPLS_GQ; a += 16) {
+    ra = ra || ppls_gram_live(g, I * PPLS_GT + wi * PPLS_GQ + a);
+    cb = cb || ppls_gram_live(g, J * PPLS_GT + wj * PPLS_GQ + a);
+  }
+  return ra && cb;
+}
+
+// The next work item of a wave: its group's queue first (blockIdx mod 8: workgroups that share an
+// XCD, whose items -- the tiles of one contiguous range, split by split -- share column panels in
+// that L2), then the other groups' (stealing: an XCD that runs ahead takes the tail of a slower
+// one).  One global atomic per item (items take tens of microseconds to milliseconds); -1 when every
+// queue is empty.
 __device__ inline int ppls_gram_next(unsigned* cnt, const int* qoff, const int* items, int g) {
   for (int k = 0; k < 8; ++k) {
     const int gg = (g + k) & 7;
@@ -110,176 +104,195 @@ __device__ inline int ppls_gram_next(unsigned* cnt, const int* qoff, const int* 
   return -1;
 }
 
-// X'X on MFMA.  Work item L = split s x lower tile t = (I, J), J <= I.  A wave owns a 64 x 64
-// sub-tile = 4 x 4 MFMA blocks (64 fp64 accumulators per lane); per 4-row k-step it reads 4 A and 4
-// B operands from LDS (lane l: row l >> 4 of the step, column l & 15 of its block) -- both straight
-// from the row-major panels, no transpose, since A[i][k] = X[k][i] and B[k][j] = X[k][j].  The next
-// stage's global loads are in flight during the MFMAs; one barrier per 16-row stage.  Output:
-// part[s][i p + j] for the tile's (i, j), i in block I >= block J (row-major of the lower blocks;
-// coalesced over j).
-//
-// Scheduling (template DYN): the static form runs one work item per workgroup, blockIdx remapped so
-// that each XCD -- blockIdx mod 8 -- gets a contiguous range of items (tiles that share column panels
-// share an L2).  Its items all take the same time, so the last round of them leaves the slots that
-// have none idle (C3: 6,336 items on 512 slots, the 13th round 3/8 full: ~5 % of the kernel).  The
-// persistent form (DYN) launches one workgroup per slot; each takes items from the queue of its group
-// (blockIdx mod 8: the same contiguous ranges), costliest first -- tiles with skipped blocks (SKIP)
-// are cheaper and come last, so the final items of every queue are short -- and steals from the
-// other groups' queues once its own is empty.  Each item's sums depend only on the item, so the
-// result is the same bit for bit whichever workgroup runs it.
-//
-// The column space is that of the joint matrix [X | Y] (ppls_xprod.hip's cross-product form of the
-// EM iteration): column c is X[:, c] for c < xcols and Y[:, c - xcols] for c - xcols < ycols (zero
-// beyond); xcols and ycols are multiples of the 16-B vector, so no load straddles the seam.  The
-// Gram of X alone is xcols = ld, ycols = 0, p the output edge.
-template <typename T, bool SKIP, bool MASKED>
-__device__ __forceinline__ void ppls_gram_item(const T* __restrict__ X, int ldx, int xcols, const T* __restrict__ Y,
-                                               int ldy, int ycols, int64_t n, int p, int ntiles, int nsplit,
-                                               int64_t L, double* __restrict__ part, int64_t part_stride,
-                                               const PplsGramCols gc, double (*sm)[2][PPLS_GK][PPLS_GLD]) {
+// A lane's MFMA operands of one 4-row k-step, per side (A: the quadrant's 64 output rows, B: its 64
+// output columns), loaded straight from the row-major data: lane l reads row k0 + (l >> 4) and, for
+// fp64, the column pairs 2 i, 2 i + 1 and 32 + 2 i, 33 + 2 i of the side's 64 (i = l & 15: each
+// 16-lane group reads 256 contiguous bytes per load); for fp32 the quad 4 i .. 4 i + 3 (one 16-B
+// load).  MFMA block m (16 output rows or columns) then holds the columns col(m, i).
+template <typename T>
+struct PplsGramOps;
+template <>
+struct PplsGramOps<double> {
+  static constexpr int NL = 2;   // 16-B loads per side per k-step
+  double2 v[2];
+  __device__ __forceinline__ void load(const double* const* ptr) {
+    v[0] = *(const double2*)ptr[0];
+    v[1] = *(const double2*)ptr[1];
+  }
+  __device__ __forceinline__ double op(int m) const { return m == 0 ? v[0].x : m == 1 ? v[0].y : m == 2 ? v[1].x : v[1].y; }
+  __host__ __device__ static int lcol(int l, int i) { return 32 * l + 2 * i; }
+  __host__ __device__ static int col(int m, int i) { return 32 * (m >> 1) + 2 * i + (m & 1); }
+};
+template <>
+struct PplsGramOps<float> {
+  static constexpr int NL = 1;
+  float4 v[1];
+  __device__ __forceinline__ void load(const float* const* ptr) { v[0] = *(const float4*)ptr[0]; }
+  __device__ __forceinline__ double op(int m) const {
+    return (double)(m == 0 ? v[0].x : m == 1 ? v[0].y : m == 2 ? v[0].z : v[0].w);
+  }
+  __host__ __device__ static int lcol(int, int i) { return 4 * i; }
+  __host__ __device__ static int col(int m, int i) { return 4 * i + m; }
+};
+
+// One work item = split s x lower tile t = (I, J) x quadrant, on ONE wave: its 64 x 64 output as 4 x 4
+// v_mfma_f64_16x16x4_f64 blocks (64 fp64 accumulators per lane), every MFMA operand loaded by the
+// lane that feeds it straight from global memory into a ring PPLS_GRING k-steps deep -- no LDS, no
+// workgroup barrier: waves never wait for each other.  The round-4 form staged 16-row panels in LDS
+// behind one barrier per stage; at C3 it took 271.6 ms against 240.8 ms for this one, bit for bit the
+// same sums (tools/gram_lab.hip, profiles/r5_gram_lab_*.txt).  Columns past p read column 0: that
+// garbage only meets its own output rows / columns, which the finish never reads, so the steady
+// state needs no masks; rows past the split's end are zeros (the one partial k-step).
+// Output: part[item][a][b], a quadrant-local row, b column (64 x 64 doubles per item).
+template <typename T>
+__device__ __forceinline__ void ppls_gram_wave_item(const T* __restrict__ X, int ldx, int xcols, const T* __restrict__ Y,
+                                                    int ldy, int ycols, int p, int ntiles, int it,
+                                                    const int64_t* __restrict__ bounds, double* __restrict__ part) {
   typedef double d4 __attribute__((ext_vector_type(4)));
-  constexpr int EV = 16 / sizeof(T);              // elements per 16-B load
-  constexpr int VPR = PPLS_GT / EV;               // 16-B vectors per panel row
-  constexpr int NV = PPLS_GK * VPR / 256;         // per thread per panel (fp64: 4, fp32: 2)
-  const int s = (int)(L / ntiles), t = (int)(L - (int64_t)s * ntiles);
+  typedef PplsGramOps<T> Op;
+  constexpr int D = PPLS_GRING;
+  const int quad = it & 3, st = it >> 2;
+  const int s = st / ntiles, t = st - s * ntiles;
   int I, J;
   ppls_gram_tile_of(t, &I, &J);
-  const int64_t r0 = n * s / nsplit, r1 = n * (s + 1) / nsplit;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wi = wave >> 1, wj = wave & 1;
-  const int colA = I * PPLS_GT, colB = J * PPLS_GT;
-  // wave-uniform (SGPR) block mask; MASKED code paths test it per MFMA, the full path does not
-  const unsigned act = SKIP ? ppls_gram_active(I, J, wi, wj, gc) : 0xffffu;
-
-  GVec<T> ra[NV], rb[NV];
-  auto load = [&](int64_t k0) {
+  const int64_t r0 = bounds[s], r1 = bounds[s + 1];
+  const int lane = threadIdx.x & 63, kr = lane >> 4, li = lane & 15;
+  const T* pa[Op::NL];
+  const T* pb[Op::NL];
+  int64_t sa[Op::NL], sb[Op::NL];
+  auto base = [&](int c, const T** pp, int64_t* step) {
+    const T* b0;
+    int64_t ld;
+    if (c < xcols && c < p) { b0 = X + c; ld = ldx; }
+    else if (c >= xcols && c - xcols < ycols && c < p) { b0 = Y + (c - xcols); ld = ldy; }
+    else { b0 = X; ld = ldx; }   // padding past p
+    *pp = b0 + (r0 + kr) * ld;
+    *step = 4 * ld;
+  };
 #pragma unroll
-    for (int v = 0; v < NV; ++v) {
-      const int c = tid + 256 * v, row = c / VPR, cv = c - row * VPR;
-      const int64_t gr = k0 + row;
-      const int ca = colA + cv * EV, cb = colB + cv * EV;
-      if (gr < r1 && ca < xcols) ra[v].load(X + gr * ldx + ca);
-      else if (gr < r1 && ca - xcols < ycols) ra[v].load(Y + gr * ldy + (ca - xcols));
-      else ra[v].zero();
-      if (gr < r1 && cb < xcols) rb[v].load(X + gr * ldx + cb);
-      else if (gr < r1 && cb - xcols < ycols) rb[v].load(Y + gr * ldy + (cb - xcols));
-      else rb[v].zero();
+  for (int l = 0; l < Op::NL; ++l) {
+    base(I * PPLS_GT + (quad >> 1) * PPLS_GQ + Op::lcol(l, li), &pa[l], &sa[l]);
+    base(J * PPLS_GT + (quad & 1) * PPLS_GQ + Op::lcol(l, li), &pb[l], &sb[l]);
+  }
+  Op ra[D], rb[D];
+  auto ld_step = [&](int d) {
+    ra[d].load(pa);
+    rb[d].load(pb);
+#pragma unroll
+    for (int l = 0; l < Op::NL; ++l) {
+      pa[l] += sa[l];
+      pb[l] += sb[l];
     }
   };
-  auto store = [&](int buf) {
-#pragma unroll
-    for (int v = 0; v < NV; ++v) {
-      const int c = tid + 256 * v, row = c / VPR, cv = c - row * VPR;
-      ra[v].store(&sm[buf][0][row][cv * EV]);
-      rb[v].store(&sm[buf][1][row][cv * EV]);
-    }
-  };
-
   d4 acc[4][4];
 #pragma unroll
   for (int m = 0; m < 4; ++m)
 #pragma unroll
     for (int q = 0; q < 4; ++q) acc[m][q] = d4{0.0, 0.0, 0.0, 0.0};
-  const int64_t nsteps = (r1 - r0 + PPLS_GK - 1) / PPLS_GK;
-  if (nsteps > 0) {
-    load(r0);
-    store(0);
-  }
-  __syncthreads();
-  const int ko = lane >> 4, cl = lane & 15;
-  for (int64_t st = 0; st < nsteps; ++st) {
-    const int buf = (int)(st & 1);
-    if (st + 1 < nsteps) load(r0 + (st + 1) * PPLS_GK);
-    if (!MASKED || act) {
+  auto mma = [&](const Op& A, const Op& B) {
+    double a[4], b[4];
 #pragma unroll
-      for (int kk = 0; kk < PPLS_GK / 4; ++kk) {
-        const double* ar = &sm[buf][0][kk * 4 + ko][wi * 64 + cl];
-        const double* br = &sm[buf][1][kk * 4 + ko][wj * 64 + cl];
-        double a[4], b[4];
+    for (int m = 0; m < 4; ++m) a[m] = A.op(m);
 #pragma unroll
-        for (int m = 0; m < 4; ++m) a[m] = ar[m * 16];
+    for (int q = 0; q < 4; ++q) b[q] = B.op(q);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) b[q] = br[q * 16];
+    for (int m = 0; m < 4; ++m)
 #pragma unroll
-        for (int m = 0; m < 4; ++m)
+      for (int q = 0; q < 4; ++q) acc[m][q] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[m], b[q], acc[m][q], 0, 0, 0);
+  };
+  const int64_t nfull = (r1 - r0) / 4;   // whole 4-row k-steps
+  int64_t kk = 0;
+  if (nfull >= 2 * D) {
 #pragma unroll
-          for (int q = 0; q < 4; ++q)
-            if (!MASKED || ((act >> (m * 4 + q)) & 1u))
-              acc[m][q] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[m], b[q], acc[m][q], 0, 0, 0);
+    for (int d = 0; d < D; ++d) {
+      ld_step(d);
+      __builtin_amdgcn_sched_barrier(0);   // the ring order of the loop (its vmcnt waits rely on it)
+    }
+    // steady state: every prefetched k-step lies inside the split, no branch between the loads;
+    // the oldest step is consumed next, so vmcnt(NL' (D - 1)) suffices
+    for (; kk + 2 * D <= nfull; kk += D) {
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        mma(ra[d], rb[d]);
+        ld_step(d);
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
-    if (st + 1 < nsteps) store(buf ^ 1);
-    __syncthreads();
+#pragma unroll
+    for (int d = 0; d < D; ++d) mma(ra[d], rb[d]);
+    kk += D;
   }
-  double* out = part + (int64_t)s * part_stride;
+  for (; kk < nfull; ++kk) {   // the last < D whole k-steps
+    ld_step(0);
+    mma(ra[0], rb[0]);
+  }
+  if (r1 - r0 > 4 * nfull) {   // a partial last k-step: rows past r1 are zeros
+    Op A, B;
+#pragma unroll
+    for (int l = 0; l < Op::NL; ++l) {
+      A.v[l] = {};
+      B.v[l] = {};
+    }
+    if (r0 + 4 * nfull + kr < r1) {
+      A.load(pa);
+      B.load(pb);
+    }
+    mma(A, B);
+  }
+  double* out = part + (int64_t)it * (PPLS_GQ * PPLS_GQ);
 #pragma unroll
   for (int m = 0; m < 4; ++m)
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const int j = colB + wj * 64 + q * 16 + cl;
+      const int b = Op::col(q, li);
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {   // f64 MFMA D map: col = lane & 15, row = (lane >> 4) + 4 g
-        const int i = colA + wi * 64 + m * 16 + ko + 4 * g;
-        if (i < p && j < p) out[(int64_t)i * p + j] = acc[m][q][g];
-      }
+      for (int g = 0; g < 4; ++g)   // f64 MFMA D map: row (lane >> 4) + 4 g, column lane & 15
+        out[Op::col(m, kr + 4 * g) * PPLS_GQ + b] = acc[m][q][g];
     }
 }
 
-template <typename T, bool DYN, bool SKIP>
+// Persistent: one workgroup per resident slot (4 independent waves); every wave takes work items
+// from the queues (ppls_gram_next) until they are empty.  Each item's sums depend only on the item,
+// so the result is the same bit for bit whichever wave runs it.
+template <typename T>
 __global__ __launch_bounds__(256, 2) void ppls_gram_mfma_kernel(const T* __restrict__ X, int ldx, int xcols,
-                                                                 const T* __restrict__ Y, int ldy, int ycols,
-                                                                 int64_t n, int p, int ntiles, int nsplit,
-                                                                 int64_t work, double* __restrict__ part,
-                                                                 int64_t part_stride, int* __restrict__ queue,
-                                                                 PplsGramCols gc) {
-  __shared__ __attribute__((aligned(16))) double sm[2][2][PPLS_GK][PPLS_GLD];
-  if constexpr (!DYN) {
-    const int64_t per = gridDim.x >> 3;
-    const int64_t L = (int64_t)(blockIdx.x & 7) * per + (blockIdx.x >> 3);
-    if (L >= work) return;
-    if (SKIP) {
-      int I, J;
-      ppls_gram_tile_of((int)(L % ntiles), &I, &J);
-      if (ppls_gram_partial(I, J, gc)) {   // a tile with skipped blocks: the masked code path
-        ppls_gram_item<T, true, true>(X, ldx, xcols, Y, ldy, ycols, n, p, ntiles, nsplit, L, part, part_stride, gc, sm);
-        return;
-      }
-    }
-    ppls_gram_item<T, false, false>(X, ldx, xcols, Y, ldy, ycols, n, p, ntiles, nsplit, L, part, part_stride, gc, sm);
-  } else {
-    // queue = [qoff (9) | counters (8, zeroed before the launch) | items (work)]
-    const int* qoff = queue;
-    unsigned* cnt = (unsigned*)(queue + 9);
-    const int* items = queue + 17;
-    __shared__ int s_next;
-    const int g = blockIdx.x & 7;
-    for (;;) {
-      if (threadIdx.x == 0) s_next = ppls_gram_next(cnt, qoff, items, g);
-      __syncthreads();
-      const int L = s_next;
-      __syncthreads();   // every thread has read s_next before thread 0 writes the next one
-      if (L < 0) return;
-      int I, J;
-      ppls_gram_tile_of(L % ntiles, &I, &J);
-      if (SKIP && ppls_gram_partial(I, J, gc))
-        ppls_gram_item<T, true, true>(X, ldx, xcols, Y, ldy, ycols, n, p, ntiles, nsplit, L, part, part_stride, gc, sm);
-      else
-        ppls_gram_item<T, false, false>(X, ldx, xcols, Y, ldy, ycols, n, p, ntiles, nsplit, L, part, part_stride, gc, sm);
-    }
+                                                                 const T* __restrict__ Y, int ldy, int ycols, int p,
+                                                                 int ntiles, int nsplit, int* __restrict__ queue,
+                                                                 double* __restrict__ part) {
+  // queue = [qoff (9) | counters (8, zeroed before the launch) | pad | row bounds (nsplit + 1 int64) | items]
+  const int* qoff = queue;
+  unsigned* cnt = (unsigned*)(queue + 9);
+  const int64_t* bounds = (const int64_t*)(queue + 18);
+  const int* items = queue + 18 + 2 * (nsplit + 1);
+  const int g = blockIdx.x & 7, lane = threadIdx.x & 63;
+  for (;;) {
+    int it = 0;
+    if (lane == 0) it = ppls_gram_next(cnt, qoff, items, g);
+    it = __builtin_amdgcn_readfirstlane(it);
+    if (it < 0) return;
+    ppls_gram_wave_item<T>(X, ldx, xcols, Y, ldy, ycols, p, ntiles, it, bounds, part);
   }
 }
 
-// G (p x p column-major, full) = sum over splits of the lower-block entries: element (a, b) is read
-// at (max, min), which lies in a computed tile and makes G exactly symmetric.
-__global__ void ppls_gram_finish_kernel(const double* __restrict__ part, int nsplit, int64_t part_stride, int p,
+// G (p x p column-major, full) = sum over the splits' quadrant partials: element (a, b) is read at
+// (max, min), which lies in a computed quadrant, so G is exactly symmetric; elements in a zero
+// padding column (never computed when their whole quadrant is padding) are 0.
+__global__ void ppls_gram_finish_kernel(const double* __restrict__ part, int nsplit, int ntiles, PplsGramCols gc,
                                         double* __restrict__ G) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int p = gc.p;
   const int64_t pp = (int64_t)p * p;
   if (e >= pp) return;
   const int b = (int)(e / p), a = (int)(e - (int64_t)b * p);
   const int hi = a > b ? a : b, lo = a > b ? b : a;
   double v = 0.0;
-  for (int s = 0; s < nsplit; ++s) v += part[(int64_t)s * part_stride + (int64_t)hi * p + lo];
+  if (ppls_gram_col_live(gc, hi) && ppls_gram_col_live(gc, lo)) {
+    const int I = hi >> 7, J = lo >> 7, t = I * (I + 1) / 2 + J;
+    const int quad = (((hi & 127) >> 6) << 1) | ((lo & 127) >> 6);
+    const int64_t off = ((int64_t)t * 4 + quad) * (PPLS_GQ * PPLS_GQ) + (hi & 63) * PPLS_GQ + (lo & 63);
+    const int64_t stride = (int64_t)ntiles * 4 * (PPLS_GQ * PPLS_GQ);
+    for (int s = 0; s < nsplit; ++s) v += part[(int64_t)s * stride + off];
+  }
   G[e] = v;
 }
 
@@ -396,125 +409,117 @@ int ppls_gram_tiles(int p) {
 
 int ppls_gram_occupancy(int f32) {
   int occ = 0;
-  hipError_t e = f32 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, ppls_gram_mfma_kernel<float, true, true>, 256, 0)
-                     : hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, ppls_gram_mfma_kernel<double, true, true>, 256, 0);
+  hipError_t e = f32 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, ppls_gram_mfma_kernel<float>, 256, 0)
+                     : hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, ppls_gram_mfma_kernel<double>, 256, 0);
   return e == hipSuccess && occ > 0 ? occ : 1;
 }
 
-// MFMA blocks an item of tile t executes (of 64): the persistent queue's cost order.
-static int ppls_gram_cost(int t, const PplsGramCols& gc, int variant) {
-  if (!(variant & PPLS_GRAM_SKIP)) return 64;
-  int I, J;
-  ppls_gram_tile_of(t, &I, &J);
-  int c = 0;
-  for (int w = 0; w < 4; ++w) c += __builtin_popcount(ppls_gram_active(I, J, w >> 1, w & 1, gc));
-  return c;
+static int ppls_gram_live_quads(const PplsGramCols& gc) {
+  const int ntiles = ppls_gram_tiles(gc.p);
+  int w = 0;
+  for (int t = 0; t < ntiles; ++t) {
+    int I, J;
+    ppls_gram_tile_of(t, &I, &J);
+    for (int qd = 0; qd < 4; ++qd) w += ppls_gram_quad_live(gc, I, J, qd) ? 1 : 0;
+  }
+  return w;
 }
 
-// Row splits of a p x p Gram over n rows (partials: nsplit x 8 p^2 bytes, kept under 4 GB).
-// Static form: enough items to fill whole rounds of the slots (>= 95 % of the last round).  Persistent
-// form: about 12 items per slot, so the queues end on short items.
-int ppls_gram_splits(int p, int64_t n, int slots, int variant) {
-  const int ntiles = ppls_gram_tiles(p);
-  const double pp = (double)p * p;
-  auto allowed = [&](int sp) { return sp == 1 || ((int64_t)sp * 512 <= n && (double)sp * pp * 8.0 <= 4.0e9); };
-  if (variant & PPLS_GRAM_DYN) {
-    int sp = (int)((12LL * slots + ntiles - 1) / ntiles);
-    sp = sp < 1 ? 1 : (sp > 32 ? 32 : sp);
-    while (sp > 1 && !allowed(sp)) --sp;
-    return sp;
+// The row splits of a Gram over n rows: nsplit_req > 0 equal splits; 0 (auto) halving splits n / 2,
+// n / 4, ..., n / 2^k, n / 2^k.  A wave's items are taken dynamically, so the run ends on the smallest
+// items: k is the first with one such item at most ~1 % of a wave slot's share of the work (C3: 8
+// splits, the last 7,812 rows), within 4 GB of partials (32 KB per live quadrant and split) and >= 256
+// rows per split.  bounds: nsplit + 1 row boundaries.
+int ppls_gram_plan(int p, int xreal, int xcols, int yreal, int64_t n, int wave_slots, int nsplit_req, int64_t* bounds) {
+  const PplsGramCols gc{p, xreal, xcols, xcols + yreal};
+  const double w1 = (double)ppls_gram_live_quads(gc);
+  if (nsplit_req > 0) {
+    if (bounds)
+      for (int s = 0; s <= nsplit_req; ++s) bounds[s] = n * s / nsplit_req;
+    return nsplit_req;
   }
-  int nsplit = 1;
-  double best = -1.0;
-  for (int sp = 1; sp <= 32; ++sp) {
-    if (!allowed(sp)) break;
-    const int64_t w = (int64_t)ntiles * sp;
-    const double eff = (double)w / (double)(((w + slots - 1) / slots) * slots);
-    if (eff > best + 1e-9) { best = eff; nsplit = sp; }
-    if (eff >= 0.95) break;
+  int k = 0;
+  while (k < 16 && (double)wave_slots / (w1 * (double)(1LL << k)) > 0.01 && (n >> (k + 1)) >= 256 &&
+         (double)(k + 2) * w1 * PPLS_GQ * PPLS_GQ * 8.0 <= 4.0e9)
+    ++k;
+  const int nsplit = k + 1;
+  if (bounds) {
+    for (int j = 0; j <= k; ++j) bounds[j] = k == 0 ? 0 : n - (n >> j);
+    bounds[nsplit] = n;
   }
   return nsplit;
 }
 
-int64_t ppls_gram_queue_ints(int p, int nsplit) { return 17 + (int64_t)ppls_gram_tiles(p) * nsplit; }
+int64_t ppls_gram_part_doubles(int p, int nsplit) {
+  return (int64_t)nsplit * ppls_gram_tiles(p) * 4 * PPLS_GQ * PPLS_GQ;
+}
 
-// The persistent form's queues (device ints, ppls_gram_queue_ints): group g gets the contiguous item
-// range [g W / 8, (g + 1) W / 8) of the split-major order (its XCD's tiles share column panels),
-// sorted costliest first (stable: ties keep the split-major order).  Synchronous (host staging);
-// the launch resets the counters, so one prepared queue serves any number of launches.
-hipError_t ppls_gram_queue_prepare(int* queue, int p, int xreal, int xcols, int yreal, int nsplit, int variant,
-                                   hipStream_t st) {
+int64_t ppls_gram_queue_ints(int p, int nsplit) { return 18 + 2 * (int64_t)(nsplit + 1) + (int64_t)ppls_gram_tiles(p) * 4 * nsplit; }
+
+// The queues (device ints, ppls_gram_queue_ints): group g (blockIdx mod 8) gets the live quadrants
+// of the tiles [g T / 8, (g + 1) T / 8) in every split, split by split (the large splits first, the
+// run ends on the small ones); the row bounds ride along.  Synchronous (host staging); the launch
+// resets the counters, so one prepared queue serves any number of launches of that shape.
+hipError_t ppls_gram_queue_prepare(int* queue, int p, int xreal, int xcols, int yreal, int64_t n, int wave_slots,
+                                   int nsplit_req, hipStream_t st) {
   const PplsGramCols gc{p, xreal, xcols, xcols + yreal};
+  const int nsplit = ppls_gram_plan(p, xreal, xcols, yreal, n, wave_slots, nsplit_req, nullptr);
   const int ntiles = ppls_gram_tiles(p);
-  const int64_t work = (int64_t)ntiles * nsplit;
   std::vector<int> h((size_t)ppls_gram_queue_ints(p, nsplit), 0);
-  std::vector<int> tc((size_t)ntiles);
-  for (int t = 0; t < ntiles; ++t) tc[(size_t)t] = ppls_gram_cost(t, gc, variant);
-  int* items = h.data() + 17;
+  ppls_gram_plan(p, xreal, xcols, yreal, n, wave_slots, nsplit_req, (int64_t*)(h.data() + 18));
+  int* items = h.data() + 18 + 2 * (nsplit + 1);
+  int w = 0;
   for (int g = 0; g < 8; ++g) {
-    const int64_t a = work * g / 8, b = work * (g + 1) / 8;
-    h[(size_t)g] = (int)a;
-    for (int64_t L = a; L < b; ++L) items[L] = (int)L;
-    std::stable_sort(items + a, items + b,
-                     [&](int x, int y) { return tc[(size_t)(x % ntiles)] > tc[(size_t)(y % ntiles)]; });
+    h[(size_t)g] = w;
+    const int t0 = ntiles * g / 8, t1 = ntiles * (g + 1) / 8;
+    for (int s = 0; s < nsplit; ++s)
+      for (int t = t0; t < t1; ++t) {
+        int I, J;
+        ppls_gram_tile_of(t, &I, &J);
+        for (int qd = 0; qd < 4; ++qd)
+          if (ppls_gram_quad_live(gc, I, J, qd)) items[w++] = ((s * ntiles + t) << 2) | qd;
+      }
   }
-  h[8] = (int)work;
+  h[8] = w;
   hipError_t e = hipMemcpyAsync(queue, h.data(), sizeof(int) * h.size(), hipMemcpyHostToDevice, st);
   if (e == hipSuccess) e = hipStreamSynchronize(st);
   return e;
 }
 
 hipError_t ppls_launch_gram_joint(const void* X, int ldx, int xcols, int xreal, const void* Y, int ldy, int ycols,
-                                  int yreal, int f32, int64_t n, int p, int nsplit, double* part, int64_t part_stride,
-                                  int* queue, int variant, hipStream_t st) {
-  if (n <= 0 || p <= 0 || nsplit < 1 || xcols + ycols < 1 || xreal > xcols || yreal > ycols) return hipErrorInvalidValue;
-  const PplsGramCols gc{p, xreal, xcols, xcols + yreal};
+                                  int yreal, int f32, int64_t n, int p, int nsplit, double* part, int* queue,
+                                  hipStream_t st) {
+  if (n <= 0 || p <= 0 || nsplit < 1 || !queue || xcols + ycols < 1 || xreal > xcols || yreal > ycols)
+    return hipErrorInvalidValue;
   const int ev = f32 ? 4 : 2;
   if (xcols % ev || ycols % ev) return hipErrorInvalidValue;
   const int ntiles = ppls_gram_tiles(p);
-  const int64_t work = (int64_t)ntiles * nsplit;
-  const bool dyn = (variant & PPLS_GRAM_DYN) != 0, skip = (variant & PPLS_GRAM_SKIP) != 0;
-  if (work > 0x7fffffff - 32) return hipErrorInvalidValue;
-  int64_t grid;
-  if (dyn) {
-    if (!queue) return hipErrorInvalidValue;
-    int dev = 0, cus = 256;
-    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    grid = (int64_t)cus * ppls_gram_occupancy(f32);
-    grid = (grid + 7) / 8 * 8;
-    hipError_t e = hipMemsetAsync(queue + 9, 0, 8 * sizeof(int), st);   // the queue counters
-    if (e != hipSuccess) return e;
-  } else {
-    grid = (work + 7) / 8 * 8;   // a multiple of 8: the XCD remap needs whole rounds
-  }
-#define PPLS_GRAM_LAUNCH(TT, D, S)                                                                           \
-  hipLaunchKernelGGL((ppls_gram_mfma_kernel<TT, D, S>), dim3((unsigned)grid), dim3(256), 0, st, (const TT*)X, ldx, \
-                     xcols, (const TT*)Y, ldy, ycols, n, p, ntiles, nsplit, work, part, part_stride, queue, gc)
-  if (f32) {
-    if (dyn && skip) PPLS_GRAM_LAUNCH(float, true, true);
-    else if (dyn) PPLS_GRAM_LAUNCH(float, true, false);
-    else if (skip) PPLS_GRAM_LAUNCH(float, false, true);
-    else PPLS_GRAM_LAUNCH(float, false, false);
-  } else {
-    if (dyn && skip) PPLS_GRAM_LAUNCH(double, true, true);
-    else if (dyn) PPLS_GRAM_LAUNCH(double, true, false);
-    else if (skip) PPLS_GRAM_LAUNCH(double, false, true);
-    else PPLS_GRAM_LAUNCH(double, false, false);
-  }
-#undef PPLS_GRAM_LAUNCH
+  if ((int64_t)ntiles * 4 * nsplit > 0x7fffffff) return hipErrorInvalidValue;
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  const int grid = (cus * ppls_gram_occupancy(f32) + 7) / 8 * 8;
+  hipError_t e = hipMemsetAsync(queue + 9, 0, 8 * sizeof(int), st);   // the queue counters
+  if (e != hipSuccess) return e;
+  if (f32)
+    hipLaunchKernelGGL(ppls_gram_mfma_kernel<float>, dim3((unsigned)grid), dim3(256), 0, st, (const float*)X, ldx, xcols,
+                       (const float*)Y, ldy, ycols, p, ntiles, nsplit, queue, part);
+  else
+    hipLaunchKernelGGL(ppls_gram_mfma_kernel<double>, dim3((unsigned)grid), dim3(256), 0, st, (const double*)X, ldx, xcols,
+                       (const double*)Y, ldy, ycols, p, ntiles, nsplit, queue, part);
   return hipGetLastError();
 }
 
-hipError_t ppls_launch_gram(const void* X, int f32, int64_t n, int ld, int p, int nsplit, double* part,
-                            int64_t part_stride, int* queue, int variant, hipStream_t st) {
-  return ppls_launch_gram_joint(X, ld, ld, p, nullptr, 0, 0, 0, f32, n, p, nsplit, part, part_stride, queue, variant, st);
+hipError_t ppls_launch_gram(const void* X, int f32, int64_t n, int ld, int p, int nsplit, double* part, int* queue,
+                            hipStream_t st) {
+  return ppls_launch_gram_joint(X, ld, ld, p, nullptr, 0, 0, 0, f32, n, p, nsplit, part, queue, st);
 }
 
-hipError_t ppls_launch_gram_finish(const double* part, int nsplit, int64_t part_stride, int p, double* G,
+hipError_t ppls_launch_gram_finish(const double* part, int nsplit, int p, int xreal, int xcols, int yreal, double* G,
                                    hipStream_t st) {
   const int64_t pp = (int64_t)p * p;
+  const PplsGramCols gc{p, xreal, xcols, xcols + yreal};
   hipLaunchKernelGGL(ppls_gram_finish_kernel, dim3((unsigned)((pp + 255) / 256)), dim3(256), 0, st, part, nsplit,
-                     part_stride, p, G);
+                     ppls_gram_tiles(p), gc, G);
   return hipGetLastError();
 }
 

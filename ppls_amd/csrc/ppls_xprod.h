@@ -16,15 +16,14 @@
 
 extern "C" {
 // Gram of the joint column space [X | Y] (xcols columns of X at stride ldx, then ycols of Y at
-// stride ldy; both multiples of the 16-B vector): lower 128 x 128 tiles per row split into part
-// (p x p row-major per split, p = output edge); ppls_launch_gram_finish mirrors them.  variant:
-// PPLS_GRAM_SKIP (no MFMAs on padding or above the diagonal) | PPLS_GRAM_DYN (persistent workgroups
-// taking items from per-XCD-group queues; `queue` = ppls_gram_queue_ints(p, nsplit) device ints
-// filled once by ppls_gram_queue_prepare).
-// xreal / yreal: X's and Y's real columns (the rest of xcols / ycols is zero padding, skipped).
+// stride ldy; both multiples of the 16-B vector; xreal / yreal of them real, the rest zero padding):
+// every live 64 x 64 quadrant of the lower 128 x 128 tiles, per row split, into part
+// (ppls_gram_part_doubles), by persistent waves taking items from `queue` (ppls_gram_queue_ints(p,
+// nsplit) device ints, filled once by ppls_gram_queue_prepare); ppls_launch_gram_finish sums and
+// mirrors them.
 hipError_t ppls_launch_gram_joint(const void* X, int ldx, int xcols, int xreal, const void* Y, int ldy, int ycols,
-                                  int yreal, int f32, int64_t n, int p, int nsplit, double* part, int64_t part_stride,
-                                  int* queue, int variant, hipStream_t st);
+                                  int yreal, int f32, int64_t n, int p, int nsplit, double* part, int* queue,
+                                  hipStream_t st);
 
 // Rows of S per wave of the tile kernel (rw_opt 1, 2, 4 or 8 (r <= 8) forces it; 0 = auto).
 int ppls_xprod_tile_rows(int P, int r, int rw_opt, int num_cus);

@@ -1,6 +1,7 @@
 """MFMA Gram timings of this tree's library: the joint S = [X Y]'[X Y] (xprod_prepare) at C3 and C5
-and X'X alone (ppls_gram) at C3, best of reps, with the fp64 TF/s of the executed tiles -- for
-same-box A/B of Gram kernel variants (tools/gram_ab.sh).
+and X'X alone (ppls_gram) at C3, best of reps, with the fp64 TF/s of the useful flops n P (P + 1)
+(lower triangle incl. the diagonal, real columns) -- for same-box A/B of Gram kernel variants
+(tools/gram_ab.sh).
 
     python tools/gram_probe.py [reps=3]
 """
@@ -27,12 +28,11 @@ for name in ("c3", "c5"):
             ctx.xprod_release()
             ms, _ = ctx.xprod_prepare()
             ts.append(ms)
-        info = ctx.xprod_info(r)
         best = min(ts[1:])
-        print(f"{name} S: {best:8.2f} ms  {info['gram_flops'] / best / 1e9:6.2f} TF/s  (all {[round(t, 2) for t in ts]})",
+        useful = float(n) * (p + q) * (p + q + 1.0)   # lower triangle incl. the diagonal, real columns
+        print(f"{name} S: {best:8.2f} ms  useful {useful / best / 1e9:6.2f} TF/s  (all {[round(t, 2) for t in ts]})",
               flush=True)
         if name == "c3":
             g = [ctx.gram(0, 0, want=False)[1] for _ in range(reps + 1)]
-            nb = (p + 127) // 128
-            fl = 2.0 * n * nb * (nb + 1) / 2 * 128 * 128
-            print(f"{name} X'X: {min(g[1:]):8.2f} ms  {fl / min(g[1:]) / 1e9:6.2f} TF/s", flush=True)
+            fl = float(n) * p * (p + 1.0)
+            print(f"{name} X'X: {min(g[1:]):8.2f} ms  useful {fl / min(g[1:]) / 1e9:6.2f} TF/s", flush=True)
