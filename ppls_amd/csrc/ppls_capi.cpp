@@ -126,6 +126,8 @@ struct ppls_ctx {
   bool xp_pending_gram = false;   // the last statistics step left the Gram B'M to the next finalize
   int xprod_fuse = 1;       // option "xprod_fuse": the finalize forms the Gram (r <= 8, P <= 6144)
   bool xp_explicit = false; // S was formed by ppls_xprod_prepare: kept until ppls_xprod_release / new data
+  int meta_device = 1;      // option "meta_device": meta_PPLSi's loop on the device (1) or per population
+                            // from the host (0; also where the split sweep does not apply)
   int vorth = 8;            // option "vorth": the finalize re-orthonormalises its carried Jacobi V every
                             // vorth-th iteration (1 = every iteration)
   double* xp_S = nullptr;
@@ -1213,6 +1215,8 @@ int ppls_set_option(ppls_ctx* c, const char* key, int64_t value) {
       HIPCHK(c, hipStreamSynchronize(c->stream));
       xprod_free(c);
     }
+  } else if (!strcmp(key, "meta_device")) {
+    c->meta_device = value ? 1 : 0;
   } else if (!strcmp(key, "vorth")) {
     if (value < 1 || value > 255) return fail(c, PPLS_E_ARG, "vorth must be in [1, 255]");
     c->vorth = (int)value;
@@ -2220,6 +2224,194 @@ int meta_sweep_all(ppls_ctx* c, std::vector<MetaPop>& pops, const std::vector<do
   return PPLS_OK;
 }
 
+// meta_PPLSi on the device (ppls_meta_step_kernel) when the r = 1 statistics take the split sweep
+// (fp64 storage, p and q within its register budget).  Wide or fp32-stored data keep the
+// per-population loop above (the panel sweep has no per-workgroup scalars).
+bool meta_device_ok(const ppls_ctx* c, int npop) {
+  return c->meta_device && npop >= 1 && npop <= PPLS_META_KMAX && !c->dtype && c->sweep_mode != 3 &&
+         ppls_split_supported(1, c->ldx, c->ldy) > 0;
+}
+
+// The whole meta_PPLSi loop (EM_W_multi.R:544-578) on the device.  Per EM step ONE segmented split
+// sweep over all rows -- workgroups partitioned over the populations in proportion to their rows
+// (each workgroup's rows in one population, using that population's scalars) -- then per population
+// a reduction of its workgroups' partials, one all-reduce of the K statistics blocks when sharded,
+// and ppls_meta_step_kernel (log-likelihoods, stop rule, M-step, the next sweep's loadings and
+// scalars).  No host round trip per step: the host enqueues at most LOOKAHEAD steps ahead and
+// stops launching once the step kernel reports the end of the fit (all ranks at the same step).
+// logvalue[1, ] comes from the first sweep (theta0 is every population's, so the full-data Gram is
+// the sum of theirs): no separate full-data sweep.
+int meta_ppls_device(ppls_ctx* c, const std::vector<MetaPop>& pops, const Rank1& t0, int max_steps, double atol,
+                     int crit_abs, ppls_meta_fit* out) {
+  const int K = (int)pops.size();
+  const int p = c->p, q = c->q;
+  int rc;
+  PplsSweepArgs a;
+  if (sweep_plan(c, 1, &a) != 3) return fail(c, PPLS_E_STATE, "meta device path needs the split sweep");
+  // workgroups per population: proportional to its local rows, at least one if it has any
+  int nz = 0;
+  for (const auto& pp : pops) nz += pp.nloc > 0 ? 1 : 0;
+  const int G = std::max(a.grid, nz);
+  std::vector<int> gk((size_t)K, 0);
+  {
+    int left = G;
+    for (int j = 0; j < K; ++j) gk[(size_t)j] = pops[j].nloc > 0 ? 1 : 0;
+    left -= nz;
+    const double nrows = (double)std::max<int64_t>(c->n_local, 1);
+    for (int j = 0; j < K && left > 0; ++j) {
+      if (pops[j].nloc <= 0) continue;
+      const int extra = std::min(left, (int)std::floor((double)(G - nz) * (double)pops[j].nloc / nrows));
+      gk[(size_t)j] += extra;
+      left -= extra;
+    }
+    for (int j = 0; left > 0; j = (j + 1) % K)   // the rounding remainder, one at a time
+      if (pops[j].nloc > 0) { ++gk[(size_t)j]; --left; }
+  }
+  std::vector<int64_t> bnd((size_t)G + 1);
+  std::vector<int> seg((size_t)G), g0((size_t)K + 1, 0);
+  {
+    int g = 0;
+    for (int j = 0; j < K; ++j) {
+      g0[(size_t)j] = g;
+      for (int u = 0; u < gk[(size_t)j]; ++u, ++g) {
+        bnd[(size_t)g] = pops[j].row0 + pops[j].nloc * u / gk[(size_t)j];
+        seg[(size_t)g] = j;
+      }
+    }
+    g0[(size_t)K] = g;
+    bnd[(size_t)G] = c->n_local;
+  }
+  if ((rc = ensure_part(c, G))) return rc;
+  if ((rc = ensure_stop(c)) || (rc = reset_stop(c))) return rc;
+  struct Dev {
+    int64_t* bnd = nullptr;
+    int* seg = nullptr;
+    double* stats = nullptr;
+    double* N = nullptr;
+    double* ssq = nullptr;
+    double* log = nullptr;
+    PplsRank1* st = nullptr;
+    PplsScalars* sc = nullptr;
+    ppls_ctx* c = nullptr;
+    std::vector<hipEvent_t> evs;
+    ~Dev() {
+      dfree(bnd); dfree(seg); dfree(stats); dfree(N); dfree(ssq); dfree(log); dfree(st); dfree(sc);
+      if (c) c->sweep_stop = nullptr;
+      for (auto e : evs) (void)hipEventDestroy(e);
+    }
+  } d;
+  d.c = c;
+  const int64_t pld = c->part_ld, lld = (int64_t)max_steps + 1;
+  if ((rc = dalloc(c, &d.bnd, (size_t)G + 1)) || (rc = dalloc(c, &d.seg, (size_t)G)) ||
+      (rc = dalloc(c, &d.stats, (size_t)K * pld)) || (rc = dalloc(c, &d.N, (size_t)K)) ||
+      (rc = dalloc(c, &d.ssq, (size_t)2 * K)) || (rc = dalloc(c, &d.log, (size_t)K * lld)) ||
+      (rc = dalloc(c, &d.st, (size_t)K)) || (rc = dalloc(c, &d.sc, (size_t)K)))
+    return rc;
+  {
+    std::vector<double> hN((size_t)K), hs((size_t)2 * K), hl((size_t)K * lld, NAN);
+    std::vector<PplsRank1> hst((size_t)K, r1_of(t0));
+    std::vector<PplsScalars> hsc((size_t)K);
+    for (int j = 0; j < K; ++j) {
+      hN[(size_t)j] = pops[j].N;
+      hs[(size_t)2 * j] = pops[j].ssq[0];
+      hs[(size_t)2 * j + 1] = pops[j].ssq[1];
+      ppls_rank1_sweep_scalars(&hst[(size_t)j], &hsc[(size_t)j]);
+    }
+    std::vector<double> wv((size_t)c->ldx, 0.0), cv((size_t)c->ldy, 0.0);
+    std::copy(t0.w.begin(), t0.w.end(), wv.begin());
+    std::copy(t0.c.begin(), t0.c.end(), cv.begin());
+    HIPCHK(c, hipMemcpyAsync(d.bnd, bnd.data(), sizeof(int64_t) * bnd.size(), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(d.seg, seg.data(), sizeof(int) * seg.size(), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(d.N, hN.data(), sizeof(double) * K, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(d.ssq, hs.data(), sizeof(double) * 2 * K, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(d.log, hl.data(), sizeof(double) * hl.size(), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(d.st, hst.data(), sizeof(PplsRank1) * K, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(d.sc, hsc.data(), sizeof(PplsScalars) * K, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->W[0], wv.data(), sizeof(double) * wv.size(), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(c->C[0], cv.data(), sizeof(double) * cv.size(), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));   // the host vectors go out of scope
+  }
+  a.X = c->X;
+  a.Y = c->Y;
+  a.n_local = c->n_local;
+  a.Wp = c->W[0];
+  a.Cp = c->C[0];
+  a.sc = d.sc;
+  a.part = c->part;
+  a.part_ld = pld;
+  a.mu = nullptr;
+  a.write_mu = 0;
+  a.grid = G;
+  a.row_bounds = d.bnd;
+  a.wg_seg = d.seg;
+  a.nt = (c->nt_loads > 0 || (c->nt_loads < 0 && 8.0 * c->n_local * (double)(c->ldx + c->ldy) > 256.0 * (1 << 20))) ? 1 : 0;
+  a.stop = c->stop_d;
+  a.trace = nullptr;
+  c->sweep_stop = c->stop_d;
+  PplsMetaStepArgs m;
+  memset(&m, 0, sizeof m);
+  m.stats = d.stats; m.part_ld = pld; m.K = K; m.p = p; m.q = q; m.ldx = c->ldx; m.ldy = c->ldy;
+  m.N = d.N; m.ssq = d.ssq; m.st = d.st; m.sc = d.sc; m.W = c->W[0]; m.C = c->C[0];
+  m.log = d.log; m.log_ld = lld; m.max_steps = max_steps; m.crit_abs = crit_abs; m.atol = atol;
+  m.stop = c->stop_d; m.stop_mirror = c->stop_mirror_dev;
+  m.ssqX = c->ssq_host[0]; m.ssqY = c->ssq_host[1]; m.Ntot = (double)c->n_total;
+  double* tmp = c->part + (size_t)c->part_groups * pld;
+  // one segmented sweep of the current parameters -> d.stats (K blocks, all-reduced)
+  auto seg_sweep = [&]() -> int {
+    if (c->n_local > 0) HIPCHK(c, ppls_launch_sweep_split(&a, c->stream));
+    for (int j = 0; j < K; ++j) {
+      const int ng = g0[(size_t)j + 1] - g0[(size_t)j];
+      if (ng > 0)
+        HIPCHK(c, ppls_launch_reduce2(c->part + (size_t)g0[(size_t)j] * pld, ng, pld, pld, d.stats + (size_t)j * pld,
+                                      tmp, c->stop_d, c->stream));
+      else
+        HIPCHK(c, hipMemsetAsync(d.stats + (size_t)j * pld, 0, sizeof(double) * pld, c->stream));
+    }
+    return allreduce(c, d.stats, (size_t)K * pld);
+  };
+  constexpr int LOOKAHEAD = 8;
+  for (int step = 0; step <= max_steps; ++step) {
+    if (step >= LOOKAHEAD) {
+      HIPCHK(c, hipEventSynchronize(d.evs[(size_t)(step - LOOKAHEAD) % LOOKAHEAD]));
+      const int ended = __atomic_load_n(c->stop_mirror, __ATOMIC_ACQUIRE);
+      if (ended != 0 && ended <= step - LOOKAHEAD) break;   // the same break step on every rank
+    }
+    if ((rc = seg_sweep())) return rc;
+    m.step = step;
+    HIPCHK(c, ppls_launch_meta_step(&m, c->stream));
+    const size_t k = (size_t)step % LOOKAHEAD;
+    if (d.evs.size() <= k) {
+      hipEvent_t e;
+      HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      d.evs.push_back(e);
+    }
+    HIPCHK(c, hipEventRecord(d.evs[k], c->stream));
+  }
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  int stop[2] = {0, 0};
+  HIPCHK(c, hipMemcpy(stop, c->stop_d, sizeof stop, hipMemcpyDeviceToHost));
+  if (stop[1] == 2)
+    return fail(c, PPLS_E_NUMERIC, "meta_PPLSi: the log-likelihood increment of EM step %d is NaN", stop[0]);
+  out->steps = stop[0] > 0 ? stop[0] : max_steps;
+  std::vector<double> hl((size_t)K * lld), hw((size_t)c->ldx), hc((size_t)c->ldy);
+  std::vector<PplsRank1> hst((size_t)K);
+  HIPCHK(c, hipMemcpy(hl.data(), d.log, sizeof(double) * hl.size(), hipMemcpyDeviceToHost));
+  HIPCHK(c, hipMemcpy(hw.data(), c->W[0], sizeof(double) * hw.size(), hipMemcpyDeviceToHost));
+  HIPCHK(c, hipMemcpy(hc.data(), c->C[0], sizeof(double) * hc.size(), hipMemcpyDeviceToHost));
+  HIPCHK(c, hipMemcpy(hst.data(), d.st, sizeof(PplsRank1) * K, hipMemcpyDeviceToHost));
+  if (out->log) std::copy(hl.begin(), hl.end(), out->log);
+  std::copy(hw.begin(), hw.begin() + p, out->W);
+  std::copy(hc.begin(), hc.begin() + q, out->C);
+  for (int j = 0; j < K; ++j) {
+    out->params[j] = hst[(size_t)j].B;
+    out->params[K + j] = hst[(size_t)j].sigE;
+    out->params[2 * K + j] = hst[(size_t)j].sigF;
+    out->params[3 * K + j] = hst[(size_t)j].sigH;
+    out->params[4 * K + j] = hst[(size_t)j].sigT;
+  }
+  return PPLS_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -2283,6 +2475,7 @@ int ppls_meta_ppls(ppls_ctx* c, int npop, const int64_t* pop_local, const int64_
   const size_t ld = (size_t)max_steps + 1;
   if (out->log)
     for (size_t e = 0; e < ld * npop; ++e) out->log[e] = NAN;
+  if (meta_device_ok(c, npop)) return meta_ppls_device(c, pops, t0, max_steps, atol, crit_abs, out);
   // logvalue[1, ] = rep(logl_W(X, Y, Wnw, Cnw, Bnw, ...), K) (:544): one full-data sweep
   {
     std::vector<double> SX, SY;

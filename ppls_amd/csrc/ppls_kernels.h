@@ -39,6 +39,8 @@ struct PplsSweepArgs {
   long long* trace;      // split sweep diagnostics: 4 wall-clock stamps per workgroup, or nullptr
   const int64_t* row_bounds;   // split sweep: grid + 1 row boundaries (workgroup g owns rows
                                // [b[g], b[g+1])), or nullptr for the even split
+  const int* wg_seg;           // split sweep: per workgroup the index of its scalars (sc[wg_seg[g]]:
+                               // meta_PPLSi's populations), or nullptr (sc for all)
 };
 
 struct PplsFinalizeArgs {
@@ -109,7 +111,31 @@ struct PplsRank1StepArgs {
   int* stop_mirror;        // host-mapped: nonzero once the fit ended
 };
 
+// One EM step of meta_PPLSi on the device (ppls_meta_step_kernel): log-likelihoods and stop rule of
+// the step's sweep, then meta_EMstep's M-step for the next sweep.
+#define PPLS_META_KMAX 1024
+struct PplsMetaStepArgs {
+  const double* stats;     // K x part_ld: per population [X_j'mu_T ldx][Y_j'mu_U ldy][Gram 4] (r = 1)
+  int64_t part_ld;
+  int K, p, q, ldx, ldy;
+  const double* N;         // K: rows of each population (all ranks)
+  const double* ssq;       // 2K: ssq(X_j), ssq(Y_j)
+  PplsRank1* st;           // K population scalars (in/out)
+  PplsScalars* sc;         // K: the next sweep's mu coefficients (out)
+  double* W;               // the next sweep's shared loadings (ldx, ldy; out)
+  double* C;
+  double* log;             // logvalue: population j's column at j log_ld, rows 0 .. max_steps
+  int64_t log_ld;
+  int step, max_steps, crit_abs;
+  double atol;
+  int* stop;               // [0] the step the fit ended at, [1] 2 = NaN increment
+  int* stop_mirror;        // host-mapped copy of stop[0], or nullptr
+  double ssqX, ssqY, Ntot; // the whole data's: step 0 writes logvalue[1, ] = rep(logl_W(theta0), K)
+                           // from the sum of the populations' Grams (theta0 is every population's)
+};
+
 extern "C" {
+hipError_t ppls_launch_meta_step(const PplsMetaStepArgs* a, hipStream_t st);
 int ppls_split_supported(int r, int ldx, int ldy);
 hipError_t ppls_launch_sweep_split(const PplsSweepArgs* a, hipStream_t st);
 int ppls_split_describe(const PplsSweepArgs* a, char* buf, int len);

@@ -310,7 +310,8 @@ __global__ __launch_bounds__(NT, 2 * NT / 512) void ppls_sweep_split_kernel(
     const double* __restrict__ X, const double* __restrict__ Y, int64_t n_local, int ldx, int ldy,
     const double* __restrict__ Wp, const double* __restrict__ Cp, const PplsScalars* __restrict__ sc,
     double* __restrict__ part, int64_t part_ld, double* __restrict__ mu, int write_mu, int nt_loads,
-    const int* __restrict__ stop, long long* __restrict__ trace, const int64_t* __restrict__ row_bounds) {
+    const int* __restrict__ stop, long long* __restrict__ trace, const int64_t* __restrict__ row_bounds,
+    const int* __restrict__ wg_seg) {
   if (stop && *stop) return;   // em_run converged earlier (device stop flag)
   static_assert(SLOTS >= 2 * RP, "ring must hold the group being read and the group in flight");
   // diagnostics (set_option "strace"): per workgroup wall-clock stamps at entry, after the ring
@@ -359,10 +360,13 @@ __global__ __launch_bounds__(NT, 2 * NT / 512) void ppls_sweep_split_kernel(
   }
   const int mj = lane / R, mk = lane - (lane / R) * R;
   if (tid < R) {
-    cf[tid] = sc->alpha[tid];
-    cf[R + tid] = sc->beta[tid];
-    cf[2 * R + tid] = sc->gamma[tid];
-    cf[3 * R + tid] = sc->delta[tid];
+    // segmented sweeps (meta_PPLSi's populations): workgroup g's rows lie in one population and use
+    // that population's scalars sc[wg_seg[g]]
+    const PplsScalars* scg = wg_seg ? sc + wg_seg[g] : sc;
+    cf[tid] = scg->alpha[tid];
+    cf[R + tid] = scg->beta[tid];
+    cf[2 * R + tid] = scg->gamma[tid];
+    cf[3 * R + tid] = scg->delta[tid];
   }
   const int ge = wave * 64 + lane;
   int gi = 0, gj = 0;
@@ -2442,6 +2446,113 @@ __global__ __launch_bounds__(1024) void ppls_rank1_step_kernel(PplsRank1StepArgs
   }
 }
 
+// One EM step of meta_PPLSi (EM_W_multi.R:551-578) on the device, after the segmented sweep of the
+// current parameters theta_i over every population (its per-population statistics stats[j] =
+// [X_j'mu_T | Y_j'mu_U | Gram]):
+//   step >= 1: logvalue[i+1, j] = logl_W of population j from its Gram (:571-573), the stop rule on
+//              critfunc(sum(logvalue[i+1, ]) - sum(logvalue[i, ])) < atol (:575) -- a NaN increment
+//              is R's `if (NA < atol)` error (stop[1] = 2) -- and the end of EMsteps;
+//   then, unless the fit ended: meta_EMstep's M-step (:453-484): meta_Mstep per population
+//              (ppls_rank1_scalars, the EMstepC_fast formulas with N_j, ssq(X_j), ssq(Y_j)), and the
+//              shared W. = orth(sum_j sign(<Cxt_1, Cxt_j>) Cxt_j), C. likewise (Cxt_j = X_j'mu_T / N_j,
+//              orth of one column = v / ||v||), written as the next sweep's loadings and scalars.
+// One 1024-thread block: population j's scalars on thread j, the p- and q-long sums block-wide.
+__global__ __launch_bounds__(1024) void ppls_meta_step_kernel(PplsMetaStepArgs a) {
+  __shared__ double sh[16 * PPLS_RMAX];
+  __shared__ int s_end;
+  __shared__ double s_sg[PPLS_META_KMAX];
+  const int tid = threadIdx.x, K = a.K;
+  if (a.stop[0]) return;   // the fit ended at an earlier step
+  const double* Gs = a.stats + a.ldx + a.ldy;   // population j's Gram at Gs + j part_ld
+  if (a.step == 0 && tid == 0) {   // logvalue[1, ] = rep(logl_W(X, Y, theta0), K) (:544)
+    double G[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int j = 0; j < K; ++j)
+      for (int e = 0; e < 4; ++e) G[e] += Gs[(int64_t)j * a.part_ld + e];
+    const double l0 = ppls_rank1_loglik(&a.st[0], G, a.ssqX, a.ssqY, a.Ntot, a.p, a.q);
+    for (int j = 0; j < K; ++j) a.log[(int64_t)j * a.log_ld] = l0;
+  }
+  if (a.step >= 1) {
+    double l = 0.0;
+    if (tid < K) {
+      const double* G = Gs + (int64_t)tid * a.part_ld;
+      const double Gj[4] = {G[0], G[1], G[2], G[3]};
+      l = ppls_rank1_loglik(&a.st[tid], Gj, a.ssq[2 * tid], a.ssq[2 * tid + 1], a.N[tid], a.p, a.q);
+      a.log[(int64_t)tid * a.log_ld + a.step] = l;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      double s_new = 0.0, s_old = 0.0;   // population order, like the host's sums
+      for (int j = 0; j < K; ++j) {
+        s_new += a.log[(int64_t)j * a.log_ld + a.step];
+        s_old += a.log[(int64_t)j * a.log_ld + a.step - 1];
+      }
+      const double incr = s_new - s_old;
+      int end = 0;
+      if (incr != incr) {
+        a.stop[1] = 2;
+        end = 1;
+      } else if ((a.crit_abs ? fabs(incr) : incr) < a.atol || a.step >= a.max_steps) {
+        end = 1;
+      }
+      if (end) {
+        a.stop[0] = a.step;
+        if (a.stop_mirror) __hip_atomic_store(a.stop_mirror, a.step, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+      s_end = end;
+    }
+    __syncthreads();
+    if (s_end) return;
+  }
+  // M-step: signs of <SX_1 / N_1, SX_j / N_j>, then the shared loadings
+  const double N1 = a.N[0];
+  for (int j0 = 0; j0 < K; j0 += PPLS_RMAX) {
+    const int nj = K - j0 < PPLS_RMAX ? K - j0 : PPLS_RMAX;
+    double v[PPLS_RMAX];
+    for (int u = 0; u < nj; ++u) v[u] = 0.0;
+    for (int i = tid; i < a.p; i += blockDim.x) {
+      const double x1 = a.stats[i] / N1;
+      for (int u = 0; u < nj; ++u) v[u] = fma(x1, a.stats[(int64_t)(j0 + u) * a.part_ld + i] / a.N[j0 + u], v[u]);
+    }
+    ppls_block_sum(v, nj, sh);
+    if (tid == 0)
+      for (int u = 0; u < nj; ++u) s_sg[j0 + u] = v[u] > 0 ? 1.0 : (v[u] < 0 ? -1.0 : 0.0);   // R's sign()
+  }
+  __syncthreads();
+  double nrm[2] = {0.0, 0.0};
+  for (int i = tid; i < a.ldx; i += blockDim.x) {
+    double w = 0.0;
+    if (i < a.p)
+      for (int j = 0; j < K; ++j) w += s_sg[j] * (a.stats[(int64_t)j * a.part_ld + i] / a.N[j]);
+    a.W[i] = w;
+    nrm[0] = fma(w, w, nrm[0]);
+  }
+  for (int i = tid; i < a.ldy; i += blockDim.x) {
+    double cv = 0.0;
+    if (i < a.q)
+      for (int j = 0; j < K; ++j) cv += s_sg[j] * (a.stats[(int64_t)j * a.part_ld + a.ldx + i] / a.N[j]);
+    a.C[i] = cv;
+    nrm[1] = fma(cv, cv, nrm[1]);
+  }
+  ppls_block_sum(nrm, 2, sh);
+  const double nw = sqrt(nrm[0]), nc = sqrt(nrm[1]);
+  for (int i = tid; i < a.ldx; i += blockDim.x) a.W[i] /= nw;
+  for (int i = tid; i < a.ldy; i += blockDim.x) a.C[i] /= nc;
+  if (tid < K) {   // meta_Mstep of population tid, then its next sweep's mu coefficients
+    const double* G = Gs + (int64_t)tid * a.part_ld;
+    const double Gj[4] = {G[0], G[1], G[2], G[3]};
+    PplsRank1 nt;
+    ppls_rank1_scalars(&a.st[tid], Gj, a.ssq[2 * tid], a.ssq[2 * tid + 1], a.N[tid], a.p, a.q, &nt);
+    a.st[tid] = nt;
+    ppls_rank1_sweep_scalars(&nt, &a.sc[tid]);
+  }
+}
+
+hipError_t ppls_launch_meta_step(const PplsMetaStepArgs* a, hipStream_t st) {
+  if (a->K < 1 || a->K > PPLS_META_KMAX) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(ppls_meta_step_kernel, dim3(1), dim3(1024), 0, st, *a);
+  return hipGetLastError();
+}
+
 // loglC_fast from explicit coefficients (the drop-in of src/loglC.cpp:318-338).
 __global__ void ppls_loglc_kernel(const double* __restrict__ G, const double* __restrict__ ssq, double N,
                                   int p, int q, int r, double sigX, double sigY,
@@ -2530,7 +2641,7 @@ hipError_t launch_split_t(const PplsSweepArgs& a, hipStream_t st) {
   }
   hipLaunchKernelGGL(kern, dim3(a.grid), dim3(512), split_lds(R, a.ldx, a.ldy, 512, RP), st, a.X, a.Y,
                      a.n_local, a.ldx, a.ldy, a.Wp, a.Cp, a.sc, a.part, a.part_ld, a.mu, a.write_mu,
-                     a.nt, a.stop, a.trace, a.row_bounds);
+                     a.nt, a.stop, a.trace, a.row_bounds, a.wg_seg);
   return hipGetLastError();
 }
 

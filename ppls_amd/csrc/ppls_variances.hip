@@ -425,11 +425,14 @@ static int ppls_gram_live_quads(const PplsGramCols& gc) {
   return w;
 }
 
-// The row splits of a Gram over n rows: nsplit_req > 0 equal splits; 0 (auto) halving splits n / 2,
-// n / 4, ..., n / 2^k, n / 2^k.  A wave's items are taken dynamically, so the run ends on the smallest
-// items: k is the first with one such item at most ~1 % of a wave slot's share of the work (C3: 8
-// splits, the last 7,812 rows), within 4 GB of partials (32 KB per live quadrant and split) and >= 256
-// rows per split.  bounds: nsplit + 1 row boundaries.
+// The row splits of a Gram over n rows: nsplit_req > 0 equal splits; 0 (auto) a guided schedule.
+// Waves take items dynamically, split by split, so the run ends on the last split's items: each
+// split holds about half the remaining work per wave slot (rows = W1 R / (2 slots) of the R rows
+// left, W1 live quadrants per split), at most half of R, at least ~1 % of a slot's whole share
+// (and 256 rows), so the first splits keep every wave busy and the last ones are short.  C3's S
+// (W1 = 2,016 on 2,048 wave slots): 8 splits of 49 %, 26 %, 13 % ... of the rows; C3's X'X alone
+// (W1 = 528): ~28 splits of 13 % of the remaining rows each; C5 (W1 ~ 14,000): 4.  Partials: 32 KB
+// per live quadrant and split, kept under 4 GB (<= 64 splits).  bounds: nsplit + 1 row boundaries.
 int ppls_gram_plan(int p, int xreal, int xcols, int yreal, int64_t n, int wave_slots, int nsplit_req, int64_t* bounds) {
   const PplsGramCols gc{p, xreal, xcols, xcols + yreal};
   const double w1 = (double)ppls_gram_live_quads(gc);
@@ -438,16 +441,25 @@ int ppls_gram_plan(int p, int xreal, int xcols, int yreal, int64_t n, int wave_s
       for (int s = 0; s <= nsplit_req; ++s) bounds[s] = n * s / nsplit_req;
     return nsplit_req;
   }
-  int k = 0;
-  while (k < 16 && (double)wave_slots / (w1 * (double)(1LL << k)) > 0.01 && (n >> (k + 1)) >= 256 &&
-         (double)(k + 2) * w1 * PPLS_GQ * PPLS_GQ * 8.0 <= 4.0e9)
-    ++k;
-  const int nsplit = k + 1;
-  if (bounds) {
-    for (int j = 0; j <= k; ++j) bounds[j] = k == 0 ? 0 : n - (n >> j);
-    bounds[nsplit] = n;
+  const double slots = wave_slots > 0 ? (double)wave_slots : 1.0;
+  int maxs = (int)(4.0e9 / (w1 * PPLS_GQ * PPLS_GQ * 8.0));
+  maxs = maxs < 1 ? 1 : (maxs > 64 ? 64 : maxs);
+  int64_t smin = (int64_t)(0.01 * w1 * (double)n / slots);
+  if (smin < 256) smin = 256;
+  int ns = 0;
+  int64_t done = 0;
+  if (bounds) bounds[0] = 0;
+  while (done < n) {
+    const int64_t R = n - done;
+    int64_t sz = (int64_t)(w1 * (double)R / (2.0 * slots));
+    if (sz > R / 2) sz = R / 2;
+    if (sz < smin) sz = smin;
+    if (R - sz < smin || ns + 1 >= maxs) sz = R;   // no sliver, and the last split allowed takes the rest
+    done += sz;
+    ++ns;
+    if (bounds) bounds[ns] = done;
   }
-  return nsplit;
+  return ns < 1 ? 1 : ns;
 }
 
 int64_t ppls_gram_part_doubles(int p, int nsplit) {

@@ -95,3 +95,31 @@ def test_meta_rejects_bad_populations(ctx):
         ctx.meta_ppls([30, 10], 5, 1e-4, init)       # sizes do not cover nrow(X)
     with pytest.raises(PplsError):
         ctx.meta_ppls([50, 0], 5, 1e-4, init)        # an empty level
+
+
+@pytest.mark.parametrize("sizes,atol", [([300, 250, 200, 250], 1e-6), ([997], -np.inf), ([3, 500, 2, 495], 1e-5),
+                                        ([40] * 25, -np.inf)],
+                         ids=["K4_stop", "K1", "tiny_pops", "K25"])
+def test_meta_device_loop_equals_host_loop(ctx, sizes, atol):
+    """The device meta_PPLSi (one segmented sweep per EM step over every population, the M-step, the
+    log-likelihoods and the stop rule in one kernel; option meta_device = 1, the default) against the
+    per-population host loop (meta_device = 0) and the oracle: the same steps, log-likelihoods to
+    1e-12, loadings and parameters to 1e-10 (the sums are regrouped: the device sweep partitions the
+    workgroups over the populations)."""
+    n = int(sum(sizes))
+    X, Y, _ = make_problem(n, 37, 29, 1, seed=n)
+    init = o.initial_guess(37, 29, "equal")
+    ctx.set_data(X, Y)
+    res = {}
+    for dev in (1, 0):
+        ctx.set_option("meta_device", dev)
+        res[dev] = ctx.meta_ppls(sizes, 40, atol, init)
+    ctx.set_option("meta_device", 1)
+    (W1, C1, P1, L1), (W0, C0, P0, L0) = res[1], res[0]
+    assert L1.shape == L0.shape
+    assert _relerr(L1, L0) < 1e-12
+    assert np.abs(W1 - W0).max() < 1e-10 and np.abs(C1 - C0).max() < 1e-10
+    assert _relerr(P1, P0) < 1e-10
+    ref = o.meta_pplsi(X, Y, sizes, 40, atol, init)
+    assert L1.shape[0] == ref["logvalue"].shape[0]
+    assert _relerr(L1, ref["logvalue"]) < 1e-10
