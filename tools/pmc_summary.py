@@ -2,6 +2,7 @@
 
     python tools/pmc_summary.py <tag> <workload> <algorithmic_bytes_per_launch> [note] [--kernels a,b]
 
+--out <name>: write profiles/pmc_<name>.json instead (a kernel other than the sweep, e.g. the Gram).
 --kernels: substrings of the kernels that make up one sweep (default "sweep"); the per-launch
 traffic of each is averaged over its dispatches and the sweep's traffic is their sum (the wide-p
 panel sweep is two kernels: panel_mfmadots + panel_acc).
@@ -55,6 +56,11 @@ def per_launch(path, counter, subs=("sweep",)):
 def main():
     args = list(sys.argv[1:])
     subs = ("sweep",)
+    out_name = None
+    if "--out" in args:   # another kernel than the sweep: profiles/pmc_<name>.json
+        i = args.index("--out")
+        out_name = args[i + 1]
+        del args[i:i + 2]
     if "--kernels" in args:
         i = args.index("--kernels")
         subs = tuple(args[i + 1].split(","))
@@ -75,7 +81,7 @@ def main():
                traffic_over_algorithmic=hbm / alg,
                source=f"rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) -- python3 bench.py; {note}",
                profiled_tree=profiled_tree())
-    path = os.path.join(ROOT, "profiles", f"pmc_sweep_{workload}.json")
+    path = os.path.join(ROOT, "profiles", f"pmc_{out_name}.json" if out_name else f"pmc_sweep_{workload}.json")
     with open(path, "w") as f:
         json.dump(out, f, indent=1)
     print(path, f"{hbm / alg:.4f} x algorithmic")
