@@ -18,12 +18,12 @@ bash tools/pmc_compute.sh r5c5 --config c5 --no-call --steps 20 --xprod-steps 10
    > "$R/gpurun_out/prof_r5meta_trace.log" 2>&1) || exit $?
 cd "$R" || exit 1
 python3 tools/pmc_summary.py r5c3 c3_dp1 32e9 "round 5" || exit $?
-python3 tools/pmc_summary.py r5c3 c3_dp1 16e9 "round 5: the MFMA Gram forming S; algorithmic = one read of X, Y" \
+python3 tools/pmc_summary.py r5c3 c3_dp1 32e9 "round 5: the MFMA Gram forming S; algorithmic = one read of X, Y" \
   --kernels gram_mfma --out gram_s_c3 || exit $?
 python3 tools/pmc_xprod_summary.py r5c3 c3 "round 5" || exit $?
 python3 tools/pmc_compute_summary.py r5c3 c3_dp1 sweep_split,gram_mfma,xprod_tile,finalize --trace gpurun_out/prof_r5c3/trace/run_kernel_stats.csv || exit $?
 python3 tools/pmc_summary.py r5c5 c5_dp1 21e9 "round 5" --kernels panel_mfmadots,panel_acc || exit $?
-python3 tools/pmc_summary.py r5c5 c5_dp1 10.5e9 "round 5: the MFMA Gram forming S; algorithmic = one read of X, Y" \
+python3 tools/pmc_summary.py r5c5 c5_dp1 21e9 "round 5: the MFMA Gram forming S; algorithmic = one read of X, Y" \
   --kernels gram_mfma --out gram_s_c5 || exit $?
 python3 tools/pmc_xprod_summary.py r5c5 c5 "round 5" --bytes 924844032 || exit $?
 python3 tools/pmc_compute_summary.py r5c5 c5_dp1 panel_mfmadots,panel_acc,gram_mfma,xprod_tile,finalize --trace gpurun_out/prof_r5c5/trace/run_kernel_stats.csv || exit $?
