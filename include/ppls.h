@@ -113,7 +113,11 @@ const char* ppls_last_error(const ppls_ctx* ctx);
  *                     itself when r <= 8 and p + q <= 6144; 0: a separate Gram kernel),
  *       "dots_rows" (panel sweep dots: rows per wave, 0 auto (64 from 32768 rows, else 32), 32, 64),
  *       "dots_pair" (panel sweep dots: a wave pair per row tile, -1 auto (when row tiles are fewer
- *                    than resident wave slots), 0, 1) */
+ *                    than resident wave slots), 0, 1),
+ *       "dots_dma" (panel sweep dots: how X tiles reach the MFMAs: -1 auto, 0 16-B loads into VGPRs +
+ *                   LDS transpose, 1 LDS-DMA, 2 LDS-DMA with non-temporal loads; auto = 2 when the
+ *                   data exceed the MALL and one wave owns a row tile, else 1; all forms give the
+ *                   same results bit for bit) */
 int ppls_set_option(ppls_ctx* ctx, const char* key, int64_t value);
 
 /* ---- multi-GPU: samples are sharded over ranks; one RCCL all-reduce per EM iteration ---- */
