@@ -2982,7 +2982,7 @@ hipError_t launch_panel_t(const PplsSweepArgs* a, const T* X, const T* Y, double
     double* mu_out = a->write_mu ? a->mu : nullptr;
     // X tiles by LDS-DMA (round 5), non-temporal where the data exceed the MALL and one wave owns a
     // row tile (full C5: 7.40 -> 7.29 ms per iteration; the C5 share's wave pairs: nt 1.5 % slower;
-    // profiles/r5_dots_dma_ab.txt); option dots_dma forces a form (0: VGPR staging)
+    // profiles/r5_dots_dma_ab_c5.txt, r5_dots_dma_ab_c5s.txt); option dots_dma forces a form (0: VGPR staging)
     const int dma = a->dots_dma >= 0 ? a->dots_dma : (a->nt && ks == 1 ? 2 : 1);
     // (also measured: the B operands prefetched a tile ahead, 256 VGPRs -- no faster, 7.70-7.88 vs
     // 7.69-7.78 ms; profiles/r2_c5_dots_rows.txt)
