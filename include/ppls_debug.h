@@ -48,6 +48,12 @@ int ppls_sweep_kernel(ppls_ctx* ctx, int r, char* buf, int len);
 /* The Gram D'D alone (D = X for xory 0, Y for 1; nsplit 0 = auto), for tests and benchmarks:
  * G (p x p, column-major, nullable), *ms = the MFMA kernel's duration. */
 int ppls_gram(ppls_ctx* ctx, int xory, int nsplit, double* G, double* ms);
+/* Inverse of a batch of symmetric positive definite matrices (host A: a x p x p, column-major, stride
+ * p^2) as variances.PPLS_simult inverts the observed information: method 1 the hand-written blocked
+ * Cholesky + inverse (ppls_linalg.hip), 2 rocSOLVER potrf + potri.  out: the full symmetric inverses;
+ * info[z] = 0, or the 1-based column of the first non-positive pivot of matrix z (then out[z] is
+ * not meaningful); *ms = device time of the factorisation and inverse. */
+int ppls_spd_inverse(ppls_ctx* ctx, const double* A, int p, int a, int method, double* out, int* info, double* ms);
 /* The generator's Philox4x32-10 block function on the device, for known-answer checks: out[4i..4i+3]
  * = philox4x32_10(ctr[4i..4i+3], key = {key & 0xffffffff, key >> 32}), i < count (host arrays).
  * The generator uses ctr = {pair lo, pair hi, stream, 0}, key = seed. */

@@ -101,6 +101,7 @@ SIGNATURES = {
     "ppls_variances": (ct.c_int, [ct.c_void_p, _dp, _dp, ct.c_double, ct.c_int, ct.c_int, _dp, _dp, _dp, _dp,
                                   _dp, _dp]),
     "ppls_gram": (ct.c_int, [ct.c_void_p, ct.c_int, ct.c_int, _dp, _dp]),
+    "ppls_spd_inverse": (ct.c_int, [ct.c_void_p, _dp, ct.c_int, ct.c_int, ct.c_int, _dp, ct.POINTER(ct.c_int), _dp]),
     "ppls_xprod_prepare": (ct.c_int, [ct.c_void_p, _dp, _dp]),
     "ppls_xprod_release": (ct.c_int, [ct.c_void_p]),
     "ppls_xprod_setup_times": (ct.c_int, [ct.c_void_p, _dp, _dp, _dp]),

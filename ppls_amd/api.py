@@ -368,6 +368,23 @@ class Context:
         self._chk(self._L.ppls_gram(self.h, int(xory), int(nsplit), dptr(G), ct.byref(ms)))
         return G, ms.value
 
+    def spd_inverse(self, A, method=1):
+        """Inverses of symmetric positive definite matrices A (a x p x p or p x p) on the device as
+        variances.PPLS_simult computes them (method 1 hand-written blocked Cholesky, 2 rocSOLVER)
+        -> (inverses, info per matrix: 0 or the 1-based column of the first bad pivot, device ms)."""
+        A = np.asarray(A, dtype=np.float64)
+        one = A.ndim == 2
+        A3 = A[None] if one else A
+        a, p = A3.shape[0], A3.shape[1]
+        Af = np.ascontiguousarray(np.transpose(A3, (0, 2, 1)))   # column-major per matrix
+        out = np.empty_like(Af)
+        info = (ct.c_int * a)()
+        ms = ct.c_double()
+        self._chk(self._L.ppls_spd_inverse(self.h, dptr(Af), int(p), int(a), int(method), dptr(out), info,
+                                            ct.byref(ms)))
+        inv = np.transpose(out, (0, 2, 1))
+        return (inv[0] if one else inv), np.array(list(info)), ms.value
+
     def xprod_prepare(self):
         """Form the cross-products S = [X Y]'[X Y] now (option "xprod") -> (Gram kernel ms, total ms);
         (0, 0) when S is already formed for the current data."""

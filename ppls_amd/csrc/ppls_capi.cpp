@@ -141,7 +141,8 @@ struct ppls_ctx {
   int* gram_q = nullptr;
   int64_t gq_key[6] = {-1, -1, -1, -1, -1, -1};   // (p, xreal, xcols, yreal, n, nsplit_req) of gram_q
   rocblas_handle blas = nullptr;   // rocSOLVER (variances.PPLS_simult's p x p inverse), created lazily
-  int var_chol = 1;                // option "var_chol": that inverse by Cholesky when positive definite (1) or LU (0)
+  int var_chol = 1;                // option "var_chol": that inverse by Cholesky when positive definite: 1 hand-written
+                                   // (ppls_linalg.hip), 2 rocSOLVER potrf/potri; 0 LU (rocSOLVER getrf/getri)
   // timing
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;
   size_t ev_used = 0;
@@ -1228,7 +1229,8 @@ int ppls_set_option(ppls_ctx* c, const char* key, int64_t value) {
   } else if (!strcmp(key, "xprod_fuse")) {
     c->xprod_fuse = value ? 1 : 0;
   } else if (!strcmp(key, "var_chol")) {
-    c->var_chol = value ? 1 : 0;
+    if (value < 0 || value > 2) return fail(c, PPLS_E_ARG, "var_chol must be 0 (LU), 1 (Cholesky) or 2 (rocSOLVER Cholesky)");
+    c->var_chol = (int)value;
   } else if (!strcmp(key, "xprod_rw")) {
     if (value != 0 && value != 1 && value != 2 && value != 4 && value != 8)
       return fail(c, PPLS_E_ARG, "xprod_rw must be 0, 1, 2, 4 or 8");
@@ -2638,7 +2640,18 @@ int ppls_variances(ppls_ctx* c, const double* mu, const double* Cdiag, double si
   // getrf + getri, from the untouched M.  Either inverse is backward stable: they agree to ~kappa eps.
   std::vector<rocblas_int> inf(a, 0);
   bool chol = c->var_chol != 0;
-  if (chol) {
+  if (chol && c->var_chol == 1) {
+    // hand-written (ppls_linalg.hip): blocked Cholesky of every matrix of the batch in the same
+    // launches, then T = L^-1 and T'T -- 3 nb + nb + 1 launches (nb = p / 64) where rocSOLVER's
+    // potrf + potri took 1,400 (profiles/r4_variances_c3_timeline.txt)
+    VRC(dalloc(c, &dMc, pp * (size_t)a + (size_t)ppls_spd_inverse_work(p, a)));
+    VCHK(hipMemcpyAsync(dMc, dM, sizeof(double) * pp * a, hipMemcpyDeviceToDevice, c->stream));
+    VCHK(ppls_launch_negate(dMc, (int64_t)pp * a, c->stream));
+    VCHK(ppls_spd_inverse_batched(dMc, p, a, dMc + pp * (size_t)a, (int*)info, c->stream));
+    VCHK(hipMemcpyAsync(inf.data(), info, sizeof(rocblas_int) * a, hipMemcpyDeviceToHost, c->stream));
+    VCHK(hipStreamSynchronize(c->stream));
+    for (int i = 0; i < a; ++i) chol = chol && inf[i] == 0;
+  } else if (chol) {
     VRC(dalloc(c, &dMc, pp * (size_t)a));
     VCHK(hipMemcpyAsync(dMc, dM, sizeof(double) * pp * a, hipMemcpyDeviceToDevice, c->stream));
     VCHK(ppls_launch_negate(dMc, (int64_t)pp * a, c->stream));
@@ -2676,6 +2689,58 @@ int ppls_variances(ppls_ctx* c, const double* mu, const double* Cdiag, double si
   VCHK(hipStreamSynchronize(c->stream));
 #undef VCHK
 #undef VRC
+  return done(PPLS_OK);
+}
+
+// Diagnostics / tests: the batched SPD inverse of variances.PPLS_simult on host matrices.
+int ppls_spd_inverse(ppls_ctx* c, const double* A, int p, int a, int method, double* out, int* info, double* ms) {
+  if (!c || !A || !out || !info || p < 1 || a < 1 || (method != 1 && method != 2)) return PPLS_E_ARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  const size_t pp = (size_t)p * p;
+  double *dA = nullptr, *dse = nullptr;
+  int* dinfo = nullptr;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  int rc = PPLS_OK;
+  auto done = [&](int code) {
+    dfree(dA); dfree(dse);
+    if (dinfo) (void)hipFree(dinfo);
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    return code;
+  };
+  const size_t work = method == 1 ? (size_t)ppls_spd_inverse_work(p, a) : 0;
+  if ((rc = dalloc(c, &dA, pp * a + work)) || (rc = dalloc(c, &dse, (size_t)p))) return done(rc);
+  if (hipMalloc((void**)&dinfo, sizeof(int) * 2 * a) != hipSuccess) return done(fail(c, PPLS_E_HIP, "hipMalloc failed"));
+  if (hipMemcpy(dA, A, sizeof(double) * pp * a, hipMemcpyHostToDevice) != hipSuccess ||
+      hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess)
+    return done(fail(c, PPLS_E_HIP, "spd_inverse: setup failed"));
+  if (method == 2) {
+    if (!c->blas && rocblas_create_handle(&c->blas) != rocblas_status_success)
+      return done(fail(c, PPLS_E_HIP, "rocblas_create_handle failed"));
+    if (rocblas_set_stream(c->blas, c->stream) != rocblas_status_success)
+      return done(fail(c, PPLS_E_HIP, "rocblas_set_stream failed"));
+  }
+  (void)hipEventRecord(e0, c->stream);
+  if (method == 1) {
+    if (ppls_spd_inverse_batched(dA, p, a, dA + pp * a, dinfo, c->stream) != hipSuccess)
+      return done(fail(c, PPLS_E_HIP, "spd_inverse: launch failed"));
+  } else if (rocsolver_dpotrf_strided_batched(c->blas, rocblas_fill_lower, p, dA, p, (rocblas_stride)pp, dinfo, a) !=
+                 rocblas_status_success ||
+             rocsolver_dpotri_strided_batched(c->blas, rocblas_fill_lower, p, dA, p, (rocblas_stride)pp, dinfo + a, a) !=
+                 rocblas_status_success) {   // (info: potrf's)
+    return done(fail(c, PPLS_E_HIP, "rocsolver potrf/potri failed"));
+  }
+  (void)hipEventRecord(e1, c->stream);
+  for (int z = 0; z < a; ++z)
+    if (ppls_launch_symdiag(dA + pp * z, p, dse, c->stream) != hipSuccess)
+      return done(fail(c, PPLS_E_HIP, "spd_inverse: symdiag failed"));
+  if (hipStreamSynchronize(c->stream) != hipSuccess ||   // (the context stream does not block with stream 0)
+      hipMemcpy(out, dA, sizeof(double) * pp * a, hipMemcpyDeviceToHost) != hipSuccess ||
+      hipMemcpy(info, dinfo, sizeof(int) * a, hipMemcpyDeviceToHost) != hipSuccess)
+    return done(fail(c, PPLS_E_HIP, "spd_inverse: copy-out failed"));
+  float t = 0.f;
+  (void)hipEventElapsedTime(&t, e0, e1);
+  if (ms) *ms = t;
   return done(PPLS_OK);
 }
 

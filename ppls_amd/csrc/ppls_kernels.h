@@ -196,6 +196,10 @@ hipError_t ppls_launch_varmat(const double* G, const double* cxt, const double* 
 hipError_t ppls_launch_negdiag(double* M, int p, double* se, hipStream_t st);
 hipError_t ppls_launch_negate(double* M, int64_t len, hipStream_t st);
 hipError_t ppls_launch_symdiag(double* M, int p, double* se, hipStream_t st);
+// ppls_linalg.hip: batched inverse of SPD matrices (blocked Cholesky + inverse of the factor; the
+// inverse's lower triangle in place), scratch and per-matrix pivot info (0, or the first bad pivot + 1)
+int64_t ppls_spd_inverse_work(int p, int a);
+hipError_t ppls_spd_inverse_batched(double* A, int p, int a, double* work, int* info, hipStream_t st);
 hipError_t ppls_launch_to_colmajor(const double* src, int64_t n, int p, int ld, double* dst,
                                    hipStream_t st);
 }

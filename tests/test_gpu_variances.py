@@ -3,8 +3,9 @@ oracle (oracle.ppls_oracle.variances_ppls_simult, a literal restatement).
 
 Tolerances (fp64): the Gram 1e-13 relative (and exactly symmetric); W 1e-10 absolute; SSt_exp,
 SSt_star 1e-11 relative; varMatrix and seLoad 1e-8 relative (the inverse of the observed information:
-rocSOLVER Cholesky potrf/potri by default, LU getrf/getri with option var_chol = 0 or when the matrix
-is not positive definite, vs LAPACK gesv -- all backward stable, they differ by ~cond * eps).
+the hand-written blocked Cholesky + inverse of ppls_linalg.hip by default, rocSOLVER potrf/potri with
+option var_chol = 2, LU getrf/getri with var_chol = 0 or when the matrix is not positive definite, vs
+LAPACK gesv -- all backward stable, they differ by ~cond * eps).
 """
 import numpy as np
 import pytest
@@ -55,7 +56,7 @@ def test_gram_fp32_storage(ctx):
     assert _rel(G, X32.T @ X32) < 1e-13
 
 
-@pytest.mark.parametrize("chol", [1, 0], ids=["chol", "lu"])
+@pytest.mark.parametrize("chol", [1, 2, 0], ids=["chol", "chol_rocsolver", "lu"])
 @pytest.mark.parametrize("from_s", [False, True], ids=["gram", "from_S"])
 @pytest.mark.parametrize("xy", ["X", "Y"])
 def test_variances_matches_oracle(ctx, xy, from_s, chol):
@@ -88,3 +89,27 @@ def test_variances_matches_oracle(ctx, xy, from_s, chol):
     assert _rel(got2["seLoad"], ref["seLoad"]) < 1e-8
     with pytest.raises(ValueError):
         ppls_amd.variances_PPLS_simult(fit, D)          # XorY left at its default c("X", "Y")
+
+
+@pytest.mark.parametrize("xy", ["X", "Y"])
+def test_variances_multi_block(ctx, xy):
+    """p = 150, q = 131: the hand-written inverse's 64 x 64 blocks, a partial last block; equal to
+    the oracle and to rocSOLVER's potrf/potri (var_chol = 2)."""
+    import ppls_amd
+    X, Y, th0 = make_problem(1500, 150, 131, 4, seed=67)
+    fit = o.ppls_simult(X, Y, 4, EMsteps=15, atol=-np.inf, theta0=th0)
+    D = X if xy == "X" else Y
+    ref = o.variances_ppls_simult(fit, D, xy)
+    ctx.set_data(X, Y)
+    got = {}
+    for chol in (1, 2):
+        ctx.set_option("var_chol", chol)
+        try:
+            got[chol] = ppls_amd.variances_PPLS_simult(fit, None, xy, ctx=ctx)
+        finally:
+            ctx.set_option("var_chol", 1)
+    for i in range(4):
+        assert _rel(got[1]["varMatrix"][i], ref["varMatrix"][i]) < 1e-8
+        assert _rel(got[1]["varMatrix"][i], got[2]["varMatrix"][i]) < 1e-9
+        assert np.array_equal(got[1]["varMatrix"][i], got[1]["varMatrix"][i].T)
+    assert _rel(got[1]["seLoad"], ref["seLoad"]) < 1e-8
