@@ -71,106 +71,156 @@ __device__ __forceinline__ void mm64(double (&acc)[4][4], const double* sA, cons
   }
 }
 
+__device__ __forceinline__ double ppls_bcast(double v, int lane) {   // lane's v, wave-uniform lane
+  const int lo = __builtin_amdgcn_readlane(__double2loint(v), lane);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), lane);
+  return __hiloint2double(hi, lo);
+}
+
 // diag(k): L_kk = chol(A_kk) (lower, written back), Li_k = L_kk^-1 into Li (64 x 64 per block,
 // column-major) and into T's diagonal block.  Padding beyond p: the identity.  Every thread of the
-// workgroup calls it (barriers); wave 0 computes -- one wave per matrix: lane i owns row i for the
-// factorisation (right-looking: at step j it scales L_ij and updates L_il for j < l <= i) and column
-// i for the inverse (forward substitution L x = e_i).  L, I: LDS of 64 x 65 doubles each.
-__device__ __forceinline__ void diag_block(double* __restrict__ A, int p, int64_t pp, int k, double* __restrict__ Li, int nb,
-                           double* __restrict__ T, int* __restrict__ info, int z, double* __restrict__ L,
-                           double* __restrict__ I) {
-  constexpr int LS = NB + 1;
+// 256-thread workgroup calls it.  Blocked by 16: for each 16-column panel J, wave 0 factors and
+// inverts the 16 x 16 diagonal sub-block in registers (lane r holds row r; columns exchanged by
+// readlane), then the workgroup scales the panel below it (L_IJ = A_IJ D_J^-T) and updates the
+// trailing lower triangle; the inverse's off-diagonal sub-blocks follow by levels I - J = 1, 2, 3:
+// Li_IJ = -Li_II sum_{K=J}^{I-1} L_IK Li_KJ (the sums parked in Li's unused upper triangle).
+// L, I: LDS, 64 x 65 doubles each.
+__device__ __forceinline__ void diag_block(double* __restrict__ A, int p, int64_t pp, int k, double* __restrict__ Li,
+                                           int nb, double* __restrict__ T, int* __restrict__ info, int z,
+                                           double* __restrict__ L, double* __restrict__ I) {
+  constexpr int LS = NB + 1, SB = 16;
   const int t = threadIdx.x;
-  const bool w0 = t < NB;
   double* Az = A + pp * z;
   const int o = NB * k, lim = p - o < NB ? p - o : NB;
-  if (w0)
-    for (int c0 = 0; c0 < NB; c0 += 16) {   // lanes along rows (coalesced columns), 16 loads in flight
-      double v[16];
+  {   // the lower triangle (identity past p): thread t row t & 63, columns 4 u + (t >> 6)
+    const int r = t & 63, c0 = t >> 6;
+    double v[16];
 #pragma unroll
-      for (int u = 0; u < 16; ++u) {
-        const int r = t, c = c0 + u;
-        v[u] = (r < lim && c < lim && r >= c) ? Az[(o + r) + (int64_t)(o + c) * p] : 0.0;   // the lower triangle
-      }
-#pragma unroll
-      for (int u = 0; u < 16; ++u) {
-        const int r = t, c = c0 + u;
-        L[r * LS + c] = (r < lim && c < lim) ? v[u] : (r == c ? 1.0 : 0.0);
-      }
+    for (int u = 0; u < 16; ++u) {
+      const int c = 4 * u + c0;
+      v[u] = (r < lim && c < lim && r >= c) ? Az[(o + r) + (int64_t)(o + c) * p] : 0.0;
     }
-  __syncthreads();
-  // factorisation; the scaled column j goes to its own array (cj) so the update loop's reads and
-  // the row's read-modify-writes are provably distinct and pipeline; trip counts are uniform
-  double* __restrict__ cj = I;   // (I is free until the inverse; restrict: the loops below pipeline)
-  int bad = 0;
-  for (int j = 0; j < NB; ++j) {
-    const double d = L[j * LS + j];
-    if (!bad && !(d > 0.0 && d < INFINITY)) bad = j + 1;   // NaN fails too
-    const double s = sqrt(d);
-    const double lij = (w0 && t > j) ? L[t * LS + j] / s : 0.0;
-    if (w0) cj[t] = lij;
-    __syncthreads();
-    if (w0 && t > j) L[t * LS + j] = lij;
-    if (t == j) L[j * LS + j] = s;
-    if (w0)   // groups of 8 from l = j + 1 (the last group shifted back to end at 63; its elements
-              // below the start add 0): no branch, loads batched.  Rows t < l get garbage in their
-              // upper triangle, which is never read.
-      for (int l0 = j + 1; l0 < NB; l0 += 8) {
-        const int b = l0 < NB - 8 ? l0 : NB - 8;
-        double cv[8], lv[8];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          cv[u] = cj[b + u];
-          lv[u] = L[t * LS + b + u];
-        }
-#pragma unroll
-        for (int u = 0; u < 8; ++u) lv[u] = fma(-(b + u >= l0 ? lij : 0.0), cv[u], lv[u]);
-#pragma unroll
-        for (int u = 0; u < 8; ++u) L[t * LS + b + u] = lv[u];
-      }
-    __syncthreads();
-  }
-  // Li = L^-1, lane c: column c, right-looking (x_i = rhs_i / L_ii, then rhs_m -= L_mi x_i for m > i;
-  // rows above c stay 0), the column held in I
-  if (w0) {
-    const int c = t;
-    for (int i = 0; i < NB; ++i) I[i * LS + c] = i == c ? 1.0 : 0.0;
-    for (int i = 0; i < NB; ++i) {
-      const double xi = I[i * LS + c] / L[i * LS + i];
-      I[i * LS + c] = xi;
-      for (int m0 = i + 1; m0 < NB; m0 += 8) {   // groups of 8, as above
-        const int b = m0 < NB - 8 ? m0 : NB - 8;
-        double lv[8], iv[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          lv[u] = L[(b + u) * LS + i];
-          iv[u] = I[(b + u) * LS + c];
-        }
-#pragma unroll
-        for (int u = 0; u < 8; ++u) iv[u] = fma(-(b + u >= m0 ? xi : 0.0), lv[u], iv[u]);
-#pragma unroll
-        for (int u = 0; u < 8; ++u) I[(b + u) * LS + c] = iv[u];
-      }
+    for (int u = 0; u < 16; ++u) {
+      const int c = 4 * u + c0;
+      L[r * LS + c] = (r < lim && c < lim) ? v[u] : (r == c ? 1.0 : 0.0);
     }
   }
   __syncthreads();
+  int bad = 0;   // (wave 0, uniform)
+  for (int J = 0; J < 4; ++J) {
+    const int c0 = SB * J;
+    if (t < 64) {   // wave 0: factor and invert the 16 x 16 diagonal sub-block (lanes >= 16 mirror 0..15)
+      const int rr = t & 15;
+      double row[SB];
+#pragma unroll
+      for (int l = 0; l < SB; ++l) row[l] = L[(c0 + rr) * LS + c0 + l];
+#pragma unroll
+      for (int j = 0; j < SB; ++j) {
+        const double d = ppls_bcast(row[j], j);
+        if (!bad && !(d > 0.0 && d < INFINITY)) bad = c0 + j + 1;   // NaN fails too
+        const double sq = sqrt(d);
+        row[j] = rr > j ? row[j] / sq : (rr == j ? sq : row[j]);
+#pragma unroll
+        for (int l = j + 1; l < SB; ++l) {
+          const double clj = ppls_bcast(row[j], l);   // L[l][j], scaled
+          row[l] = fma(-((rr > j && l <= rr) ? row[j] : 0.0), clj, row[l]);
+        }
+      }
+      double x[SB];   // column rr of the sub-block's inverse
+#pragma unroll
+      for (int i = 0; i < SB; ++i) {
+        double sacc = i == rr ? 1.0 : 0.0;
+#pragma unroll
+        for (int m = 0; m < i; ++m) sacc = fma(-ppls_bcast(row[m], i), x[m], sacc);
+        x[i] = i >= rr ? sacc / ppls_bcast(row[i], i) : 0.0;
+      }
+      if (t < SB) {
+#pragma unroll
+        for (int l = 0; l < SB; ++l) {
+          if (l <= rr) L[(c0 + rr) * LS + c0 + l] = row[l];
+          I[(c0 + l) * LS + c0 + rr] = x[l];   // Li's diagonal sub-block, column rr
+        }
+      }
+    }
+    __syncthreads();
+    const int nr = NB - c0 - SB;   // rows below the sub-block
+    if (nr > 0) {
+      // panel: L[r][c0 + c] = sum_m A[r][c0 + m] Di[c][m] for r >= c0 + 16 (thread: a row, 4 columns)
+      double pv[4] = {0.0, 0.0, 0.0, 0.0};
+      const int r = c0 + SB + (t >> 2), cq = 4 * (t & 3);
+      const bool act = (t >> 2) < nr;
+      if (act) {
+        double arow[SB];
+#pragma unroll
+        for (int m = 0; m < SB; ++m) arow[m] = L[r * LS + c0 + m];
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+#pragma unroll
+          for (int m = 0; m < SB; ++m) pv[c] = fma(arow[m], I[(c0 + cq + c) * LS + c0 + m], pv[c]);
+      }
+      __syncthreads();
+      if (act)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) L[r * LS + c0 + cq + c] = pv[c];
+      __syncthreads();
+      // trailing update of the lower triangle: L[r][l] -= sum_m L[r][c0 + m] L[l][c0 + m]
+      for (int e = t; e < nr * nr; e += 256) {
+        const int ri = e / nr, li = e - ri * nr;
+        if (li <= ri) {
+          const int rA = c0 + SB + ri, lA = c0 + SB + li;
+          double sacc = 0.0;
+#pragma unroll
+          for (int m = 0; m < SB; ++m) sacc = fma(L[rA * LS + c0 + m], L[lA * LS + c0 + m], sacc);
+          L[rA * LS + lA] -= sacc;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  // off-diagonal sub-blocks of Li by levels: S = sum_{K=J}^{I-1} L_IK Li_KJ into Li's (J, I) block,
+  // then Li_IJ = -Li_II S
+  for (int dl = 1; dl < 4; ++dl) {
+    const int np = 4 - dl;
+    for (int e = t; e < np * 256; e += 256) {
+      const int J = e >> 8, Ib = J + dl, a = (e >> 4) & 15, b2 = e & 15;
+      double sacc = 0.0;
+      for (int K = J; K < Ib; ++K)
+#pragma unroll
+        for (int m = 0; m < SB; ++m) sacc = fma(L[(SB * Ib + a) * LS + SB * K + m], I[(SB * K + m) * LS + SB * J + b2], sacc);
+      I[(SB * J + a) * LS + SB * Ib + b2] = sacc;
+    }
+    __syncthreads();
+    for (int e = t; e < np * 256; e += 256) {
+      const int J = e >> 8, Ib = J + dl, a = (e >> 4) & 15, b2 = e & 15;
+      double sacc = 0.0;
+#pragma unroll
+      for (int m = 0; m < SB; ++m) sacc = fma(I[(SB * Ib + a) * LS + SB * Ib + m], I[(SB * J + m) * LS + SB * Ib + b2], sacc);
+      I[(SB * Ib + a) * LS + SB * J + b2] = -sacc;
+    }
+    __syncthreads();
+  }
   double* Lz = Li + ((int64_t)z * nb + k) * NB * NB;
   double* Tz = T + pp * z;
-  if (w0)
-    for (int c = 0; c < NB; ++c) {
-      const int r = t;
-      Lz[r + NB * c] = I[r * LS + c];
+  {
+    const int r = t & 63, c0 = t >> 6;
+#pragma unroll 4
+    for (int u = 0; u < 16; ++u) {
+      const int c = 4 * u + c0;
+      const double iv = r >= c ? I[r * LS + c] : 0.0;   // (the upper triangle held the level sums)
+      Lz[r + NB * c] = iv;
       if (r < lim && c < lim) {
         if (r >= c) Az[(o + r) + (int64_t)(o + c) * p] = L[r * LS + c];
-        Tz[(o + r) + (int64_t)(o + c) * p] = I[r * LS + c];
+        Tz[(o + r) + (int64_t)(o + c) * p] = iv;
       }
     }
+  }
   if (t == 0 && bad && info[z] == 0) info[z] = o + bad;
 }
 
-__global__ __launch_bounds__(64) void chol_diag_kernel(double* __restrict__ A, int p, int64_t pp, int k,
-                                                      double* __restrict__ Li, int nb, double* __restrict__ T,
-                                                      int* __restrict__ info) {
+__global__ __launch_bounds__(256) void chol_diag_kernel(double* __restrict__ A, int p, int64_t pp, int k,
+                                                       double* __restrict__ Li, int nb, double* __restrict__ T,
+                                                       int* __restrict__ info) {
   __shared__ double L[NB * (NB + 1)], I[NB * (NB + 1)];
   diag_block(A, p, pp, k, Li, nb, T, info, blockIdx.y, L, I);
 }
@@ -354,7 +404,7 @@ hipError_t ppls_spd_inverse_batched(double* A, int p, int a, double* work, int* 
   double* Li = work + (int64_t)a * pp;
   hipError_t e = hipMemsetAsync(info, 0, sizeof(int) * a, st);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(chol_diag_kernel, dim3(1, a), dim3(64), 0, st, A, p, pp, 0, Li, nb, T, info);
+  hipLaunchKernelGGL(chol_diag_kernel, dim3(1, a), dim3(256), 0, st, A, p, pp, 0, Li, nb, T, info);
   for (int k = 0; k + 1 < nb; ++k) {   // (update(k) also factors block k + 1)
     const int nt = nb - 1 - k;
     hipLaunchKernelGGL(chol_panel_kernel, dim3(nt, a), dim3(256), 0, st, A, p, pp, k, Li, nb);
