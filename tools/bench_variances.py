@@ -6,8 +6,8 @@ Data: the bench's synthetic simulC model generated on the device; the fit is a s
 PPLS_simult run (its Expectations feed variances).  Prints one JSON line: Gram kernel time and
 fp64 MFMA TFLOP/s (executed tile flops and the useful n p (p + 1) SYRK flops) against the 78.6 TF
 fp64 matrix peak, and the wall time of the whole variances call (Cxt pass, Gram, per-component
-p x p build + rocSOLVER inverse + copies), after one untimed call, for the Cholesky and the LU
-inverse alternately.
+p x p build + inverse + copies), after one untimed call, for the hand-written Cholesky inverse
+(var_chol 1), rocSOLVER's potrf/potri (2) and its LU (0) in turn.
 """
 import argparse
 import json
@@ -30,7 +30,7 @@ def main():
     ap.add_argument("--nsplit", type=int, default=0)
     ap.add_argument("--em-steps", type=int, default=3)
     ap.add_argument("--no-full", action="store_true", help="skip the whole variances call")
-    ap.add_argument("--chol", type=int, default=1, help="the arm variances_s reports: 1 Cholesky (default), 0 LU")
+    ap.add_argument("--chol", type=int, default=1, help="the arm variances_s reports: 1 Cholesky (default), 2 rocSOLVER Cholesky, 0 LU")
     ap.add_argument("--full-reps", type=int, default=3, help="timed whole calls per arm after one warm-up")
     args = ap.parse_args()
     from ppls_amd import Context
@@ -54,7 +54,7 @@ def main():
                tiles=tiles)
     if not args.no_full:
         est, ll, eout, _ = ctx.em_run(th0, args.em_steps, -np.inf, 0, want_eout=True, want_mu=True)
-        arms = {"chol": 1, "lu": 0}
+        arms = {"chol": 1, "chol_rocsolver": 2, "lu": 0}
         secs = {k: [] for k in arms}
         for rep in range(args.full_reps + 1):   # rep 0: warm-up (rocSOLVER/rocBLAS code objects, handle)
             for k, v in arms.items():
@@ -68,7 +68,7 @@ def main():
         ctx.set_option("var_chol", args.chol)
         for k in arms:
             out[f"variances_s_{k}"] = secs[k]
-        out["variances_s"] = float(np.median(secs["chol" if args.chol else "lu"]))
+        out["variances_s"] = float(np.median(secs[{1: "chol", 2: "chol_rocsolver", 0: "lu"}[args.chol]]))
     ctx.close()
     print(json.dumps(out), flush=True)
 
