@@ -3068,7 +3068,8 @@ int ppls_sweep_kernel(ppls_ctx* c, int r, char* buf, int len) {
     const bool rows64 = c->dots_rows ? c->dots_rows == 64 : sweep_rows(c) >= 32768;
     const int64_t wtiles = (sweep_rows(c) + (rows64 ? 63 : 31)) / (rows64 ? 64 : 32);
     const bool pair = c->dots_pair >= 0 ? c->dots_pair == 1 : wtiles < (int64_t)c->num_cus * 4 * (rows64 ? 2 : 3);
-    const int dma = c->dots_dma >= 0 ? c->dots_dma : (nt && !pair ? 2 : 1);
+    const bool dma_ok = (int64_t)(rows64 ? 64 : 32) * std::max(c->ldx, c->ldy) * (c->dtype ? 4 : 8) < ((int64_t)1 << 31);
+    const int dma = !dma_ok ? 0 : c->dots_dma >= 0 ? c->dots_dma : (nt && !pair ? 2 : 1);
     snprintf(k, sizeof k, "panel<%s,%d> (%s %d rows/%s + acc, %d chunks)", c->dtype ? "float" : "double", r,
              dma == 2 ? "dmadots nt" : dma ? "dmadots" : "mfmadots", rows64 ? 64 : 32, pair ? "wave pair" : "wave",
              a.grid);

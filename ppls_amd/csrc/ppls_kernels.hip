@@ -2983,7 +2983,9 @@ hipError_t launch_panel_t(const PplsSweepArgs* a, const T* X, const T* Y, double
     // X tiles by LDS-DMA (round 5), non-temporal where the data exceed the MALL and one wave owns a
     // row tile (full C5: 7.40 -> 7.29 ms per iteration; the C5 share's wave pairs: nt 1.5 % slower;
     // profiles/r5_dots_dma_ab_c5.txt, r5_dots_dma_ab_c5s.txt); option dots_dma forces a form (0: VGPR staging)
-    const int dma = a->dots_dma >= 0 ? a->dots_dma : (a->nt && ks == 1 ? 2 : 1);
+    // (the LDS-DMA form addresses a row tile by 32-bit byte offsets: rows of up to 2^31 / rb bytes)
+    const bool dma_ok = (int64_t)rb * (a->ldx > a->ldy ? a->ldx : a->ldy) * (int64_t)sizeof(T) < ((int64_t)1 << 31);
+    const int dma = !dma_ok ? 0 : a->dots_dma >= 0 ? a->dots_dma : (a->nt && ks == 1 ? 2 : 1);
     // (also measured: the B operands prefetched a tile ahead, 256 VGPRs -- no faster, 7.70-7.88 vs
     // 7.69-7.78 ms; profiles/r2_c5_dots_rows.txt)
 #define PPLS_LAUNCH_DOTS(NBV, KSV)                                                                   \
