@@ -117,7 +117,11 @@ const char* ppls_last_error(const ppls_ctx* ctx);
  *       "dots_dma" (panel sweep dots: how X tiles reach the MFMAs: -1 auto, 0 16-B loads into VGPRs +
  *                   LDS transpose, 1 LDS-DMA, 2 LDS-DMA with non-temporal loads; auto = 2 when the
  *                   data exceed the MALL and one wave owns a row tile, else 1; all forms give the
- *                   same results bit for bit) */
+ *                   same results bit for bit; rows wider than 2^31 / 64 bytes always take 0),
+ *       "var_chol" (ppls_variances' inverse of the observed information: 1, default, the
+ *                   hand-written batched Cholesky + inverse (ppls_linalg.hip); 2 rocSOLVER
+ *                   potrf/potri; 0 rocSOLVER LU getrf/getri; a matrix that is not positive definite
+ *                   sends the batch to LU, as R's solve() would) */
 int ppls_set_option(ppls_ctx* ctx, const char* key, int64_t value);
 
 /* ---- multi-GPU: samples are sharded over ranks; one RCCL all-reduce per EM iteration ---- */
