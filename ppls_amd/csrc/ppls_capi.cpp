@@ -2640,11 +2640,19 @@ int ppls_variances(ppls_ctx* c, const double* mu, const double* Cdiag, double si
   // getrf + getri, from the untouched M.  Either inverse is backward stable: they agree to ~kappa eps.
   std::vector<rocblas_int> inf(a, 0);
   bool chol = c->var_chol != 0;
-  if (chol && c->var_chol == 1) {
+  int chol_mode = c->var_chol;
+  if (chol_mode == 1) {   // the hand-written inverse needs a p^2 scratch per matrix more than rocSOLVER
+    const size_t need = sizeof(double) * (pp * (size_t)a + (size_t)ppls_spd_inverse_work(p, a));
+    if (hipMalloc((void**)&dMc, need) != hipSuccess) {
+      (void)hipGetLastError();   // (clear it) not enough HBM: rocSOLVER's in-place potrf/potri instead
+      dMc = nullptr;
+      chol_mode = 2;
+    }
+  }
+  if (chol && chol_mode == 1) {
     // hand-written (ppls_linalg.hip): blocked Cholesky of every matrix of the batch in the same
-    // launches, then T = L^-1 and T'T -- 3 nb + nb + 1 launches (nb = p / 64) where rocSOLVER's
-    // potrf + potri took 1,400 (profiles/r4_variances_c3_timeline.txt)
-    VRC(dalloc(c, &dMc, pp * (size_t)a + (size_t)ppls_spd_inverse_work(p, a)));
+    // launches, then T = L^-1 and T'T -- 3 nb launches (nb = p / 64) where rocSOLVER's potrf + potri
+    // took 1,400 (profiles/r4_variances_c3_timeline.txt)
     VCHK(hipMemcpyAsync(dMc, dM, sizeof(double) * pp * a, hipMemcpyDeviceToDevice, c->stream));
     VCHK(ppls_launch_negate(dMc, (int64_t)pp * a, c->stream));
     VCHK(ppls_spd_inverse_batched(dMc, p, a, dMc + pp * (size_t)a, (int*)info, c->stream));
