@@ -2540,7 +2540,9 @@ int ppls_variances(ppls_ctx* c, const double* mu, const double* Cdiag, double si
   double *dmu = nullptr, *dpart = nullptr, *dS = nullptr, *dG = nullptr, *dM = nullptr, *dv = nullptr, *dMc = nullptr;
   double *dexp = nullptr, *dstar = nullptr, *dse = nullptr;
   rocblas_int *ipiv = nullptr, *info = nullptr;
+  hipEvent_t evS = nullptr;
   auto done = [&](int code) {
+    if (evS) (void)hipEventDestroy(evS);
     dfree(dmu); dfree(dpart); dfree(dS); dfree(dG); dfree(dM); dfree(dMc); dfree(dv); dfree(dexp); dfree(dstar); dfree(dse);
     if (ipiv) (void)hipFree(ipiv);
     if (info) (void)hipFree(info);
@@ -2577,14 +2579,8 @@ int ppls_variances(ppls_ctx* c, const double* mu, const double* Cdiag, double si
   VRC(allreduce(c, dS, (size_t)sld + a));
   std::vector<double> S((size_t)sld + a);
   VCHK(hipMemcpyAsync(S.data(), dS, sizeof(double) * S.size(), hipMemcpyDeviceToHost, c->stream));
-  VCHK(hipStreamSynchronize(c->stream));
-  std::vector<double> Sp((size_t)p * a);   // t(data) %*% mu (p x a, column-major)
-  for (int k = 0; k < a; ++k)
-    for (int i = 0; i < p; ++i) Sp[(size_t)k * p + i] = S[(size_t)k * ld + i];
-  for (int k = 0; k < a; ++k) mu2[k] = S[(size_t)sld + k];
-  // W = orth(t(data) %*% mu, type = "SVD") (:831-832)
-  if ((rc = host_orth(Sp.data(), p, a, PPLS_ORTH_SVD, W)))
-    return done(fail(c, rc, "orth(t(data) %%*%% mu): rank-deficient"));
+  VCHK(hipEventCreateWithFlags(&evS, hipEventDisableTiming));
+  VCHK(hipEventRecord(evS, c->stream));   // the host's orth below overlaps the Gram
   // ---- G = D'D on MFMA, split over row ranges, all-reduced -- or, when the cross-product form
   // has formed S = [X Y]'[X Y] for this data (ppls_xprod.hip), its X'X or Y'Y block as it stands
   // (already summed over ranks; symmetric, so its row-major block is the column-major G) ------
@@ -2601,6 +2597,14 @@ int ppls_variances(ppls_ctx* c, const double* mu, const double* Cdiag, double si
     }
     VRC(allreduce(c, dG, pp));
   }
+  VCHK(hipEventSynchronize(evS));
+  std::vector<double> Sp((size_t)p * a);   // t(data) %*% mu (p x a, column-major)
+  for (int k = 0; k < a; ++k)
+    for (int i = 0; i < p; ++i) Sp[(size_t)k * p + i] = S[(size_t)k * ld + i];
+  for (int k = 0; k < a; ++k) mu2[k] = S[(size_t)sld + k];
+  // W = orth(t(data) %*% mu, type = "SVD") (:831-832)
+  if ((rc = host_orth(Sp.data(), p, a, PPLS_ORTH_SVD, W)))
+    return done(fail(c, rc, "orth(t(data) %%*%% mu): rank-deficient"));
   // ---- per component: M = B_exp - SSt_exp, varMatrix = -solve(M), seLoad --------------------
   if (!c->blas) {
     if (rocblas_create_handle(&c->blas) != rocblas_status_success) return done(fail(c, PPLS_E_HIP, "rocblas_create_handle failed"));
