@@ -154,6 +154,8 @@ def test_dots_wave_pair_equals_single_wave(dtype, n, p, q, r, grid):
     (0, 333, 40, 20, 16, 64, -1, 2),       # r = 16, fp64, pairs, looping grid
     (1, 5000, 31, 2, 2, 32, 0, 2),         # one column tile per matrix
     (1, 130, 200, 300, 5, 64, 0, 0),       # Y wider than X
+    (1, 3, 70, 40, 2, 0, -1, 0),           # 3 rows: one partial row tile
+    (0, 1, 33, 17, 1, 64, 0, 0),           # 1 row
 ])
 def test_dots_dma_equals_register_staging(dtype, n, p, q, r, rows, pair, grid):
     """ppls_panel_dmadots_kernel (option dots_dma = 1, or 2 with non-temporal loads: X tiles HBM -> LDS
@@ -173,6 +175,7 @@ def test_dots_dma_equals_register_staging(dtype, n, p, q, r, rows, pair, grid):
             c.set_option("dots_rows", rows)
             c.set_option("dots_pair", pair)
             c.set_option("dots_dma", dma)
+            c.set_option("sweep", 3)   # the panel sweep even where the split sweep would be chosen
             c.set_data(X, Y)
             assert ["(mfmadots ", "(dmadots ", "(dmadots nt "][dma] in c.sweep_kernel(r)
             e = c.estep(_theta(th0))

@@ -95,3 +95,16 @@ def test_spd_inverse_faster_than_rocsolver(ctx):
     _check(inv[0], A[0], np.linalg.cond(A0))
     print(f"spd inverse {a} x {p}: hand-written {t1:.2f} ms, rocSOLVER {t2:.2f} ms")
     assert t1 < t2
+
+
+def test_spd_inverse_random_sizes(ctx):
+    """Random sizes and batch counts (partial last blocks of every width, batches of 1 to 6)."""
+    rng = np.random.default_rng(8)
+    for _ in range(12):
+        p = int(rng.integers(1, 400))
+        a = int(rng.integers(1, 7))
+        A = np.stack([_spd(rng, p, cond=10.0 ** rng.uniform(0, 6)) for _ in range(a)])
+        inv, info, _ = ctx.spd_inverse(A, 1)
+        assert (info == 0).all(), (p, a, info)
+        for z in range(a):
+            _check(inv[z], A[z], np.linalg.cond(A[z]))
