@@ -548,8 +548,7 @@ def main():
         # rocprofv3 PMC counters (SQ_VALU_MFMA_BUSY_CYCLES, SQ_ACTIVE_INST_VALU, GRBM_GUI_ACTIVE) of the
         # sweep kernel(s) at this workload, committed under profiles/ (readbacks, see their source)
         if info["variant"] == "panel":
-            dots = "panel_dmadots" if "dmadots" in roofline["kernel"] else "panel_mfmadots"
-            roofline["counters"] = {k: load_compute_counters(wl, k) for k in (dots, "panel_acc")}
+            roofline["counters"] = {k: load_compute_counters(wl, k) for k in ("panel_mfmadots", "panel_acc")}
         else:
             roofline["counters"] = {"sweep_split": load_compute_counters(wl, "sweep_split")}
         if xp is not None:

@@ -114,10 +114,6 @@ const char* ppls_last_error(const ppls_ctx* ctx);
  *       "dots_rows" (panel sweep dots: rows per wave, 0 auto (64 from 32768 rows, else 32), 32, 64),
  *       "dots_pair" (panel sweep dots: a wave pair per row tile, -1 auto (when row tiles are fewer
  *                    than resident wave slots), 0, 1),
- *       "dots_dma" (panel sweep dots: how X tiles reach the MFMAs: -1 auto, 0 16-B loads into VGPRs +
- *                   LDS transpose, 1 LDS-DMA, 2 LDS-DMA with non-temporal loads; auto = 2 when the
- *                   data exceed the MALL and one wave owns a row tile, else 1; all forms give the
- *                   same results bit for bit; rows wider than 2^31 / 64 bytes always take 0),
  *       "var_chol" (ppls_variances' inverse of the observed information: 1, default, the
  *                   hand-written batched Cholesky + inverse (ppls_linalg.hip); 2 rocSOLVER
  *                   potrf/potri; 0 rocSOLVER LU getrf/getri; a matrix that is not positive definite

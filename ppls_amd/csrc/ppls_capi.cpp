@@ -38,7 +38,6 @@ struct ppls_ctx {
   int pipe_opt = 1;     // split kernel: software-pipelined order
   int dots_rows = 0;   // panel dots rows per wave: 0 auto, 32, 64 (tests of both forms)
   int dots_pair = -1;  // panel dots wave pair per row tile: -1 auto, 0, 1
-  int dots_dma = -1;   // panel dots X tiles: -1 auto, 0 VGPR staging, 1 LDS-DMA, 2 LDS-DMA nt
   int team_rows = 0;   // finalize polar team: rows of S per member (0: PPLS_TEAM_ROWS)
   int polar1 = 1;   // finalize polar: Cholesky-QR1 fast path when kappa(X'mu) <= PPLS_POLAR1_KAPPA
   int polar1_kappa = 0;   // its bound on ||R1||_F ||R1^-1||_F (0 = min(8 r, 40))
@@ -410,7 +409,6 @@ int sweep_plan(ppls_ctx* c, int r, PplsSweepArgs* a) {
   a->num_cus = c->num_cus;
   a->dots_rows = c->dots_rows;
   a->dots_pair = c->dots_pair;
-  a->dots_dma = c->dots_dma;
   if (c->sweep_mode != 3 && !c->dtype && nsplit > 0) {
     a->ns = nsplit;
     a->pipe = c->pipe_opt;
@@ -1172,9 +1170,6 @@ int ppls_set_option(ppls_ctx* c, const char* key, int64_t value) {
   } else if (!strcmp(key, "dots_rows")) {
     if (value != 0 && value != 32 && value != 64) return fail(c, PPLS_E_ARG, "dots_rows must be 0 (auto), 32 or 64");
     c->dots_rows = (int)value;
-  } else if (!strcmp(key, "dots_dma")) {
-    if (value < -1 || value > 2) return fail(c, PPLS_E_ARG, "dots_dma must be -1 (auto), 0, 1 or 2 (non-temporal)");
-    c->dots_dma = (int)value;
   } else if (!strcmp(key, "dots_pair")) {
     if (value < -1 || value > 1) return fail(c, PPLS_E_ARG, "dots_pair must be -1 (auto), 0 or 1");
     c->dots_pair = (int)value;
@@ -2808,7 +2803,7 @@ int ppls_scores(ppls_ctx* c, const double* W, const double* C, int k, double* T,
   memset(&a, 0, sizeof a);
   a.X = c->X; a.Y = c->Y; a.n_local = c->n_local; a.p = c->p; a.q = c->q; a.ldx = c->ldx; a.ldy = c->ldy;
   a.Wp = c->W[0]; a.Cp = c->C[0]; a.sc = c->sc[0]; a.mu = c->mu; a.write_mu = 1; a.r = k;
-  a.num_cus = c->num_cus; a.dots_rows = c->dots_rows; a.dots_pair = c->dots_pair; a.dots_dma = c->dots_dma;
+  a.num_cus = c->num_cus; a.dots_rows = c->dots_rows; a.dots_pair = c->dots_pair;
   HIPCHK(c, ppls_launch_panel_dots(&a, c->dtype, c->Z, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   const size_t blk = sizeof(double) * (size_t)c->n_local * k;
@@ -3080,11 +3075,8 @@ int ppls_sweep_kernel(ppls_ctx* c, int r, char* buf, int len) {
     const bool rows64 = c->dots_rows ? c->dots_rows == 64 : sweep_rows(c) >= 32768;
     const int64_t wtiles = (sweep_rows(c) + (rows64 ? 63 : 31)) / (rows64 ? 64 : 32);
     const bool pair = c->dots_pair >= 0 ? c->dots_pair == 1 : wtiles < (int64_t)c->num_cus * 4 * (rows64 ? 2 : 3);
-    const bool dma_ok = (int64_t)(rows64 ? 64 : 32) * std::max(c->ldx, c->ldy) * (c->dtype ? 4 : 8) < ((int64_t)1 << 31);
-    const int dma = !dma_ok ? 0 : c->dots_dma >= 0 ? c->dots_dma : (nt && !pair ? 2 : 1);
-    snprintf(k, sizeof k, "panel<%s,%d> (%s %d rows/%s + acc, %d chunks)", c->dtype ? "float" : "double", r,
-             dma == 2 ? "dmadots nt" : dma ? "dmadots" : "mfmadots", rows64 ? 64 : 32, pair ? "wave pair" : "wave",
-             a.grid);
+    snprintf(k, sizeof k, "panel<%s,%d> (mfmadots %d rows/%s + acc, %d chunks)", c->dtype ? "float" : "double", r,
+             rows64 ? 64 : 32, pair ? "wave pair" : "wave", a.grid);
   }
   snprintf(buf, (size_t)len, "%s%s", k, plan == 3 && nt ? " nt" : "");
   return PPLS_OK;

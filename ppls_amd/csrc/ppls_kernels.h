@@ -33,7 +33,6 @@ struct PplsSweepArgs {
   int dots_grid;         // panel dots workgroups (0 = enough for every row tile, capped)
   int dots_rows;         // panel dots rows per wave: 0 auto (64 from 32768 rows, else 32), 32, 64
   int dots_pair;         // panel dots wave pair per row tile: -1 auto (when tiles < wave slots), 0, 1
-  int dots_dma;          // panel dots X tiles: -1 auto, 0 VGPR staging, 1 LDS-DMA, 2 LDS-DMA non-temporal
   int dots_only;         // panel: the dots pass only (Z and mu; scores)
   int num_cus;           // compute units of the device (panel dots: wave pairs on small shards)
   const int* stop;       // device stop flag (em_run's convergence test) or nullptr: kernels exit if set

@@ -849,225 +849,6 @@ __global__ __launch_bounds__(256) void ppls_panel_mfmadots_kernel(
   }
 }
 
-// ---- LDS-DMA dots (round 5)
-// One global_load_lds_dwordx4: 64 lanes x 16 B from sbase + voff (wave-uniform base, per-lane byte
-// offset) into LDS at the wave-uniform byte address lds_dst + 16 lane (M0 is set and restored inside the statement; the compiler neither
-// sees nor counts this load: the caller waits for it with its own s_waitcnt vmcnt).
-template <bool NT = false>
-__device__ __forceinline__ void ppls_glds16(const void* sbase, unsigned voff, unsigned lds_dst) {
-  unsigned keep;
-  if constexpr (NT)   // non-temporal: the once-read stream
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2 nt\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep) : "v"(voff), "s"(sbase), "s"(lds_dst) : "memory");
-  else
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep) : "v"(voff), "s"(sbase), "s"(lds_dst) : "memory");
-}
-
-typedef double ppls_d2v __attribute__((ext_vector_type(2)));
-// A 16-B load (wave-uniform base + per-lane byte offset) the compiler does not count (so its waits
-// do not drain the LDS-DMA loads issued after it); the destination is valid only after the
-// caller's ppls_wait_b (which names it).
-__device__ __forceinline__ ppls_d2v ppls_load16_uncounted(const void* sbase, unsigned voff) {
-  ppls_d2v v;
-  asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(v) : "v"(voff), "s"(sbase) : "memory");
-  return v;
-}
-
-// s_waitcnt vmcnt(N) that also names the uncounted B registers (read-write), so no use of them is
-// scheduled before it.  N: the vector-memory operations allowed to stay in flight.
-template <int NBW, int N>
-__device__ __forceinline__ void ppls_wait_b(ppls_d2v (&b)[NBW]) {
-  static_assert(NBW == 2 || NBW == 4, "B registers per tile");
-  static_assert(N == 0 || N == 4 || N == 8, "counts of the LDS-DMA pieces per tile");
-#define PPLS_WB2(S) asm volatile("s_waitcnt vmcnt(" S ")" : "+v"(b[0]), "+v"(b[1]) :: "memory")
-#define PPLS_WB4(S) asm volatile("s_waitcnt vmcnt(" S ")" : "+v"(b[0]), "+v"(b[1]), "+v"(b[2]), "+v"(b[3]) :: "memory")
-  if constexpr (NBW == 2) {
-    if constexpr (N == 0) PPLS_WB2("0");
-    else if constexpr (N == 4) PPLS_WB2("4");
-    else PPLS_WB2("8");
-  } else {
-    if constexpr (N == 0) PPLS_WB4("0");
-    else if constexpr (N == 4) PPLS_WB4("4");
-    else PPLS_WB4("8");
-  }
-#undef PPLS_WB2
-#undef PPLS_WB4
-}
-
-// The MFMA dots of ppls_panel_mfmadots_kernel (same tiles, k order, B layout, lane map, epilogue
-// and wave pairs: the dot sums are the same bit for bit), with the X tiles moved HBM -> LDS by
-// LDS-DMA instead of 16-B loads into VGPRs + ds_write.  Each wave owns two tile buffers; a tile's A
-// operands are read into VGPRs as soon as it lands (one ds_read_b128 per two MFMA steps), which frees
-// its buffer for the tile after next: TWO tiles of X stream in while the MFMAs of the third run
-// (the register-staged form holds one: its VGPRs cap the bytes in flight).  The DMA image is
-// lane-linear (64 lanes x 16 B = 8 rows x 128 B per piece); the 16-B chunk c of tile row i sits
-// in slot c ^ ((i >> 1) & 7) (the source address is swizzled), so the 16 rows one ds_read_b128
-// spans fill all 64 banks.  The B operands are loaded a tile ahead, uncounted by the compiler; the
-// waits are explicit: at tile t, glds(t) and B(t) are complete while glds(t + 1) stays in flight.
-template <typename T, int R, int NB, int KS, bool NTX>
-__global__ __launch_bounds__(256, 2) void ppls_panel_dmadots_kernel(
-    const T* __restrict__ X, const T* __restrict__ Y, int64_t n, int ldx, int ldy, int px, int py,
-    const double* __restrict__ Wt, const double* __restrict__ Ct, const PplsScalars* __restrict__ sc,
-    double* __restrict__ Z, double* __restrict__ mu,
-    const int* __restrict__ stop) {
-  if (stop && *stop) return;   // em_run converged earlier (device stop flag)
-  typedef double d4 __attribute__((ext_vector_type(4)));
-  constexpr int ES = (int)sizeof(T);
-  constexpr int KT = 128 / ES;        // columns per tile
-  constexpr int KQ = KT / 4;          // MFMA steps per tile (columns per lane group)
-  constexpr int RB = 16 * NB;         // rows per wave
-  constexpr int NL = RB / 8;          // LDS-DMA pieces per tile (8 rows x 128 B each)
-  constexpr int TB = RB * 128;        // tile bytes
-  constexpr int NBW = KQ / 2;         // 16-B B loads per lane per tile
-  constexpr int NH = KQ * ES / 16;    // ds_read_b128 per 16-row block per tile
-  constexpr int V4 = 4 * R;
-  static_assert(R <= 16, "one 16-wide MFMA tile of components");
-  static_assert(2 * NB * 4 * 64 * 8 <= 2 * TB, "a wave's dot sums fit its tile buffers");
-  __shared__ __attribute__((aligned(16))) char lds[4 * 2 * TB];
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int i16 = lane & 15, kq = lane >> 4;
-  const int lrow = lane >> 3, lchunk = lane & 7;
-  const int comp = i16 < R ? i16 : 0;
-  const double al = sc->alpha[comp], be = sc->beta[comp], ga = sc->gamma[comp], de = sc->delta[comp];
-  static_assert(KS == 1 || KS == 2, "one wave or a wave pair per row tile");
-  constexpr int TPW = 4 / KS;
-  const int part = wave % KS;
-  const int64_t ntiles = (n + RB - 1) / RB;
-  char* wbuf = lds + wave * 2 * TB;   // this wave's two tile buffers
-  const unsigned wbuf_lds = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)wbuf;
-  for (int64_t tb = (int64_t)blockIdx.x * TPW; tb < ntiles; tb += (int64_t)gridDim.x * TPW) {
-    const int64_t t = tb + wave / KS;
-    const bool active = t < ntiles;
-    const int64_t row0 = t * RB;
-    d4 res[2][NB];
-    if (active) {
-#pragma unroll
-    for (int mat = 0; mat < 2; ++mat) {
-      const T* M = mat ? Y : X;
-      const int ld = mat ? ldy : ldx, pc = mat ? py : px;
-      const double* Wm = mat ? Ct : Wt;
-      d4 acc[NB];
-#pragma unroll
-      for (int bk = 0; bk < NB; ++bk) acc[bk] = d4{0.0, 0.0, 0.0, 0.0};
-      // per-lane byte offsets from the row tile's base (loop-invariant; rows past n clamped)
-      unsigned xoff[NL];
-#pragma unroll
-      for (int u = 0; u < NL; ++u) {
-        const int lr = lrow + 8 * u;   // tile row of this lane's piece-u chunk
-        const int64_t rr = row0 + lr < n ? lr : n - 1 - row0;
-        xoff[u] = (unsigned)((rr * ld + (lchunk ^ ((lr >> 1) & 7)) * (16 / ES)) * ES);
-      }
-      const T* xbase = M + row0 * ld;   // wave-uniform
-      const int ntc = (pc + KT - 1) / KT;
-      const int tc0 = ntc * part / KS, tc1 = ntc * (part + 1) / KS;
-      const unsigned boff = (unsigned)(((int64_t)kq * KQ * 16 + 2 * i16) * 8);   // pair layout (transpose kernel)
-      auto issue_x = [&](int tc, int buf) {   // tile tc -> buffer buf (tc & 1 but for re-reads)
-        const unsigned dst = wbuf_lds + (unsigned)((buf & 1) * TB);
-        const T* sb = xbase + (int64_t)tc * KT;
-#pragma unroll
-        for (int u = 0; u < NL; ++u) ppls_glds16<NTX>(sb, xoff[u], dst + 1024u * u);
-      };
-      auto issue_b = [&](int tc, ppls_d2v (&b)[NBW]) {
-        const double* wb = Wm + (int64_t)tc * KT * 16;
-#pragma unroll
-        for (int s = 0; s < NBW; ++s) b[s] = ppls_load16_uncounted(wb, boff + 256u * s);
-      };
-      // tile tc: its A operands out of LDS (freeing the buffer), the next tile's B and the tile
-      // after next's X issued, then the MFMAs.  Every step issues the same loads (past the last
-      // tile they re-read it: B into the idle registers, X into the idle buffer), so every wait is
-      // the same vmcnt(NL) -- no branch around a wait, whose register merges would make the
-      // compiler copy B registers before their loads land.
-      auto step = [&](int tc, ppls_d2v (&bc)[NBW], ppls_d2v (&bn)[NBW]) {
-        ppls_wait_b<NBW, NL>(bc);   // glds(tc) and B(tc) done; glds(tc + 1) stays in flight
-        const char* buf = wbuf + (tc & 1) * TB;
-        float4 av[NB][NH];
-#pragma unroll
-        for (int bk = 0; bk < NB; ++bk) {
-          const int row = 16 * bk + i16;
-#pragma unroll
-          for (int h = 0; h < NH; ++h) {
-            const int c = kq * NH + h;
-            av[bk][h] = *(const float4*)(buf + row * 128 + ((c ^ ((row >> 1) & 7)) << 4));
-          }
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the buffer is free again
-        issue_b(tc + 1 < tc1 ? tc + 1 : tc1 - 1, bn);
-        issue_x(tc + 2 < tc1 ? tc + 2 : tc, tc);
-#pragma unroll
-        for (int bk = 0; bk < NB; ++bk) {
-          const T* a = (const T*)&av[bk][0];
-#pragma unroll
-          for (int s = 0; s < KQ; ++s) {
-            const double bw = (s & 1) ? bc[s >> 1].y : bc[s >> 1].x;
-            acc[bk] = __builtin_amdgcn_mfma_f64_16x16x4f64((double)a[s], bw, acc[bk], 0, 0, 0);
-          }
-        }
-      };
-      if (tc0 < tc1) {
-        ppls_d2v ba[NBW], bb[NBW];
-        issue_b(tc0, ba);
-        issue_x(tc0, tc0);
-        issue_x(tc0 + 1 < tc1 ? tc0 + 1 : tc0, tc0 + 1);
-        int tc = tc0;
-        for (; tc + 1 < tc1; tc += 2) {
-          step(tc, ba, bb);
-          step(tc + 1, bb, ba);
-        }
-        if (tc < tc1) step(tc, ba, bb);
-        // the re-reads past the last tile land before the registers / buffers are reused
-        ppls_wait_b<NBW, 0>(ba);
-        ppls_wait_b<NBW, 0>(bb);
-      }
-#pragma unroll
-      for (int bk = 0; bk < NB; ++bk) res[mat][bk] = acc[bk];
-    }
-    }   // active
-    if constexpr (KS == 2) {
-      double* cb = (double*)(lds + (wave | 1) * 2 * TB);
-      if (active && part == 1) {
-#pragma unroll
-        for (int mat = 0; mat < 2; ++mat)
-#pragma unroll
-          for (int bk = 0; bk < NB; ++bk)
-#pragma unroll
-            for (int reg = 0; reg < 4; ++reg) cb[((mat * NB + bk) * 4 + reg) * 64 + lane] = res[mat][bk][reg];
-      }
-      __syncthreads();
-      if (active && part == 0) {
-#pragma unroll
-        for (int mat = 0; mat < 2; ++mat)
-#pragma unroll
-          for (int bk = 0; bk < NB; ++bk)
-#pragma unroll
-            for (int reg = 0; reg < 4; ++reg) res[mat][bk][reg] += cb[((mat * NB + bk) * 4 + reg) * 64 + lane];
-      }
-      __syncthreads();
-    }
-    if (active && part == 0 && i16 < R) {
-#pragma unroll
-      for (int blk = 0; blk < NB; ++blk)
-#pragma unroll
-        for (int reg = 0; reg < 4; ++reg) {
-          const int64_t row = row0 + 16 * blk + kq + 4 * reg;
-          if (row >= n) continue;
-          const double a = res[0][blk][reg], bb = res[1][blk][reg];
-          const double mt = al * a + be * bb, mu_u = ga * a + de * bb;
-          double* zr = Z + row * V4;
-          zr[i16] = a;
-          zr[R + i16] = bb;
-          zr[2 * R + i16] = mt;
-          zr[3 * R + i16] = mu_u;
-          if (mu) {
-            mu[(int64_t)i16 * n + row] = mt;
-            mu[(int64_t)(R + i16) * n + row] = mu_u;
-          }
-        }
-    }
-  }
-}
-
 // W (ldx x r, column-major) -> Wt (ldxp x rs: rows >= ldx and columns >= r zero, pair layout below); C alike.
 __global__ void ppls_transpose_wc_kernel(const double* __restrict__ W, const double* __restrict__ C,
                                          int ldx, int ldy, int ldxp, int ldyp, int r, int rs, double* __restrict__ Wt,
@@ -2980,26 +2761,13 @@ hipError_t launch_panel_t(const PplsSweepArgs* a, const T* X, const T* Y, double
     // the grid option (dots_grid) forces a smaller grid: tests of the grid-stride loop
     const int mblocks = (int)(a->dots_grid > 0 && a->dots_grid < wgs ? a->dots_grid : wgs < 16384 ? wgs : 16384);
     double* mu_out = a->write_mu ? a->mu : nullptr;
-    // X tiles by LDS-DMA (round 5), non-temporal where the data exceed the MALL and one wave owns a
-    // row tile (full C5: 7.40 -> 7.29 ms per iteration; the C5 share's wave pairs: nt 1.5 % slower;
-    // profiles/r5_dots_dma_ab_c5.txt, r5_dots_dma_ab_c5s.txt); option dots_dma forces a form (0: VGPR staging)
-    // (the LDS-DMA form addresses a row tile by 32-bit byte offsets: rows of up to 2^31 / rb bytes)
-    const bool dma_ok = (int64_t)rb * (a->ldx > a->ldy ? a->ldx : a->ldy) * (int64_t)sizeof(T) < ((int64_t)1 << 31);
-    const int dma = !dma_ok ? 0 : a->dots_dma >= 0 ? a->dots_dma : (a->nt && ks == 1 ? 2 : 1);
     // (also measured: the B operands prefetched a tile ahead, 256 VGPRs -- no faster, 7.70-7.88 vs
-    // 7.69-7.78 ms; profiles/r2_c5_dots_rows.txt)
+    // 7.69-7.78 ms; profiles/r2_c5_dots_rows.txt.  Round 5: X tiles by LDS-DMA, two in flight per
+    // wave, 1.5 % faster at C5 -- removed: its uncounted inline-asm B loads were copied by the register
+    // allocator before they landed in some instantiations)
 #define PPLS_LAUNCH_DOTS(NBV, KSV)                                                                   \
-  do {                                                                                              \
-    if (dma == 2)                                                                                   \
-      hipLaunchKernelGGL((ppls_panel_dmadots_kernel<T, R, NBV, KSV, true>), dim3(mblocks), dim3(256), 0, st, \
-                         X, Y, a->n_local, a->ldx, a->ldy, a->p, a->q, Wt, Ct, a->sc, Z, mu_out, a->stop); \
-    else if (dma)                                                                                   \
-      hipLaunchKernelGGL((ppls_panel_dmadots_kernel<T, R, NBV, KSV, false>), dim3(mblocks), dim3(256), 0, st, \
-                         X, Y, a->n_local, a->ldx, a->ldy, a->p, a->q, Wt, Ct, a->sc, Z, mu_out, a->stop); \
-    else                                                                                            \
-      hipLaunchKernelGGL((ppls_panel_mfmadots_kernel<T, R, NBV, KSV>), dim3(mblocks), dim3(256), 0, st, X, \
-                         Y, a->n_local, a->ldx, a->ldy, a->p, a->q, Wt, Ct, a->sc, Z, mu_out, a->stop);  \
-  } while (0)
+  hipLaunchKernelGGL((ppls_panel_mfmadots_kernel<T, R, NBV, KSV>), dim3(mblocks), dim3(256), 0, st, X, Y, \
+                     a->n_local, a->ldx, a->ldy, a->p, a->q, Wt, Ct, a->sc, Z, mu_out, a->stop)
     if (rb == 64 && ks == 2) PPLS_LAUNCH_DOTS(4, 2);
     else if (rb == 64) PPLS_LAUNCH_DOTS(4, 1);
     else if (ks == 2) PPLS_LAUNCH_DOTS(2, 2);

@@ -145,47 +145,3 @@ def test_dots_wave_pair_equals_single_wave(dtype, n, p, q, r, grid):
     assert np.abs(mus[0][0] - mus[1][0]).max() < 1e-13 * scale
     assert np.abs(mus[0][1] - mus[1][1]).max() < 1e-13 * scale
 
-
-@pytest.mark.parametrize("dtype,n,p,q,r,rows,pair,grid", [
-    (1, 2000, 1500, 90, 10, 0, -1, 0),     # 32-row waves, wave pairs
-    (1, 2000, 1500, 90, 10, 64, 0, 0),     # 64-row waves, one wave per tile
-    (1, 701, 65, 33, 3, 64, -1, 3),        # ragged rows, pairs, looping grid
-    (0, 900, 2300, 17, 9, 0, 0, 0),        # fp64 storage: 16-column tiles
-    (0, 333, 40, 20, 16, 64, -1, 2),       # r = 16, fp64, pairs, looping grid
-    (1, 5000, 31, 2, 2, 32, 0, 2),         # one column tile per matrix
-    (1, 130, 200, 300, 5, 64, 0, 0),       # Y wider than X
-    (1, 3, 70, 40, 2, 0, -1, 0),           # 3 rows: one partial row tile
-    (0, 1, 33, 17, 1, 64, 0, 0),           # 1 row
-])
-def test_dots_dma_equals_register_staging(dtype, n, p, q, r, rows, pair, grid):
-    """ppls_panel_dmadots_kernel (option dots_dma = 1, or 2 with non-temporal loads: X tiles HBM -> LDS
-    by LDS-DMA, two tiles in flight per wave) multiplies the same tiles in the same order as
-    ppls_panel_mfmadots_kernel (dots_dma = 0, VGPR staging): mu and a whole EM step are equal bit for
-    bit, and mu matches the oracle's E-step."""
-    from ppls_amd import Context
-    X, Y, th0 = make_problem(n, p, q, r, seed=7 * n + p)
-    if dtype:
-        X, Y = _round32(X), _round32(Y)
-    out = []
-    for dma in (0, 1, 2):
-        with Context(0) as c:
-            c.set_option("dtype", dtype)
-            if grid:
-                c.set_option("grid", grid)
-            c.set_option("dots_rows", rows)
-            c.set_option("dots_pair", pair)
-            c.set_option("dots_dma", dma)
-            c.set_option("sweep", 3)   # the panel sweep even where the split sweep would be chosen
-            c.set_data(X, Y)
-            assert ["(mfmadots ", "(dmadots ", "(dmadots nt "][dma] in c.sweep_kernel(r)
-            e = c.estep(_theta(th0))
-            one, _ = c.em_step(_theta(th0))
-            out.append((e.mu_T, e.mu_U, one))
-    (mt0, mu0, o0) = out[0]
-    for (mt1, mu1, o1) in out[1:]:
-        assert np.array_equal(mt0, mt1) and np.array_equal(mu0, mu1)
-        assert np.array_equal(o0.W, o1.W) and np.array_equal(o0.C, o1.C) and np.array_equal(o0.B, o1.B)
-    ref = o.expect_m(X, Y, *(th0[k] for k in ("W", "C", "B", "sigE", "sigF", "sigH", "sigT")))
-    scale = max(np.abs(ref["mu_T"]).max(), np.abs(ref["mu_U"]).max())
-    assert np.abs(mt1 - ref["mu_T"]).max() < 1e-12 * scale
-    assert np.abs(mu1 - ref["mu_U"]).max() < 1e-12 * scale

@@ -1,0 +1,66 @@
+"""Randomised shapes through the whole EM loop on every statistics path, against the CPU oracle
+(oracle/ppls_oracle.ppls_simult, EM_W_multi.R:758-807): 3 iterations from a perturbed theta0;
+log-likelihood trace within 1e-10 relative, loadings within 1e-8 (the headline tolerances).
+
+The shapes are drawn once from a fixed seed (so a failure names a reproducible case): n from 2 r to
+3000, p and q from r to 700 (odd widths, X narrower or wider than Y), r from 1 to 12, fp64 or fp32
+storage (n >= 2 r), and the path -- split sweep, panel sweep (64-row dots waves, non-temporal loads,
+wave pairs or one wave per row tile forced at random), or the cross-product form."""
+import numpy as np
+import pytest
+
+from conftest import make_problem
+from oracle import ppls_oracle as o
+
+pytestmark = pytest.mark.gpu
+
+
+def _cases(count=96, seed=20261018):
+    rng = np.random.default_rng(seed)
+    out = []
+    for i in range(count):
+        r = int(rng.integers(1, 13))
+        p = int(rng.integers(r, 701))
+        q = int(rng.integers(r, 701))
+        # (n >= 2 r: below that X'mu is rank-deficient and the loadings are not determined -- the
+        # degenerate-input tests cover those shapes)
+        n = int(rng.choice([2 * r, 2 * r + 1, int(rng.integers(2 * r, 200)), int(rng.integers(200, 3001))]))
+        dtype = int(rng.integers(0, 2))
+        path = ["split", "panel", "panel_rows64", "panel_nt_single", "panel_pair", "xprod"][int(rng.integers(0, 6))]
+        if dtype == 1 and path == "split":
+            path = "panel"   # fp32 storage always takes the panel sweep
+        out.append((i, n, p, q, r, dtype, path))
+    return out
+
+
+def _theta(th):
+    from ppls_amd import Theta
+    return Theta(**th)
+
+
+@pytest.mark.parametrize("i,n,p,q,r,dtype,path", _cases(), ids=lambda v: str(v))
+def test_fuzz_em_run_vs_oracle(i, n, p, q, r, dtype, path):
+    from ppls_amd import Context
+    X, Y, th0 = make_problem(n, p, q, r, seed=1000 + i)
+    if dtype:
+        X = X.astype(np.float32).astype(np.float64)
+        Y = Y.astype(np.float32).astype(np.float64)
+    opts = dict(split=dict(sweep=0), panel=dict(sweep=3), panel_rows64=dict(sweep=3, dots_rows=64),
+                panel_nt_single=dict(sweep=3, nt=1, dots_pair=0), panel_pair=dict(sweep=3, dots_pair=1),
+                xprod=dict(xprod=1))[path]
+    with Context(0) as c:
+        c.set_option("dtype", dtype)
+        for k, v in opts.items():
+            c.set_option(k, v)
+        c.set_data(X, Y)
+        try:
+            est, ll, _, _ = c.em_run(_theta(th0), 3, -np.inf, 0, want_eout=False)
+        except Exception as e:   # the oracle must fail the same way (too few rows for the model)
+            with pytest.raises(Exception):
+                o.ppls_simult(X, Y, r, EMsteps=3, atol=-np.inf, theta0=th0)
+            return
+    ref = o.ppls_simult(X, Y, r, EMsteps=3, atol=-np.inf, theta0=th0)
+    rl = np.abs(np.asarray(ll) - ref["loglik"]).max() / np.abs(ref["loglik"]).max()
+    assert rl < 1e-10, rl
+    assert np.abs(est.W - ref["estimates"]["W"]).max() < 1e-8
+    assert np.abs(est.C - ref["estimates"]["C"]).max() < 1e-8

@@ -5,7 +5,7 @@
 --out <name>: write profiles/pmc_<name>.json instead (a kernel other than the sweep, e.g. the Gram).
 --kernels: substrings of the kernels that make up one sweep (default "sweep"); the per-launch
 traffic of each is averaged over its dispatches and the sweep's traffic is their sum (the wide-p
-panel sweep is two kernels: panel_dmadots (round 5; panel_mfmadots before) + panel_acc).
+panel sweep is two kernels: panel_mfmadots + panel_acc).
 
 Reads gpurun_out/prof_<tag>/pmc_{FETCH_SIZE,WRITE_SIZE}/run_counter_collection.csv and writes
 profiles/pmc_sweep_<workload>.json.  gfx950 correction (MI355X_MICROARCH.md, HBM section):

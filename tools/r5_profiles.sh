@@ -22,11 +22,11 @@ python3 tools/pmc_summary.py r5c3 c3_dp1 32e9 "round 5: the MFMA Gram forming S;
   --kernels gram_mfma --out gram_s_c3 || exit $?
 python3 tools/pmc_xprod_summary.py r5c3 c3 "round 5" || exit $?
 python3 tools/pmc_compute_summary.py r5c3 c3_dp1 sweep_split,gram_mfma,xprod_tile,finalize --trace gpurun_out/prof_r5c3/trace/run_kernel_stats.csv || exit $?
-python3 tools/pmc_summary.py r5c5 c5_dp1 21e9 "round 5" --kernels panel_dmadots,panel_acc || exit $?
+python3 tools/pmc_summary.py r5c5 c5_dp1 21e9 "round 5" --kernels panel_mfmadots,panel_acc || exit $?
 python3 tools/pmc_summary.py r5c5 c5_dp1 21e9 "round 5: the MFMA Gram forming S; algorithmic = one read of X, Y" \
   --kernels gram_mfma --out gram_s_c5 || exit $?
 python3 tools/pmc_xprod_summary.py r5c5 c5 "round 5" --bytes 924844032 || exit $?
-python3 tools/pmc_compute_summary.py r5c5 c5_dp1 panel_dmadots,panel_acc,gram_mfma,xprod_tile,finalize --trace gpurun_out/prof_r5c5/trace/run_kernel_stats.csv || exit $?
+python3 tools/pmc_compute_summary.py r5c5 c5_dp1 panel_mfmadots,panel_acc,gram_mfma,xprod_tile,finalize --trace gpurun_out/prof_r5c5/trace/run_kernel_stats.csv || exit $?
 cp profiles/pmc_*_dp1.json profiles/pmc_gram_s_c3.json profiles/pmc_gram_s_c5.json "$O/"
 cp gpurun_out/prof_r5c3/trace/run_kernel_stats.csv "$O/r5_c3_kernel_stats.csv"
 cp gpurun_out/prof_r5c5/trace/run_kernel_stats.csv "$O/r5_c5_kernel_stats.csv"
