@@ -64,3 +64,73 @@ def test_fuzz_em_run_vs_oracle(i, n, p, q, r, dtype, path):
     assert rl < 1e-10, rl
     assert np.abs(est.W - ref["estimates"]["W"]).max() < 1e-8
     assert np.abs(est.C - ref["estimates"]["C"]).max() < 1e-8
+
+
+def _relerr(a, b):
+    a, b = np.asarray(a, dtype=float), np.asarray(b, dtype=float)
+    return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-300))
+
+
+def _init_cases(count=32, seed=20261019):
+    rng = np.random.default_rng(seed)
+    out = []
+    for i in range(count):
+        a = int(rng.integers(1, 5))
+        p, q = int(rng.integers(a + 1, 400)), int(rng.integers(a + 1, 400))
+        n = int(rng.choice([int(rng.integers(4 * a, 100)), int(rng.integers(100, 2000))]))
+        out.append((i, n, p, q, a, int(rng.integers(0, 2)), int(rng.integers(0, 2))))
+    return out
+
+
+@pytest.mark.parametrize("i,n,p,q,a,dtype,xprod", _init_cases(), ids=lambda v: str(v))
+def test_fuzz_initialiser_vs_oracle(i, n, p, q, a, dtype, xprod):
+    """The sequential initialiser PPLS(X, Y, a, 8, -Inf, random draws) (EM_W_multi.R:229-279) on
+    random shapes, fp64 or fp32 storage, streaming or cross-product statistics, against the
+    oracle's explicit-deflation restatement: log-likelihoods 1e-10, loadings 1e-8."""
+    from ppls_amd import Context
+    X, Y, _ = make_problem(n, p, q, a, seed=2000 + i)
+    if dtype:
+        X = X.astype(np.float32).astype(np.float64)
+        Y = Y.astype(np.float32).astype(np.float64)
+    rng = np.random.default_rng(3000 + i)
+    inits = [o.initial_guess(p, q, "random", rng) for _ in range(a)]
+    ref = o.ppls(X, Y, a, 8, -np.inf, inits)
+    with Context(0) as c:
+        c.set_option("dtype", dtype)
+        c.set_option("xprod", xprod)
+        c.set_data(X, Y)
+        f = c.ppls(a, 8, -np.inf, inits)
+    assert _relerr(f["Other_output"]["Loglikelihoods"], ref["Other_output"]["Loglikelihoods"]) < 1e-10
+    assert np.abs(f["W"] - ref["W"]).max() < 1e-8 and np.abs(f["C"] - ref["C"]).max() < 1e-8
+
+
+def _meta_cases(count=24, seed=20261020):
+    rng = np.random.default_rng(seed)
+    out = []
+    for i in range(count):
+        K = int(rng.integers(1, 6))
+        sizes = [int(rng.choice([int(rng.integers(2, 8)), int(rng.integers(8, 600))])) for _ in range(K)]
+        p, q = int(rng.integers(2, 300)), int(rng.integers(2, 300))
+        out.append((i, tuple(sizes), p, q, int(rng.integers(0, 2))))
+    return out
+
+
+@pytest.mark.parametrize("i,sizes,p,q,dtype", _meta_cases(), ids=lambda v: str(v))
+def test_fuzz_meta_vs_oracle(i, sizes, p, q, dtype):
+    """meta_PPLSi (EM_W_multi.R:509-589) with 1-5 populations of random sizes (some of 2-7 rows),
+    fp64 (the device loop) or fp32 storage (the host-driven loop), 10 EM steps: the per-population
+    log-likelihoods 1e-10, the shared loadings 1e-8."""
+    from ppls_amd import Context
+    n = int(sum(sizes))
+    X, Y, _ = make_problem(n, p, q, 1, seed=4000 + i)
+    if dtype:
+        X = X.astype(np.float32).astype(np.float64)
+        Y = Y.astype(np.float32).astype(np.float64)
+    init = o.initial_guess(p, q, "random", np.random.default_rng(5000 + i))
+    ref = o.meta_pplsi(X, Y, list(sizes), 10, -np.inf, init)
+    with Context(0) as c:
+        c.set_option("dtype", dtype)
+        c.set_data(X, Y)
+        W, C, P, lg = c.meta_ppls(np.array(sizes), 10, -np.inf, init)
+    assert _relerr(lg, ref["logvalue"]) < 1e-10
+    assert np.abs(W - ref["W"]).max() < 1e-8 and np.abs(C - ref["C"]).max() < 1e-8
