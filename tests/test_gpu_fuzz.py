@@ -134,3 +134,84 @@ def test_fuzz_meta_vs_oracle(i, sizes, p, q, dtype):
         W, C, P, lg = c.meta_ppls(np.array(sizes), 10, -np.inf, init)
     assert _relerr(lg, ref["logvalue"]) < 1e-10
     assert np.abs(W - ref["W"]).max() < 1e-8 and np.abs(C - ref["C"]).max() < 1e-8
+
+
+def _var_cases(count=20, seed=20261021):
+    rng = np.random.default_rng(seed)
+    out = []
+    for i in range(count):
+        r = int(rng.integers(1, 6))
+        p, q = int(rng.integers(r + 1, 260)), int(rng.integers(r + 1, 260))
+        n = int(rng.integers(2 * max(p, q), 3000))
+        out.append((i, n, p, q, r, ["X", "Y"][int(rng.integers(0, 2))], int(rng.integers(0, 2)),
+                    [1, 2][int(rng.integers(0, 2))]))
+    return out
+
+
+@pytest.mark.parametrize("i,n,p,q,r,xy,from_s,chol", _var_cases(), ids=lambda v: str(v))
+def test_fuzz_variances_vs_oracle(i, n, p, q, r, xy, from_s, chol):
+    """variances_PPLS_simult (EM_W_multi.R:834-905) on random widths (the hand-written inverse's
+    partial 64-blocks, 1-4 of them), the Gram of its own or S's block, the hand-written inverse or
+    rocSOLVER's: every component's information matrix inverse 1e-8, the standard errors 1e-8."""
+    import ppls_amd
+    from ppls_amd import Context
+    X, Y, th0 = make_problem(n, p, q, r, seed=6000 + i)
+    fit = o.ppls_simult(X, Y, r, EMsteps=10, atol=-np.inf, theta0=th0)
+    D = X if xy == "X" else Y
+    ref = o.variances_ppls_simult(fit, D, xy)
+    with Context(0) as c:
+        c.set_option("var_chol", chol)
+        c.set_data(X, Y)
+        if from_s:
+            c.xprod_prepare()
+        got = ppls_amd.variances_PPLS_simult(fit, None, xy, ctx=c)
+    for k in range(r):
+        assert _relerr(got["varMatrix"][k], ref["varMatrix"][k]) < 1e-8
+    assert _relerr(got["seLoad"], ref["seLoad"]) < 1e-8
+
+
+def _shard_cases(count=24, seed=20261022):
+    rng = np.random.default_rng(seed)
+    out = []
+    for i in range(count):
+        k = int(rng.integers(2, 6))
+        r = int(rng.integers(1, 11))
+        p, q = int(rng.integers(r, 600)), int(rng.integers(r, 600))
+        n = int(rng.integers(max(2 * r, k), 2500))
+        dtype = int(rng.integers(0, 2))
+        path = ["auto", "panel", "xprod"][int(rng.integers(0, 3))]
+        out.append((i, k, n, p, q, r, dtype, path))
+    return out
+
+
+@pytest.mark.parametrize("i,k,n,p,q,r,dtype,path", _shard_cases(), ids=lambda v: str(v))
+def test_fuzz_sharded_vs_oracle(i, k, n, p, q, r, dtype, path):
+    """Rows sharded over k = 2-5 contexts (host threads, summing through ppls_set_reducer in rank
+    order; tests/test_gpu_multirank.py): every rank's estimates bit-identical, and equal to the
+    oracle on the whole data (1e-10 log-likelihood, 1e-8 loadings), 4 EM iterations."""
+    from test_gpu_multirank import _run_ranks
+    from ppls_amd import Context
+    X, Y, th0 = make_problem(n, p, q, r, seed=7000 + i)
+    if dtype:
+        X = X.astype(np.float32).astype(np.float64)
+        Y = Y.astype(np.float32).astype(np.float64)
+
+    def work(rank, c):
+        r0, nl = Context.shard_range(n, k, rank)
+        c.set_option("dtype", dtype)
+        if path == "panel":
+            c.set_option("sweep", 3)
+        elif path == "xprod":
+            c.set_option("xprod", 1)
+        c.set_data(X[r0:r0 + nl], Y[r0:r0 + nl], n_total=n)
+        est, ll, _, _ = c.em_run(_theta(th0), 4, -np.inf, 0, want_eout=False)
+        return est, ll
+
+    res = _run_ranks(k, work)
+    for est, ll in res[1:]:
+        assert np.array_equal(est.W, res[0][0].W) and np.array_equal(ll, res[0][1])
+    ref = o.ppls_simult(X, Y, r, EMsteps=4, atol=-np.inf, theta0=th0)
+    est, ll = res[0]
+    assert _relerr(ll, ref["loglik"]) < 1e-10
+    assert np.abs(est.W - ref["estimates"]["W"]).max() < 1e-8
+    assert np.abs(est.C - ref["estimates"]["C"]).max() < 1e-8
