@@ -114,6 +114,7 @@ const char* ppls_last_error(const ppls_ctx* ctx);
  *       "dots_rows" (panel sweep dots: rows per wave, 0 auto (64 from 32768 rows, else 32), 32, 64),
  *       "dots_pair" (panel sweep dots: a wave pair per row tile, -1 auto (when row tiles are fewer
  *                    than resident wave slots), 0, 1),
+ *       "acc_chunks" (panel sweep accumulation: row chunks, 0 auto, else that many),
  *       "var_chol" (ppls_variances' inverse of the observed information: 1, default, the
  *                   hand-written batched Cholesky + inverse (ppls_linalg.hip); 2 rocSOLVER
  *                   potrf/potri; 0 rocSOLVER LU getrf/getri; a matrix that is not positive definite

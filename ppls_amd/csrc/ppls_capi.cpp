@@ -38,6 +38,7 @@ struct ppls_ctx {
   int pipe_opt = 1;     // split kernel: software-pipelined order
   int dots_rows = 0;   // panel dots rows per wave: 0 auto, 32, 64 (tests of both forms)
   int dots_pair = -1;  // panel dots wave pair per row tile: -1 auto, 0, 1
+  int acc_chunks = 0;  // panel accumulation row chunks: 0 auto (ppls_panel_chunks), else forced
   int team_rows = 0;   // finalize polar team: rows of S per member (0: PPLS_TEAM_ROWS)
   int polar1 = 1;   // finalize polar: Cholesky-QR1 fast path when kappa(X'mu) <= PPLS_POLAR1_KAPPA
   int polar1_kappa = 0;   // its bound on ||R1||_F ||R1^-1||_F (0 = min(8 r, 40))
@@ -421,7 +422,8 @@ int sweep_plan(ppls_ctx* c, int r, PplsSweepArgs* a) {
     return 3;
   }
   // wide data / large r / fp32 storage: the panel sweep (two GEMM-shaped passes)
-  a->grid = c->grid_opt > 0 ? c->grid_opt : ppls_panel_chunks(nrows, c->ldx, c->ldy, c->num_cus, c->dtype, r);
+  a->grid = c->acc_chunks > 0 ? c->acc_chunks
+          : c->grid_opt > 0 ? c->grid_opt : ppls_panel_chunks(nrows, c->ldx, c->ldy, c->num_cus, c->dtype, r);
   a->dots_grid = c->grid_opt;   // the grid option also sets the dots grid (tests: grid-stride path)
   return 4;
 }
@@ -1173,6 +1175,9 @@ int ppls_set_option(ppls_ctx* c, const char* key, int64_t value) {
   } else if (!strcmp(key, "dots_pair")) {
     if (value < -1 || value > 1) return fail(c, PPLS_E_ARG, "dots_pair must be -1 (auto), 0 or 1");
     c->dots_pair = (int)value;
+  } else if (!strcmp(key, "acc_chunks")) {
+    if (value < 0 || value > 65535) return fail(c, PPLS_E_ARG, "acc_chunks must be in [0, 65535]");
+    c->acc_chunks = (int)value;
   } else if (!strcmp(key, "strace")) {
     if (value && !c->strace) {
       HIPCHK(c, hipMalloc(&c->strace, (size_t)PPLS_STRACE_MAX_WG * 4 * sizeof(long long)));

@@ -905,7 +905,10 @@ __global__ __launch_bounds__(256) void ppls_panel_acc_kernel(
   // mu (mu_T for X tiles, mu_U for Y tiles) of BR rows at a time in LDS (every lane reads the same
   // address: broadcast).  Software-pipelined: the next batch's mu is loaded into registers while the
   // current batch is computed (LDS double-buffered, one barrier per batch), and the X rows stream in
-  // groups of 8 with the next group's loads in flight during the current group's FMAs.
+  // groups of 8 with the next group's loads in flight during the current group's FMAs.  (Round 5:
+  // each row's mu read a row ahead into registers, so its LDS reads overlap the previous row's FMAs:
+  // 4 % faster in isolated launches at C5, 0.2 % in back-to-back iterations -- the clock, not the LDS
+  // latency, bounds the FMAs -- and 1 % slower at C5's 8-GPU share; not kept.  DESIGN.md 4.2)
   constexpr int BR = 128;
   constexpr int MPT = (BR * R + 255) / 256;
   __shared__ double smu[2][BR * R];
@@ -2871,6 +2874,11 @@ int ppls_panel_chunks(int64_t n_local, int ldx, int ldy, int num_cus, int dtype_
   // (profiles/r2_row_alignment_probe.txt: the write-out is the kernel's largest overhead).  Now 4
   // rounds, half of them large chunks (PplsChunks): half the partials, about the same tail.
   int64_t ch = 4 * slots / tiles;
+  // Round 5: where those chunks would be short (< 1200 rows on average), 2 rounds: the partials'
+  // write-out and reduction outweigh the longer tail.  C5's 8-GPU share (62,500 rows, 336 rows per
+  // chunk at 4 rounds): 1.04-1.05 -> 1.008 ms per iteration; 1.25e5 / 1.875e5 rows: 1 % / 0.2 %
+  // faster; 2.5e5 and the full 5e5: 4 rounds stay 0.3-0.4 % faster (profiles/r5_acc_chunks_ab.txt).
+  if (n_local < 1200 * ch) ch = 2 * slots / tiles;
   if (ch > maxch) ch = maxch;
   if (ch > 1024) ch = 1024;
   if (ch < 1) ch = 1;

@@ -5,7 +5,8 @@ log-likelihood trace within 1e-10 relative, loadings within 1e-8 (the headline t
 The shapes are drawn once from a fixed seed (so a failure names a reproducible case): n from 2 r to
 3000, p and q from r to 700 (odd widths, X narrower or wider than Y), r from 1 to 12, fp64 or fp32
 storage (n >= 2 r), and the path -- split sweep, panel sweep (64-row dots waves, non-temporal loads,
-wave pairs or one wave per row tile forced at random), or the cross-product form."""
+wave pairs or one wave per row tile forced at random; the accumulation over 1-7 row chunks), or the
+cross-product form."""
 import numpy as np
 import pytest
 
@@ -27,6 +28,8 @@ def _cases(count=96, seed=20261018):
         n = int(rng.choice([2 * r, 2 * r + 1, int(rng.integers(2 * r, 200)), int(rng.integers(200, 3001))]))
         dtype = int(rng.integers(0, 2))
         path = ["split", "panel", "panel_rows64", "panel_nt_single", "panel_pair", "xprod"][int(rng.integers(0, 6))]
+        if path == "panel" and i % 2:
+            path = "panel_chunks"   # (not drawn from rng: the shapes of every case stay as they were)
         if dtype == 1 and path == "split":
             path = "panel"   # fp32 storage always takes the panel sweep
         out.append((i, n, p, q, r, dtype, path))
@@ -47,6 +50,7 @@ def test_fuzz_em_run_vs_oracle(i, n, p, q, r, dtype, path):
         Y = Y.astype(np.float32).astype(np.float64)
     opts = dict(split=dict(sweep=0), panel=dict(sweep=3), panel_rows64=dict(sweep=3, dots_rows=64),
                 panel_nt_single=dict(sweep=3, nt=1, dots_pair=0), panel_pair=dict(sweep=3, dots_pair=1),
+                panel_chunks=dict(sweep=3, acc_chunks=int(1 + i % 7)),
                 xprod=dict(xprod=1))[path]
     with Context(0) as c:
         c.set_option("dtype", dtype)

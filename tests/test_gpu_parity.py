@@ -18,11 +18,14 @@ pytestmark = pytest.mark.gpu
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
 # sweep-kernel variants (context options): split ownership (default; auto = 2 rows per step,
 # occupancy grid), split 1 row/step pipelined / unpipelined, the same with non-temporal loads,
-# panel (wide p) with 32 and (option dots_rows, auto below 32768 rows = 32) 64 rows per dots wave
+# panel (wide p) with 32 and (option dots_rows, auto below 32768 rows = 32) 64 rows per dots wave;
+# the panel accumulation over few long row chunks (acc_chunks)
 SWEEPS = [dict(), dict(rows_per_step=1, pipe=1), dict(rows_per_step=1, pipe=0), dict(nt=1),
-          dict(sweep=3), dict(sweep=3, dots_rows=64), dict(sweep=3, dots_rows=64, dots_pair=0, nt=1)]
-SWEEP_IDS = ["split", "split_rp1", "split_rp1_nopipe", "split_nt", "panel", "panel_rows64", "panel_nt_single"]
-DEFAULTS = dict(sweep=0, grid=0, rows_per_step=0, pipe=1, nt=-1, dots_rows=0, dots_pair=-1)
+          dict(sweep=3), dict(sweep=3, dots_rows=64), dict(sweep=3, dots_rows=64, dots_pair=0, nt=1),
+          dict(sweep=3, acc_chunks=1), dict(sweep=3, acc_chunks=3, nt=1)]
+SWEEP_IDS = ["split", "split_rp1", "split_rp1_nopipe", "split_nt", "panel", "panel_rows64", "panel_nt_single",
+             "panel_chunks1", "panel_chunks3_nt"]
+DEFAULTS = dict(sweep=0, grid=0, rows_per_step=0, pipe=1, nt=-1, dots_rows=0, dots_pair=-1, acc_chunks=0)
 
 
 @pytest.fixture(scope="module")

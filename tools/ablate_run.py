@@ -15,7 +15,7 @@ ctx = Context(0)
 if cfg.get("storage") == "f32":
     ctx.set_option("dtype", 1)
 truth, th0 = make_truth_and_theta0(cfg["p"], cfg["q"], cfg["r"])
-ctx.generate_synthetic(cfg["n"], cfg["p"], cfg["q"], truth, seed=20261015)
+ctx.generate_synthetic(int(os.environ.get("AB_N", cfg["n"])), cfg["p"], cfg["q"], truth, seed=20261015)
 done = 0
 t0 = time.perf_counter()
 for _ in range(60):

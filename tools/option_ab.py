@@ -36,6 +36,7 @@ def main():
     if cfg.get("storage") == "f32":
         ctx.set_option("dtype", 1)
     truth, th0 = make_truth_and_theta0(p, q, r)
+    n = int(os.environ.get("AB_N", n))   # row-count override (same p, q, r, storage)
     ctx.generate_synthetic(n, p, q, truth, seed=20261015)
     res = {s: [] for s in specs}
     keys = sorted({k for s in specs for k, _ in parse(s)})
