@@ -43,7 +43,8 @@ def main():
     for rep in range(reps):
         for s in specs:
             for k in keys:   # back to the defaults, then this arm's values
-                ctx.set_option(k, {"polar1": 1, "nt": -1, "pipe": 1, "xprod_waves": 4, "exact_gram": 1}.get(k, 0))
+                ctx.set_option(k, {"polar1": 1, "nt": -1, "pipe": 1, "xprod_waves": 4, "exact_gram": 1, "dots_pair": -1, "xprod": 0,
+                                 "var_chol": 1, "vorth": 8, "meta_device": 1, "xprod_fuse": 1}.get(k, 0))
             for k, v in parse(s):
                 ctx.set_option(k, v)
             ctx.em_begin(th0)
