@@ -7,6 +7,8 @@ The shapes are drawn once from a fixed seed (so a failure names a reproducible c
 storage (n >= 2 r), and the path -- split sweep, panel sweep (64-row dots waves, non-temporal loads,
 wave pairs or one wave per row tile forced at random; the accumulation over 1-7 row chunks), or the
 cross-product form."""
+import os
+
 import numpy as np
 import pytest
 
@@ -15,8 +17,14 @@ from oracle import ppls_oracle as o
 
 pytestmark = pytest.mark.gpu
 
+# PPLS_FUZZ_SCALE = k multiplies every case count (k x 196 cases) and PPLS_FUZZ_SEED shifts the seeds:
+# a longer hunt on the GPU box (profiles/r5_fuzz_scale8.log); the default run is the fixed 196 cases
+_SCALE = max(1, int(os.environ.get("PPLS_FUZZ_SCALE", "1")))
+_SEED = int(os.environ.get("PPLS_FUZZ_SEED", "0"))
+
 
 def _cases(count=96, seed=20261018):
+    count, seed = count * _SCALE, seed + _SEED
     rng = np.random.default_rng(seed)
     out = []
     for i in range(count):
@@ -76,6 +84,7 @@ def _relerr(a, b):
 
 
 def _init_cases(count=32, seed=20261019):
+    count, seed = count * _SCALE, seed + _SEED
     rng = np.random.default_rng(seed)
     out = []
     for i in range(count):
@@ -86,11 +95,29 @@ def _init_cases(count=32, seed=20261019):
     return out
 
 
+def _oracle_spread(X, Y, a, steps, inits, ref, draws=2):
+    """How far the oracle's own PPLS fit moves when the starting scalars are changed by about one
+    ulp: the reference's EMstepC_fast coefficients (loglC.cpp:354-361, e.g. -c1 + 1/sig2X) cancel
+    badly at extreme random starts (sigE ~ 0.03), so rounding alone moves the loadings that far."""
+    spread = 0.0
+    for s in range(draws):
+        r = np.random.default_rng(s)
+        pin = [dict(d, **{k: d[k] * (1 + 2e-16 * r.standard_normal()) for k in ("sigE", "sigF", "sigH", "sigT", "B")})
+               for d in inits]
+        f = o.ppls(X, Y, a, steps, -np.inf, pin)
+        spread = max(spread, np.abs(f["W"] - ref["W"]).max(), np.abs(f["C"] - ref["C"]).max())
+    return spread
+
+
 @pytest.mark.parametrize("i,n,p,q,a,dtype,xprod", _init_cases(), ids=lambda v: str(v))
 def test_fuzz_initialiser_vs_oracle(i, n, p, q, a, dtype, xprod):
     """The sequential initialiser PPLS(X, Y, a, 8, -Inf, random draws) (EM_W_multi.R:229-279) on
     random shapes, fp64 or fp32 storage, streaming or cross-product statistics, against the
-    oracle's explicit-deflation restatement: log-likelihoods 1e-10, loadings 1e-8."""
+    oracle's explicit-deflation restatement: log-likelihoods 1e-10, loadings 1e-8 -- or, where the
+    start itself makes the fit that sensitive to rounding, within 10x of the oracle's own move under
+    1-ulp changes of the starting scalars (found by PPLS_FUZZ_SCALE = 8: n = 56, p = 360, a = 4,
+    starts with sigE, sigF = 0.03-0.07: the device's 4th-component loadings 1.2e-8 from the oracle,
+    the oracle's own 1-ulp spread 1.2e-8; profiles/r5_fuzz_scale8.log)."""
     from ppls_amd import Context
     X, Y, _ = make_problem(n, p, q, a, seed=2000 + i)
     if dtype:
@@ -105,10 +132,14 @@ def test_fuzz_initialiser_vs_oracle(i, n, p, q, a, dtype, xprod):
         c.set_data(X, Y)
         f = c.ppls(a, 8, -np.inf, inits)
     assert _relerr(f["Other_output"]["Loglikelihoods"], ref["Other_output"]["Loglikelihoods"]) < 1e-10
-    assert np.abs(f["W"] - ref["W"]).max() < 1e-8 and np.abs(f["C"] - ref["C"]).max() < 1e-8
+    err = max(np.abs(f["W"] - ref["W"]).max(), np.abs(f["C"] - ref["C"]).max())
+    if err >= 1e-8:
+        spread = _oracle_spread(X, Y, a, 8, inits, ref)
+        assert err < 10 * spread, (err, spread)
 
 
 def _meta_cases(count=24, seed=20261020):
+    count, seed = count * _SCALE, seed + _SEED
     rng = np.random.default_rng(seed)
     out = []
     for i in range(count):
@@ -141,6 +172,7 @@ def test_fuzz_meta_vs_oracle(i, sizes, p, q, dtype):
 
 
 def _var_cases(count=20, seed=20261021):
+    count, seed = count * _SCALE, seed + _SEED
     rng = np.random.default_rng(seed)
     out = []
     for i in range(count):
@@ -175,6 +207,7 @@ def test_fuzz_variances_vs_oracle(i, n, p, q, r, xy, from_s, chol):
 
 
 def _shard_cases(count=24, seed=20261022):
+    count, seed = count * _SCALE, seed + _SEED
     rng = np.random.default_rng(seed)
     out = []
     for i in range(count):
