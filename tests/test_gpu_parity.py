@@ -430,3 +430,17 @@ def test_edge_shapes_vs_oracle(ctx, sweep, n, p, q, r):
     assert np.abs(est.C - ref["estimates"]["C"]).max() < tol
     assert _relerr([est.sigE, est.sigF, est.sigH], [ref["estimates"][k] for k in ("sigE", "sigF", "sigH")]) < tol
     assert _relerr(eout.mu_T, ref["Expectations"]["mu_T"]) < tol
+
+
+def test_option_values_are_validated(ctx):
+    """ppls_set_option rejects out-of-range values and unknown keys with PPLS_E_ARG (include/ppls.h),
+    and the context keeps its previous setting."""
+    from ppls_amd import PplsError
+    bad = dict(dots_rows=48, dots_pair=2, acc_chunks=-1, var_chol=3, polar1_kappa=256, vorth=0)
+    for k, v in bad.items():
+        with pytest.raises(PplsError):
+            ctx.set_option(k, v)
+    with pytest.raises(PplsError, match="unknown option"):
+        ctx.set_option("no_such_option", 1)
+    ctx.set_option("acc_chunks", 65535)   # the largest accepted value
+    ctx.set_option("acc_chunks", 0)
