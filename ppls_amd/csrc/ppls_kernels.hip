@@ -688,7 +688,7 @@ __device__ __forceinline__ PplsVec16<T> ppls_load16(const T* p) {
 // (the second half's dot sums are added to the first's through LDS, in that fixed order): for
 // shards with fewer row tiles than resident wave slots (C5's 8-GPU share: 977 tiles of 64 rows for
 // 2,048 slots), which would otherwise run one wave per SIMD.
-template <typename T, int R, int NB, int KS>
+template <typename T, int R, int NB, int KS, bool NT>
 __global__ __launch_bounds__(256) void ppls_panel_mfmadots_kernel(
     const T* __restrict__ X, const T* __restrict__ Y, int64_t n, int ldx, int ldy, int px, int py,
     const double* __restrict__ Wt, const double* __restrict__ Ct, const PplsScalars* __restrict__ sc,
@@ -755,7 +755,13 @@ __global__ __launch_bounds__(256) void ppls_panel_mfmadots_kernel(
       // the last tile re-read it.  Issue order per tile: this tile's B operands, then the next
       // tile's X loads, so the MFMAs wait only for B while the next tile streams in.
       f4 xa[NL];
-      auto ld4 = [&](const T* p) -> f4 { return *(const f4*)p; };   // (non-temporal: 16 % slower here)
+      // NT (the sweep's nt policy: data larger than the MALL): non-temporal X/Y loads -- round 5,
+      // steady state at C5: 7.24 vs 7.33-7.36 ms per iteration over 6 interleaved pairs, the 8-GPU
+      // share even (profiles/r5_dots_nt_ab.txt; round 2's isolated-launch A/B had them 16 % slower)
+      auto ld4 = [&](const T* p) -> f4 {
+        if constexpr (NT) return __builtin_nontemporal_load((const f4*)p);
+        else return *(const f4*)p;
+      };
       auto load_tile = [&](int tc, f4 (&b)[NL]) {
         const int c = tc < tc1 ? tc : tc1 - 1;   // a prefetch past the range re-reads its last tile
 #pragma unroll
@@ -2768,13 +2774,20 @@ hipError_t launch_panel_t(const PplsSweepArgs* a, const T* X, const T* Y, double
     // 7.69-7.78 ms; profiles/r2_c5_dots_rows.txt.  Round 5: X tiles by LDS-DMA, two in flight per
     // wave, 1.5 % faster at C5 -- removed: its uncounted inline-asm B loads were copied by the register
     // allocator before they landed in some instantiations)
-#define PPLS_LAUNCH_DOTS(NBV, KSV)                                                                   \
-  hipLaunchKernelGGL((ppls_panel_mfmadots_kernel<T, R, NBV, KSV>), dim3(mblocks), dim3(256), 0, st, X, Y, \
+#define PPLS_LAUNCH_DOTS(NBV, KSV, NTV)                                                              \
+  hipLaunchKernelGGL((ppls_panel_mfmadots_kernel<T, R, NBV, KSV, NTV>), dim3(mblocks), dim3(256), 0, st, X, Y, \
                      a->n_local, a->ldx, a->ldy, a->p, a->q, Wt, Ct, a->sc, Z, mu_out, a->stop)
-    if (rb == 64 && ks == 2) PPLS_LAUNCH_DOTS(4, 2);
-    else if (rb == 64) PPLS_LAUNCH_DOTS(4, 1);
-    else if (ks == 2) PPLS_LAUNCH_DOTS(2, 2);
-    else PPLS_LAUNCH_DOTS(2, 1);
+    if (a->nt) {
+      if (rb == 64 && ks == 2) PPLS_LAUNCH_DOTS(4, 2, true);
+      else if (rb == 64) PPLS_LAUNCH_DOTS(4, 1, true);
+      else if (ks == 2) PPLS_LAUNCH_DOTS(2, 2, true);
+      else PPLS_LAUNCH_DOTS(2, 1, true);
+    } else {
+      if (rb == 64 && ks == 2) PPLS_LAUNCH_DOTS(4, 2, false);
+      else if (rb == 64) PPLS_LAUNCH_DOTS(4, 1, false);
+      else if (ks == 2) PPLS_LAUNCH_DOTS(2, 2, false);
+      else PPLS_LAUNCH_DOTS(2, 1, false);
+    }
 #undef PPLS_LAUNCH_DOTS
   }
   constexpr int VEC = PplsVec16<T>::N;
