@@ -52,6 +52,37 @@ CALL_SEED = 20261017    # numpy stream of the 'random' initial guesses of the ti
 READBACK = "readback of a committed rocprofv3 PMC summary under profiles/ (not measured in this run)"
 
 
+class _Markers:
+    """roctx ranges around the bench's phases when PPLS_ROCTX=1 (a rocprofv3 --marker-trace run):
+    tools/timed_launches.py then splits the kernel trace into the balance calibration, warm-up,
+    timed, cross-product and whole-call launches.  Without the variable nothing is loaded."""
+
+    def __init__(self):
+        self.lib = None
+        if os.environ.get("PPLS_ROCTX") != "1":
+            return
+        import ctypes
+        for name in ("librocprofiler-sdk-roctx.so.1", "libroctx64.so"):
+            try:
+                lib = ctypes.CDLL(name)
+                lib.roctxRangePushA.argtypes = [ctypes.c_char_p]
+                self.lib = lib
+                break
+            except (OSError, AttributeError):
+                continue
+
+    def push(self, label):
+        if self.lib is not None:
+            self.lib.roctxRangePushA(f"bench:{label}".encode())
+
+    def pop(self):
+        if self.lib is not None:
+            self.lib.roctxRangePop()
+
+
+MARK = _Markers()
+
+
 def polar(M):
     U, _, Vt = np.linalg.svd(M, full_matrices=False)
     return U @ Vt
@@ -120,15 +151,27 @@ def load_compute_counters(workload_key, kernel_sub):
                 source=dict(_source(name, js), kernel=kernel_sub))
 
 
+def affinity_cores():
+    """The CPUs this process may run on (its affinity mask; os.cpu_count() without one)."""
+    try:
+        return len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        return os.cpu_count() or 1
+
+
 def host_cores():
     """What "all cores" means on this host: the machine's CPUs (os.cpu_count = nproc without an
-    affinity mask), the CPUs this process may run on (its affinity mask), and the OpenMP thread
-    count the C baseline runs with (OMP_NUM_THREADS or the runtime default)."""
+    affinity mask), the CPUs this process may run on (its affinity mask), the inherited
+    OMP_NUM_THREADS, and the cgroup CPU quota (cpu.max: a quota below the mask caps what more
+    threads can buy)."""
+    quota = None
     try:
-        aff = len(os.sched_getaffinity(0))
-    except (AttributeError, OSError):
-        aff = None
-    return dict(nproc=os.cpu_count(), affinity=aff, omp_num_threads_env=os.environ.get("OMP_NUM_THREADS"))
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota = f.read().strip()
+    except OSError:
+        pass
+    return dict(nproc=os.cpu_count(), affinity=affinity_cores(), omp_num_threads_env=os.environ.get("OMP_NUM_THREADS"),
+                cgroup_cpu_max=quota)
 
 
 def cpu_model():
@@ -145,21 +188,33 @@ def cpu_model():
 def cpu_baseline(ctx, th0, cfg, iters=3, one_core_rows=100_000):
     """Time the C restatement of the reference path (oracle/cpu_ref.c: its pass structure, OpenMP
     over rows) on the host cores, on the SAME rows the GPU holds (full n, >= 3 steady-
-    state iterations after one untimed iteration, all cores; plus 1 core on a row sample, scaled
-    linearly in n), and compare the CPU's log-likelihood trace and loadings with the GPU's first
-    iterations from the same theta0."""
+    state iterations after one untimed iteration, OpenMP over every CPU of the affinity mask --
+    whatever OMP_NUM_THREADS the process inherited; the inherited thread count as a second figure;
+    plus 1 core on a row sample, scaled linearly in n), and compare the CPU's log-likelihood trace
+    and loadings with the GPU's first iterations from the same theta0."""
     from oracle import cpu_ref
     from oracle.ppls_oracle import canonicalize
     th = th0.as_dict()
-    cores = cpu_ref.load().cpu_ref_max_threads()
+    env_threads = cpu_ref.load().cpu_ref_max_threads()   # the runtime default (OMP_NUM_THREADS)
+    cores = affinity_cores()
     X, Y = ctx.get_data_rows()             # all rows, row-major (what cpu_ref streams)
-    t0 = time.perf_counter()
-    th1, ll1 = cpu_ref.em_steps(X, Y, th, 1)        # untimed: faults the pages in, spins up OpenMP
-    t_first = time.perf_counter() - t0
-    t0 = time.perf_counter()
-    th_cpu, ll_cpu = cpu_ref.em_steps(X, Y, th1, iters)
-    dt = time.perf_counter() - t0
-    ll_all = np.concatenate([ll1, ll_cpu])
+
+    def timed(nthreads):   # 1 untimed iteration (faults the pages in, spins up OpenMP), then `iters`
+        t0 = time.perf_counter()
+        th1, ll1 = cpu_ref.em_steps(X, Y, th, 1, nthreads=nthreads)
+        t_first = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        th_cpu, ll_cpu = cpu_ref.em_steps(X, Y, th1, iters, nthreads=nthreads)
+        return th_cpu, np.concatenate([ll1, ll_cpu]), time.perf_counter() - t0, t_first
+
+    th_cpu, ll_all, dt, t_first = timed(cores)
+    inherited = None
+    if env_threads != cores:
+        _, ll_env, dt_env, _ = timed(env_threads)
+        inherited = dict(value=iters / dt_env, unit="EM iterations/s", cores=int(env_threads),
+                         sample=f"the same {iters} iterations on {env_threads} OpenMP threads (the inherited "
+                                f"OMP_NUM_THREADS / runtime default) in {dt_env:.1f} s",
+                         loglik_equal_to_all_core_run=bool(np.array_equal(ll_env, ll_all)))
     # 1 core on the first rows (bounded time), per-row rate scaled to the full n
     ns = int(min(one_core_rows, X.shape[0]))
     Xs, Ys = X[:ns], Y[:ns]
@@ -178,8 +233,9 @@ def cpu_baseline(ctx, th0, cfg, iters=3, one_core_rows=100_000):
     one_core = iters * ns / dt1 / n
     return dict(value=iters / dt, unit="EM iterations/s", cores=int(cores), kind="port", host=host_cores(),
                 sample=f"{iters} steady-state EM iterations (after 1 untimed, {t_first:.1f} s) on all n={n} rows "
-                       f"in {dt:.1f} s: oracle/cpu_ref.c (reference pass structure), OpenMP {cores} threads, "
-                       f"-O3 -march=native, {cpu_model()}",
+                       f"in {dt:.1f} s: oracle/cpu_ref.c (reference pass structure), OpenMP {cores} threads "
+                       f"(the affinity mask), -O3 -march=native, {cpu_model()}",
+                inherited_threads=inherited,
                 one_core=dict(value=one_core, unit="EM iterations/s", cores=1,
                               sample=f"{iters} EM iterations on the first {ns} rows in {dt1:.1f} s, 1 thread; "
                                      f"value = rows*iterations/s / n")), rel, werr
@@ -303,9 +359,9 @@ def cpu_call_baseline(ctx, r, cfg, device, rows):
     X, Y = ctx.get_data_rows(0, rows)
     rng = np.random.default_rng(CALL_SEED)
     inits = [initial_guess(cfg["p"], cfg["q"], "random", rng) for _ in range(r)]
-    cores = cpu_ref.load().cpu_ref_max_threads()
+    cores = affinity_cores()
     t0 = time.perf_counter()
-    est, ll, cs, secs = cpu_ref.ppls_simult_call(X, Y, r, inits)
+    est, ll, cs, secs = cpu_ref.ppls_simult_call(X, Y, r, inits, nthreads=cores)
     dt = time.perf_counter() - t0
     with Context(device) as c2:   # the GPU on the same rows, same draws (streaming statistics)
         c2.set_data(X, Y)
@@ -456,15 +512,22 @@ def main():
     def tmax(v):
         return _reduce_max(dist, torch, v)
 
+    MARK.push("em_begin")   # the split sweep's balance calibration launches run here
     ctx.em_begin(th0)
+    barrier()
+    MARK.pop()
+    MARK.push("warmup")
     ctx.em_iterate(args.warmup)
     barrier()
+    MARK.pop()
     ctx.set_option("timing", args.timing_every)
     ctx.sweep_timing(reset=True)
+    MARK.push("timed")
     t0 = time.perf_counter()
     ctx.em_iterate(args.steps)
     barrier()
     dt = tmax(time.perf_counter() - t0)
+    MARK.pop()
     ctx.set_option("timing", 0)
     kern_ms, launches = ctx.sweep_timing(reset=True)
     est, ll = ctx.em_state()
@@ -473,12 +536,16 @@ def main():
     digest_parts = _theta_arrays(est, ll)
     xp = None
     if args.xprod_steps > 0:
+        MARK.push("xprod")
         est_x, ll_x, xp = bench_xprod(ctx, th0, args, barrier, tmax, r, ll, dt / args.steps)
+        MARK.pop()
         digest_parts += _theta_arrays(est_x, ll_x)
         ctx.set_option("xprod", 0)
     call = None
     if not args.no_call:
+        MARK.push("call")
         call = bench_call(ctx, r, barrier, tmax)
+        MARK.pop()
         for mode in ("stream", "xprod", "auto"):
             f = call.pop(f"_{mode}_fit")
             e = f["estimates"]
@@ -596,7 +663,9 @@ def main():
                                     "initialiser, EMsteps 10, atol 1e-4, Expectations to the host; S formed inside "
                                     "the xprod / auto calls", **call)
         if world == 1 and not args.no_cpu:
+            MARK.push("cpu_baseline")
             cb, rel, werr = cpu_baseline(ctx, th0, cfg, args.cpu_iters)
+            MARK.pop()
             out["cpu_baseline"] = cb
             out["loglik_rel_err_vs_cpu"] = rel
             out["W_abs_err_vs_cpu"] = werr

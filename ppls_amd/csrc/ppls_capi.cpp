@@ -139,7 +139,9 @@ struct ppls_ctx {
   int xp_nsplit = 0;
   // the MFMA Gram's work queue (S, variances' X'X), prepared for one shape
   int* gram_q = nullptr;
-  int64_t gq_key[6] = {-1, -1, -1, -1, -1, -1};   // (p, xreal, xcols, yreal, n, nsplit_req) of gram_q
+  // (p, xreal, xcols, yreal, n, nsplit_req, nsplit, wave slots) of gram_q: the queue layout depends
+  // on the split count and the slot count, which follow the storage dtype's occupancy
+  int64_t gq_key[8] = {-1, -1, -1, -1, -1, -1, -1, -1};
   rocblas_handle blas = nullptr;   // rocSOLVER (variances.PPLS_simult's p x p inverse), created lazily
   int var_chol = 1;                // option "var_chol": that inverse by Cholesky when positive definite: 1 hand-written
                                    // (ppls_linalg.hip), 2 rocSOLVER potrf/potri; 0 LU (rocSOLVER getrf/getri)
@@ -675,9 +677,11 @@ int gram_nsplit(const ppls_ctx* c, const GramShape& g, int64_t n, int req) {
   return ppls_gram_plan(g.p, g.xreal, g.xcols, g.yreal, n, gram_wave_slots(c), req, nullptr);
 }
 
-// The Gram's work queue for (shape, n, req), prepared once and kept while the shape repeats.
+// The Gram's work queue for (shape, n, req, split plan, wave slots), prepared once and kept while
+// all of them repeat.
 int gram_queue(ppls_ctx* c, const GramShape& g, int64_t n, int req, int** q) {
-  const int64_t key[6] = {g.p, g.xreal, g.xcols, g.yreal, n, req};
+  const int nsplit = gram_nsplit(c, g, n, req);
+  const int64_t key[8] = {g.p, g.xreal, g.xcols, g.yreal, n, req, nsplit, gram_wave_slots(c)};
   if (c->gram_q && !memcmp(key, c->gq_key, sizeof key)) {
     *q = c->gram_q;
     return PPLS_OK;
@@ -685,7 +689,6 @@ int gram_queue(ppls_ctx* c, const GramShape& g, int64_t n, int req, int** q) {
   *q = nullptr;
   int rc;
   c->gq_key[0] = -1;
-  const int nsplit = gram_nsplit(c, g, n, req);
   if ((rc = dalloc(c, &c->gram_q, (size_t)ppls_gram_queue_ints(g.p, nsplit)))) return rc;
   HIPCHK(c, ppls_gram_queue_prepare(c->gram_q, g.p, g.xreal, g.xcols, g.yreal, n, gram_wave_slots(c), req, c->stream));
   memcpy(c->gq_key, key, sizeof key);
@@ -695,14 +698,15 @@ int gram_queue(ppls_ctx* c, const GramShape& g, int64_t n, int req, int** q) {
 
 // G (device, p x p column-major) = the Gram of this rank's n rows: the MFMA kernel into per-item
 // partials, then the finish (sum over splits, mirrored).  ms: the MFMA kernel's duration (HIP
-// events), if not null.  The partials are allocated here and freed.
-int gram_run(ppls_ctx* c, const GramShape& g, int64_t n, int req, double* G, float* ms) {
+// events), if not null.  The partials are allocated here and freed, unless the caller passes them
+// (part_in, ppls_gram_part_doubles(g.p, nsplit) doubles; the caller frees them).
+int gram_run(ppls_ctx* c, const GramShape& g, int64_t n, int req, double* G, float* ms, double* part_in = nullptr) {
   int rc;
   const int nsplit = gram_nsplit(c, g, n, req);
-  double* part = nullptr;
+  double* part = part_in;
   int* q = nullptr;
-  if ((rc = dalloc(c, &part, (size_t)ppls_gram_part_doubles(g.p, nsplit)))) return rc;
-  if ((rc = gram_queue(c, g, n, req, &q))) { dfree(part); return rc; }
+  if (!part_in && (rc = dalloc(c, &part, (size_t)ppls_gram_part_doubles(g.p, nsplit)))) return rc;
+  if ((rc = gram_queue(c, g, n, req, &q))) { if (!part_in) dfree(part); return rc; }
   hipEvent_t e0 = nullptr, e1 = nullptr;
   hipError_t e = hipSuccess;
   if (ms) {
@@ -719,7 +723,7 @@ int gram_run(ppls_ctx* c, const GramShape& g, int64_t n, int req, double* G, flo
   if (e == hipSuccess && ms) e = hipEventElapsedTime(ms, e0, e1);
   if (e0) (void)hipEventDestroy(e0);
   if (e1) (void)hipEventDestroy(e1);
-  dfree(part);
+  if (!part_in) dfree(part);
   if (e != hipSuccess) return fail(c, PPLS_E_HIP, "MFMA Gram: %s", hipGetErrorString(e));
   return PPLS_OK;
 }
@@ -763,38 +767,43 @@ int xprod_setup(ppls_ctx* c) {
   const size_t PP = (size_t)P * P;
   int rc;
   const auto t0 = std::chrono::steady_clock::now();
-  // S (and, inside gram_run, the Gram partials); with collectives every rank must know that all ranks
-  // allocated S before anyone enters the all-reduce of S (a rank that returned here alone would leave
-  // the others waiting in it), so the allocation outcome is all-reduced first -- the partials are
-  // allocated beside S and released at once, so their outcome is part of it
+  // S, the Gram partials and the Gram's work queue; with collectives every rank must know that all
+  // ranks allocated them before anyone enters the all-reduce of S (a rank that returned here alone
+  // would leave the others waiting in it), so the allocation outcome is all-reduced first, and the
+  // partials and queue allocated here are the ones gram_run uses (no allocation after the agreement)
   const GramShape g = gram_shape(c, true, 0);
+  double* part = nullptr;
   int rc_alloc = dalloc(c, &c->xp_S, PP);
   if (!rc_alloc && c->n_local > 0) {
-    double* probe = nullptr;
-    rc_alloc = dalloc(c, &probe, (size_t)ppls_gram_part_doubles(P, gram_nsplit(c, g, c->n_local, 0)));
-    dfree(probe);
+    int* q = nullptr;
+    rc_alloc = dalloc(c, &part, (size_t)ppls_gram_part_doubles(P, gram_nsplit(c, g, c->n_local, 0)));
+    if (!rc_alloc) rc_alloc = gram_queue(c, g, c->n_local, 0, &q);
   }
   if (c->nranks > 1 || c->reducer) {
     const double f = rc_alloc ? 1.0 : 0.0;
     double tot = 0.0;
     HIPCHK(c, hipMemcpyAsync(c->flag, &f, sizeof f, hipMemcpyHostToDevice, c->stream));
-    if ((rc = allreduce(c, c->flag, 1))) { dfree(c->xp_S); return rc; }
+    if ((rc = allreduce(c, c->flag, 1))) { dfree(c->xp_S); dfree(part); return rc; }
     HIPCHK(c, hipMemcpyAsync(&tot, c->flag, sizeof tot, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     if (tot > 0.0) {
       dfree(c->xp_S);
+      dfree(part);
       return fail(c, PPLS_E_NOMEM, "cross-products S: %d rank(s) could not allocate %.3g GB of S and Gram partials",
                   (int)tot, xprod_bytes(c) / 1e9);
     }
   } else if (rc_alloc) {
     dfree(c->xp_S);
+    dfree(part);
     return rc_alloc;
   }
   c->xp_setup_ms = 0.0;
   if (c->n_local > 0) {
     c->xp_nsplit = gram_nsplit(c, g, c->n_local, 0);
     float ms = 0.f;
-    if ((rc = gram_run(c, g, c->n_local, 0, c->xp_S, &ms))) { dfree(c->xp_S); return rc; }
+    rc = gram_run(c, g, c->n_local, 0, c->xp_S, &ms, part);
+    dfree(part);
+    if (rc) { dfree(c->xp_S); return rc; }
     c->xp_setup_ms = ms;
   } else {
     HIPCHK(c, hipMemsetAsync(c->xp_S, 0, sizeof(double) * PP, c->stream));
@@ -2255,12 +2264,14 @@ int meta_ppls_device(ppls_ctx* c, const std::vector<MetaPop>& pops, const Rank1&
   int rc;
   PplsSweepArgs a;
   if (sweep_plan(c, 1, &a) != 3) return fail(c, PPLS_E_STATE, "meta device path needs the split sweep");
-  // workgroups per population: proportional to its local rows, at least one if it has any
+  // workgroups per population: proportional to its local rows, at least one if it has any.  A rank
+  // with no local rows (nz = 0) gets no workgroups: it launches no sweep, zeroes its K statistics
+  // blocks and still joins every all-reduce (the remainder loop below never ended there).
   int nz = 0;
   for (const auto& pp : pops) nz += pp.nloc > 0 ? 1 : 0;
-  const int G = std::max(a.grid, nz);
+  const int G = nz > 0 ? std::max(a.grid, nz) : 0;
   std::vector<int> gk((size_t)K, 0);
-  {
+  if (nz > 0) {
     int left = G;
     for (int j = 0; j < K; ++j) gk[(size_t)j] = pops[j].nloc > 0 ? 1 : 0;
     left -= nz;
@@ -2271,7 +2282,7 @@ int meta_ppls_device(ppls_ctx* c, const std::vector<MetaPop>& pops, const Rank1&
       gk[(size_t)j] += extra;
       left -= extra;
     }
-    for (int j = 0; left > 0; j = (j + 1) % K)   // the rounding remainder, one at a time
+    for (int j = 0; left > 0; j = (j + 1) % K)   // the rounding remainder, one at a time (nz > 0: ends)
       if (pops[j].nloc > 0) { ++gk[(size_t)j]; --left; }
   }
   std::vector<int64_t> bnd((size_t)G + 1);
@@ -2288,7 +2299,7 @@ int meta_ppls_device(ppls_ctx* c, const std::vector<MetaPop>& pops, const Rank1&
     g0[(size_t)K] = g;
     bnd[(size_t)G] = c->n_local;
   }
-  if ((rc = ensure_part(c, G))) return rc;
+  if ((rc = ensure_part(c, std::max(G, 1)))) return rc;
   if ((rc = ensure_stop(c)) || (rc = reset_stop(c))) return rc;
   struct Dev {
     int64_t* bnd = nullptr;
@@ -2309,7 +2320,7 @@ int meta_ppls_device(ppls_ctx* c, const std::vector<MetaPop>& pops, const Rank1&
   } d;
   d.c = c;
   const int64_t pld = c->part_ld, lld = (int64_t)max_steps + 1;
-  if ((rc = dalloc(c, &d.bnd, (size_t)G + 1)) || (rc = dalloc(c, &d.seg, (size_t)G)) ||
+  if ((rc = dalloc(c, &d.bnd, (size_t)G + 1)) || (rc = dalloc(c, &d.seg, (size_t)std::max(G, 1))) ||
       (rc = dalloc(c, &d.stats, (size_t)K * pld)) || (rc = dalloc(c, &d.N, (size_t)K)) ||
       (rc = dalloc(c, &d.ssq, (size_t)2 * K)) || (rc = dalloc(c, &d.log, (size_t)K * lld)) ||
       (rc = dalloc(c, &d.st, (size_t)K)) || (rc = dalloc(c, &d.sc, (size_t)K)))
@@ -2365,7 +2376,7 @@ int meta_ppls_device(ppls_ctx* c, const std::vector<MetaPop>& pops, const Rank1&
   double* tmp = c->part + (size_t)c->part_groups * pld;
   // one segmented sweep of the current parameters -> d.stats (K blocks, all-reduced)
   auto seg_sweep = [&]() -> int {
-    if (c->n_local > 0) HIPCHK(c, ppls_launch_sweep_split(&a, c->stream));
+    if (G > 0) HIPCHK(c, ppls_launch_sweep_split(&a, c->stream));
     for (int j = 0; j < K; ++j) {
       const int ng = g0[(size_t)j + 1] - g0[(size_t)j];
       if (ng > 0)

@@ -27,6 +27,16 @@ namespace {
 constexpr int NB = 64;     // block size
 constexpr int SL = 66;     // LDS row stride (doubles): 16-B aligned rows, writes 4-way at worst
 
+// LDS per workgroup: two 64 x 66 double tiles (67.6 KB; the diagonal-block kernel two 64 x 65) --
+// over the 64 KB of earlier CDNA parts, within gfx950's 160 KB.  gfx950 is the only target
+// (build.py's PPLS_OFFLOAD_ARCH would otherwise fail at launch, not at build).
+constexpr int kLdsLimit = 160 * 1024;
+static_assert(2 * NB * SL * sizeof(double) <= kLdsLimit, "ppls_linalg.hip: tile pair exceeds gfx950 LDS");
+static_assert(2 * NB * (NB + 1) * sizeof(double) <= kLdsLimit, "ppls_linalg.hip: diag tiles exceed gfx950 LDS");
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "ppls_linalg.hip needs gfx950 (67.6 KB of LDS per workgroup); build with --offload-arch=gfx950"
+#endif
+
 // An op(X) block (64 x 64, element (r, m)) of a column-major matrix with leading dimension ld into
 // LDS as s[m][r] (the micro-kernel's k-major image).  trans: op(X)(r, m) = X(m, r).  Elements past
 // `lim` rows / cols of the stored matrix read 0 (lim = valid extent of the block's rows and cols).

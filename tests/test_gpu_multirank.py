@@ -154,6 +154,39 @@ def test_k_contexts_initialiser_and_meta_sharded():
     assert np.allclose(m[3], ref[1][3], rtol=1e-12, atol=0, equal_nan=True)
 
 
+@pytest.mark.timeout(120)
+def test_k_contexts_meta_with_an_empty_shard():
+    """meta_PPLSi's device loop with a rank that holds no rows (its workgroup split never
+    ended there, and the others waited in the next all-reduce).  Shards [0, 500), [], [500, 700),
+    [700, 900): the empty rank launches no sweep, zeroes its statistics and joins every collective;
+    all ranks are bitwise equal and equal the unsharded fit."""
+    from ppls_amd import Context
+    from ppls_amd.api import initial_guess
+    n, p, q = 900, 60, 40
+    X, Y, _ = make_problem(n, p, q, 1, seed=11)
+    sizes = [300, 350, 250]
+    init = initial_guess(p, q, "equal")
+    shards = [(0, 500), (500, 0), (500, 200), (700, 200)]
+
+    with Context(0) as c:
+        c.set_data(X, Y)
+        ref = c.meta_ppls(sizes, 25, 1e-6, init)
+
+    def work(rank, c):
+        r0, nl = shards[rank]
+        c.set_data(X[r0:r0 + nl], Y[r0:r0 + nl], n_total=n)
+        c.row0 = r0
+        return c.meta_ppls(sizes, 25, 1e-6, init)
+
+    res = _run_ranks(len(shards), work)
+    for m in res:
+        assert np.array_equal(m[0], res[0][0]) and np.array_equal(m[2], res[0][2])
+    m = res[0]
+    assert np.abs(m[0] - ref[0]).max() < 1e-12 and np.abs(m[1] - ref[1]).max() < 1e-12
+    assert np.abs(m[2] - ref[2]).max() < 1e-11
+    assert np.allclose(m[3], ref[3], rtol=1e-12, atol=0, equal_nan=True)
+
+
 def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))

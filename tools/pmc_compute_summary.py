@@ -37,23 +37,33 @@ def profiled_tree():
     except (OSError, subprocess.CalledProcessError):
         return None
 
-def load(path, sub):
-    """{counter: average per dispatch} over the dispatches of kernels whose name contains sub."""
+def load(path, sub, ordinals=None):
+    """{counter: average per dispatch} over the dispatches of kernels whose name contains sub (only
+    those at the given ordinal positions in dispatch order, when ordinals is given)."""
     acc = defaultdict(lambda: defaultdict(float))
     names = set()
     for r in csv.DictReader(open(path)):
         if sub in r["Kernel_Name"]:
             acc[r["Counter_Name"]][r["Dispatch_Id"]] += float(r["Counter_Value"])
             names.add(r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0])
+    if ordinals is not None:
+        acc = {k: {d: v[d] for i, d in enumerate(sorted(v, key=int)) if i in ordinals} for k, v in acc.items()}
     return {k: sum(v.values()) / len(v) for k, v in acc.items()}, {k: len(v) for k, v in acc.items()}, names
 
 
 def main():
     args = sys.argv[1:]
-    trace = None
-    if "--trace" in args:
+    traces = []   # kernel-stats CSVs; the first that names a kernel gives its duration
+    while "--trace" in args:
         i = args.index("--trace")
-        trace = args[i + 1]
+        traces.append(args[i + 1])
+        del args[i:i + 2]
+    ordinals = {}   # kernel substring -> ordinals of its timed launches (tools/timed_launches.py)
+    while "--ordinals" in args:
+        i = args.index("--ordinals")
+        sub, path = args[i + 1].split("=", 1)
+        with open(path) as f:
+            ordinals[sub] = set(json.load(f)["ordinals"]["timed"])
         del args[i:i + 2]
     tag, workload, subs = args[0], args[1], args[2].split(",")
     base = os.path.join(ROOT, "gpurun_out", f"pmcc_{tag}")
@@ -61,16 +71,16 @@ def main():
                source=f"tools/pmc_compute.sh {tag} (rocprofv3 --pmc, 2 passes, separate runs)",
                profiled_tree=profiled_tree())
     durations = {}
-    if trace:
+    for trace in traces:
         for r in csv.DictReader(open(trace)):
-            durations[r["Name"].replace("(anonymous namespace)::", "").split("(")[0]] = float(r["AverageNs"])
+            durations.setdefault(r["Name"].replace("(anonymous namespace)::", "").split("(")[0], float(r["AverageNs"]))
     for sub in subs:
         c = {}
         n = {}
         names = set()
         for p in ("p1", "p2"):
             f = os.path.join(base, p, "run_counter_collection.csv")
-            vals, cnt, nm = load(f, sub)
+            vals, cnt, nm = load(f, sub, ordinals.get(sub))
             names |= nm
             for k, v in vals.items():
                 if k == "GRBM_GUI_ACTIVE" and k in c:
@@ -80,6 +90,7 @@ def main():
                 n[k] = cnt[k]
         cyc = c["GRBM_GUI_ACTIVE"] / 8.0
         d = dict(kernel=" / ".join(sorted(names)), dispatches=n.get("GRBM_GUI_ACTIVE"), counters=c,
+                 launches_selected="timed launches only" if sub in ordinals else "every launch",
                  cycles_per_xcd=cyc,
                  mfma_busy=c.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0) / (1024.0 * cyc),
                  valu_busy=c.get("SQ_ACTIVE_INST_VALU", 0.0) / (256.0 * cyc))

@@ -39,14 +39,35 @@ def profiled_tree():
     except (OSError, subprocess.CalledProcessError):
         return None
 
-def per_launch(path, counter, subs=("sweep",)):
-    """Sum over the kernels matching subs of the kernel's average counter value per dispatch."""
+def load_ordinals(path, phase="timed"):
+    """The ordinal positions (among the kernel's dispatches) of one phase's launches, from
+    tools/timed_launches.py's summary of the kernel trace of the same command."""
+    with open(path) as f:
+        return set(json.load(f)["ordinals"][phase])
+
+
+def keep_ordinals(acc, ordinals):
+    """acc {(kernel, dispatch id): value} restricted to the dispatches whose position in dispatch
+    order (per kernel name) is in ordinals (None: all)."""
+    if ordinals is None:
+        return acc
+    out = {}
+    for name in {k[0] for k in acc}:
+        ids = sorted((k for k in acc if k[0] == name), key=lambda k: int(k[1]))
+        out.update({k: acc[k] for i, k in enumerate(ids) if i in ordinals})
+    return out
+
+
+def per_launch(path, counter, subs=("sweep",), ordinals=None):
+    """Sum over the kernels matching subs of the kernel's average counter value per dispatch
+    (only the dispatches at the given ordinal positions, when ordinals is given)."""
     total, names, launches = 0.0, set(), 0
     for sub in subs:
         acc = defaultdict(float)
         for r in csv.DictReader(open(path)):
             if sub in r["Kernel_Name"] and r["Counter_Name"] == counter:
                 acc[(r["Kernel_Name"], r["Dispatch_Id"])] += float(r["Counter_Value"])
+        acc = keep_ordinals(acc, ordinals)
         names |= {k[0] for k in acc}
         launches = max(launches, len(acc))
         total += sum(acc.values()) / max(len(acc), 1)
@@ -65,12 +86,19 @@ def main():
         i = args.index("--kernels")
         subs = tuple(args[i + 1].split(","))
         del args[i:i + 2]
+    ordinals, ord_src = None, None
+    if "--ordinals" in args:   # only the timed launches (tools/timed_launches.py of the same command)
+        i = args.index("--ordinals")
+        ord_src = args[i + 1]
+        ordinals = load_ordinals(ord_src)
+        del args[i:i + 2]
     tag, workload, alg = args[0], args[1], int(float(args[2]))
     note = args[3] if len(args) > 3 else ""
     base = os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
     names, n, fetch = per_launch(os.path.join(base, "pmc_FETCH_SIZE", "run_counter_collection.csv"), "FETCH_SIZE",
-                                 subs)
-    _, _, write = per_launch(os.path.join(base, "pmc_WRITE_SIZE", "run_counter_collection.csv"), "WRITE_SIZE", subs)
+                                 subs, ordinals)
+    _, _, write = per_launch(os.path.join(base, "pmc_WRITE_SIZE", "run_counter_collection.csv"), "WRITE_SIZE", subs,
+                             ordinals)
     hbm = 2.0 * fetch * 1024 + write * 1024
     out = dict(workload=workload, kernel=" + ".join(sorted(k.split("(")[0] for k in names)) if names else None,
                launches=n,
@@ -80,6 +108,8 @@ def main():
                hbm_bytes_per_launch=hbm, algorithmic_bytes_per_launch=alg,
                traffic_over_algorithmic=hbm / alg,
                source=f"rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) -- python3 bench.py; {note}",
+               launches_selected=("the timed launches only (ordinals from " + os.path.basename(ord_src) + ")")
+               if ord_src else "every launch of the kernel",
                profiled_tree=profiled_tree())
     path = os.path.join(ROOT, "profiles", f"pmc_{out_name}.json" if out_name else f"pmc_sweep_{workload}.json")
     with open(path, "w") as f:
