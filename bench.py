@@ -138,6 +138,21 @@ def load_xprod_traffic(config):
     return None, None
 
 
+def load_timed_profile(config):
+    """The committed rocprofv3 kernel trace of this bench command (tools/r6_profiles.sh,
+    tools/timed_launches.py): the timed launches' average duration and roofline, split from the
+    warm-up and every other phase by roctx ranges -- a readback, or None."""
+    name = f"r6{config}_timed_launches.json"
+    js = _profile_json(name)
+    if not js:
+        return None
+    t = js["phases"]["timed"]
+    return dict(file=f"profiles/{name}", profiled_tree=js.get("profiled_tree"), command=js.get("command"),
+                kernel=js.get("kernel"), timed_launches=t["launches"], avg_ms=t["avg_ms"], min_ms=t["min_ms"],
+                max_ms=t["max_ms"], frac=t.get("frac"), line_of_that_run=js.get("bench_line"),
+                check=js.get("check"), kind=READBACK.replace("PMC summary", "kernel trace"))
+
+
 def load_compute_counters(workload_key, kernel_sub):
     """Counter-based MFMA / VALU utilisation of a kernel from a committed rocprofv3 PMC pass
     (profiles/pmc_compute_<workload>.json, tools/pmc_compute.sh + pmc_compute_summary.py), or None."""
@@ -159,6 +174,25 @@ def affinity_cores():
         return os.cpu_count() or 1
 
 
+def cgroup_cpus():
+    """The cgroup v2 CPU quota in CPUs (cpu.max "quota period"), or None when unlimited / absent."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        return None if quota == "max" else max(1, int(int(quota) // int(period)))
+    except (OSError, ValueError):
+        return None
+
+
+def usable_cores():
+    """All the CPU this process can use: its affinity mask, capped by the cgroup CPU quota.  On the
+    GPU box the mask holds 256 CPUs but cpu.max grants 16: 256 OpenMP threads there ran the C3
+    baseline at 0.21 it/s against 0.63 it/s on 16 (profiles/r6_bench_c3_first.log, round 6) --
+    threads beyond the quota only queue for it."""
+    q = cgroup_cpus()
+    return min(affinity_cores(), q) if q else affinity_cores()
+
+
 def host_cores():
     """What "all cores" means on this host: the machine's CPUs (os.cpu_count = nproc without an
     affinity mask), the CPUs this process may run on (its affinity mask), the inherited
@@ -171,7 +205,7 @@ def host_cores():
     except OSError:
         pass
     return dict(nproc=os.cpu_count(), affinity=affinity_cores(), omp_num_threads_env=os.environ.get("OMP_NUM_THREADS"),
-                cgroup_cpu_max=quota)
+                cgroup_cpu_max=quota, usable=usable_cores())
 
 
 def cpu_model():
@@ -188,15 +222,16 @@ def cpu_model():
 def cpu_baseline(ctx, th0, cfg, iters=3, one_core_rows=100_000):
     """Time the C restatement of the reference path (oracle/cpu_ref.c: its pass structure, OpenMP
     over rows) on the host cores, on the SAME rows the GPU holds (full n, >= 3 steady-
-    state iterations after one untimed iteration, OpenMP over every CPU of the affinity mask --
-    whatever OMP_NUM_THREADS the process inherited; the inherited thread count as a second figure;
-    plus 1 core on a row sample, scaled linearly in n), and compare the CPU's log-likelihood trace
-    and loadings with the GPU's first iterations from the same theta0."""
+    state iterations after one untimed iteration, OpenMP over all the CPU the process can use -- the
+    affinity mask capped by the cgroup quota, whatever OMP_NUM_THREADS it inherited; the inherited
+    thread count as a second figure when it differs; plus 1 core on a row sample, scaled linearly in
+    n), and compare the CPU's log-likelihood trace and loadings with the GPU's first iterations
+    from the same theta0."""
     from oracle import cpu_ref
     from oracle.ppls_oracle import canonicalize
     th = th0.as_dict()
     env_threads = cpu_ref.load().cpu_ref_max_threads()   # the runtime default (OMP_NUM_THREADS)
-    cores = affinity_cores()
+    cores = usable_cores()
     X, Y = ctx.get_data_rows()             # all rows, row-major (what cpu_ref streams)
 
     def timed(nthreads):   # 1 untimed iteration (faults the pages in, spins up OpenMP), then `iters`
@@ -234,7 +269,7 @@ def cpu_baseline(ctx, th0, cfg, iters=3, one_core_rows=100_000):
     return dict(value=iters / dt, unit="EM iterations/s", cores=int(cores), kind="port", host=host_cores(),
                 sample=f"{iters} steady-state EM iterations (after 1 untimed, {t_first:.1f} s) on all n={n} rows "
                        f"in {dt:.1f} s: oracle/cpu_ref.c (reference pass structure), OpenMP {cores} threads "
-                       f"(the affinity mask), -O3 -march=native, {cpu_model()}",
+                       f"(the affinity mask capped by the cgroup CPU quota), -O3 -march=native, {cpu_model()}",
                 inherited_threads=inherited,
                 one_core=dict(value=one_core, unit="EM iterations/s", cores=1,
                               sample=f"{iters} EM iterations on the first {ns} rows in {dt1:.1f} s, 1 thread; "
@@ -359,7 +394,7 @@ def cpu_call_baseline(ctx, r, cfg, device, rows):
     X, Y = ctx.get_data_rows(0, rows)
     rng = np.random.default_rng(CALL_SEED)
     inits = [initial_guess(cfg["p"], cfg["q"], "random", rng) for _ in range(r)]
-    cores = affinity_cores()
+    cores = usable_cores()
     t0 = time.perf_counter()
     est, ll, cs, secs = cpu_ref.ppls_simult_call(X, Y, r, inits, nthreads=cores)
     dt = time.perf_counter() - t0
@@ -611,7 +646,8 @@ def main():
                         grid=info["grid"], fp64_valu_tflops=tflops, fp64_valu_peak_tflops=FP64_PEAK_TF,
                         fp64_valu_frac=(tflops / FP64_PEAK_TF) if tflops else None,
                         measured_read_ceiling=READ_CEILING_GBS,
-                        frac_of_measured_ceiling=(achieved / READ_CEILING_GBS) if achieved else None)
+                        frac_of_measured_ceiling=(achieved / READ_CEILING_GBS) if achieved else None,
+                        profile=load_timed_profile(args.config) if world == 1 else None)
         # rocprofv3 PMC counters (SQ_VALU_MFMA_BUSY_CYCLES, SQ_ACTIVE_INST_VALU, GRBM_GUI_ACTIVE) of the
         # sweep kernel(s) at this workload, committed under profiles/ (readbacks, see their source)
         if info["variant"] == "panel":
