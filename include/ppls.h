@@ -103,9 +103,10 @@ const char* ppls_last_error(const ppls_ctx* ctx);
  *                non-zero to 0 (not for an S of ppls_xprod_prepare), or ppls_xprod_release; setting 0
  *                ends an ppls_em_begin session that reads S: ppls_em_iterate then returns
  *                PPLS_E_STATE until the next ppls_em_begin -- never a silent switch to streaming),
- *       "meta_device" (ppls_meta_ppls: 1, default, the whole loop on the device -- one segmented sweep
- *                      per EM step over every population; 0 the per-population loop driven by the host;
- *                      fp32 or panel-sweep data always take the latter),
+ *       "meta_device" (ppls_meta_ppls: 1, default, the whole loop on the device -- the statistics of
+ *                      every population from one read of X, Y per EM step (the split sweep: one
+ *                      segmented launch; fp32 storage / wide p, the panel sweep: one launch per
+ *                      population); 0 the per-population loop driven by the host),
  *       "vorth" (the finalize re-orthonormalises the Jacobi warm start it carries between
  *                iterations every vorth-th iteration: 1 .. 255, default 8),
  *       "xprod_rw" (rows of S per wave of the cross-product tile kernel: 0 auto, 1, 2, 4, 8),

@@ -45,6 +45,10 @@ int ppls_sweep_info(ppls_ctx* ctx, int r, int64_t* bytes_per_sweep, int* variant
 /* The sweep kernel instantiation the next EM iteration with r components launches, as text
  * (e.g. "split<5,4,512,2,false,4,4> nt"): tests assert the production kernel is the one checked. */
 int ppls_sweep_kernel(ppls_ctx* ctx, int r, char* buf, int len);
+/* The path the last ppls_meta_ppls took: 0 none yet, 1 the host loop, 2 the device loop on the split
+ * sweep (one segmented launch per EM step), 3 the device loop on the panel sweep (one launch per
+ * population and step). */
+int ppls_meta_info(ppls_ctx* ctx, int* path);
 /* The Gram D'D alone (D = X for xory 0, Y for 1; nsplit 0 = auto), for tests and benchmarks:
  * G (p x p, column-major, nullable), *ms = the MFMA kernel's duration. */
 int ppls_gram(ppls_ctx* ctx, int xory, int nsplit, double* G, double* ms);

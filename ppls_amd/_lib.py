@@ -118,6 +118,7 @@ SIGNATURES = {
     "ppls_sweep_info": (ct.c_int, [ct.c_void_p, ct.c_int, ct.POINTER(ct.c_int64), ct.POINTER(ct.c_int),
                                    ct.POINTER(ct.c_int)]),
     "ppls_sweep_kernel": (ct.c_int, [ct.c_void_p, ct.c_int, ct.c_char_p, ct.c_int]),
+    "ppls_meta_info": (ct.c_int, [ct.c_void_p, ct.POINTER(ct.c_int)]),
     "ppls_finalize_host": (ct.c_int, [_dp, _dp, _dp, ct.c_double, ct.c_double, ct.c_double, ct.c_int,
                                       ct.c_int, ct.c_int, ct.POINTER(PplsTheta), ct.c_int,
                                       ct.POINTER(PplsTheta), ct.POINTER(PplsExpect), _dp]),

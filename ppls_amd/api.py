@@ -517,6 +517,12 @@ class Context:
         self._chk(self._L.ppls_sweep_info(self.h, int(r), ct.byref(b), ct.byref(v), ct.byref(g)))
         return dict(bytes_per_sweep=b.value, variant={4: "split512", 5: "panel"}[v.value], grid=g.value)
 
+    def meta_info(self):
+        """The path the last meta_ppls took: "none", "host", "device_split" or "device_panel"."""
+        v = ct.c_int()
+        self._chk(self._L.ppls_meta_info(self.h, ct.byref(v)))
+        return ("none", "host", "device_split", "device_panel")[v.value]
+
     def sweep_kernel(self, r):
         """The sweep kernel instantiation an EM iteration with r components launches (text)."""
         buf = ct.create_string_buffer(256)

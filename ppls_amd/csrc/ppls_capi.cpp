@@ -127,6 +127,7 @@ struct ppls_ctx {
   bool xp_pending_gram = false;   // the last statistics step left the Gram B'M to the next finalize
   int xprod_fuse = 1;       // option "xprod_fuse": the finalize forms the Gram (r <= 8, P <= 6144)
   bool xp_explicit = false; // S was formed by ppls_xprod_prepare: kept until ppls_xprod_release / new data
+  int meta_path = 0;        // the last ppls_meta_ppls: 1 host loop, 2 device split, 3 device panel
   int meta_device = 1;      // option "meta_device": meta_PPLSi's loop on the device (1) or per population
                             // from the host (0; also where the split sweep does not apply)
   int vorth = 8;            // option "vorth": the finalize re-orthonormalises its carried Jacobi V every
@@ -2240,20 +2241,21 @@ int meta_sweep_all(ppls_ctx* c, std::vector<MetaPop>& pops, const std::vector<do
   return PPLS_OK;
 }
 
-// meta_PPLSi on the device (ppls_meta_step_kernel) when the r = 1 statistics take the split sweep
-// (fp64 storage, p and q within its register budget).  Wide or fp32-stored data keep the
-// per-population loop above (the panel sweep has no per-workgroup scalars).
+// meta_PPLSi on the device (ppls_meta_step_kernel) for every storage and shape: one segmented
+// sweep per EM step -- the split sweep (fp64, p and q within its register budget) or, round 6, the
+// panel sweep (fp32 storage, wide p).  Option meta_device = 0 keeps the per-population host loop.
 bool meta_device_ok(const ppls_ctx* c, int npop) {
-  return c->meta_device && npop >= 1 && npop <= PPLS_META_KMAX && !c->dtype && c->sweep_mode != 3 &&
-         ppls_split_supported(1, c->ldx, c->ldy) > 0;
+  return c->meta_device && npop >= 1 && npop <= PPLS_META_KMAX;
 }
 
-// The whole meta_PPLSi loop (EM_W_multi.R:544-578) on the device.  Per EM step ONE segmented split
-// sweep over all rows -- workgroups partitioned over the populations in proportion to their rows
-// (each workgroup's rows in one population, using that population's scalars) -- then per population
-// a reduction of its workgroups' partials, one all-reduce of the K statistics blocks when sharded,
-// and ppls_meta_step_kernel (log-likelihoods, stop rule, M-step, the next sweep's loadings and
-// scalars).  No host round trip per step: the host enqueues at most LOOKAHEAD steps ahead and
+// The whole meta_PPLSi loop (EM_W_multi.R:544-578) on the device.  Per EM step the statistics of
+// every population from ONE segmented sweep over X and Y -- the split sweep: workgroups partitioned
+// over the populations in proportion to their rows (each workgroup's rows in one population, using
+// that population's scalars); the panel sweep (fp32 storage, wide p): the dots give every row its
+// population's mu, and the accumulation's row chunks are partitioned like those workgroups -- then per
+// population a reduction of its workgroups' partials, one all-reduce of the K statistics blocks when
+// sharded, and ppls_meta_step_kernel (log-likelihoods, stop rule, M-step, the next sweep's loadings
+// and scalars).  No host round trip per step: the host enqueues at most LOOKAHEAD steps ahead and
 // stops launching once the step kernel reports the end of the fit (all ranks at the same step).
 // logvalue[1, ] comes from the first sweep (theta0 is every population's, so the full-data Gram is
 // the sum of theirs): no separate full-data sweep.
@@ -2263,15 +2265,21 @@ int meta_ppls_device(ppls_ctx* c, const std::vector<MetaPop>& pops, const Rank1&
   const int p = c->p, q = c->q;
   int rc;
   PplsSweepArgs a;
-  if (sweep_plan(c, 1, &a) != 3) return fail(c, PPLS_E_STATE, "meta device path needs the split sweep");
+  const int plan = sweep_plan(c, 1, &a);
+  if (plan != 3 && plan != 4) return fail(c, PPLS_E_STATE, "meta device path: no sweep for this shape");
+  const bool panel = plan == 4;
+  c->meta_path = panel ? 3 : 2;
   // workgroups per population: proportional to its local rows, at least one if it has any.  A rank
   // with no local rows (nz = 0) gets no workgroups: it launches no sweep, zeroes its K statistics
   // blocks and still joins every all-reduce (the remainder loop below never ended there).
+  // Panel: the same partition of the accumulation's row chunks (a.grid: the chunk policy of a sweep of
+  // every local row), so each chunk lies in one population.
   int nz = 0;
   for (const auto& pp : pops) nz += pp.nloc > 0 ? 1 : 0;
-  const int G = nz > 0 ? std::max(a.grid, nz) : 0;
   std::vector<int> gk((size_t)K, 0);
+  int G = 0;
   if (nz > 0) {
+    G = std::max(a.grid, nz);
     int left = G;
     for (int j = 0; j < K; ++j) gk[(size_t)j] = pops[j].nloc > 0 ? 1 : 0;
     left -= nz;
@@ -2300,9 +2308,16 @@ int meta_ppls_device(ppls_ctx* c, const std::vector<MetaPop>& pops, const Rank1&
     bnd[(size_t)G] = c->n_local;
   }
   if ((rc = ensure_part(c, std::max(G, 1)))) return rc;
+  if (panel && c->z_cols < 4) {   // Z = [Xw | Yc | mu_T | mu_U] rows + the transposed W, C
+    dfree(c->Z);
+    c->z_cols = 0;
+    if ((rc = dalloc(c, &c->Z, (size_t)ppls_panel_z_len(c->n_local, c->ldx, c->ldy, 1)))) return rc;
+    c->z_cols = 4;
+  }
   if ((rc = ensure_stop(c)) || (rc = reset_stop(c))) return rc;
   struct Dev {
     int64_t* bnd = nullptr;
+    int64_t* segend = nullptr;
     int* seg = nullptr;
     double* stats = nullptr;
     double* N = nullptr;
@@ -2313,7 +2328,7 @@ int meta_ppls_device(ppls_ctx* c, const std::vector<MetaPop>& pops, const Rank1&
     ppls_ctx* c = nullptr;
     std::vector<hipEvent_t> evs;
     ~Dev() {
-      dfree(bnd); dfree(seg); dfree(stats); dfree(N); dfree(ssq); dfree(log); dfree(st); dfree(sc);
+      dfree(bnd); dfree(segend); dfree(seg); dfree(stats); dfree(N); dfree(ssq); dfree(log); dfree(st); dfree(sc);
       if (c) c->sweep_stop = nullptr;
       for (auto e : evs) (void)hipEventDestroy(e);
     }
@@ -2321,6 +2336,7 @@ int meta_ppls_device(ppls_ctx* c, const std::vector<MetaPop>& pops, const Rank1&
   d.c = c;
   const int64_t pld = c->part_ld, lld = (int64_t)max_steps + 1;
   if ((rc = dalloc(c, &d.bnd, (size_t)G + 1)) || (rc = dalloc(c, &d.seg, (size_t)std::max(G, 1))) ||
+      (rc = dalloc(c, &d.segend, (size_t)K)) ||
       (rc = dalloc(c, &d.stats, (size_t)K * pld)) || (rc = dalloc(c, &d.N, (size_t)K)) ||
       (rc = dalloc(c, &d.ssq, (size_t)2 * K)) || (rc = dalloc(c, &d.log, (size_t)K * lld)) ||
       (rc = dalloc(c, &d.st, (size_t)K)) || (rc = dalloc(c, &d.sc, (size_t)K)))
@@ -2340,6 +2356,9 @@ int meta_ppls_device(ppls_ctx* c, const std::vector<MetaPop>& pops, const Rank1&
     std::copy(t0.c.begin(), t0.c.end(), cv.begin());
     HIPCHK(c, hipMemcpyAsync(d.bnd, bnd.data(), sizeof(int64_t) * bnd.size(), hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipMemcpyAsync(d.seg, seg.data(), sizeof(int) * seg.size(), hipMemcpyHostToDevice, c->stream));
+    std::vector<int64_t> se((size_t)K);
+    for (int j = 0; j < K; ++j) se[(size_t)j] = pops[j].row0 + pops[j].nloc;
+    HIPCHK(c, hipMemcpyAsync(d.segend, se.data(), sizeof(int64_t) * K, hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipMemcpyAsync(d.N, hN.data(), sizeof(double) * K, hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipMemcpyAsync(d.ssq, hs.data(), sizeof(double) * 2 * K, hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipMemcpyAsync(d.log, hl.data(), sizeof(double) * hl.size(), hipMemcpyHostToDevice, c->stream));
@@ -2375,8 +2394,18 @@ int meta_ppls_device(ppls_ctx* c, const std::vector<MetaPop>& pops, const Rank1&
   m.ssqX = c->ssq_host[0]; m.ssqY = c->ssq_host[1]; m.Ntot = (double)c->n_total;
   double* tmp = c->part + (size_t)c->part_groups * pld;
   // one segmented sweep of the current parameters -> d.stats (K blocks, all-reduced)
+  if (panel) {   // the dots use each row's population scalars; the accumulation's chunks are bnd
+    a.row_bounds = nullptr;
+    a.wg_seg = nullptr;
+    a.seg_ends = d.segend;
+    a.nseg = K;
+    a.chunk_bounds = d.bnd;
+  }
   auto seg_sweep = [&]() -> int {
-    if (G > 0) HIPCHK(c, ppls_launch_sweep_split(&a, c->stream));
+    if (G > 0) {
+      if (panel) HIPCHK(c, ppls_launch_sweep_panel(&a, c->dtype, c->Z, G, c->stream));
+      else HIPCHK(c, ppls_launch_sweep_split(&a, c->stream));
+    }
     for (int j = 0; j < K; ++j) {
       const int ng = g0[(size_t)j + 1] - g0[(size_t)j];
       if (ng > 0)
@@ -2494,6 +2523,7 @@ int ppls_meta_ppls(ppls_ctx* c, int npop, const int64_t* pop_local, const int64_
   if (out->log)
     for (size_t e = 0; e < ld * npop; ++e) out->log[e] = NAN;
   if (meta_device_ok(c, npop)) return meta_ppls_device(c, pops, t0, max_steps, atol, crit_abs, out);
+  c->meta_path = 1;
   // logvalue[1, ] = rep(logl_W(X, Y, Wnw, Cnw, Bnw, ...), K) (:544): one full-data sweep
   {
     std::vector<double> SX, SY;
@@ -3073,6 +3103,12 @@ int ppls_sweep_info(ppls_ctx* c, int r, int64_t* bytes_per_sweep, int* variant, 
   if (bytes_per_sweep) *bytes_per_sweep = (int64_t)(c->dtype ? 4 : 8) * c->n_local * ((int64_t)c->p + c->q);
   if (variant) *variant = plan == 4 ? 5 : plan == 3 ? 4 : 2;
   if (grid) *grid = a.grid;
+  return PPLS_OK;
+}
+
+int ppls_meta_info(ppls_ctx* c, int* path) {
+  if (!c || !path) return PPLS_E_ARG;
+  *path = c->meta_path;
   return PPLS_OK;
 }
 

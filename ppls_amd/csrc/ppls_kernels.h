@@ -41,6 +41,10 @@ struct PplsSweepArgs {
                                // [b[g], b[g+1])), or nullptr for the even split
   const int* wg_seg;           // split sweep: per workgroup the index of its scalars (sc[wg_seg[g]]:
                                // meta_PPLSi's populations), or nullptr (sc for all)
+  const int64_t* seg_ends;     // panel sweep, meta_PPLSi: nseg cumulative row ends of the populations;
+  int nseg;                    // row i uses sc[j], j the first segment with i < seg_ends[j] (or nullptr)
+  const int64_t* chunk_bounds; // panel accumulation: grid + 1 row boundaries of its chunks (each inside
+                               // one population), or nullptr for the guided default
 };
 
 struct PplsFinalizeArgs {

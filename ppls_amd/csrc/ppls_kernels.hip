@@ -693,7 +693,7 @@ __global__ __launch_bounds__(256) void ppls_panel_mfmadots_kernel(
     const T* __restrict__ X, const T* __restrict__ Y, int64_t n, int ldx, int ldy, int px, int py,
     const double* __restrict__ Wt, const double* __restrict__ Ct, const PplsScalars* __restrict__ sc,
     double* __restrict__ Z, double* __restrict__ mu,
-    const int* __restrict__ stop) {
+    const int* __restrict__ stop, const int64_t* __restrict__ seg_ends, int nseg) {
   if (stop && *stop) return;   // em_run converged earlier (device stop flag)
   // Round 3 at the C5 share (compile-time ablations of an experiment build: no MFMAs, no X loads,
   // no B loads -- every variant ran 574-591 us, profiles/r3_dots_ablate_c5s.txt): the per-tile LDS
@@ -833,14 +833,35 @@ __global__ __launch_bounds__(256) void ppls_panel_mfmadots_kernel(
       __syncthreads();   // the buffer is the partner's again
     }
     if (active && part == 0 && i16 < R) {
+      // segmented (meta_PPLSi): each row's population scalars; the lane's rows increase, so its
+      // segment index only moves forward from the tile's first row's (a wave-uniform binary search)
+      int sj = 0;
+      if (seg_ends) {
+        int lo = 0, hi = nseg - 1;
+        while (lo < hi) {
+          const int mid = (lo + hi) >> 1;
+          if (row0 < seg_ends[mid]) hi = mid;
+          else lo = mid + 1;
+        }
+        sj = lo;
+      }
 #pragma unroll
       for (int blk = 0; blk < NB; ++blk)
 #pragma unroll
         for (int reg = 0; reg < 4; ++reg) {
           const int64_t row = row0 + 16 * blk + kq + 4 * reg;
           if (row >= n) continue;
+          double cal = al, cbe = be, cga = ga, cde = de;
+          if (seg_ends) {
+            while (sj + 1 < nseg && row >= seg_ends[sj]) ++sj;
+            const PplsScalars* ss = sc + sj;
+            cal = ss->alpha[comp];
+            cbe = ss->beta[comp];
+            cga = ss->gamma[comp];
+            cde = ss->delta[comp];
+          }
           const double a = res[0][blk][reg], bb = res[1][blk][reg];
-          const double mt = al * a + be * bb, mu_u = ga * a + de * bb;
+          const double mt = cal * a + cbe * bb, mu_u = cga * a + cde * bb;
           double* zr = Z + row * V4;
           zr[i16] = a;
           zr[R + i16] = bb;
@@ -879,10 +900,17 @@ __global__ void ppls_transpose_wc_kernel(const double* __restrict__ W, const dou
 // rows (a guided static schedule: workgroups are dispatched in chunk order, so the large chunks run
 // first and the small ones fill the tail; fewer partials to write and reduce than equal chunks with
 // the same tail).  Fixed by (n, chunk count), so results stay deterministic.
+// bnd (meta_PPLSi on the panel sweep): explicit boundaries instead, each chunk inside one population.
 struct PplsChunks {
   int64_t big, small;
   int nbig;
+  const int64_t* bnd;
   __host__ __device__ void range(int c, int64_t n, int64_t& r0, int64_t& r1) const {
+    if (bnd) {
+      r0 = bnd[c];
+      r1 = bnd[c + 1];
+      return;
+    }
     r0 = c < nbig ? (int64_t)c * big : (int64_t)nbig * big + (int64_t)(c - nbig) * small;
     const int64_t len = c < nbig ? big : small;
     if (r0 > n) r0 = n;
@@ -2776,7 +2804,8 @@ hipError_t launch_panel_t(const PplsSweepArgs* a, const T* X, const T* Y, double
     // allocator before they landed in some instantiations)
 #define PPLS_LAUNCH_DOTS(NBV, KSV, NTV)                                                              \
   hipLaunchKernelGGL((ppls_panel_mfmadots_kernel<T, R, NBV, KSV, NTV>), dim3(mblocks), dim3(256), 0, st, X, Y, \
-                     a->n_local, a->ldx, a->ldy, a->p, a->q, Wt, Ct, a->sc, Z, mu_out, a->stop)
+                     a->n_local, a->ldx, a->ldy, a->p, a->q, Wt, Ct, a->sc, Z, mu_out, a->stop, a->seg_ends, \
+                     a->nseg)
     if (a->nt) {
       if (rb == 64 && ks == 2) PPLS_LAUNCH_DOTS(4, 2, true);
       else if (rb == 64) PPLS_LAUNCH_DOTS(4, 1, true);
@@ -2793,6 +2822,7 @@ hipError_t launch_panel_t(const PplsSweepArgs* a, const T* X, const T* Y, double
   constexpr int VEC = PplsVec16<T>::N;
   if (a->dots_only) return hipGetLastError();   // scores: Z and mu only
   PplsChunks ck;   // half the chunks at 4x the rows of the other half (equal chunks: profiles/r2_c5_dots_rows.txt)
+  ck.bnd = a->chunk_bounds;
   ck.nbig = chunks / 2;
   const int nsmall = chunks - ck.nbig;
   ck.big = (4 * a->n_local + 4 * ck.nbig + nsmall - 1) / (4 * ck.nbig + nsmall);

@@ -97,24 +97,33 @@ def test_meta_rejects_bad_populations(ctx):
         ctx.meta_ppls([50, 0], 5, 1e-4, init)        # an empty level
 
 
+@pytest.mark.parametrize("storage", ["f64", "f32", "wide"])
 @pytest.mark.parametrize("sizes,atol", [([300, 250, 200, 250], 1e-6), ([997], -np.inf), ([3, 500, 2, 495], 1e-5),
                                         ([40] * 25, -np.inf)],
                          ids=["K4_stop", "K1", "tiny_pops", "K25"])
-def test_meta_device_loop_equals_host_loop(ctx, sizes, atol):
-    """The device meta_PPLSi (one segmented sweep per EM step over every population, the M-step, the
-    log-likelihoods and the stop rule in one kernel; option meta_device = 1, the default) against the
-    per-population host loop (meta_device = 0) and the oracle: the same steps, log-likelihoods to
-    1e-12, loadings and parameters to 1e-10 (the sums are regrouped: the device sweep partitions the
-    workgroups over the populations)."""
+def test_meta_device_loop_equals_host_loop(ctx, sizes, atol, storage):
+    """The device meta_PPLSi (the statistics of every population from one read of X, Y per EM step,
+    the M-step, the log-likelihoods and the stop rule in one kernel; option meta_device = 1, the
+    default) against the per-population host loop (meta_device = 0) and the oracle: the same steps,
+    log-likelihoods to 1e-12, loadings and parameters to 1e-10 (the sums are regrouped).  storage:
+    fp64 (the split sweep, one segmented launch), fp32 storage and fp64 wide p (the panel sweep, one
+    launch per population) -- fp32 against the oracle on the fp32-rounded data."""
     n = int(sum(sizes))
-    X, Y, _ = make_problem(n, 37, 29, 1, seed=n)
-    init = o.initial_guess(37, 29, "equal")
+    p, q = (4200, 29) if storage == "wide" else (37, 29)
+    X, Y, _ = make_problem(n, p, q, 1, seed=n)
+    if storage == "f32":
+        X = X.astype(np.float32).astype(np.float64)
+        Y = Y.astype(np.float32).astype(np.float64)
+    init = o.initial_guess(p, q, "equal")
+    ctx.set_option("dtype", 1 if storage == "f32" else 0)
     ctx.set_data(X, Y)
     res = {}
     for dev in (1, 0):
         ctx.set_option("meta_device", dev)
         res[dev] = ctx.meta_ppls(sizes, 40, atol, init)
+        assert ctx.meta_info() == ("host" if not dev else "device_split" if storage == "f64" else "device_panel")
     ctx.set_option("meta_device", 1)
+    ctx.set_option("dtype", 0)
     (W1, C1, P1, L1), (W0, C0, P0, L0) = res[1], res[0]
     assert L1.shape == L0.shape
     assert _relerr(L1, L0) < 1e-12
