@@ -48,6 +48,7 @@ READ_CEILING_GBS = 6848.0   # measured read-only ceiling, profiles/r1_read_bw_pr
 MALL_REREAD_GBS = 6800.0    # measured re-read of a 128 MB (MALL-resident) buffer, low end of 6.8-7.8 TB/s
                             # (profiles/r3_mall_read_probe.txt, tools/mall_read_probe.hip)
 FP64_PEAK_TF = 78.6     # MI355X fp64 vector (= fp64 MFMA) dense peak, TFLOP/s
+INT8_PEAK_TOPS = 5000.0  # MI355X int8 MFMA dense peak (2x BF16's 2.5 PF, MI355X_MICROARCH.md:435), TOP/s
 CALL_SEED = 20261017    # numpy stream of the 'random' initial guesses of the timed PPLS_simult calls
 READBACK = "readback of a committed rocprofv3 PMC summary under profiles/ (not measured in this run)"
 
@@ -322,6 +323,28 @@ def bench_xprod(ctx, th0, args, barrier, tmax, r, ll_stream, t_stream):
     useful = float(ctx.n_local) * Pr * (Pr + 1.0)   # this rank's rows: its kernel's time
     gram_tf = useful / (gram_ms * 1e-3) / 1e12 if gram_ms > 0 else None
     traffic, traffic_src = load_xprod_traffic(args.config)
+    gi = ctx.gram_info()
+    if gi["int8"]:
+        # the int8 CRT form (ppls_ozaki.hip): nmod int8 SYRKs of residue planes; the SYRK kernel's
+        # rate against the int8 MFMA peak, and the whole Gram's fp64-equivalent rate (gram_tflops)
+        syrk_ms = gi["ms"][1]
+        tops = gi["nmod"] * useful / (syrk_ms * 1e-3) / 1e12 if syrk_ms > 0 else None
+        gram_roof = dict(bound="mfma", achieved=tops, peak=INT8_PEAK_TOPS, unit="TOP/s",
+                         frac=(tops / INT8_PEAK_TOPS) if tops else None,
+                         kernel="ppls_oz_syrk_kernel<514> (v_mfma_i32_32x32x32_i8), one plane per modulus",
+                         ops_per_launch=gi["nmod"] * useful,
+                         ops="useful: nmod n P (P + 1), P = p + q, this rank's rows",
+                         fp64_equivalent_tflops=gram_tf, fp64_equivalent_frac_of_fp64_peak=(gram_tf / FP64_PEAK_TF)
+                         if gram_tf else None)
+        gram_path = dict(path="int8-crt", nmod=gi["nmod"], L=gi["L"],
+                         ms=dict(stats_and_residues=gi["ms"][0], syrk=gi["ms"][1], crt=gi["ms"][2], total=gi["ms"][3]))
+    else:
+        gram_roof = dict(bound="mfma", achieved=gram_tf, peak=FP64_PEAK_TF, unit="TFLOP/s",
+                         frac=(gram_tf / FP64_PEAK_TF) if gram_tf else None,
+                         flops_per_launch=useful, flops="useful: n P (P + 1), P = p + q, this rank's rows",
+                         tile_flops_per_launch=info["gram_flops"],
+                         counters=load_compute_counters(f"{args.config}_dp1", "gram_mfma"))
+        gram_path = dict(path="fp64-mfma")
 
     def fit_s(steps):   # a PPLS_simult loop of `steps` iterations (+1 sweep for the last loglik)
         return dict(stream=(steps + 1) * t_stream, xprod=t_setup + (steps + 1) * t_x)
@@ -331,12 +354,7 @@ def bench_xprod(ctx, th0, args, barrier, tmax, r, ll_stream, t_stream):
              "iteration reads S instead of X, Y (no per-iteration collective); same iterates, sums reordered",
         setup_s=t_setup, gram_kernel_ms=gram_ms, gram_tflops=gram_tf,
         setup_allreduce_ms=ar_ms, setup_allreduce_bytes=info["bytes_per_pass"] if ar_ms > 0 else 0,
-        setup_total_ms_rank0=total_ms,
-        gram_roofline=dict(bound="mfma", achieved=gram_tf, peak=FP64_PEAK_TF, unit="TFLOP/s",
-                           frac=(gram_tf / FP64_PEAK_TF) if gram_tf else None,
-                           flops_per_launch=useful, flops="useful: n P (P + 1), P = p + q, this rank's rows",
-                           tile_flops_per_launch=info["gram_flops"],
-                           counters=load_compute_counters(f"{args.config}_dp1", "gram_mfma")),
+        setup_total_ms_rank0=total_ms, gram=gram_path, gram_roofline=gram_roof,
         steps=args.xprod_steps, ms_per_step=1e3 * t_x, it_per_s=1.0 / t_x,
         roofline=dict(bound="hbm", achieved=achieved, peak=HBM_PEAK_GBS, unit="GB/s",
                       frac=(achieved / HBM_PEAK_GBS) if achieved else None,
@@ -376,6 +394,10 @@ def bench_call(ctx, r, barrier, tmax):
         out[mode] = dict(seconds=dt, init_seconds=tmax(tm["init"]), loop_seconds=tmax(tm["loop"]),
                          init_steps=[int(v) for v in tm["init_steps"]], em_steps=int(len(ll)),
                          read_S=bool(ctx.xprod_info(r)["ready"]), loglik_last=float(ll[-1]))
+        if out[mode]["read_S"]:
+            gi = ctx.gram_info()
+            out[mode]["gram"] = "int8-crt" if gi["int8"] else "fp64-mfma"
+            out[mode]["gram_ms"] = gi["ms"][3] if gi["int8"] else None
         out[f"_{mode}_fit"] = fit
     ctx.set_option("xprod", 0)
     ref = out["stream"]["loglik_last"]
@@ -484,6 +506,9 @@ def main():
     ap.add_argument("--xprod-steps", type=int, default=2000,
                     help="iterations of the cross-product form timed after the headline (0: skip it)")
     ap.add_argument("--no-call", action="store_true", help="skip the whole-call PPLS_simult timings")
+    ap.add_argument("--gram-int8", type=int, default=None, choices=[0, 1],
+                    help="the Gram that forms S for the xprod / call sections: 1 the int8-MFMA CRT form "
+                         "(ppls_ozaki.hip), 0 the fp64 MFMA Gram (default: the library's default)")
     ap.add_argument("--comm", default="rccl", choices=["rccl", "host"],
                     help="N>1 statistics all-reduce: RCCL (default) or the host reducer hook over gloo "
                          "(ppls_set_reducer; rehearses the multi-rank bench with several ranks on one GPU)")
@@ -522,6 +547,8 @@ def main():
     if cfg.get("storage") == "f32":
         ctx.set_option("dtype", 1)
     ctx.set_option("sweep", args.sweep)
+    if args.gram_int8 is not None:
+        ctx.set_option("gram_int8", args.gram_int8)
     if world > 1 and args.comm == "rccl":
         uid = [Context.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
@@ -660,13 +687,20 @@ def main():
             # X'mu_T runs on fp64 VALU (r = 5 fills 5 of an MFMA's 16 columns, gfx950's fp64 MFMA and
             # VALU rates are equal, and the sweep already sits at its HBM read ceiling)
             g = xp["gram_roofline"]
-            roofline["mfma_gemm"] = dict(
-                gemm="S = [X Y]'[X Y], the cross-product form of the M-step sums X'mu_T, Y'mu_U and the E-step Gram "
-                     "(EM_W_multi.R:689-690, 732-733); variances.PPLS_simult's X'X (:846) runs the same kernel",
-                kernel="ppls_gram_mfma_kernel (v_mfma_f64_16x16x4_f64)", fp64_mfma_tflops=g["achieved"],
-                peak_tflops=FP64_PEAK_TF, frac=g["frac"], kernel_ms=xp["gram_kernel_ms"],
-                flops=g["flops"], counters=g["counters"],
-                sweep_note="the streaming sweep's X'mu_T / Y'mu_U run on fp64 VALU (counters.sweep_split)")
+            gemm = ("S = [X Y]'[X Y], the cross-product form of the M-step sums X'mu_T, Y'mu_U and the E-step "
+                    "Gram (EM_W_multi.R:689-690, 732-733); variances.PPLS_simult's X'X (:846) runs the same kernel")
+            note = "the streaming sweep's X'mu_T / Y'mu_U run on fp64 VALU (counters.sweep_split)"
+            if xp["gram"]["path"] == "int8-crt":
+                roofline["mfma_gemm"] = dict(
+                    gemm=gemm, kernel=g["kernel"], int8_mfma_tops=g["achieved"], peak_tops=INT8_PEAK_TOPS,
+                    frac=g["frac"], syrk_ms=xp["gram"]["ms"]["syrk"], kernel_ms=xp["gram_kernel_ms"],
+                    nmod=xp["gram"]["nmod"], ops=g["ops"], fp64_equivalent_tflops=g["fp64_equivalent_tflops"],
+                    sweep_note=note)
+            else:
+                roofline["mfma_gemm"] = dict(
+                    gemm=gemm, kernel="ppls_gram_mfma_kernel (v_mfma_f64_16x16x4_f64)", fp64_mfma_tflops=g["achieved"],
+                    peak_tflops=FP64_PEAK_TF, frac=g["frac"], kernel_ms=xp["gram_kernel_ms"],
+                    flops=g["flops"], counters=g["counters"], sweep_note=note)
         out = dict(metric=METRIC, value=its, unit="EM iterations/s", n_gpus=world, steps=args.steps,
                    warmup=args.warmup, ms_per_step=1e3 * dt / args.steps, higher_is_better=True,
                    scaling="strong", vs_baseline=None, dtype="f64",

@@ -45,6 +45,19 @@ int ppls_sweep_info(ppls_ctx* ctx, int r, int64_t* bytes_per_sweep, int* variant
 /* The sweep kernel instantiation the next EM iteration with r components launches, as text
  * (e.g. "split<5,4,512,2,false,4,4> nt"): tests assert the production kernel is the one checked. */
 int ppls_sweep_kernel(ppls_ctx* ctx, int r, char* buf, int len);
+/* The Gram by the int8-MFMA Chinese-remainder form (ppls_ozaki.hip) alone, for tests and
+ * benchmarks: which = 0 X'X, 1 Y'Y, 2 the joint [X Y]'[X Y] (P = ldx + ldy, padding columns 0);
+ * G (column-major, nullable); *nmod moduli, *L bits per integer; ms[4] = stats + residues, SYRK,
+ * CRT, total (HIP events).  PPLS_E_NUMERIC when the columns' spread is too wide for it. */
+int ppls_gram_int8(ppls_ctx* ctx, int which, double* G, int* nmod, int* L, double* ms);
+/* Host copies of the int8 Gram's arithmetic (no GPU needed; tests/test_ozaki_host.py): the symmetric
+ * residue of x' = rint(x 2^shift) modulo the l-th modulus (|x'| < 2^62), the l-th modulus, and the
+ * CRT of nmod residues (0 <= r_l < m_l) to the nearest double of the integer in (-M/2, M/2). */
+int ppls_oz_residue_host(double x, int shift, int l, int* r);
+int ppls_oz_crt_host(const int* r, int nmod, double* out);
+int ppls_oz_modulus(int l);
+/* Which Gram formed the last S (1 int8 CRT form, 0 fp64 MFMA), its moduli, bits and phases (ms[4]). */
+int ppls_gram_info(ppls_ctx* ctx, int* int8_used, int* nmod, int* L, double* ms);
 /* The path the last ppls_meta_ppls took: 0 none yet, 1 the host loop, 2 the device loop on the split
  * sweep (one segmented launch per EM step), 3 the device loop on the panel sweep (one launch per
  * population and step). */

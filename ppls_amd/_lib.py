@@ -119,6 +119,12 @@ SIGNATURES = {
                                    ct.POINTER(ct.c_int)]),
     "ppls_sweep_kernel": (ct.c_int, [ct.c_void_p, ct.c_int, ct.c_char_p, ct.c_int]),
     "ppls_meta_info": (ct.c_int, [ct.c_void_p, ct.POINTER(ct.c_int)]),
+    "ppls_gram_int8": (ct.c_int, [ct.c_void_p, ct.c_int, _dp, ct.POINTER(ct.c_int), ct.POINTER(ct.c_int), _dp]),
+    "ppls_oz_residue_host": (ct.c_int, [ct.c_double, ct.c_int, ct.c_int, ct.POINTER(ct.c_int)]),
+    "ppls_oz_crt_host": (ct.c_int, [ct.POINTER(ct.c_int), ct.c_int, _dp]),
+    "ppls_oz_modulus": (ct.c_int, [ct.c_int]),
+    "ppls_gram_info": (ct.c_int, [ct.c_void_p, ct.POINTER(ct.c_int), ct.POINTER(ct.c_int), ct.POINTER(ct.c_int),
+                                  _dp]),
     "ppls_finalize_host": (ct.c_int, [_dp, _dp, _dp, ct.c_double, ct.c_double, ct.c_double, ct.c_int,
                                       ct.c_int, ct.c_int, ct.POINTER(PplsTheta), ct.c_int,
                                       ct.POINTER(PplsTheta), ct.POINTER(PplsExpect), _dp]),

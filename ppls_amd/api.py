@@ -368,6 +368,22 @@ class Context:
         self._chk(self._L.ppls_gram(self.h, int(xory), int(nsplit), dptr(G), ct.byref(ms)))
         return G, ms.value
 
+    def gram_int8(self, which=2, want=True):
+        """The Gram by the int8-MFMA Chinese-remainder form alone (which: 0 X'X, 1 Y'Y, 2 the joint
+        [X Y]'[X Y] over the padded columns) -> (G or None, dict(nmod, L, ms = [stats + residues, SYRK,
+        CRT, total]))."""
+        P = self.p if which == 0 else self.q if which == 1 else int(round(np.sqrt(self.xprod_info()["bytes_per_pass"] / 8)))
+        G = np.zeros((P, P), order="F") if want else None
+        nm, L, ms = ct.c_int(), ct.c_int(), np.zeros(4)
+        self._chk(self._L.ppls_gram_int8(self.h, int(which), dptr(G), ct.byref(nm), ct.byref(L), dptr(ms)))
+        return G, dict(nmod=nm.value, L=L.value, ms=ms.tolist())
+
+    def gram_info(self):
+        """Which Gram formed the last S: dict(int8 (bool), nmod, L, ms = [stats + residues, SYRK, CRT, total])."""
+        u, nm, L, ms = ct.c_int(), ct.c_int(), ct.c_int(), np.zeros(4)
+        self._chk(self._L.ppls_gram_info(self.h, ct.byref(u), ct.byref(nm), ct.byref(L), dptr(ms)))
+        return dict(int8=bool(u.value), nmod=nm.value, L=L.value, ms=ms.tolist())
+
     def spd_inverse(self, A, method=1):
         """Inverses of symmetric positive definite matrices A (a x p x p or p x p) on the device as
         variances.PPLS_simult computes them (method 1 hand-written blocked Cholesky, 2 rocSOLVER)

@@ -17,7 +17,8 @@ LIB = os.path.join(HERE, "libppls_amd.so")
 ARCH = os.environ.get("PPLS_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
-SOURCES = ["ppls_kernels.hip", "ppls_variances.hip", "ppls_xprod.hip", "ppls_linalg.hip", "ppls_capi.cpp"]
+SOURCES = ["ppls_kernels.hip", "ppls_variances.hip", "ppls_xprod.hip", "ppls_linalg.hip", "ppls_ozaki.hip",
+           "ppls_capi.cpp"]
 # Per-file flags.  ppls_kernels.hip: the panel dots kernel keeps its MFMA accumulators in VGPRs
 # (the default AGPR form copied them VGPR <-> AGPR on every tile; its only MFMA user).
 FILE_FLAGS = {"ppls_kernels.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"]}

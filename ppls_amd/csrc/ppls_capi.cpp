@@ -122,6 +122,10 @@ struct ppls_ctx {
   // formed once per data set, then every statistics step reads S instead of X and Y
   int xprod = 0;            // option "xprod": 0 stream X, Y (default), 1 cross-products, -1 auto (cost model)
   int xprod_rw = 0;         // option "xprod_rw": rows of S per wave of the tile kernel (0 auto)
+  int gram_int8 = 0;        // option "gram_int8": S by the int8-MFMA CRT form (1, when the column spread
+                            // allows; else the fp64 MFMA Gram) or the fp64 MFMA Gram (0)
+  int oz_used = 0, oz_nmod = 0, oz_L = 0;   // the last formation of S: which Gram, moduli, bits
+  double oz_ms[4] = {0, 0, 0, 0};           // its phases (HIP events): stats+residues, SYRK, CRT, total
   bool xp_ready = false;    // S holds the (all-reduced) cross-products of the current data
   bool xp_active = false;   // statistics steps of the current run read S
   bool xp_pending_gram = false;   // the last statistics step left the Gram B'M to the next finalize
@@ -729,6 +733,118 @@ int gram_run(ppls_ctx* c, const GramShape& g, int64_t n, int req, double* G, flo
   return PPLS_OK;
 }
 
+// The int8-MFMA (Chinese-remainder) form of the same Gram (ppls_ozaki.hip).  Plan from the column
+// statistics: e_j with max_k |D_kj| < 2^e_j, c_j = 2^e_j sqrt(n / sum_k D_kj^2) (>= 1; about 8 for
+// Gaussian columns), L = 53 + ceil(log2 max_j c_j) + 2 bits per integer -- the rounding error of
+// every S_ij is then <= 2^-(L+1) (2^e_i sum|D_kj| + 2^e_j sum|D_ki|) <= 2^-55 sqrt(S_ii S_jj), under
+// the fp64 GEMM's own bound u sum_k |D_ki D_kj| wherever sum |D_ki D_kj| >= sqrt(S_ii S_jj) / 4
+// (tests/test_gpu_ozaki.py checks both on sampled entries against double-double sums) -- and the
+// fewest moduli with prod m_l > 2 max_j sum_k x'_kj^2 (>= |sum_k x'_ki x'_kj| by Cauchy-Schwarz).
+// Returns 1 (not an error) when L > 62, more than PPLS_OZ_MAXMOD moduli are needed or the residue
+// planes do not fit: the caller then runs the fp64 MFMA Gram.
+int gram_run_oz(ppls_ctx* c, const GramShape& g, int64_t n, double* G, float* ms) {
+  const int P = g.p, Pp = (P + 255) / 256 * 256;
+  const int64_t nkb = (n + PPLS_OZ_KS - 1) / PPLS_OZ_KS;
+  const int dtype = c->dtype;
+  struct Bufs {
+    double* part = nullptr;
+    double* st = nullptr;
+    int* shift = nullptr;
+    int8_t* planes = nullptr;
+    uint8_t* res = nullptr;
+    hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+    ~Bufs() {
+      dfree(part); dfree(st); dfree(shift); dfree(planes); dfree(res);
+      for (auto e : ev) if (e) (void)hipEventDestroy(e);
+    }
+  } b;
+  int rc;
+  const int chunks = (int)std::max<int64_t>(1, std::min<int64_t>(256, n / 2048));
+  if ((rc = dalloc(c, &b.part, (size_t)chunks * 2 * Pp)) || (rc = dalloc(c, &b.st, (size_t)2 * Pp)) ||
+      (rc = dalloc(c, &b.shift, (size_t)Pp)))
+    return rc;
+  for (auto& e : b.ev) HIPCHK(c, hipEventCreate(&e));
+  HIPCHK(c, hipEventRecord(b.ev[0], c->stream));
+  HIPCHK(c, ppls_launch_oz_colstats(g.X, g.ldx, g.xcols, g.xreal, g.Y, g.ldy, g.yreal, dtype, Pp, n, chunks, b.part,
+                                    b.st, c->stream));
+  std::vector<double> st((size_t)2 * Pp);
+  HIPCHK(c, hipMemcpyAsync(st.data(), b.st, sizeof(double) * st.size(), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  auto live = [&](int j) { return j < g.xreal || (j >= g.xcols && j - g.xcols < g.yreal); };
+  double cmax = 1.0;
+  std::vector<int> e((size_t)Pp, 0);
+  for (int j = 0; j < P; ++j) {
+    if (!live(j) || !(st[(size_t)j] > 0.0)) continue;
+    int ex = 0;
+    (void)std::frexp(st[(size_t)j], &ex);   // max = f 2^ex, f in [0.5, 1): max < 2^ex
+    e[(size_t)j] = ex;
+    cmax = std::max(cmax, std::ldexp(1.0, ex) * std::sqrt((double)n / st[(size_t)Pp + j]));
+  }
+  const int L = 53 + (int)std::ceil(std::log2(cmax)) + 2;
+  c->oz_L = L;
+  if (L > 62) return 1;
+  std::vector<int> shift((size_t)Pp, 0);
+  double qmax = 0.0;   // max_j sum_k x'_kj^2 <= (2^(L - e_j) ||D_j|| + sqrt(n) / 2)^2
+  for (int j = 0; j < P; ++j) {
+    if (!live(j) || !(st[(size_t)j] > 0.0)) continue;
+    shift[(size_t)j] = L - e[(size_t)j];
+    const double q = std::ldexp(std::sqrt(st[(size_t)Pp + j]), L - e[(size_t)j]) + 0.5 * std::sqrt((double)n);
+    qmax = std::max(qmax, q * q);
+  }
+  const double need = std::log2(std::max(qmax, 1.0)) + 2.0;   // bits of M > 2 max |sum| (+1 margin)
+  double bits = 0.0;
+  int nmod = 0;
+  while (nmod < PPLS_OZ_MAXMOD && bits < need) bits += std::log2((double)ppls_oz_modulus(nmod++));
+  if (bits < need) return 1;
+  nmod = std::max(nmod, 12);
+  c->oz_nmod = nmod;
+  const int T = Pp / 256, ntiles = T * (T + 1) / 2, nsplit = ppls_oz_splits(nkb);
+  const int64_t pstride = nkb * Pp * PPLS_OZ_KS;
+  size_t fr = 0, tot = 0;
+  if (hipMemGetInfo(&fr, &tot) != hipSuccess) return 1;
+  const double want = (double)nmod * (double)pstride + (double)nmod * nsplit * ntiles * 65536.0;
+  if (want > (double)fr - std::max(1073741824.0, 0.05 * (double)fr)) return 1;
+  if (dalloc(c, &b.planes, (size_t)nmod * pstride) || dalloc(c, &b.res, (size_t)nmod * nsplit * ntiles * 65536)) {
+    c->err.clear();
+    return 1;
+  }
+  HIPCHK(c, hipMemcpyAsync(b.shift, shift.data(), sizeof(int) * Pp, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, ppls_launch_oz_residues(g.X, g.ldx, g.xcols, g.xreal, g.Y, g.ldy, g.yreal, dtype, Pp, n, nkb, b.shift,
+                                    nmod, b.planes, pstride, c->stream));
+  HIPCHK(c, hipEventRecord(b.ev[1], c->stream));
+  HIPCHK(c, ppls_launch_oz_syrk(b.planes, pstride, Pp, nkb, nmod, b.res, c->stream));
+  HIPCHK(c, hipEventRecord(b.ev[2], c->stream));
+  HIPCHK(c, ppls_launch_oz_finish(b.res, nmod, nsplit, Pp, g.xcols, g.xreal, g.yreal, P, b.shift, G, c->stream));
+  HIPCHK(c, hipEventRecord(b.ev[3], c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  float t01 = 0.f, t12 = 0.f, t23 = 0.f, t03 = 0.f;
+  HIPCHK(c, hipEventElapsedTime(&t01, b.ev[0], b.ev[1]));
+  HIPCHK(c, hipEventElapsedTime(&t12, b.ev[1], b.ev[2]));
+  HIPCHK(c, hipEventElapsedTime(&t23, b.ev[2], b.ev[3]));
+  HIPCHK(c, hipEventElapsedTime(&t03, b.ev[0], b.ev[3]));
+  c->oz_ms[0] = t01;
+  c->oz_ms[1] = t12;
+  c->oz_ms[2] = t23;
+  c->oz_ms[3] = t03;
+  if (ms) *ms = t03;
+  return PPLS_OK;
+}
+
+// The Gram of the joint columns for S: the int8 form when option gram_int8 asks for it and the data
+// allow it, else (or on its fallback) the fp64 MFMA Gram; c->oz_used records which ran.
+int gram_run_s(ppls_ctx* c, const GramShape& g, int64_t n, double* G, float* ms, double* part) {
+  c->oz_used = 0;
+  if (c->gram_int8) {
+    const int rc = gram_run_oz(c, g, n, G, ms);
+    if (rc == PPLS_OK) {
+      c->oz_used = 1;
+      return PPLS_OK;
+    }
+    if (rc < 0) return rc;
+  }
+  return gram_run(c, g, n, 0, G, ms, part);
+}
+
 int xprod_setup(ppls_ctx* c);
 bool xprod_choose(ppls_ctx* c, int max_steps, int r);
 
@@ -802,7 +918,7 @@ int xprod_setup(ppls_ctx* c) {
   if (c->n_local > 0) {
     c->xp_nsplit = gram_nsplit(c, g, c->n_local, 0);
     float ms = 0.f;
-    rc = gram_run(c, g, c->n_local, 0, c->xp_S, &ms, part);
+    rc = gram_run_s(c, g, c->n_local, c->xp_S, &ms, part);
     dfree(part);
     if (rc) { dfree(c->xp_S); return rc; }
     c->xp_setup_ms = ms;
@@ -837,7 +953,9 @@ bool xprod_choose(ppls_ctx* c, int max_steps, int r) {
   const bool split = c->sweep_mode != 3 && !c->dtype && ppls_split_supported(r, c->ldx, c->ldy) > 0;
   const double t_sweep = (split ? 1.0 : 2.0) * esz * n * P / 6.5e12 + 5e-6;
   const double t_pass = 8.0 * P * P / 6.5e12 + 5e-6;
-  const double t_setup = c->xp_ready ? 0.0 : n * P * P / 55e12 + (c->nranks > 1 ? 16.0 * P * P / 100e9 : 0.0);
+  // the Gram's rate in n P^2 per second: fp64 MFMA ~55e12 (C3 226 ms); the int8 CRT form ~1e14
+  const double gram_rate = c->gram_int8 ? 1.0e14 : 55e12;
+  const double t_setup = c->xp_ready ? 0.0 : n * P * P / gram_rate + (c->nranks > 1 ? 16.0 * P * P / 100e9 : 0.0);
   return ((double)max_steps + 1.0) * (t_sweep - t_pass) > t_setup;
 }
 
@@ -1241,6 +1359,15 @@ int ppls_set_option(ppls_ctx* c, const char* key, int64_t value) {
   } else if (!strcmp(key, "var_chol")) {
     if (value < 0 || value > 2) return fail(c, PPLS_E_ARG, "var_chol must be 0 (LU), 1 (Cholesky) or 2 (rocSOLVER Cholesky)");
     c->var_chol = (int)value;
+  } else if (!strcmp(key, "gram_int8")) {
+    if (value < 0 || value > 1) return fail(c, PPLS_E_ARG, "gram_int8 must be 0 (fp64 MFMA Gram) or 1 (int8 CRT form)");
+    if ((int)value != c->gram_int8) {
+      c->gram_int8 = (int)value;
+      if (c->xp_ready && !c->xp_explicit) {   // a different Gram: S is formed again when next needed
+        dfree(c->xp_S);
+        c->xp_ready = false;
+      }
+    }
   } else if (!strcmp(key, "xprod_rw")) {
     if (value != 0 && value != 1 && value != 2 && value != 4 && value != 8)
       return fail(c, PPLS_E_ARG, "xprod_rw must be 0, 1, 2, 4 or 8");
@@ -3103,6 +3230,39 @@ int ppls_sweep_info(ppls_ctx* c, int r, int64_t* bytes_per_sweep, int* variant, 
   if (bytes_per_sweep) *bytes_per_sweep = (int64_t)(c->dtype ? 4 : 8) * c->n_local * ((int64_t)c->p + c->q);
   if (variant) *variant = plan == 4 ? 5 : plan == 3 ? 4 : 2;
   if (grid) *grid = a.grid;
+  return PPLS_OK;
+}
+
+int ppls_gram_int8(ppls_ctx* c, int which, double* G, int* nmod, int* L, double* ms) {
+  if (!c) return PPLS_E_ARG;
+  if (!c->have_data) return fail(c, PPLS_E_STATE, "no data");
+  if (which < 0 || which > 2) return fail(c, PPLS_E_ARG, "which must be 0 (X), 1 (Y) or 2 (joint [X Y])");
+  if (c->n_local <= 0) return fail(c, PPLS_E_STATE, "no rows on this rank");
+  HIPCHK(c, hipSetDevice(c->device));
+  const GramShape g = which == 2 ? gram_shape(c, true, 0) : gram_shape(c, false, which);
+  const size_t pp = (size_t)g.p * g.p;
+  int rc;
+  double* dG = nullptr;
+  if ((rc = dalloc(c, &dG, pp))) return rc;
+  float t = 0.f;
+  rc = gram_run_oz(c, g, c->n_local, dG, &t);
+  if (nmod) *nmod = c->oz_nmod;
+  if (L) *L = c->oz_L;
+  if (rc == 1) rc = fail(c, PPLS_E_NUMERIC, "int8 Gram: the column spread needs L = %d bits or more than %d moduli, "
+                         "or the residue planes do not fit", c->oz_L, PPLS_OZ_MAXMOD);
+  if (!rc && G && hipMemcpy(G, dG, sizeof(double) * pp, hipMemcpyDeviceToHost) != hipSuccess)
+    rc = fail(c, PPLS_E_HIP, "int8 gram: copy-out failed");
+  dfree(dG);
+  if (!rc && ms) for (int k = 0; k < 4; ++k) ms[k] = c->oz_ms[k];
+  return rc;
+}
+
+int ppls_gram_info(ppls_ctx* c, int* int8_used, int* nmod, int* L, double* ms) {
+  if (!c) return PPLS_E_ARG;
+  if (int8_used) *int8_used = c->oz_used;
+  if (nmod) *nmod = c->oz_nmod;
+  if (L) *L = c->oz_L;
+  if (ms) for (int k = 0; k < 4; ++k) ms[k] = c->oz_ms[k];
   return PPLS_OK;
 }
 

@@ -118,6 +118,8 @@ struct PplsRank1StepArgs {
 // One EM step of meta_PPLSi on the device (ppls_meta_step_kernel): log-likelihoods and stop rule of
 // the step's sweep, then meta_EMstep's M-step for the next sweep.
 #define PPLS_META_KMAX 1024
+#define PPLS_OZ_MAXMOD 20   // int8 Gram (ppls_ozaki.hip): at most this many CRT moduli
+#define PPLS_OZ_KS 64       // int8 Gram: rows per residue-plane stage (planes are [n / KS][Pp][KS] int8)
 struct PplsMetaStepArgs {
   const double* stats;     // K x part_ld: per population [X_j'mu_T ldx][Y_j'mu_U ldy][Gram 4] (r = 1)
   int64_t part_ld;
@@ -205,4 +207,18 @@ int64_t ppls_spd_inverse_work(int p, int a);
 hipError_t ppls_spd_inverse_batched(double* A, int p, int a, double* work, int* info, hipStream_t st);
 hipError_t ppls_launch_to_colmajor(const double* src, int64_t n, int p, int ld, double* dst,
                                    hipStream_t st);
+// ppls_ozaki.hip: the cross-product Gram D'D on int8 MFMA (Chinese-remainder form): column statistics
+// (out = [max |D| | sum D^2] per joint column, Pp of each), residue planes [nkb][Pp][128] per modulus,
+// the per-modulus SYRK of the lower 256 x 256 tiles (uint8 residues), and the CRT into G (P x P)
+int ppls_oz_modulus(int l);
+hipError_t ppls_launch_oz_colstats(const void* X, int ldx, int xcols, int xreal, const void* Y, int ldy, int yreal,
+                                   int f32, int Pp, int64_t n, int chunks, double* part, double* out, hipStream_t st);
+hipError_t ppls_launch_oz_residues(const void* X, int ldx, int xcols, int xreal, const void* Y, int ldy, int yreal,
+                                   int f32, int Pp, int64_t n, int64_t nkb, const int* shift, int nmod, int8_t* planes,
+                                   int64_t pstride, hipStream_t st);
+int ppls_oz_splits(int64_t nkb);   // row splits of the SYRK (65,536 rows each: exact int32 sums)
+hipError_t ppls_launch_oz_syrk(const int8_t* planes, int64_t pstride, int Pp, int64_t nkb, int nmod, uint8_t* part,
+                               hipStream_t st);
+hipError_t ppls_launch_oz_finish(const uint8_t* part, int nmod, int nsplit, int Pp, int xcols, int xreal, int yreal,
+                                 int P, const int* shift, double* G, hipStream_t st);
 }

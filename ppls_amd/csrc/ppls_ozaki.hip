@@ -1,0 +1,826 @@
+// ppls_ozaki.hip -- the cross-product Gram S = D'D (D = [X | Y], ppls_xprod.hip's S) on INT8 MFMA
+// by the Chinese-remainder ("Ozaki scheme II") form (round 6).  S is 92 % of a
+// default PPLS_simult call and the fp64 MFMA Gram runs at 0.90 of the fp64 peak; gfx950's
+// v_mfma_i32_32x32x32_i8 issues 64x the fp64 MFMA's multiply-adds per clock.
+//
+//   1. column scaling (host, from ppls_oz_colstats_kernel): per live column j, e_j with
+//      max_k |D_kj| < 2^e_j; every element becomes the integer  x'_kj = rint(D_kj 2^(L - e_j)),
+//      |x'| < 2^L, exact in fp64 (a power-of-2 scale, then a rounding to an integer).  L is chosen
+//      from the columns' spread (ppls_oz_plan): the rounding error of S_ij is then at most
+//      2^-(L+1) (2^e_i sum|D_kj| + 2^e_j sum|D_ki|) <= 2^-L c_max sqrt(S_ii S_jj),
+//      c_j = 2^e_j sqrt(n) / sqrt(S_jj).
+//   2. residues (ppls_oz_residue_kernel): x' mod m_l for NMOD pairwise coprime moduli m_l <= 256,
+//      symmetric (|r| <= 128, int8), written as NMOD planes [n / 64][Pp][64] (a stage's 64 rows of
+//      one column contiguous: 16 KB per 256-column panel stage).
+//   3. SYRK per modulus (ppls_oz_syrk_kernel): the lower 256 x 256 tiles of R_l' R_l on
+//      v_mfma_i32_32x32x32_i8, exact in int32 (reduced mod m_l every 65,536 rows), -> uint8 residues.
+//   4. CRT (ppls_oz_finish_kernel): Garner's mixed-radix digits of the NMOD residues, the exact
+//      integer sum_k x'_ki x'_kj in 192 bits (|.| < M / 2, M = prod m_l > 2 max_ij |sum|), ONE
+//      rounding to fp64, times 2^(e_i + e_j - 2L) -> S, mirrored.
+// Integer sums are exact, so S depends on the data only (not on the schedule): bitwise repeatable.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <type_traits>
+
+#include "ppls_device.h"
+#include "ppls_kernels.h"
+
+namespace {
+
+constexpr int OZ_TT = 256;                 // output tile edge
+constexpr int OZ_KS = PPLS_OZ_KS;          // rows per stage (one column's stage: 64 B)
+constexpr int OZ_PANEL = OZ_TT * OZ_KS;    // bytes of one 256-column panel stage (16 KB)
+constexpr int OZ_SPLIT_STAGES = 1024;      // stages per SYRK item: 65,536 rows, |sum| <= 2^30 in int32
+#ifndef OZ_SYRK_VARIANT
+#define OZ_SYRK_VARIANT 514
+#endif
+
+// pairwise coprime moduli, largest first: 2^8, 3*5*17, 11*23, 251, 13*19, then primes and 7*31.  A
+// switch, so an unrolled loop over l sees compile-time moduli (multiply-high forms of % m).
+__host__ __device__ constexpr int oz_mod(int l) {
+  switch (l) {
+    case 0: return 256;  case 1: return 255;  case 2: return 253;  case 3: return 251;  case 4: return 247;
+    case 5: return 241;  case 6: return 239;  case 7: return 233;  case 8: return 229;  case 9: return 227;
+    case 10: return 223; case 11: return 217; case 12: return 211; case 13: return 199; case 14: return 197;
+    case 15: return 193; case 16: return 191; case 17: return 181; case 18: return 179; case 19: return 173;
+    default: return 1;
+  }
+}
+
+constexpr int oz_inv(int a, int m) {   // a^-1 mod m (gcd 1), extended Euclid
+  int t = 0, nt = 1, r = m, nr = ((a % m) + m) % m;
+  while (nr) {
+    const int q = r / nr;
+    const int tt = t - q * nt;
+    t = nt;
+    nt = tt;
+    const int rr = r - q * nr;
+    r = nr;
+    nr = rr;
+  }
+  return t < 0 ? t + m : t;
+}
+
+// Garner's inverses inv[l][k] = m_k^-1 mod m_l (k < l) and, per modulus count N, M_N = prod_{l<N} m_l
+// and floor(M_N / 2) in 6 little-endian 32-bit limbs.
+struct OzTab {
+  int inv[PPLS_OZ_MAXMOD][PPLS_OZ_MAXMOD];
+  uint32_t M[PPLS_OZ_MAXMOD + 1][6], halfM[PPLS_OZ_MAXMOD + 1][6];
+};
+constexpr OzTab oz_make_tab() {
+  OzTab t{};
+  for (int l = 0; l < PPLS_OZ_MAXMOD; ++l)
+    for (int k = 0; k < l; ++k) t.inv[l][k] = oz_inv(oz_mod(k), oz_mod(l));
+  uint64_t w[6] = {1, 0, 0, 0, 0, 0};
+  for (int n = 0; n <= PPLS_OZ_MAXMOD; ++n) {
+    for (int q = 0; q < 6; ++q) t.M[n][q] = (uint32_t)w[q];
+    uint32_t c = 0;
+    for (int q = 5; q >= 0; --q) {
+      t.halfM[n][q] = (t.M[n][q] >> 1) | (c << 31);
+      c = t.M[n][q] & 1u;
+    }
+    if (n < PPLS_OZ_MAXMOD) {
+      uint64_t carry = 0;
+      for (int q = 0; q < 6; ++q) {
+        const uint64_t v = w[q] * (uint64_t)oz_mod(n) + carry;
+        w[q] = v & 0xffffffffull;
+        carry = v >> 32;
+      }
+    }
+  }
+  return t;
+}
+__constant__ OzTab oz_tab = oz_make_tab();
+
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef int v16i __attribute__((ext_vector_type(16)));
+
+// s_waitcnt immediate (gfx9 encoding) that waits for vmcnt <= N only: expcnt 7, lgkmcnt 15 (no wait)
+#define OZ_VMCNT(N) (((N) & 15) | (7 << 4) | (15 << 8) | (((N) >> 4) << 14))
+
+__host__ __device__ inline void oz_tile_of(int t, int* I, int* J) {
+  int i = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
+  while ((i + 1) * (i + 2) / 2 <= t) ++i;
+  while (i * (i + 1) / 2 > t) --i;
+  *I = i;
+  *J = t - i * (i + 1) / 2;
+}
+
+// a joint column c of [X | Y] (X's xcols stored columns, then Y's): its row base and whether live
+struct OzCols {
+  int xreal, xcols, yreal;
+};
+__device__ __forceinline__ bool oz_live(const OzCols& g, int c) {
+  return c < g.xreal || (c >= g.xcols && c - g.xcols < g.yreal);
+}
+
+template <typename T>
+__device__ __forceinline__ double oz_ld(const T* X, int ldx, const T* Y, int ldy, const OzCols& g, int64_t row, int c) {
+  if (c < g.xreal) return (double)X[row * ldx + c];
+  if (c >= g.xcols && c - g.xcols < g.yreal) return (double)Y[row * ldy + (c - g.xcols)];
+  return 0.0;
+}
+
+}  // namespace
+
+// The symmetric residue of x' = u - 2^62 (u = hi 2^32 + lo) modulo m: |result| <= m / 2 <= 128.
+// c32 = 2^32 mod m, c62 = 2^62 mod m.  (With a compile-time m the three % are multiply-high forms.)
+__host__ __device__ __forceinline__ int oz_residue(uint32_t hi, uint32_t lo, uint32_t m, uint32_t c32, uint32_t c62) {
+  uint32_t r = ((hi % m) * c32 + lo % m) % m;   // u mod m
+  r = r >= c62 ? r - c62 : r + m - c62;         // x' mod m in [0, m)
+  return (int)r > (int)(m / 2) ? (int)r - (int)m : (int)r;
+}
+
+// ---------------------------------------------------------------------------- 1. column statistics
+// part[chunk][2][Pp]: per column the max |D| and sum D^2 over the chunk's rows (one thread per
+// column, rows strided by the grid's y dimension).
+template <typename T>
+__global__ __launch_bounds__(256) void ppls_oz_colstats_kernel(const T* __restrict__ X, int ldx, const T* __restrict__ Y,
+                                                               int ldy, OzCols g, int Pp, int64_t n, int64_t rpc,
+                                                               double* __restrict__ part) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= Pp) return;
+  const int64_t r0 = (int64_t)blockIdx.y * rpc, r1 = r0 + rpc < n ? r0 + rpc : n;
+  double mx = 0.0, ss = 0.0;
+  if (oz_live(g, c))
+    for (int64_t r = r0; r < r1; ++r) {
+      const double v = oz_ld(X, ldx, Y, ldy, g, r, c);
+      mx = fmax(mx, fabs(v));
+      ss = fma(v, v, ss);
+    }
+  double* o = part + (int64_t)blockIdx.y * 2 * Pp;
+  o[c] = mx;
+  o[Pp + c] = ss;
+}
+
+__global__ void ppls_oz_colstats_finish_kernel(const double* __restrict__ part, int chunks, int Pp, double* __restrict__ out) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= Pp) return;
+  double mx = 0.0, ss = 0.0;
+  for (int k = 0; k < chunks; ++k) {   // fixed order
+    mx = fmax(mx, part[(int64_t)k * 2 * Pp + c]);
+    ss += part[(int64_t)k * 2 * Pp + Pp + c];
+  }
+  out[c] = mx;
+  out[Pp + c] = ss;
+}
+
+// ---------------------------------------------------------------------------- 2. residue planes
+// Block: one 64-row stage kb x 64 columns.  Thread: column c0 + (tid & 63), rows 16 (tid >> 6) ..
+// + 15 of the stage.  x' = rint(D 2^shift_c) (exact), u = x' + 2^62 >= 0 split into 32-bit halves,
+// u mod m = ((hi mod m) (2^32 mod m) + lo mod m) mod m, then minus 2^62 mod m, symmetric.
+template <typename T, int NMOD>
+__global__ __launch_bounds__(256) void ppls_oz_residue_kernel(const T* __restrict__ X, int ldx, const T* __restrict__ Y,
+                                                              int ldy, OzCols g, int Pp, int64_t n,
+                                                              const int* __restrict__ shift, int8_t* __restrict__ planes,
+                                                              int64_t pstride) {
+  const int tid = threadIdx.x;
+  const int c = blockIdx.x * 64 + (tid & 63), grp = tid >> 6;
+  const int64_t kb = blockIdx.y;
+  const int64_t row0 = kb * OZ_KS + 16 * grp;
+  uint32_t hi[16], lo[16];
+  const bool live = c < Pp && oz_live(g, c);
+  const int sh = live ? shift[c] : 0;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int64_t row = row0 + k;
+    const double x = (live && row < n) ? oz_ld(X, ldx, Y, ldy, g, row, c) : 0.0;
+    const double xs = rint(ldexp(x, sh));                        // |xs| < 2^L <= 2^62, an exact integer
+    const uint64_t u = (uint64_t)((int64_t)xs + (int64_t)(1ull << 62));
+    hi[k] = (uint32_t)(u >> 32);
+    lo[k] = (uint32_t)u;
+  }
+  if (c >= Pp) return;
+  int8_t* dst = planes + (kb * Pp + c) * OZ_KS + 16 * grp;
+#pragma unroll
+  for (int l = 0; l < NMOD; ++l) {
+    const uint32_t m = (uint32_t)oz_mod(l);
+    const uint32_t c32 = (uint32_t)((1ull << 32) % m), c62 = (uint32_t)((1ull << 62) % m);
+    uint32_t w[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < 16; ++k) w[k >> 2] |= ((uint32_t)oz_residue(hi[k], lo[k], m, c32, c62) & 255u) << (8 * (k & 3));
+    *(v4i*)(dst + (int64_t)l * pstride) = v4i{(int)w[0], (int)w[1], (int)w[2], (int)w[3]};
+  }
+}
+
+// ---------------------------------------------------------------------------- 3. int8 SYRK per modulus
+// One workgroup per (modulus, 65,536-row split, lower 256 x 256 tile); 4 waves of 128 x 128 (4 x 4
+// blocks of v_mfma_i32_32x32x32_i8, 256 int32 accumulators per lane).  The panels of a 64-row stage
+// (16 KB each; one for a diagonal tile) go HBM -> LDS by LDS-DMA (global_load_lds_dwordx4, no VGPR
+// staging) into a ring of 4 buffers, three stages in flight; one barrier per stage, before which
+// every wave waits for its own copies of that stage (vmcnt <= the copies it issued for the two
+// later stages: 2 x 4 on the diagonal, 2 x 8 off it).  The product form (V = 512) issues the copies
+// through inline asm (ppls_dma16s) so the compiler does not track them: tracked, it put vmcnt(0) --
+// the whole prefetch -- in front of the first fragment read of three stages in four (it cannot tell
+// the ring buffers apart across the loop's joins), and DMA and MFMA time added up (10.3 ms per C3
+// plane against 6.0 compute-only and 6.4 copies-only; 7.8 ms untracked, tools/oz_lab.hip).  The
+// copies of stage s + 3 go out during stage s's first k-step, the second k-step's fragments are read
+// during the first's MFMAs.  V = 514 copies both panels for a diagonal tile too (its B panel is its A
+// panel): one code path, 8 % faster than specialising the diagonal (V = 512, 8.5 ms) on this grid.  The 16-B chunks are XOR-swizzled on the source side (LDS chunk q of
+// column c holds global chunk q ^ ((c >> 2) & 3)), so the fragment reads (ds_read_b128) are
+// conflict-free.  Both MFMA operands are read from the same layout, so whatever order the
+// instruction gives the 32 k values of a step, each k meets itself.
+// |r| <= 128: a split's 65,536 rows sum to at most 2^30 -- exact in int32, no reduction in the loop
+// (one there made the compiler spill the accumulators).  Output: the split's tile sums mod m, uint8,
+// column-major [col][row].  (Variants other than 512/513 are lab ablations, built under OZ_LAB.)
+__device__ __forceinline__ int oz_lds_off(int c, int q) { return c * OZ_KS + ((q ^ ((c >> 2) & 3)) << 4); }
+
+typedef __attribute__((address_space(3))) void* oz_lptr;
+
+template <int V>
+__global__ __launch_bounds__((V & 4) ? 512 : 256, 1) void ppls_oz_syrk_kernel(
+    const int8_t* __restrict__ planes, int64_t pstride, int Pp, int64_t nkb, int nmod, int nsplit, int ntiles,
+    uint8_t* __restrict__ out) {
+  // V & 4: 8 waves (two per SIMD) of 128 x 64, else 4 waves of 128 x 128
+  constexpr int NWV = (V & 4) ? 8 : 4;
+  constexpr int CT = 256 / (NWV / 2);   // output columns per wave
+  constexpr int NJ = CT / 32;           // 32-column MFMA blocks per wave
+  constexpr int NU = 16 / NWV;          // LDS-DMA instructions per wave per panel stage
+  // four ring buffers, each [A panel | B panel] of one stage; separate objects, so the compiler's
+  // own LDS-DMA tracking tells them apart
+  __shared__ __attribute__((aligned(16))) int8_t lb0[((V & 1024) ? 8 : 2) * OZ_PANEL];   // (V & 1024: the whole ring)
+  __shared__ __attribute__((aligned(16))) int8_t lb1[2 * OZ_PANEL];
+  __shared__ __attribute__((aligned(16))) int8_t lb2[2 * OZ_PANEL];
+  __shared__ __attribute__((aligned(16))) int8_t lb3[2 * OZ_PANEL];
+  const int b = blockIdx.x, nb = gridDim.x;
+  const int it = (b & 7) * (nb >> 3) + (b >> 3);   // XCD x (b mod 8) takes a contiguous item range
+  if (it >= nmod * nsplit * ntiles) return;
+  // item = (modulus, split, tile), tile fastest: concurrent items share the split's row stages
+  const int l = it / (nsplit * ntiles), rem = it - l * nsplit * ntiles;
+  const int sp = rem / ntiles, t = rem - sp * ntiles;
+  // (lab ablations, tools/oz_lab.hip only: V & 8 every item reads split 0's rows of plane 0 -- the
+  // stream stays cache-resident; V & 16 no copies at all; V & 64 no fragment reads or MFMAs)
+  const int64_t s0 = (V & 8) ? 0 : (int64_t)sp * OZ_SPLIT_STAGES;
+  const int64_t s1 = s0 + OZ_SPLIT_STAGES < nkb ? s0 + OZ_SPLIT_STAGES : nkb;
+  const int m = oz_mod(l);
+  int I, J;
+  oz_tile_of(t, &I, &J);
+  const bool diag = I == J;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wi = wave / (NWV / 2), wj = wave % (NWV / 2);
+  const bool idle = diag && wi == 0 && wj * CT >= 128;   // in the diagonal tile's upper-right quadrant
+  const int8_t* pl = planes + ((V & 8) ? 0 : (int64_t)l * pstride);
+  const int8_t* pa = pl + (int64_t)I * OZ_PANEL;
+  const int8_t* pb = pl + (int64_t)J * OZ_PANEL;
+  const int64_t sstride = (int64_t)Pp * OZ_KS;
+  v16i acc[4][NJ];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = v16i{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  // this lane's source offset in a panel stage: wave instruction g = NU wave + u fills LDS bytes
+  // [1024 g, + 1024); lane l the 16 B at 16 l: column 16 g + l / 4, chunk l % 4
+  int soff[NU];
+#pragma unroll
+  for (int u = 0; u < NU; ++u) {
+    const int c = 16 * (NU * wave + u) + (lane >> 2), pos = lane & 3;
+    soff[u] = c * OZ_KS + ((pos ^ ((c >> 2) & 3)) << 4);
+  }
+  auto issue = [&](int8_t* buf, int64_t s) __attribute__((always_inline)) {
+    if constexpr ((V & 16) != 0) return;
+    const int8_t* ga = pa + s * sstride;
+#pragma unroll
+    for (int u = 0; u < NU; ++u)
+      __builtin_amdgcn_global_load_lds((const void*)(ga + soff[u]), (oz_lptr)(buf + 1024 * (NU * wave + u)), 16, 0, 0);
+    if (!diag) {
+      const int8_t* gb = pb + s * sstride;
+#pragma unroll
+      for (int u = 0; u < NU; ++u)
+        __builtin_amdgcn_global_load_lds((const void*)(gb + soff[u]), (oz_lptr)(buf + OZ_PANEL + 1024 * (NU * wave + u)),
+                                         16, 0, 0);
+    }
+  };
+  // wait until at most `later` stages of this wave's copies are in flight (they retire in order):
+  // NU copies per panel, one panel on the diagonal, two off it
+  auto wait_stages = [&](int64_t later) __attribute__((always_inline)) {
+    if (later >= 2) {
+      if (diag) __builtin_amdgcn_s_waitcnt(OZ_VMCNT(2 * NU));
+      else __builtin_amdgcn_s_waitcnt(OZ_VMCNT(4 * NU));
+    } else if (later == 1) {
+      if (diag) __builtin_amdgcn_s_waitcnt(OZ_VMCNT(NU));
+      else __builtin_amdgcn_s_waitcnt(OZ_VMCNT(2 * NU));
+    } else {
+      __builtin_amdgcn_s_waitcnt(OZ_VMCNT(0));
+    }
+  };
+  const int ca0 = 128 * wi + (lane & 31), cb0 = CT * wj + (lane & 31), h = lane >> 5;
+  auto compute = [&](const int8_t* buf) __attribute__((always_inline)) {
+    if constexpr ((V & 64) != 0) return;   // (lab ablation: the copies alone)
+    const int8_t* la = buf;
+    const int8_t* lbp = diag ? buf : buf + OZ_PANEL;
+    if constexpr ((V & 1) != 0) {   // every fragment of the stage read first (in order), then the MFMAs
+      v4i a[OZ_KS / 32][4], bb[OZ_KS / 32][NJ];
+#pragma unroll
+      for (int kb = 0; kb < OZ_KS / 32; ++kb) {
+        const int q = 2 * kb + h;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) a[kb][i] = *(const v4i*)(la + oz_lds_off(ca0 + 32 * i, q));
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) bb[kb][j] = *(const v4i*)(lbp + oz_lds_off(cb0 + 32 * j, q));
+      }
+      if constexpr ((V & 2) != 0) __builtin_amdgcn_iglp_opt(1);
+#pragma unroll
+      for (int kb = 0; kb < OZ_KS / 32; ++kb)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < NJ; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[kb][i], bb[kb][j], acc[i][j], 0, 0, 0);
+    } else {
+#pragma unroll
+      for (int kb = 0; kb < OZ_KS / 32; ++kb) {
+        v4i a[4], bb[NJ];
+        const int q = 2 * kb + h;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) a[i] = *(const v4i*)(la + oz_lds_off(ca0 + 32 * i, q));
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) bb[j] = *(const v4i*)(lbp + oz_lds_off(cb0 + 32 * j, q));
+        if constexpr ((V & 2) != 0) __builtin_amdgcn_iglp_opt(1);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)   // (the diagonal tile's idle wave computes too: no branch here)
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[i], bb[j], acc[i][j], 0, 0, 0);
+      }
+    }
+  };
+  // one stage: its copies landed (every wave), then the buffer of the stage before it is free for
+  // the stage three ahead
+  auto step = [&](int8_t* cur, int8_t* nxt3, int64_t s) __attribute__((always_inline)) {
+    wait_stages(s1 - 1 - s < 2 ? s1 - 1 - s : 2);
+    __builtin_amdgcn_s_barrier();
+    if (s + 3 < s1) issue(nxt3, s + 3);
+    compute(cur);
+  };
+  if constexpr ((V & 512) != 0) {
+    // V & 512: the copies through inline asm (ppls_dma16s), invisible to the compiler's wait
+    // insertion, which otherwise puts vmcnt(0) -- every copy in flight, i.e. the whole prefetch --
+    // in front of the first fragment read of most stages (it cannot tell the ring buffers apart
+    // across the loop's joins).  The ring's completion is waited for by hand: vmcnt <= the 2 x 2 NU
+    // copies of the two later stages, then the barrier.  The stage is branch-free as in V & 128 and
+    // the copies spread one per MFMA group.
+    static_assert((V & 4) == 0 && (V & 32) == 0, "asm copies: 4 waves of 128 x 128 only");
+    const uint32_t lds0 = (uint32_t)(uintptr_t)(oz_lptr)lb0, lds1 = (uint32_t)(uintptr_t)(oz_lptr)lb1;
+    const uint32_t lds2 = (uint32_t)(uintptr_t)(oz_lptr)lb2, lds3 = (uint32_t)(uintptr_t)(oz_lptr)lb3;
+    auto last = [&](int64_t s) { return s < s1 ? s : s1 - 1; };
+    auto dma = [&](uint32_t lbuf, int64_t s, int g) __attribute__((always_inline)) {
+      const int8_t* src = (g < NU ? pa : pb) + s * sstride;
+      const int u = g < NU ? g : g - NU;
+      const uint32_t dst = lbuf + (uint32_t)((g < NU ? 0 : OZ_PANEL) + 1024 * (NU * wave + u));
+      ppls_dma16s(src, (uint32_t)soff[u], (uint32_t)__builtin_amdgcn_readfirstlane((int)dst));   // wave-uniform
+    };
+    // a diagonal tile (DG) copies and reads one panel: NU copies per stage, else 2 NU
+    auto run = [&](auto dg) __attribute__((always_inline)) {
+      constexpr bool DG = decltype(dg)::value;
+      constexpr int NC = DG ? NU : 2 * NU;   // copies per wave per stage
+      auto mstep = [&](const int8_t* cur, uint32_t nxt3, int64_t s) __attribute__((always_inline)) {
+        ppls_wait_vmcnt(2 * NC);   // own copies of stage s landed (s + 1, s + 2 in flight)
+        ppls_lds_barrier();        // everyone's; buffer of s - 1 free
+        const int64_t sn = last(s + 3);
+        const int8_t* curb = DG ? cur : cur + OZ_PANEL;
+        if constexpr ((V & 1) != 0) {
+#pragma unroll
+          for (int g = 0; g < NC; ++g) dma(nxt3, sn, g);
+        }
+        v4i a0[4], b0[NJ], a1[4], b1[NJ];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) a0[i] = *(const v4i*)(cur + oz_lds_off(ca0 + 32 * i, h));
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) b0[j] = *(const v4i*)(curb + oz_lds_off(cb0 + 32 * j, h));
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0[i], b0[j], acc[i][j], 0, 0, 0);
+          if constexpr ((V & 1) == 0) dma(nxt3, sn, i);
+          // the second step's fragments, two per group
+          if (i < 2) a1[2 * i] = *(const v4i*)(cur + oz_lds_off(ca0 + 32 * (2 * i), 2 + h)),
+                     a1[2 * i + 1] = *(const v4i*)(cur + oz_lds_off(ca0 + 32 * (2 * i + 1), 2 + h));
+          else b1[2 * (i - 2)] = *(const v4i*)(curb + oz_lds_off(cb0 + 32 * (2 * (i - 2)), 2 + h)),
+               b1[2 * (i - 2) + 1] = *(const v4i*)(curb + oz_lds_off(cb0 + 32 * (2 * (i - 2) + 1), 2 + h));
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1[i], b1[j], acc[i][j], 0, 0, 0);
+          if constexpr ((V & 1) == 0 && !DG) dma(nxt3, sn, 4 + i);
+        }
+      };
+      const uint32_t p1 = (V & 1024) ? lds0 + 2 * OZ_PANEL : lds1, p2 = (V & 1024) ? lds0 + 4 * OZ_PANEL : lds2;
+#pragma unroll
+      for (int g = 0; g < NC; ++g) dma(lds0, last(s0), g);
+#pragma unroll
+      for (int g = 0; g < NC; ++g) dma(p1, last(s0 + 1), g);
+#pragma unroll
+      for (int g = 0; g < NC; ++g) dma(p2, last(s0 + 2), g);
+      if constexpr ((V & 1024) != 0) {
+        // V & 1024: one stage per trip, the ring buffer from the stage index (a quarter of the code)
+#pragma unroll 1
+        for (int64_t s = s0; s < s1; ++s) {
+          const int bq = (int)((s - s0) & 3);
+          mstep(lb0 + bq * 2 * OZ_PANEL, lds0 + (uint32_t)(((bq + 3) & 3) * 2 * OZ_PANEL), s);
+        }
+      } else {
+        for (int64_t s = s0; s < s1; s += 4) {
+          mstep(lb0, lds3, s);
+          if (s + 1 < s1) mstep(lb1, lds0, s + 1);
+          if (s + 2 < s1) mstep(lb2, lds1, s + 2);
+          if (s + 3 < s1) mstep(lb3, lds2, s + 3);
+        }
+      }
+    };
+    if constexpr ((V & 2) != 0) run(std::false_type{});   // (V & 2: a diagonal tile copies both panels too)
+    else if (diag) run(std::true_type{});
+    else run(std::false_type{});
+    ppls_wait_vmcnt(0);   // no copy may land after the workgroup's LDS is gone
+  } else if constexpr ((V & 128) != 0) {
+    // V & 128: the stage-ahead copies spread one per 4 MFMAs through the stage's compute instead of a
+    // burst after the barrier (a burst of LDS-DMA pieces stalls the issuing wave's MFMA stream).
+    // Branch-free stage: both panels always copied (a diagonal tile's B panel is its A panel) and the
+    // tail re-copies the last stage into a buffer no one reads, so every wait is the same count.
+    static_assert((V & 4) == 0 && (V & 32) == 0, "spread copies: 4 waves of 128 x 128 only");
+    auto issue2 = [&](int8_t* buf, int64_t s, int g) __attribute__((always_inline)) {
+      const int8_t* src = (g < NU ? pa : pb) + s * sstride;
+      const int u = g < NU ? g : g - NU;
+      __builtin_amdgcn_global_load_lds((const void*)(src + soff[u]),
+                                       (oz_lptr)(buf + (g < NU ? 0 : OZ_PANEL) + 1024 * (NU * wave + u)), 16, 0, 0);
+    };
+    auto last = [&](int64_t s) { return s < s1 ? s : s1 - 1; };
+    auto sstep = [&](int8_t* cur, int8_t* nxt3, int64_t s) __attribute__((always_inline)) {
+      __builtin_amdgcn_s_waitcnt(OZ_VMCNT(4 * NU));   // own copies of stage s landed (s + 1, s + 2 in flight)
+      __builtin_amdgcn_s_barrier();                    // everyone's; buffer of s - 1 free
+      const int64_t sn = last(s + 3);
+#pragma unroll
+      for (int kb = 0; kb < OZ_KS / 32; ++kb) {
+        v4i a[4], bb[NJ];
+        const int q = 2 * kb + h;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) a[i] = *(const v4i*)(cur + oz_lds_off(ca0 + 32 * i, q));
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) bb[j] = *(const v4i*)(cur + OZ_PANEL + oz_lds_off(cb0 + 32 * j, q));
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[i], bb[j], acc[i][j], 0, 0, 0);
+          issue2(nxt3, sn, 4 * kb + i);
+        }
+      }
+      if constexpr ((V & 256) != 0) {
+        // V & 256: the second step's fragment reads, two per MFMA group, inside the first step
+        __builtin_amdgcn_sched_group_barrier(0x100, 4 + NJ, 0);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x008, NJ, 0);
+          __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, (4 + NJ) / 4, 0);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x008, NJ, 0);
+          __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+        }
+      } else {
+#pragma unroll
+        for (int kb = 0; kb < OZ_KS / 32; ++kb) {
+          __builtin_amdgcn_sched_group_barrier(0x100, 4 + NJ, 0);   // the step's fragment reads
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, NJ, 0);     // 4 MFMAs
+            __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);      // then one copy
+          }
+        }
+      }
+    };
+    auto issue_all = [&](int8_t* buf, int64_t s) __attribute__((always_inline)) {
+#pragma unroll
+      for (int g = 0; g < 2 * NU; ++g) issue2(buf, last(s), g);
+    };
+    issue_all(lb0, s0);
+    issue_all(lb1, s0 + 1);
+    issue_all(lb2, s0 + 2);
+    for (int64_t s = s0; s < s1; s += 4) {
+      sstep(lb0, lb3, s);
+      if (s + 1 < s1) sstep(lb1, lb0, s + 1);
+      if (s + 2 < s1) sstep(lb2, lb1, s + 2);
+      if (s + 3 < s1) sstep(lb3, lb2, s + 3);
+    }
+    __builtin_amdgcn_s_waitcnt(OZ_VMCNT(0));   // no copy may land after the workgroup's LDS is gone
+  } else {
+  if (s0 < s1) issue(lb0, s0);
+  if (s0 + 1 < s1) issue(lb1, s0 + 1);
+  if (s0 + 2 < s1) issue(lb2, s0 + 2);
+  if constexpr ((V & 32) == 0) {
+    for (int64_t s = s0; s < s1; s += 4) {
+      step(lb0, lb3, s);
+      if (s + 1 < s1) step(lb1, lb0, s + 1);
+      if (s + 2 < s1) step(lb2, lb1, s + 2);
+      if (s + 3 < s1) step(lb3, lb2, s + 3);
+    }
+  } else {
+    // V & 32: the fragments of stage s + 1 are read while the second half of stage s's MFMAs runs;
+    // the barrier that makes stage s + 1's copies visible sits between the two halves
+    v4i fa[2][2][4], fb[2][2][NJ];   // [register set][kb][block]
+    auto rd = [&](const int8_t* buf, v4i (&xa)[2][4], v4i (&xb)[2][NJ]) __attribute__((always_inline)) {
+      const int8_t* lbp = diag ? buf : buf + OZ_PANEL;
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb) {
+        const int q = 2 * kb + h;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) xa[kb][i] = *(const v4i*)(buf + oz_lds_off(ca0 + 32 * i, q));
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) xb[kb][j] = *(const v4i*)(lbp + oz_lds_off(cb0 + 32 * j, q));
+      }
+    };
+    auto mm = [&](int kb, const v4i (&xa)[2][4], const v4i (&xb)[2][NJ]) __attribute__((always_inline)) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(xa[kb][i], xb[kb][j], acc[i][j], 0, 0, 0);
+    };
+    // stage s in registers set R; its second half overlaps the reads of stage s + 1 into set 1 - R
+    auto pstep = [&](int R, int8_t* nbuf, int8_t* buf3, int64_t s) __attribute__((always_inline)) {
+      mm(0, fa[R], fb[R]);
+      if (s + 1 < s1) {
+        wait_stages(s1 - 1 - (s + 1) < 1 ? s1 - 1 - (s + 1) : 1);   // own copies of s + 1 landed
+        __builtin_amdgcn_s_barrier();                                // everyone's; buffer s - 1 free
+        if (s + 3 < s1) issue(buf3, s + 3);
+        rd(nbuf, fa[1 - R], fb[1 - R]);
+      }
+      mm(1, fa[R], fb[R]);
+    };
+    if (s0 < s1) {
+      wait_stages(s1 - 1 - s0 < 2 ? s1 - 1 - s0 : 2);
+      __builtin_amdgcn_s_barrier();
+      rd(lb0, fa[0], fb[0]);
+    }
+    for (int64_t s = s0; s < s1; s += 4) {
+      pstep(0, lb1, lb3, s);
+      if (s + 1 < s1) pstep(1, lb2, lb0, s + 1);
+      if (s + 2 < s1) pstep(0, lb3, lb1, s + 2);
+      if (s + 3 < s1) pstep(1, lb0, lb2, s + 3);
+    }
+  }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int v = acc[i][j][r] % m;
+        acc[i][j][r] = v < 0 ? v + m : v;
+      }
+  if (idle) return;
+  uint8_t* o = out + (int64_t)it * OZ_TT * OZ_TT;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int col = CT * wj + 32 * j + (lane & 31);
+#pragma unroll
+      for (int gq = 0; gq < 4; ++gq) {   // 32 x 32 D map: rows (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
+        const int row = 128 * wi + 32 * i + 8 * gq + 4 * h;
+        const uint32_t v = (uint32_t)acc[i][j][4 * gq] | ((uint32_t)acc[i][j][4 * gq + 1] << 8) |
+                           ((uint32_t)acc[i][j][4 * gq + 2] << 16) | ((uint32_t)acc[i][j][4 * gq + 3] << 24);
+        *(uint32_t*)(o + (int64_t)col * OZ_TT + row) = v;
+      }
+    }
+}
+
+// ---------------------------------------------------------------------------- 4. CRT and scaling
+namespace {
+
+// The signed integer with residues r[l] (0 <= r < m_l, |value| < M / 2) as a double (one rounding).
+template <int NMOD>
+__host__ __device__ __forceinline__ double oz_crt(const int (&r)[NMOD], const OzTab& tab) {
+  int d[NMOD];
+#pragma unroll
+  for (int l = 0; l < NMOD; ++l) {
+    const int m = oz_mod(l);
+    int t = r[l];
+#pragma unroll
+    for (int k = 0; k < l; ++k) {
+      t = t - d[k] + 2 * m;                    // >= 0: d[k] < 256 <= 2 m
+      t = (t * tab.inv[l][k]) % m;             // < 3 m 256: int
+    }
+    d[l] = t;
+  }
+  // v = d0 + m0 (d1 + m1 (d2 + ...)): Horner from the top digit in 6 x 32-bit limbs
+  uint32_t v[6] = {(uint32_t)d[NMOD - 1], 0, 0, 0, 0, 0};
+#pragma unroll
+  for (int l = NMOD - 2; l >= 0; --l) {
+    uint64_t carry = (uint64_t)d[l];
+#pragma unroll
+    for (int q = 0; q < 6; ++q) {
+      const uint64_t x = (uint64_t)v[q] * (uint64_t)oz_mod(l) + carry;
+      v[q] = (uint32_t)x;
+      carry = x >> 32;
+    }
+  }
+  // v > M / 2 -> negative: |value| = M - v
+  bool gt = false, eq = true;
+#pragma unroll
+  for (int q = 5; q >= 0; --q) {
+    if (eq && v[q] != tab.halfM[NMOD][q]) {
+      gt = v[q] > tab.halfM[NMOD][q];
+      eq = false;
+    }
+  }
+  const bool neg = gt;
+  if (neg) {
+    uint64_t borrow = 0;
+#pragma unroll
+    for (int q = 0; q < 6; ++q) {
+      const uint64_t x = (uint64_t)tab.M[NMOD][q] - (uint64_t)v[q] - borrow;
+      v[q] = (uint32_t)x;
+      borrow = (x >> 32) & 1u;
+    }
+  }
+  // top 64 bits + sticky -> double (correctly rounded), times 2^(32 k)
+  int top = 5;
+  while (top > 0 && v[top] == 0) --top;
+  if (top == 0) return neg ? -(double)v[0] : (double)v[0];
+  uint64_t hi = ((uint64_t)v[top] << 32) | v[top - 1];
+  int e = 32 * (top - 1);
+  uint32_t sticky = 0;
+  for (int q = 0; q < top - 1; ++q) sticky |= v[q];
+  const int lz = __builtin_clzll(hi);   // hi >= 2^32: lz <= 31
+  if (lz > 0 && top >= 2) {   // pull the next limb's bits under the leading zeros
+    hi = (hi << lz) | ((uint64_t)v[top - 2] >> (32 - lz));
+    e -= lz;
+    sticky = (v[top - 2] & ((1u << (32 - lz)) - 1u)) != 0u ? 1u : 0u;   // the bits not pulled up
+    for (int q = 0; q < top - 2; ++q) sticky |= v[q];
+  } else if (lz > 0) {
+    hi <<= lz;
+    e -= lz;
+  }
+  const double dv = ldexp((double)(hi | (sticky ? 1ull : 0ull)), e);
+  return neg ? -dv : dv;
+}
+
+}  // namespace
+
+// One workgroup per lower 256 x 256 tile and 16-column strip: thread i computes rows i of the
+// strip's 16 columns (element (I 256 + i, J 256 + j)), writes it column-major into G, and the
+// mirror element through an LDS transpose.  Columns / rows not live are 0.
+template <int NMOD>
+__global__ __launch_bounds__(256) void ppls_oz_finish_kernel(const uint8_t* __restrict__ part, int nsplit, int ntiles,
+                                                             OzCols g, int P, const int* __restrict__ shift,
+                                                             double* __restrict__ G) {
+  __shared__ double tr[16][OZ_TT + 1];
+  const int t = blockIdx.x, strip = blockIdx.y;
+  int I, J;
+  oz_tile_of(t, &I, &J);
+  const int i = threadIdx.x;
+  const int a = I * OZ_TT + i;
+#pragma unroll 1
+  for (int jj = 0; jj < 16; ++jj) {
+    const int j = strip * 16 + jj;
+    const int bcol = J * OZ_TT + j;
+    double v = 0.0;
+    const bool lower = !(I == J && j > i);
+    if (a < P && bcol < P && lower && oz_live(g, a) && oz_live(g, bcol)) {
+      int r[NMOD];
+#pragma unroll
+      for (int l = 0; l < NMOD; ++l) {   // the splits' residues, summed mod m_l
+        int acc = 0;
+        for (int sp = 0; sp < nsplit; ++sp)
+          acc += part[(((int64_t)l * nsplit + sp) * ntiles + t) * OZ_TT * OZ_TT + (int64_t)j * OZ_TT + i];
+        r[l] = acc % oz_mod(l);
+      }
+      v = ldexp(oz_crt<NMOD>(r, oz_tab), -(shift[a] + shift[bcol]));
+    }
+    tr[jj][i] = v;
+    if (a < P && bcol < P && lower) G[(int64_t)bcol * P + a] = v;   // (a, b) of the lower triangle
+  }
+  __syncthreads();
+  // mirror: element (b, a) = G[a * P + b]; lanes along b (16 columns) x 16 rows a per pass
+  const int jj = threadIdx.x & 15;
+  for (int ib = threadIdx.x >> 4; ib < OZ_TT; ib += 16) {
+    const int aa = I * OZ_TT + ib, bb = J * OZ_TT + strip * 16 + jj;
+    if (aa < P && bb < P && !(I == J && strip * 16 + jj >= ib)) G[(int64_t)aa * P + bb] = tr[jj][ib];
+  }
+}
+
+extern "C" {
+
+int ppls_oz_modulus(int l) { return l >= 0 && l < PPLS_OZ_MAXMOD ? oz_mod(l) : 0; }
+
+// Host copies of the device arithmetic, for unit tests without a GPU (tests/test_ozaki_host.py).
+int ppls_oz_residue_host(double x, int shift, int l, int* r) {
+  if (l < 0 || l >= PPLS_OZ_MAXMOD || !r) return -1;
+  const double xs = rint(ldexp(x, shift));
+  if (!(fabs(xs) < 4611686018427387904.0)) return -1;   // |x'| < 2^62
+  const uint64_t u = (uint64_t)((int64_t)xs + (int64_t)(1ull << 62));
+  const uint32_t m = (uint32_t)oz_mod(l);
+  *r = oz_residue((uint32_t)(u >> 32), (uint32_t)u, m, (uint32_t)((1ull << 32) % m), (uint32_t)((1ull << 62) % m));
+  return 0;
+}
+
+int ppls_oz_crt_host(const int* r, int nmod, double* out) {
+  static constexpr OzTab tab = oz_make_tab();
+  if (!r || !out) return -1;
+#define OZ_CRT_H(N)                                         \
+  case N: {                                                 \
+    int rr[N];                                              \
+    for (int l = 0; l < N; ++l) rr[l] = r[l];               \
+    *out = oz_crt<N>(rr, tab);                              \
+    return 0;                                               \
+  }
+  switch (nmod) {
+    OZ_CRT_H(12) OZ_CRT_H(13) OZ_CRT_H(14) OZ_CRT_H(15) OZ_CRT_H(16) OZ_CRT_H(17) OZ_CRT_H(18) OZ_CRT_H(19)
+    OZ_CRT_H(20)
+    default: return -1;
+  }
+#undef OZ_CRT_H
+}
+
+hipError_t ppls_launch_oz_colstats(const void* X, int ldx, int xcols, int xreal, const void* Y, int ldy, int yreal,
+                                   int f32, int Pp, int64_t n, int chunks, double* part, double* out, hipStream_t st) {
+  const OzCols g{xreal, xcols, yreal};
+  const int64_t rpc = (n + chunks - 1) / chunks;
+  const dim3 grid((unsigned)((Pp + 255) / 256), (unsigned)chunks);
+  if (f32)
+    hipLaunchKernelGGL(ppls_oz_colstats_kernel<float>, grid, dim3(256), 0, st, (const float*)X, ldx, (const float*)Y,
+                       ldy, g, Pp, n, rpc, part);
+  else
+    hipLaunchKernelGGL(ppls_oz_colstats_kernel<double>, grid, dim3(256), 0, st, (const double*)X, ldx,
+                       (const double*)Y, ldy, g, Pp, n, rpc, part);
+  hipLaunchKernelGGL(ppls_oz_colstats_finish_kernel, dim3((unsigned)((Pp + 255) / 256)), dim3(256), 0, st, part, chunks,
+                     Pp, out);
+  return hipGetLastError();
+}
+
+#define OZ_NMOD_CASES(X) X(12) X(13) X(14) X(15) X(16) X(17) X(18) X(19) X(20)
+
+hipError_t ppls_launch_oz_residues(const void* X, int ldx, int xcols, int xreal, const void* Y, int ldy, int yreal,
+                                   int f32, int Pp, int64_t n, int64_t nkb, const int* shift, int nmod, int8_t* planes,
+                                   int64_t pstride, hipStream_t st) {
+  const OzCols g{xreal, xcols, yreal};
+  const dim3 grid((unsigned)((Pp + 63) / 64), (unsigned)nkb);
+#define OZ_RES(N)                                                                                               \
+  case N:                                                                                                       \
+    if (f32)                                                                                                    \
+      hipLaunchKernelGGL((ppls_oz_residue_kernel<float, N>), grid, dim3(256), 0, st, (const float*)X, ldx,      \
+                         (const float*)Y, ldy, g, Pp, n, shift, planes, pstride);                               \
+    else                                                                                                        \
+      hipLaunchKernelGGL((ppls_oz_residue_kernel<double, N>), grid, dim3(256), 0, st, (const double*)X, ldx,    \
+                         (const double*)Y, ldy, g, Pp, n, shift, planes, pstride);                              \
+    break;
+  switch (nmod) {
+    OZ_NMOD_CASES(OZ_RES)
+    default: return hipErrorInvalidValue;
+  }
+#undef OZ_RES
+  return hipGetLastError();
+}
+
+int ppls_oz_splits(int64_t nkb) { return (int)((nkb + OZ_SPLIT_STAGES - 1) / OZ_SPLIT_STAGES); }
+
+hipError_t ppls_launch_oz_syrk_v(int variant, const int8_t* planes, int64_t pstride, int Pp, int64_t nkb, int nmod,
+                                 uint8_t* part, hipStream_t st) {
+  const int T = Pp / OZ_TT, ntiles = T * (T + 1) / 2, nsplit = ppls_oz_splits(nkb);
+  const int64_t items = (int64_t)nmod * nsplit * ntiles;
+  const int64_t grid = (items + 7) / 8 * 8;
+  if (grid > 0x7fffffff) return hipErrorInvalidValue;
+#define OZ_SYRK(VV)                                                                                             \
+  case VV:                                                                                                      \
+    hipLaunchKernelGGL(ppls_oz_syrk_kernel<VV>, dim3((unsigned)grid), dim3(((VV) & 4) ? 512 : 256), 0, st, planes, \
+                       pstride, Pp, nkb, nmod, nsplit, ntiles, part);                                           \
+    break;
+  switch (variant) {
+    OZ_SYRK(514)
+#ifdef OZ_LAB
+    OZ_SYRK(512) OZ_SYRK(513) OZ_SYRK(1538) OZ_SYRK(1536)
+    OZ_SYRK(0) OZ_SYRK(1) OZ_SYRK(2) OZ_SYRK(3) OZ_SYRK(4) OZ_SYRK(5) OZ_SYRK(6) OZ_SYRK(7)
+    OZ_SYRK(8) OZ_SYRK(12) OZ_SYRK(16) OZ_SYRK(20) OZ_SYRK(64) OZ_SYRK(72) OZ_SYRK(32) OZ_SYRK(36) OZ_SYRK(40)
+    OZ_SYRK(48) OZ_SYRK(128) OZ_SYRK(384)
+#endif
+    default: return hipErrorInvalidValue;
+  }
+#undef OZ_SYRK
+  return hipGetLastError();
+}
+
+hipError_t ppls_launch_oz_syrk(const int8_t* planes, int64_t pstride, int Pp, int64_t nkb, int nmod, uint8_t* part,
+                               hipStream_t st) {
+  return ppls_launch_oz_syrk_v(OZ_SYRK_VARIANT, planes, pstride, Pp, nkb, nmod, part, st);
+}
+
+hipError_t ppls_launch_oz_finish(const uint8_t* part, int nmod, int nsplit, int Pp, int xcols, int xreal, int yreal,
+                                 int P, const int* shift, double* G, hipStream_t st) {
+  const OzCols g{xreal, xcols, yreal};
+  const int T = Pp / OZ_TT, ntiles = T * (T + 1) / 2;
+  const dim3 grid((unsigned)ntiles, (unsigned)(OZ_TT / 16));
+#define OZ_FIN(N)                                                                                               \
+  case N:                                                                                                       \
+    hipLaunchKernelGGL((ppls_oz_finish_kernel<N>), grid, dim3(256), 0, st, part, nsplit, ntiles, g, P, shift, G); \
+    break;
+  switch (nmod) {
+    OZ_NMOD_CASES(OZ_FIN)
+    default: return hipErrorInvalidValue;
+  }
+#undef OZ_FIN
+  return hipGetLastError();
+}
+
+}  // extern "C"

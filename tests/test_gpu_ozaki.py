@@ -1,0 +1,183 @@
+"""The int8-MFMA Gram of the cross-products in its Chinese-remainder form (ppls_ozaki.hip; VERDICT r5
+item 3): S = [X Y]'[X Y] (the sums EM_W_multi.R:689-690, 732-733 read off it, and variances' X'X
+:846) from v_mfma_i32_32x32x32_i8 SYRKs of residue planes.
+
+Checked against EXACT sums: every sampled entry's reference is the correctly rounded sum of the
+exact products (Dekker's two-product split, then math.fsum over products and their errors).  Per
+entry the int8 result must lie within
+
+  (a) its a-priori bound  2^-(L+1) (2^e_i sum_k |x_kj| + 2^e_j sum_k |x_ki|) + n 2^(e_i + e_j - 2L - 2)
+      + 2 2^-53 |S_ij|   (the rounding of x to x' = rint(x 2^(L - e)), the one final rounding, and the
+      reference's own rounding to fp64), and
+  (b) the fp64 GEMM's own bound  u sum_k |x_ki x_kj|,  u = 2^-53,
+
+on Gaussian data (fp64 and fp32 storage, row counts across the 65,536-row SYRK splits and partial
+64-row stages, odd widths).  The fp64 MFMA Gram's own error on the same entries is printed beside it.
+Then the fits: the cross-product EM run with the int8 Gram equals the streaming one (log-likelihood
+1e-12, loadings 1e-10), and data whose column spread the scheme cannot cover fall back to the fp64
+Gram (gram_info) with the same fit.
+"""
+import math
+
+import numpy as np
+import pytest
+
+from conftest import make_problem
+
+pytestmark = pytest.mark.gpu
+
+U = 2.0 ** -53
+
+
+def _split(a):
+    c = 134217729.0 * a
+    hi = c - (c - a)
+    return hi, a - hi
+
+
+def exact_dot(a, b):
+    """The correctly rounded value of sum_k a_k b_k (fp64 inputs) and sum_k |a_k b_k|."""
+    p = a * b
+    ah, al = _split(a)
+    bh, bl = _split(b)
+    e = ((ah * bh - p) + ah * bl + al * bh) + al * bl
+    return math.fsum(np.concatenate([p, e])), math.fsum(np.abs(p))
+
+
+def _check_entries(D, G, L, nsample, rng, label):
+    n, p = D.shape
+    mx = np.abs(D).max(axis=0)
+    e = np.array([math.frexp(v)[1] if v > 0 else 0 for v in mx])
+    asum = np.abs(D).sum(axis=0)
+    worst_a = worst_b = 0.0
+    pairs = [(i, i) for i in range(min(p, 8))] + [(int(rng.integers(p)), int(rng.integers(p))) for _ in range(nsample)]
+    for i, j in pairs:
+        if mx[i] == 0 or mx[j] == 0:
+            assert G[i, j] == 0.0
+            continue
+        s, sa = exact_dot(D[:, i], D[:, j])
+        err = abs(G[i, j] - s)
+        # the integer rounding of x, the one rounding of the exact integer sum, and the rounding of
+        # the reference s itself (the correctly rounded exact sum: |G - s| can reach a whole ulp when
+        # the scaled integer sum and the exact sum straddle a midpoint)
+        bound = (2.0 ** -(L + 1)) * (2.0 ** e[i] * asum[j] + 2.0 ** e[j] * asum[i]) + n * 2.0 ** (e[i] + e[j] - 2 * L - 2) \
+            + 2 * U * abs(s)
+        assert err <= bound * (1 + 1e-12), (label, i, j, err, bound)
+        worst_a = max(worst_a, err / bound)
+        worst_b = max(worst_b, err / (U * sa))
+    return worst_a, worst_b
+
+
+def _check_integer_pipeline(D, G, L, pairs):
+    """Bit for bit: G_ij = the correctly rounded 2^(e_i + e_j - 2L) sum_k x'_ki x'_kj, x' = rint(x 2^(L - e))
+    in Python integers (the residues, SYRKs and CRT reproduce the integer sum exactly)."""
+    from fractions import Fraction
+    e = [math.frexp(v)[1] if v > 0 else 0 for v in np.abs(D).max(axis=0)]
+    for i, j in pairs:
+        xi = [round(Fraction(float(a)) * 2 ** (L - e[i])) for a in D[:, i]]
+        xj = [round(Fraction(float(a)) * 2 ** (L - e[j])) for a in D[:, j]]
+        want = float(Fraction(sum(a * b for a, b in zip(xi, xj))) * Fraction(2) ** (e[i] + e[j] - 2 * L))
+        assert G[i, j] == want, (i, j, G[i, j].hex(), want.hex())
+
+
+@pytest.mark.parametrize("dtype", [0, 1], ids=["f64", "f32"])
+@pytest.mark.parametrize("n,p,q", [(1, 3, 2), (5, 17, 4), (127, 40, 9), (3000, 300, 31), (70_001, 70, 13),
+                                   (140_000, 33, 5)])
+def test_int8_gram_matches_exact_sums(dtype, n, p, q):
+    from ppls_amd import Context
+    X, Y, _ = make_problem(n, p, q, 1, seed=n + p)
+    if dtype:
+        X = X.astype(np.float32).astype(np.float64)
+        Y = Y.astype(np.float32).astype(np.float64)
+    rng = np.random.default_rng(7)
+    with Context(0) as c:
+        c.set_option("dtype", dtype)
+        c.set_data(X, Y)
+        for which, D in ((0, X), (1, Y)):
+            G, info = c.gram_int8(which)
+            assert 12 <= info["nmod"] <= 20 and info["L"] <= 62
+            assert np.array_equal(G, G.T)
+            wa, wb = _check_entries(D, G, info["L"], 200 if n < 100_000 else 60, rng, (which, n, p))
+            if n <= 5000:
+                k = D.shape[1]
+                _check_integer_pipeline(D, G, info["L"], [(0, 0), (k - 1, 0), (k - 1, k - 1)] +
+                                        [(int(rng.integers(k)), int(rng.integers(k))) for _ in range(12)])
+            Gf, _ = c.gram(which)   # the fp64 MFMA Gram, for the record
+            if n >= 100:
+                assert wb <= 1.0, (which, wb)   # (b): within the fp64 GEMM's own bound
+            print(f"n={n} which={which} dtype={dtype}: nmod {info['nmod']} L {info['L']}: int8 error / a-priori "
+                  f"bound {wa:.3g}, / (u sum|x x|) {wb:.3g}; fp64-MFMA max |diff| to int8 "
+                  f"{np.abs(Gf - G).max() / max(np.abs(G).max(), 1e-300):.2e} rel")
+
+
+def test_int8_joint_gram_blocks():
+    """The joint [X Y]'[X Y] over the padded columns (what forms S): its X'X and Y'Y blocks equal the
+    per-block int8 Grams bit for bit (the same column scalings, exact integer sums), the X'Y block
+    matches exact sums within its bound, padding columns are 0."""
+    from ppls_amd import Context
+    n, p, q = 9000, 61, 45
+    X, Y, _ = make_problem(n, p, q, 1, seed=3)
+    with Context(0) as c:
+        c.set_data(X, Y)
+        GJ, info = c.gram_int8(2)
+        GX, ix = c.gram_int8(0)
+        GY, iy = c.gram_int8(1)
+    ldx = GJ.shape[0] - (q + 1) // 2 * 2   # fp64 rows of p <= 2048 columns are padded to even lengths
+    assert ldx >= p
+    if info["L"] == ix["L"]:
+        assert np.array_equal(GJ[:p, :p], GX)
+    if info["L"] == iy["L"]:
+        assert np.array_equal(GJ[ldx:ldx + q, ldx:ldx + q], GY)
+    assert np.all(GJ[p:ldx, :] == 0) and np.all(GJ[:, p:ldx] == 0)
+    D = np.hstack([X, np.zeros((n, ldx - p)), Y, np.zeros((n, GJ.shape[0] - ldx - q))])
+    _check_entries(D, GJ, info["L"], 150, np.random.default_rng(2), "joint")
+
+
+@pytest.mark.parametrize("dtype", [0, 1], ids=["f64", "f32"])
+def test_xprod_fit_with_int8_gram_equals_streaming(dtype):
+    """The EM loop from S formed by the int8 Gram = the streaming fit (the iterates of
+    EM_W_multi.R:780-793 to rounding); gram_info names the Gram that ran."""
+    from ppls_amd import Context, Theta
+    n, p, q, r = 20_000, 150, 90, 4
+    X, Y, th0 = make_problem(n, p, q, r, seed=11)
+    th = Theta(th0["W"], th0["C"], th0["B"], th0["sigE"], th0["sigF"], th0["sigH"], th0["sigT"])
+    with Context(0) as c:
+        c.set_option("dtype", dtype)
+        c.set_data(X, Y)
+        c.set_option("xprod", 0)
+        est_s, ll_s, _, _ = c.em_run(th, 12, -np.inf, 0, want_eout=False)
+        c.set_option("xprod", 1)
+        c.set_option("gram_int8", 1)
+        est_x, ll_x, _, _ = c.em_run(th, 12, -np.inf, 0, want_eout=False)
+        gi = c.gram_info()
+        assert gi["int8"] and c.xprod_info(r)["ready"]
+        assert np.abs(ll_x - ll_s).max() / np.abs(ll_s).max() < 1e-12
+        assert np.abs(est_x.W - est_s.W).max() < 1e-10 and np.abs(est_x.C - est_s.C).max() < 1e-10
+        # option changes drop S; the fp64 Gram forms it again and gives the same fit
+        c.set_option("gram_int8", 0)
+        est_f, ll_f, _, _ = c.em_run(th, 12, -np.inf, 0, want_eout=False)
+        assert not c.gram_info()["int8"]
+        assert np.abs(ll_f - ll_x).max() / np.abs(ll_s).max() < 1e-12
+
+
+def test_int8_gram_falls_back_when_the_spread_is_too_wide():
+    """A column whose largest value dwarfs its typical ones needs L > 62 bits (c_j = 2^e_j sqrt(n /
+    sum x^2) huge): the int8 form declines and S comes from the fp64 MFMA Gram -- same fit."""
+    from ppls_amd import Context, PplsError, Theta
+    n, p, q, r = 40_000, 40, 30, 2
+    X, Y, th0 = make_problem(n, p, q, r, seed=5)
+    # column 3: one huge value among O(1) ones: c_3 ~ 2^30 / 1e9 sqrt(n) ~ 215 > 2^7, L = 63 (a lone
+    # outlier gives c <= 2 sqrt(n): at n = 4,000 it would still fit in L = 62)
+    X[17, 3] = 1e9
+    th = Theta(th0["W"], th0["C"], th0["B"], th0["sigE"], th0["sigF"], th0["sigH"], th0["sigT"])
+    with Context(0) as c:
+        c.set_data(X, Y)
+        with pytest.raises(PplsError):
+            c.gram_int8(0)
+        c.set_option("xprod", 0)
+        _, ll_s, _, _ = c.em_run(th, 6, -np.inf, 0, want_eout=False)
+        c.set_option("xprod", 1)
+        c.set_option("gram_int8", 1)
+        _, ll_x, _, _ = c.em_run(th, 6, -np.inf, 0, want_eout=False)
+        assert not c.gram_info()["int8"]
+        assert np.abs(ll_x - ll_s).max() / np.abs(ll_s).max() < 1e-12

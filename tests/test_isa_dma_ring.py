@@ -10,7 +10,10 @@ states why that is safe and what must hold, and these tests check it mechanicall
   * the schedule: every instantiation's (SLOTS, RP, CPW) from the built symbols, every row count a
     workgroup can get (0 .. 80, and large ones), both mu modes: no row read before its copies
     landed, no slot refilled before its row was read; a count one row too large is caught;
-  * the sources: no other inline asm issues a memory load.
+  * the sources: no other inline asm issues a memory load;
+  * the int8 Gram's SYRK ring (ppls_ozaki.hip, V = 512/513; the same asm copies): hand wait before
+    every barrier, only vmcnt(0 | 2 NC), a drain after the last copy, and its ring restated and
+    simulated for every stage count of a split (1 .. 1024) with a negative control.
 """
 import os
 
@@ -33,14 +36,18 @@ def kernels():
     return {n: ins for n, ins in fns.items() if any(x[1].startswith(ic.DMA) for x in ins)}
 
 
-def test_only_split_sweep_kernels_use_lds_dma(kernels):
+def test_only_split_sweep_and_syrk_kernels_use_lds_dma(kernels):
     assert kernels, "no LDS-DMA kernel found: the split sweep should use it"
-    assert all(ic.split_params(n) for n in kernels), [n for n in kernels if not ic.split_params(n)]
+    other = [n for n in kernels if not ic.split_params(n) and not (ic.oz_variant(n) or 0) & 512]
+    assert not other, other
+    assert any(ic.split_params(n) for n in kernels) and any(ic.oz_variant(n) for n in kernels)
 
 
 def test_built_split_kernels_dma_form_and_runs(kernels):
     bad = {}
     for n, ins in kernels.items():
+        if not ic.split_params(n):
+            continue
         pr = ic.check_kernel(ins, ic.split_params(n)[6])
         if pr:
             bad[n[:80]] = pr[:5]
@@ -48,7 +55,7 @@ def test_built_split_kernels_dma_form_and_runs(kernels):
 
 
 def test_ring_schedule_every_built_instantiation(kernels):
-    shapes = {(p[5], p[3], p[6]) for p in map(ic.split_params, kernels)}   # (SLOTS, RP, CPW)
+    shapes = {(p[5], p[3], p[6]) for p in map(ic.split_params, kernels) if p}   # (SLOTS, RP, CPW)
     assert shapes
     for SLOTS, RP, CPW in sorted(shapes):
         for write_mu in (False, True):
@@ -82,3 +89,25 @@ def test_isa_checker_negative_controls():
 
 def test_no_other_inline_asm_loads():
     assert ic.sources_with_asm_loads() == []
+
+
+def test_built_syrk_ring_waits(kernels):
+    oz = {n: ins for n, ins in kernels.items() if (ic.oz_variant(n) or 0) & 512}
+    assert oz
+    bad = {n[:60]: ic.check_oz_kernel(ins)[:5] for n, ins in oz.items() if ic.check_oz_kernel(ins)}
+    assert not bad, bad
+
+
+def test_syrk_ring_schedule_and_negative_control():
+    for NC in (4, 8):
+        for ns in list(range(1, 41)) + [255, 1023, 1024]:
+            pr = ic.ring_schedule_oz(ns, NC)
+            assert not pr, (NC, ns, pr[:3])
+        # one stage too many in flight at the wait: a read before its copies landed must be caught
+        assert any(ic.ring_schedule_oz(ns, NC, bias=NC) for ns in range(2, 20)), NC
+    # the checker flags a barrier whose hand wait is missing and a kernel that never drains
+    dma = [(0, "s_mov_b32", "m0, s4", None), (4, "s_nop", "0", None), (8, "global_load_lds_dwordx4", "v1, s[2:3]", None)]
+    assert ic.check_oz_kernel(dma + [(12, "s_waitcnt", "vmcnt(16)", None), (16, "s_barrier", "", None),
+                                     (20, "s_waitcnt", "vmcnt(0)", None)]) == []
+    assert ic.check_oz_kernel(dma + [(16, "s_barrier", "", None), (20, "s_waitcnt", "vmcnt(0)", None)])
+    assert ic.check_oz_kernel(dma + [(12, "s_waitcnt", "vmcnt(16)", None), (16, "s_barrier", "", None)])

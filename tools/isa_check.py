@@ -16,7 +16,8 @@ only make a wait stricter).  That argument holds only if
       move code between the M0 write and the copy;
   (2) each row issue is exactly CPW copies in straight-line code (the count k is in units of CPW
       copies per row): the DMA ops form unbranched runs of exactly CPW;
-  (3) no kernel other than the split sweep issues LDS-DMA (no experiment code left in the product);
+  (3) no kernel other than the split sweep and the int8 Gram's SYRK (ppls_ozaki.hip:
+      ppls_oz_syrk_kernel, variants 512..514) issues LDS-DMA (no experiment code in the product);
   (4) the k the kernel computes is right: the ring schedule of ppls_kernels.hip:496-541, restated in
       ring_schedule() below, is simulated for every instantiation and every row count of a workgroup
       (in-order retirement, CPW copies per row per DMA wave), checking that every row a workgroup
@@ -24,7 +25,12 @@ only make a wait stricter).  That argument holds only if
   (5) no other inline asm in the product issues a memory load (no VGPR-destination asm loads):
       sources_with_asm_loads() scans ppls_amd/csrc.
 
-tests/test_isa_dma_ring.py runs all five on the product library.
+  (6) the SYRK ring (4 buffers, copies of stage s + 3 issued during stage s, NC = 4 or 8 copies per
+      wave per stage): every barrier is preceded by a hand wait vmcnt(2 NC), every vmcnt wait is 0
+      or 2 NC, the kernel drains (vmcnt(0)) after its last copy, and ring_schedule_oz() -- the loop
+      restated -- reads no stage before its copies landed and refills no buffer before it was read.
+
+tests/test_isa_dma_ring.py runs all six on the product library.
 """
 from __future__ import annotations
 
@@ -40,15 +46,27 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 DMA = ("global_load_lds_", "buffer_load_lds_")  # LDS-DMA mnemonics (gfx950: global_load_lds_dwordx4 ...)
 
 
+_MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
+
+
 def disassemble(lib: str) -> str:
-    """llvm-objdump of the gfx950 code object inside a HIP object / shared library."""
+    """llvm-objdump of every gfx950 code object inside a HIP object / shared library (a linked
+    library's .hip_fatbin holds one offload bundle per translation unit, back to back)."""
     with tempfile.TemporaryDirectory() as d:
-        fb, co = os.path.join(d, "fb"), os.path.join(d, "co")
+        fb = os.path.join(d, "fb")
         subprocess.run(["objcopy", "-O", "binary", "--only-section=.hip_fatbin", lib, fb], check=True)
-        subprocess.run([f"{LLVM}/clang-offload-bundler", "--unbundle", "--type=o", f"--input={fb}",
-                        "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={co}"], check=True)
-        return subprocess.run([f"{LLVM}/llvm-objdump", "-d", "--no-show-raw-insn", co], capture_output=True,
-                              text=True, check=True).stdout
+        blob = open(fb, "rb").read()
+        starts = [m.start() for m in re.finditer(re.escape(_MAGIC), blob)]
+        out = []
+        for k, a in enumerate(starts):
+            part, co = os.path.join(d, f"b{k}"), os.path.join(d, f"co{k}")
+            with open(part, "wb") as f:
+                f.write(blob[a:starts[k + 1] if k + 1 < len(starts) else len(blob)])
+            subprocess.run([f"{LLVM}/clang-offload-bundler", "--unbundle", "--type=o", f"--input={part}",
+                            "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={co}"], check=True)
+            out.append(subprocess.run([f"{LLVM}/llvm-objdump", "-d", "--no-show-raw-insn", co],
+                                      capture_output=True, text=True, check=True).stdout)
+        return "\n".join(out)
 
 
 _FUNC = re.compile(r"^([0-9a-f]+) <([^>]+)>:$")
@@ -84,6 +102,99 @@ def split_params(name: str):
     """(R, NSH, NT, RP, PIPE, SLOTS, CPW) of a split-sweep instantiation from its mangled name."""
     m = _TARGS.search(name)
     return tuple(int(g) for g in m.groups()) if m else None
+
+
+_OZ = re.compile(r"ppls_oz_syrk_kernelILi(\d+)EE")
+
+
+def oz_variant(name: str):
+    """The SYRK variant V of a ppls_oz_syrk_kernel<V> instantiation, else None."""
+    m = _OZ.search(name)
+    return int(m.group(1)) if m else None
+
+
+def dma_form_problems(ins: list) -> list:
+    """Check (1) alone: every DMA is the asm triple (s_mov_b32 m0 ; s_nop ; copy vOFF, s[base])."""
+    probs = []
+    for i, (a, mn, ops, _) in enumerate(ins):
+        if not mn.startswith(DMA):
+            continue
+        fields = [f.strip() for f in ops.replace(" nt", "").split(",")]
+        if not (len(fields) == 2 and re.fullmatch(r"v\d+", fields[0]) and re.fullmatch(r"s\[\d+:\d+\]", fields[1])):
+            probs.append(f"{a:x}: DMA operands not (vOFF, s[base]): {mn} {ops}")
+        j = i - 1
+        while j >= 0 and ins[j][1] == "s_nop":
+            j -= 1
+        if j < 0 or ins[j][1] != "s_mov_b32" or not ins[j][2].startswith("m0,"):
+            probs.append(f"{a:x}: DMA not directly preceded by its s_mov_b32 m0")
+    return probs
+
+
+_VMC = re.compile(r"vmcnt\((\d+)\)")
+
+
+def check_oz_kernel(ins: list) -> list:
+    """Check (6) on the built SYRK: hand waits before barriers, wait counts, the final drain."""
+    probs = dma_form_problems(ins)
+    ks = {int(m.group(1)) for (_, mn, ops, _) in ins if mn == "s_waitcnt" for m in [_VMC.search(ops)] if m}
+    if not ks <= {0, 8, 16}:
+        probs.append(f"vmcnt waits {sorted(ks)}: only 0 and 2 NC (8 on the diagonal, 16 off it) are scheduled")
+    for i, (a, mn, _, _) in enumerate(ins):
+        if mn != "s_barrier":
+            continue
+        k, j = None, i - 1
+        while j >= 0 and not ins[j][1].startswith(DMA) and ins[j][1] not in ("s_barrier",):
+            if ins[j][1] == "s_waitcnt":
+                m = _VMC.search(ins[j][2])
+                if m:
+                    k = int(m.group(1))
+                    break
+            j -= 1
+        if k not in (8, 16):
+            probs.append(f"{a:x}: barrier without its hand wait vmcnt(8 | 16) after the last copy (found {k})")
+    last_dma = max((n for n, x in enumerate(ins) if x[1].startswith(DMA)), default=None)
+    if last_dma is not None:
+        tail = ins[last_dma + 1:]
+        drained = any(x[1] == "s_waitcnt" and _VMC.search(x[2]) and int(_VMC.search(x[2]).group(1)) == 0 for x in tail)
+        if not drained:
+            probs.append("no vmcnt(0) after the last copy: copies could land after the workgroup's LDS is gone")
+    return probs
+
+
+def ring_schedule_oz(nstages: int, NC: int, bias: int = 0) -> list:
+    """Restatement of ppls_oz_syrk_kernel's ring (V = 512; ppls_ozaki.hip, `run`): 4 buffers, the
+    prologue copies stages 0..2 (clamped to the last stage), step s waits vmcnt <= 2 NC, barriers,
+    reads stage s from buffer s % 4 and copies stage min(s + 3, last) into buffer (s + 3) % 4; the
+    tail drains.  One wave, in-order retirement.  bias is added to the wait (negative control)."""
+    q = deque()                 # outstanding copies: (buffer, stage)
+    buf = {}                    # buffer -> stage it holds or is receiving
+    read = set()
+    probs = []
+    last = lambda s: min(s, nstages - 1)
+
+    def issue(b, st):
+        old = buf.get(b)
+        if old is not None and old not in read and old != st:
+            probs.append(f"stage {st} refills buffer {b} before stage {old} was read")
+        buf[b] = st
+        q.extend([(b, st)] * NC)
+
+    if nstages <= 0:
+        return probs
+    for k in range(3):
+        issue(k, last(k))
+    for s in range(nstages):
+        while len(q) > 2 * NC + bias:
+            q.popleft()
+        # barrier; every wave's copies of stage s landed (each waited for its own)
+        if any(b == s % 4 for (b, _) in q):
+            probs.append(f"stage {s} read while a copy into its buffer is in flight")
+        if buf.get(s % 4) != s:
+            probs.append(f"stage {s}'s buffer holds stage {buf.get(s % 4)}")
+        read.add(s)
+        issue((s + 3) % 4, last(s + 3))
+    q.clear()
+    return probs
 
 
 def check_kernel(ins: list, cpw: int) -> list:
@@ -210,7 +321,12 @@ def main():
         if not n_dma:
             continue
         pr = split_params(name)
-        probs = check_kernel(ins, pr[6]) if pr else [f"LDS-DMA in a kernel that is not the split sweep: {name}"]
+        if pr:
+            probs = check_kernel(ins, pr[6])
+        elif (oz_variant(name) or 0) & 512:
+            probs = check_oz_kernel(ins)
+        else:
+            probs = [f"LDS-DMA in a kernel that is not the split sweep or the SYRK: {name}"]
         total += len(probs)
         print(f"{name[:90]}: {n_dma} DMA ops, {len(ins)} instructions, {len(probs)} problems")
         for p in probs[:10]:
