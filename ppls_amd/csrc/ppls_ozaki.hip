@@ -124,14 +124,6 @@ __device__ __forceinline__ double oz_ld(const T* X, int ldx, const T* Y, int ldy
 
 }  // namespace
 
-// The symmetric residue of x' = u - 2^62 (u = hi 2^32 + lo) modulo m: |result| <= m / 2 <= 128.
-// c32 = 2^32 mod m, c62 = 2^62 mod m.  (With a compile-time m the three % are multiply-high forms.)
-__host__ __device__ __forceinline__ int oz_residue(uint32_t hi, uint32_t lo, uint32_t m, uint32_t c32, uint32_t c62) {
-  uint32_t r = ((hi % m) * c32 + lo % m) % m;   // u mod m
-  r = r >= c62 ? r - c62 : r + m - c62;         // x' mod m in [0, m)
-  return (int)r > (int)(m / 2) ? (int)r - (int)m : (int)r;
-}
-
 // ---------------------------------------------------------------------------- 1. column statistics
 // part[chunk][2][Pp]: per column the max |D| and sum D^2 over the chunk's rows (one thread per
 // column, rows strided by the grid's y dimension).
@@ -167,19 +159,31 @@ __global__ void ppls_oz_colstats_finish_kernel(const double* __restrict__ part, 
 }
 
 // ---------------------------------------------------------------------------- 2. residue planes
-// Block: one 64-row stage kb x 64 columns.  Thread: column c0 + (tid & 63), rows 16 (tid >> 6) ..
-// + 15 of the stage.  x' = rint(D 2^shift_c) (exact), u = x' + 2^62 >= 0 split into 32-bit halves,
-// u mod m = ((hi mod m) (2^32 mod m) + lo mod m) mod m, then minus 2^62 mod m, symmetric.
+// Block: one 64-row stage kb x 64 columns.  Thread: column c0 + (tid >> 2), rows 16 (tid & 3) .. + 15
+// of the stage.  x' = rint(D 2^shift_c) (exact), u = x' + 2^62 in [0, 2^63) as three 21-bit limbs
+// u = a 2^42 + b 2^21 + c; per modulus  u mod m = (a (2^42 mod m) + b (2^21 mod m) + c) mod m  -- two
+// 24-bit multiply-adds (operands < 2^24) and ONE 32-bit reduction of a value < 2^31 -- then minus
+// 2^62 mod m (folded into the sum as m - (2^62 mod m)), symmetric.  (The residue arithmetic, not the
+// 106 GB of C3 traffic, bounded the first form's three 32-bit reductions per residue: 41 ms.)
+__host__ __device__ __forceinline__ int oz_residue21(uint32_t a, uint32_t b, uint32_t c, uint32_t m, uint32_t k42,
+                                                     uint32_t k21, uint32_t bias) {
+  const uint32_t t = a * k42 + b * k21 + c + bias;   // < 2^21 255 2 + 2^21 + 256 < 2^31
+  const uint32_t r = t % m;                           // x' mod m in [0, m)
+  return (int)r > (int)(m / 2) ? (int)r - (int)m : (int)r;
+}
+
 template <typename T, int NMOD>
 __global__ __launch_bounds__(256) void ppls_oz_residue_kernel(const T* __restrict__ X, int ldx, const T* __restrict__ Y,
                                                               int ldy, OzCols g, int Pp, int64_t n,
                                                               const int* __restrict__ shift, int8_t* __restrict__ planes,
                                                               int64_t pstride) {
   const int tid = threadIdx.x;
-  const int c = blockIdx.x * 64 + (tid & 63), grp = tid >> 6;
+  // 4 lanes per column (row groups fastest): a wave stores 16 columns x 64 B = 1 KB contiguous per
+  // plane (lanes 64 B apart, the first form, left every store a 16-B scatter) and loads 4 rows x 128 B
+  const int c = blockIdx.x * 64 + (tid >> 2), grp = tid & 3;
   const int64_t kb = blockIdx.y;
   const int64_t row0 = kb * OZ_KS + 16 * grp;
-  uint32_t hi[16], lo[16];
+  uint32_t la[16], lb[16], lc[16];
   const bool live = c < Pp && oz_live(g, c);
   const int sh = live ? shift[c] : 0;
 #pragma unroll
@@ -188,18 +192,21 @@ __global__ __launch_bounds__(256) void ppls_oz_residue_kernel(const T* __restric
     const double x = (live && row < n) ? oz_ld(X, ldx, Y, ldy, g, row, c) : 0.0;
     const double xs = rint(ldexp(x, sh));                        // |xs| < 2^L <= 2^62, an exact integer
     const uint64_t u = (uint64_t)((int64_t)xs + (int64_t)(1ull << 62));
-    hi[k] = (uint32_t)(u >> 32);
-    lo[k] = (uint32_t)u;
+    la[k] = (uint32_t)(u >> 42);
+    lb[k] = (uint32_t)(u >> 21) & 0x1FFFFFu;
+    lc[k] = (uint32_t)u & 0x1FFFFFu;
   }
   if (c >= Pp) return;
   int8_t* dst = planes + (kb * Pp + c) * OZ_KS + 16 * grp;
 #pragma unroll
   for (int l = 0; l < NMOD; ++l) {
     const uint32_t m = (uint32_t)oz_mod(l);
-    const uint32_t c32 = (uint32_t)((1ull << 32) % m), c62 = (uint32_t)((1ull << 62) % m);
+    const uint32_t k42 = (uint32_t)((1ull << 42) % m), k21 = (uint32_t)((1ull << 21) % m);
+    const uint32_t bias = m - (uint32_t)((1ull << 62) % m);
     uint32_t w[4] = {0, 0, 0, 0};
 #pragma unroll
-    for (int k = 0; k < 16; ++k) w[k >> 2] |= ((uint32_t)oz_residue(hi[k], lo[k], m, c32, c62) & 255u) << (8 * (k & 3));
+    for (int k = 0; k < 16; ++k)
+      w[k >> 2] |= ((uint32_t)oz_residue21(la[k], lb[k], lc[k], m, k42, k21, bias) & 255u) << (8 * (k & 3));
     *(v4i*)(dst + (int64_t)l * pstride) = v4i{(int)w[0], (int)w[1], (int)w[2], (int)w[3]};
   }
 }
@@ -712,7 +719,8 @@ int ppls_oz_residue_host(double x, int shift, int l, int* r) {
   if (!(fabs(xs) < 4611686018427387904.0)) return -1;   // |x'| < 2^62
   const uint64_t u = (uint64_t)((int64_t)xs + (int64_t)(1ull << 62));
   const uint32_t m = (uint32_t)oz_mod(l);
-  *r = oz_residue((uint32_t)(u >> 32), (uint32_t)u, m, (uint32_t)((1ull << 32) % m), (uint32_t)((1ull << 62) % m));
+  *r = oz_residue21((uint32_t)(u >> 42), (uint32_t)(u >> 21) & 0x1FFFFFu, (uint32_t)u & 0x1FFFFFu, m,
+                    (uint32_t)((1ull << 42) % m), (uint32_t)((1ull << 21) % m), m - (uint32_t)((1ull << 62) % m));
   return 0;
 }
 
