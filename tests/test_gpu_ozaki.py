@@ -110,6 +110,30 @@ def test_int8_gram_matches_exact_sums(dtype, n, p, q):
                   f"{np.abs(Gf - G).max() / max(np.abs(G).max(), 1e-300):.2e} rel")
 
 
+@pytest.mark.parametrize("dtype,n,p,q", [(0, 1_000_000, 300, 100), (1, 500_000, 1500, 100)], ids=["c3_rows_f64", "c5_rows_f32"])
+def test_int8_gram_full_row_counts(dtype, n, p, q):
+    """At the bench configs' row counts (C3's 1e6 rows in 16 SYRK splits, C5's 5e5 fp32-stored rows in 8;
+    fewer columns so the host reference stays cheap): sampled entries of the joint Gram within the
+    a-priori bound and within u sum|x_ki x_kj| against double-double exact sums."""
+    from ppls_amd import Context
+    rng = np.random.default_rng(n)
+    X = rng.standard_normal((n, p)) * np.exp(rng.uniform(-3, 3, p))   # columns of different scales
+    Y = rng.standard_normal((n, q))
+    if dtype:
+        X = X.astype(np.float32).astype(np.float64)
+        Y = Y.astype(np.float32).astype(np.float64)
+    with Context(0) as c:
+        c.set_option("dtype", dtype)
+        c.set_data(X, Y)
+        for which, D in ((0, X), (1, Y)):
+            G, info = c.gram_int8(which)
+            assert info["L"] <= 62 and info["nmod"] <= 20
+            wa, wb = _check_entries(D, G, info["L"], 24, rng, (which, n, p))
+            assert wb <= 1.0, (which, wb)
+            print(f"n={n} which={which} dtype={dtype}: nmod {info['nmod']} L {info['L']}: / a-priori {wa:.3g}, "
+                  f"/ (u sum|x x|) {wb:.3g}, SYRK {info['ms'][1]:.1f} ms")
+
+
 def test_int8_joint_gram_blocks():
     """The joint [X Y]'[X Y] over the padded columns (what forms S): its X'X and Y'Y blocks equal the
     per-block int8 Grams bit for bit (the same column scalings, exact integer sums), the X'Y block
