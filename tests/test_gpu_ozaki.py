@@ -205,3 +205,44 @@ def test_int8_gram_falls_back_when_the_spread_is_too_wide():
         _, ll_x, _, _ = c.em_run(th, 6, -np.inf, 0, want_eout=False)
         assert not c.gram_info()["int8"]
         assert np.abs(ll_x - ll_s).max() / np.abs(ll_s).max() < 1e-12
+
+
+@pytest.mark.parametrize("k", [2, 3])
+def test_int8_gram_sharded_equals_unsharded(k):
+    """Row shards each forming their S by the int8 form (their own column plans), ONE all-reduce of S
+    (host reducer), then the iterations: ranks bitwise identical, the fit equal to the unsharded int8 and
+    streaming fits.  One rank's outlier makes only that rank fall back to the fp64 Gram: no collective
+    depends on the choice."""
+    from ppls_amd import Context, Theta
+    from test_gpu_multirank import _run_ranks
+    n, p, q, r = 60_000, 60, 40, 2   # shards of >= 20,000 rows: the outlier's c ~ 1.05 sqrt(rows) > 2^7
+    X, Y, th0 = make_problem(n, p, q, r, seed=k)
+    th = Theta(th0["W"], th0["C"], th0["B"], th0["sigE"], th0["sigF"], th0["sigH"], th0["sigT"])
+
+    def fit(c, Xs, Ys, n_total, xprod):
+        c.set_option("xprod", xprod)
+        c.set_option("gram_int8", 1)
+        c.set_data(Xs, Ys, n_total=n_total)
+        est, ll, _, _ = c.em_run(th, 8, -np.inf, 0, want_eout=False)
+        return est, ll, c.gram_info()["int8"] if xprod else None
+
+    for outlier in (False, True):
+        Xo = X.copy()
+        if outlier:
+            Xo[n - 5, 2] = 1e6   # in the last shard only: L = 63 there
+        with Context(0) as c:
+            ref_s = fit(c, Xo, Y, None, 0)
+
+        def work(rank, c):
+            r0, nl = Context.shard_range(n, k, rank)
+            return fit(c, Xo[r0:r0 + nl], Y[r0:r0 + nl], n, 1)
+
+        res = _run_ranks(k, work)
+        for est, ll, _ in res:
+            assert np.array_equal(est.W, res[0][0].W) and np.array_equal(ll, res[0][1])
+        used = [u for _, _, u in res]
+        assert used[:-1] == [True] * (k - 1) and used[-1] == (not outlier), used
+        est, ll, _ = res[0]
+        assert np.abs(ll - ref_s[1]).max() / np.abs(ref_s[1]).max() < 1e-11
+        if not outlier:   # (a 1e6 entry makes the loadings sensitive to any reordering of the sums)
+            assert np.abs(est.W - ref_s[0].W).max() < 1e-9 and np.abs(est.C - ref_s[0].C).max() < 1e-9
