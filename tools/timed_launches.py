@@ -60,6 +60,9 @@ def main():
     ap.add_argument("--name", required=True)
     ap.add_argument("--bench-json", default=None)
     ap.add_argument("--command", default=None)
+    ap.add_argument("--group", type=int, default=1,
+                    help="consecutive matching launches of a phase that form one unit (their durations summed): "
+                         "2 for the panel sweep's dots + accumulation per iteration (--kernel panel_)")
     a = ap.parse_args()
     kt = _csv(a.trace_dir, "kernel_trace.csv")
     ranges = marker_ranges(_csv(a.trace_dir, "marker_api_trace.csv"))
@@ -90,6 +93,8 @@ def main():
             ordinal += 1
     if "timed" not in per:
         sys.exit(f"no {a.kernel} launch inside bench:timed")
+    if a.group > 1:   # one unit = a.group consecutive launches (e.g. one sweep = dots + accumulation)
+        per = {ph: [sum(v[i:i + a.group]) for i in range(0, len(v) - a.group + 1, a.group)] for ph, v in per.items()}
 
     def stats(v):
         return dict(launches=len(v), avg_ms=statistics.fmean(v) / 1e6, min_ms=min(v) / 1e6, max_ms=max(v) / 1e6)
@@ -99,7 +104,7 @@ def main():
     t["achieved_GBs"] = a.bytes / (t["avg_ms"] * 1e-3) / 1e9
     t["frac"] = t["achieved_GBs"] * 1e9 / HBM_PEAK
     from pmc_summary import profiled_tree
-    out = dict(kernel=a.kernel, algorithmic_bytes_per_launch=a.bytes, hbm_peak_GBs=HBM_PEAK / 1e9,
+    out = dict(kernel=a.kernel, launches_per_unit=a.group, algorithmic_bytes_per_launch=a.bytes, hbm_peak_GBs=HBM_PEAK / 1e9,
                command=a.command, profiled_tree=profiled_tree(), phases=phases,
                ordinals={ph: v for ph, v in ords.items()}, kernel_dispatches_total=ordinal,
                timed_iteration_kernels={k: stats(v) for k, v in timed_all.items()},
