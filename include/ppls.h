@@ -107,8 +107,10 @@ const char* ppls_last_error(const ppls_ctx* ctx);
  *                      every population from one read of X, Y per EM step (the split sweep: one
  *                      segmented launch; fp32 storage / wide p, the panel sweep: one launch per
  *                      population); 0 the per-population loop driven by the host),
- *       "gram_int8" (the Gram that forms S: 0, default, fp64 MFMA; 1 the int8-MFMA Chinese-remainder
- *                    form when the columns' spread allows it -- else the fp64 one; ppls_gram_info),
+ *       "gram_int8" (the Gram that forms S and ppls_variances' X'X: 0, default, fp64 MFMA; 1 the
+ *                    int8-MFMA Chinese-remainder form when the columns' spread allows it -- else the
+ *                    fp64 one; ppls_gram_info.  Its residue planes (18 x n x (p + q) bytes at C3's
+ *                    spread) stay allocated until ppls_xprod_release, new data or gram_int8 = 0),
  *       "vorth" (the finalize re-orthonormalises the Jacobi warm start it carries between
  *                iterations every vorth-th iteration: 1 .. 255, default 8),
  *       "xprod_rw" (rows of S per wave of the cross-product tile kernel: 0 auto, 1, 2, 4, 8),

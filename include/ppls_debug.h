@@ -56,7 +56,8 @@ int ppls_gram_int8(ppls_ctx* ctx, int which, double* G, int* nmod, int* L, doubl
 int ppls_oz_residue_host(double x, int shift, int l, int* r);
 int ppls_oz_crt_host(const int* r, int nmod, double* out);
 int ppls_oz_modulus(int l);
-/* Which Gram formed the last S (1 int8 CRT form, 0 fp64 MFMA), its moduli, bits and phases (ms[4]). */
+/* Which Gram ran last -- forming S, or ppls_variances' X'X / Y'Y (1 int8 CRT form, 0 fp64 MFMA) -- its
+ * moduli, bits and phases (ms[4]). */
 int ppls_gram_info(ppls_ctx* ctx, int* int8_used, int* nmod, int* L, double* ms);
 /* The path the last ppls_meta_ppls took: 0 none yet, 1 the host loop, 2 the device loop on the split
  * sweep (one segmented launch per EM step), 3 the device loop on the panel sweep (one launch per

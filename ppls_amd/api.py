@@ -379,7 +379,8 @@ class Context:
         return G, dict(nmod=nm.value, L=L.value, ms=ms.tolist())
 
     def gram_info(self):
-        """Which Gram formed the last S: dict(int8 (bool), nmod, L, ms = [stats + residues, SYRK, CRT, total])."""
+        """Which Gram ran last (forming S, or variances' X'X / Y'Y): dict(int8 (bool), nmod, L, ms =
+        [stats + residues, SYRK, CRT, total])."""
         u, nm, L, ms = ct.c_int(), ct.c_int(), ct.c_int(), np.zeros(4)
         self._chk(self._L.ppls_gram_info(self.h, ct.byref(u), ct.byref(nm), ct.byref(L), dptr(ms)))
         return dict(int8=bool(u.value), nmod=nm.value, L=L.value, ms=ms.tolist())

@@ -126,6 +126,12 @@ struct ppls_ctx {
                             // allows; else the fp64 MFMA Gram) or the fp64 MFMA Gram (0)
   int oz_used = 0, oz_nmod = 0, oz_L = 0;   // the last formation of S: which Gram, moduli, bits
   double oz_ms[4] = {0, 0, 0, 0};           // its phases (HIP events): stats+residues, SYRK, CRT, total
+  // the int8 Gram's residue planes and SYRK output, kept between formations (allocating and freeing
+  // tens of GB per call made later calls' hipMalloc / hipFree take ~1 s each after a dozen calls,
+  // tools/oz_repeat_probe.py); freed with ppls_xprod_release, new data, gram_int8 = 0 or the context
+  int8_t* oz_planes = nullptr;
+  uint8_t* oz_res = nullptr;
+  size_t oz_planes_len = 0, oz_res_len = 0;
   bool xp_ready = false;    // S holds the (all-reduced) cross-products of the current data
   bool xp_active = false;   // statistics steps of the current run read S
   bool xp_pending_gram = false;   // the last statistics step left the Gram B'M to the next finalize
@@ -742,6 +748,14 @@ int gram_run(ppls_ctx* c, const GramShape& g, int64_t n, int req, double* G, flo
 // fewest moduli with prod m_l > 2 max_j sum_k x'_kj^2 (>= |sum_k x'_ki x'_kj| by Cauchy-Schwarz).
 // Returns 1 (not an error) when L > 62, more than PPLS_OZ_MAXMOD moduli are needed or the residue
 // planes do not fit: the caller then runs the fp64 MFMA Gram.
+void oz_free(ppls_ctx* c) {
+  dfree(c->oz_planes);
+  dfree(c->oz_res);
+  c->oz_planes = nullptr;
+  c->oz_res = nullptr;
+  c->oz_planes_len = c->oz_res_len = 0;
+}
+
 int gram_run_oz(ppls_ctx* c, const GramShape& g, int64_t n, double* G, float* ms) {
   const int P = g.p, Pp = (P + 255) / 256 * 256;
   const int64_t nkb = (n + PPLS_OZ_KS - 1) / PPLS_OZ_KS;
@@ -750,11 +764,9 @@ int gram_run_oz(ppls_ctx* c, const GramShape& g, int64_t n, double* G, float* ms
     double* part = nullptr;
     double* st = nullptr;
     int* shift = nullptr;
-    int8_t* planes = nullptr;
-    uint8_t* res = nullptr;
     hipEvent_t ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
     ~Bufs() {
-      dfree(part); dfree(st); dfree(shift); dfree(planes); dfree(res);
+      dfree(part); dfree(st); dfree(shift);
       for (auto e : ev) if (e) (void)hipEventDestroy(e);
     }
   } b;
@@ -800,21 +812,31 @@ int gram_run_oz(ppls_ctx* c, const GramShape& g, int64_t n, double* G, float* ms
   c->oz_nmod = nmod;
   const int T = Pp / 256, ntiles = T * (T + 1) / 2, nsplit = ppls_oz_splits(nkb);
   const int64_t pstride = nkb * Pp * PPLS_OZ_KS;
-  size_t fr = 0, tot = 0;
-  if (hipMemGetInfo(&fr, &tot) != hipSuccess) return 1;
-  const double want = (double)nmod * (double)pstride + (double)nmod * nsplit * ntiles * 65536.0;
-  if (want > (double)fr - std::max(1073741824.0, 0.05 * (double)fr)) return 1;
-  if (dalloc(c, &b.planes, (size_t)nmod * pstride) || dalloc(c, &b.res, (size_t)nmod * nsplit * ntiles * 65536)) {
-    c->err.clear();
-    return 1;
+  const size_t need_planes = (size_t)nmod * pstride, need_res = (size_t)nmod * nsplit * ntiles * 65536;
+  if (need_planes > c->oz_planes_len || need_res > c->oz_res_len) {   // (re)allocate the kept buffers
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    oz_free(c);
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) != hipSuccess) return 1;
+    const double want = (double)need_planes + (double)need_res;
+    if (want > (double)fr - std::max(1073741824.0, 0.05 * (double)fr)) return 1;
+    if (dalloc(c, &c->oz_planes, need_planes) || dalloc(c, &c->oz_res, need_res)) {
+      c->err.clear();
+      oz_free(c);
+      return 1;
+    }
+    c->oz_planes_len = need_planes;
+    c->oz_res_len = need_res;
   }
+  int8_t* planes = c->oz_planes;
+  uint8_t* res = c->oz_res;
   HIPCHK(c, hipMemcpyAsync(b.shift, shift.data(), sizeof(int) * Pp, hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, ppls_launch_oz_residues(g.X, g.ldx, g.xcols, g.xreal, g.Y, g.ldy, g.yreal, dtype, Pp, n, nkb, b.shift,
-                                    nmod, b.planes, pstride, c->stream));
+                                    nmod, planes, pstride, c->stream));
   HIPCHK(c, hipEventRecord(b.ev[1], c->stream));
-  HIPCHK(c, ppls_launch_oz_syrk(b.planes, pstride, Pp, nkb, nmod, b.res, c->stream));
+  HIPCHK(c, ppls_launch_oz_syrk(planes, pstride, Pp, nkb, nmod, res, c->stream));
   HIPCHK(c, hipEventRecord(b.ev[2], c->stream));
-  HIPCHK(c, ppls_launch_oz_finish(b.res, nmod, nsplit, Pp, g.xcols, g.xreal, g.yreal, P, b.shift, G, c->stream));
+  HIPCHK(c, ppls_launch_oz_finish(res, nmod, nsplit, Pp, g.xcols, g.xreal, g.yreal, P, b.shift, G, c->stream));
   HIPCHK(c, hipEventRecord(b.ev[3], c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   float t01 = 0.f, t12 = 0.f, t23 = 0.f, t03 = 0.f;
@@ -1023,6 +1045,7 @@ void xprod_free(ppls_ctx* c) {
   c->xp_active = false;
   dfree(c->xp_S);
   dfree(c->xp_M);
+  oz_free(c);
 }
 
 int compute_ssq(ppls_ctx* c) {
@@ -1254,6 +1277,7 @@ void ppls_ctx_destroy(ppls_ctx* c) {
   dfree(c->stop_d);
   dfree(c->xp_S);
   dfree(c->xp_M);
+  oz_free(c);
   dfree(c->bal_bounds);
   dfree(c->team_bar);
   dfree(c->team_part);
@@ -1366,6 +1390,10 @@ int ppls_set_option(ppls_ctx* c, const char* key, int64_t value) {
       if (c->xp_ready && !c->xp_explicit) {   // a different Gram: S is formed again when next needed
         dfree(c->xp_S);
         c->xp_ready = false;
+      }
+      if (!c->gram_int8) {
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        oz_free(c);
       }
     }
   } else if (!strcmp(key, "xprod_rw")) {
@@ -2758,8 +2786,8 @@ int ppls_variances(ppls_ctx* c, const double* mu, const double* Cdiag, double si
     VCHK(hipMemcpy2DAsync(dG, sizeof(double) * p, c->xp_S + off * P + off, sizeof(double) * P, sizeof(double) * p, p,
                           hipMemcpyDeviceToDevice, c->stream));
   } else {
-    if (n > 0) {
-      VRC(gram_run(c, gram_shape(c, false, xory), n, 0, dG, nullptr));
+    if (n > 0) {   // (option gram_int8: the int8 CRT form, else / on its fallback the fp64 MFMA Gram)
+      VRC(gram_run_s(c, gram_shape(c, false, xory), n, dG, nullptr, nullptr));
     } else {
       VCHK(hipMemsetAsync(dG, 0, sizeof(double) * pp, c->stream));
     }

@@ -246,3 +246,26 @@ def test_int8_gram_sharded_equals_unsharded(k):
         assert np.abs(ll - ref_s[1]).max() / np.abs(ref_s[1]).max() < 1e-11
         if not outlier:   # (a 1e6 entry makes the loadings sensitive to any reordering of the sums)
             assert np.abs(est.W - ref_s[0].W).max() < 1e-9 and np.abs(est.C - ref_s[0].C).max() < 1e-9
+
+
+@pytest.mark.parametrize("xy", ["X", "Y"])
+def test_variances_with_int8_gram(xy):
+    """variances.PPLS_simult (EM_W_multi.R:830-860) with its X'X / Y'Y from the int8 form (option
+    gram_int8, no S formed): equal to the oracle at the same tolerances as the fp64 Gram's test."""
+    import ppls_amd
+    from ppls_amd import Context
+    from oracle import ppls_oracle as o
+    X, Y, th0 = make_problem(1500, 150, 131, 4, seed=67)
+    fit = o.ppls_simult(X, Y, 4, EMsteps=15, atol=-np.inf, theta0=th0)
+    D = X if xy == "X" else Y
+    ref = o.variances_ppls_simult(fit, D, xy)
+    with Context(0) as c:
+        c.set_data(X, Y)
+        c.set_option("gram_int8", 1)
+        got = ppls_amd.variances_PPLS_simult(fit, None, xy, ctx=c)
+        assert c.gram_info()["int8"]
+    rel = lambda a, b: np.abs(a - b).max() / np.abs(b).max()
+    assert np.abs(got["W"] - ref["W"]).max() < 1e-10
+    for i in range(4):
+        assert rel(got["varMatrix"][i], ref["varMatrix"][i]) < 1e-8
+    assert rel(got["seLoad"], ref["seLoad"]) < 1e-8

@@ -32,6 +32,7 @@ def main():
     ap.add_argument("--no-full", action="store_true", help="skip the whole variances call")
     ap.add_argument("--chol", type=int, default=1, help="the arm variances_s reports: 1 Cholesky (default), 2 rocSOLVER Cholesky, 0 LU")
     ap.add_argument("--full-reps", type=int, default=3, help="timed whole calls per arm after one warm-up")
+    ap.add_argument("--gram-int8", type=int, default=0, help="1: X'X by the int8 CRT form (option gram_int8)")
     args = ap.parse_args()
     from ppls_amd import Context
     cfg = CONFIGS[args.config]
@@ -52,6 +53,12 @@ def main():
                gram_exec_tflops=exec_flops / ms / 1e9, gram_useful_tflops=useful / ms / 1e9,
                fp64_mfma_peak_tflops=FP64_PEAK_TF, mfma_frac=exec_flops / ms / 1e9 / FP64_PEAK_TF,
                tiles=tiles)
+    if args.gram_int8:
+        ctx.set_option("gram_int8", 1)
+        ctx.gram_int8(0, want=False)
+        infos = [ctx.gram_int8(0, want=False)[1] for _ in range(args.reps)]
+        out["gram_int8"] = dict(total_ms=[i["ms"][3] for i in infos], syrk_ms=[i["ms"][1] for i in infos],
+                                nmod=infos[0]["nmod"], L=infos[0]["L"])
     if not args.no_full:
         est, ll, eout, _ = ctx.em_run(th0, args.em_steps, -np.inf, 0, want_eout=True, want_mu=True)
         arms = {"chol": 1, "chol_rocsolver": 2, "lu": 0}
