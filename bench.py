@@ -331,7 +331,7 @@ def bench_xprod(ctx, th0, args, barrier, tmax, r, ll_stream, t_stream):
         tops = gi["nmod"] * useful / (syrk_ms * 1e-3) / 1e12 if syrk_ms > 0 else None
         gram_roof = dict(bound="mfma", achieved=tops, peak=INT8_PEAK_TOPS, unit="TOP/s",
                          frac=(tops / INT8_PEAK_TOPS) if tops else None,
-                         kernel="ppls_oz_syrk_kernel<514> (v_mfma_i32_32x32x32_i8), one plane per modulus",
+                         kernel="ppls_oz_syrk_kernel (v_mfma_i32_32x32x32_i8), one plane per modulus",
                          ops_per_launch=gi["nmod"] * useful,
                          ops="useful: nmod n P (P + 1), P = p + q, this rank's rows",
                          fp64_equivalent_tflops=gram_tf, fp64_equivalent_frac_of_fp64_peak=(gram_tf / FP64_PEAK_TF)

@@ -32,9 +32,6 @@ constexpr int OZ_TT = 256;                 // output tile edge
 constexpr int OZ_KS = PPLS_OZ_KS;          // rows per stage (one column's stage: 64 B)
 constexpr int OZ_PANEL = OZ_TT * OZ_KS;    // bytes of one 256-column panel stage (16 KB)
 constexpr int OZ_SPLIT_STAGES = 1024;      // stages per SYRK item: 65,536 rows, |sum| <= 2^30 in int32
-#ifndef OZ_SYRK_VARIANT
-#define OZ_SYRK_VARIANT 514
-#endif
 
 // pairwise coprime moduli, largest first: 2^8, 3*5*17, 11*23, 251, 13*19, then primes and 7*31.  A
 // switch, so an unrolled loop over l sees compile-time moduli (multiply-high forms of % m).
@@ -213,364 +210,134 @@ __global__ __launch_bounds__(256) void ppls_oz_residue_kernel(const T* __restric
 
 // ---------------------------------------------------------------------------- 3. int8 SYRK per modulus
 // One workgroup per (modulus, 65,536-row split, lower 256 x 256 tile); 4 waves of 128 x 128 (4 x 4
-// blocks of v_mfma_i32_32x32x32_i8, 256 int32 accumulators per lane).  The panels of a 64-row stage
-// (16 KB each; one for a diagonal tile) go HBM -> LDS by LDS-DMA (global_load_lds_dwordx4, no VGPR
-// staging) into a ring of 4 buffers, three stages in flight; one barrier per stage, before which
-// every wave waits for its own copies of that stage (vmcnt <= the copies it issued for the two
-// later stages: 2 x 4 on the diagonal, 2 x 8 off it).  The product form (V = 512) issues the copies
-// through inline asm (ppls_dma16s) so the compiler does not track them: tracked, it put vmcnt(0) --
-// the whole prefetch -- in front of the first fragment read of three stages in four (it cannot tell
-// the ring buffers apart across the loop's joins), and DMA and MFMA time added up (10.3 ms per C3
-// plane against 6.0 compute-only and 6.4 copies-only; 7.8 ms untracked, tools/oz_lab.hip).  The
-// copies of stage s + 3 go out during stage s's first k-step, the second k-step's fragments are read
-// during the first's MFMAs.  V = 514 copies both panels for a diagonal tile too (its B panel is its A
-// panel): one code path, 8 % faster than specialising the diagonal (V = 512, 8.5 ms) on this grid.  The 16-B chunks are XOR-swizzled on the source side (LDS chunk q of
-// column c holds global chunk q ^ ((c >> 2) & 3)), so the fragment reads (ds_read_b128) are
-// conflict-free.  Both MFMA operands are read from the same layout, so whatever order the
-// instruction gives the 32 k values of a step, each k meets itself.
+// blocks of v_mfma_i32_32x32x32_i8, 256 int32 accumulators per lane).  The two panels of a 64-row
+// stage (16 KB each; a diagonal tile's B panel is its A panel, copied twice: one code path, 8 % faster
+// on the C3 grid than a diagonal specialised to one panel) go HBM -> LDS by LDS-DMA
+// (global_load_lds_dwordx4, no VGPR staging) into a ring of 4 buffers, three stages in flight; one
+// barrier per stage, before which every wave waits for its own copies of that stage: vmcnt <= the
+// 2 x 8 copies it issued for the two later stages.  The copies go through the product's inline-asm
+// helper (ppls_dma16s), which the compiler does not track: with the compiler's own builtin it put
+// vmcnt(0) -- the whole prefetch -- in front of the first fragment read of three stages in four (it
+// cannot tell the ring's buffers apart across the loop's joins), and DMA and MFMA time added up
+// (10.3 ms per C3 plane against 6.1 compute-only and 6.4 copies-only; 7.8 ms untracked;
+// profiles/r6_int8_syrk_ab.txt, tools/oz_lab.hip).  Hand-counted waits as in the split sweep, checked
+// on the built code object by tools/isa_check.py (tests/test_isa_dma_ring.py).  The stage is
+// branch-free: the tail copies the last stage again into the buffer no one reads, so every wait is the
+// same count.  The copies of stage s + 3 go out one per MFMA group during stage s's first k-step, and
+// the second k-step's fragments are read during the first's MFMAs.  The 16-B chunks are XOR-swizzled
+// on the source side (LDS chunk q of column c holds global chunk q ^ ((c >> 2) & 3)), so the fragment
+// reads (ds_read_b128) are conflict-free.  Both MFMA operands are read from the same layout, so
+// whatever order the instruction gives the 32 k values of a step, each k meets itself.
 // |r| <= 128: a split's 65,536 rows sum to at most 2^30 -- exact in int32, no reduction in the loop
 // (one there made the compiler spill the accumulators).  Output: the split's tile sums mod m, uint8,
-// column-major [col][row].  (Variants other than 512/513 are lab ablations, built under OZ_LAB.)
+// column-major [col][row].
+//   A (lab ablations, tools/oz_lab.hip only; 0 in the product): A & 1 no copies (compute on whatever
+//   the ring holds), A & 2 no fragment reads or MFMAs (the copies alone).
 __device__ __forceinline__ int oz_lds_off(int c, int q) { return c * OZ_KS + ((q ^ ((c >> 2) & 3)) << 4); }
 
 typedef __attribute__((address_space(3))) void* oz_lptr;
 
-template <int V>
-__global__ __launch_bounds__((V & 4) ? 512 : 256, 1) void ppls_oz_syrk_kernel(
-    const int8_t* __restrict__ planes, int64_t pstride, int Pp, int64_t nkb, int nmod, int nsplit, int ntiles,
-    uint8_t* __restrict__ out) {
-  // V & 4: 8 waves (two per SIMD) of 128 x 64, else 4 waves of 128 x 128
-  constexpr int NWV = (V & 4) ? 8 : 4;
-  constexpr int CT = 256 / (NWV / 2);   // output columns per wave
-  constexpr int NJ = CT / 32;           // 32-column MFMA blocks per wave
-  constexpr int NU = 16 / NWV;          // LDS-DMA instructions per wave per panel stage
-  // four ring buffers, each [A panel | B panel] of one stage; separate objects, so the compiler's
-  // own LDS-DMA tracking tells them apart
-  __shared__ __attribute__((aligned(16))) int8_t lb0[((V & 1024) ? 8 : 2) * OZ_PANEL];   // (V & 1024: the whole ring)
-  __shared__ __attribute__((aligned(16))) int8_t lb1[2 * OZ_PANEL];
-  __shared__ __attribute__((aligned(16))) int8_t lb2[2 * OZ_PANEL];
-  __shared__ __attribute__((aligned(16))) int8_t lb3[2 * OZ_PANEL];
+template <int A>
+__global__ __launch_bounds__(256, 1) void ppls_oz_syrk_kernel(const int8_t* __restrict__ planes, int64_t pstride,
+                                                              int Pp, int64_t nkb, int nmod, int nsplit, int ntiles,
+                                                              uint8_t* __restrict__ out) {
+  constexpr int NU = 4;      // LDS-DMA instructions per wave per panel stage (16 KB / 4 waves / 1 KB)
+  constexpr int NC = 2 * NU; // per wave per stage: both panels
+  __shared__ __attribute__((aligned(16))) int8_t ring[4 * 2 * OZ_PANEL];   // 4 x [A panel | B panel]
   const int b = blockIdx.x, nb = gridDim.x;
   const int it = (b & 7) * (nb >> 3) + (b >> 3);   // XCD x (b mod 8) takes a contiguous item range
   if (it >= nmod * nsplit * ntiles) return;
   // item = (modulus, split, tile), tile fastest: concurrent items share the split's row stages
   const int l = it / (nsplit * ntiles), rem = it - l * nsplit * ntiles;
   const int sp = rem / ntiles, t = rem - sp * ntiles;
-  // (lab ablations, tools/oz_lab.hip only: V & 8 every item reads split 0's rows of plane 0 -- the
-  // stream stays cache-resident; V & 16 no copies at all; V & 64 no fragment reads or MFMAs)
-  const int64_t s0 = (V & 8) ? 0 : (int64_t)sp * OZ_SPLIT_STAGES;
+  const int64_t s0 = (int64_t)sp * OZ_SPLIT_STAGES;
   const int64_t s1 = s0 + OZ_SPLIT_STAGES < nkb ? s0 + OZ_SPLIT_STAGES : nkb;
   const int m = oz_mod(l);
   int I, J;
   oz_tile_of(t, &I, &J);
-  const bool diag = I == J;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wi = wave / (NWV / 2), wj = wave % (NWV / 2);
-  const bool idle = diag && wi == 0 && wj * CT >= 128;   // in the diagonal tile's upper-right quadrant
-  const int8_t* pl = planes + ((V & 8) ? 0 : (int64_t)l * pstride);
+  const int wi = wave >> 1, wj = wave & 1;
+  const bool idle = I == J && wi == 0 && wj == 1;   // the diagonal tile's upper-right quadrant
+  const int8_t* pl = planes + (int64_t)l * pstride;
   const int8_t* pa = pl + (int64_t)I * OZ_PANEL;
   const int8_t* pb = pl + (int64_t)J * OZ_PANEL;
   const int64_t sstride = (int64_t)Pp * OZ_KS;
-  v16i acc[4][NJ];
+  v16i acc[4][4];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) acc[i][j] = v16i{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    for (int j = 0; j < 4; ++j) acc[i][j] = v16i{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   // this lane's source offset in a panel stage: wave instruction g = NU wave + u fills LDS bytes
-  // [1024 g, + 1024); lane l the 16 B at 16 l: column 16 g + l / 4, chunk l % 4
+  // [1024 g, + 1024); lane l the 16 B at 16 l: column 16 g + l / 4, chunk l % 4 (swizzled)
   int soff[NU];
 #pragma unroll
   for (int u = 0; u < NU; ++u) {
     const int c = 16 * (NU * wave + u) + (lane >> 2), pos = lane & 3;
     soff[u] = c * OZ_KS + ((pos ^ ((c >> 2) & 3)) << 4);
   }
-  auto issue = [&](int8_t* buf, int64_t s) __attribute__((always_inline)) {
-    if constexpr ((V & 16) != 0) return;
-    const int8_t* ga = pa + s * sstride;
+  const uint32_t lring = (uint32_t)(uintptr_t)(oz_lptr)ring;
+  auto last = [&](int64_t s) { return s < s1 ? s : s1 - 1; };
+  // copy g of this wave's NC for stage s into ring buffer bq
+  auto dma = [&](int bq, int64_t s, int g) __attribute__((always_inline)) {
+    if constexpr ((A & 1) != 0) return;
+    const int8_t* src = (g < NU ? pa : pb) + s * sstride;
+    const int u = g < NU ? g : g - NU;
+    const uint32_t dst = lring + (uint32_t)(bq * 2 * OZ_PANEL + (g < NU ? 0 : OZ_PANEL) + 1024 * (NU * wave + u));
+    ppls_dma16s(src, (uint32_t)soff[u], (uint32_t)__builtin_amdgcn_readfirstlane((int)dst));   // wave-uniform
+  };
+  const int ca0 = 128 * wi + (lane & 31), cb0 = 128 * wj + (lane & 31), h = lane >> 5;
+  // stage s from ring buffer bq; meanwhile the copies of stage s + 3 into buffer (bq + 3) % 4
+  auto stage = [&](int bq, int64_t s) __attribute__((always_inline)) {
+    ppls_wait_vmcnt(2 * NC);   // own copies of stage s landed (s + 1, s + 2 in flight)
+    ppls_lds_barrier();        // everyone's; the buffer of stage s - 1 is free
+    const int64_t sn = last(s + 3);
+    const int nq = (bq + 3) & 3;
+    if constexpr ((A & 2) != 0) {
 #pragma unroll
-    for (int u = 0; u < NU; ++u)
-      __builtin_amdgcn_global_load_lds((const void*)(ga + soff[u]), (oz_lptr)(buf + 1024 * (NU * wave + u)), 16, 0, 0);
-    if (!diag) {
-      const int8_t* gb = pb + s * sstride;
+      for (int g = 0; g < NC; ++g) dma(nq, sn, g);
+      return;
+    }
+    const int8_t* ca = ring + bq * 2 * OZ_PANEL;
+    const int8_t* cbp = ca + OZ_PANEL;
+    v4i a0[4], b0[4], a1[4], b1[4];
 #pragma unroll
-      for (int u = 0; u < NU; ++u)
-        __builtin_amdgcn_global_load_lds((const void*)(gb + soff[u]), (oz_lptr)(buf + OZ_PANEL + 1024 * (NU * wave + u)),
-                                         16, 0, 0);
+    for (int i = 0; i < 4; ++i) a0[i] = *(const v4i*)(ca + oz_lds_off(ca0 + 32 * i, h));
+#pragma unroll
+    for (int j = 0; j < 4; ++j) b0[j] = *(const v4i*)(cbp + oz_lds_off(cb0 + 32 * j, h));
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0[i], b0[j], acc[i][j], 0, 0, 0);
+      dma(nq, sn, i);
+      // the second k-step's fragments, two per group
+      if (i < 2) a1[2 * i] = *(const v4i*)(ca + oz_lds_off(ca0 + 32 * (2 * i), 2 + h)),
+                 a1[2 * i + 1] = *(const v4i*)(ca + oz_lds_off(ca0 + 32 * (2 * i + 1), 2 + h));
+      else b1[2 * (i - 2)] = *(const v4i*)(cbp + oz_lds_off(cb0 + 32 * (2 * (i - 2)), 2 + h)),
+           b1[2 * (i - 2) + 1] = *(const v4i*)(cbp + oz_lds_off(cb0 + 32 * (2 * (i - 2) + 1), 2 + h));
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1[i], b1[j], acc[i][j], 0, 0, 0);
+      dma(nq, sn, 4 + i);
     }
   };
-  // wait until at most `later` stages of this wave's copies are in flight (they retire in order):
-  // NU copies per panel, one panel on the diagonal, two off it
-  auto wait_stages = [&](int64_t later) __attribute__((always_inline)) {
-    if (later >= 2) {
-      if (diag) __builtin_amdgcn_s_waitcnt(OZ_VMCNT(2 * NU));
-      else __builtin_amdgcn_s_waitcnt(OZ_VMCNT(4 * NU));
-    } else if (later == 1) {
-      if (diag) __builtin_amdgcn_s_waitcnt(OZ_VMCNT(NU));
-      else __builtin_amdgcn_s_waitcnt(OZ_VMCNT(2 * NU));
-    } else {
-      __builtin_amdgcn_s_waitcnt(OZ_VMCNT(0));
-    }
-  };
-  const int ca0 = 128 * wi + (lane & 31), cb0 = CT * wj + (lane & 31), h = lane >> 5;
-  auto compute = [&](const int8_t* buf) __attribute__((always_inline)) {
-    if constexpr ((V & 64) != 0) return;   // (lab ablation: the copies alone)
-    const int8_t* la = buf;
-    const int8_t* lbp = diag ? buf : buf + OZ_PANEL;
-    if constexpr ((V & 1) != 0) {   // every fragment of the stage read first (in order), then the MFMAs
-      v4i a[OZ_KS / 32][4], bb[OZ_KS / 32][NJ];
+  // prologue: stages s0 .. s0 + 2 (clamped) into buffers 0 .. 2
 #pragma unroll
-      for (int kb = 0; kb < OZ_KS / 32; ++kb) {
-        const int q = 2 * kb + h;
+  for (int k = 0; k < 3; ++k)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) a[kb][i] = *(const v4i*)(la + oz_lds_off(ca0 + 32 * i, q));
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) bb[kb][j] = *(const v4i*)(lbp + oz_lds_off(cb0 + 32 * j, q));
-      }
-      if constexpr ((V & 2) != 0) __builtin_amdgcn_iglp_opt(1);
-#pragma unroll
-      for (int kb = 0; kb < OZ_KS / 32; ++kb)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < NJ; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[kb][i], bb[kb][j], acc[i][j], 0, 0, 0);
-    } else {
-#pragma unroll
-      for (int kb = 0; kb < OZ_KS / 32; ++kb) {
-        v4i a[4], bb[NJ];
-        const int q = 2 * kb + h;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) a[i] = *(const v4i*)(la + oz_lds_off(ca0 + 32 * i, q));
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) bb[j] = *(const v4i*)(lbp + oz_lds_off(cb0 + 32 * j, q));
-        if constexpr ((V & 2) != 0) __builtin_amdgcn_iglp_opt(1);
-#pragma unroll
-        for (int i = 0; i < 4; ++i)   // (the diagonal tile's idle wave computes too: no branch here)
-#pragma unroll
-          for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[i], bb[j], acc[i][j], 0, 0, 0);
-      }
-    }
-  };
-  // one stage: its copies landed (every wave), then the buffer of the stage before it is free for
-  // the stage three ahead
-  auto step = [&](int8_t* cur, int8_t* nxt3, int64_t s) __attribute__((always_inline)) {
-    wait_stages(s1 - 1 - s < 2 ? s1 - 1 - s : 2);
-    __builtin_amdgcn_s_barrier();
-    if (s + 3 < s1) issue(nxt3, s + 3);
-    compute(cur);
-  };
-  if constexpr ((V & 512) != 0) {
-    // V & 512: the copies through inline asm (ppls_dma16s), invisible to the compiler's wait
-    // insertion, which otherwise puts vmcnt(0) -- every copy in flight, i.e. the whole prefetch --
-    // in front of the first fragment read of most stages (it cannot tell the ring buffers apart
-    // across the loop's joins).  The ring's completion is waited for by hand: vmcnt <= the 2 x 2 NU
-    // copies of the two later stages, then the barrier.  The stage is branch-free as in V & 128 and
-    // the copies spread one per MFMA group.
-    static_assert((V & 4) == 0 && (V & 32) == 0, "asm copies: 4 waves of 128 x 128 only");
-    const uint32_t lds0 = (uint32_t)(uintptr_t)(oz_lptr)lb0, lds1 = (uint32_t)(uintptr_t)(oz_lptr)lb1;
-    const uint32_t lds2 = (uint32_t)(uintptr_t)(oz_lptr)lb2, lds3 = (uint32_t)(uintptr_t)(oz_lptr)lb3;
-    auto last = [&](int64_t s) { return s < s1 ? s : s1 - 1; };
-    auto dma = [&](uint32_t lbuf, int64_t s, int g) __attribute__((always_inline)) {
-      const int8_t* src = (g < NU ? pa : pb) + s * sstride;
-      const int u = g < NU ? g : g - NU;
-      const uint32_t dst = lbuf + (uint32_t)((g < NU ? 0 : OZ_PANEL) + 1024 * (NU * wave + u));
-      ppls_dma16s(src, (uint32_t)soff[u], (uint32_t)__builtin_amdgcn_readfirstlane((int)dst));   // wave-uniform
-    };
-    // a diagonal tile (DG) copies and reads one panel: NU copies per stage, else 2 NU
-    auto run = [&](auto dg) __attribute__((always_inline)) {
-      constexpr bool DG = decltype(dg)::value;
-      constexpr int NC = DG ? NU : 2 * NU;   // copies per wave per stage
-      auto mstep = [&](const int8_t* cur, uint32_t nxt3, int64_t s) __attribute__((always_inline)) {
-        ppls_wait_vmcnt(2 * NC);   // own copies of stage s landed (s + 1, s + 2 in flight)
-        ppls_lds_barrier();        // everyone's; buffer of s - 1 free
-        const int64_t sn = last(s + 3);
-        const int8_t* curb = DG ? cur : cur + OZ_PANEL;
-        if constexpr ((V & 1) != 0) {
-#pragma unroll
-          for (int g = 0; g < NC; ++g) dma(nxt3, sn, g);
-        }
-        v4i a0[4], b0[NJ], a1[4], b1[NJ];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) a0[i] = *(const v4i*)(cur + oz_lds_off(ca0 + 32 * i, h));
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) b0[j] = *(const v4i*)(curb + oz_lds_off(cb0 + 32 * j, h));
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-#pragma unroll
-          for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0[i], b0[j], acc[i][j], 0, 0, 0);
-          if constexpr ((V & 1) == 0) dma(nxt3, sn, i);
-          // the second step's fragments, two per group
-          if (i < 2) a1[2 * i] = *(const v4i*)(cur + oz_lds_off(ca0 + 32 * (2 * i), 2 + h)),
-                     a1[2 * i + 1] = *(const v4i*)(cur + oz_lds_off(ca0 + 32 * (2 * i + 1), 2 + h));
-          else b1[2 * (i - 2)] = *(const v4i*)(curb + oz_lds_off(cb0 + 32 * (2 * (i - 2)), 2 + h)),
-               b1[2 * (i - 2) + 1] = *(const v4i*)(curb + oz_lds_off(cb0 + 32 * (2 * (i - 2) + 1), 2 + h));
-        }
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-#pragma unroll
-          for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1[i], b1[j], acc[i][j], 0, 0, 0);
-          if constexpr ((V & 1) == 0 && !DG) dma(nxt3, sn, 4 + i);
-        }
-      };
-      const uint32_t p1 = (V & 1024) ? lds0 + 2 * OZ_PANEL : lds1, p2 = (V & 1024) ? lds0 + 4 * OZ_PANEL : lds2;
-#pragma unroll
-      for (int g = 0; g < NC; ++g) dma(lds0, last(s0), g);
-#pragma unroll
-      for (int g = 0; g < NC; ++g) dma(p1, last(s0 + 1), g);
-#pragma unroll
-      for (int g = 0; g < NC; ++g) dma(p2, last(s0 + 2), g);
-      if constexpr ((V & 1024) != 0) {
-        // V & 1024: one stage per trip, the ring buffer from the stage index (a quarter of the code)
-#pragma unroll 1
-        for (int64_t s = s0; s < s1; ++s) {
-          const int bq = (int)((s - s0) & 3);
-          mstep(lb0 + bq * 2 * OZ_PANEL, lds0 + (uint32_t)(((bq + 3) & 3) * 2 * OZ_PANEL), s);
-        }
-      } else {
-        for (int64_t s = s0; s < s1; s += 4) {
-          mstep(lb0, lds3, s);
-          if (s + 1 < s1) mstep(lb1, lds0, s + 1);
-          if (s + 2 < s1) mstep(lb2, lds1, s + 2);
-          if (s + 3 < s1) mstep(lb3, lds2, s + 3);
-        }
-      }
-    };
-    if constexpr ((V & 2) != 0) run(std::false_type{});   // (V & 2: a diagonal tile copies both panels too)
-    else if (diag) run(std::true_type{});
-    else run(std::false_type{});
-    ppls_wait_vmcnt(0);   // no copy may land after the workgroup's LDS is gone
-  } else if constexpr ((V & 128) != 0) {
-    // V & 128: the stage-ahead copies spread one per 4 MFMAs through the stage's compute instead of a
-    // burst after the barrier (a burst of LDS-DMA pieces stalls the issuing wave's MFMA stream).
-    // Branch-free stage: both panels always copied (a diagonal tile's B panel is its A panel) and the
-    // tail re-copies the last stage into a buffer no one reads, so every wait is the same count.
-    static_assert((V & 4) == 0 && (V & 32) == 0, "spread copies: 4 waves of 128 x 128 only");
-    auto issue2 = [&](int8_t* buf, int64_t s, int g) __attribute__((always_inline)) {
-      const int8_t* src = (g < NU ? pa : pb) + s * sstride;
-      const int u = g < NU ? g : g - NU;
-      __builtin_amdgcn_global_load_lds((const void*)(src + soff[u]),
-                                       (oz_lptr)(buf + (g < NU ? 0 : OZ_PANEL) + 1024 * (NU * wave + u)), 16, 0, 0);
-    };
-    auto last = [&](int64_t s) { return s < s1 ? s : s1 - 1; };
-    auto sstep = [&](int8_t* cur, int8_t* nxt3, int64_t s) __attribute__((always_inline)) {
-      __builtin_amdgcn_s_waitcnt(OZ_VMCNT(4 * NU));   // own copies of stage s landed (s + 1, s + 2 in flight)
-      __builtin_amdgcn_s_barrier();                    // everyone's; buffer of s - 1 free
-      const int64_t sn = last(s + 3);
-#pragma unroll
-      for (int kb = 0; kb < OZ_KS / 32; ++kb) {
-        v4i a[4], bb[NJ];
-        const int q = 2 * kb + h;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) a[i] = *(const v4i*)(cur + oz_lds_off(ca0 + 32 * i, q));
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) bb[j] = *(const v4i*)(cur + OZ_PANEL + oz_lds_off(cb0 + 32 * j, q));
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-#pragma unroll
-          for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[i], bb[j], acc[i][j], 0, 0, 0);
-          issue2(nxt3, sn, 4 * kb + i);
-        }
-      }
-      if constexpr ((V & 256) != 0) {
-        // V & 256: the second step's fragment reads, two per MFMA group, inside the first step
-        __builtin_amdgcn_sched_group_barrier(0x100, 4 + NJ, 0);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          __builtin_amdgcn_sched_group_barrier(0x008, NJ, 0);
-          __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x100, (4 + NJ) / 4, 0);
-        }
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          __builtin_amdgcn_sched_group_barrier(0x008, NJ, 0);
-          __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
-        }
-      } else {
-#pragma unroll
-        for (int kb = 0; kb < OZ_KS / 32; ++kb) {
-          __builtin_amdgcn_sched_group_barrier(0x100, 4 + NJ, 0);   // the step's fragment reads
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            __builtin_amdgcn_sched_group_barrier(0x008, NJ, 0);     // 4 MFMAs
-            __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);      // then one copy
-          }
-        }
-      }
-    };
-    auto issue_all = [&](int8_t* buf, int64_t s) __attribute__((always_inline)) {
-#pragma unroll
-      for (int g = 0; g < 2 * NU; ++g) issue2(buf, last(s), g);
-    };
-    issue_all(lb0, s0);
-    issue_all(lb1, s0 + 1);
-    issue_all(lb2, s0 + 2);
-    for (int64_t s = s0; s < s1; s += 4) {
-      sstep(lb0, lb3, s);
-      if (s + 1 < s1) sstep(lb1, lb0, s + 1);
-      if (s + 2 < s1) sstep(lb2, lb1, s + 2);
-      if (s + 3 < s1) sstep(lb3, lb2, s + 3);
-    }
-    __builtin_amdgcn_s_waitcnt(OZ_VMCNT(0));   // no copy may land after the workgroup's LDS is gone
-  } else {
-  if (s0 < s1) issue(lb0, s0);
-  if (s0 + 1 < s1) issue(lb1, s0 + 1);
-  if (s0 + 2 < s1) issue(lb2, s0 + 2);
-  if constexpr ((V & 32) == 0) {
-    for (int64_t s = s0; s < s1; s += 4) {
-      step(lb0, lb3, s);
-      if (s + 1 < s1) step(lb1, lb0, s + 1);
-      if (s + 2 < s1) step(lb2, lb1, s + 2);
-      if (s + 3 < s1) step(lb3, lb2, s + 3);
-    }
-  } else {
-    // V & 32: the fragments of stage s + 1 are read while the second half of stage s's MFMAs runs;
-    // the barrier that makes stage s + 1's copies visible sits between the two halves
-    v4i fa[2][2][4], fb[2][2][NJ];   // [register set][kb][block]
-    auto rd = [&](const int8_t* buf, v4i (&xa)[2][4], v4i (&xb)[2][NJ]) __attribute__((always_inline)) {
-      const int8_t* lbp = diag ? buf : buf + OZ_PANEL;
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb) {
-        const int q = 2 * kb + h;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) xa[kb][i] = *(const v4i*)(buf + oz_lds_off(ca0 + 32 * i, q));
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) xb[kb][j] = *(const v4i*)(lbp + oz_lds_off(cb0 + 32 * j, q));
-      }
-    };
-    auto mm = [&](int kb, const v4i (&xa)[2][4], const v4i (&xb)[2][NJ]) __attribute__((always_inline)) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(xa[kb][i], xb[kb][j], acc[i][j], 0, 0, 0);
-    };
-    // stage s in registers set R; its second half overlaps the reads of stage s + 1 into set 1 - R
-    auto pstep = [&](int R, int8_t* nbuf, int8_t* buf3, int64_t s) __attribute__((always_inline)) {
-      mm(0, fa[R], fb[R]);
-      if (s + 1 < s1) {
-        wait_stages(s1 - 1 - (s + 1) < 1 ? s1 - 1 - (s + 1) : 1);   // own copies of s + 1 landed
-        __builtin_amdgcn_s_barrier();                                // everyone's; buffer s - 1 free
-        if (s + 3 < s1) issue(buf3, s + 3);
-        rd(nbuf, fa[1 - R], fb[1 - R]);
-      }
-      mm(1, fa[R], fb[R]);
-    };
-    if (s0 < s1) {
-      wait_stages(s1 - 1 - s0 < 2 ? s1 - 1 - s0 : 2);
-      __builtin_amdgcn_s_barrier();
-      rd(lb0, fa[0], fb[0]);
-    }
-    for (int64_t s = s0; s < s1; s += 4) {
-      pstep(0, lb1, lb3, s);
-      if (s + 1 < s1) pstep(1, lb2, lb0, s + 1);
-      if (s + 2 < s1) pstep(0, lb3, lb1, s + 2);
-      if (s + 3 < s1) pstep(1, lb0, lb2, s + 3);
-    }
+    for (int g = 0; g < NC; ++g) dma(k, last(s0 + k), g);
+  for (int64_t s = s0; s < s1; s += 4) {
+    stage(0, s);
+    if (s + 1 < s1) stage(1, s + 1);
+    if (s + 2 < s1) stage(2, s + 2);
+    if (s + 3 < s1) stage(3, s + 3);
   }
-  }
+  ppls_wait_vmcnt(0);   // no copy may land after the workgroup's LDS is gone
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < NJ; ++j)
+    for (int j = 0; j < 4; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int v = acc[i][j][r] % m;
@@ -581,8 +348,8 @@ __global__ __launch_bounds__((V & 4) ? 512 : 256, 1) void ppls_oz_syrk_kernel(
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      const int col = CT * wj + 32 * j + (lane & 31);
+    for (int j = 0; j < 4; ++j) {
+      const int col = 128 * wj + 32 * j + (lane & 31);
 #pragma unroll
       for (int gq = 0; gq < 4; ++gq) {   // 32 x 32 D map: rows (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
         const int row = 128 * wi + 32 * i + 8 * gq + 4 * h;
@@ -790,18 +557,15 @@ hipError_t ppls_launch_oz_syrk_v(int variant, const int8_t* planes, int64_t pstr
   const int64_t items = (int64_t)nmod * nsplit * ntiles;
   const int64_t grid = (items + 7) / 8 * 8;
   if (grid > 0x7fffffff) return hipErrorInvalidValue;
-#define OZ_SYRK(VV)                                                                                             \
-  case VV:                                                                                                      \
-    hipLaunchKernelGGL(ppls_oz_syrk_kernel<VV>, dim3((unsigned)grid), dim3(((VV) & 4) ? 512 : 256), 0, st, planes, \
-                       pstride, Pp, nkb, nmod, nsplit, ntiles, part);                                           \
+#define OZ_SYRK(AV)                                                                                             \
+  case AV:                                                                                                      \
+    hipLaunchKernelGGL(ppls_oz_syrk_kernel<AV>, dim3((unsigned)grid), dim3(256), 0, st, planes, pstride, Pp, nkb, \
+                       nmod, nsplit, ntiles, part);                                                             \
     break;
   switch (variant) {
-    OZ_SYRK(514)
+    OZ_SYRK(0)
 #ifdef OZ_LAB
-    OZ_SYRK(512) OZ_SYRK(513) OZ_SYRK(1538) OZ_SYRK(1536)
-    OZ_SYRK(0) OZ_SYRK(1) OZ_SYRK(2) OZ_SYRK(3) OZ_SYRK(4) OZ_SYRK(5) OZ_SYRK(6) OZ_SYRK(7)
-    OZ_SYRK(8) OZ_SYRK(12) OZ_SYRK(16) OZ_SYRK(20) OZ_SYRK(64) OZ_SYRK(72) OZ_SYRK(32) OZ_SYRK(36) OZ_SYRK(40)
-    OZ_SYRK(48) OZ_SYRK(128) OZ_SYRK(384)
+    OZ_SYRK(1) OZ_SYRK(2)
 #endif
     default: return hipErrorInvalidValue;
   }
@@ -811,7 +575,7 @@ hipError_t ppls_launch_oz_syrk_v(int variant, const int8_t* planes, int64_t pstr
 
 hipError_t ppls_launch_oz_syrk(const int8_t* planes, int64_t pstride, int Pp, int64_t nkb, int nmod, uint8_t* part,
                                hipStream_t st) {
-  return ppls_launch_oz_syrk_v(OZ_SYRK_VARIANT, planes, pstride, Pp, nkb, nmod, part, st);
+  return ppls_launch_oz_syrk_v(0, planes, pstride, Pp, nkb, nmod, part, st);
 }
 
 hipError_t ppls_launch_oz_finish(const uint8_t* part, int nmod, int nsplit, int Pp, int xcols, int xreal, int yreal,

@@ -11,7 +11,7 @@ states why that is safe and what must hold, and these tests check it mechanicall
     workgroup can get (0 .. 80, and large ones), both mu modes: no row read before its copies
     landed, no slot refilled before its row was read; a count one row too large is caught;
   * the sources: no other inline asm issues a memory load;
-  * the int8 Gram's SYRK ring (ppls_ozaki.hip, V = 512/513; the same asm copies): hand wait before
+  * the int8 Gram's SYRK ring (ppls_ozaki.hip; the same asm copies): hand wait before
     every barrier, only vmcnt(0 | 2 NC), a drain after the last copy, and its ring restated and
     simulated for every stage count of a split (1 .. 1024) with a negative control.
 """
@@ -38,9 +38,9 @@ def kernels():
 
 def test_only_split_sweep_and_syrk_kernels_use_lds_dma(kernels):
     assert kernels, "no LDS-DMA kernel found: the split sweep should use it"
-    other = [n for n in kernels if not ic.split_params(n) and not (ic.oz_variant(n) or 0) & 512]
+    other = [n for n in kernels if not ic.split_params(n) and ic.oz_variant(n) is None]
     assert not other, other
-    assert any(ic.split_params(n) for n in kernels) and any(ic.oz_variant(n) for n in kernels)
+    assert any(ic.split_params(n) for n in kernels) and any(ic.oz_variant(n) is not None for n in kernels)
 
 
 def test_built_split_kernels_dma_form_and_runs(kernels):
@@ -92,7 +92,7 @@ def test_no_other_inline_asm_loads():
 
 
 def test_built_syrk_ring_waits(kernels):
-    oz = {n: ins for n, ins in kernels.items() if (ic.oz_variant(n) or 0) & 512}
+    oz = {n: ins for n, ins in kernels.items() if ic.oz_variant(n) is not None}
     assert oz
     bad = {n[:60]: ic.check_oz_kernel(ins)[:5] for n, ins in oz.items() if ic.check_oz_kernel(ins)}
     assert not bad, bad

@@ -17,7 +17,7 @@ only make a wait stricter).  That argument holds only if
   (2) each row issue is exactly CPW copies in straight-line code (the count k is in units of CPW
       copies per row): the DMA ops form unbranched runs of exactly CPW;
   (3) no kernel other than the split sweep and the int8 Gram's SYRK (ppls_ozaki.hip:
-      ppls_oz_syrk_kernel, variants 512..514) issues LDS-DMA (no experiment code in the product);
+      ppls_oz_syrk_kernel) issues LDS-DMA (no experiment code in the product);
   (4) the k the kernel computes is right: the ring schedule of ppls_kernels.hip:496-541, restated in
       ring_schedule() below, is simulated for every instantiation and every row count of a workgroup
       (in-order retirement, CPW copies per row per DMA wave), checking that every row a workgroup
@@ -323,7 +323,7 @@ def main():
         pr = split_params(name)
         if pr:
             probs = check_kernel(ins, pr[6])
-        elif (oz_variant(name) or 0) & 512:
+        elif oz_variant(name) is not None:
             probs = check_oz_kernel(ins)
         else:
             probs = [f"LDS-DMA in a kernel that is not the split sweep or the SYRK: {name}"]

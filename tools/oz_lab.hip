@@ -3,11 +3,13 @@
 // exact int64 sums on the host.  Not part of the product.
 //
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -Iinclude -Ippls_amd/csrc -o tools/oz_lab tools/oz_lab.hip
-//   tools/oz_lab <n> <P> <planes> [check]
+//   tools/oz_lab <n> <P> <planes> [check] [variant]
 //
 // Random int8 residues in the product's plane layout [n / 64][Pp][64]; `planes` moduli go through ONE
-// launch of the product SYRK (ppls_ozaki.hip: ppls_launch_oz_syrk), and sampled entries are checked
-// against exact int64 sums mod m on the host.
+// launch of the product SYRK (ppls_ozaki.hip: ppls_launch_oz_syrk_v; variant 0 the product, 1 no
+// copies, 2 the copies alone), and sampled entries are checked against exact int64 sums mod m on
+// the host.  (The round-6 variants of profiles/r6_int8_syrk_ab.txt were built in this lab at
+// commits 4a40cc5 .. aac738c and removed from the product source afterwards.)
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -71,7 +73,7 @@ int main(int argc, char** argv) {
   const size_t obytes = (size_t)ntiles * nsplit * TT * TT;   // per modulus
   CHK(hipMalloc(&dout, obytes * planes));
   const int variant = argc > 5 ? atoi(argv[5]) : -1;   // -1: every variant
-  for (int v : {514, 1538, 1536, 514, 1538}) {
+  for (int v : {0, 1, 2, 0}) {
     if (variant >= 0 && v != variant) continue;
     for (int w = 0; w < 2; ++w) CHK(ppls_launch_oz_syrk_v(v, dp, (int64_t)pbytes, Pp, nkb, planes, dout, 0));
     CHK(hipDeviceSynchronize());
