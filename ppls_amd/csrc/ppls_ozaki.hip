@@ -232,17 +232,22 @@ __global__ __launch_bounds__(256) void ppls_oz_residue_kernel(const T* __restric
 // (one there made the compiler spill the accumulators).  Output: the split's tile sums mod m, uint8,
 // column-major [col][row].
 //   A (lab ablations, tools/oz_lab.hip only; 0 in the product): A & 1 no copies (compute on whatever
-//   the ring holds), A & 2 no fragment reads or MFMAs (the copies alone).
+//   the ring holds), A & 2 no fragment reads or MFMAs (the copies alone), A & 4 eight waves of
+//   128 x 64 (two per SIMD: one can issue MFMAs while the other stalls on a copy) -- 7.30-7.40 vs
+//   7.36 ms per C3 plane, no gain (profiles/r6_int8_syrk_ab.txt).
 __device__ __forceinline__ int oz_lds_off(int c, int q) { return c * OZ_KS + ((q ^ ((c >> 2) & 3)) << 4); }
 
 typedef __attribute__((address_space(3))) void* oz_lptr;
 
 template <int A>
-__global__ __launch_bounds__(256, 1) void ppls_oz_syrk_kernel(const int8_t* __restrict__ planes, int64_t pstride,
-                                                              int Pp, int64_t nkb, int nmod, int nsplit, int ntiles,
-                                                              uint8_t* __restrict__ out) {
-  constexpr int NU = 4;      // LDS-DMA instructions per wave per panel stage (16 KB / 4 waves / 1 KB)
-  constexpr int NC = 2 * NU; // per wave per stage: both panels
+__global__ __launch_bounds__((A & 4) ? 512 : 256, 1) void ppls_oz_syrk_kernel(
+    const int8_t* __restrict__ planes, int64_t pstride, int Pp, int64_t nkb, int nmod, int nsplit, int ntiles,
+    uint8_t* __restrict__ out) {
+  constexpr int NWV = (A & 4) ? 8 : 4;   // (lab: A & 4, 8 waves of 128 x 64, two per SIMD)
+  constexpr int CT = 256 / (NWV / 2);    // output columns per wave
+  constexpr int NJ = CT / 32;            // 32-column MFMA blocks per wave
+  constexpr int NU = 16 / NWV;           // LDS-DMA instructions per wave per panel stage (16 KB / 1 KB)
+  constexpr int NC = 2 * NU;             // per wave per stage: both panels
   __shared__ __attribute__((aligned(16))) int8_t ring[4 * 2 * OZ_PANEL];   // 4 x [A panel | B panel]
   const int b = blockIdx.x, nb = gridDim.x;
   const int it = (b & 7) * (nb >> 3) + (b >> 3);   // XCD x (b mod 8) takes a contiguous item range
@@ -256,17 +261,17 @@ __global__ __launch_bounds__(256, 1) void ppls_oz_syrk_kernel(const int8_t* __re
   int I, J;
   oz_tile_of(t, &I, &J);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wi = wave >> 1, wj = wave & 1;
-  const bool idle = I == J && wi == 0 && wj == 1;   // the diagonal tile's upper-right quadrant
+  const int wi = wave / (NWV / 2), wj = wave % (NWV / 2);
+  const bool idle = I == J && wi == 0 && wj * CT >= 128;   // the diagonal tile's upper-right quadrant
   const int8_t* pl = planes + (int64_t)l * pstride;
   const int8_t* pa = pl + (int64_t)I * OZ_PANEL;
   const int8_t* pb = pl + (int64_t)J * OZ_PANEL;
   const int64_t sstride = (int64_t)Pp * OZ_KS;
-  v16i acc[4][4];
+  v16i acc[4][NJ];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = v16i{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    for (int j = 0; j < NJ; ++j) acc[i][j] = v16i{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   // this lane's source offset in a panel stage: wave instruction g = NU wave + u fills LDS bytes
   // [1024 g, + 1024); lane l the 16 B at 16 l: column 16 g + l / 4, chunk l % 4 (swizzled)
   int soff[NU];
@@ -285,7 +290,7 @@ __global__ __launch_bounds__(256, 1) void ppls_oz_syrk_kernel(const int8_t* __re
     const uint32_t dst = lring + (uint32_t)(bq * 2 * OZ_PANEL + (g < NU ? 0 : OZ_PANEL) + 1024 * (NU * wave + u));
     ppls_dma16s(src, (uint32_t)soff[u], (uint32_t)__builtin_amdgcn_readfirstlane((int)dst));   // wave-uniform
   };
-  const int ca0 = 128 * wi + (lane & 31), cb0 = 128 * wj + (lane & 31), h = lane >> 5;
+  const int ca0 = 128 * wi + (lane & 31), cb0 = CT * wj + (lane & 31), h = lane >> 5;
   // stage s from ring buffer bq; meanwhile the copies of stage s + 3 into buffer (bq + 3) % 4
   auto stage = [&](int bq, int64_t s) __attribute__((always_inline)) {
     ppls_wait_vmcnt(2 * NC);   // own copies of stage s landed (s + 1, s + 2 in flight)
@@ -299,27 +304,25 @@ __global__ __launch_bounds__(256, 1) void ppls_oz_syrk_kernel(const int8_t* __re
     }
     const int8_t* ca = ring + bq * 2 * OZ_PANEL;
     const int8_t* cbp = ca + OZ_PANEL;
-    v4i a0[4], b0[4], a1[4], b1[4];
+    v4i a0[4], b0[NJ], a1[4], b1[NJ];
 #pragma unroll
     for (int i = 0; i < 4; ++i) a0[i] = *(const v4i*)(ca + oz_lds_off(ca0 + 32 * i, h));
 #pragma unroll
-    for (int j = 0; j < 4; ++j) b0[j] = *(const v4i*)(cbp + oz_lds_off(cb0 + 32 * j, h));
+    for (int j = 0; j < NJ; ++j) b0[j] = *(const v4i*)(cbp + oz_lds_off(cb0 + 32 * j, h));
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0[i], b0[j], acc[i][j], 0, 0, 0);
-      dma(nq, sn, i);
-      // the second k-step's fragments, two per group
-      if (i < 2) a1[2 * i] = *(const v4i*)(ca + oz_lds_off(ca0 + 32 * (2 * i), 2 + h)),
-                 a1[2 * i + 1] = *(const v4i*)(ca + oz_lds_off(ca0 + 32 * (2 * i + 1), 2 + h));
-      else b1[2 * (i - 2)] = *(const v4i*)(cbp + oz_lds_off(cb0 + 32 * (2 * (i - 2)), 2 + h)),
-           b1[2 * (i - 2) + 1] = *(const v4i*)(cbp + oz_lds_off(cb0 + 32 * (2 * (i - 2) + 1), 2 + h));
+      for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a0[i], b0[j], acc[i][j], 0, 0, 0);
+      if (i < NC) dma(nq, sn, i);
+      // the second k-step's fragments, spread over the groups
+      a1[i] = *(const v4i*)(ca + oz_lds_off(ca0 + 32 * i, 2 + h));
+      if (i < NJ) b1[i] = *(const v4i*)(cbp + oz_lds_off(cb0 + 32 * i, 2 + h));
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1[i], b1[j], acc[i][j], 0, 0, 0);
-      dma(nq, sn, 4 + i);
+      for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a1[i], b1[j], acc[i][j], 0, 0, 0);
+      if (4 + i < NC) dma(nq, sn, 4 + i);
     }
   };
   // prologue: stages s0 .. s0 + 2 (clamped) into buffers 0 .. 2
@@ -337,7 +340,7 @@ __global__ __launch_bounds__(256, 1) void ppls_oz_syrk_kernel(const int8_t* __re
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+    for (int j = 0; j < NJ; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int v = acc[i][j][r] % m;
@@ -348,8 +351,8 @@ __global__ __launch_bounds__(256, 1) void ppls_oz_syrk_kernel(const int8_t* __re
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int col = 128 * wj + 32 * j + (lane & 31);
+    for (int j = 0; j < NJ; ++j) {
+      const int col = CT * wj + 32 * j + (lane & 31);
 #pragma unroll
       for (int gq = 0; gq < 4; ++gq) {   // 32 x 32 D map: rows (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
         const int row = 128 * wi + 32 * i + 8 * gq + 4 * h;
@@ -559,13 +562,13 @@ hipError_t ppls_launch_oz_syrk_v(int variant, const int8_t* planes, int64_t pstr
   if (grid > 0x7fffffff) return hipErrorInvalidValue;
 #define OZ_SYRK(AV)                                                                                             \
   case AV:                                                                                                      \
-    hipLaunchKernelGGL(ppls_oz_syrk_kernel<AV>, dim3((unsigned)grid), dim3(256), 0, st, planes, pstride, Pp, nkb, \
-                       nmod, nsplit, ntiles, part);                                                             \
+    hipLaunchKernelGGL(ppls_oz_syrk_kernel<AV>, dim3((unsigned)grid), dim3(((AV) & 4) ? 512 : 256), 0, st, planes, \
+                       pstride, Pp, nkb, nmod, nsplit, ntiles, part);                                           \
     break;
   switch (variant) {
     OZ_SYRK(0)
 #ifdef OZ_LAB
-    OZ_SYRK(1) OZ_SYRK(2)
+    OZ_SYRK(1) OZ_SYRK(2) OZ_SYRK(4) OZ_SYRK(5) OZ_SYRK(6)
 #endif
     default: return hipErrorInvalidValue;
   }

@@ -73,7 +73,7 @@ int main(int argc, char** argv) {
   const size_t obytes = (size_t)ntiles * nsplit * TT * TT;   // per modulus
   CHK(hipMalloc(&dout, obytes * planes));
   const int variant = argc > 5 ? atoi(argv[5]) : -1;   // -1: every variant
-  for (int v : {0, 1, 2, 0}) {
+  for (int v : {0, 4, 5, 6, 0, 4}) {
     if (variant >= 0 && v != variant) continue;
     for (int w = 0; w < 2; ++w) CHK(ppls_launch_oz_syrk_v(v, dp, (int64_t)pbytes, Pp, nkb, planes, dout, 0));
     CHK(hipDeviceSynchronize());
