@@ -162,11 +162,12 @@ __global__ void ppls_oz_colstats_finish_kernel(const double* __restrict__ part, 
 // 24-bit multiply-adds (operands < 2^24) and ONE 32-bit reduction of a value < 2^31 -- then minus
 // 2^62 mod m (folded into the sum as m - (2^62 mod m)), symmetric.  (The residue arithmetic, not the
 // 106 GB of C3 traffic, bounded the first form's three 32-bit reductions per residue: 41 ms.)
+// biash = m - (2^62 mod m) + floor(m / 2): then (t mod m) - floor(m / 2) is the symmetric residue
+// (in [-(m-1)/2, (m-1)/2] for odd m, [-128, 127] for 256) without a compare and select.
 __host__ __device__ __forceinline__ int oz_residue21(uint32_t a, uint32_t b, uint32_t c, uint32_t m, uint32_t k42,
-                                                     uint32_t k21, uint32_t bias) {
-  const uint32_t t = a * k42 + b * k21 + c + bias;   // < 2^21 255 2 + 2^21 + 256 < 2^31
-  const uint32_t r = t % m;                           // x' mod m in [0, m)
-  return (int)r > (int)(m / 2) ? (int)r - (int)m : (int)r;
+                                                     uint32_t k21, uint32_t biash) {
+  const uint32_t t = a * k42 + b * k21 + c + biash;   // < 2^21 255 2 + 2^21 + 384 < 2^31
+  return (int)(t % m) - (int)(m / 2);
 }
 
 template <typename T, int NMOD>
@@ -199,7 +200,7 @@ __global__ __launch_bounds__(256) void ppls_oz_residue_kernel(const T* __restric
   for (int l = 0; l < NMOD; ++l) {
     const uint32_t m = (uint32_t)oz_mod(l);
     const uint32_t k42 = (uint32_t)((1ull << 42) % m), k21 = (uint32_t)((1ull << 21) % m);
-    const uint32_t bias = m - (uint32_t)((1ull << 62) % m);
+    const uint32_t bias = m - (uint32_t)((1ull << 62) % m) + m / 2;
     uint32_t w[4] = {0, 0, 0, 0};
 #pragma unroll
     for (int k = 0; k < 16; ++k)
@@ -490,7 +491,7 @@ int ppls_oz_residue_host(double x, int shift, int l, int* r) {
   const uint64_t u = (uint64_t)((int64_t)xs + (int64_t)(1ull << 62));
   const uint32_t m = (uint32_t)oz_mod(l);
   *r = oz_residue21((uint32_t)(u >> 42), (uint32_t)(u >> 21) & 0x1FFFFFu, (uint32_t)u & 0x1FFFFFu, m,
-                    (uint32_t)((1ull << 42) % m), (uint32_t)((1ull << 21) % m), m - (uint32_t)((1ull << 62) % m));
+                    (uint32_t)((1ull << 42) % m), (uint32_t)((1ull << 21) % m), m - (uint32_t)((1ull << 62) % m) + m / 2);
   return 0;
 }
 
