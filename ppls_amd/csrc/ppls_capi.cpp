@@ -803,7 +803,9 @@ int gram_run_oz(ppls_ctx* c, const GramShape& g, int64_t n, double* G, float* ms
     const double q = std::ldexp(std::sqrt(st[(size_t)Pp + j]), L - e[(size_t)j]) + 0.5 * std::sqrt((double)n);
     qmax = std::max(qmax, q * q);
   }
-  const double need = std::log2(std::max(qmax, 1.0)) + 2.0;   // bits of M > 2 max |sum| (+1 margin)
+  // M > 2 max |sum| (the CRT's range (-M/2, M/2)); qmax is an upper bound up to the rounding of the
+  // device's sum of squares (relative <= n u ~ 1e-10 at 1e6 rows), covered by the 1e-7 bit
+  const double need = std::log2(std::max(qmax, 1.0)) + 1.0 + 1e-7;
   double bits = 0.0;
   int nmod = 0;
   while (nmod < PPLS_OZ_MAXMOD && bits < need) bits += std::log2((double)ppls_oz_modulus(nmod++));
