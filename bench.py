@@ -251,6 +251,16 @@ def cpu_baseline(ctx, th0, cfg, iters=3, one_core_rows=100_000):
                          sample=f"the same {iters} iterations on {env_threads} OpenMP threads (the inherited "
                                 f"OMP_NUM_THREADS / runtime default) in {dt_env:.1f} s",
                          loglik_equal_to_all_core_run=bool(np.array_equal(ll_env, ll_all)))
+    # the whole affinity mask as OpenMP threads, when the cgroup quota caps the
+    # usable CPUs below it: reported beside the value, which stays the faster, quota-sized run
+    affinity = None
+    aff = affinity_cores()
+    if aff != cores:
+        _, ll_aff, dt_aff, _ = timed(aff)
+        affinity = dict(value=iters / dt_aff, unit="EM iterations/s", cores=int(aff),
+                        sample=f"the same {iters} iterations on {aff} OpenMP threads (every CPU of the affinity "
+                               f"mask) in {dt_aff:.1f} s, time-sliced onto the cgroup's quota",
+                        loglik_equal_to_value_run=bool(np.array_equal(ll_aff, ll_all)))
     # 1 core on the first rows (bounded time), per-row rate scaled to the full n
     ns = int(min(one_core_rows, X.shape[0]))
     Xs, Ys = X[:ns], Y[:ns]
@@ -271,7 +281,7 @@ def cpu_baseline(ctx, th0, cfg, iters=3, one_core_rows=100_000):
                 sample=f"{iters} steady-state EM iterations (after 1 untimed, {t_first:.1f} s) on all n={n} rows "
                        f"in {dt:.1f} s: oracle/cpu_ref.c (reference pass structure), OpenMP {cores} threads "
                        f"(the affinity mask capped by the cgroup CPU quota), -O3 -march=native, {cpu_model()}",
-                inherited_threads=inherited,
+                inherited_threads=inherited, affinity_threads=affinity,
                 one_core=dict(value=one_core, unit="EM iterations/s", cores=1,
                               sample=f"{iters} EM iterations on the first {ns} rows in {dt1:.1f} s, 1 thread; "
                                      f"value = rows*iterations/s / n")), rel, werr
