@@ -60,6 +60,7 @@ def main():
     ap.add_argument("--name", required=True)
     ap.add_argument("--bench-json", default=None)
     ap.add_argument("--command", default=None)
+    ap.add_argument("--out-dir", default=os.path.join(ROOT, "profiles"), help="where the summaries go")
     ap.add_argument("--group", type=int, default=1,
                     help="consecutive matching launches of a phase that form one unit (their durations summed): "
                          "2 for the panel sweep's dots + accumulation per iteration (--kernel panel_)")
@@ -103,7 +104,11 @@ def main():
     t = phases["timed"]
     t["achieved_GBs"] = a.bytes / (t["avg_ms"] * 1e-3) / 1e9
     t["frac"] = t["achieved_GBs"] * 1e9 / HBM_PEAK
-    from pmc_summary import profiled_tree
+    try:
+        from pmc_summary import profiled_tree
+    except ImportError:   # (the summary's provenance helper; absent in a bare checkout of the tool)
+        def profiled_tree():
+            return os.environ.get("PPLS_PROFILED_TREE")
     out = dict(kernel=a.kernel, launches_per_unit=a.group, algorithmic_bytes_per_launch=a.bytes, hbm_peak_GBs=HBM_PEAK / 1e9,
                command=a.command, profiled_tree=profiled_tree(), phases=phases,
                ordinals={ph: v for ph, v in ords.items()}, kernel_dispatches_total=ordinal,
@@ -119,10 +124,10 @@ def main():
             timed_avg_le_ms_per_step=t["avg_ms"] <= b["ms_per_step"],
             frac_trace_over_line=t["frac"] / b["roofline"]["frac"],
             timed_launches_eq_steps=t["launches"] == b["steps"])
-    path = os.path.join(ROOT, "profiles", a.name + ".json")
+    path = os.path.join(a.out_dir, a.name + ".json")
     with open(path, "w") as f:
         json.dump(out, f, indent=1)
-    with open(os.path.join(ROOT, "profiles", a.name + "_kernel_stats.csv"), "w", newline="") as f:
+    with open(os.path.join(a.out_dir, a.name + "_kernel_stats.csv"), "w", newline="") as f:
         w = csv.writer(f, quoting=csv.QUOTE_NONNUMERIC)
         w.writerow(["Name", "Calls", "TotalDurationNs", "AverageNs", "MinNs", "MaxNs", "Phase"])
         for k, v in sorted(timed_all.items(), key=lambda kv: -sum(kv[1])):
