@@ -111,3 +111,18 @@ def test_syrk_ring_schedule_and_negative_control():
                                      (20, "s_waitcnt", "vmcnt(0)", None)]) == []
     assert ic.check_oz_kernel(dma + [(16, "s_barrier", "", None), (20, "s_waitcnt", "vmcnt(0)", None)])
     assert ic.check_oz_kernel(dma + [(12, "s_waitcnt", "vmcnt(16)", None), (16, "s_barrier", "", None)])
+
+
+def test_steady_state_wait_is_compiled(kernels):
+    """The steady-state wait of the restated ring, vmcnt(AHEAD RP CPW) with AHEAD = SLOTS / RP - 2
+    (ppls_kernels.hip:510-512), is an instruction of every built split-sweep instantiation that needs
+    one (a count the compiler never sees could otherwise be dropped or merged unnoticed)."""
+    import re
+    for n, ins in kernels.items():
+        p = ic.split_params(n)
+        if not p:
+            continue
+        _, _, _, RP, _, SLOTS, CPW = p
+        k = (SLOTS // RP - 2) * RP * CPW
+        waits = {int(m) for (_, mn, ops, _) in ins if mn == "s_waitcnt" for m in re.findall(r"vmcnt\((\d+)\)", ops)}
+        assert k in waits, (n[:70], k, sorted(waits))
