@@ -319,3 +319,31 @@ def test_int8_gram_fuzz(case):
             if n <= 3000:
                 k = D.shape[1]
                 _check_integer_pipeline(D, G, info["L"], [(int(rng.integers(k)), int(rng.integers(k))) for _ in range(8)])
+
+
+@pytest.mark.parametrize("config", ["c3", "c5"])
+def test_int8_gram_full_size_fit_equals_streaming(config):
+    """The bench configs at full size with S from the int8 Gram (C3: 1e6 x 4000 fp64, 18 moduli; C5:
+    5e5 x 10,500 fp32-stored, 17 moduli): the cross-product EM iterations equal the streaming ones at
+    tests/test_gpu_xprod_full.py's tolerances (loglik 1e-12 relative, loadings 1e-10)."""
+    import bench
+    from ppls_amd import Context, Theta
+    cfg = bench.CONFIGS[config]
+    n, p, q, r = cfg["n"], cfg["p"], cfg["q"], cfg["r"]
+    truth, th0 = bench.make_truth_and_theta0(p, q, r)
+    th = Theta(th0["W"], th0["C"], th0["B"], th0["sigE"], th0["sigF"], th0["sigH"], th0["sigT"]) \
+        if isinstance(th0, dict) else th0
+    steps = 3
+    with Context(0) as c:
+        if cfg.get("storage") == "f32":
+            c.set_option("dtype", 1)
+        c.generate_synthetic(n, p, q, truth, seed=20261015)
+        c.set_option("xprod", 0)
+        est_s, ll_s, _, _ = c.em_run(th, steps, -np.inf, 0, want_eout=False)
+        c.set_option("xprod", 1)
+        c.set_option("gram_int8", 1)
+        est_x, ll_x, _, _ = c.em_run(th, steps, -np.inf, 0, want_eout=False)
+        gi = c.gram_info()
+        assert gi["int8"] and 12 <= gi["nmod"] <= 20, gi
+    assert np.abs(ll_x - ll_s).max() / np.abs(ll_s).max() < 1e-12
+    assert np.abs(est_x.W - est_s.W).max() < 1e-10 and np.abs(est_x.C - est_s.C).max() < 1e-10
