@@ -109,8 +109,10 @@ const char* ppls_last_error(const ppls_ctx* ctx);
  *                      population); 0 the per-population loop driven by the host),
  *       "gram_int8" (the Gram that forms S and ppls_variances' X'X: 0, default, fp64 MFMA; 1 the
  *                    int8-MFMA Chinese-remainder form when the columns' spread allows it -- else the
- *                    fp64 one; ppls_gram_info.  Its residue planes (18 x n x (p + q) bytes at C3's
- *                    spread) stay allocated until ppls_xprod_release, new data or gram_int8 = 0),
+ *                    fp64 one; ppls_gram_info.  Its residue planes (17 x n x (p + q) bytes at C3's
+ *                    spread) are a workspace kept between formations -- also across
+ *                    ppls_xprod_release and new data -- until gram_int8 = 0 or ppls_ctx_destroy; a
+ *                    device allocation of the library that fails frees them and tries again),
  *       "vorth" (the finalize re-orthonormalises the Jacobi warm start it carries between
  *                iterations every vorth-th iteration: 1 .. 255, default 8),
  *       "xprod_rw" (rows of S per wave of the cross-product tile kernel: 0 auto, 1, 2, 4, 8),
@@ -274,7 +276,8 @@ int ppls_variances(ppls_ctx* ctx, const double* mu, const double* Cdiag, double 
  * allocation; both nullable) -- otherwise the first run that reads S forms it.  Collective when the
  * rows are sharded: every rank calls it (one all-reduce of (p+q)^2 doubles). */
 int ppls_xprod_prepare(ppls_ctx* ctx, double* ms, double* total_ms);
-/* Free S (and its scratch) now; the next run that reads S forms it again. */
+/* Free S (and its scratch) now; the next run that reads S forms it again.  (The int8 Gram's
+ * residue planes stay: see option "gram_int8".) */
 int ppls_xprod_release(ppls_ctx* ctx);
 
 /* ---- host-side algebra (no GPU; the same code the device finalize runs) ------------------------ */

@@ -47,9 +47,12 @@ int ppls_sweep_info(ppls_ctx* ctx, int r, int64_t* bytes_per_sweep, int* variant
 int ppls_sweep_kernel(ppls_ctx* ctx, int r, char* buf, int len);
 /* The Gram by the int8-MFMA Chinese-remainder form (ppls_ozaki.hip) alone, for tests and
  * benchmarks: which = 0 X'X, 1 Y'Y, 2 the joint [X Y]'[X Y] (P = ldx + ldy, padding columns 0);
- * G (column-major, nullable); *nmod moduli, *L bits per integer; ms[4] = stats + residues, SYRK,
- * CRT, total (HIP events).  PPLS_E_NUMERIC when the columns' spread is too wide for it. */
+ * G (column-major, nullable); *nmod moduli, *L bits of the widest column's integers; ms[4] = stats +
+ * residues, SYRK, CRT, total (HIP events).  PPLS_E_NUMERIC when the columns' spread is too wide. */
 int ppls_gram_int8(ppls_ctx* ctx, int which, double* G, int* nmod, int* L, double* ms);
+/* The per-column scalings of the last int8 Gram (x'_kj = rint(D_kj 2^shift[j]); 0 for empty and
+ * padding columns): the first min(P, *count) of them, *count = its column count. */
+int ppls_gram_shifts(ppls_ctx* ctx, int* shift, int P, int* count);
 /* Host copies of the int8 Gram's arithmetic (no GPU needed; tests/test_ozaki_host.py): the symmetric
  * residue of x' = rint(x 2^shift) modulo the l-th modulus (|x'| < 2^62), the l-th modulus, and the
  * CRT of nmod residues (0 <= r_l < m_l) to the nearest double of the integer in (-M/2, M/2). */

@@ -125,6 +125,7 @@ SIGNATURES = {
     "ppls_oz_modulus": (ct.c_int, [ct.c_int]),
     "ppls_gram_info": (ct.c_int, [ct.c_void_p, ct.POINTER(ct.c_int), ct.POINTER(ct.c_int), ct.POINTER(ct.c_int),
                                   _dp]),
+    "ppls_gram_shifts": (ct.c_int, [ct.c_void_p, ct.POINTER(ct.c_int), ct.c_int, ct.POINTER(ct.c_int)]),
     "ppls_finalize_host": (ct.c_int, [_dp, _dp, _dp, ct.c_double, ct.c_double, ct.c_double, ct.c_int,
                                       ct.c_int, ct.c_int, ct.POINTER(PplsTheta), ct.c_int,
                                       ct.POINTER(PplsTheta), ct.POINTER(PplsExpect), _dp]),

@@ -371,12 +371,20 @@ class Context:
     def gram_int8(self, which=2, want=True):
         """The Gram by the int8-MFMA Chinese-remainder form alone (which: 0 X'X, 1 Y'Y, 2 the joint
         [X Y]'[X Y] over the padded columns) -> (G or None, dict(nmod, L, ms = [stats + residues, SYRK,
-        CRT, total]))."""
+        CRT, total], shift = the per-column scalings))."""
         P = self.p if which == 0 else self.q if which == 1 else int(round(np.sqrt(self.xprod_info()["bytes_per_pass"] / 8)))
         G = np.zeros((P, P), order="F") if want else None
         nm, L, ms = ct.c_int(), ct.c_int(), np.zeros(4)
         self._chk(self._L.ppls_gram_int8(self.h, int(which), dptr(G), ct.byref(nm), ct.byref(L), dptr(ms)))
-        return G, dict(nmod=nm.value, L=L.value, ms=ms.tolist())
+        return G, dict(nmod=nm.value, L=L.value, ms=ms.tolist(), shift=self.gram_shifts())
+
+    def gram_shifts(self):
+        """The last int8 Gram's per-column scalings: x'_kj = rint(D_kj 2^shift[j]) (int array)."""
+        k = ct.c_int()
+        self._chk(self._L.ppls_gram_shifts(self.h, None, 0, ct.byref(k)))
+        out = (ct.c_int * max(k.value, 1))()
+        self._chk(self._L.ppls_gram_shifts(self.h, out, k.value, ct.byref(k)))
+        return np.array(out[:k.value], dtype=np.int64)
 
     def gram_info(self):
         """Which Gram ran last (forming S, or variances' X'X / Y'Y): dict(int8 (bool), nmod, L, ms =

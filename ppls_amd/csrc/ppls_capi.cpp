@@ -125,6 +125,7 @@ struct ppls_ctx {
   int gram_int8 = 0;        // option "gram_int8": S by the int8-MFMA CRT form (1, when the column spread
                             // allows; else the fp64 MFMA Gram) or the fp64 MFMA Gram (0)
   int oz_used = 0, oz_nmod = 0, oz_L = 0;   // the last formation of S: which Gram, moduli, bits
+  std::vector<int> oz_shift;                 // its per-column scalings x' = rint(D 2^shift)
   double oz_ms[4] = {0, 0, 0, 0};           // its phases (HIP events): stats+residues, SYRK, CRT, total
   // the int8 Gram's residue planes and SYRK output, kept between formations (allocating and freeing
   // tens of GB per call made later calls' hipMalloc / hipFree take ~1 s each after a dozen calls,
@@ -195,6 +196,9 @@ int fail(ppls_ctx* c, int code, const char* fmt, ...) {
       return fail((c), PPLS_E_COMM, "%s: %s", #call, ncclGetErrorString(e_));            \
   } while (0)
 
+void oz_free(ppls_ctx* c);
+bool oz_held(const ppls_ctx* c);
+
 template <typename T>
 int dalloc(ppls_ctx* c, T** p, size_t count) {
   if (*p) {
@@ -203,6 +207,13 @@ int dalloc(ppls_ctx* c, T** p, size_t count) {
   }
   if (count == 0) count = 1;
   hipError_t e = hipMalloc((void**)p, count * sizeof(T));
+  if (e == hipErrorOutOfMemory && oz_held(c) && (void*)p != (void*)&c->oz_planes && (void*)p != (void*)&c->oz_res) {
+    // the int8 Gram's kept workspace gives way first
+    (void)hipGetLastError();
+    (void)hipStreamSynchronize(c->stream);
+    oz_free(c);
+    e = hipMalloc((void**)p, count * sizeof(T));
+  }
   if (e != hipSuccess) {
     *p = nullptr;
     return fail(c, PPLS_E_NOMEM, "hipMalloc(%zu bytes): %s", count * sizeof(T), hipGetErrorString(e));
@@ -741,13 +752,17 @@ int gram_run(ppls_ctx* c, const GramShape& g, int64_t n, int req, double* G, flo
 
 // The int8-MFMA (Chinese-remainder) form of the same Gram (ppls_ozaki.hip).  Plan from the column
 // statistics: e_j with max_k |D_kj| < 2^e_j, c_j = 2^e_j sqrt(n / sum_k D_kj^2) (>= 1; about 8 for
-// Gaussian columns), L = 53 + ceil(log2 max_j c_j) + 2 bits per integer -- the rounding error of
-// every S_ij is then <= 2^-(L+1) (2^e_i sum|D_kj| + 2^e_j sum|D_ki|) <= 2^-55 sqrt(S_ii S_jj), under
-// the fp64 GEMM's own bound u sum_k |D_ki D_kj| wherever sum |D_ki D_kj| >= sqrt(S_ii S_jj) / 4
-// (tests/test_gpu_ozaki.py checks both on sampled entries against double-double sums) -- and the
-// fewest moduli with prod m_l > 2 max_j sum_k x'_kj^2 (>= |sum_k x'_ki x'_kj| by Cauchy-Schwarz).
-// Returns 1 (not an error) when L > 62, more than PPLS_OZ_MAXMOD moduli are needed or the residue
-// planes do not fit: the caller then runs the fp64 MFMA Gram.
+// Gaussian columns), L_j = 53 + ceil(log2 c_j) + 2 bits for column j's integers x' = rint(D 2^s_j),
+// s_j = L_j - e_j -- the rounding error of every S_ij is then
+// <= 2^-(s_i+1) sum|D_kj| + 2^-(s_j+1) sum|D_ki| <= 2^-55 sqrt(S_ii S_jj), under the fp64 GEMM's own
+// bound u sum_k |D_ki D_kj| wherever sum |D_ki D_kj| >= sqrt(S_ii S_jj) / 4 (tests/test_gpu_ozaki.py
+// checks both on sampled entries against double-double sums) -- and the fewest moduli with
+// prod m_l > 2 max_j sum_k x'_kj^2 (>= |sum_k x'_ki x'_kj| by Cauchy-Schwarz).  Per-column widths keep
+// every column's sum_k x'^2 below n 2^112 (one shared L = max_j L_j put up to 2 more bits on columns of
+// small c_j).  Returns 1 (not an error) when L = max_j L_j > 62, more than PPLS_OZ_MAXMOD moduli are
+// needed or the residue planes do not fit: the caller then runs the fp64 MFMA Gram.
+bool oz_held(const ppls_ctx* c) { return c->oz_planes || c->oz_res; }
+
 void oz_free(ppls_ctx* c) {
   dfree(c->oz_planes);
   dfree(c->oz_res);
@@ -783,26 +798,23 @@ int gram_run_oz(ppls_ctx* c, const GramShape& g, int64_t n, double* G, float* ms
   HIPCHK(c, hipMemcpyAsync(st.data(), b.st, sizeof(double) * st.size(), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   auto live = [&](int j) { return j < g.xreal || (j >= g.xcols && j - g.xcols < g.yreal); };
-  double cmax = 1.0;
-  std::vector<int> e((size_t)Pp, 0);
+  int L = 55;
+  std::vector<int> shift((size_t)Pp, 0);
+  double qmax = 0.0;   // max_j sum_k x'_kj^2 <= (2^s_j ||D_j|| + sqrt(n) / 2)^2
   for (int j = 0; j < P; ++j) {
     if (!live(j) || !(st[(size_t)j] > 0.0)) continue;
     int ex = 0;
     (void)std::frexp(st[(size_t)j], &ex);   // max = f 2^ex, f in [0.5, 1): max < 2^ex
-    e[(size_t)j] = ex;
-    cmax = std::max(cmax, std::ldexp(1.0, ex) * std::sqrt((double)n / st[(size_t)Pp + j]));
-  }
-  const int L = 53 + (int)std::ceil(std::log2(cmax)) + 2;
-  c->oz_L = L;
-  if (L > 62) return 1;
-  std::vector<int> shift((size_t)Pp, 0);
-  double qmax = 0.0;   // max_j sum_k x'_kj^2 <= (2^(L - e_j) ||D_j|| + sqrt(n) / 2)^2
-  for (int j = 0; j < P; ++j) {
-    if (!live(j) || !(st[(size_t)j] > 0.0)) continue;
-    shift[(size_t)j] = L - e[(size_t)j];
-    const double q = std::ldexp(std::sqrt(st[(size_t)Pp + j]), L - e[(size_t)j]) + 0.5 * std::sqrt((double)n);
+    const double cj = std::max(1.0, std::ldexp(1.0, ex) * std::sqrt((double)n / st[(size_t)Pp + j]));
+    const int Lj = 53 + (int)std::ceil(std::log2(cj)) + 2;
+    L = std::max(L, Lj);
+    shift[(size_t)j] = Lj - ex;
+    const double q = std::ldexp(std::sqrt(st[(size_t)Pp + j]), Lj - ex) + 0.5 * std::sqrt((double)n);
     qmax = std::max(qmax, q * q);
   }
+  c->oz_L = L;
+  c->oz_shift.assign(shift.begin(), shift.begin() + P);
+  if (L > 62) return 1;
   // M > 2 max |sum| (the CRT's range (-M/2, M/2)); qmax is an upper bound up to the rounding of the
   // device's sum of squares (relative <= n u ~ 1e-10 at 1e6 rows), covered by the 1e-7 bit
   const double need = std::log2(std::max(qmax, 1.0)) + 1.0 + 1e-7;
@@ -1047,7 +1059,9 @@ void xprod_free(ppls_ctx* c) {
   c->xp_active = false;
   dfree(c->xp_S);
   dfree(c->xp_M);
-  oz_free(c);
+  // (the int8 Gram's residue planes are a workspace, not S: kept until gram_int8 = 0, the context's
+  // end or an allocation that needs the room -- freeing and re-allocating tens of GB per formation
+  // cost 1-5 s per call on some boxes, profiles/r6_gram_int8_percol_c3.jsonl)
 }
 
 int compute_ssq(ppls_ctx* c) {
@@ -3285,6 +3299,14 @@ int ppls_gram_int8(ppls_ctx* c, int which, double* G, int* nmod, int* L, double*
   dfree(dG);
   if (!rc && ms) for (int k = 0; k < 4; ++k) ms[k] = c->oz_ms[k];
   return rc;
+}
+
+int ppls_gram_shifts(ppls_ctx* c, int* shift, int P, int* count) {
+  if (!c) return PPLS_E_ARG;
+  const int k = (int)c->oz_shift.size();
+  if (count) *count = k;
+  if (shift) for (int j = 0; j < std::min(P, k); ++j) shift[j] = c->oz_shift[(size_t)j];
+  return PPLS_OK;
 }
 
 int ppls_gram_info(ppls_ctx* c, int* int8_used, int* nmod, int* L, double* ms) {

@@ -3,12 +3,12 @@
 // default PPLS_simult call and the fp64 MFMA Gram runs at 0.90 of the fp64 peak; gfx950's
 // v_mfma_i32_32x32x32_i8 issues 64x the fp64 MFMA's multiply-adds per clock.
 //
-//   1. column scaling (host, from ppls_oz_colstats_kernel): per live column j, e_j with
-//      max_k |D_kj| < 2^e_j; every element becomes the integer  x'_kj = rint(D_kj 2^(L - e_j)),
-//      |x'| < 2^L, exact in fp64 (a power-of-2 scale, then a rounding to an integer).  L is chosen
-//      from the columns' spread (ppls_oz_plan): the rounding error of S_ij is then at most
-//      2^-(L+1) (2^e_i sum|D_kj| + 2^e_j sum|D_ki|) <= 2^-L c_max sqrt(S_ii S_jj),
-//      c_j = 2^e_j sqrt(n) / sqrt(S_jj).
+//   1. column scaling (host, from ppls_oz_colstats_kernel; gram_run_oz in ppls_capi.cpp): per live
+//      column j, e_j with max_k |D_kj| < 2^e_j and L_j bits from the column's spread
+//      c_j = 2^e_j sqrt(n) / sqrt(S_jj); every element becomes the integer x'_kj = rint(D_kj 2^s_j),
+//      s_j = L_j - e_j, |x'| < 2^L_j, exact in fp64 (a power-of-2 scale, then a rounding to an
+//      integer).  The rounding error of S_ij is then at most
+//      2^-(s_i+1) sum|D_kj| + 2^-(s_j+1) sum|D_ki| <= 2^-55 sqrt(S_ii S_jj).
 //   2. residues (ppls_oz_residue_kernel): x' mod m_l for NMOD pairwise coprime moduli m_l <= 256,
 //      symmetric (|r| <= 128, int8), written as NMOD planes [n / 64][Pp][64] (a stage's 64 rows of
 //      one column contiguous: 16 KB per 256-column panel stage).
@@ -16,7 +16,7 @@
 //      v_mfma_i32_32x32x32_i8, exact in int32 (reduced mod m_l every 65,536 rows), -> uint8 residues.
 //   4. CRT (ppls_oz_finish_kernel): Garner's mixed-radix digits of the NMOD residues, the exact
 //      integer sum_k x'_ki x'_kj in 192 bits (|.| < M / 2, M = prod m_l > 2 max_ij |sum|), ONE
-//      rounding to fp64, times 2^(e_i + e_j - 2L) -> S, mirrored.
+//      rounding to fp64, times 2^-(s_i + s_j) -> S, mirrored.
 // Integer sums are exact, so S depends on the data only (not on the schedule): bitwise repeatable.
 #include <hip/hip_runtime.h>
 #include <stdint.h>

@@ -6,9 +6,9 @@ Checked against EXACT sums: every sampled entry's reference is the correctly rou
 exact products (Dekker's two-product split, then math.fsum over products and their errors).  Per
 entry the int8 result must lie within
 
-  (a) its a-priori bound  2^-(L+1) (2^e_i sum_k |x_kj| + 2^e_j sum_k |x_ki|) + n 2^(e_i + e_j - 2L - 2)
-      + 2 2^-53 |S_ij|   (the rounding of x to x' = rint(x 2^(L - e)), the one final rounding, and the
-      reference's own rounding to fp64), and
+  (a) its a-priori bound  2^-(s_i+1) sum_k |x_kj| + 2^-(s_j+1) sum_k |x_ki| + n 2^-(s_i + s_j + 2)
+      + 2 2^-53 |S_ij|   (the rounding of x to x' = rint(x 2^s), s the column's scaling the library
+      reports, the one final rounding, and the reference's own rounding to fp64), and
   (b) the fp64 GEMM's own bound  u sum_k |x_ki x_kj|,  u = 2^-53,
 
 on Gaussian data (fp64 and fp32 storage, row counts across the 65,536-row SYRK splits and partial
@@ -44,10 +44,11 @@ def exact_dot(a, b):
     return math.fsum(np.concatenate([p, e])), math.fsum(np.abs(p))
 
 
-def _check_entries(D, G, L, nsample, rng, label):
+def _check_entries(D, G, shift, nsample, rng, label):
     n, p = D.shape
     mx = np.abs(D).max(axis=0)
-    e = np.array([math.frexp(v)[1] if v > 0 else 0 for v in mx])
+    s_ = np.asarray(shift, dtype=np.float64)
+    assert len(s_) == p
     asum = np.abs(D).sum(axis=0)
     worst_a = worst_b = 0.0
     pairs = [(i, i) for i in range(min(p, 8))] + [(int(rng.integers(p)), int(rng.integers(p))) for _ in range(nsample)]
@@ -60,7 +61,7 @@ def _check_entries(D, G, L, nsample, rng, label):
         # the integer rounding of x, the one rounding of the exact integer sum, and the rounding of
         # the reference s itself (the correctly rounded exact sum: |G - s| can reach a whole ulp when
         # the scaled integer sum and the exact sum straddle a midpoint)
-        bound = (2.0 ** -(L + 1)) * (2.0 ** e[i] * asum[j] + 2.0 ** e[j] * asum[i]) + n * 2.0 ** (e[i] + e[j] - 2 * L - 2) \
+        bound = 2.0 ** -(s_[i] + 1) * asum[j] + 2.0 ** -(s_[j] + 1) * asum[i] + n * 2.0 ** -(s_[i] + s_[j] + 2) \
             + 2 * U * abs(s)
         assert err <= bound * (1 + 1e-12), (label, i, j, err, bound)
         worst_a = max(worst_a, err / bound)
@@ -69,15 +70,34 @@ def _check_entries(D, G, L, nsample, rng, label):
     return worst_a, worst_b
 
 
-def _check_integer_pipeline(D, G, L, pairs):
-    """Bit for bit: G_ij = the correctly rounded 2^(e_i + e_j - 2L) sum_k x'_ki x'_kj, x' = rint(x 2^(L - e))
-    in Python integers (the residues, SYRKs and CRT reproduce the integer sum exactly)."""
+def _check_shift_rule(D, shift, L):
+    """The scalings follow the plan (ppls_capi.cpp gram_run_oz): s_j = L_j - e_j with max|D_j| < 2^e_j,
+    L_j = 55 + ceil(log2 c_j), c_j = 2^e_j sqrt(n / sum D_j^2) -- columns whose log2 c_j lies within
+    1e-9 of an integer are skipped (the device's sum of squares may round the other way) -- and
+    L = max_j L_j."""
+    n = D.shape[0]
+    mx = np.abs(D).max(axis=0)
+    ss = (D * D).sum(axis=0)
+    Lmax = 55
+    for j in np.nonzero(mx > 0)[0]:
+        e = math.frexp(mx[j])[1]
+        lc = math.log2(max(1.0, 2.0 ** e * math.sqrt(n / ss[j])))
+        Lj = e + int(shift[j])
+        Lmax = max(Lmax, Lj)
+        if abs(lc - round(lc)) > 1e-9:
+            assert Lj == 55 + math.ceil(lc), (j, Lj, lc)
+    assert Lmax == L
+
+
+def _check_integer_pipeline(D, G, shift, pairs):
+    """Bit for bit: G_ij = the correctly rounded 2^-(s_i + s_j) sum_k x'_ki x'_kj, x' = rint(x 2^s) in
+    Python integers (the residues, SYRKs and CRT reproduce the integer sum exactly)."""
     from fractions import Fraction
-    e = [math.frexp(v)[1] if v > 0 else 0 for v in np.abs(D).max(axis=0)]
+    s_ = [int(v) for v in shift]
     for i, j in pairs:
-        xi = [round(Fraction(float(a)) * 2 ** (L - e[i])) for a in D[:, i]]
-        xj = [round(Fraction(float(a)) * 2 ** (L - e[j])) for a in D[:, j]]
-        want = float(Fraction(sum(a * b for a, b in zip(xi, xj))) * Fraction(2) ** (e[i] + e[j] - 2 * L))
+        xi = [round(Fraction(float(a)) * Fraction(2) ** s_[i]) for a in D[:, i]]
+        xj = [round(Fraction(float(a)) * Fraction(2) ** s_[j]) for a in D[:, j]]
+        want = float(Fraction(sum(a * b for a, b in zip(xi, xj))) * Fraction(2) ** -(s_[i] + s_[j]))
         assert G[i, j] == want, (i, j, G[i, j].hex(), want.hex())
 
 
@@ -97,11 +117,12 @@ def test_int8_gram_matches_exact_sums(dtype, n, p, q):
         for which, D in ((0, X), (1, Y)):
             G, info = c.gram_int8(which)
             assert 12 <= info["nmod"] <= 20 and info["L"] <= 62
+            _check_shift_rule(D, info["shift"], info["L"])
             assert np.array_equal(G, G.T)
-            wa, wb = _check_entries(D, G, info["L"], 200 if n < 100_000 else 60, rng, (which, n, p))
+            wa, wb = _check_entries(D, G, info["shift"], 200 if n < 100_000 else 60, rng, (which, n, p))
             if n <= 5000:
                 k = D.shape[1]
-                _check_integer_pipeline(D, G, info["L"], [(0, 0), (k - 1, 0), (k - 1, k - 1)] +
+                _check_integer_pipeline(D, G, info["shift"], [(0, 0), (k - 1, 0), (k - 1, k - 1)] +
                                         [(int(rng.integers(k)), int(rng.integers(k))) for _ in range(12)])
             Gf, _ = c.gram(which)   # the fp64 MFMA Gram, for the record
             if n >= 100:
@@ -115,7 +136,9 @@ def test_int8_gram_matches_exact_sums(dtype, n, p, q):
 def test_int8_gram_full_row_counts(dtype, n, p, q):
     """At the bench configs' row counts (C3's 1e6 rows in 16 SYRK splits, C5's 5e5 fp32-stored rows in 8;
     fewer columns so the host reference stays cheap): sampled entries of the joint Gram within the
-    a-priori bound and within u sum|x_ki x_kj| against double-double exact sums."""
+    a-priori bound and within u sum|x_ki x_kj| against double-double exact sums.  Per-column widths
+    keep every sum_k x'^2 below n 2^112: 17 moduli at both row counts (one shared width took 18 at
+    1e6 rows)."""
     from ppls_amd import Context
     rng = np.random.default_rng(n)
     X = rng.standard_normal((n, p)) * np.exp(rng.uniform(-3, 3, p))   # columns of different scales
@@ -128,8 +151,9 @@ def test_int8_gram_full_row_counts(dtype, n, p, q):
         c.set_data(X, Y)
         for which, D in ((0, X), (1, Y)):
             G, info = c.gram_int8(which)
-            assert info["L"] <= 62 and info["nmod"] <= 20
-            wa, wb = _check_entries(D, G, info["L"], 24, rng, (which, n, p))
+            assert info["L"] <= 62 and info["nmod"] == 17, info["nmod"]
+            _check_shift_rule(D, info["shift"], info["L"])
+            wa, wb = _check_entries(D, G, info["shift"], 24, rng, (which, n, p))
             assert wb <= 1.0, (which, wb)
             print(f"n={n} which={which} dtype={dtype}: nmod {info['nmod']} L {info['L']}: / a-priori {wa:.3g}, "
                   f"/ (u sum|x x|) {wb:.3g}, SYRK {info['ms'][1]:.1f} ms")
@@ -137,8 +161,8 @@ def test_int8_gram_full_row_counts(dtype, n, p, q):
 
 def test_int8_joint_gram_blocks():
     """The joint [X Y]'[X Y] over the padded columns (what forms S): its X'X and Y'Y blocks equal the
-    per-block int8 Grams bit for bit (the same column scalings, exact integer sums), the X'Y block
-    matches exact sums within its bound, padding columns are 0."""
+    per-block int8 Grams bit for bit (each column's scaling depends on that column alone, integer sums
+    are exact), the X'Y block matches exact sums within its bound, padding columns are 0."""
     from ppls_amd import Context
     n, p, q = 9000, 61, 45
     X, Y, _ = make_problem(n, p, q, 1, seed=3)
@@ -149,13 +173,13 @@ def test_int8_joint_gram_blocks():
         GY, iy = c.gram_int8(1)
     ldx = GJ.shape[0] - (q + 1) // 2 * 2   # fp64 rows of p <= 2048 columns are padded to even lengths
     assert ldx >= p
-    if info["L"] == ix["L"]:
-        assert np.array_equal(GJ[:p, :p], GX)
-    if info["L"] == iy["L"]:
-        assert np.array_equal(GJ[ldx:ldx + q, ldx:ldx + q], GY)
+    assert np.array_equal(info["shift"][:p], ix["shift"]) and np.array_equal(info["shift"][ldx:ldx + q], iy["shift"])
+    assert np.all(info["shift"][p:ldx] == 0)
+    assert np.array_equal(GJ[:p, :p], GX)
+    assert np.array_equal(GJ[ldx:ldx + q, ldx:ldx + q], GY)
     assert np.all(GJ[p:ldx, :] == 0) and np.all(GJ[:, p:ldx] == 0)
     D = np.hstack([X, np.zeros((n, ldx - p)), Y, np.zeros((n, GJ.shape[0] - ldx - q))])
-    _check_entries(D, GJ, info["L"], 150, np.random.default_rng(2), "joint")
+    _check_entries(D, GJ, info["shift"], 150, np.random.default_rng(2), "joint")
 
 
 @pytest.mark.parametrize("dtype", [0, 1], ids=["f64", "f32"])
@@ -183,6 +207,35 @@ def test_xprod_fit_with_int8_gram_equals_streaming(dtype):
         est_f, ll_f, _, _ = c.em_run(th, 12, -np.inf, 0, want_eout=False)
         assert not c.gram_info()["int8"]
         assert np.abs(ll_f - ll_x).max() / np.abs(ll_s).max() < 1e-12
+
+
+def test_int8_workspace_reused_across_release_and_new_data():
+    """The residue planes outlive ppls_xprod_release and new data (a workspace, ppls.h "gram_int8"):
+    S formed again after a release is bitwise the same (integer sums); a smaller problem in the larger
+    workspace and the workspace freed by gram_int8 = 0 and allocated again give exact-sum results."""
+    from ppls_amd import Context, Theta
+    n, p, q, r = 30_000, 200, 70, 3
+    X, Y, th0 = make_problem(n, p, q, r, seed=21)
+    th = Theta(th0["W"], th0["C"], th0["B"], th0["sigE"], th0["sigF"], th0["sigH"], th0["sigT"])
+    rng = np.random.default_rng(5)
+    with Context(0) as c:
+        c.set_data(X, Y)
+        c.set_option("xprod", 1)
+        c.set_option("gram_int8", 1)
+        est1, ll1, _, _ = c.em_run(th, 8, -np.inf, 0, want_eout=False)
+        assert c.gram_info()["int8"]
+        c.xprod_release()
+        est2, ll2, _, _ = c.em_run(th, 8, -np.inf, 0, want_eout=False)
+        assert c.gram_info()["int8"]
+        assert np.array_equal(ll1, ll2) and np.array_equal(est1.W, est2.W) and np.array_equal(est1.C, est2.C)
+        X2, Y2, _ = make_problem(4000, 90, 33, 1, seed=22)
+        c.set_data(X2, Y2)
+        for step in range(2):
+            G, info = c.gram_int8(0)
+            _check_entries(X2, G, info["shift"], 60, rng, ("reuse", step))
+            _check_integer_pipeline(X2, G, info["shift"], [(0, 0), (89, 3), (17, 17)])
+            c.set_option("gram_int8", 0)   # frees the workspace; the next formation allocates it again
+            c.set_option("gram_int8", 1)
 
 
 def test_int8_gram_falls_back_when_the_spread_is_too_wide():
@@ -315,10 +368,10 @@ def test_int8_gram_fuzz(case):
             except PplsError:
                 continue
             assert np.array_equal(G, G.T)
-            _check_entries(D, G, info["L"], 40, rng, ("fuzz", case, which, n))
+            _check_entries(D, G, info["shift"], 40, rng, ("fuzz", case, which, n))
             if n <= 3000:
                 k = D.shape[1]
-                _check_integer_pipeline(D, G, info["L"], [(int(rng.integers(k)), int(rng.integers(k))) for _ in range(8)])
+                _check_integer_pipeline(D, G, info["shift"], [(int(rng.integers(k)), int(rng.integers(k))) for _ in range(8)])
 
 
 @pytest.mark.parametrize("config", ["c3", "c5"])
