@@ -40,8 +40,31 @@ def test_residues_of_scaled_integers(L):
             assert L.ppls_oz_residue_host(x, shift, l, ct.byref(out)) == 0
             m = L.ppls_oz_modulus(l)
             r = out.value
-            assert -m // 2 <= r <= m // 2 and -128 <= r <= 128
+            assert -(m // 2) <= r <= m // 2 and -128 <= r <= 127
             assert (r - xs) % m == 0, (x, shift, l, r, xs % m)
+
+
+def test_residues_at_the_limb_extremes(L):
+    """The fp32 residue form (five 13-bit limbs of |x'|, |t| < 2^23, one rint against 1.5 2^23): the
+    largest integers (|x'| up to 2^62 - 2^10), every limb at its maximum, single limbs, both signs,
+    and the rounding boundaries of t / m -- a congruent residue within [-m//2, m//2] every time."""
+    out = ct.c_int()
+    vals = {0, 1, 2 ** 62 - 2 ** 10, (2 ** 53 - 1) * 2 ** 9, 2 ** 52 * 1023, 8191, 8191 * 2 ** 13, 8191 * 2 ** 26,
+            8191 * 2 ** 39}
+    vals |= {sum(8191 << (13 * i) for i in range(k)) for k in range(1, 5)}   # all-ones limbs (< 2^53: exact)
+    for m_ in (255, 253, 251, 173):
+        vals |= {m_ * k + d for k in (1, 1000, 2 ** 20, 2 ** 40) for d in (m_ // 2, m_ // 2 + 1, -(m_ // 2), 0)}
+    for v in sorted(vals):
+        for sgn in (1, -1):
+            xs = sgn * v
+            x = float(xs)
+            if int(x) != xs:   # (only exactly representable integers: shift 0 keeps them)
+                continue
+            for l in range(20):
+                assert L.ppls_oz_residue_host(x, 0, l, ct.byref(out)) == 0
+                m = L.ppls_oz_modulus(l)
+                r = out.value
+                assert -(m // 2) <= r <= m // 2 and (r - xs) % m == 0, (xs, m, r)
 
 
 @pytest.mark.parametrize("nmod", [12, 16, 18, 20])
