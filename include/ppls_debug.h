@@ -66,8 +66,10 @@ int ppls_gram_info(ppls_ctx* ctx, int* int8_used, int* nmod, int* L, double* ms)
  * sweep (one segmented launch per EM step), 3 the device loop on the panel sweep (one launch per
  * population and step). */
 int ppls_meta_info(ppls_ctx* ctx, int* path);
-/* The Gram D'D alone (D = X for xory 0, Y for 1; nsplit 0 = auto), for tests and benchmarks:
- * G (p x p, column-major, nullable), *ms = the MFMA kernel's duration. */
+/* The Gram D'D alone (D = X for xory 0, Y for 1, the joint [X Y] for 2; nsplit 0 = auto; this rank's
+ * rows), for tests, benchmarks and the 'o2m' starting values of the Python PPLS / PPLSi /
+ * meta_PPLSi: G (p x p, q x q or (p + q) x (p + q) without padding columns, column-major,
+ * nullable), *ms = the MFMA kernel's duration. */
 int ppls_gram(ppls_ctx* ctx, int xory, int nsplit, double* G, double* ms);
 /* Inverse of a batch of symmetric positive definite matrices (host A: a x p x p, column-major, stride
  * p^2) as variances.PPLS_simult inverts the observed information: method 1 the hand-written blocked

@@ -19,6 +19,9 @@ Every function cites the reference line it restates (paths relative to /root/ref
 * ``ppls``               Package/PPLS/R/EM_W_multi.R:229-279 (sequential fit with deflation)
 * ``initial_guess``      Package/PPLS/R/EM_W_multi.R:126-140 ('equal'; 'random' from an R stream,
                          oracle/r_rng.py, or numpy draws)
+* ``initial_guess_o2m``  Package/PPLS/R/EM_W_multi.R:126-131 / :520-525 ('o2m'), over ``o2m_1``
+* ``o2m_1``              OmicsPLS::o2m(X, Y, 1, 0, 0) (not vendored, no version pinned: DESCRIPTION
+                         Imports "OmicsPLS"); the published O2PLS algorithm's n = 1, nx = ny = 0 case
 * ``print_ppls``         Package/PPLS/R/EM_W_multi.R:336-354 (print.PPLS's variance table)
 * ``scores_ppls``        Package/PPLS/R/EM_W_multi.R:411-420
 * ``ppls_simult_to_o2m`` Package/PPLS/R/PPLS_to_o2m.R:82-140
@@ -477,6 +480,35 @@ def initial_guess(p, q, kind="equal", rng=None):
     raise ValueError(kind)
 
 
+def o2m_1(X, Y):
+    """OmicsPLS::o2m(X, Y, n = 1, nx = 0, ny = 0): the fields PPLSi reads (EM_W_multi.R:127-130).
+    OmicsPLS is not vendored and its version is not pinned (DESCRIPTION Imports "OmicsPLS"); restated
+    from the published O2PLS algorithm (el Bouhaddani et al.): with no orthogonal components nothing
+    is filtered, the joint loadings W., C. are the first left / right singular vectors of X'Y, the
+    scores Tt = X W., U = Y C., and the inner relation B_T. = (Tt'Tt)^-1 Tt'U.  (For p, q above its
+    size thresholds OmicsPLS reaches the same pair by power iterations.)  The sign of the pair is
+    LAPACK's (numpy's svd, the dgesdd R's svd calls; flipping both leaves B_T. and the fit's
+    likelihood unchanged).  Parity unpinned: no file of the reference holds an o2m fit."""
+    U_, _, Vt = np.linalg.svd(X.T @ Y, full_matrices=False)
+    W, C = U_[:, 0], Vt[0]
+    Tt, U = X @ W, Y @ C
+    return dict(W=W, C=C, Tt=Tt, U=U, B_T=float(Tt @ U) / float(Tt @ Tt))
+
+
+def initial_guess_o2m(X, Y):
+    """PPLSi's 'o2m' starting values -- EM_W_multi.R:126-131 (meta_PPLSi :520-525): W., C., B_T.[1]
+    of o2m(X, Y, 1, 0, 0), sig = sqrt(c((ssq(X) - ssq(Tt)) / N / p, (ssq(Y) - ssq(U)) / N / q)) and
+    siglat = sqrt(c(ssq(U) - ssq(Tt B), ssq(Tt)) / N)."""
+    N, p = X.shape
+    q = Y.shape[1]
+    sim = o2m_1(X, Y)
+    B = sim["B_T"]
+    Tt, U = sim["Tt"], sim["U"]
+    return dict(W=sim["W"], C=sim["C"], B=B, sigE=math.sqrt((ssq(X) - ssq(Tt)) / N / p),
+                sigF=math.sqrt((ssq(Y) - ssq(U)) / N / q), sigH=math.sqrt((ssq(U) - ssq(Tt * B)) / N),
+                sigT=math.sqrt(ssq(Tt) / N))
+
+
 def fconstraint(constraints=None):
     """fconstraint -- Package/PPLS/R/EM_W_multi.R:85-92: the 7 named constraints, None = free."""
     out = dict(W=None, C=None, B=None, sigE=None, sigF=None, sigH=None, sigT=None)
@@ -533,8 +565,9 @@ def pplsi(X, Y, EMsteps=100, atol=1e-4, theta0=None, constraints=None, critfunc=
 
 def ppls(X, Y, nr_comp=1, EMsteps=100, atol=1e-4, theta0s=None, constraints=None, critfunc=None):
     """PPLS -- Package/PPLS/R/EM_W_multi.R:229-279: nr_comp PPLSi fits on successively deflated
-    X, Y (:270-271).  theta0s: one starting-value dict per component (initial_guess); constraints:
-    one fconstraint dict per component (:230, :255) or None."""
+    X, Y (:270-271).  theta0s: one starting-value dict per component (initial_guess), or "o2m" for
+    the o2m starting values of the deflated Xc, Yc that component sees (:126-131 inside PPLSi);
+    constraints: one fconstraint dict per component (:230, :255) or None."""
     X = np.asarray(X, dtype=np.float64)
     Y = np.asarray(Y, dtype=np.float64)
     a = nr_comp
@@ -545,7 +578,8 @@ def ppls(X, Y, nr_comp=1, EMsteps=100, atol=1e-4, theta0s=None, constraints=None
     Xc, Yc = X, Y
     done = 0
     for i in range(a):                                                              # :254
-        fit = pplsi(Xc, Yc, EMsteps, atol, theta0s[i], None if constraints is None else constraints[i],
+        th0 = initial_guess_o2m(Xc, Yc) if isinstance(theta0s[i], str) and theta0s[i] == "o2m" else theta0s[i]
+        fit = pplsi(Xc, Yc, EMsteps, atol, th0, None if constraints is None else constraints[i],
                     critfunc)                                                       # :256-257
         if fit["B"] is None:                                                        # :258-263
             break

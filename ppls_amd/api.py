@@ -361,8 +361,9 @@ class Context:
         return W, Bx, tr(V), se, tr(SE), tr(SS)
 
     def gram(self, xory=0, nsplit=0, want=True):
-        """D'D (D = X or Y) on the MFMA Gram kernel alone -> (G or None, kernel ms)."""
-        p = self.q if xory else self.p
+        """D'D (D = X, Y, or xory = 2 the joint [X Y], (p + q) x (p + q)) on the fp64 MFMA Gram kernel
+        alone, this rank's rows -> (G or None, kernel ms)."""
+        p = self.p + self.q if xory == 2 else self.q if xory else self.p
         G = np.zeros((p, p), order="F") if want else None
         ms = ct.c_double()
         self._chk(self._L.ppls_gram(self.h, int(xory), int(nsplit), dptr(G), ct.byref(ms)))
@@ -660,7 +661,7 @@ def initial_guess(p, q, kind="equal", rng=None):
     restatement of R's Mersenne-Twister/Inversion defaults) reproduces R's draws after the same
     ``set.seed``; a numpy ``Generator`` draws from the same distributions.  ``orth`` of a positive
     vector is taken as v/||v|| (the QR form's -v/||v|| gives the mirrored, equivalent fit).
-    'o2m' needs OmicsPLS: not provided."""
+    'o2m' depends on the data: PPLS / PPLSi / meta_PPLSi compute it (o2m_guess_from_gram)."""
     if kind == "equal":
         return dict(W=np.ones(p) / np.sqrt(p), C=np.ones(q) / np.sqrt(q), B=1.0, sigE=1.0 / p,
                     sigF=1.0 / q, sigH=1.0, sigT=1.0)
@@ -681,8 +682,60 @@ def initial_guess(p, q, kind="equal", rng=None):
         return dict(W=W / np.linalg.norm(W), C=C / np.linalg.norm(C), B=float(B), sigE=float(sig[0]),
                     sigF=float(sig[1]), sigH=float(siglat[0]), sigT=float(siglat[1]))
     if kind == "o2m":
-        raise NotImplementedError("initialGuess='o2m' needs OmicsPLS::o2m (out of scope)")
+        raise ValueError("initialGuess='o2m' depends on the data: PPLS / PPLSi / meta_PPLSi compute it "
+                         "(o2m_guess_from_gram)")
     raise ValueError(f"unknown initialGuess {kind!r}")
+
+
+def o2m_guess_from_gram(G, N, p, q, Wprev=None, Cprev=None):
+    """PPLSi's 'o2m' starting values (EM_W_multi.R:126-131; meta_PPLSi :520-525) from the joint Gram
+    G = [X Y]'[X Y] ((p + q) x (p + q), Context.gram(2)) of N rows, for the data PPLS deflated by the
+    earlier components' loadings Wprev (p x k), Cprev (q x k): Xc = X P_1 ... P_k, P_j = I - w_j w_j'
+    (:270-271, sequentially, as the reference does).  o2m(Xc, Yc, 1, 0, 0) of OmicsPLS (not vendored,
+    no version pinned) with no orthogonal parts: W., C. = the first singular pair of Xc'Yc (numpy's
+    LAPACK svd on the host: p x q), Tt = Xc W., U = Yc C., B = Tt'U / Tt'Tt -- every sum of squares
+    and product read off G (ssq(Tt) = z'X'Xz with z = P_1 ... P_k W.), so no pass over the rows.
+    Returns the starting-value dict (W, C, B, sigE, sigF, sigH, sigT).  Parity unpinned against R
+    (no reference file holds an o2m fit); checked against the oracle's restatement on the explicit
+    deflated data (tests/test_o2m_host.py, tests/test_gpu_o2m.py)."""
+    G = np.asarray(G, dtype=np.float64)
+    Gxx, Gyy, Gxy = G[:p, :p], G[p:, p:], G[:p, p:]
+    Wp = np.zeros((p, 0)) if Wprev is None else np.asarray(Wprev, dtype=np.float64).reshape(p, -1)
+    Cp = np.zeros((q, 0)) if Cprev is None else np.asarray(Cprev, dtype=np.float64).reshape(q, -1)
+    M = Gxy.copy()                          # Xc'Yc = P_k ... P_1 X'Y Q_1 ... Q_k
+    for j in range(Wp.shape[1]):
+        M -= np.outer(Wp[:, j], Wp[:, j] @ M)
+    for j in range(Cp.shape[1]):
+        M -= np.outer(M @ Cp[:, j], Cp[:, j])
+
+    def chain(Vp, v):                       # P_1 ... P_k v
+        for j in reversed(range(Vp.shape[1])):
+            v = v - Vp[:, j] * (Vp[:, j] @ v)
+        return v
+
+    def ssq_deflated(Gd, Vp):               # ssq(D P_1 ... P_k): ssq(A P) = ssq(A) - (2 - w'w) ||A w||^2
+        t = float(np.trace(Gd))
+        for j in range(Vp.shape[1]):
+            z = chain(Vp[:, :j], Vp[:, j])  # A_{j-1} w_j = D z
+            t -= (2.0 - float(Vp[:, j] @ Vp[:, j])) * float(z @ Gd @ z)
+        return t
+
+    U_, _, Vt = np.linalg.svd(M, full_matrices=False)
+    w, c = U_[:, 0].copy(), Vt[0].copy()
+    zx, zy = chain(Wp, w), chain(Cp, c)
+    sst, ssu, tu = float(zx @ Gxx @ zx), float(zy @ Gyy @ zy), float(zx @ Gxy @ zy)
+    B = tu / sst
+    ssx, ssy = ssq_deflated(Gxx, Wp), ssq_deflated(Gyy, Cp)
+    return dict(W=w, C=c, B=B, sigE=float(np.sqrt((ssx - sst) / N / p)), sigF=float(np.sqrt((ssy - ssu) / N / q)),
+                sigH=float(np.sqrt((ssu - B * B * sst) / N)), sigT=float(np.sqrt(sst / N)))
+
+
+def _joint_gram(ctx):
+    if ctx.n_local != ctx.n_total:
+        raise NotImplementedError("initialGuess='o2m' on row shards: all-reduce the ranks' Context.gram(2) "
+                                  "and call o2m_guess_from_gram")
+    G, _ = ctx.gram(2)
+    return G
 
 
 def fconstraint(constraints=None):
@@ -713,13 +766,29 @@ def PPLS(X, Y, nr_comp=1, EMsteps=100, atol=1e-4, initialGuess=("equal", "o2m", 
     kind = initialGuess if isinstance(initialGuess, str) else initialGuess[0]
     if customGuess is not None:
         kind = "custom"
+    if constraints is not None and len(constraints) != nr_comp:
+        raise ValueError("There should be a list of constraints for each component, see ?PPLS.")   # :240
     if kind == "custom":
         inits = list(customGuess) if isinstance(customGuess, (list, tuple)) else [customGuess] * nr_comp
+    elif kind == "o2m":
+        # component i starts from o2m of the data deflated by components 1 .. i-1 (:256-257 with
+        # :126-131): the device refits 1 .. i from the same starting values (deterministic) to learn
+        # W_1 .. W_i, C_1 .. C_i, then the next starting values come from the joint Gram
+        G = _joint_gram(ctx)
+        inits, Wp, Cp = [], None, None
+        for i in range(nr_comp):
+            inits.append(o2m_guess_from_gram(G, ctx.n_total, ctx.p, ctx.q, Wp, Cp))
+            if i + 1 == nr_comp:
+                break
+            f = ctx.ppls(i + 1, int(EMsteps), float(atol), inits, None if constraints is None else constraints[:i + 1],
+                         _crit_abs(critfunc))
+            if f["ncomp"] < i + 1:   # the fit stops there anyway (:258-263); later values are never used
+                inits += [initial_guess(ctx.p, ctx.q, "equal")] * (nr_comp - len(inits))
+                break
+            Wp, Cp = f["W"], f["C"]
     else:
         rng = rng if rng is not None else np.random.default_rng()
         inits = [initial_guess(ctx.p, ctx.q, kind, rng) for _ in range(nr_comp)]
-    if constraints is not None and len(constraints) != nr_comp:
-        raise ValueError("There should be a list of constraints for each component, see ?PPLS.")   # :240
     out = ctx.ppls(int(nr_comp), int(EMsteps), float(atol), inits, constraints, _crit_abs(critfunc))
     if out["ncomp"] < nr_comp:
         warnings.warn(f"From component {out['ncomp'] + 1} on the residuals are of rank < 1e-14 and "
@@ -915,6 +984,8 @@ def meta_PPLSi(X, Y, Ipopu, EMsteps=100, atol=1e-4, initialGuess=("equal", "o2m"
         g = customGuess
         init = dict(W=np.ravel(g["W"]), C=np.ravel(g["C"]), B=g["B"], sigE=g["sigE"], sigF=g["sigF"],
                     sigH=g["sigH"], sigT=g["sigT"])
+    elif kind == "o2m":
+        init = o2m_guess_from_gram(_joint_gram(ctx), ctx.n_total, ctx.p, ctx.q)   # :520-525
     else:
         init = initial_guess(ctx.p, ctx.q, kind, rng if rng is not None else np.random.default_rng())
     if constraints:

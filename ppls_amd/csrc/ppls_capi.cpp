@@ -2975,17 +2975,32 @@ int ppls_spd_inverse(ppls_ctx* c, const double* A, int p, int a, int method, dou
 int ppls_gram(ppls_ctx* c, int xory, int nsplit, double* G, double* ms) {
   if (!c) return PPLS_E_ARG;
   if (!c->have_data) return fail(c, PPLS_E_STATE, "no data");
+  if (xory < 0 || xory > 2) return fail(c, PPLS_E_ARG, "xory must be 0 (X'X), 1 (Y'Y) or 2 ([X Y]'[X Y])");
   HIPCHK(c, hipSetDevice(c->device));
-  const int p = xory ? c->q : c->p;
-  const size_t pp = (size_t)p * p;
+  const GramShape g = xory == 2 ? gram_shape(c, true, 0) : gram_shape(c, false, xory);
+  const size_t pp = (size_t)g.p * g.p;
   if (c->n_local <= 0) return fail(c, PPLS_E_STATE, "no rows on this rank");
   int rc;
   double* dG = nullptr;
   if ((rc = dalloc(c, &dG, pp))) return rc;
   float t = 0.f;
-  rc = gram_run(c, gram_shape(c, false, xory), c->n_local, nsplit > 0 ? nsplit : 0, dG, &t);
-  if (!rc && G && hipMemcpy(G, dG, sizeof(double) * pp, hipMemcpyDeviceToHost) != hipSuccess)
-    rc = fail(c, PPLS_E_HIP, "gram: copy-out failed");
+  rc = gram_run(c, g, c->n_local, nsplit > 0 ? nsplit : 0, dG, &t);
+  if (!rc && G) {
+    if (xory < 2) {
+      if (hipMemcpy(G, dG, sizeof(double) * pp, hipMemcpyDeviceToHost) != hipSuccess)
+        rc = fail(c, PPLS_E_HIP, "gram: copy-out failed");
+    } else {   // the joint Gram without the row padding between X's and Y's columns: (p + q)^2
+      std::vector<double> full(pp);
+      if (hipMemcpy(full.data(), dG, sizeof(double) * pp, hipMemcpyDeviceToHost) != hipSuccess) {
+        rc = fail(c, PPLS_E_HIP, "gram: copy-out failed");
+      } else {
+        const int P = c->p + c->q;
+        auto src = [&](int k) { return k < c->p ? k : c->ldx + (k - c->p); };
+        for (int b = 0; b < P; ++b)
+          for (int a = 0; a < P; ++a) G[(size_t)b * P + a] = full[(size_t)src(b) * g.p + src(a)];
+      }
+    }
+  }
   dfree(dG);
   if (!rc && ms) *ms = t;
   return rc;
